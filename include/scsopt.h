@@ -1,0 +1,187 @@
+/*
+ * scsopt.h -- C ABI of libscsopt, the MI355X (gfx950) implementation of the
+ * SCORE inner iteration of SelfConcordantSmoothOptimization.jl.
+ *
+ * The reference has no FFI: its plugin boundary is Julia multiple dispatch on
+ * `step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter)`
+ * (src/algorithms/iterate.jl:52-54) plus the objective closures evaluated by
+ * `optim_loop!` (iterate.jl:168, :189-190).  Each entry point below replaces
+ * one of those Julia-side pieces; the Julia `ccall` binding a maintainer adds
+ * is in INTEGRATION.md, the Python ctypes binding is
+ * selfconcordantsmoothoptimization.jl_amd/scsopt/_lib.py.
+ *
+ * Conventions
+ *   - All functions return SCS_OK (0) or an error code; the message is
+ *     available from scs_last_error(ctx) (errors the reference raises with
+ *     Base.error carry the reference's message text).
+ *   - Host pointers are borrowed for the duration of the call.  Vectors of
+ *     length m (x, x_prev, x_new, dx) are host fp64 arrays.
+ *   - A is column-major (Julia Matrix{Float64} layout) with leading dimension
+ *     lda >= N.  In a multi-rank context each rank holds rows
+ *     [row0, row0 + N) of the global N_global x m matrix (row-sharded).
+ *   - A context is not thread-safe; all device work is ordered on its stream.
+ */
+#ifndef SCSOPT_H
+#define SCSOPT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCS_OK 0
+#define SCS_ERR_ARG 1      /* invalid argument / unsupported combination     */
+#define SCS_ERR_HIP 2      /* HIP runtime / device failure                   */
+#define SCS_ERR_SOLVE 3    /* factorization failed (singular system)         */
+#define SCS_ERR_STATE 4    /* call order (e.g. step before data)             */
+#define SCS_ERR_REF 5      /* an error the reference itself raises           */
+#define SCS_ERR_COMM 6     /* all-reduce callback failed                     */
+
+/* f(A, y, x) kinds -- closed forms of the reference's user callbacks.       */
+enum scs_loss_kind {
+  SCS_LOSS_LOGISTIC_MARGIN = 1, /* c*sum(log(1+exp(-y.*(A*x))))  test/test_algs.jl:9  */
+  SCS_LOSS_LOGISTIC_CE = 2,     /* f(y, sigmoid(A*x)), cross-entropy  SURVEY §8a C3 */
+  SCS_LOSS_LEAST_SQUARES = 3,   /* 0.5*sum((A*x-y).^2)*c           README.md:212-214 */
+  SCS_LOSS_QUADRATIC = 4,       /* 1/2*(x'*(A*x)) + y'*x             test/test_algs.jl:90 */
+  SCS_LOSS_ROSENBROCK = 5       /* chained Rosenbrock, no data        README.md:49 */
+};
+
+/* (out_fn, f(y, ŷ)) pairs used by ProxGGNSCORE (prox-GGN-SCORE.jl:44-56).    */
+enum scs_ggn_kind {
+  SCS_GGN_NONE = 0,
+  SCS_GGN_SIGMOID_CE = 1,       /* Mfunc = sigmoid(A*x), CE on ŷ   test/test_algs.jl:10-11 */
+  SCS_GGN_LINEAR_LS = 2         /* out_fn = A*x, 0.5*c*sum((ŷ-y).^2) README.md:233-239 */
+};
+
+/* reg_name strings of get_reg / invoke_prox (regularizers.jl:4-31,
+ * prox-operators.jl:68-79).                                                 */
+enum scs_reg_kind { SCS_REG_L1 = 1, SCS_REG_L2 = 2, SCS_REG_INDBOX = 3, SCS_REG_GL = 4 };
+
+/* Smoother types (phuber-smooth.jl, exponential-smooth.jl).                 */
+enum scs_smoother_kind {
+  SCS_SMOOTH_PHUBER_L1L2 = 1,   /* PHuberSmootherL1L2(μ)          phuber-smooth.jl:27   */
+  SCS_SMOOTH_PHUBER_INDBOX = 2, /* PHuberSmootherIndBox(lb,ub,μ)  phuber-smooth.jl:59   */
+  SCS_SMOOTH_PHUBER_GL = 3,     /* PHuberSmootherGL(μ, problem)   phuber-smooth.jl:137  */
+  SCS_SMOOTH_EXP_INDBOX = 4     /* ExponentialSmootherIndBox      exponential-smooth.jl:28 */
+};
+
+/* ProximalMethod subtypes (src/algorithms/prox-*-SCORE.jl).                 */
+enum scs_method_kind { SCS_PROX_NSCORE = 1, SCS_PROX_GGNSCORE = 2, SCS_PROX_LQNSCORE = 3 };
+
+typedef struct scs_ctx scs_ctx;
+
+/* All-reduce hook for row-sharded contexts: sum `count` fp64 values in place
+ * across ranks.  `dev_buf` is the device buffer registered with
+ * scs_set_reduce_buffer (offset 0); `stream` is the context stream.  Return 0
+ * on success.  Called between the local partial Gram/gradient and the m x m
+ * solve (the only exchange point of the path).              */
+typedef int (*scs_allreduce_fn)(void* dev_buf, int64_t count, void* stream, void* user);
+
+/* Synthetic on-device data (counter-based RNG; every row is reproducible from
+ * its global index, so any row shard is generated in place).               */
+typedef struct scs_synth {
+  int64_t N_global;  /* total rows                                        */
+  int64_t row0;      /* first global row held by this context             */
+  int64_t N;         /* rows held by this context                         */
+  int64_t m;         /* columns                                           */
+  uint64_t seed;
+  int kind;          /* 1: A ~ N(0,1)/sqrt(m); y ~ Bernoulli(sigmoid(A x_true)) in {0,1}
+                        2: A ~ N(0,1)/sqrt(m); y ~ ±1 with P(+1) = sigmoid(A x_true)
+                        3: A ~ N(0,1);         y = A x_true + 0.1 eps              */
+  double density;    /* fraction of nonzero entries of x_true             */
+} scs_synth;
+
+/* Per-kernel device-time accumulators (hipEvent elapsed, ms), read by bench. */
+typedef struct scs_timing {
+  double gram_ms;    int64_t gram_calls;   /* MFMA Aᵀ diag(w) A                */
+  double gemv_ms;    int64_t gemv_calls;   /* A*x and Aᵀ*v streaming passes    */
+  double solve_ms;   int64_t solve_calls;  /* m x m factor + solve             */
+  double step_ms;    int64_t step_calls;   /* whole scs_step                   */
+  double reduce_ms;  int64_t reduce_calls; /* all-reduce callback              */
+} scs_timing;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+const char* scs_version(void);
+/* Create a context on HIP device `device`; `stream` = existing hipStream_t or
+ * NULL to create one.                                                       */
+int scs_create(int device, void* stream, scs_ctx** out);
+int scs_destroy(scs_ctx* ctx);
+const char* scs_last_error(const scs_ctx* ctx);
+int scs_get_stream(scs_ctx* ctx, void** stream);
+
+/* ---- row sharding ------------------------------------------------------- */
+int scs_set_comm(scs_ctx* ctx, int rank, int nranks, scs_allreduce_fn fn, void* user);
+/* Device buffer (>= scs_reduce_buffer_size() doubles) owned by the caller,
+ * used as the in-place all-reduce payload.                                  */
+int scs_reduce_buffer_size(scs_ctx* ctx, int64_t* ndoubles);
+int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
+
+/* ---- data  (Problem(A, y, ...) -- problems.jl:61-81) --------------------- */
+/* Upload host A (column-major, N x m, leading dim lda) and y (N).  N is the
+ * local row count; N_global/row0 describe the shard.  A may be NULL with
+ * m > 0 only for SCS_LOSS_ROSENBROCK (ProblemGeneric, problems.jl:44-59).   */
+int scs_set_data(scs_ctx* ctx, int64_t N, int64_t m, const double* A, int64_t lda,
+                 const double* y, int64_t N_global, int64_t row0);
+int scs_gen_data(scs_ctx* ctx, const scs_synth* spec);
+/* Copy device A rows [r0, r0+nr) (column-major, lda_out) and y back.       */
+int scs_get_data(scs_ctx* ctx, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y);
+int scs_get_dims(scs_ctx* ctx, int64_t* N, int64_t* m, int64_t* N_global, int64_t* row0);
+
+/* ---- problem / regularizer / smoother ----------------------------------- */
+int scs_set_loss(scs_ctx* ctx, int loss_kind, int ggn_kind, double scale);
+/* λ: nlam = 1 (scalar) or 2 ([λ1, λ2] for "gl").  Box (indbox): lb/ub are
+ * nbound = 1 scalars or nbound = m vectors (C_set).  Groups (gl): ind is the
+ * 3 x ngroups Int matrix of get_P (column-major, 1-based start, end, weight;
+ * prox-reg-utils.jl:27-62); groups must tile 1..m contiguously.            */
+int scs_set_reg(scs_ctx* ctx, int reg_kind, const double* lam, int nlam,
+                const double* lb, const double* ub, int64_t nbound,
+                const int64_t* ind, int64_t ngroups);
+/* Mh/nu as in the smoother struct (e.g. 2.0/2.6 for pseudo-Huber).  lb/ub
+ * (indbox smoothers) follow bounds_sanity_check (prox-reg-utils.jl:144-158). */
+int scs_set_smoother(scs_ctx* ctx, int kind, double mu, double Mh, double nu,
+                     const double* lb, const double* ub, int64_t nbound);
+/* model.L (nothing <=> has_L = 0); iterate!(…; α) sets L = 1/α.            */
+int scs_set_L(scs_ctx* ctx, int has_L, double L);
+
+/* ---- method  (init! / step!) -------------------------------------------- */
+/* init!(method, x): select the method and reset its state (L-BFGS memory,
+ * prox-L-BFGS-SCORE.jl:31-36).  mem = ProxLQNSCORE.m.                       */
+int scs_method_init(scs_ctx* ctx, int method, int ss_type, int use_prox, int mem);
+/* f(A, y, x) (iterate.jl:168).                                             */
+int scs_eval_f(scs_ctx* ctx, const double* x, double* fval);
+/* ∇f(A, y, x) (grad_fx; the ForwardDiff gradient of f when the user gives none,
+ * prox-L-BFGS-SCORE.jl:84-97).                                              */
+int scs_eval_grad(scs_ctx* ctx, const double* x, double* g);
+/* get_reg(model, x, reg_name) (regularizers.jl:4-31).                      */
+int scs_eval_reg(scs_ctx* ctx, const double* x, double* gval);
+/* step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter;
+ *       return_dx) (prox-N-SCORE.jl:34, prox-GGN-SCORE.jl:34,
+ * prox-L-BFGS-SCORE.jl:69).  dx may be NULL.                               */
+int scs_step(scs_ctx* ctx, const double* x, const double* x_prev, int64_t iter,
+             double* x_new, double* dx, double* pri_res_norm);
+
+/* ---- kernel-level entry points (parity tests) --------------------------- */
+/* hμ.grad(Cmat, x), hμ.hess(Cmat, x)                                       */
+int scs_smoother_eval(scs_ctx* ctx, const double* x, double* gr, double* Hr);
+/* prox_step(invoke_prox(model, reg_name, z, 1 ./ Hr, λ, α))                */
+int scs_prox_eval(scs_ctx* ctx, const double* z, const double* Hr, double lam,
+                  double alpha, double* out);
+/* G = Aᵀ diag(w) A (local rows; lower triangle + diagonal tiles), ldg >= m. */
+int scs_gram_eval(scs_ctx* ctx, const double* w, double* G, int64_t ldg);
+/* out = Aᵀ v (local rows)                                                  */
+int scs_gemv_t_eval(scs_ctx* ctx, const double* v, double* out);
+/* out = A x (local rows)                                                   */
+int scs_gemv_n_eval(scs_ctx* ctx, const double* x, double* out);
+
+/* ---- timing ------------------------------------------------------------- */
+int scs_timing_enable(scs_ctx* ctx, int on);
+int scs_timing_get(scs_ctx* ctx, scs_timing* out);
+int scs_timing_reset(scs_ctx* ctx);
+/* Wait for all work on the context stream.                                 */
+int scs_sync(scs_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCSOPT_H */

@@ -1,0 +1,306 @@
+// Sample-space (length-N) kernels: the two streaming passes over A and the
+// per-sample loss epilogue, plus on-device synthetic data.
+//
+//   z = A*x         gemv_n   (HBM-bound: reads A once, 8·N·m bytes)
+//   per-sample      epilogue (sums the z partials in a fixed order, then the
+//                    loss value / gradient coefficient / Hessian weight /
+//                    GGN (w = s²q, v = s·r) of the selected loss kind)
+//   Aᵀ*v            gemv_t   (HBM-bound: reads A once; v staged in LDS)
+//
+// A is column-major with lda = Npad (Npad % 16 == 0, zero rows beyond N).
+#include "common.h"
+#include "kernels.h"
+
+namespace scs {
+
+// ---------------------------------------------------------------------------
+// z = A x : 256 threads x 2 rows (16-B loads along the contiguous sample
+// axis), columns split over blockIdx.y when there are too few row blocks.
+// ---------------------------------------------------------------------------
+constexpr int GN_ROWS = 512;
+
+int gemv_n_splits(int64_t Npad, int64_t m) {
+  const int64_t rb = ceil_div(Npad, GN_ROWS);
+  int64_t s = ceil_div(2048, rb);
+  const int64_t smax = ceil_div(m, 256);
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  return (int)s;
+}
+
+__global__ __launch_bounds__(256) void gemv_n_kernel(const double* __restrict__ A, int64_t lda, int64_t Npad,
+                                                     int64_t m, const double* __restrict__ x, int64_t cps,
+                                                     double* __restrict__ part, int64_t ldo) {
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+  if (r >= Npad) return;
+  const int64_t c0 = (int64_t)blockIdx.y * cps;
+  const int64_t c1 = (c0 + cps < m) ? c0 + cps : m;
+  v2d acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
+  const double* p = A + c0 * lda + r;
+  int64_t j = c0;
+  for (; j + 8 <= c1; j += 8) {
+    const v2d a0 = *(const v2d*)(p);
+    const v2d a1 = *(const v2d*)(p + lda);
+    const v2d a2 = *(const v2d*)(p + 2 * lda);
+    const v2d a3 = *(const v2d*)(p + 3 * lda);
+    const v2d a4 = *(const v2d*)(p + 4 * lda);
+    const v2d a5 = *(const v2d*)(p + 5 * lda);
+    const v2d a6 = *(const v2d*)(p + 6 * lda);
+    const v2d a7 = *(const v2d*)(p + 7 * lda);
+    acc0 += a0 * x[j];
+    acc1 += a1 * x[j + 1];
+    acc0 += a2 * x[j + 2];
+    acc1 += a3 * x[j + 3];
+    acc0 += a4 * x[j + 4];
+    acc1 += a5 * x[j + 5];
+    acc0 += a6 * x[j + 6];
+    acc1 += a7 * x[j + 7];
+    p += 8 * lda;
+  }
+  for (; j < c1; ++j) {
+    acc0 += *(const v2d*)(p) * x[j];
+    p += lda;
+  }
+  *(v2d*)(part + (int64_t)blockIdx.y * ldo + r) = acc0 + acc1;
+}
+
+hipError_t launch_gemv_n(const double* A, int64_t lda, int64_t Npad, int64_t m, const double* x, int nsplit,
+                         double* part, int64_t ldo, hipStream_t st) {
+  int64_t cps = ceil_div(m, nsplit);
+  const int ns = (int)ceil_div(m, cps);
+  // unused trailing splits (if any) are zeroed so the epilogue can sum nsplit slices
+  if (ns < nsplit) {
+    hipError_t e = hipMemsetAsync(part + (int64_t)ns * ldo, 0, sizeof(double) * ldo * (nsplit - ns), st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(gemv_n_kernel, dim3((unsigned)ceil_div(Npad, GN_ROWS), (unsigned)ns), dim3(256), 0, st, A, lda,
+                     Npad, m, x, cps, part, ldo);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Loss epilogue  (closed forms; see oracle/scsopt_oracle.py Loss for the
+// reference expressions they restate, test/test_algs.jl:9-11)
+// ---------------------------------------------------------------------------
+constexpr int EPI_PER_BLOCK = 2048;
+
+int epilogue_blocks(int64_t Npad) { return (int)ceil_div(Npad, EPI_PER_BLOCK); }
+
+__global__ __launch_bounds__(256) void epilogue_kernel(int loss, int ggn, int flags, const double* __restrict__ zpart,
+                                                       int nsplit, int64_t ldz, const double* __restrict__ y,
+                                                       int64_t N, int64_t Npad, double c, double* __restrict__ zout,
+                                                       double* __restrict__ gout, double* __restrict__ hout,
+                                                       double* __restrict__ wout, double* __restrict__ vout,
+                                                       double* __restrict__ valpart) {
+  __shared__ double sh[4];
+  double acc = 0.0;
+  const int64_t base = (int64_t)blockIdx.x * EPI_PER_BLOCK;
+  for (int k = 0; k < EPI_PER_BLOCK / 256; ++k) {
+    const int64_t n = base + k * 256 + threadIdx.x;
+    if (n >= Npad) break;
+    double z = 0.0;
+    for (int s = 0; s < nsplit; ++s) z += zpart[(int64_t)s * ldz + n];
+    if (flags & EPI_Z) zout[n] = z;
+    if (n >= N) {
+      if (flags & EPI_GRAD) gout[n] = 0.0;
+      if (flags & EPI_HESS) hout[n] = 0.0;
+      if (flags & EPI_GGN) { wout[n] = 0.0; vout[n] = 0.0; }
+      continue;
+    }
+    const double yn = y[n];
+    if (loss == SCS_LOSS_LOGISTIC_MARGIN) {
+      const double e = exp(-yn * z);
+      if (flags & EPI_VAL) acc += log(1.0 + e);
+      if (flags & EPI_GRAD) gout[n] = c * ((-yn * e) / (1.0 + e));
+      if (flags & EPI_HESS) hout[n] = c * (yn * yn) * e / ((1.0 + e) * (1.0 + e));
+    } else if (loss == SCS_LOSS_LOGISTIC_CE) {
+      const double e = exp(-z);
+      const double yh = 1.0 / (1.0 + e);
+      if (flags & EPI_VAL) acc += yn * log(yh) + (1.0 - yn) * log(1.0 - yh);
+      if (flags & (EPI_GRAD | EPI_HESS)) {
+        const double s = e / ((1.0 + e) * (1.0 + e));
+        const double r = -c * (yn / yh - (1.0 - yn) / (1.0 - yh));
+        if (flags & EPI_GRAD) gout[n] = s * r;
+        if (flags & EPI_HESS) {
+          const double q = c * (yn / (yh * yh) + (1.0 - yn) / ((1.0 - yh) * (1.0 - yh)));
+          hout[n] = s * s * q + r * (s * (1.0 - 2.0 * yh));
+        }
+      }
+    } else if (loss == SCS_LOSS_LEAST_SQUARES) {
+      const double res = z - yn;
+      if (flags & EPI_VAL) acc += res * res;
+      if (flags & EPI_GRAD) gout[n] = res * c;
+      if (flags & EPI_HESS) hout[n] = c;
+    }
+    if (flags & EPI_GGN) {
+      if (ggn == SCS_GGN_SIGMOID_CE) {
+        const double e = exp(-z);
+        const double yh = 1.0 / (1.0 + e);
+        const double s = e / ((1.0 + e) * (1.0 + e));
+        const double r = -c * (yn / yh - (1.0 - yn) / (1.0 - yh));
+        const double q = c * (yn / (yh * yh) + (1.0 - yn) / ((1.0 - yh) * (1.0 - yh)));
+        wout[n] = s * s * q;
+        vout[n] = s * r;
+      } else {  // SCS_GGN_LINEAR_LS
+        wout[n] = 1.0 * 1.0 * c;
+        vout[n] = 1.0 * ((z - yn) * c);
+      }
+    }
+  }
+  if (flags & EPI_VAL) {
+    const double s = block_sum<256>(acc, sh);
+    if (threadIdx.x == 0) valpart[blockIdx.x] = s;
+  }
+}
+
+hipError_t launch_epilogue(int loss, int ggn, int flags, const double* zpart, int nsplit, int64_t ldz,
+                           const double* y, int64_t N, int64_t Npad, double c, double* z, double* g, double* h,
+                           double* w, double* v, double* valpart, hipStream_t st) {
+  hipLaunchKernelGGL(epilogue_kernel, dim3(epilogue_blocks(Npad)), dim3(256), 0, st, loss, ggn, flags, zpart, nsplit,
+                     ldz, y, N, Npad, c, z, g, h, w, v, valpart);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(1024) void sum_partials_kernel(const double* __restrict__ part, int n,
+                                                            double* __restrict__ out) {
+  __shared__ double sh[16];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) acc += part[i];
+  const double s = block_sum<1024>(acc, sh);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+hipError_t launch_sum_partials(const double* part, int n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, st, part, n, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Aᵀ v : block = (4096-row chunk, 64 columns); v chunk staged in LDS, each
+// wave owns 16 columns, 4 at a time; lanes stride the contiguous samples.
+// ---------------------------------------------------------------------------
+constexpr int GT_ROWS = 4096;
+
+int gemv_t_chunks(int64_t Npad) { return (int)ceil_div(Npad, GT_ROWS); }
+
+__global__ __launch_bounds__(256) void gemv_t_kernel(const double* __restrict__ A, int64_t lda, int64_t Npad,
+                                                     int64_t m, const double* __restrict__ v,
+                                                     double* __restrict__ part, int64_t ldp) {
+  __shared__ v2d vs[GT_ROWS / 2];
+  const int64_t r0 = (int64_t)blockIdx.x * GT_ROWS;
+  const int64_t nr = (Npad - r0 < GT_ROWS) ? Npad - r0 : GT_ROWS;
+  const int nh = (int)(nr / 2);
+  for (int i = threadIdx.x; i < nh; i += 256) vs[i] = *(const v2d*)(v + r0 + 2 * i);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t jbase = (int64_t)blockIdx.y * 64 + wid * 16;
+  for (int cc = 0; cc < 16; cc += 4) {
+    const int64_t j = jbase + cc;
+    if (j >= m) break;
+    v2d acc[4] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+    const double* p0 = A + j * lda + r0;
+    for (int i = lane; i < nh; i += 64) {
+      const v2d vv = vs[i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (j + q < m) acc[q] += *(const v2d*)(p0 + q * lda + 2 * i) * vv;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double s = wave_sum(acc[q][0] + acc[q][1]);
+      if (lane == 0 && j + q < m) part[(int64_t)blockIdx.x * ldp + j + q] = s;
+    }
+  }
+}
+
+hipError_t launch_gemv_t(const double* A, int64_t lda, int64_t Npad, int64_t m, int64_t mpad, const double* v,
+                         double* part, hipStream_t st) {
+  hipLaunchKernelGGL(gemv_t_kernel, dim3((unsigned)gemv_t_chunks(Npad), (unsigned)ceil_div(m, 64)), dim3(256), 0, st,
+                     A, lda, Npad, m, v, part, mpad);
+  return hipGetLastError();
+}
+
+__global__ void gemv_t_finalize_kernel(const double* __restrict__ part, int nchunk, int64_t ldp, int64_t m,
+                                       double* __restrict__ out) {
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  double s = 0.0;
+  for (int c = 0; c < nchunk; ++c) s += part[(int64_t)c * ldp + j];
+  out[j] = s;
+}
+
+hipError_t launch_gemv_t_finalize(const double* part, int nchunk, int64_t mpad, int64_t m, double* out,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(gemv_t_finalize_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, st, part, nchunk, mpad,
+                     m, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic data: counter-based RNG (splitmix64 finaliser over (seed, index)),
+// so every element is a pure function of its global index -> row shards are
+// generated in place and agree with any other sharding.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t smix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ double uni(uint64_t seed, uint64_t idx) {
+  const uint64_t h = smix(smix(seed) ^ idx);
+  return ((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ double gauss(uint64_t seed, uint64_t idx) {
+  const double u1 = uni(seed, 2 * idx), u2 = uni(seed, 2 * idx + 1);
+  return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+}
+
+__global__ void gen_A_kernel(double* __restrict__ A, int64_t lda, int64_t N, int64_t m, int64_t row0,
+                             uint64_t seed, double scale) {
+  const int64_t j = blockIdx.y;
+  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < lda; n += (int64_t)gridDim.x * blockDim.x) {
+    double v = 0.0;
+    if (n < N && j < m) v = scale * gauss(seed, (uint64_t)(row0 + n) * (uint64_t)m + (uint64_t)j);
+    A[j * lda + n] = v;
+  }
+}
+
+hipError_t launch_gen_A(double* A, int64_t lda, int64_t N, int64_t m, int64_t row0, uint64_t seed, double scale,
+                        hipStream_t st) {
+  int64_t gx = ceil_div(lda, 256);
+  if (gx > 64) gx = 64;
+  hipLaunchKernelGGL(gen_A_kernel, dim3((unsigned)gx, (unsigned)m), dim3(256), 0, st, A, lda, N, m, row0, seed,
+                     scale);
+  return hipGetLastError();
+}
+
+__global__ void gen_xtrue_kernel(double* __restrict__ x, int64_t m, uint64_t seed, double density) {
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  x[j] = (uni(seed + 1, j) < density) ? gauss(seed + 2, j) : 0.0;
+}
+
+hipError_t launch_gen_xtrue(double* x, int64_t m, uint64_t seed, double density, hipStream_t st) {
+  hipLaunchKernelGGL(gen_xtrue_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, st, x, m, seed, density);
+  return hipGetLastError();
+}
+
+__global__ void gen_y_kernel(int kind, const double* __restrict__ z, double* __restrict__ y, int64_t N, int64_t row0,
+                             uint64_t seed) {
+  const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const uint64_t gi = (uint64_t)(row0 + n);
+  const double p = 1.0 / (1.0 + exp(-z[n]));
+  if (kind == 1) y[n] = (uni(seed + 3, gi) < p) ? 1.0 : 0.0;
+  else if (kind == 2) y[n] = (uni(seed + 3, gi) < p) ? 1.0 : -1.0;
+  else y[n] = z[n] + 0.1 * gauss(seed + 4, gi);
+}
+
+hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t row0, uint64_t seed,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(gen_y_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, st, kind, z, y, N, row0, seed);
+  return hipGetLastError();
+}
+
+}  // namespace scs

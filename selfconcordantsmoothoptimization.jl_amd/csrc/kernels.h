@@ -1,0 +1,83 @@
+// Launcher declarations shared by the kernel files and the orchestration.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/scsopt.h"
+
+namespace scs {
+
+// host-side mirror of the prox/regularizer parameters (device pointers inside)
+struct ProxArgsH {
+  int reg = 0;
+  int use_prox = 1;
+  double lam = 0.0, lam2 = 0.0;
+  const double* lb = nullptr;
+  const double* ub = nullptr;
+  const int* gstart = nullptr;
+  const int* gend = nullptr;
+  const double* gw = nullptr;
+  int ngroups = 0;
+};
+
+// ---- gram.hip
+void gram_tile_list(int nb, int2* out, int* ntiles);
+hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
+                       double* G, int64_t ldg, int packed, hipStream_t st);
+hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,
+                              hipStream_t st);
+
+// ---- vec.hip
+hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,
+                           const double* wel, double* gr, double* Hr, hipStream_t st);
+hipError_t launch_score_tail(const double* x, const double* d, const double* gr, const double* Hr, int64_t m,
+                             double lam, double Mg, double step_host, const double* step_dev, const ProxArgsH& P,
+                             double* hinv, double* zbuf, double* x_new, double* dx, double* scal, hipStream_t st);
+hipError_t launch_prox_only(const ProxArgsH& P, const double* z, const double* Hr, double step, int64_t m,
+                            double* hinv, double* out, hipStream_t st);
+hipError_t launch_reg_value(const ProxArgsH& P, const double* x, int64_t m, double* out, hipStream_t st);
+hipError_t launch_dot(const double* a, const double* b, int64_t m, double* out, hipStream_t st);
+hipError_t launch_axpby(const double* a, double lam, const double* b, int64_t m, double* out, hipStream_t st);
+hipError_t launch_sub(const double* a, const double* b, int64_t m, double* out, hipStream_t st);
+hipError_t launch_neg(const double* a, int64_t m, double* out, hipStream_t st);
+hipError_t launch_trial_point(const double* x, const double* d, double alpha, int64_t m, double* out,
+                              hipStream_t st);
+hipError_t launch_bb_step(const double* x, const double* xp, const double* g, const double* gp, int64_t m,
+                          double* out, hipStream_t st);
+hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
+                           const double* g, int64_t m, double* q, double* d, double* ab, hipStream_t st);
+hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
+                               double* Yslot, double* scal, hipStream_t st);
+hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st);
+hipError_t launch_symmetrize(double* G, int64_t ldg, int64_t m, hipStream_t st);
+hipError_t launch_half_sym(const double* A, int64_t lda, int64_t m, double* G, int64_t ldg, hipStream_t st);
+hipError_t launch_rosen(const double* x, int64_t m, int what, double* out, double* G, int64_t ldg, hipStream_t st);
+
+// ---- data.hip
+// z-partials: out[split][ldo] ; returns the number of splits used
+int gemv_n_splits(int64_t Npad, int64_t m);
+hipError_t launch_gemv_n(const double* A, int64_t lda, int64_t Npad, int64_t m, const double* x, int nsplit,
+                         double* part, int64_t ldo, hipStream_t st);
+// loss epilogue over samples: sums the z-partials, writes z / coefficient vectors and
+// per-block loss partials.  Returns the number of value partials written.
+enum { EPI_Z = 1, EPI_VAL = 2, EPI_GRAD = 4, EPI_HESS = 8, EPI_GGN = 16 };
+int epilogue_blocks(int64_t Npad);
+hipError_t launch_epilogue(int loss, int ggn, int flags, const double* zpart, int nsplit, int64_t ldz,
+                           const double* y, int64_t N, int64_t Npad, double c, double* z, double* g, double* h,
+                           double* w, double* v, double* valpart, hipStream_t st);
+// out[0] = Σ part[0..n)  (fixed order)
+hipError_t launch_sum_partials(const double* part, int n, double* out, hipStream_t st);
+// Aᵀ v (column partial sums over row chunks, then a fixed-order finalize)
+int gemv_t_chunks(int64_t Npad);
+hipError_t launch_gemv_t(const double* A, int64_t lda, int64_t Npad, int64_t m, int64_t mpad, const double* v,
+                         double* part, hipStream_t st);
+// out[j] = Σ_chunk part[chunk][j] (+ lam*add[j] if add)
+hipError_t launch_gemv_t_finalize(const double* part, int nchunk, int64_t mpad, int64_t m, double* out,
+                                  hipStream_t st);
+// synthetic data
+hipError_t launch_gen_A(double* A, int64_t lda, int64_t N, int64_t m, int64_t row0, uint64_t seed, double scale,
+                        hipStream_t st);
+hipError_t launch_gen_xtrue(double* x, int64_t m, uint64_t seed, double density, hipStream_t st);
+hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t row0, uint64_t seed,
+                        hipStream_t st);
+
+}  // namespace scs

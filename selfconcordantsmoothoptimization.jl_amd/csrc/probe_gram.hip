@@ -1,0 +1,95 @@
+// probe_gram: standalone correctness + speed check of gram.hip (no library).
+//   probe_gram            -> small-size exactness check vs a CPU fp64 loop, then timing
+//   probe_gram N m reps   -> timing only at N x m
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include <vector>
+#include "common.h"
+
+namespace scs {
+void gram_tile_list(int nb, int2* out, int* ntiles);
+hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
+                       double* G, int64_t ldg, int packed, hipStream_t st);
+}
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+__device__ inline uint64_t smix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void fill_kernel(double* p, size_t n, uint64_t seed, double scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t h = smix(seed ^ (i * 0x632BE59BD9B4E019ull));
+    p[i] = scale * (((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0) - 0.5);
+  }
+}
+
+static int run(int64_t N, int64_t m, int reps, bool check) {
+  const int64_t lda = N;
+  double *A, *w, *G;
+  CK(hipMalloc(&A, (size_t)lda * m * 8));
+  CK(hipMalloc(&w, (size_t)N * 8));
+  CK(hipMalloc(&G, (size_t)m * m * 8));
+  fill_kernel<<<4096, 256>>>(A, (size_t)lda * m, 1234, 2.0);
+  fill_kernel<<<256, 256>>>(w, (size_t)N, 99, 1.0);
+  CK(hipMemset(G, 0, (size_t)m * m * 8));
+  const int nb = (int)(m / 128);
+  std::vector<int2> tl((size_t)nb * (nb + 1) / 2);
+  int nt = 0;
+  scs::gram_tile_list(nb, tl.data(), &nt);
+  int2* dtl;
+  CK(hipMalloc(&dtl, nt * sizeof(int2)));
+  CK(hipMemcpy(dtl, tl.data(), nt * sizeof(int2), hipMemcpyHostToDevice));
+  CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, 0));
+  CK(hipDeviceSynchronize());
+  if (check) {
+    std::vector<double> hA((size_t)lda * m), hw(N), hG((size_t)m * m);
+    CK(hipMemcpy(hA.data(), A, hA.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hw.data(), w, hw.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hG.data(), G, hG.size() * 8, hipMemcpyDeviceToHost));
+    double maxrel = 0;
+    for (int64_t j = 0; j < m; ++j)
+      for (int64_t i = j; i < m; ++i) {
+        double s = 0, sa = 0;
+        for (int64_t n = 0; n < N; ++n) {
+          double t = hA[i * lda + n] * hw[n] * hA[j * lda + n];
+          s += t; sa += fabs(t);
+        }
+        double e = fabs(hG[j * m + i] - s) / (sa > 0 ? sa : 1);
+        if (e > maxrel) maxrel = e;
+      }
+    printf("CHECK N=%ld m=%ld max |G-ref|/sum|terms| = %.3e  %s\n", (long)N, (long)m, maxrel,
+           maxrel < 1e-14 ? "PASS" : "FAIL");
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, 0));
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  double alg = (double)N * m * (m + 1);   // symmetric Gram, algorithmic
+  double exe = 2.0 * N * 128.0 * 128.0 * nt;  // executed incl. full diagonal tiles
+  printf("GRAM N=%ld m=%ld tiles=%d: %.3f ms/launch  alg %.2f TF/s  exec %.2f TF/s\n", (long)N, (long)m, nt, ms,
+         alg / ms / 1e9, exe / ms / 1e9);
+  CK(hipFree(A)); CK(hipFree(w)); CK(hipFree(G)); CK(hipFree(dtl));
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc >= 3) return run(atoll(argv[1]), atoll(argv[2]), argc > 3 ? atoi(argv[3]) : 3, false);
+  run(48, 256, 1, true);
+  run(1024, 384, 1, true);
+  run(4096, 1024, 1, true);
+  run(1 << 17, 8192, 3, false);
+  run(1 << 17, 16384, 2, false);
+  return 0;
+}

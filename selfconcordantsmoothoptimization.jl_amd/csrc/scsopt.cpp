@@ -1,0 +1,1179 @@
+// libscsopt: C ABI + per-method step orchestration of the SCORE inner
+// iteration on MI355X.  Device work is issued on the context stream; the host
+// reads back only the scalars the reference's control flow needs.
+//
+// Method map (reference -> here):
+//   step!(::ProxNSCORE)   prox-N-SCORE.jl:34-119     -> step_newton(NSCORE)
+//   step!(::ProxGGNSCORE) prox-GGN-SCORE.jl:34-135   -> step_newton(GGN)
+//   step!(::ProxLQNSCORE) prox-L-BFGS-SCORE.jl:69-169 -> step_lqn
+//   linesearch / inv_BB_step  utils.jl:27-48           -> line_search / bb kernel
+//   get_Mg                    smoothing.jl:12-25        -> get_Mg
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/scsopt.h"
+#include "common.h"
+#include "kernels.h"
+
+using namespace scs;
+
+namespace {
+
+struct Pending {
+  int cat;
+  hipEvent_t e0, e1;
+};
+enum { T_GRAM = 0, T_GEMV, T_SOLVE, T_STEP, T_REDUCE, T_N };
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct scs_ctx {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  bool own_stream = false;
+  std::string err;
+
+  // row sharding
+  int rank = 0, nranks = 1;
+  scs_allreduce_fn ar = nullptr;
+  void* ar_user = nullptr;
+  double* red = nullptr;
+  int64_t red_cap = 0;
+
+  // data
+  int64_t N = 0, Npad = 0, m = 0, mpad = 0, Nglob = 0, row0 = 0;
+  bool has_data = false;
+  bool generic = false;  // ProblemGeneric (no A)
+  double* A = nullptr;
+  double* y = nullptr;
+
+  // problem
+  int loss = 0, ggn = 0;
+  double scale = 1.0;
+  bool loss_set = false;
+  int reg = 0;
+  double lam = 0.0, lam2 = 0.0;
+  int nlam = 1;
+  bool reg_set = false;
+  double* clb = nullptr;  // C_set (raw) bounds, length mpad
+  double* cub = nullptr;
+  int ngroups = 0;
+  int* gstart = nullptr;
+  int* gend = nullptr;
+  double* gw = nullptr;
+  double* wel = nullptr;  // per-element group weight (Cmat diagonal)
+  int smooth = 0;
+  double mu = 1.0, Mh = 2.0, nu = 2.6;
+  bool smooth_set = false;
+  double* slb = nullptr;  // sanitized smoother bounds
+  double* sub = nullptr;
+  bool has_L = false;
+  double L = 0.0;
+
+  // method
+  int method = 0, ss_type = 1, use_prox = 1, mem = 10;
+  bool method_set = false;
+  double* S = nullptr;  // [mem+1][mpad]
+  double* Yv = nullptr;
+  std::vector<int> ring;  // physical slots, oldest -> newest
+  int spare = 0;
+  int* d_order = nullptr;
+  double H0 = 1.0;
+
+  // m-space workspace
+  double *x = nullptr, *xp = nullptr, *xn = nullptr, *dxv = nullptr, *gr = nullptr, *Hr = nullptr, *hinv = nullptr,
+         *zb = nullptr, *d = nullptr, *gq = nullptr, *gqn = nullptr, *gtmp = nullptr, *gtmp2 = nullptr, *q = nullptr,
+         *ab = nullptr, *scal = nullptr, *gcache[2] = {nullptr, nullptr};
+  double* hscal = nullptr;  // pinned host scalars
+  // N-space workspace
+  int nsplit = 1;
+  double *zpart = nullptr, *z = nullptr, *gN = nullptr, *hN = nullptr, *wN = nullptr, *vN = nullptr,
+         *valpart = nullptr;
+  int nval = 1;
+  int nchunk = 1;
+  double* tpart = nullptr;
+  // Gram / solve
+  double *G = nullptr, *Gc = nullptr;
+  int2* tiles = nullptr;
+  int ntiles = 0;
+  rocblas_handle blas = nullptr;
+  rocblas_int* dinfo = nullptr;
+  rocblas_int* ipiv = nullptr;
+  bool lu_fallback_used = false;
+
+  // caches (CSE of identical evaluations; keyed by the host x content)
+  std::vector<double> zkey;
+  bool zvalid = false;
+  double zfval = 0.0;  // f(x) for zkey (global, scaled)
+  std::vector<double> gkey[2];
+  bool gvalid[2] = {false, false};
+  int gnext = 0;
+
+  // timing
+  bool timing = false;
+  std::vector<Pending> pending;
+  double tms[T_N] = {0, 0, 0, 0, 0};
+  int64_t tcalls[T_N] = {0, 0, 0, 0, 0};
+
+  std::vector<DevBuf> allocs;
+};
+
+// ---------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Fail {
+  int code;
+};
+
+void set_err(scs_ctx* c, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+}
+
+#define HCK(expr)                                                                                      \
+  do {                                                                                                 \
+    hipError_t e__ = (expr);                                                                           \
+    if (e__ != hipSuccess) {                                                                           \
+      set_err(c, "HIP error '%s' at %s:%d (%s)", hipGetErrorString(e__), __FILE__, __LINE__, #expr); \
+      throw Fail{SCS_ERR_HIP};                                                                         \
+    }                                                                                                  \
+  } while (0)
+
+#define RCK(expr)                                                                              \
+  do {                                                                                         \
+    rocblas_status s__ = (expr);                                                               \
+    if (s__ != rocblas_status_success) {                                                       \
+      set_err(c, "rocBLAS/rocSOLVER status %d at %s:%d (%s)", (int)s__, __FILE__, __LINE__, #expr); \
+      throw Fail{SCS_ERR_HIP};                                                                 \
+    }                                                                                          \
+  } while (0)
+
+[[noreturn]] void fail(scs_ctx* c, int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  c->err = buf;
+  throw Fail{code};
+}
+
+template <class F>
+int guarded(scs_ctx* c, F&& f) {
+  if (!c) return SCS_ERR_ARG;
+  try {
+    c->err.clear();
+    f();
+    return SCS_OK;
+  } catch (const Fail& e) {
+    return e.code;
+  } catch (const std::exception& e) {
+    c->err = e.what();
+    return SCS_ERR_HIP;
+  }
+}
+
+template <class T>
+T* dalloc(scs_ctx* c, size_t n) {
+  void* p = nullptr;
+  const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) fail(c, SCS_ERR_HIP, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+  HCK(hipMemsetAsync(p, 0, bytes, c->st));
+  c->allocs.push_back({p, bytes});
+  return (T*)p;
+}
+
+void dfree(scs_ctx* c, void*& p) {
+  if (!p) return;
+  for (size_t i = 0; i < c->allocs.size(); ++i)
+    if (c->allocs[i].p == p) {
+      c->allocs.erase(c->allocs.begin() + i);
+      break;
+    }
+  (void)hipFree(p);
+  p = nullptr;
+}
+template <class T>
+void dfree_t(scs_ctx* c, T*& p) {
+  void* v = (void*)p;
+  dfree(c, v);
+  p = nullptr;
+}
+
+void h2d(scs_ctx* c, double* dst, const double* src, int64_t n) {
+  HCK(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+}
+void d2h(scs_ctx* c, double* dst, const double* src, int64_t n) {
+  HCK(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
+}
+void sync(scs_ctx* c) { HCK(hipStreamSynchronize(c->st)); }
+
+void tbegin(scs_ctx* c, int cat, hipEvent_t* e0) {
+  if (!c->timing) return;
+  HCK(hipEventCreate(e0));
+  HCK(hipEventRecord(*e0, c->st));
+  (void)cat;
+}
+void tend(scs_ctx* c, int cat, hipEvent_t e0) {
+  if (!c->timing) return;
+  hipEvent_t e1;
+  HCK(hipEventCreate(&e1));
+  HCK(hipEventRecord(e1, c->st));
+  c->pending.push_back({cat, e0, e1});
+}
+void tresolve(scs_ctx* c) {
+  if (c->pending.empty()) return;
+  for (auto& p : c->pending) {
+    HCK(hipEventSynchronize(p.e1));
+    float ms = 0.f;
+    HCK(hipEventElapsedTime(&ms, p.e0, p.e1));
+    c->tms[p.cat] += ms;
+    c->tcalls[p.cat] += 1;
+    (void)hipEventDestroy(p.e0);
+    (void)hipEventDestroy(p.e1);
+  }
+  c->pending.clear();
+}
+
+// get_Mg (smoothing.jl:12-25)
+double get_Mg(scs_ctx* c, double Mh, double nu, double mu, int64_t n) {
+  if (Mh < 0) fail(c, SCS_ERR_REF, "Mh must be nonnegative.");
+  if (mu <= 0) fail(c, SCS_ERR_REF, "μ must be positive.");
+  if (0 < nu && nu <= 3) return std::pow((double)n, (3 - nu) / 2) * std::pow(mu, nu / 2 - 2) * Mh;
+  if (nu > 3) return std::pow(mu, 4 - 3 * nu / 2) * Mh;
+  fail(c, SCS_ERR_REF, "ν must be positive.");
+}
+
+double jl_min_h(double x, double y) {
+  auto isless = [](double a, double b) { return (a < b) || (std::signbit(a) && !std::signbit(b)); };
+  return (std::isnan(x) || (!std::isnan(y) && isless(x, y))) ? x : y;
+}
+
+bool same_x(const std::vector<double>& key, const double* x, int64_t m) {
+  return (int64_t)key.size() == m && std::memcmp(key.data(), x, sizeof(double) * m) == 0;
+}
+
+ProxArgsH prox_args(scs_ctx* c) {
+  ProxArgsH P;
+  P.reg = c->reg;
+  P.use_prox = c->use_prox;
+  P.lam = c->lam;
+  P.lam2 = c->lam2;
+  P.lb = c->clb;
+  P.ub = c->cub;
+  P.gstart = c->gstart;
+  P.gend = c->gend;
+  P.gw = c->gw;
+  P.ngroups = c->ngroups;
+  return P;
+}
+
+void require_ready(scs_ctx* c, bool need_method) {
+  if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
+  if (!c->loss_set) fail(c, SCS_ERR_STATE, "no loss: call scs_set_loss first");
+  if (!c->reg_set) fail(c, SCS_ERR_STATE, "no regularizer: call scs_set_reg first");
+  if (need_method && !c->smooth_set) fail(c, SCS_ERR_STATE, "no smoother: call scs_set_smoother first");
+  if (need_method && !c->method_set) fail(c, SCS_ERR_STATE, "no method: call scs_method_init first");
+}
+
+void allreduce(scs_ctx* c, double* buf, int64_t count) {
+  if (c->nranks <= 1) return;
+  if (!c->ar) fail(c, SCS_ERR_COMM, "multi-rank context without an all-reduce callback");
+  if (buf != c->red) fail(c, SCS_ERR_COMM, "internal: all-reduce payload must live in the reduce buffer");
+  if (count > c->red_cap) fail(c, SCS_ERR_COMM, "reduce buffer too small (%lld < %lld doubles)",
+                               (long long)c->red_cap, (long long)count);
+  hipEvent_t e0;
+  tbegin(c, T_REDUCE, &e0);
+  int rc = c->ar(buf, count, (void*)c->st, c->ar_user);
+  if (rc != 0) fail(c, SCS_ERR_COMM, "all-reduce callback returned %d", rc);
+  tend(c, T_REDUCE, e0);
+}
+
+// ---------------------------------------------------------------------------
+// workspace
+// ---------------------------------------------------------------------------
+void alloc_mspace(scs_ctx* c) {
+  const int64_t mp = c->mpad;
+  double** vs[] = {&c->x, &c->xp, &c->xn, &c->dxv, &c->gr, &c->Hr, &c->hinv, &c->zb, &c->d,
+                   &c->gq, &c->gqn, &c->gtmp, &c->gtmp2, &c->q, &c->gcache[0], &c->gcache[1]};
+  for (double** v : vs) {
+    dfree_t(c, *v);
+    *v = dalloc<double>(c, mp);
+  }
+  dfree_t(c, c->scal);
+  c->scal = dalloc<double>(c, 64);
+  if (!c->hscal) HCK(hipHostMalloc((void**)&c->hscal, 64 * sizeof(double), hipHostMallocDefault));
+}
+
+void alloc_nspace(scs_ctx* c) {
+  if (c->generic) return;
+  c->nsplit = gemv_n_splits(c->Npad, c->m);
+  c->nval = epilogue_blocks(c->Npad);
+  c->nchunk = gemv_t_chunks(c->Npad);
+  dfree_t(c, c->zpart);
+  dfree_t(c, c->z);
+  dfree_t(c, c->gN);
+  dfree_t(c, c->hN);
+  dfree_t(c, c->wN);
+  dfree_t(c, c->vN);
+  dfree_t(c, c->valpart);
+  dfree_t(c, c->tpart);
+  c->zpart = dalloc<double>(c, (size_t)c->nsplit * c->Npad);
+  c->z = dalloc<double>(c, c->Npad);
+  c->gN = dalloc<double>(c, c->Npad);
+  c->hN = dalloc<double>(c, c->Npad);
+  c->wN = dalloc<double>(c, c->Npad);
+  c->vN = dalloc<double>(c, c->Npad);
+  c->valpart = dalloc<double>(c, c->nval);
+  c->tpart = dalloc<double>(c, (size_t)c->nchunk * c->mpad);
+}
+
+void ensure_gram(scs_ctx* c) {
+  if (c->G) return;
+  const int64_t mp = c->mpad;
+  c->G = dalloc<double>(c, (size_t)mp * mp);
+  c->Gc = dalloc<double>(c, (size_t)mp * mp);
+  const int nb = (int)(mp / 128);
+  std::vector<int2> tl((size_t)nb * (nb + 1) / 2);
+  int nt = 0;
+  gram_tile_list(nb, tl.data(), &nt);
+  c->tiles = dalloc<int2>(c, nt);
+  HCK(hipMemcpyAsync(c->tiles, tl.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->st));
+  c->ntiles = nt;
+  c->dinfo = dalloc<rocblas_int>(c, 1);
+  c->ipiv = dalloc<rocblas_int>(c, mp);
+  if (!c->blas) {
+    RCK(rocblas_create_handle(&c->blas));
+    RCK(rocblas_set_stream(c->blas, c->st));
+  }
+  sync(c);
+}
+
+void invalidate_caches(scs_ctx* c) {
+  c->zvalid = false;
+  c->gvalid[0] = c->gvalid[1] = false;
+}
+
+// ---------------------------------------------------------------------------
+// f / ∇f building blocks
+// ---------------------------------------------------------------------------
+// finalize a loss sum: the per-kind constant of f (see epilogue_kernel)
+double loss_scale_value(scs_ctx* c, double s) {
+  switch (c->loss) {
+    case SCS_LOSS_LOGISTIC_MARGIN: return c->scale * s;
+    case SCS_LOSS_LOGISTIC_CE: return -c->scale * s;
+    case SCS_LOSS_LEAST_SQUARES: return 0.5 * s * c->scale;
+    default: return s;
+  }
+}
+
+// Forward pass at the device vector xd whose host copy is xh: z = A x (or the
+// cached z), then the epilogue with `flags`.  Always refreshes the f-value
+// cache; returns f(x) (global).
+double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
+  const bool cached = c->zvalid && same_x(c->zkey, xh, c->m);
+  hipEvent_t e0;
+  if (!cached) {
+    tbegin(c, T_GEMV, &e0);
+    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, c->nsplit, c->zpart, c->Npad, c->st));
+    tend(c, T_GEMV, e0);
+    flags |= EPI_Z | EPI_VAL;
+    HCK(launch_epilogue(c->loss, c->ggn, flags, c->zpart, c->nsplit, c->Npad, c->y, c->N, c->Npad, c->scale, c->z,
+                        c->gN, c->hN, c->wN, c->vN, c->valpart, c->st));
+    // loss sum -> scal[8] (reduce buffer slot 0 in multi-rank)
+    double* dst = (c->nranks > 1) ? c->red : c->scal + 8;
+    HCK(launch_sum_partials(c->valpart, c->nval, dst, c->st));
+    allreduce(c, c->red, 1);
+    if (c->nranks > 1) HCK(hipMemcpyAsync(c->scal + 8, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+    d2h(c, c->hscal + 8, c->scal + 8, 1);
+    sync(c);
+    c->zfval = loss_scale_value(c, c->hscal[8]);
+    c->zkey.assign(xh, xh + c->m);
+    c->zvalid = true;
+  } else if (flags & ~(EPI_VAL | EPI_Z)) {
+    flags &= ~(EPI_Z | EPI_VAL);
+    HCK(launch_epilogue(c->loss, c->ggn, flags, c->z, 1, c->Npad, c->y, c->N, c->Npad, c->scale, c->z, c->gN, c->hN,
+                        c->wN, c->vN, c->valpart, c->st));
+  }
+  return c->zfval;
+}
+
+// out (device, m) = Aᵀ v (local, then all-reduced across ranks)
+void gemv_t_global(scs_ctx* c, const double* v, double* out) {
+  hipEvent_t e0;
+  tbegin(c, T_GEMV, &e0);
+  HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
+  tend(c, T_GEMV, e0);
+  if (c->nranks > 1) {
+    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, c->red, c->st));
+    allreduce(c, c->red, c->m);
+    HCK(hipMemcpyAsync(out, c->red, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+  } else {
+    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, out, c->st));
+  }
+}
+
+// f(x) for a device vector with host copy xh
+double eval_f_dev(scs_ctx* c, const double* xh, const double* xd) {
+  if (c->loss == SCS_LOSS_ROSENBROCK) {
+    HCK(launch_rosen(xd, c->m, 0, c->scal + 8, nullptr, 0, c->st));
+    d2h(c, c->hscal + 8, c->scal + 8, 1);
+    sync(c);
+    return c->hscal[8];
+  }
+  if (c->loss == SCS_LOSS_QUADRATIC) {
+    // 1/2*(x'*(A*x)) + y'*x
+    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, 1, c->zpart, c->Npad, c->st));
+    HCK(launch_dot(xd, c->zpart, c->m, c->scal + 8, c->st));
+    HCK(launch_dot(c->y, xd, c->m, c->scal + 9, c->st));
+    d2h(c, c->hscal + 8, c->scal + 8, 2);
+    sync(c);
+    return 0.5 * c->hscal[8] + c->hscal[9];
+  }
+  return forward(c, xh, xd, 0);
+}
+
+// ∇f(x) -> out (device)
+void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
+  if (c->loss == SCS_LOSS_ROSENBROCK) {
+    HCK(launch_rosen(xd, c->m, 1, out, nullptr, 0, c->st));
+    return;
+  }
+  if (c->loss == SCS_LOSS_QUADRATIC) {
+    // 0.5*(A*x + Aᵀ*x) + y
+    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, 1, c->zpart, c->Npad, c->st));
+    gemv_t_global(c, xd, c->gtmp2);
+    HCK(launch_axpby(c->zpart, 1.0, c->gtmp2, c->m, c->gtmp2, c->st));
+    HCK(launch_axpby(c->y, 0.5, c->gtmp2, c->m, out, c->st));  // y + 0.5*(Ax + Aᵀx)
+    return;
+  }
+  forward(c, xh, xd, EPI_GRAD);
+  gemv_t_global(c, c->gN, out);
+}
+
+// ∇q(x) = ∇f(x) + λ hμ.grad(x) -> out (device); uses the 2-slot cache.
+void grad_q_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
+  for (int s = 0; s < 2; ++s)
+    if (c->gvalid[s] && same_x(c->gkey[s], xh, c->m)) {
+      HCK(hipMemcpyAsync(out, c->gcache[s], sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+      return;
+    }
+  grad_f_dev(c, xh, xd, c->gtmp);
+  HCK(launch_smoother(c->smooth, xd, c->m, c->mu, c->slb, c->sub, c->wel, c->zb, c->hinv, c->st));
+  HCK(launch_axpby(c->gtmp, c->lam, c->zb, c->m, out, c->st));
+  const int s = c->gnext;
+  c->gnext ^= 1;
+  HCK(hipMemcpyAsync(c->gcache[s], out, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+  c->gkey[s].assign(xh, xh + c->m);
+  c->gvalid[s] = true;
+}
+
+double eval_reg_dev(scs_ctx* c, const double* xd) {
+  HCK(launch_reg_value(prox_args(c), xd, c->m, c->scal + 10, c->st));
+  d2h(c, c->hscal + 10, c->scal + 10, 1);
+  sync(c);
+  return c->hscal[10];
+}
+
+// linesearch (utils.jl:27-35): Armijo with ρ = 0.5, c = 1e-4 and no cap.
+// obj(x) and grad_q(x) are evaluated once (the reference re-evaluates the
+// same deterministic values on every trial).
+double line_search(scs_ctx* c, const double* xh, const double* xd, const double* dd) {
+  const double f0 = eval_f_dev(c, xh, xd) + eval_reg_dev(c, xd);
+  grad_q_dev(c, xh, xd, c->gqn);
+  HCK(launch_dot(c->gqn, dd, c->m, c->scal + 11, c->st));
+  d2h(c, c->hscal + 11, c->scal + 11, 1);
+  sync(c);
+  const double gd = c->hscal[11];
+  std::vector<double> xt(c->m);
+  double alpha = 1.0;
+  for (int trial = 0; trial < 100000; ++trial) {
+    HCK(launch_trial_point(xd, dd, alpha, c->m, c->zb, c->st));
+    d2h(c, xt.data(), c->zb, c->m);
+    sync(c);
+    // trial point evaluated at a scratch copy (keeps xd / caches intact)
+    HCK(hipMemcpyAsync(c->gtmp2, c->zb, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+    const double ft = eval_f_dev(c, xt.data(), c->gtmp2) + eval_reg_dev(c, c->gtmp2);
+    if (!(ft > f0 + 1e-4 * alpha * gd)) return alpha;
+    alpha = 0.5 * alpha;
+  }
+  fail(c, SCS_ERR_REF, "linesearch did not terminate");
+}
+
+// solve (G + λ diag Hr) sol = rhs in place (rhs -> sol).  Cholesky first; LU
+// with partial pivoting (the reference's `\`, prox-N-SCORE.jl:204) when the
+// matrix is not numerically SPD (e.g. the indefinite Q of a CE loss on ±1
+// labels, test/test_algs.jl:10).
+void solve_system(scs_ctx* c, double* rhs) {
+  const int64_t m = c->m, ld = c->mpad;
+  hipEvent_t e0;
+  tbegin(c, T_SOLVE, &e0);
+  HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * m, hipMemcpyDeviceToDevice, c->st));
+  RCK(rocsolver_dpotrf(c->blas, rocblas_fill_lower, (rocblas_int)m, c->G, (rocblas_int)ld, c->dinfo));
+  int info = 0;
+  HCK(hipMemcpyAsync(&info, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  if (info == 0) {
+    RCK(rocsolver_dpotrs(c->blas, rocblas_fill_lower, (rocblas_int)m, 1, c->G, (rocblas_int)ld, rhs,
+                         (rocblas_int)m));
+    c->lu_fallback_used = false;
+  } else {
+    HCK(launch_symmetrize(c->Gc, ld, m, c->st));
+    RCK(rocsolver_dgetrf(c->blas, (rocblas_int)m, (rocblas_int)m, c->Gc, (rocblas_int)ld, c->ipiv, c->dinfo));
+    HCK(hipMemcpyAsync(&info, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
+    RCK(rocsolver_dgetrs(c->blas, rocblas_operation_none, (rocblas_int)m, 1, c->Gc, (rocblas_int)ld, c->ipiv, rhs,
+                         (rocblas_int)m));
+    c->lu_fallback_used = true;
+  }
+  tend(c, T_SOLVE, e0);
+}
+
+// Gram of the local rows with weights w -> c->G (single rank) or the packed
+// reduce buffer (multi-rank; then all-reduced together with `vec`).
+void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
+  ensure_gram(c);
+  hipEvent_t e0;
+  if (c->nranks > 1) {
+    const int64_t tsz = (int64_t)c->ntiles * 128 * 128;
+    tbegin(c, T_GRAM, &e0);
+    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->red, c->mpad, 1, c->st));
+    tend(c, T_GRAM, e0);
+    HCK(hipMemcpyAsync(c->red + tsz, vec_dev, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+    allreduce(c, c->red, tsz + c->m);
+    HCK(gram_unpack_launch(c->red, c->tiles, c->ntiles, c->G, c->mpad, c->st));
+    HCK(hipMemcpyAsync(vec_dev, c->red + tsz, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+  } else {
+    tbegin(c, T_GRAM, &e0);
+    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->st));
+    tend(c, T_GRAM, e0);
+  }
+}
+
+// fixed step-size rules shared by ProxNSCORE / ProxGGNSCORE
+double step_size_newton(scs_ctx* c, int64_t iter, bool* needs_ls) {
+  *needs_ls = false;
+  if (c->ss_type == 1 && c->has_L) return jl_min_h(1 / c->L, 1.0);
+  if (c->ss_type == 1 && !c->has_L) return 0.5;
+  if (c->ss_type == 2) {
+    if (iter == 1) return 1.0;
+    // prox-N-SCORE.jl:81-83 / prox-GGN-SCORE.jl:78-80 call hμ.grad(x_prev) with one
+    // argument and use an undefined ∇f: the reference raises a MethodError here.
+    fail(c, SCS_ERR_REF, "MethodError: ss_type=2 calls hμ.grad(x_prev) with the wrong arity (reference bug, "
+                         "prox-N-SCORE.jl:81 / prox-GGN-SCORE.jl:78)");
+  }
+  if (c->ss_type == 3) {
+    *needs_ls = true;
+    return 0.0;
+  }
+  fail(c, SCS_ERR_REF, "Please, choose ss_type in [1, 2, 3].");
+}
+
+// ProxNSCORE / ProxGGNSCORE step
+void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, double* dx, double* pri) {
+  const int64_t m = c->m;
+  HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
+  ensure_gram(c);
+  if (c->method == SCS_PROX_NSCORE) {
+    // H = hess_fx, ∇q = grad_fx + λ gr  (prox-N-SCORE.jl:183-204)
+    if (c->loss == SCS_LOSS_ROSENBROCK) {
+      HCK(launch_rosen(c->x, m, 2, nullptr, c->G, c->mpad, c->st));
+      HCK(launch_rosen(c->x, m, 1, c->gtmp, nullptr, 0, c->st));
+    } else if (c->loss == SCS_LOSS_QUADRATIC) {
+      HCK(launch_half_sym(c->A, c->Npad, m, c->G, c->mpad, c->st));
+      grad_f_dev(c, xh, c->x, c->gtmp);
+    } else {
+      forward(c, xh, c->x, EPI_GRAD | EPI_HESS);
+      // local Aᵀg (not yet reduced); reduced together with the Gram
+      HCK(launch_gemv_t(c->A, c->Npad, c->Npad, m, c->mpad, c->gN, c->tpart, c->st));
+      HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, m, c->gtmp, c->st));
+      gram_and_reduce(c, c->hN, c->gtmp);
+    }
+  } else {
+    if (c->ggn == SCS_GGN_NONE) fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs an out_fn / GGN loss kind");
+    // J, residual, Q (prox-GGN-SCORE.jl:44-56) -> w = s²q, v = s·r
+    forward(c, xh, c->x, EPI_GGN);
+    HCK(launch_gemv_t(c->A, c->Npad, c->Npad, m, c->mpad, c->vN, c->tpart, c->st));
+    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, m, c->gtmp, c->st));
+    gram_and_reduce(c, c->wN, c->gtmp);
+  }
+  // rhs = ∇f + λ gr (NSCORE) | Jᵀr + λ gr (GGN: Jt*[r;1], prox-GGN-SCORE.jl:121-130)
+  HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
+  HCK(launch_diag_add(c->G, c->mpad, m, c->lam, c->Hr, c->st));
+  solve_system(c, c->gq);
+  HCK(launch_neg(c->gq, m, c->d, c->st));  // d = -sol
+  bool ls = false;
+  double step = step_size_newton(c, iter, &ls);
+  if (ls) step = line_search(c, xh, c->x, c->d);
+  const double Mg = get_Mg(c, c->Mh, c->nu, c->mu, m);
+  HCK(launch_score_tail(c->x, c->d, c->gr, c->Hr, m, c->lam, Mg, step, nullptr, prox_args(c), c->hinv, c->zb, c->xn,
+                        c->dxv, c->scal, c->st));
+  d2h(c, x_new, c->xn, m);
+  if (dx) d2h(c, dx, c->dxv, m);
+  d2h(c, c->hscal, c->scal, 4);
+  sync(c);
+  *pri = c->hscal[0];
+}
+
+// ProxLQNSCORE step (prox-L-BFGS-SCORE.jl:69-169)
+void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, double* x_new, double* dx,
+              double* pri) {
+  const int64_t m = c->m;
+  HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
+  grad_q_dev(c, xh, c->x, c->gq);  // ∇q = grad_f(x) + λgr
+  const int k = (int)c->ring.size();
+  if (iter == 1 || k == 0) {
+    HCK(launch_neg(c->gq, m, c->d, c->st));
+  } else {
+    HCK(hipMemcpyAsync(c->d_order, c->ring.data(), sizeof(int) * k, hipMemcpyHostToDevice, c->st));
+    HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->st));
+  }
+  double step = 0.0;
+  const double* step_dev = nullptr;
+  if (c->ss_type == 1 && c->has_L) {
+    step = jl_min_h(1 / c->L, 1.0);
+  } else if (c->ss_type == 1 && !c->has_L) {
+    step = 0.5;
+  } else if (c->ss_type == 2 || !c->has_L) {
+    if (iter == 1) {
+      step = 1.0;
+    } else {
+      grad_q_dev(c, xph, c->xp, c->gqn);  // ∇q(x_prev)
+      HCK(launch_bb_step(c->x, c->xp, c->gq, c->gqn, m, c->scal + 12, c->st));
+      step_dev = c->scal + 12;
+    }
+  } else if (c->ss_type == 3) {
+    step = line_search(c, xh, c->x, c->d);
+  } else {
+    fail(c, SCS_ERR_REF, "Please, choose ss_type in [1, 2, 3].");
+  }
+  const double Mg = get_Mg(c, c->Mh, c->nu, c->mu, m);
+  HCK(launch_score_tail(c->x, c->d, c->gr, c->Hr, m, c->lam, Mg, step, step_dev, prox_args(c), c->hinv, c->zb, c->xn,
+                        c->dxv, c->scal, c->st));
+  d2h(c, x_new, c->xn, m);
+  if (dx) d2h(c, dx, c->dxv, m);
+  d2h(c, c->hscal, c->scal, 4);
+  sync(c);
+  *pri = c->hscal[0];
+  // δh = x_new − x (prox) | dx ; ∇q_new = grad_f(x_new) + λ gr(x_new)
+  const double* dh = c->use_prox ? c->zb : c->dxv;
+  if (c->use_prox) HCK(launch_sub(c->xn, c->x, m, c->zb, c->st));
+  // keep δh safe from grad_q_dev's scratch use of zb
+  HCK(hipMemcpyAsync(c->q, dh, sizeof(double) * m, hipMemcpyDeviceToDevice, c->st));
+  grad_q_dev(c, x_new, c->xn, c->gqn);
+  const int slot = c->spare;
+  HCK(launch_lbfgs_update(c->q, c->gqn, c->gq, m, c->S + (int64_t)slot * c->mpad, c->Yv + (int64_t)slot * c->mpad,
+                          c->scal + 16, c->st));
+  d2h(c, c->hscal + 16, c->scal + 16, 2);
+  sync(c);
+  const double dg = c->hscal[16], gg = c->hscal[17];
+  if (dg > 1e-10) {  // prox-L-BFGS-SCORE.jl:154-162
+    if ((int)c->ring.size() == c->mem) {
+      c->spare = c->ring.front();
+      c->ring.erase(c->ring.begin());
+    } else {
+      // the next unused physical slot becomes the spare
+      std::vector<bool> used(c->mem + 1, false);
+      for (int r : c->ring) used[r] = true;
+      used[slot] = true;
+      for (int i = 0; i <= c->mem; ++i)
+        if (!used[i]) { c->spare = i; break; }
+    }
+    c->ring.push_back(slot);
+    c->H0 = dg / gg;
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+const char* scs_version(void) { return "libscsopt 0.1.0 (gfx950)"; }
+
+int scs_create(int device, void* stream, scs_ctx** out) {
+  if (!out) return SCS_ERR_ARG;
+  *out = nullptr;
+  scs_ctx* c = new scs_ctx();
+  int rc = guarded(c, [&] {
+    HCK(hipSetDevice(device));
+    c->dev = device;
+    if (stream) {
+      c->st = (hipStream_t)stream;
+    } else {
+      HCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+      c->own_stream = true;
+    }
+  });
+  if (rc != SCS_OK) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return SCS_OK;
+}
+
+int scs_destroy(scs_ctx* c) {
+  if (!c) return SCS_OK;
+  (void)hipSetDevice(c->dev);
+  (void)hipStreamSynchronize(c->st);
+  for (auto& p : c->pending) {
+    (void)hipEventDestroy(p.e0);
+    (void)hipEventDestroy(p.e1);
+  }
+  for (auto& a : c->allocs) (void)hipFree(a.p);
+  if (c->hscal) (void)hipHostFree(c->hscal);
+  if (c->blas) (void)rocblas_destroy_handle(c->blas);
+  if (c->own_stream) (void)hipStreamDestroy(c->st);
+  delete c;
+  return SCS_OK;
+}
+
+const char* scs_last_error(const scs_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int scs_get_stream(scs_ctx* c, void** stream) {
+  return guarded(c, [&] { *stream = (void*)c->st; });
+}
+
+int scs_set_comm(scs_ctx* c, int rank, int nranks, scs_allreduce_fn fn, void* user) {
+  return guarded(c, [&] {
+    if (nranks < 1 || rank < 0 || rank >= nranks) fail(c, SCS_ERR_ARG, "bad rank/nranks %d/%d", rank, nranks);
+    if (nranks > 1 && !fn) fail(c, SCS_ERR_ARG, "nranks > 1 needs an all-reduce callback");
+    c->rank = rank;
+    c->nranks = nranks;
+    c->ar = fn;
+    c->ar_user = user;
+  });
+}
+
+int scs_reduce_buffer_size(scs_ctx* c, int64_t* nd) {
+  return guarded(c, [&] {
+    if (!c->has_data) fail(c, SCS_ERR_STATE, "reduce buffer size needs the data dimensions");
+    const int64_t nb = c->mpad / 128;
+    const int64_t tsz = nb * (nb + 1) / 2 * 128 * 128;
+    *nd = std::max<int64_t>(tsz + c->mpad, c->mpad) + 64;
+  });
+}
+
+int scs_set_reduce_buffer(scs_ctx* c, void* p, int64_t nd) {
+  return guarded(c, [&] {
+    c->red = (double*)p;
+    c->red_cap = nd;
+  });
+}
+
+static void set_dims(scs_ctx* c, int64_t N, int64_t m, int64_t Nglob, int64_t row0) {
+  if (m <= 0 || N < 0) fail(c, SCS_ERR_ARG, "bad dimensions N=%lld m=%lld", (long long)N, (long long)m);
+  c->N = N;
+  c->m = m;
+  c->Npad = std::max<int64_t>(round_up(std::max<int64_t>(N, 1), 16), 16);
+  c->mpad = round_up(m, 128);
+  c->Nglob = Nglob > 0 ? Nglob : N;
+  c->row0 = row0;
+}
+
+static void reset_data(scs_ctx* c) {
+  dfree_t(c, c->A);
+  dfree_t(c, c->y);
+  dfree_t(c, c->G);
+  dfree_t(c, c->Gc);
+  dfree_t(c, c->tiles);
+  c->ntiles = 0;
+  invalidate_caches(c);
+  c->has_data = false;
+  c->reg_set = c->smooth_set = c->method_set = false;
+}
+
+int scs_set_data(scs_ctx* c, int64_t N, int64_t m, const double* A, int64_t lda, const double* y, int64_t Nglob,
+                 int64_t row0) {
+  return guarded(c, [&] {
+    HCK(hipSetDevice(c->dev));
+    reset_data(c);
+    set_dims(c, N, m, Nglob, row0);
+    c->generic = (A == nullptr);
+    if (!c->generic) {
+      if (lda < N) fail(c, SCS_ERR_ARG, "lda (%lld) < N (%lld)", (long long)lda, (long long)N);
+      c->A = dalloc<double>(c, (size_t)c->Npad * c->mpad);
+      c->y = dalloc<double>(c, c->Npad);
+      if (N > 0) {
+        HCK(hipMemcpy2DAsync(c->A, sizeof(double) * c->Npad, A, sizeof(double) * lda, sizeof(double) * N, m,
+                             hipMemcpyHostToDevice, c->st));
+        if (y) h2d(c, c->y, y, N);
+      }
+    }
+    alloc_mspace(c);
+    alloc_nspace(c);
+    sync(c);
+    c->has_data = true;
+  });
+}
+
+int scs_gen_data(scs_ctx* c, const scs_synth* s) {
+  return guarded(c, [&] {
+    if (!s) fail(c, SCS_ERR_ARG, "null synth spec");
+    HCK(hipSetDevice(c->dev));
+    reset_data(c);
+    set_dims(c, s->N, s->m, s->N_global, s->row0);
+    c->generic = false;
+    c->A = dalloc<double>(c, (size_t)c->Npad * c->mpad);
+    c->y = dalloc<double>(c, c->Npad);
+    alloc_mspace(c);
+    alloc_nspace(c);
+    const double scale = (s->kind == 3) ? 1.0 : 1.0 / std::sqrt((double)s->m);
+    HCK(launch_gen_A(c->A, c->Npad, c->N, c->mpad, c->row0, s->seed, scale, c->st));
+    // the padded columns beyond m must be zero: generate with m columns of data
+    if (c->mpad > c->m)
+      HCK(hipMemsetAsync(c->A + c->m * c->Npad, 0, sizeof(double) * c->Npad * (c->mpad - c->m), c->st));
+    HCK(launch_gen_xtrue(c->xn, c->m, s->seed, s->density, c->st));
+    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, c->xn, 1, c->zpart, c->Npad, c->st));
+    HCK(launch_gen_y(s->kind, c->zpart, c->y, c->N, c->row0, s->seed, c->st));
+    sync(c);
+    c->has_data = true;
+  });
+}
+
+int scs_get_data(scs_ctx* c, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y) {
+  return guarded(c, [&] {
+    if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    if (r0 < 0 || nr < 0 || r0 + nr > c->N) fail(c, SCS_ERR_ARG, "row range out of bounds");
+    if (A && nr > 0)
+      HCK(hipMemcpy2DAsync(A, sizeof(double) * lda_out, c->A + r0, sizeof(double) * c->Npad, sizeof(double) * nr,
+                           c->m, hipMemcpyDeviceToHost, c->st));
+    if (y && nr > 0) d2h(c, y, c->y + r0, nr);
+    sync(c);
+  });
+}
+
+int scs_get_dims(scs_ctx* c, int64_t* N, int64_t* m, int64_t* Ng, int64_t* r0) {
+  return guarded(c, [&] {
+    if (N) *N = c->N;
+    if (m) *m = c->m;
+    if (Ng) *Ng = c->Nglob;
+    if (r0) *r0 = c->row0;
+  });
+}
+
+int scs_set_loss(scs_ctx* c, int loss, int ggn, double scale) {
+  return guarded(c, [&] {
+    if (loss < SCS_LOSS_LOGISTIC_MARGIN || loss > SCS_LOSS_ROSENBROCK) fail(c, SCS_ERR_ARG, "unknown loss %d", loss);
+    if (ggn < SCS_GGN_NONE || ggn > SCS_GGN_LINEAR_LS) fail(c, SCS_ERR_ARG, "unknown ggn kind %d", ggn);
+    if ((loss == SCS_LOSS_QUADRATIC || loss == SCS_LOSS_ROSENBROCK) && c->nranks > 1)
+      fail(c, SCS_ERR_ARG, "quadratic / Rosenbrock problems are not row-sharded");
+    c->loss = loss;
+    c->ggn = ggn;
+    c->scale = scale;
+    c->loss_set = true;
+    invalidate_caches(c);
+  });
+}
+
+static double* upload_bounds(scs_ctx* c, double* old, const double* v, int64_t nb, bool sanitize, bool lower) {
+  dfree_t(c, old);
+  std::vector<double> h(c->mpad, 0.0);
+  for (int64_t i = 0; i < c->m; ++i) {
+    double b = (nb == 1) ? v[0] : v[i];
+    if (sanitize) {
+      if (lower && b == -INFINITY) b = -1e32;  // L_INF_CACHE, prox-reg-utils.jl:6
+      if (!lower && b == INFINITY) b = 1e32;   // U_INF_CACHE
+    }
+    h[i] = b;
+  }
+  double* d = dalloc<double>(c, c->mpad);
+  h2d(c, d, h.data(), c->mpad);
+  sync(c);
+  return d;
+}
+
+int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* lb, const double* ub, int64_t nbound,
+                const int64_t* ind, int64_t ngroups) {
+  return guarded(c, [&] {
+    if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the regularizer");
+    if (reg < SCS_REG_L1 || reg > SCS_REG_GL) fail(c, SCS_ERR_REF, "reg_name not valid.");
+    if (nlam < 1 || nlam > 2 || !lam) fail(c, SCS_ERR_ARG, "λ must have 1 or 2 entries");
+    if (reg == SCS_REG_GL && nlam != 2)
+      fail(c, SCS_ERR_REF, "Please provide a Tuple or Vector with exactly two entries for λ, e.g. [λ1, λ2]");
+    c->reg = reg;
+    c->nlam = nlam;
+    c->lam = lam[0];  // step! uses λ = model.λ[1] when length(λ) > 1
+    c->lam2 = nlam > 1 ? lam[1] : 0.0;
+    if (reg == SCS_REG_INDBOX) {
+      if (!lb || !ub || (nbound != 1 && nbound != c->m)) fail(c, SCS_ERR_ARG, "indbox needs C_set bounds (1 or m)");
+      c->clb = upload_bounds(c, c->clb, lb, nbound, false, true);
+      c->cub = upload_bounds(c, c->cub, ub, nbound, false, false);
+    }
+    if (reg == SCS_REG_GL) {
+      if (!ind || ngroups < 1) fail(c, SCS_ERR_ARG, "gl needs the group index matrix");
+      std::vector<int> hs(ngroups), he(ngroups);
+      std::vector<double> hw(ngroups), wel(c->mpad, 0.0);
+      int64_t expect = 1;
+      for (int64_t g = 0; g < ngroups; ++g) {
+        const int64_t s = ind[3 * g], e = ind[3 * g + 1], w = ind[3 * g + 2];
+        if (s != expect || e < s || e > c->m)
+          fail(c, SCS_ERR_ARG, "groups must tile 1..m contiguously (group %lld = %lld:%lld)", (long long)g + 1,
+               (long long)s, (long long)e);
+        expect = e + 1;
+        hs[g] = (int)(s - 1);
+        he[g] = (int)(e - 1);
+        hw[g] = (double)w;
+        for (int64_t k = s - 1; k < e; ++k) wel[k] = (double)w;
+      }
+      if (expect != c->m + 1) fail(c, SCS_ERR_ARG, "groups must tile 1..m (covered 1..%lld)", (long long)expect - 1);
+      dfree_t(c, c->gstart);
+      dfree_t(c, c->gend);
+      dfree_t(c, c->gw);
+      dfree_t(c, c->wel);
+      c->gstart = dalloc<int>(c, ngroups);
+      c->gend = dalloc<int>(c, ngroups);
+      c->gw = dalloc<double>(c, ngroups);
+      c->wel = dalloc<double>(c, c->mpad);
+      HCK(hipMemcpyAsync(c->gstart, hs.data(), sizeof(int) * ngroups, hipMemcpyHostToDevice, c->st));
+      HCK(hipMemcpyAsync(c->gend, he.data(), sizeof(int) * ngroups, hipMemcpyHostToDevice, c->st));
+      h2d(c, c->gw, hw.data(), ngroups);
+      h2d(c, c->wel, wel.data(), c->mpad);
+      c->ngroups = (int)ngroups;
+      sync(c);
+    }
+    c->reg_set = true;
+  });
+}
+
+int scs_set_smoother(scs_ctx* c, int kind, double mu, double Mh, double nu, const double* lb, const double* ub,
+                     int64_t nbound) {
+  return guarded(c, [&] {
+    if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the smoother");
+    if (kind < SCS_SMOOTH_PHUBER_L1L2 || kind > SCS_SMOOTH_EXP_INDBOX) fail(c, SCS_ERR_ARG, "unknown smoother %d", kind);
+    if (kind == SCS_SMOOTH_PHUBER_INDBOX || kind == SCS_SMOOTH_EXP_INDBOX) {
+      if (!lb || !ub || (nbound != 1 && nbound != c->m))
+        fail(c, SCS_ERR_REF, "Lengths of the bounds do not match that of the variable.");
+      c->slb = upload_bounds(c, c->slb, lb, nbound, true, true);
+      c->sub = upload_bounds(c, c->sub, ub, nbound, true, false);
+    }
+    if (kind == SCS_SMOOTH_PHUBER_GL && !c->wel) fail(c, SCS_ERR_STATE, "PHuberSmootherGL needs the gl groups (scs_set_reg)");
+    c->smooth = kind;
+    c->mu = mu;
+    c->Mh = Mh;
+    c->nu = nu;
+    c->smooth_set = true;
+    invalidate_caches(c);
+  });
+}
+
+int scs_set_L(scs_ctx* c, int has_L, double L) {
+  return guarded(c, [&] {
+    c->has_L = has_L != 0;
+    c->L = L;
+  });
+}
+
+int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) {
+  return guarded(c, [&] {
+    if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the method");
+    if (method < SCS_PROX_NSCORE || method > SCS_PROX_LQNSCORE) fail(c, SCS_ERR_ARG, "unknown method %d", method);
+    if (method == SCS_PROX_GGNSCORE && (c->generic || c->loss == SCS_LOSS_QUADRATIC))
+      fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs a data problem with an out_fn (GGN kind)");
+    if (method == SCS_PROX_GGNSCORE && c->N + 1 <= c->m)
+      fail(c, SCS_ERR_ARG, "ProxGGNSCORE sample-space branch (N+1 <= m, prox-GGN-SCORE.jl:124-127) is not "
+                           "implemented on the device yet");
+    c->method = method;
+    c->ss_type = ss_type;
+    c->use_prox = use_prox;
+    c->mem = mem;
+    if (method == SCS_PROX_LQNSCORE) {
+      if (mem < 1) fail(c, SCS_ERR_ARG, "L-BFGS memory must be >= 1");
+      dfree_t(c, c->S);
+      dfree_t(c, c->Yv);
+      dfree_t(c, c->d_order);
+      dfree_t(c, c->ab);
+      c->S = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
+      c->Yv = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
+      c->d_order = dalloc<int>(c, mem + 1);
+      c->ab = dalloc<double>(c, 2 * (mem + 1));
+      sync(c);
+    }
+    // init! (prox-L-BFGS-SCORE.jl:31-36)
+    c->ring.clear();
+    c->spare = 0;
+    c->H0 = 1.0;
+    c->method_set = true;
+    invalidate_caches(c);
+  });
+}
+
+int scs_eval_f(scs_ctx* c, const double* x, double* fval) {
+  return guarded(c, [&] {
+    if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
+    if (!c->loss_set) fail(c, SCS_ERR_STATE, "no loss: call scs_set_loss first");
+    HCK(hipSetDevice(c->dev));
+    h2d(c, c->xn, x, c->m);
+    *fval = eval_f_dev(c, x, c->xn);
+  });
+}
+
+int scs_eval_grad(scs_ctx* c, const double* x, double* g) {
+  return guarded(c, [&] {
+    if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
+    if (!c->loss_set) fail(c, SCS_ERR_STATE, "no loss: call scs_set_loss first");
+    HCK(hipSetDevice(c->dev));
+    h2d(c, c->xn, x, c->m);
+    grad_f_dev(c, x, c->xn, c->gqn);
+    d2h(c, g, c->gqn, c->m);
+    sync(c);
+  });
+}
+
+int scs_eval_reg(scs_ctx* c, const double* x, double* gval) {
+  return guarded(c, [&] {
+    require_ready(c, false);
+    HCK(hipSetDevice(c->dev));
+    h2d(c, c->xn, x, c->m);
+    *gval = eval_reg_dev(c, c->xn);
+  });
+}
+
+int scs_step(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, double* x_new, double* dx,
+             double* pri) {
+  return guarded(c, [&] {
+    require_ready(c, true);
+    HCK(hipSetDevice(c->dev));
+    hipEvent_t e0;
+    tbegin(c, T_STEP, &e0);
+    h2d(c, c->x, x, c->m);
+    h2d(c, c->xp, x_prev ? x_prev : x, c->m);
+    std::vector<double> xnew_h(c->m);
+    if (c->method == SCS_PROX_LQNSCORE)
+      step_lqn(c, x, x_prev ? x_prev : x, iter, xnew_h.data(), dx, pri);
+    else
+      step_newton(c, x, iter, xnew_h.data(), dx, pri);
+    std::memcpy(x_new, xnew_h.data(), sizeof(double) * c->m);
+    tend(c, T_STEP, e0);
+    if (c->timing) tresolve(c);
+  });
+}
+
+int scs_smoother_eval(scs_ctx* c, const double* x, double* gr, double* Hr) {
+  return guarded(c, [&] {
+    if (!c->smooth_set) fail(c, SCS_ERR_STATE, "no smoother");
+    h2d(c, c->xn, x, c->m);
+    HCK(launch_smoother(c->smooth, c->xn, c->m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
+    d2h(c, gr, c->gr, c->m);
+    d2h(c, Hr, c->Hr, c->m);
+    sync(c);
+  });
+}
+
+int scs_prox_eval(scs_ctx* c, const double* z, const double* Hr, double lam, double alpha, double* out) {
+  return guarded(c, [&] {
+    if (!c->reg_set) fail(c, SCS_ERR_STATE, "no regularizer");
+    h2d(c, c->zb, z, c->m);
+    h2d(c, c->Hr, Hr, c->m);
+    ProxArgsH P = prox_args(c);
+    P.lam = lam;
+    HCK(launch_prox_only(P, c->zb, c->Hr, alpha, c->m, c->hinv, c->xn, c->st));
+    d2h(c, out, c->xn, c->m);
+    sync(c);
+  });
+}
+
+int scs_gram_eval(scs_ctx* c, const double* w, double* G, int64_t ldg) {
+  return guarded(c, [&] {
+    if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    std::vector<double> wp(c->Npad, 0.0);
+    std::memcpy(wp.data(), w, sizeof(double) * c->N);
+    h2d(c, c->wN, wp.data(), c->Npad);
+    ensure_gram(c);
+    hipEvent_t e0;
+    tbegin(c, T_GRAM, &e0);
+    HCK(gram_launch(c->A, c->Npad, c->wN, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->st));
+    tend(c, T_GRAM, e0);
+    HCK(hipMemcpy2DAsync(G, sizeof(double) * ldg, c->G, sizeof(double) * c->mpad, sizeof(double) * c->m, c->m,
+                         hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    if (c->timing) tresolve(c);
+  });
+}
+
+int scs_gemv_t_eval(scs_ctx* c, const double* v, double* out) {
+  return guarded(c, [&] {
+    if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    std::vector<double> vp(c->Npad, 0.0);
+    std::memcpy(vp.data(), v, sizeof(double) * c->N);
+    h2d(c, c->vN, vp.data(), c->Npad);
+    HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, c->vN, c->tpart, c->st));
+    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, c->gtmp, c->st));
+    d2h(c, out, c->gtmp, c->m);
+    sync(c);
+  });
+}
+
+int scs_gemv_n_eval(scs_ctx* c, const double* x, double* out) {
+  return guarded(c, [&] {
+    if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    h2d(c, c->xn, x, c->m);
+    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, c->xn, c->nsplit, c->zpart, c->Npad, c->st));
+    HCK(launch_epilogue(c->loss ? c->loss : SCS_LOSS_LEAST_SQUARES, SCS_GGN_NONE, EPI_Z, c->zpart, c->nsplit, c->Npad,
+                        c->y, c->N, c->Npad, 1.0, c->z, nullptr, nullptr, nullptr, nullptr, c->valpart, c->st));
+    d2h(c, out, c->z, c->N);
+    sync(c);
+    c->zvalid = false;
+  });
+}
+
+int scs_timing_enable(scs_ctx* c, int on) {
+  return guarded(c, [&] { c->timing = on != 0; });
+}
+
+int scs_timing_get(scs_ctx* c, scs_timing* t) {
+  return guarded(c, [&] {
+    tresolve(c);
+    t->gram_ms = c->tms[T_GRAM];
+    t->gram_calls = c->tcalls[T_GRAM];
+    t->gemv_ms = c->tms[T_GEMV];
+    t->gemv_calls = c->tcalls[T_GEMV];
+    t->solve_ms = c->tms[T_SOLVE];
+    t->solve_calls = c->tcalls[T_SOLVE];
+    t->step_ms = c->tms[T_STEP];
+    t->step_calls = c->tcalls[T_STEP];
+    t->reduce_ms = c->tms[T_REDUCE];
+    t->reduce_calls = c->tcalls[T_REDUCE];
+  });
+}
+
+int scs_timing_reset(scs_ctx* c) {
+  return guarded(c, [&] {
+    tresolve(c);
+    for (int i = 0; i < T_N; ++i) {
+      c->tms[i] = 0;
+      c->tcalls[i] = 0;
+    }
+  });
+}
+
+int scs_sync(scs_ctx* c) {
+  return guarded(c, [&] { sync(c); });
+}
+
+}  // extern "C"

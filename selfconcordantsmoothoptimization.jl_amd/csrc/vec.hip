@@ -1,0 +1,519 @@
+// Feature-space (length-m) kernels of the SCORE step: smoothers, the fused
+// SCORE tail (η, α, prox, primal residual), regularizer value, L-BFGS vector
+// algebra and small matrix fix-ups around the m x m solve.
+//
+// Reductions whose value feeds a decision or the history (η, ‖x_new − x‖,
+// dots of the two-loop recursion, get_reg) run in a fixed order (per-thread
+// sequential strides, then a fixed wave/block tree), so repeated runs are
+// bitwise identical.  Expressions follow the reference's evaluation order
+// so that, on identical inputs, elementwise outputs match the oracle bit for
+// bit (IEEE +,-,*,/,sqrt); pow() may differ by <= 1-2 ulp from Julia's.
+#include "common.h"
+#include "kernels.h"
+
+namespace scs {
+
+constexpr int VB = 1024;  // single-workgroup kernels: 16 waves
+
+// ---------------------------------------------------------------------------
+// Smoothers  (phuber-smooth.jl, exponential-smooth.jl)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double huber_grad_d(double x, double mu) {   // phuber-smooth.jl:31-33
+  return x * pow(mu * mu + x * x, -0.5);
+}
+__device__ __forceinline__ double huber_hess_d(double x, double mu) {   // phuber-smooth.jl:34-36
+  return (mu * mu) * pow(mu * mu + x * x, -1.5);
+}
+__device__ __forceinline__ double pseudo_huber_d(double x, double mu) { // phuber-smooth.jl:28-30
+  const double v = mu * mu + x * x;
+  return (mu * mu - mu * sqrt(v) + x * x) * pow(v, -0.5);
+}
+
+__global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64_t m, double mu,
+                                   const double* __restrict__ a, const double* __restrict__ b,
+                                   double* __restrict__ gr, double* __restrict__ Hr) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const double xi = x[i];
+  double g, h;
+  if (kind == SCS_SMOOTH_PHUBER_L1L2) {
+    g = huber_grad_d(xi, mu);
+    h = huber_hess_d(xi, mu);
+  } else if (kind == SCS_SMOOTH_PHUBER_INDBOX) {
+    const double ai = a[i], bi = b[i];
+    // huber_grad_indbox (phuber-smooth.jl:83-98): note the `-x < a` test.
+    if (-xi < ai) {
+      g = pow(ai * ai - 2.0 * xi * ai + mu * mu + xi * xi, -0.5) * (-xi + ai);
+    } else if (xi == ai || xi < bi) {
+      g = JL_EPS;
+    } else {
+      g = pow(bi * bi - 2.0 * bi * xi + mu * mu + xi * xi, -0.5) * (bi - xi);
+    }
+    // huber_hess_indbox (phuber-smooth.jl:99-114)
+    if (xi <= ai) {
+      h = (mu * mu) * pow(ai * ai - 2.0 * ai * xi + mu * mu + xi * xi, -1.5);
+    } else if (ai < xi && xi < bi) {
+      h = JL_EPS;
+    } else if (xi >= bi) {
+      h = (mu * mu) * pow(bi * bi - 2.0 * bi * xi + mu * mu + xi * xi, -1.5);
+    } else {
+      h = __builtin_nan("");  // NaN x: the reference leaves the entry undefined
+    }
+  } else {  // SCS_SMOOTH_EXP_INDBOX (exponential-smooth.jl:41-50)
+    const double e = exp((-xi + a[i]) / mu);
+    g = -e;
+    h = 1.0 / mu * e;
+  }
+  gr[i] = g;
+  Hr[i] = h;
+}
+
+// PHuberSmootherGL grad/hess (phuber-smooth.jl:150-164).  Cmat for a
+// contiguous partition is diag(group weight); the Hessian carries the global
+// dot(Dg, Dg).  Single workgroup: the dot is one fixed-order reduction.
+__global__ __launch_bounds__(VB) void smooth_gl_kernel(const double* __restrict__ x, int64_t m, double mu,
+                                                       const double* __restrict__ wel,
+                                                       double* __restrict__ gr, double* __restrict__ Hr) {
+  __shared__ double sh[VB / 64];
+  double part = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += VB) {
+    const double Dg = huber_grad_d(x[i], mu);
+    part += Dg * Dg;
+  }
+  const double dd = block_sum<VB>(part, sh);
+  for (int64_t i = threadIdx.x; i < m; i += VB) {
+    const double xi = x[i];
+    const double g = pseudo_huber_d(xi, mu);
+    const double Dg = huber_grad_d(xi, mu);
+    const double DDg = huber_hess_d(xi, mu);
+    const double Cg = wel[i] * g;
+    gr[i] = huber_grad_d(Cg, mu) * Dg;
+    Hr[i] = huber_hess_d(Cg, mu) * dd + huber_grad_d(Cg, mu) * DDg;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Prox operators (prox-operators.jl) -- elementwise parts
+// ---------------------------------------------------------------------------
+// h = 1 ./ Hr is passed as computed by the caller (Hdiag_inv).
+__device__ __forceinline__ double prox_l1_d(double z, double hinv, double lam, double alpha) {
+  const double t = (alpha * lam) / hinv;                      // prox-operators.jl:10
+  return jl_sign(z) * jl_max(fabs(z) - t, 0.0);               // prox-operators.jl:11
+}
+__device__ __forceinline__ double prox_l2_d(double z, double hinv, double lam, double alpha) {
+  const double t = (alpha * lam) / hinv;                      // prox-operators.jl:23
+  return z * jl_max(1.0 - t / (z * z), 0.0);                  // prox-operators.jl:24
+}
+__device__ __forceinline__ double prox_box_d(double z, double lb, double ub) {
+  return jl_min(jl_max(z, lb), ub);                           // prox-operators.jl:45
+}
+
+struct ProxArgs {
+  int reg;            // scs_reg_kind
+  int use_prox;
+  double lam;         // λ (λ1 for gl)
+  double lam2;        // λ2 (gl)
+  const double* lb;   // C_set lower (length m, raw, may be -Inf)
+  const double* ub;
+  const int* gstart;  // gl groups (0-based, contiguous partition)
+  const int* gend;
+  const double* gw;   // group weights (Int in the reference)
+  int ngroups;
+};
+
+// Elementwise prox + the gl group pass, inside one workgroup.
+// z: input (x + dx), hinv: 1/Hr, out: result.  step = α of invoke_prox.
+__device__ void prox_block(const ProxArgs& P, const double* __restrict__ z, const double* __restrict__ hinv,
+                           double step, int64_t m, double* __restrict__ out) {
+  if (P.reg == SCS_REG_L1) {
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) out[i] = prox_l1_d(z[i], hinv[i], P.lam, step);
+  } else if (P.reg == SCS_REG_L2) {
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) out[i] = prox_l2_d(z[i], hinv[i], P.lam, step);
+  } else if (P.reg == SCS_REG_INDBOX) {
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) out[i] = prox_box_d(z[i], P.lb[i], P.ub[i]);
+  } else {  // gl: prox-operators.jl:55-66 -> ProxL2 (prox-reg-utils.jl:84-99)
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) {
+      const double t = P.lam / hinv[i];                       // λ1 ./ h (no α)
+      out[i] = jl_sign(z[i]) * jl_max(fabs(z[i]) - t, 0.0);
+    }
+    __syncthreads();
+    const double beta_scale = step * P.lam2;                  // α*λ2
+    for (int g = threadIdx.x; g < P.ngroups; g += blockDim.x) {
+      const int s = P.gstart[g], e = P.gend[g];
+      const double beta = beta_scale * P.gw[g];
+      double nrm2 = 0.0;
+      for (int k = s; k <= e; ++k) nrm2 += out[k] * out[k];  // twonorm: sequential
+      const double nrm = sqrt(nrm2);
+      for (int k = s; k <= e; ++k) out[k] = out[k] * jl_max(1.0 - beta / (hinv[k] * nrm), 0.0);
+    }
+  }
+  __syncthreads();
+}
+
+// Fused SCORE tail shared by the three step! methods
+// (prox-N-SCORE.jl:226-246, prox-GGN-SCORE.jl:65-105, prox-L-BFGS-SCORE.jl:127-146):
+//   Hinv = 1 ./ Hr;  η = sqrt(λgr' * (Hinv .* λgr));  α = step/(1 + Mg*η)
+//   safe_α = min(1, α);  dx = safe_α*d;  x_new = prox(x + dx) | x + dx
+//   pri = ‖x_new − x‖ | ‖dx‖
+// step_dev (if non-null) overrides step_host (BB / line search results).
+__global__ __launch_bounds__(VB) void score_tail_kernel(
+    const double* __restrict__ x, const double* __restrict__ d, const double* __restrict__ gr,
+    const double* __restrict__ Hr, int64_t m, double lam, double Mg, double step_host,
+    const double* __restrict__ step_dev, ProxArgs P, double* __restrict__ hinv, double* __restrict__ zbuf,
+    double* __restrict__ x_new, double* __restrict__ dx, double* __restrict__ scal) {
+  __shared__ double sh[VB / 64];
+  const double step = step_dev ? *step_dev : step_host;
+  double part = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += VB) {
+    const double hi = 1.0 / Hr[i];
+    hinv[i] = hi;
+    const double lgr = lam * gr[i];
+    part += lgr * (hi * lgr);
+  }
+  const double eta2 = block_sum<VB>(part, sh);
+  const double eta = sqrt(eta2);
+  const double alpha = step / (1.0 + Mg * eta);
+  const double safe_alpha = jl_min(1.0, alpha);
+  for (int64_t i = threadIdx.x; i < m; i += VB) {
+    const double dxi = safe_alpha * d[i];
+    dx[i] = dxi;
+    zbuf[i] = x[i] + dxi;
+  }
+  __syncthreads();
+  if (P.use_prox) {
+    prox_block(P, zbuf, hinv, step, m, x_new);
+  } else {
+    for (int64_t i = threadIdx.x; i < m; i += VB) x_new[i] = zbuf[i];
+    __syncthreads();
+  }
+  part = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += VB) {
+    const double r = P.use_prox ? (x_new[i] - x[i]) : dx[i];
+    part += r * r;
+  }
+  const double pri2 = block_sum<VB>(part, sh);
+  if (threadIdx.x == 0) {
+    scal[0] = sqrt(pri2);  // pri_res_norm
+    scal[1] = eta;
+    scal[2] = alpha;
+    scal[3] = step;
+  }
+}
+
+// prox only (kernel-level parity entry point)
+__global__ __launch_bounds__(VB) void prox_only_kernel(ProxArgs P, const double* __restrict__ z,
+                                                       const double* __restrict__ Hr, double step, int64_t m,
+                                                       double* __restrict__ hinv, double* __restrict__ out) {
+  for (int64_t i = threadIdx.x; i < m; i += VB) hinv[i] = 1.0 / Hr[i];
+  __syncthreads();
+  prox_block(P, z, hinv, step, m, out);
+}
+
+// get_reg (regularizers.jl:4-31); gl with G = identity selector.
+__global__ __launch_bounds__(VB) void reg_value_kernel(ProxArgs P, const double* __restrict__ x, int64_t m,
+                                                       double* __restrict__ out) {
+  __shared__ double sh[VB / 64];
+  __shared__ double gsum[1];
+  double part = 0.0;
+  if (P.reg == SCS_REG_INDBOX) {
+    for (int64_t i = threadIdx.x; i < m; i += VB) part += (x[i] < P.lb[i] || x[i] > P.ub[i]) ? 1.0 : 0.0;
+    const double nout = block_sum<VB>(part, sh);
+    if (threadIdx.x == 0) out[0] = nout > 0 ? __builtin_inf() : 0.0;
+    return;
+  }
+  for (int64_t i = threadIdx.x; i < m; i += VB) part += (P.reg == SCS_REG_L2) ? x[i] * x[i] : fabs(x[i]);
+  const double s = block_sum<VB>(part, sh);
+  if (P.reg != SCS_REG_GL) {
+    if (threadIdx.x == 0) out[0] = P.lam * s;
+    return;
+  }
+  // fz (prox-reg-utils.jl:101-110): sequential over groups, twonorm sequential
+  if (threadIdx.x == 0) {
+    double fz = 0.0;
+    for (int g = 0; g < P.ngroups; ++g) {
+      double nrm2 = 0.0;
+      for (int k = P.gstart[g]; k <= P.gend[g]; ++k) nrm2 += x[k] * x[k];
+      fz += P.gw[g] * sqrt(nrm2);
+    }
+    gsum[0] = fz;
+    out[0] = P.lam2 * fz + P.lam * s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small helpers
+// ---------------------------------------------------------------------------
+// out[0] = Σ a_i b_i  (fixed order)
+__global__ __launch_bounds__(VB) void dot_kernel(const double* __restrict__ a, const double* __restrict__ b,
+                                                 int64_t m, double* __restrict__ out) {
+  __shared__ double sh[VB / 64];
+  double part = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += VB) part += a[i] * b[i];
+  const double s = block_sum<VB>(part, sh);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// out = a + lam*b   (∇q = ∇f + λ gr)
+__global__ void axpby_kernel(const double* __restrict__ a, double lam, const double* __restrict__ b, int64_t m,
+                             double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < m) out[i] = a[i] + lam * b[i];
+}
+
+// out = a - b
+__global__ void sub_kernel(const double* __restrict__ a, const double* __restrict__ b, int64_t m,
+                           double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < m) out[i] = a[i] - b[i];
+}
+
+// out = -a
+__global__ void neg_kernel(const double* __restrict__ a, int64_t m, double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < m) out[i] = -a[i];
+}
+
+// x + α d with α read from the device (line search trial point)
+__global__ void trial_point_kernel(const double* __restrict__ x, const double* __restrict__ d, double alpha,
+                                   int64_t m, double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < m) out[i] = x[i] + alpha * d[i];
+}
+
+// inv_BB_step (utils.jl:43-48): (γ⋅γ)/(δ'γ), δ = x − x_prev, γ = g − g_prev
+__global__ __launch_bounds__(VB) void bb_step_kernel(const double* __restrict__ x, const double* __restrict__ xp,
+                                                     const double* __restrict__ g, const double* __restrict__ gp,
+                                                     int64_t m, double* __restrict__ out) {
+  __shared__ double sh[VB / 64];
+  double gg = 0.0, dg = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += VB) {
+    const double dl = x[i] - xp[i];
+    const double gm = g[i] - gp[i];
+    gg += gm * gm;
+    dg += dl * gm;
+  }
+  gg = block_sum<VB>(gg, sh);
+  dg = block_sum<VB>(dg, sh);
+  if (threadIdx.x == 0) out[0] = gg / dg;
+}
+
+// L-BFGS two-loop recursion (prox-L-BFGS-SCORE.jl:47-68) for one workgroup.
+// S, Y: ring buffers [mem][ld]; order[k] = ring slot of the k-th oldest pair.
+// Writes d = -r.  Dots are recomputed exactly as the reference does.
+__global__ __launch_bounds__(VB) void two_loop_kernel(const double* __restrict__ S, const double* __restrict__ Y,
+                                                      int64_t ld, const int* __restrict__ order, int k,
+                                                      double H0, const double* __restrict__ g, int64_t m,
+                                                      double* __restrict__ q, double* __restrict__ dout,
+                                                      double* __restrict__ ab /*[2*k]*/) {
+  __shared__ double sh[VB / 64];
+  for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = g[i];
+  __syncthreads();
+  for (int t = k - 1; t >= 0; --t) {           // newest -> oldest
+    const double* s = S + (int64_t)order[t] * ld;
+    const double* y = Y + (int64_t)order[t] * ld;
+    double ys = 0.0, sq = 0.0;
+    for (int64_t i = threadIdx.x; i < m; i += VB) {
+      ys += y[i] * s[i];
+      sq += s[i] * q[i];
+    }
+    ys = block_sum<VB>(ys, sh);
+    sq = block_sum<VB>(sq, sh);
+    const double rho = 1.0 / ys;
+    const double al = rho * sq;
+    for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = q[i] - al * y[i];
+    if (threadIdx.x == 0) { ab[2 * t] = al; ab[2 * t + 1] = rho; }
+    __syncthreads();
+  }
+  for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = H0 * q[i];   // r = H0*q (in place)
+  __syncthreads();
+  for (int t = 0; t < k; ++t) {                // oldest -> newest
+    const double* s = S + (int64_t)order[t] * ld;
+    const double* y = Y + (int64_t)order[t] * ld;
+    double yr = 0.0;
+    for (int64_t i = threadIdx.x; i < m; i += VB) yr += y[i] * q[i];
+    yr = block_sum<VB>(yr, sh);
+    const double al = ab[2 * t], rho = ab[2 * t + 1];
+    const double beta = rho * yr;
+    for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = q[i] + s[i] * (al - beta);
+    __syncthreads();
+  }
+  for (int64_t i = threadIdx.x; i < m; i += VB) dout[i] = -q[i];
+}
+
+// L-BFGS memory update (prox-L-BFGS-SCORE.jl:148-162): γh = ∇q_new − ∇q,
+// store (δh, γh) into ring slot `slot` when δhᵀγh > 1e-10.  scal[0] = δhᵀγh,
+// scal[1] = γhᵀγh.  The host reads scal and advances the ring.
+__global__ __launch_bounds__(VB) void lbfgs_update_kernel(const double* __restrict__ dh,
+                                                          const double* __restrict__ gq_new,
+                                                          const double* __restrict__ gq, int64_t m,
+                                                          double* __restrict__ Sslot, double* __restrict__ Yslot,
+                                                          double* __restrict__ scal) {
+  __shared__ double sh[VB / 64];
+  double dg = 0.0, gg = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += VB) {
+    const double gh = gq_new[i] - gq[i];
+    Yslot[i] = gh;                 // staged; committed only if accepted (slot is free)
+    Sslot[i] = dh[i];
+    dg += dh[i] * gh;
+    gg += gh * gh;
+  }
+  dg = block_sum<VB>(dg, sh);
+  gg = block_sum<VB>(gg, sh);
+  if (threadIdx.x == 0) { scal[0] = dg; scal[1] = gg; }
+}
+
+// G[i,i] += λ·Hr[i]   (H + λ.*Diagonal(Hr), prox-N-SCORE.jl:177,204; prox-GGN-SCORE.jl:129)
+__global__ void diag_add_kernel(double* __restrict__ G, int64_t ldg, int64_t m, double lam,
+                                const double* __restrict__ Hr) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < m) G[i * ldg + i] += lam * Hr[i];
+}
+
+// copy the strictly-lower triangle onto the upper one (LU fallback needs the full matrix)
+__global__ void symmetrize_kernel(double* __restrict__ G, int64_t ldg, int64_t m) {
+  const int64_t j = blockIdx.y;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < j; i += (int64_t)gridDim.x * blockDim.x)
+    G[j * ldg + i] = G[i * ldg + j];
+}
+
+// G = 0.5*(A + Aᵀ) for the quadratic loss (Hessian of 1/2 x'Ax, m x m A)
+__global__ void half_sym_kernel(const double* __restrict__ A, int64_t lda, int64_t m, double* __restrict__ G,
+                                int64_t ldg) {
+  const int64_t j = blockIdx.y;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    G[j * ldg + i] = 0.5 * (A[j * lda + i] + A[i * lda + j]);
+}
+
+// ---------------------------------------------------------------------------
+// Rosenbrock (ProblemGeneric of README.md:49; chained form for m > 2)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(VB) void rosen_kernel(const double* __restrict__ x, int64_t m, int what,
+                                                   double* __restrict__ out, double* __restrict__ G, int64_t ldg) {
+  __shared__ double sh[VB / 64];
+  if (what == 0) {  // value
+    double part = 0.0;
+    for (int64_t i = threadIdx.x; i + 1 < m; i += VB) {
+      const double a = x[i + 1] - x[i] * x[i];
+      const double b = 1.0 - x[i];
+      part += 100.0 * a * a + b * b;
+    }
+    const double s = block_sum<VB>(part, sh);
+    if (threadIdx.x == 0) out[0] = s;
+  } else if (what == 1) {  // gradient
+    for (int64_t i = threadIdx.x; i < m; i += VB) {
+      double g = 0.0;
+      if (i + 1 < m) {
+        const double a = x[i + 1] - x[i] * x[i];
+        g += -400.0 * x[i] * a - 2.0 * (1.0 - x[i]);
+      }
+      if (i > 0) g += 200.0 * (x[i] - x[i - 1] * x[i - 1]);
+      out[i] = g;
+    }
+  } else {  // Hessian (dense, tridiagonal)
+    for (int64_t j = 0; j < m; ++j)
+      for (int64_t i = threadIdx.x; i < m; i += VB) G[j * ldg + i] = 0.0;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < m; i += VB) {
+      double hii = 0.0;
+      if (i + 1 < m) {
+        hii += 1200.0 * x[i] * x[i] - 400.0 * x[i + 1] + 2.0;
+        G[(i + 1) * ldg + i] = -400.0 * x[i];
+        G[i * ldg + i + 1] = -400.0 * x[i];
+      }
+      if (i > 0) hii += 200.0;
+      G[i * ldg + i] = hii;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
+
+hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,
+                           const double* wel, double* gr, double* Hr, hipStream_t st) {
+  if (kind == SCS_SMOOTH_PHUBER_GL)
+    hipLaunchKernelGGL(smooth_gl_kernel, dim3(1), dim3(VB), 0, st, x, m, mu, wel, gr, Hr);
+  else
+    hipLaunchKernelGGL(smooth_elem_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, kind, x, m, mu, a, b, gr, Hr);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_tail(const double* x, const double* d, const double* gr, const double* Hr, int64_t m,
+                             double lam, double Mg, double step_host, const double* step_dev, const ProxArgsH& Ph,
+                             double* hinv, double* zbuf, double* x_new, double* dx, double* scal, hipStream_t st) {
+  ProxArgs P{Ph.reg, Ph.use_prox, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups};
+  hipLaunchKernelGGL(score_tail_kernel, dim3(1), dim3(VB), 0, st, x, d, gr, Hr, m, lam, Mg, step_host, step_dev, P,
+                     hinv, zbuf, x_new, dx, scal);
+  return hipGetLastError();
+}
+
+hipError_t launch_prox_only(const ProxArgsH& Ph, const double* z, const double* Hr, double step, int64_t m,
+                            double* hinv, double* out, hipStream_t st) {
+  ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups};
+  hipLaunchKernelGGL(prox_only_kernel, dim3(1), dim3(VB), 0, st, P, z, Hr, step, m, hinv, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_reg_value(const ProxArgsH& Ph, const double* x, int64_t m, double* out, hipStream_t st) {
+  ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups};
+  hipLaunchKernelGGL(reg_value_kernel, dim3(1), dim3(VB), 0, st, P, x, m, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_dot(const double* a, const double* b, int64_t m, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(dot_kernel, dim3(1), dim3(VB), 0, st, a, b, m, out);
+  return hipGetLastError();
+}
+hipError_t launch_axpby(const double* a, double lam, const double* b, int64_t m, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(axpby_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, a, lam, b, m, out);
+  return hipGetLastError();
+}
+hipError_t launch_sub(const double* a, const double* b, int64_t m, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(sub_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, a, b, m, out);
+  return hipGetLastError();
+}
+hipError_t launch_neg(const double* a, int64_t m, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(neg_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, a, m, out);
+  return hipGetLastError();
+}
+hipError_t launch_trial_point(const double* x, const double* d, double alpha, int64_t m, double* out,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(trial_point_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, x, d, alpha, m, out);
+  return hipGetLastError();
+}
+hipError_t launch_bb_step(const double* x, const double* xp, const double* g, const double* gp, int64_t m,
+                          double* out, hipStream_t st) {
+  hipLaunchKernelGGL(bb_step_kernel, dim3(1), dim3(VB), 0, st, x, xp, g, gp, m, out);
+  return hipGetLastError();
+}
+hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
+                           const double* g, int64_t m, double* q, double* d, double* ab, hipStream_t st) {
+  hipLaunchKernelGGL(two_loop_kernel, dim3(1), dim3(VB), 0, st, S, Y, ld, order, k, H0, g, m, q, d, ab);
+  return hipGetLastError();
+}
+hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
+                               double* Yslot, double* scal, hipStream_t st) {
+  hipLaunchKernelGGL(lbfgs_update_kernel, dim3(1), dim3(VB), 0, st, dh, gq_new, gq, m, Sslot, Yslot, scal);
+  return hipGetLastError();
+}
+hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st) {
+  hipLaunchKernelGGL(diag_add_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, G, ldg, m, lam, Hr);
+  return hipGetLastError();
+}
+hipError_t launch_symmetrize(double* G, int64_t ldg, int64_t m, hipStream_t st) {
+  hipLaunchKernelGGL(symmetrize_kernel, dim3(4, (unsigned)m), dim3(256), 0, st, G, ldg, m);
+  return hipGetLastError();
+}
+hipError_t launch_half_sym(const double* A, int64_t lda, int64_t m, double* G, int64_t ldg, hipStream_t st) {
+  hipLaunchKernelGGL(half_sym_kernel, dim3(4, (unsigned)m), dim3(256), 0, st, A, lda, m, G, ldg);
+  return hipGetLastError();
+}
+hipError_t launch_rosen(const double* x, int64_t m, int what, double* out, double* G, int64_t ldg,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(rosen_kernel, dim3(1), dim3(VB), 0, st, x, m, what, out, G, ldg);
+  return hipGetLastError();
+}
+
+}  // namespace scs

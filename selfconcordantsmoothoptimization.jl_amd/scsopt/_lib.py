@@ -1,0 +1,163 @@
+"""ctypes binding of libscsopt (include/scsopt.h).
+
+The library is built in-tree (``make -C selfconcordantsmoothoptimization.jl_amd/csrc``)
+and is the only compute path: nothing here falls back to a CPU
+implementation.  If the shared object is missing, importing this module
+raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SCSOPT_LIB", os.path.join(_HERE, "libscsopt.so"))
+
+SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS_ERR_COMM = range(7)
+
+LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5}
+GGN = {None: 0, "sigmoid_ce": 1, "linear_ls": 2}
+REG = {"l1": 1, "l2": 2, "indbox": 3, "gl": 4}
+SMOOTH = {"phuber_l1l2": 1, "phuber_indbox": 2, "phuber_gl": 3, "exp_indbox": 4}
+METHOD = {"nscore": 1, "ggnscore": 2, "lqnscore": 3}
+
+# One HIP runtime per process: torch's wheel bundles ROCm libraries whose NEEDED
+# names ("libamdhip64.so") differ from the SONAMEs ("libamdhip64.so.7"), so if
+# libscsopt pulled /opt/rocm's copies in first, importing torch afterwards would
+# load a second runtime and crash.  Importing torch first makes libscsopt's
+# NEEDED entries resolve to the already-loaded (torch-bundled) runtime, rocBLAS
+# and rocSOLVER.  torch is plumbing only (streams, torch.distributed).
+import torch  # noqa: E402,F401  (must precede the CDLL below)
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libscsopt.so not found at {LIB_PATH}: build it with "
+        "`make -C selfconcordantsmoothoptimization.jl_amd/csrc` (there is no CPU fallback)")
+
+lib = C.CDLL(LIB_PATH)
+
+c_dp = C.POINTER(C.c_double)
+c_i64p = C.POINTER(C.c_int64)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
+
+
+class Synth(C.Structure):
+    _fields_ = [("N_global", C.c_int64), ("row0", C.c_int64), ("N", C.c_int64), ("m", C.c_int64),
+                ("seed", C.c_uint64), ("kind", C.c_int), ("density", C.c_double)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("gram_ms", C.c_double), ("gram_calls", C.c_int64),
+                ("gemv_ms", C.c_double), ("gemv_calls", C.c_int64),
+                ("solve_ms", C.c_double), ("solve_calls", C.c_int64),
+                ("step_ms", C.c_double), ("step_calls", C.c_int64),
+                ("reduce_ms", C.c_double), ("reduce_calls", C.c_int64)]
+
+
+_SIGS = {
+    "scs_version": (C.c_char_p, []),
+    "scs_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
+    "scs_destroy": (C.c_int, [C.c_void_p]),
+    "scs_last_error": (C.c_char_p, [C.c_void_p]),
+    "scs_get_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "scs_set_comm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, C.c_void_p]),
+    "scs_reduce_buffer_size": (C.c_int, [C.c_void_p, c_i64p]),
+    "scs_set_reduce_buffer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "scs_set_data": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_dp, C.c_int64, c_dp, C.c_int64, C.c_int64]),
+    "scs_gen_data": (C.c_int, [C.c_void_p, C.POINTER(Synth)]),
+    "scs_get_data": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_dp, C.c_int64, c_dp]),
+    "scs_get_dims": (C.c_int, [C.c_void_p, c_i64p, c_i64p, c_i64p, c_i64p]),
+    "scs_set_loss": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double]),
+    "scs_set_reg": (C.c_int, [C.c_void_p, C.c_int, c_dp, C.c_int, c_dp, c_dp, C.c_int64, c_i64p, C.c_int64]),
+    "scs_set_smoother": (C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_double, c_dp, c_dp,
+                                   C.c_int64]),
+    "scs_set_L": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+    "scs_method_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "scs_eval_f": (C.c_int, [C.c_void_p, c_dp, c_dp]),
+    "scs_eval_grad": (C.c_int, [C.c_void_p, c_dp, c_dp]),
+    "scs_eval_reg": (C.c_int, [C.c_void_p, c_dp, c_dp]),
+    "scs_step": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, c_dp, c_dp, c_dp]),
+    "scs_smoother_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, c_dp]),
+    "scs_prox_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_double, C.c_double, c_dp]),
+    "scs_gram_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64]),
+    "scs_gemv_t_eval": (C.c_int, [C.c_void_p, c_dp, c_dp]),
+    "scs_gemv_n_eval": (C.c_int, [C.c_void_p, c_dp, c_dp]),
+    "scs_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "scs_timing_get": (C.c_int, [C.c_void_p, C.POINTER(Timing)]),
+    "scs_timing_reset": (C.c_int, [C.c_void_p]),
+    "scs_sync": (C.c_int, [C.c_void_p]),
+}
+
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)  # AttributeError here = the .so does not export the header's symbol
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_SIGS)
+
+
+class ScsError(RuntimeError):
+    """A non-reference failure (HIP, argument, state, communication)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"[scsopt rc={code}] {msg}")
+        self.code = code
+
+
+class ScsReferenceError(ScsError):
+    """An error the reference itself raises via Base.error (same message text)."""
+
+
+def version():
+    return lib.scs_version().decode()
+
+
+def dptr(a):
+    """Pointer to a C-contiguous float64 numpy array (or None)."""
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"], "expected a contiguous float64 array"
+    return a.ctypes.data_as(c_dp)
+
+
+class Context:
+    """Owns one scs_ctx (one device, one stream)."""
+
+    def __init__(self, device=0, stream=None):
+        h = C.c_void_p()
+        rc = lib.scs_create(int(device), stream, C.byref(h))
+        if rc != SCS_OK:
+            raise ScsError(rc, f"scs_create(device={device}) failed")
+        self.h = h
+        self.device = device
+        self._keep = []  # ctypes callbacks / buffers that must outlive the context
+
+    def check(self, rc):
+        if rc != SCS_OK:
+            msg = lib.scs_last_error(self.h).decode(errors="replace")
+            if rc == SCS_ERR_REF:
+                raise ScsReferenceError(rc, msg)
+            raise ScsError(rc, msg)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.scs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream(self):
+        s = C.c_void_p()
+        self.check(lib.scs_get_stream(self.h, C.byref(s)))
+        return s.value
+
+    def timing(self):
+        t = Timing()
+        self.check(lib.scs_timing_get(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in Timing._fields_}

@@ -1,0 +1,177 @@
+"""iterate! / optim_loop! / Solution (src/algorithms/iterate.jl) over the device step.
+
+The loop logic -- history pushes, the duplicated last-epoch entry, the
+termination tests on the pre-step f_rel_error, the α -> L = 1/α mutation --
+restates iterate.jl:56-76,100-267 line by line; every f(x), get_reg(x) and
+step! runs in libscsopt on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import logging
+import math
+import sys
+import time
+from dataclasses import dataclass, field
+from typing import Any
+
+import numpy as np
+
+from . import _lib
+from ._lib import dptr
+from .methods import ProximalMethod, ProxLQNSCORE
+
+log = logging.getLogger("scsopt")
+
+
+@dataclass
+class Solution:
+    """iterate.jl:3-32."""
+    x: np.ndarray
+    obj: list
+    fval: list
+    pri_res_norm: list
+    fvaltest: list
+    rel: list
+    objrel: list
+    metricvals: dict
+    times: list
+    epochs: int
+    model: Any
+
+
+def _jl_max(a, b):
+    """Julia max(::Float64, ::Float64): NaN propagates, -0.0 < +0.0."""
+    a = float(a)
+    b = float(b)
+    if math.isnan(a):
+        return a
+    if math.isnan(b):
+        return b
+    if b < a or (math.copysign(1.0, b) < 0 < math.copysign(1.0, a)):
+        return a
+    return b
+
+
+def _norm(v):
+    return float(np.linalg.norm(v))
+
+
+def step(method, model, reg_name, hmu, x, x_prev, iter_, return_dx=False):
+    """step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter; return_dx)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    x_prev = np.ascontiguousarray(x_prev, dtype=np.float64)
+    x_new = np.empty_like(x)
+    dx = np.empty_like(x) if return_dx else None
+    pri = C.c_double()
+    model.ctx.check(_lib.lib.scs_step(model.ctx.h, dptr(x), dptr(x_prev), int(iter_), dptr(x_new), dptr(dx),
+                                      C.byref(pri)))
+    if return_dx:
+        return x_new, dx, pri.value
+    return x_new, pri.value
+
+
+def init_method(method, model):
+    """init!(method, x) on the device (resets the L-BFGS memory)."""
+    mem = method.m if isinstance(method, ProxLQNSCORE) else 0
+    model.ctx.check(_lib.lib.scs_method_init(model.ctx.h, method.code, int(method.ss_type), int(bool(method.use_prox)),
+                                             int(mem)))
+
+
+def iterate(method: ProximalMethod, model, reg_name, hmu, *, metrics=None, alpha=None, batch_size=None,
+            slice_samples=False, shuffle_batch=True, max_epoch=1000, comm_rounds=100, local_max_iter=None,
+            x_tol=1e-10, f_tol=1e-10, verbose=1):
+    """iterate!(method, model, reg_name, hμ; kwargs...) (iterate.jl:56-76)."""
+    if local_max_iter is not None:
+        max_epoch = 1
+    if batch_size is not None or slice_samples:
+        raise NotImplementedError("minibatch / slice_samples paths are not on the device yet (SURVEY §8f rank 3)")
+    return optim_loop(method, model, reg_name, hmu, metrics=metrics, alpha=alpha, max_epoch=max_epoch,
+                      x_tol=x_tol, f_tol=f_tol, verbose=verbose)
+
+
+def _show(opt_verbose, label, tag, epoch, obj, fval, pri, rel, dt):
+    if opt_verbose > 1:
+        print("\n" + "=" * 30)
+        print(f"Optimizer:\t{label}")
+        print(f"{tag} = {epoch}\nobj = {obj}\nfval = {fval}\npri_res_norm = {pri}\nrel_error = {rel}\nΔtime = {dt}")
+
+
+def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_epoch=1000, x_tol=1e-10,
+               f_tol=1e-10, verbose=1):
+    """optim_loop! (iterate.jl:100-267) for the full-batch case."""
+    implemented = []
+    method.set_name(implemented)
+    if alpha is not None:
+        model.L = 1 / alpha                                   # iterate.jl:113-115
+    if method.name in implemented and method.ss_type == 1 and model.L is None and verbose > 0:
+        print("[ Info: Neither L nor α is set for the problem... Now fixing α = 0.5...", file=sys.stderr)
+    model.configure(reg_name, hmu)
+    f = model.fx
+    greg = model.get_reg
+    fvals, pris, objs, rels, frels, times = [], [], [], [], [], []
+    metric_vals = {k: [] for k in (metrics or {})}
+    epochs = 0
+    x_star = model.x
+    pri = None
+    obj_star = f(x_star) + greg(x_star)
+    x = model.x0.copy()
+    x_prev = x.copy()
+    init_method(method, model)
+    t0 = time.monotonic()
+
+    def now():
+        return int((time.monotonic() - t0) * 1000) / 1000   # Dates.now() has ms resolution
+
+    def rel_of(xx):
+        if reg_name == "gl":
+            d = x_star - xx
+            return float(np.mean(d * d))                       # mean_square_error (utils.jl:3-5)
+        return _jl_max(_norm(xx - x_star) / _jl_max(_norm(x_star), 1.0), x_tol)
+
+    def frel_of(ob):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            q = np.float64(abs(ob - obj_star)) / np.float64(abs(obj_star))
+        return _jl_max(q, f_tol)
+
+    def push(ob, fv, pr, rl, fr, dt, xx):
+        objs.append(ob); fvals.append(fv); pris.append(pr); rels.append(rl); frels.append(fr); times.append(dt)
+        for k in metric_vals:
+            metric_vals[k].append(metrics[k](model, xx))
+
+    for epoch_t in range(1, max_epoch + 1):
+        dt = now()
+        fval = f(x)
+        obj = fval + greg(x)
+        rel_error = rel_of(x)
+        f_rel_error = frel_of(obj)
+        _show(verbose, method.label, "epoch", epoch_t - 1, obj, fval, pri, rel_error, dt)
+        push(obj, fval, pri, rel_error, f_rel_error, dt, x)
+        if epoch_t == max_epoch:                              # iterate.jl:219-231
+            dt = now()
+            fval = f(x)
+            obj = fval + greg(x)
+            rel_error = rel_of(x)
+            _show(verbose, method.label, "max_epoch", epoch_t, obj, fval, pri, rel_error, dt)
+            f_rel_error = frel_of(obj)
+            push(obj, fval, pri, rel_error, f_rel_error, dt, x)
+        x_new, pri = step(method, model, reg_name, hmu, x, x_prev, epoch_t)
+        if _norm(x_new - x) < x_tol * max(_norm(x), 1.0) or f_rel_error <= f_tol or pri < x_tol:
+            if epoch_t != max_epoch:                          # iterate.jl:235-247
+                dt = now()
+                fval = f(x_new)
+                obj = fval + greg(x_new)
+                rel_error = rel_of(x_new)
+                _show(verbose, method.label, "terminate_epoch", epoch_t, obj, fval, pri, rel_error, dt)
+                f_rel_error = frel_of(obj)
+                push(obj, fval, pri, rel_error, f_rel_error, dt, x_new)
+            x_prev = x
+            x = x_new
+            epochs += 1
+        else:
+            x_prev = x
+            x = x_new
+        if _norm(x - x_prev) < x_tol * max(_norm(x_prev), 1.0) or f_rel_error <= f_tol or pri < x_tol:
+            break                                             # iterate.jl:257-259
+        epochs += 1
+    return Solution(x, objs, fvals, pris, [], rels, frels, metric_vals, times, epochs, model)

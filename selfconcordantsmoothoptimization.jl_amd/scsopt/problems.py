@@ -1,0 +1,232 @@
+"""Problem containers (src/problems.jl) backed by a device context.
+
+``Problem(A, y, x0, f, λ; ...)`` uploads A (column-major, the Julia Matrix
+layout) and y to HBM once; ``Problem(x0, f, λ; ...)`` is the data-free
+ProblemGeneric (problems.jl:44-59).  ``Problem.synthetic(...)`` generates A
+and y on the device (counter-based RNG, any row shard in place), which is how
+the BASELINE configurations are built without ever materialising A on the
+host.  Row sharding: pass ``comm=shard.Comm(...)`` and the local rows.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Any, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import LOSS, GGN, REG, SMOOTH, dptr
+from .losses import Loss, OutFn, ggn_kind
+from .smoothers import Smoother, bounds_array
+
+
+@dataclass
+class GetP:
+    """get_P(n, G, ind) (prox-reg-utils.jl:9-62): group structure for "gl".
+    ind is 3 x grpNUM (1-based start, end; Int weight); G maps the selected
+    entries to variables (identity for contiguous, non-overlapping groups)."""
+    n: int
+    G: np.ndarray
+    ind: np.ndarray
+
+    def __post_init__(self):
+        self.ind = np.asarray(self.ind, dtype=np.int64)
+        self.G = np.asarray(self.G, dtype=np.int64)
+        if self.ind.ndim != 2 or self.ind.shape[0] != 3:
+            raise ValueError("ind must be a 3 x grpNUM integer matrix")
+        self.grpNUM = int(self.ind.shape[1])
+        self.grpSIZES = self.ind[1] - self.ind[0] + 1
+        self.ntotal = int(self.grpSIZES.sum())
+        if not np.array_equal(self.G, np.arange(1, self.n + 1)) or self.ntotal != self.n:
+            raise NotImplementedError("device gl path supports contiguous groups tiling 1..n (G = 1:n)")
+
+
+def get_P(n, G, ind):
+    return GetP(int(n), np.asarray(G), np.asarray(ind))
+
+
+def _lam_tuple(lam):
+    if isinstance(lam, (list, tuple, np.ndarray)):
+        v = [float(t) for t in lam]
+    else:
+        v = [float(lam)]
+    if len(v) not in (1, 2):
+        raise ValueError("λ must be a scalar or a pair")
+    return v
+
+
+class Problem:
+    """problems.jl:21-40 (data) / :5-19 (generic)."""
+
+    def __init__(self, *args, L=None, sol=None, C_set=None, P=None, out_fn: Optional[OutFn] = None,
+                 name=None, device=0, comm=None, N_global=None, row0=0, _ctx=None):
+        if len(args) == 5:
+            A, y, x0, f, lam = args
+        elif len(args) == 3:
+            A, y = None, None
+            x0, f, lam = args
+        else:
+            raise TypeError("Problem(A, y, x0, f, λ; ...) or Problem(x0, f, λ; ...)")
+        if not isinstance(f, Loss):
+            raise TypeError("f must be a scsopt.losses kind (device losses replace Julia closures)")
+        self.x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64))
+        self.m = int(self.x0.shape[0])
+        self.f = f
+        self.λ = lam
+        self.L = L
+        self.x = np.zeros(self.m) if sol is None else np.ascontiguousarray(np.asarray(sol, dtype=np.float64))
+        self.C_set = C_set
+        self.P = P
+        self.out_fn = out_fn
+        self.name = name
+        self.comm = comm
+        self.generic = A is None and _ctx is None
+        self.ctx = _ctx if _ctx is not None else _lib.Context(device)
+        if comm is not None and comm.world > 1:
+            comm.attach(self.ctx)
+        if _ctx is None:
+            if self.generic:
+                self.N = 0
+                self.ctx.check(_lib.lib.scs_set_data(self.ctx.h, 0, self.m, None, 0, None, 0, 0))
+            else:
+                A = np.asarray(A, dtype=np.float64)
+                if A.ndim != 2 or A.shape[1] != self.m:
+                    raise ValueError(f"A must be N x m with m = length(x0) = {self.m}")
+                Af = np.asfortranarray(A)  # Julia layout: column-major, lda = N
+                yv = np.ascontiguousarray(np.asarray(y, dtype=np.float64).reshape(-1))
+                self.N = int(A.shape[0])
+                Ng = self.N if N_global is None else int(N_global)
+                self.ctx.check(_lib.lib.scs_set_data(self.ctx.h, self.N, self.m,
+                                                     Af.ctypes.data_as(_lib.c_dp), self.N, dptr(yv), Ng,
+                                                     int(row0)))
+        else:
+            N = C.c_int64()
+            self.ctx.check(_lib.lib.scs_get_dims(self.ctx.h, C.byref(N), None, None, None))
+            self.N = int(N.value)
+        if comm is not None and comm.world > 1:
+            comm.bind_buffer(self.ctx)
+        ggn = ggn_kind(out_fn)
+        if out_fn is not None and f.kind in ("quadratic", "rosenbrock"):
+            raise ValueError("out_fn needs a data loss")
+        if out_fn is not None and out_fn.scale != f.scale:
+            raise ValueError("f and out_fn must use the same scale (one device loss scale)")
+        scale = f.scale
+        self.ctx.check(_lib.lib.scs_set_loss(self.ctx.h, LOSS[f.kind], GGN[ggn], scale))
+
+    @classmethod
+    def synthetic(cls, N, m, x0, f, lam, *, kind=1, seed=1234, density=0.1, out_fn=None, device=0,
+                  comm=None, **kw):
+        """A ~ N(0,1)/sqrt(m) (kind 1, 2) or N(0,1) (kind 3) generated on the device, y from a
+        sparse x_true (kind 1: Bernoulli(σ(A x_true)) ∈ {0,1}; kind 2: ±1; kind 3: A x_true + 0.1ε).
+        With comm, this rank generates its contiguous row shard in place."""
+        from .shard import row_range
+        rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
+        r0, r1 = row_range(N, world, rank)
+        ctx = _lib.Context(device)
+        if comm is not None and world > 1:
+            comm.attach(ctx)
+        spec = _lib.Synth(N_global=N, row0=r0, N=r1 - r0, m=m, seed=seed, kind=kind, density=density)
+        ctx.check(_lib.lib.scs_gen_data(ctx.h, C.byref(spec)))
+        return cls(x0, f, lam, out_fn=out_fn, device=device, comm=comm, _ctx=ctx, **kw)
+
+    # device evaluation helpers ------------------------------------------------
+    def fx(self, x):
+        """f(A, y, x) on the device (iterate.jl:168)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = C.c_double()
+        self.ctx.check(_lib.lib.scs_eval_f(self.ctx.h, dptr(x), C.byref(out)))
+        return out.value
+
+    def gradx(self, x):
+        """∇f(A, y, x) on the device (grad_fx)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        g = np.empty(self.m)
+        self.ctx.check(_lib.lib.scs_eval_grad(self.ctx.h, dptr(x), dptr(g)))
+        return g
+
+    def get_data(self, r0=0, nr=None):
+        nr = self.N - r0 if nr is None else nr
+        A = np.zeros((self.m, nr), dtype=np.float64)   # column-major view: A.T is N x m
+        y = np.zeros(nr, dtype=np.float64)
+        self.ctx.check(_lib.lib.scs_get_data(self.ctx.h, r0, nr, dptr(A), nr, dptr(y)))
+        return np.ascontiguousarray(A.T), y
+
+    def configure(self, reg_name, hmu: Smoother):
+        """Push reg_name / λ / C_set / P and the smoother to the device context."""
+        if reg_name not in REG:
+            raise _lib.ScsReferenceError(_lib.SCS_ERR_REF, "reg_name not valid.")
+        lam = np.ascontiguousarray(_lam_tuple(self.λ), dtype=np.float64)
+        lb = ub = None
+        nb = 0
+        ind = None
+        ng = 0
+        if reg_name == "indbox":
+            if self.C_set is None:
+                raise ValueError("indbox needs C_set")
+            lo, hi = self.C_set[0], self.C_set[1]
+            lb, ub = bounds_array(lo, self.m), bounds_array(hi, self.m)
+            if lb.size != ub.size:
+                lb = np.broadcast_to(lb, (self.m,)).copy()
+                ub = np.broadcast_to(ub, (self.m,)).copy()
+            nb = lb.size
+        if reg_name == "gl":
+            if self.P is None:
+                raise ValueError("gl needs P = get_P(n, G, ind)")
+            ind = np.ascontiguousarray(self.P.ind.T.reshape(-1), dtype=np.int64)  # column-major 3 x G
+            ng = self.P.grpNUM
+        self.ctx.check(_lib.lib.scs_set_reg(self.ctx.h, REG[reg_name], dptr(lam), lam.size, dptr(lb), dptr(ub),
+                                            nb, ind.ctypes.data_as(_lib.c_i64p) if ind is not None else None,
+                                            ng))
+        slb = sub = None
+        snb = 0
+        if hmu.kind in ("phuber_indbox", "exp_indbox"):
+            slb, sub = bounds_array(hmu.lb, self.m), bounds_array(hmu.ub, self.m)
+            if slb.size != sub.size:
+                slb = np.broadcast_to(slb, (self.m,)).copy()
+                sub = np.broadcast_to(sub, (self.m,)).copy()
+            snb = slb.size
+        self.ctx.check(_lib.lib.scs_set_smoother(self.ctx.h, SMOOTH[hmu.kind], hmu.mu, hmu.Mh, hmu.nu, dptr(slb),
+                                                 dptr(sub), snb))
+        self.ctx.check(_lib.lib.scs_set_L(self.ctx.h, int(self.L is not None),
+                                          float(self.L) if self.L is not None else 0.0))
+
+    def get_reg(self, x):
+        """get_reg(model, x, reg_name) for the configured reg_name (regularizers.jl:4-31)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = C.c_double()
+        self.ctx.check(_lib.lib.scs_eval_reg(self.ctx.h, dptr(x), C.byref(out)))
+        return out.value
+
+    def _smoother_eval(self, hmu, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        gr = np.empty(self.m)
+        Hr = np.empty(self.m)
+        self.ctx.check(_lib.lib.scs_smoother_eval(self.ctx.h, dptr(x), dptr(gr), dptr(Hr)))
+        return gr, Hr
+
+    # kernel-level entry points used by the parity tests -----------------------
+    def prox(self, z, Hr, lam, alpha):
+        z = np.ascontiguousarray(z, dtype=np.float64)
+        Hr = np.ascontiguousarray(Hr, dtype=np.float64)
+        out = np.empty(self.m)
+        self.ctx.check(_lib.lib.scs_prox_eval(self.ctx.h, dptr(z), dptr(Hr), float(lam), float(alpha), dptr(out)))
+        return out
+
+    def gram(self, w):
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        G = np.zeros((self.m, self.m))
+        self.ctx.check(_lib.lib.scs_gram_eval(self.ctx.h, dptr(w), dptr(G), self.m))
+        return G.T.copy()  # column-major -> row-major (lower triangle valid)
+
+    def gemv_t(self, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        out = np.empty(self.m)
+        self.ctx.check(_lib.lib.scs_gemv_t_eval(self.ctx.h, dptr(v), dptr(out)))
+        return out
+
+    def gemv_n(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.empty(self.N)
+        self.ctx.check(_lib.lib.scs_gemv_n_eval(self.ctx.h, dptr(x), dptr(out)))
+        return out

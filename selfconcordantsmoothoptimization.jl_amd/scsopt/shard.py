@@ -1,0 +1,75 @@
+"""Row sharding of A across ranks (one process per GPU).
+
+The path shards by samples: rank r holds rows ``row_range(N, world, r)`` of
+A (and of y), generated or uploaded in place; x and every length-m vector are
+replicated.  The only exchange of an iteration is one in-place fp64 sum
+(SURVEY.md §8e): [packed lower-triangular Gram tiles ‖ Aᵀv] for
+ProxGGNSCORE / ProxNSCORE, the length-m gradient for ProxLQNSCORE, and one
+scalar per objective evaluation.  libscsopt calls back into ``Comm`` at
+those points; the sum itself is ``torch.distributed.all_reduce`` (RCCL over
+xGMI with the "nccl" backend on MI355X, gloo on CPU).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+
+def row_range(N, world, rank):
+    """Contiguous, balanced [r0, r1) row block of `rank` (first N % world ranks get one more row)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad rank {rank} / world {world}")
+    base, rem = divmod(int(N), int(world))
+    r0 = rank * base + min(rank, rem)
+    return r0, r0 + base + (1 if rank < rem else 0)
+
+
+def allreduce_inplace(t, group=None):
+    """Sum `t` over the process group in place (the whole exchange step)."""
+    import torch.distributed as dist
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+class Comm:
+    """Binds a libscsopt context to a torch.distributed process group."""
+
+    def __init__(self, rank=None, world=None, group=None, device=None):
+        import torch.distributed as dist
+        self.rank = dist.get_rank(group) if rank is None else int(rank)
+        self.world = dist.get_world_size(group) if world is None else int(world)
+        self.group = group
+        self.device = device
+        self.buf = None
+        self._cb = None
+        self._ctx = None
+
+    def attach(self, ctx):
+        from . import _lib
+        self._ctx = ctx
+        self._cb = _lib.ALLREDUCE_FN(self._callback)
+        ctx._keep.append(self._cb)
+        ctx.check(_lib.lib.scs_set_comm(ctx.h, self.rank, self.world, self._cb, None))
+
+    def bind_buffer(self, ctx):
+        """Allocate the all-reduce payload buffer (torch-owned device memory) once the dims are known."""
+        import torch
+        from . import _lib
+        n = C.c_int64()
+        ctx.check(_lib.lib.scs_reduce_buffer_size(ctx.h, C.byref(n)))
+        dev = torch.device("cuda", ctx.device) if self.device is None else self.device
+        self.buf = torch.zeros(int(n.value), dtype=torch.float64, device=dev)
+        ctx._keep.append(self.buf)
+        ctx.check(_lib.lib.scs_set_reduce_buffer(ctx.h, C.c_void_p(self.buf.data_ptr()), int(n.value)))
+
+    def _callback(self, dev_ptr, count, stream, user):
+        try:
+            import torch
+            assert self.buf is not None and dev_ptr == self.buf.data_ptr()
+            ext = torch.cuda.ExternalStream(stream, device=self.buf.device)
+            with torch.cuda.stream(ext):
+                allreduce_inplace(self.buf[: int(count)], self.group)
+            return 0
+        except Exception as e:  # surfaced by libscsopt as SCS_ERR_COMM
+            import sys
+            print(f"[scsopt] all-reduce failed: {e!r}", file=sys.stderr)
+            return 1

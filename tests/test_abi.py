@@ -1,0 +1,82 @@
+"""CPU: the C-ABI library loads, exports every entry point include/scsopt.h declares,
+the Python host mirrors the reference API, and the product path has no CPU fallback."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, LIB
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "scsopt.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(scs_[A-Za-z0-9_]+)\s*\(", src))
+    names.discard("scs_allreduce_fn")
+    return sorted(names)
+
+
+def test_library_exports_every_header_symbol():
+    import ctypes
+    lib = ctypes.CDLL(LIB)
+    missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, f"missing exports: {missing}"
+    assert len(header_functions()) >= 25
+
+
+def test_binding_covers_header():
+    from scsopt import _lib
+    assert set(header_functions()) == set(_lib.EXPORTED)
+    assert "gfx950" in _lib.version()
+
+
+def test_no_cpu_fallback_without_gpu():
+    """Creating a context on a host without a HIP device raises (no silent CPU path)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import scsopt
+    with pytest.raises(scsopt.ScsError):
+        scsopt.Problem(np.zeros((4, 2)), np.zeros(4), np.zeros(2), scsopt.losses.least_squares(), 1.0)
+
+
+def test_api_surface_mirrors_reference():
+    import scsopt
+    for name in ("Problem", "iterate", "Solution", "ProxNSCORE", "ProxGGNSCORE", "ProxLQNSCORE",
+                 "PHuberSmootherL1L2", "PHuberSmootherIndBox", "PHuberSmootherGL", "ExponentialSmootherIndBox",
+                 "get_P"):
+        assert hasattr(scsopt, name), name
+    h = scsopt.PHuberSmootherL1L2(1)
+    assert (h.μ, h.Mh, h.ν) == (1.0, 2.0, 2.6)          # test/test_smooth.jl:7-8
+    h = scsopt.PHuberSmootherIndBox(-1.0, 1.0, 1)
+    assert (h.Mh, h.ν) == (2.0, 2.6)                    # test/test_smooth.jl:13-14
+    m = scsopt.ProxLQNSCORE()
+    assert (m.ss_type, m.use_prox, m.m, m.name, m.label) == (1, True, 10, "prox-lbfgsscore", "Prox-LBFGS-SCORE")
+    g = scsopt.ProxGGNSCORE(use_prox=False)
+    impl = []
+    g.set_name(impl)
+    assert (g.name, g.label, impl) == ("ggnscore", "GGN-SCORE", ["ggnscore"])  # prox-GGN-SCORE.jl:24-33
+    f = scsopt.Solution.__dataclass_fields__
+    for k in ("x", "obj", "fval", "pri_res_norm", "fvaltest", "rel", "objrel", "metricvals", "times", "epochs",
+              "model"):
+        assert k in f                                      # iterate.jl:3-32
+
+
+def test_row_range_partitions():
+    from scsopt.shard import row_range
+    for N in (1, 7, 16, 1000, 1 << 20):
+        for world in (1, 2, 3, 4, 8):
+            spans = [row_range(N, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == N
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_get_P_validates_partition():
+    import scsopt
+    P = scsopt.get_P(6, np.arange(1, 7), np.array([[1, 4], [3, 6], [1, 2]]))
+    assert P.grpNUM == 2 and list(P.grpSIZES) == [3, 3]
+    with pytest.raises(NotImplementedError):
+        scsopt.get_P(6, np.array([1, 2, 3, 3, 4, 5]), np.array([[1, 4], [3, 6], [1, 1]]))

@@ -1,0 +1,310 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Tolerances (fp64):
+  * prox outputs on identical inputs: bit-exact (IEEE +,-,*,/ only; signed zeros included);
+  * smoother grad/hess on identical inputs: rtol 1e-14 (GPU pow vs libm pow, <= 2 ulp);
+  * Gram / A·x / Aᵀ·v: |err| <= 1e-13 · Σ|terms| (summation order differs);
+  * trajectories: objective history rtol 1e-8 (north-star bar), identical history length and
+    termination epoch; prox sign/support patterns exact except coordinates within 1e-9·t of
+    the soft-threshold t (ulp-level upstream differences can flip those).
+"""
+import numpy as np
+import pytest
+
+import scsopt
+import scsopt_oracle as O
+from scsopt import losses
+from make_golden import LOGI_A, LOGI_Y, X0, QP_A, QP_Y, QP_X0, QP_XS
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.int64)
+
+
+def small_problem(N=16, m=64, seed=0):
+    rng = np.random.default_rng(seed)
+    A = rng.standard_normal((N, m))
+    y = rng.standard_normal(N)
+    return scsopt.Problem(A, y, np.zeros(m), losses.least_squares(1.0 / N), 0.3)
+
+
+# ---------------------------------------------------------------------------
+# kernel level
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("reg", ["l1", "l2", "indbox", "gl"])
+def test_prox_bit_exact(reg):
+    m = 64
+    p = small_problem(m=m)
+    rng = np.random.default_rng(1)
+    z = rng.standard_normal(m) * 0.8
+    z[:6] = [0.0, -0.0, 1e-300, -1e-300, 2.0, -2.0]
+    Hr = np.abs(rng.standard_normal(m)) + 0.05
+    lam, alpha = 0.3, 0.7
+    if reg == "gl":
+        ind = np.array([[1 + 8 * g for g in range(8)], [8 + 8 * g for g in range(8)], [1 + g % 3 for g in range(8)]])
+        p.P = scsopt.get_P(m, np.arange(1, m + 1), ind)
+        p.λ = [lam, 0.2]
+        p.configure("gl", scsopt.PHuberSmootherL1L2(1.0))
+        op = O.GroupP(m, ind, np.arange(1, m + 1))
+        model = O.Problem(np.zeros((1, m)), np.zeros(1), np.zeros(m), O.Loss("least_squares"), [lam, 0.2], P=op)
+        ref = O.prox_gl(model, z, 1.0 / Hr, alpha)
+    elif reg == "indbox":
+        p.C_set = [-0.5, 0.25]
+        p.configure("indbox", scsopt.PHuberSmootherL1L2(1.0))
+        model = O.Problem(np.zeros((1, m)), np.zeros(1), np.zeros(m), O.Loss("least_squares"), lam,
+                          C_set=[-0.5, 0.25])
+        ref = O.prox_indbox(model, z)
+    else:
+        p.configure(reg, scsopt.PHuberSmootherL1L2(1.0))
+        ref = (O.prox_l1 if reg == "l1" else O.prox_l2)(z, 1.0 / Hr, lam, alpha)
+    with np.errstate(divide="ignore"):
+        got = p.prox(z, Hr, lam, alpha)
+    assert np.array_equal(bits(got), bits(ref)), np.nonzero(bits(got) != bits(ref))
+
+
+@pytest.mark.parametrize("kind", ["phuber_l1l2", "phuber_indbox", "exp_indbox", "phuber_gl"])
+def test_smoother_kernels(golden, kind):
+    x = np.array(golden["kernels"]["x"])
+    m = x.size
+    p = small_problem(m=m)
+    if kind == "phuber_l1l2":
+        hm, ohm = scsopt.PHuberSmootherL1L2(0.3), O.PHuberSmootherL1L2(0.3)
+        p.configure("l1", hm)
+    elif kind == "phuber_indbox":
+        hm, ohm = scsopt.PHuberSmootherIndBox(-1.0, 1.0, 0.6), O.PHuberSmootherIndBox(-1.0, 1.0, 0.6)
+        p.C_set = [-1.0, 1.0]
+        p.configure("indbox", hm)
+    elif kind == "exp_indbox":
+        hm, ohm = scsopt.ExponentialSmootherIndBox(-1.0, 1.0, 0.6), O.ExponentialSmootherIndBox(-1.0, 1.0, 0.6)
+        p.C_set = [-1.0, 1.0]
+        p.configure("indbox", hm)
+    else:
+        ind = np.array([[1 + 16 * g for g in range(4)], [16 + 16 * g for g in range(4)], [1, 2, 3, 1]])
+        p.P = scsopt.get_P(m, np.arange(1, m + 1), ind)
+        p.λ = [1e-3, 0.1]
+        hm = scsopt.PHuberSmootherGL(0.5, p)
+        p.configure("gl", hm)
+        ohm = O.Smoother("phuber_gl", 0.5, 2.0, 2.6, P=O.GroupP(m, ind, np.arange(1, m + 1)))
+    gr, Hr = p._smoother_eval(hm, x)
+    np.testing.assert_allclose(gr, ohm.grad(None, x), rtol=1e-14, atol=1e-300)
+    np.testing.assert_allclose(Hr, ohm.hess(None, x), rtol=1e-14, atol=1e-300)
+    if kind == "phuber_indbox":  # exact branch values (eps(), 0.0) survive bitwise
+        g_ref = ohm.grad(None, x)
+        sel = (g_ref == O.EPS) | (g_ref == 0.0)
+        assert np.array_equal(bits(gr[sel]), bits(g_ref[sel]))
+
+
+@pytest.mark.parametrize("N,m", [(48, 256), (1000, 300), (4099, 130), (5, 2)])
+def test_gram_and_gemv(N, m):
+    rng = np.random.default_rng(N + m)
+    A = rng.standard_normal((N, m))
+    w = rng.standard_normal(N)
+    p = scsopt.Problem(A, np.zeros(N), np.zeros(m), losses.least_squares(), 1.0)
+    G = p.gram(w)
+    terms = np.abs(A).T @ (np.abs(w)[:, None] * np.abs(A))
+    ref = A.T @ (w[:, None] * A)
+    lo = np.tril_indices(m)
+    assert np.all(np.abs(G[lo] - ref[lo]) <= 1e-13 * terms[lo] + 1e-300)
+    x = rng.standard_normal(m)
+    z = p.gemv_n(x)
+    np.testing.assert_allclose(z, A @ x, rtol=0, atol=1e-13 * float(np.max(np.abs(A) @ np.abs(x))))
+    t = p.gemv_t(w)
+    np.testing.assert_allclose(t, A.T @ w, rtol=0, atol=1e-13 * float(np.max(np.abs(A).T @ np.abs(w))))
+
+
+def test_gram_linearity_large():
+    """Size-independent property at a larger size: G(w1 + w2) == G(w1) + G(w2) (fp64 tolerance)."""
+    N, m = 1 << 15, 1024
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3)
+    rng = np.random.default_rng(3)
+    w1, w2 = rng.random(N), rng.random(N)
+    G1, G2, G12 = p.gram(w1), p.gram(w2), p.gram(w1 + w2)
+    lo = np.tril_indices(m)
+    scale = np.abs(G12[lo]).max()
+    assert np.max(np.abs(G12[lo] - G1[lo] - G2[lo])) <= 1e-12 * scale
+
+
+# ---------------------------------------------------------------------------
+# the reference's own test problems through iterate()
+# ---------------------------------------------------------------------------
+def _compare_solution(sol, ref, rtol=1e-8):
+    assert sol.epochs == ref["epochs"]
+    assert len(sol.obj) == len(ref["obj"])
+    np.testing.assert_allclose(sol.obj, ref["obj"], rtol=rtol, atol=0)
+    np.testing.assert_allclose(sol.fval, ref["fval"], rtol=rtol, atol=0)
+    np.testing.assert_allclose(sol.x, ref["x"], rtol=1e-7, atol=1e-12)
+
+
+@pytest.mark.parametrize("mname,meth", [("nscore", scsopt.ProxNSCORE), ("ggnscore", scsopt.ProxGGNSCORE),
+                                        ("lqnscore", scsopt.ProxLQNSCORE)])
+@pytest.mark.parametrize("reg", ["l1", "l2"])
+def test_reference_logistic(golden, mname, meth, reg):
+    """test/test_algs.jl:15-78 on the device + golden trajectory."""
+    model = scsopt.Problem(np.array(LOGI_A), np.array(LOGI_Y, float), X0, losses.logistic_margin(1 / 5), 1,
+                           out_fn=losses.sigmoid_ce(1 / 5))
+    sol = scsopt.iterate(meth(), model, reg, scsopt.PHuberSmootherL1L2(1), verbose=0)
+    assert np.allclose(model.x, 0.0)
+    assert sol.epochs + 1 >= 1
+    assert sol.rel[-1] <= 1e-6
+    assert sol.objrel[-1] <= 1e-6
+    _compare_solution(sol, golden["cases"][f"logistic_{mname}_{reg}"])
+    assert np.array_equal(np.signbit(sol.x), np.signbit(np.array(golden["cases"][f"logistic_{mname}_{reg}"]["x"])))
+
+
+@pytest.mark.parametrize("sname,alpha", [("phuber", 0.8), ("exp", 1.0)])
+def test_reference_indbox(golden, sname, alpha):
+    """test/test_algs.jl:82-108."""
+    model = scsopt.Problem(np.array(QP_A), np.array(QP_Y), QP_X0, losses.quadratic(), 1e-4, C_set=[-1.0, 1.0],
+                           sol=np.array(QP_XS))
+    hm = (scsopt.PHuberSmootherIndBox(-1.0, 1.0, 0.6) if sname == "phuber"
+          else scsopt.ExponentialSmootherIndBox(-1.0, 1.0, 0.6))
+    sol = scsopt.iterate(scsopt.ProxNSCORE(), model, "indbox", hm, alpha=alpha, verbose=0)
+    assert sol.rel[-1] <= 1e-3
+    assert sol.objrel[-1] <= 1e-3
+    _compare_solution(sol, golden["cases"][f"boxqp_nscore_{sname}"])
+
+
+def test_rosenbrock_c1(golden):
+    """BASELINE configs[0]: README quick start (ProblemGeneric, ProxLQNSCORE m=10, l1 λ=1e-8)."""
+    model = scsopt.Problem(X0, losses.rosenbrock(), 1e-8)
+    sol = scsopt.iterate(scsopt.ProxLQNSCORE(use_prox=True, m=10), model, "l1", scsopt.PHuberSmootherL1L2(1.0),
+                         verbose=0)
+    np.testing.assert_allclose(sol.x, [1.0, 1.0], atol=1e-6)
+    _compare_solution(sol, golden["cases"]["rosenbrock_lqnscore_l1"], rtol=1e-7)
+
+
+# ---------------------------------------------------------------------------
+# medium synthetic problems: device trajectory vs oracle on identical inputs
+# ---------------------------------------------------------------------------
+def _synthetic_pair(method, N=4096, m=256, reg="l1", lam=2e-3, mu=1.0, max_epoch=12, **mkw):
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    if method == "ggn":
+        f, out, kind, of = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N), 1, \
+            O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+    elif method == "nscore":
+        f, out, kind, of = losses.logistic_margin(1.0 / N), None, 2, O.Loss("logistic_margin", 1.0 / N)
+    else:
+        f, out, kind, of = losses.least_squares(1.0 / N), None, 3, O.Loss("least_squares", 1.0 / N)
+    p = scsopt.Problem.synthetic(N, m, x0, f, lam, kind=kind, seed=99, out_fn=out)
+    A, y = p.get_data()
+    om = O.Problem(A, y, x0, of, lam)
+    meth = {"ggn": (scsopt.ProxGGNSCORE, O.ProxGGNSCORE), "nscore": (scsopt.ProxNSCORE, O.ProxNSCORE),
+            "lqn": (scsopt.ProxLQNSCORE, O.ProxLQNSCORE)}[method]
+    sol = scsopt.iterate(meth[0](**mkw), p, reg, scsopt.PHuberSmootherL1L2(mu), max_epoch=max_epoch, verbose=0)
+    osol = O.iterate(meth[1](**mkw), om, reg, O.PHuberSmootherL1L2(mu), max_epoch=max_epoch)
+    return p, om, sol, osol
+
+
+@pytest.mark.parametrize("method", ["ggn", "nscore", "lqn"])
+def test_synthetic_trajectory(method):
+    p, om, sol, osol = _synthetic_pair(method)
+    assert sol.epochs == osol.epochs
+    assert len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("method", ["ggn", "nscore", "lqn"])
+def test_prox_support_pattern_per_step(method):
+    """Lock-step: both implementations step from the same x; sign/support of x_new must match
+    except within 1e-9·t of the l1 threshold."""
+    N, m, lam = 2048, 192, 5e-3
+    p, om, _, _ = _synthetic_pair(method, N=N, m=m, lam=lam, max_epoch=1)
+    hm, ohm = scsopt.PHuberSmootherL1L2(1.0), O.PHuberSmootherL1L2(1.0)
+    meth = {"ggn": (scsopt.ProxGGNSCORE, O.ProxGGNSCORE), "nscore": (scsopt.ProxNSCORE, O.ProxNSCORE),
+            "lqn": (scsopt.ProxLQNSCORE, O.ProxLQNSCORE)}[method]
+    dm, omth = meth[0](), meth[1]()
+    p.configure("l1", hm)
+    from scsopt.iterate import init_method, step
+    init_method(dm, p)
+    omth.init(om.x0)
+    x = om.x0.copy()
+    xp = x.copy()
+    checked = 0
+    for it in range(1, 6):
+        xn_d, dx_d, pri_d = step(dm, p, "l1", hm, x, xp, it, return_dx=True)
+        xn_o, pri_o = O.step(omth, om, "l1", ohm, x, xp, None, it)
+        t = (0.5 * lam) / (1.0 / ohm.hess(None, x))  # prox threshold, step_size 0.5 (ss_type 1, L = nothing)
+        z = x + dx_d
+        sel = np.abs(np.abs(z) - t) > 1e-9 * t          # away from the soft-threshold
+        assert np.array_equal((xn_d == 0)[sel], (xn_o == 0)[sel])
+        assert np.array_equal(np.signbit(xn_d)[sel], np.signbit(xn_o)[sel])
+        np.testing.assert_allclose(xn_d, xn_o, rtol=1e-7, atol=1e-10)
+        assert pri_d == pytest.approx(pri_o, rel=1e-7)
+        checked += int(sel.sum())
+        xp, x = x, xn_o
+    assert checked > 0
+
+
+def test_lqn_bb_and_linesearch():
+    """ss_type 2 (inverse BB, utils.jl:43-48) and ss_type 3 with L set (linesearch, utils.jl:27-35)."""
+    for ss, alpha in ((2, None), (3, 0.5)):
+        N, m = 1024, 64
+        x0 = np.random.default_rng(5).standard_normal(m)
+        p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=5)
+        A, y = p.get_data()
+        om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), 1e-3)
+        sol = scsopt.iterate(scsopt.ProxLQNSCORE(ss_type=ss, m=5), p, "l1", scsopt.PHuberSmootherL1L2(0.5),
+                             alpha=alpha, max_epoch=15, verbose=0)
+        osol = O.iterate(O.ProxLQNSCORE(ss_type=ss, m=5), om, "l1", O.PHuberSmootherL1L2(0.5), alpha=alpha,
+                         max_epoch=15)
+        assert len(sol.obj) == len(osol.obj)
+        np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
+
+
+def test_nscore_linesearch():
+    N, m = 1024, 48
+    x0 = np.random.default_rng(6).standard_normal(m)
+    p = scsopt.Problem.synthetic(N, m, x0, losses.logistic_margin(1.0 / N), 1e-3, kind=2, seed=6)
+    A, y = p.get_data()
+    om = O.Problem(A, y, x0, O.Loss("logistic_margin", 1.0 / N), 1e-3)
+    sol = scsopt.iterate(scsopt.ProxNSCORE(ss_type=3), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=8,
+                         verbose=0)
+    osol = O.iterate(O.ProxNSCORE(ss_type=3), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=8)
+    assert len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
+
+
+def test_group_lasso_ggn():
+    """C4 in miniature: least squares + sparse-group lasso, ProxGGNSCORE + PHuberSmootherGL."""
+    N, m, gs = 2048, 128, 16
+    x0 = np.random.default_rng(8).standard_normal(m)
+    ng = m // gs
+    ind = np.array([[1 + gs * g for g in range(ng)], [gs + gs * g for g in range(ng)], [1] * ng])
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), [1e-8, 0.05], kind=3, seed=8,
+                                 out_fn=losses.linear_ls(1.0 / N))
+    p.P = scsopt.get_P(m, np.arange(1, m + 1), ind)
+    A, y = p.get_data()
+    op = O.GroupP(m, ind, np.arange(1, m + 1))
+    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N, ggn="linear_ls"), [1e-8, 0.05], P=op)
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "gl", scsopt.PHuberSmootherGL(1e-2, p), max_epoch=10, verbose=0)
+    osol = O.iterate(O.ProxGGNSCORE(), om, "gl", O.PHuberSmootherGL(1e-2, om), max_epoch=10)
+    assert len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
+    np.testing.assert_allclose(sol.rel, osol.rel, rtol=1e-6)
+
+
+def test_determinism():
+    _, _, s1, _ = _synthetic_pair("ggn", N=2048, m=128, max_epoch=4)
+    _, _, s2, _ = _synthetic_pair("ggn", N=2048, m=128, max_epoch=4)
+    assert np.array_equal(bits(s1.x), bits(s2.x))
+    assert s1.obj == s2.obj
+
+
+# ---------------------------------------------------------------------------
+# reference error behaviour
+# ---------------------------------------------------------------------------
+def test_reference_errors():
+    model = scsopt.Problem(np.array(LOGI_A), np.array(LOGI_Y, float), X0, losses.logistic_margin(1 / 5), 1)
+    with pytest.raises(scsopt.ScsReferenceError, match="reg_name not valid."):
+        scsopt.iterate(scsopt.ProxNSCORE(), model, "l0", scsopt.PHuberSmootherL1L2(1), verbose=0)
+    with pytest.raises(scsopt.ScsReferenceError, match=r"Please, choose ss_type in \[1, 2, 3\]."):
+        scsopt.iterate(scsopt.ProxNSCORE(ss_type=4), model, "l1", scsopt.PHuberSmootherL1L2(1), verbose=0)
+    with pytest.raises(scsopt.ScsReferenceError, match="MethodError"):
+        scsopt.iterate(scsopt.ProxNSCORE(ss_type=2), model, "l1", scsopt.PHuberSmootherL1L2(1), verbose=0)
+    m2 = scsopt.Problem(np.array(LOGI_A), np.array(LOGI_Y, float), X0, losses.logistic_margin(1 / 5), 1,
+                        P=scsopt.get_P(2, np.arange(1, 3), np.array([[1], [2], [1]])))
+    with pytest.raises(scsopt.ScsReferenceError, match="exactly two entries"):
+        m2.configure("gl", scsopt.PHuberSmootherL1L2(1))

@@ -1,0 +1,131 @@
+"""CPU: pin the oracle against the reference's own tests, analytic known answers and
+the committed golden fixtures (tests/golden/make_golden.py)."""
+import math
+
+import numpy as np
+import pytest
+
+import scsopt_oracle as O
+from make_golden import LOGI_A, LOGI_Y, X0, QP_A, QP_Y, QP_X0, QP_XS
+
+
+def logistic_model(ggn=True):
+    return O.Problem(np.array(LOGI_A), np.array(LOGI_Y, float), X0,
+                     O.Loss("logistic_margin", 1 / 5, ggn="sigmoid_ce" if ggn else None), 1)
+
+
+@pytest.mark.parametrize("meth", [O.ProxNSCORE, O.ProxGGNSCORE, O.ProxLQNSCORE])
+@pytest.mark.parametrize("reg", ["l1", "l2"])
+def test_reference_logistic_assertions(meth, reg):
+    """test/test_algs.jl:22-51 (and the batch/slice_samples copies :54-78)."""
+    model = logistic_model()
+    sol = O.iterate(meth(), model, reg, O.PHuberSmootherL1L2(1))
+    assert np.allclose(model.sol, 0.0)
+    assert sol.epochs + 1 >= 1
+    assert sol.rel[-1] <= 1e-6
+    assert sol.objrel[-1] <= 1e-6
+
+
+@pytest.mark.parametrize("smoother,alpha", [("phuber", 0.8), ("exp", 1.0)])
+def test_reference_indbox_assertions(smoother, alpha):
+    """test/test_algs.jl:82-108."""
+    sm = (O.PHuberSmootherIndBox(-1.0, 1.0, 0.6) if smoother == "phuber"
+          else O.ExponentialSmootherIndBox(-1.0, 1.0, 0.6))
+    model = O.Problem(np.array(QP_A), np.array(QP_Y), QP_X0, O.Loss("quadratic"), 1e-4, C_set=[-1.0, 1.0],
+                      sol=np.array(QP_XS))
+    sol = O.iterate(O.ProxNSCORE(), model, "indbox", sm, alpha=alpha)
+    assert sol.rel[-1] <= 1e-3
+    assert sol.objrel[-1] <= 1e-3
+
+
+def test_smoother_constants():
+    """test/test_smooth.jl:7-8, 13-14."""
+    h = O.PHuberSmootherL1L2(1)
+    assert h.Mh == 2.0 and h.nu == 2.6
+    h = O.PHuberSmootherIndBox(-1.0, 1.0, 1)
+    assert h.Mh == 2.0 and h.nu == 2.6
+
+
+def test_kat_boxqp_interior_optimum():
+    """x_star of test_algs.jl:85 is the unconstrained optimum A⁻¹(−y) (interior of the box)."""
+    xs = np.linalg.solve(np.array(QP_A), -np.array(QP_Y))
+    assert np.max(np.abs(xs - np.array(QP_XS))) < 3e-6
+    assert np.all(np.abs(xs) < 1)
+
+
+def test_kat_l1_logistic_zero():
+    """λ = 1 ≥ ‖∇f(0)‖∞ ⇒ x* = 0 exactly; the prox lands on exact zeros."""
+    model = logistic_model()
+    g0 = model.gradx(np.zeros(2))
+    assert np.max(np.abs(g0)) <= 1
+    sol = O.iterate(O.ProxNSCORE(), model, "l1", O.PHuberSmootherL1L2(1))
+    assert np.all(sol.x == 0.0)
+
+
+def test_kat_rosenbrock():
+    model = O.Problem(None, None, X0, O.Loss("rosenbrock"), 1e-8)
+    sol = O.iterate(O.ProxLQNSCORE(m=10), model, "l1", O.PHuberSmootherL1L2(1.0))
+    assert np.allclose(sol.x, [1.0, 1.0], atol=1e-6)
+
+
+def test_history_semantics_max_epoch():
+    """iterate.jl:219-231: with no early stop the pre-step x is pushed twice at max_epoch."""
+    model = O.Problem(None, None, X0, O.Loss("rosenbrock"), 1e-8)
+    sol = O.iterate(O.ProxLQNSCORE(m=10), model, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=5)
+    assert len(sol.obj) == 6
+    assert sol.obj[-1] == sol.obj[-2]
+    assert sol.pri_res_norm[0] is None
+    assert sol.epochs == 5
+
+
+def test_julia_scalar_semantics():
+    assert math.copysign(1, float(O.jl_max(-0.0, 0.0))) == 1.0
+    assert math.copysign(1, float(O.jl_max(0.0, -0.0))) == 1.0
+    assert math.copysign(1, float(O.jl_min(0.0, -0.0))) == -1.0
+    assert math.isnan(float(O.jl_max(np.nan, 1.0))) and math.isnan(float(O.jl_max(1.0, np.nan)))
+    assert math.copysign(1, float(O.jl_sign(-0.0))) == -1.0 and float(O.jl_sign(-3.0)) == -1.0
+    # prox l1 keeps signed zeros: sign(z)*max(|z|-t, 0)
+    out = O.prox_l1(np.array([-0.1, 0.1, -0.0, 0.0]), np.ones(4), 1.0, 1.0)
+    assert list(np.signbit(out)) == [True, False, True, False]
+
+
+def test_get_Mg_values():
+    """get_Mg(2, 2.6, 1, m) for the config sizes."""
+    assert O.get_Mg(2.0, 2.6, 1.0, 8192) == pytest.approx(12.1257, abs=1e-4)
+    assert O.get_Mg(2.0, 2.6, 1.0, 16384) == pytest.approx(13.9288, abs=1e-4)
+    assert O.get_Mg(2.0, 2.6, 1.0, 65536) == pytest.approx(18.3792, abs=1e-4)
+    with pytest.raises(ValueError, match="μ must be positive"):
+        O.get_Mg(2.0, 2.6, 0.0, 5)
+
+
+def test_phuber_indbox_kat():
+    """the `-x < a` quirk (phuber-smooth.jl:89) at x ∈ {−2,…,2}, μ = 0.6, box [−1, 1]."""
+    x = np.array([-2.0, -1.0, 0.0, 1.0, 2.0])
+    g = O.huber_grad_indbox(x, 0.6, -1.0, 1.0)
+    h = O.huber_hess_indbox(x, 0.6, -1.0, 1.0)
+    assert list(g[:3]) == [O.EPS] * 3 and g[3] == 0.0
+    assert g[4] == pytest.approx(-0.98058, abs=1e-5)
+    assert h[0] == pytest.approx(0.22698, abs=1e-5) and h[4] == pytest.approx(0.22698, abs=1e-5)
+    assert h[1] == pytest.approx(1 / 0.6, rel=1e-12) and h[3] == pytest.approx(1 / 0.6, rel=1e-12)
+    assert h[2] == O.EPS
+
+
+def test_golden_fixtures_reproduce(golden):
+    """The committed trajectories are what this oracle produces (regression pin)."""
+    import make_golden
+    fresh = make_golden.cases()
+    for name, ref in golden["cases"].items():
+        got = fresh[name]
+        assert got["epochs"] == ref["epochs"], name
+        assert len(got["obj"]) == len(ref["obj"]), name
+        np.testing.assert_allclose(got["obj"], ref["obj"], rtol=1e-13, atol=0, err_msg=name)
+        np.testing.assert_allclose(got["x"], ref["x"], rtol=1e-12, atol=1e-300, err_msg=name)
+
+
+def test_golden_kernel_vectors(golden):
+    k = golden["kernels"]
+    x = np.array(k["x"])
+    np.testing.assert_array_equal(O.huber_grad(x, 1.0), np.array(k["phuber_l1l2_mu1"]["grad"]))
+    p = k["prox_in"]
+    out = O.prox_l1(np.array(p["z"]), 1.0 / np.array(p["Hr"]), p["lam"], p["alpha"])
+    np.testing.assert_array_equal(out, np.array(k["prox_l1"]))
