@@ -129,7 +129,8 @@ def main():
                          "kernel": "gram_f64_kernel", "avg_ms": gram_avg_ms,
                          "flops_per_launch": gram_flops},
             "breakdown_ms_per_step": {k.replace("_ms", ""): tm[k] / args.steps for k in tm if k.endswith("_ms")},
-            "hbm_gbs_streaming": (2.0 * 8 * N_local * m) / (tm["gemv_ms"] * 1e-3) / 1e9 / max(1, tm["gemv_calls"] / 2)
+            # streaming passes (A·x in f(x), Aᵀv in step!): each reads the local A once
+            "hbm_gbs_streaming": (tm["gemv_calls"] * 8.0 * N_local * m) / (tm["gemv_ms"] * 1e-3) / 1e9
             if tm["gemv_calls"] else None,
             "objective_last": objs[-1],
         }

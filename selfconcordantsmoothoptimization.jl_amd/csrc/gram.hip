@@ -39,9 +39,21 @@ constexpr int GBK = 16;   // samples per stage
 
 __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
 
+// Workgroup barrier that orders LDS only: the staged global loads (two stages
+// ahead) stay in flight across it (a __syncthreads() here makes hipcc drain
+// vmcnt(0) first).  "memory" clobbers keep the compiler from moving LDS
+// accesses across.
+#define LDS_BARRIER()                                          \
+  do {                                                         \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
+    __builtin_amdgcn_s_barrier();                              \
+    asm volatile("" ::: "memory");                             \
+  } while (0)
+
+template <bool NOLOAD>
 __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
-    const double* __restrict__ A, int64_t lda, const double* __restrict__ w, int64_t Nk,
-    const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int packed) {
+    const double* __restrict__ A, int64_t lda, const double* __restrict__ w, int64_t k0, int64_t Nk,
+    const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int packed, int accumulate) {
   // All LDS in ONE array (cdna_hip_programming.md §5 item 4a): [buf][panel][128 x 16]
   __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GT * GBK];
 
@@ -63,6 +75,7 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
   v2d ra[4], rb[4], rw;
 
   auto gload = [&](int64_t n0) {
+    if (NOLOAD && n0 > k0) return;  // timing-only experiment: operands stay in registers
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t f = sf0 + 32 * i;
@@ -90,13 +103,13 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
 
   const int fl = lane & 15, g = lane >> 4, s = swz(fl);
-  const int nk = (int)(Nk / GBK);
+  const int nk = (int)((Nk - k0) / GBK);
 
-  gload(0);
+  gload(k0);
   swrite(0);
   __syncthreads();
   for (int k = 0; k < nk; ++k) {
-    if (k + 1 < nk) gload((int64_t)(k + 1) * GBK);
+    if (k + 1 < nk) gload(k0 + (int64_t)(k + 1) * GBK);
     const double* la = lds + ((k & 1) * 2 + 0) * GT * GBK;
     const double* lb = lds + ((k & 1) * 2 + 1) * GT * GBK;
 #pragma unroll
@@ -132,7 +145,8 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
         for (int r = 0; r < 4; ++r) {
           const int row = wr * 64 + 16 * ti + g + 4 * r;
           const int col = wc * 64 + 16 * tj + fl;
-          Gt[col * GT + row] = acc[ti][tj][r];
+          if (accumulate) Gt[col * GT + row] += acc[ti][tj][r];
+          else Gt[col * GT + row] = acc[ti][tj][r];
         }
   } else {
 #pragma unroll
@@ -143,7 +157,137 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
         for (int r = 0; r < 4; ++r) {
           const int64_t row = (int64_t)bi * GT + wr * 64 + 16 * ti + g + 4 * r;
           const int64_t col = (int64_t)bj * GT + wc * 64 + 16 * tj + fl;
-          G[col * ldg + row] = acc[ti][tj][r];
+          if (accumulate) G[col * ldg + row] += acc[ti][tj][r];
+          else G[col * ldg + row] = acc[ti][tj][r];
+        }
+  }
+}
+
+// Variant: global loads issued two stages ahead (two register staging sets,
+// loop unrolled by 2 so every set index is static).
+__global__ __launch_bounds__(256, 2) void gram_f64_pf2_kernel(
+    const double* __restrict__ A, int64_t lda, const double* __restrict__ w, int64_t k0, int64_t Nk,
+    const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int packed, int accumulate) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GT * GBK];
+  const int orig = blockIdx.x;
+  const int q8 = ntiles / 8, r8 = ntiles % 8, xcd = orig % 8;
+  const int tix = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int2 tl = tiles[tix];
+  const int bi = tl.x, bj = tl.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const double* __restrict__ Ai = A + (int64_t)bi * GT * lda;
+  const double* __restrict__ Aj = A + (int64_t)bj * GT * lda;
+  const int sc = tid & 7;
+  const int sf0 = tid >> 3;
+  v2d ra0[4], rb0[4], rw0, ra1[4], rb1[4], rw1;
+  const int nk = (int)((Nk - k0) / GBK);
+
+  // buffer loads: wave-uniform descriptors (panel bases), one 32-bit per-lane offset,
+  // the feature-group / sample offsets in soffset (cdna_hip_programming.md T8/T20)
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ai, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Aj, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rWv = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, 0x7fffffff, 0x00020000);
+  const int voff = (int)(((int64_t)sf0 * lda + 2 * sc) * 8);
+  const int wvoff = 2 * sc * 8;
+  const int fstride = (int)(32 * lda * 8);
+#define GLOAD(RA, RB, RW, n0)                                                                              \
+  do {                                                                                                     \
+    const int nb_ = (int)((n0) * 8);                                                                       \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                        \
+      RA[i] = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rA, voff, nb_ + i * fstride, 0)); \
+      RB[i] = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rB, voff, nb_ + i * fstride, 0)); \
+    }                                                                                                      \
+    RW = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rWv, wvoff, nb_, 0));               \
+    __builtin_amdgcn_sched_barrier(0); /* keep each set's loads contiguous in issue order */               \
+  } while (0)
+#define SWRITE(RA, RB, RW, buf)                                            \
+  do {                                                                     \
+    double* la_ = lds + ((buf) * 2 + 0) * GT * GBK;                        \
+    double* lb_ = lds + ((buf) * 2 + 1) * GT * GBK;                        \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                        \
+      const int f = sf0 + 32 * i;                                          \
+      const int off = f * GBK + 2 * (sc ^ swz(f));                         \
+      *(v2d*)(la_ + off) = RA[i];                                          \
+      *(v2d*)(lb_ + off) = RB[i] * RW;                                     \
+    }                                                                      \
+  } while (0)
+
+  v4d acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
+  const int fl = lane & 15, g = lane >> 4, s = swz(fl);
+
+  auto compute = [&](int buf) {
+    const double* la = lds + (buf * 2 + 0) * GT * GBK;
+    const double* lb = lds + (buf * 2 + 1) * GT * GBK;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int pc = ((4 * p + g) ^ s) * 2;
+      v2d a[4], b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a[t] = *(const v2d*)(la + (wr * 64 + 16 * t + fl) * GBK + pc);
+        b[t] = *(const v2d*)(lb + (wc * 64 + 16 * t + fl) * GBK + pc);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < 4; ++tj)
+            acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
+    }
+  };
+
+  // prologue: stage 0 -> LDS buf 0, stage 1 in flight (set 1)
+  GLOAD(ra0, rb0, rw0, k0);
+  if (nk > 1) GLOAD(ra1, rb1, rw1, k0 + GBK);
+  SWRITE(ra0, rb0, rw0, 0);
+  LDS_BARRIER();
+  int k = 0;
+  for (; k + 2 <= nk; k += 2) {
+    // even step: compute buf0 (stage k); set0 <- stage k+2; buf1 <- set1 (stage k+1)
+    if (k + 2 < nk) GLOAD(ra0, rb0, rw0, k0 + (int64_t)(k + 2) * GBK);
+    compute(0);
+    SWRITE(ra1, rb1, rw1, 1);
+    LDS_BARRIER();
+    // odd step: compute buf1 (stage k+1); set1 <- stage k+3; buf0 <- set0 (stage k+2)
+    if (k + 3 < nk) GLOAD(ra1, rb1, rw1, k0 + (int64_t)(k + 3) * GBK);
+    compute(1);
+    if (k + 2 < nk) SWRITE(ra0, rb0, rw0, 0);
+    LDS_BARRIER();
+  }
+  if (k < nk) compute(0);  // odd stage count: last stage sits in buf 0
+#undef GLOAD
+#undef SWRITE
+
+  if (packed) {
+    double* Gt = G + (int64_t)tix * GT * GT;
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wr * 64 + 16 * ti + g + 4 * r;
+          const int col = wc * 64 + 16 * tj + fl;
+          if (accumulate) Gt[col * GT + row] += acc[ti][tj][r];
+          else Gt[col * GT + row] = acc[ti][tj][r];
+        }
+  } else {
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = (int64_t)bi * GT + wr * 64 + 16 * ti + g + 4 * r;
+          const int64_t col = (int64_t)bj * GT + wc * 64 + 16 * tj + fl;
+          if (accumulate) G[col * ldg + row] += acc[ti][tj][r];
+          else G[col * ldg + row] = acc[ti][tj][r];
         }
   }
 }
@@ -175,8 +319,23 @@ void gram_tile_list(int nb, int2* out, int* ntiles) {
 
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,
                        int ntiles, double* G, int64_t ldg, int packed, hipStream_t st) {
-  hipLaunchKernelGGL(gram_f64_kernel, dim3(ntiles), dim3(256), 0, st, A, lda, w, Nk, tiles, ntiles, G, ldg,
-                     packed);
+  hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
+                     ntiles, G, ldg, packed, 0);
+  return hipGetLastError();
+}
+
+// experiment hook (probe_gram): K range [k0, k1), accumulate into G, optional no-load timing build
+hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
+                          int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
+  if (noload == 2)
+    hipLaunchKernelGGL(gram_f64_pf2_kernel, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G, ldg,
+                       0, accumulate);
+  else if (noload)
+    hipLaunchKernelGGL(gram_f64_kernel<true>, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G,
+                       ldg, 0, accumulate);
+  else
+    hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G,
+                       ldg, 0, accumulate);
   return hipGetLastError();
 }
 

@@ -12,6 +12,8 @@ namespace scs {
 void gram_tile_list(int nb, int2* out, int* ntiles);
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
                        double* G, int64_t ldg, int packed, hipStream_t st);
+hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
+                          int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st);
 }
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -76,7 +78,44 @@ static int run(int64_t N, int64_t m, int reps, bool check) {
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= reps;
-  double alg = (double)N * m * (m + 1);   // symmetric Gram, algorithmic
+  const double alg = (double)N * m * (m + 1);   // symmetric Gram, algorithmic
+  if (getenv("GRAM_EXPERIMENTS")) {
+    // (a) operands held in registers after the first stage: compute + LDS + barrier ceiling
+    CK(hipEventRecord(e0));
+    CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 1, 0));
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float t; CK(hipEventElapsedTime(&t, e0, e1));
+    printf("EXP noload: %.3f ms  %.2f TF/s\n", t, alg / t / 1e9);
+    // (d) prefetch distance 2
+    {
+      CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 2, 0));
+      CK(hipEventRecord(e0));
+      CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 2, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      printf("EXP prefetch2: %.3f ms  %.2f TF/s\n", t, alg / t / 1e9);
+    }
+    // (c) only the first 512*floor(nt/512) tiles: whole rounds, no partial tail round
+    {
+      const int ntr = (nt / 512) * 512;
+      CK(hipEventRecord(e0));
+      CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, ntr, G, m, 0, 0, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      printf("EXP whole-rounds %d tiles: %.3f ms  %.2f TF/s (per-tile rate)\n", ntr, t,
+             alg * ntr / nt / t / 1e9);
+    }
+    // (b) K split into chunks of 2^k samples, one launch per chunk, accumulating
+    for (int64_t kc : {(int64_t)1 << 17, (int64_t)1 << 15, (int64_t)1 << 13}) {
+      if (kc >= N) continue;
+      CK(hipEventRecord(e0));
+      for (int64_t k0 = 0; k0 < N; k0 += kc)
+        CK(scs::gram_launch_ex(A, lda, w, k0, k0 + kc < N ? k0 + kc : N, dtl, nt, G, m, k0 > 0, 0, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      printf("EXP kchunk %ld: %.3f ms  %.2f TF/s\n", (long)kc, t, alg / t / 1e9);
+    }
+  }
   double exe = 2.0 * N * 128.0 * 128.0 * nt;  // executed incl. full diagonal tiles
   printf("GRAM N=%ld m=%ld tiles=%d: %.3f ms/launch  alg %.2f TF/s  exec %.2f TF/s\n", (long)N, (long)m, nt, ms,
          alg / ms / 1e9, exe / ms / 1e9);

@@ -419,6 +419,15 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
   return c->zfval;
 }
 
+// out (device, m) = Aᵀ v over the local rows (no reduction)
+void gemv_t_local(scs_ctx* c, const double* v, double* out) {
+  hipEvent_t e0;
+  tbegin(c, T_GEMV, &e0);
+  HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
+  HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, out, c->st));
+  tend(c, T_GEMV, e0);
+}
+
 // out (device, m) = Aᵀ v (local, then all-reduced across ranks)
 void gemv_t_global(scs_ctx* c, const double* v, double* out) {
   hipEvent_t e0;
@@ -607,16 +616,14 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
     } else {
       forward(c, xh, c->x, EPI_GRAD | EPI_HESS);
       // local Aᵀg (not yet reduced); reduced together with the Gram
-      HCK(launch_gemv_t(c->A, c->Npad, c->Npad, m, c->mpad, c->gN, c->tpart, c->st));
-      HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, m, c->gtmp, c->st));
+      gemv_t_local(c, c->gN, c->gtmp);
       gram_and_reduce(c, c->hN, c->gtmp);
     }
   } else {
     if (c->ggn == SCS_GGN_NONE) fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs an out_fn / GGN loss kind");
     // J, residual, Q (prox-GGN-SCORE.jl:44-56) -> w = s²q, v = s·r
     forward(c, xh, c->x, EPI_GGN);
-    HCK(launch_gemv_t(c->A, c->Npad, c->Npad, m, c->mpad, c->vN, c->tpart, c->st));
-    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, m, c->gtmp, c->st));
+    gemv_t_local(c, c->vN, c->gtmp);
     gram_and_reduce(c, c->wN, c->gtmp);
   }
   // rhs = ∇f + λ gr (NSCORE) | Jᵀr + λ gr (GGN: Jt*[r;1], prox-GGN-SCORE.jl:121-130)
