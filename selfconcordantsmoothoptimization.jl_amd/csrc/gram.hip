@@ -35,6 +35,7 @@
 namespace scs {
 
 constexpr int GT = 128;   // output tile edge
+enum { GRAM_PACKED = 1, GRAM_ACCUMULATE = 2, GRAM_UPPER = 4 };
 constexpr int GBK = 16;   // samples per stage
 
 __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
@@ -52,8 +53,10 @@ __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
 
 template <bool NOLOAD>
 __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
-    const double* __restrict__ A, int64_t lda, const double* __restrict__ w, int64_t k0, int64_t Nk,
-    const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int packed, int accumulate) {
+    const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
+    const double* __restrict__ w, int64_t k0, int64_t Nk, const int2* __restrict__ tiles, int ntiles,
+    double* __restrict__ G, int64_t ldg, int flags) {
+  const int packed = flags & GRAM_PACKED, accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
   // All LDS in ONE array (cdna_hip_programming.md §5 item 4a): [buf][panel][128 x 16]
   __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GT * GBK];
 
@@ -66,8 +69,8 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const double* __restrict__ Ai = A + (int64_t)bi * GT * lda;
-  const double* __restrict__ Aj = A + (int64_t)bj * GT * lda;
+  const double* __restrict__ Ai = A1 + (int64_t)bi * GT * lda1;
+  const double* __restrict__ Aj = A2 + (int64_t)bj * GT * lda2;
 
   // staging map: chunk q = tid + 256*i  ->  feature f = (tid>>3) + 32 i, chunk c = tid & 7
   const int sc = tid & 7;
@@ -79,8 +82,8 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t f = sf0 + 32 * i;
-      ra[i] = *(const v2d*)(Ai + f * lda + n0 + 2 * sc);
-      rb[i] = *(const v2d*)(Aj + f * lda + n0 + 2 * sc);
+      ra[i] = *(const v2d*)(Ai + f * lda1 + n0 + 2 * sc);
+      rb[i] = *(const v2d*)(Aj + f * lda2 + n0 + 2 * sc);
     }
     rw = *(const v2d*)(w + n0 + 2 * sc);
   };
@@ -134,33 +137,27 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
   }
 
   // Epilogue.  v_mfma_f64_16x16x4_f64 C/D map: col = lane&15, row = (lane>>4) + 4*r
-  // (cdna_hip_programming.md §3; verified by probe_mfma).
-  if (packed) {
-    double* Gt = G + (int64_t)tix * GT * GT;  // tile-local column-major, packed in list order
+  // (cdna_hip_programming.md §3; verified by probe_mfma).  Element (i, j) of the
+  // tile (i in panel bi of A1, j in panel bj of A2) goes to
+  //   packed : tile-local column-major slot tix  (row i, col j)
+  //   upper  : G[(bi*128+i)*ldg + bj*128+j]       (transposed: row j, col i -- the
+  //            upper triangle when bi >= bj; consecutive lanes store consecutive j)
+  //   default: G[(bj*128+j)*ldg + bi*128+i]       (lower triangle when bi >= bj)
 #pragma unroll
-    for (int ti = 0; ti < 4; ++ti)
+  for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
-      for (int tj = 0; tj < 4; ++tj)
+    for (int tj = 0; tj < 4; ++tj)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wr * 64 + 16 * ti + g + 4 * r;
-          const int col = wc * 64 + 16 * tj + fl;
-          if (accumulate) Gt[col * GT + row] += acc[ti][tj][r];
-          else Gt[col * GT + row] = acc[ti][tj][r];
-        }
-  } else {
-#pragma unroll
-    for (int ti = 0; ti < 4; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < 4; ++tj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = (int64_t)bi * GT + wr * 64 + 16 * ti + g + 4 * r;
-          const int64_t col = (int64_t)bj * GT + wc * 64 + 16 * tj + fl;
-          if (accumulate) G[col * ldg + row] += acc[ti][tj][r];
-          else G[col * ldg + row] = acc[ti][tj][r];
-        }
-  }
+      for (int r = 0; r < 4; ++r) {
+        const int il = wr * 64 + 16 * ti + g + 4 * r;
+        const int jl = wc * 64 + 16 * tj + fl;
+        double* dst;
+        if (packed) dst = G + (int64_t)tix * GT * GT + jl * GT + il;
+        else if (upper) dst = G + ((int64_t)bi * GT + il) * ldg + (int64_t)bj * GT + jl;
+        else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GT + il;
+        if (accumulate) *dst += acc[ti][tj][r];
+        else *dst = acc[ti][tj][r];
+      }
 }
 
 // Variant: global loads issued two stages ahead (two register staging sets,
@@ -292,15 +289,16 @@ __global__ __launch_bounds__(256, 2) void gram_f64_pf2_kernel(
   }
 }
 
-// Scatter packed tiles (list order) into a column-major m_pad x m_pad matrix.
+// Scatter packed tiles (list order) into the upper triangle of a column-major
+// m_pad x m_pad matrix (same placement as GRAM_UPPER).
 __global__ void gram_unpack_kernel(const double* __restrict__ P, const int2* __restrict__ tiles,
                                    double* __restrict__ G, int64_t ldg) {
   const int t = blockIdx.y;
   const int2 tl = tiles[t];
   const double* Pt = P + (int64_t)t * GT * GT;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < GT * GT; e += gridDim.x * blockDim.x) {
-    const int col = e / GT, row = e % GT;
-    G[((int64_t)tl.y * GT + col) * ldg + (int64_t)tl.x * GT + row] = Pt[e];
+    const int j = e / GT, i = e % GT;   // packed: (row i, col j) column-major
+    G[((int64_t)tl.x * GT + i) * ldg + (int64_t)tl.y * GT + j] = Pt[e];
   }
 }
 
@@ -317,25 +315,45 @@ void gram_tile_list(int nb, int2* out, int* ntiles) {
   *ntiles = t;
 }
 
+// Row-major lower-triangle order: the first nb'(nb'+1)/2 entries are the list for nb' <= nb.
+void gram_tile_list_rowmajor(int nb, int2* out) {
+  int t = 0;
+  for (int i = 0; i < nb; ++i)
+    for (int j = 0; j <= i; ++j) out[t++] = make_int2(i, j);
+}
+
+hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                           int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
+                           hipStream_t st);
+
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,
                        int ntiles, double* G, int64_t ldg, int packed, hipStream_t st) {
-  hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
-                     ntiles, G, ldg, packed, 0);
+  return gram_launch_gen(A, lda, A, lda, w, 0, Nk, tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER, st);
+}
+
+// General form: operand panels from two matrices, K range [k0, k1), flags GRAM_*.
+hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                           int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
+                           hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles,
+                     ntiles, G, ldg, flags);
   return hipGetLastError();
 }
 
 // experiment hook (probe_gram): K range [k0, k1), accumulate into G, optional no-load timing build
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
+  const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
   if (noload == 2)
     hipLaunchKernelGGL(gram_f64_pf2_kernel, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G, ldg,
                        0, accumulate);
   else if (noload)
-    hipLaunchKernelGGL(gram_f64_kernel<true>, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G,
-                       ldg, 0, accumulate);
+    hipLaunchKernelGGL(gram_f64_kernel<true>, dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags);
   else
-    hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G,
-                       ldg, 0, accumulate);
+    hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags);
   return hipGetLastError();
 }
 

@@ -23,8 +23,18 @@ struct ProxArgsH {
 void gram_tile_list(int nb, int2* out, int* ntiles);
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
                        double* G, int64_t ldg, int packed, hipStream_t st);
+void gram_tile_list_rowmajor(int nb, int2* out);
+hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                           int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
+                           hipStream_t st);
 hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,
                               hipStream_t st);
+
+// ---- chol.hip (upper Cholesky on MFMA; W holds the inverted diagonal blocks)
+hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const double* wpm,
+                       const int2* rowlist, const int2* trilist, int* info, hipStream_t st);
+hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
+                      hipStream_t st);
 
 // ---- vec.hip
 hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,

@@ -63,7 +63,7 @@ static int run(int64_t N, int64_t m, int reps, bool check) {
           double t = hA[i * lda + n] * hw[n] * hA[j * lda + n];
           s += t; sa += fabs(t);
         }
-        double e = fabs(hG[j * m + i] - s) / (sa > 0 ? sa : 1);
+        double e = fabs(hG[i * m + j] - s) / (sa > 0 ? sa : 1);  // upper triangle: (row j, col i)
         if (e > maxrel) maxrel = e;
       }
     printf("CHECK N=%ld m=%ld max |G-ref|/sum|terms| = %.3e  %s\n", (long)N, (long)m, maxrel,

@@ -110,6 +110,12 @@ struct scs_ctx {
   double *G = nullptr, *Gc = nullptr;
   int2* tiles = nullptr;
   int ntiles = 0;
+  double* W = nullptr;      // inverted diagonal blocks of the Cholesky factor [mpad/128][128*128]
+  double* wpm = nullptr;    // [128 x +1.0, 128 x -1.0] Gram weights for the factorization
+  double* ysol = nullptr;   // triangular-solve scratch (mpad)
+  int2* rowlist = nullptr;  // (0, j) tiles
+  int2* trilist = nullptr;  // row-major lower tiles
+  int* cinfo = nullptr;
   rocblas_handle blas = nullptr;
   rocblas_int* dinfo = nullptr;
   rocblas_int* ipiv = nullptr;
@@ -361,12 +367,25 @@ void ensure_gram(scs_ctx* c) {
   c->tiles = dalloc<int2>(c, nt);
   HCK(hipMemcpyAsync(c->tiles, tl.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->st));
   c->ntiles = nt;
+  {
+    const int nb2 = (int)(mp / 128);
+    c->W = dalloc<double>(c, (size_t)mp * 128);
+    c->ysol = dalloc<double>(c, mp);
+    c->wpm = dalloc<double>(c, 256);
+    std::vector<double> hw(256);
+    for (int i = 0; i < 256; ++i) hw[i] = i < 128 ? 1.0 : -1.0;
+    h2d(c, c->wpm, hw.data(), 256);
+    std::vector<int2> rl(nb2), tr((size_t)nb2 * (nb2 + 1) / 2);
+    for (int j = 0; j < nb2; ++j) rl[j] = make_int2(0, j);
+    gram_tile_list_rowmajor(nb2, tr.data());
+    c->rowlist = dalloc<int2>(c, nb2);
+    c->trilist = dalloc<int2>(c, tr.size());
+    HCK(hipMemcpyAsync(c->rowlist, rl.data(), sizeof(int2) * nb2, hipMemcpyHostToDevice, c->st));
+    HCK(hipMemcpyAsync(c->trilist, tr.data(), sizeof(int2) * tr.size(), hipMemcpyHostToDevice, c->st));
+    c->cinfo = dalloc<int>(c, 1);
+  }
   c->dinfo = dalloc<rocblas_int>(c, 1);
   c->ipiv = dalloc<rocblas_int>(c, mp);
-  if (!c->blas) {
-    RCK(rocblas_create_handle(&c->blas));
-    RCK(rocblas_set_stream(c->blas, c->st));
-  }
   sync(c);
 }
 
@@ -530,24 +549,29 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
   fail(c, SCS_ERR_REF, "linesearch did not terminate");
 }
 
-// solve (G + λ diag Hr) sol = rhs in place (rhs -> sol).  Cholesky first; LU
-// with partial pivoting (the reference's `\`, prox-N-SCORE.jl:204) when the
-// matrix is not numerically SPD (e.g. the indefinite Q of a CE loss on ±1
-// labels, test/test_algs.jl:10).
+// solve (G + λ diag Hr) sol = rhs in place (rhs -> sol, length m_pad, zero-padded).
+// Hand-written blocked Cholesky on MFMA (chol.hip) first; LU with partial
+// pivoting (the reference's `\`, prox-N-SCORE.jl:204) from the saved copy when
+// a pivot is not positive (e.g. the indefinite Q of a CE loss on ±1 labels,
+// test/test_algs.jl:10).
 void solve_system(scs_ctx* c, double* rhs) {
   const int64_t m = c->m, ld = c->mpad;
   hipEvent_t e0;
   tbegin(c, T_SOLVE, &e0);
-  HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * m, hipMemcpyDeviceToDevice, c->st));
-  RCK(rocsolver_dpotrf(c->blas, rocblas_fill_lower, (rocblas_int)m, c->G, (rocblas_int)ld, c->dinfo));
+  HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+  HCK(chol_factor(c->G, ld, m, ld, c->W, c->wpm, c->rowlist, c->trilist, c->cinfo, c->st));
   int info = 0;
-  HCK(hipMemcpyAsync(&info, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
   if (info == 0) {
-    RCK(rocsolver_dpotrs(c->blas, rocblas_fill_lower, (rocblas_int)m, 1, c->G, (rocblas_int)ld, rhs,
-                         (rocblas_int)m));
+    HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, c->st));
     c->lu_fallback_used = false;
   } else {
+    if (!c->blas) {
+      RCK(rocblas_create_handle(&c->blas));
+      RCK(rocblas_set_stream(c->blas, c->st));
+    }
     HCK(launch_symmetrize(c->Gc, ld, m, c->st));
     RCK(rocsolver_dgetrf(c->blas, (rocblas_int)m, (rocblas_int)m, c->Gc, (rocblas_int)ld, c->ipiv, c->dinfo));
     HCK(hipMemcpyAsync(&info, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
@@ -809,6 +833,14 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->G);
   dfree_t(c, c->Gc);
   dfree_t(c, c->tiles);
+  dfree_t(c, c->W);
+  dfree_t(c, c->wpm);
+  dfree_t(c, c->ysol);
+  dfree_t(c, c->rowlist);
+  dfree_t(c, c->trilist);
+  dfree_t(c, c->cinfo);
+  dfree_t(c, c->dinfo);
+  dfree_t(c, c->ipiv);
   c->ntiles = 0;
   invalidate_caches(c);
   c->has_data = false;
@@ -1116,6 +1148,7 @@ int scs_gram_eval(scs_ctx* c, const double* w, double* G, int64_t ldg) {
     tbegin(c, T_GRAM, &e0);
     HCK(gram_launch(c->A, c->Npad, c->wN, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->st));
     tend(c, T_GRAM, e0);
+    HCK(launch_symmetrize(c->G, c->mpad, c->m, c->st));
     HCK(hipMemcpy2DAsync(G, sizeof(double) * ldg, c->G, sizeof(double) * c->mpad, sizeof(double) * c->m, c->m,
                          hipMemcpyDeviceToHost, c->st));
     sync(c);

@@ -369,11 +369,12 @@ __global__ void diag_add_kernel(double* __restrict__ G, int64_t ldg, int64_t m, 
   if (i < m) G[i * ldg + i] += lam * Hr[i];
 }
 
-// copy the strictly-lower triangle onto the upper one (LU fallback needs the full matrix)
+// copy the strictly-upper triangle onto the lower one (the Gram stores the upper
+// triangle; the LU fallback and host copies need the full matrix)
 __global__ void symmetrize_kernel(double* __restrict__ G, int64_t ldg, int64_t m) {
-  const int64_t j = blockIdx.y;
+  const int64_t j = blockIdx.y;   // column of the upper element (row i < j)
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < j; i += (int64_t)gridDim.x * blockDim.x)
-    G[j * ldg + i] = G[i * ldg + j];
+    G[i * ldg + j] = G[j * ldg + i];
 }
 
 // G = 0.5*(A + Aᵀ) for the quadratic loss (Hessian of 1/2 x'Ax, m x m A)

@@ -312,3 +312,35 @@ def test_reference_errors():
                         P=scsopt.get_P(2, np.arange(1, 3), np.array([[1], [2], [1]])))
     with pytest.raises(scsopt.ScsReferenceError, match="exactly two entries"):
         m2.configure("gl", scsopt.PHuberSmootherL1L2(1))
+
+
+@pytest.mark.parametrize("m", [1000, 384])
+def test_blocked_cholesky_solve(m):
+    """The m x m solve (hand-written blocked Cholesky, chol.hip) inside ProxNSCORE steps,
+    m not a multiple of the 128 block (identity-padded tail), vs the oracle's LU."""
+    N = 4 * m + 37
+    x0 = np.random.default_rng(m).standard_normal(m)
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=m)
+    A, y = p.get_data()
+    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), 1e-3)
+    sol = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", scsopt.PHuberSmootherL1L2(0.5), max_epoch=4, verbose=0)
+    osol = O.iterate(O.ProxNSCORE(), om, "l1", O.PHuberSmootherL1L2(0.5), max_epoch=4)
+    assert len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-10)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-8, atol=1e-12)
+
+
+def test_indefinite_system_lu_fallback():
+    """Cross-entropy GGN on ±1 labels (test/test_algs.jl:10 form) gives an indefinite Q:
+    the Cholesky reports a non-positive pivot and the LU path (the reference's `\\`) takes over."""
+    N, m = 400, 24
+    rng = np.random.default_rng(4)
+    A = rng.standard_normal((N, m)) * 2.0
+    y = np.where(rng.random(N) < 0.5, -1.0, 1.0)
+    x0 = rng.standard_normal(m)
+    p = scsopt.Problem(A, y, x0, losses.logistic_margin(1 / N), 1e-3, out_fn=losses.sigmoid_ce(1 / N))
+    om = O.Problem(A, y, x0, O.Loss("logistic_margin", 1 / N, ggn="sigmoid_ce"), 1e-3)
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=3, verbose=0)
+    osol = O.iterate(O.ProxGGNSCORE(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=3)
+    assert len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
