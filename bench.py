@@ -1,17 +1,21 @@
-"""bench.py -- iterate!() iterations/s of ProxGGNSCORE on the BASELINE headline config.
+"""bench.py -- iterate!() iterations/s on the BASELINE configurations.
 
-Workload (BASELINE.json metric, configs[2]): sparse logistic regression,
-N = 2^20 samples x m = 2^14 features, fp64, A ~ N(0,1)/sqrt(m) generated on
-the device (synthetic; no dataset), y ~ Bernoulli(σ(A x_true)) ∈ {0,1},
+Default (the driver's line): BASELINE.json configs[2] -- ProxGGNSCORE sparse
+logistic regression, N = 2^20 samples x m = 2^14 features, fp64, A ~ N(0,1)/sqrt(m)
+generated on the device (synthetic; no dataset), y ~ Bernoulli(σ(A x_true)) ∈ {0,1},
 x_true 10 % dense, l1 with λ = 0.1·‖∇f(0)‖∞, PHuberSmootherL1L2(μ = 1),
 ProxGGNSCORE(ss_type = 1), f(A,y,x) = CE(y, σ(Ax)) with scale 1/N.
 
-One "step" = one iterate! epoch: f(x) + get_reg(x) + step!(ProxGGNSCORE)
-(J/residual/Q from σ(Ax), the MFMA Gram JᵀQJ = Aᵀ diag(s²q) A, Jᵀr, λ·diag(Hr),
-the m x m solve, SCORE damping and the prox).  N GPUs: A is row-sharded
-(strong scaling: the global problem is fixed), one all-reduce per step.
+One "step" = one iterate! epoch: f(x) + get_reg(x) + step! (for GGN: J/residual/Q
+from σ(Ax), the MFMA Gram JᵀQJ = Aᵀ diag(s²q) A, Jᵀr, λ·diag(Hr), the m x m
+Cholesky solve, SCORE damping and the prox).  N GPUs: A is row-sharded (strong
+scaling: the global problem is fixed), one all-reduce per step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Other configs (--config): c1 Rosenbrock ProxLQNSCORE (configs[0]), c2 ProxNSCORE
+logistic N=100k m=8k (configs[1]), c4 ProxGGNSCORE sparse-group lasso N=4M m=32k
+(configs[3]; needs >= 4 GPUs at full size).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -24,8 +28,63 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd"))
 
-FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix, AMD spec (not in the local guide)
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix, AMD spec; 64 cycles/MFMA confirmed by PMC
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "iterate!() iterations/sec + achieved HBM GB/s, ProxGGNSCORE n=1M m=16k"
+
+CONFIGS = {
+    "c1": dict(method="lqn", loss="rosenbrock", N=0, m=2, reg="l1", lam=1e-8, mu=1.0, mem=10,
+               workload="ProxLQNSCORE Rosenbrock + l1, BASELINE configs[0]"),
+    "c2": dict(method="nscore", loss="logistic_margin", kind=2, N=100_000, m=8192, reg="l1", lam_frac=0.1, mu=1.0,
+               workload="ProxNSCORE sparse-logistic (margin form) l1, BASELINE configs[1]"),
+    "c3": dict(method="ggn", loss="logistic_ce", kind=1, N=1 << 20, m=1 << 14, reg="l1", lam_frac=0.1, mu=1.0,
+               workload="ProxGGNSCORE sparse-logistic l1, BASELINE configs[2]"),
+    "c4": dict(method="ggn", loss="least_squares", kind=3, N=1 << 22, m=1 << 15, reg="gl", lam1=1e-8, lam_frac=0.1,
+               mu=1e-2, group=32, workload="ProxGGNSCORE sparse-group lasso (l1 + gl), BASELINE configs[3]"),
+    "c5": dict(method="lqn", loss="least_squares", sparse=True, N=1 << 20, m=1 << 16, rho=0.01, reg="indbox",
+               lam=1e-4, mu=0.6, mem=20,
+               workload="ProxLQNSCORE(mem=20) box-constrained least squares, sparse A (CSR+CSC, rho=0.01), "
+                        "indbox + PHuberSmootherIndBox, BASELINE configs[4]"),
+}
+
+
+def build_problem(cfg, N, m, comm, local, f32=False):
+    import numpy as np
+    import scsopt
+    from scsopt import losses
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    if cfg["loss"] == "rosenbrock":
+        x0 = np.array([0.5908446386657102, 0.7667970365022592])
+        model = scsopt.Problem(x0, losses.rosenbrock(), cfg["lam"], device=local)
+        return model, scsopt.PHuberSmootherL1L2(cfg["mu"]), scsopt.ProxLQNSCORE(m=cfg["mem"])
+    out = None
+    if cfg.get("sparse"):
+        model = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), cfg["lam"],
+                                                density=cfg["rho"], seed=2026, f32=f32, device=local,
+                                                C_set=[-1.0, 1.0])
+        return model, scsopt.PHuberSmootherIndBox(-1.0, 1.0, cfg["mu"]), scsopt.ProxLQNSCORE(m=cfg["mem"])
+    if cfg["loss"] == "logistic_ce":
+        f, out = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N)
+    elif cfg["loss"] == "logistic_margin":
+        f = losses.logistic_margin(1.0 / N)
+    else:
+        f, out = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N)
+    model = scsopt.Problem.synthetic(N, m, x0, f, 1.0, kind=cfg["kind"], seed=2026, density=0.1, out_fn=out,
+                                     device=local, comm=comm)
+    g0 = model.gradx(np.zeros(m))
+    if cfg["reg"] == "gl":
+        gs = cfg["group"]
+        ng = m // gs
+        ind = np.array([[1 + gs * g for g in range(ng)], [gs * (g + 1) for g in range(ng)], [1] * ng])
+        model.P = scsopt.get_P(m, np.arange(1, m + 1), ind)
+        gmax = float(np.max(np.linalg.norm(g0.reshape(ng, gs), axis=1)))
+        model.λ = [cfg["lam1"], cfg["lam_frac"] * gmax]
+        hmu = scsopt.PHuberSmootherGL(cfg["mu"], model)
+    else:
+        model.λ = cfg["lam_frac"] * float(np.max(np.abs(g0)))
+        hmu = scsopt.PHuberSmootherL1L2(cfg["mu"])
+    meth = {"ggn": scsopt.ProxGGNSCORE, "nscore": scsopt.ProxNSCORE, "lqn": scsopt.ProxLQNSCORE}[cfg["method"]]()
+    return model, hmu, meth
 
 
 def main():
@@ -33,18 +92,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--N", type=int, default=1 << 20)
-    ap.add_argument("--m", type=int, default=1 << 14)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--N", type=int, default=0, help="override the config's N")
+    ap.add_argument("--m", type=int, default=0, help="override the config's m")
+    ap.add_argument("--f32", action="store_true", help="c5: fp32-stored sparse values (fp64 accumulation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-Ns", type=int, default=2048)
     ap.add_argument("--cpu-ms", type=int, default=4096)
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
 
     import numpy as np
     import torch
     import torch.distributed as dist
     import scsopt
-    from scsopt import losses, shard
+    from scsopt import shard
     from scsopt.iterate import init_method, step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -55,15 +117,13 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         comm = shard.Comm(device=torch.device("cuda", local))
-    N, m = args.N, args.m
-    x0 = np.random.default_rng(1234).standard_normal(m)
-    model = scsopt.Problem.synthetic(N, m, x0, losses.logistic_ce(1.0 / N), 1.0, kind=1, seed=2026, density=0.1,
-                                     out_fn=losses.sigmoid_ce(1.0 / N), device=local, comm=comm)
-    g0 = model.gradx(np.zeros(m))
-    model.λ = 0.1 * float(np.max(np.abs(g0)))
-    hmu = scsopt.PHuberSmootherL1L2(1.0)
-    method = scsopt.ProxGGNSCORE()
-    model.configure("l1", hmu)
+    N = args.N or cfg["N"]
+    m = args.m or cfg["m"]
+    if cfg.get("sparse") and world > 1:
+        raise SystemExit("c5 runs on one GPU (BASELINE configs[4]); the sparse generator is single-context")
+    model, hmu, method = build_problem(cfg, N, m, comm, local, f32=args.f32)
+    reg = cfg["reg"]
+    model.configure(reg, hmu)
     init_method(method, model)
     ctx = model.ctx
 
@@ -73,7 +133,7 @@ def main():
         torch.cuda.synchronize()
         ctx.check(scsopt._lib.lib.scs_sync(ctx.h))
 
-    x = x0.copy()
+    x = model.x0.copy()
     x_prev = x.copy()
     it = 0
 
@@ -82,18 +142,21 @@ def main():
         it += 1
         fval = model.fx(x)                       # iterate.jl:189-190
         obj = fval + model.get_reg(x)
-        x_new, pri = step(method, model, "l1", hmu, x, x_prev, it)   # iterate.jl:233
+        x_new, pri = step(method, model, reg, hmu, x, x_prev, it)   # iterate.jl:233
         x_prev, x = x, x_new
         return obj, pri
 
+    steps, warmup = args.steps, args.warmup
+    if cfg["loss"] == "rosenbrock" and steps < 50:
+        steps = 50                               # microsecond-scale steps: time a meaningful batch
     ctx.check(scsopt._lib.lib.scs_timing_enable(ctx.h, 1))
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         one_epoch()
     barrier()
     ctx.check(scsopt._lib.lib.scs_timing_reset(ctx.h))
     t0 = time.perf_counter()
     objs = []
-    for _ in range(args.steps):
+    for _ in range(steps):
         objs.append(one_epoch()[0])
     barrier()
     dt = time.perf_counter() - t0
@@ -104,43 +167,63 @@ def main():
         dt = float(t.item())
 
     if rank == 0:
-        ms_step = 1e3 * dt / args.steps
-        value = args.steps / dt
+        ms_step = 1e3 * dt / steps
+        value = steps / dt
         N_local = model.N
-        gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])
-        gram_flops = float(N_local) * m * (m + 1)   # algorithmic symmetric Gram per launch
-        achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "r01_gram_pmc.json")
-        if os.path.exists(pmc) and world == 1:
-            with open(pmc) as f:
-                pm = json.load(f)
-            if pm.get("N") == N and pm.get("m") == m:
-                traffic = pm.get("hbm_bytes_per_launch")
         line = {
-            "metric": "iterate!() iterations/sec + achieved HBM GB/s, ProxGGNSCORE n=1M m=16k",
-            "value": value, "unit": "iterations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "metric": METRIC if args.config == "c3" else f"iterate!() iterations/sec, {cfg['workload']}",
+            "value": value, "unit": "iterations/s", "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": ms_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic (on-device counter RNG: A ~ N(0,1)/sqrt(m), y ~ Bernoulli)",
-            "config": {"workload": "ProxGGNSCORE sparse-logistic l1, BASELINE configs[2]", "N": N, "m": m,
-                       "lambda": model.λ, "mu": 1.0, "ss_type": 1, "parallelism": f"row-shard x{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "gram_f64_kernel", "avg_ms": gram_avg_ms,
-                         "flops_per_launch": gram_flops},
-            "breakdown_ms_per_step": {k.replace("_ms", ""): tm[k] / args.steps for k in tm if k.endswith("_ms")},
-            # streaming passes (A·x in f(x), Aᵀv in step!): each reads the local A once
-            "hbm_gbs_streaming": (tm["gemv_calls"] * 8.0 * N_local * m) / (tm["gemv_ms"] * 1e-3) / 1e9
-            if tm["gemv_calls"] else None,
-            "objective_last": objs[-1],
+            "dtype": ("f64 (fp32-stored A values)" if args.f32 else "f64"), "data": "synthetic (on-device counter RNG: A ~ N(0,1)/sqrt(m), y from a sparse x_true)",
+            "config": {"workload": cfg["workload"], "N": N, "m": m, "lambda": model.λ, "mu": hmu.mu,
+                       "method": type(method).__name__, "ss_type": method.ss_type,
+                       "parallelism": f"row-shard x{world}"},
         }
-        if not args.no_cpu_baseline:
+        if tm["gram_calls"]:
+            main_calls = steps                      # one Gram per GGN/NSCORE step; the solver's own
+            gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])   # launches are timed under "solve"
+            gram_flops = float(N_local) * m * (m + 1)   # algorithmic symmetric Gram per launch
+            achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "r01_gram_pmc.json")
+            if os.path.exists(pmc) and world == 1:
+                with open(pmc) as f:
+                    pm = json.load(f)
+                if pm.get("N") == N and pm.get("m") == m:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            line["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
+                                "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                                "kernel": "gram_f64_kernel", "avg_ms": gram_avg_ms, "launches": main_calls,
+                                "flops_per_launch": gram_flops}
+        if tm["gemv_calls"] and cfg.get("sparse"):
+            # CSR (A·x, N rows) and CSC (Aᵀ·v, m columns) gathers, launched equally often: algorithmic
+            # bytes per launch = nnz·(value + 4 B index) + 8 B pointer + 8 B output per row (column)
+            # + the gathered vector read once (mean of the two launches)
+            nnz = model.nnz
+            vb = 4 if args.f32 else 8
+            csr = nnz * (vb + 4) + 8 * (N + 1) + 8 * N + 8 * m
+            csc = nnz * (vb + 4) + 8 * (m + 1) + 8 * m + 8 * N
+            per_launch = 0.5 * (csr + csc)
+            avg_ms = tm["gemv_ms"] / tm["gemv_calls"]
+            achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "spmv_kernel",
+                                "avg_ms": avg_ms, "launches_per_step": tm["gemv_calls"] / steps,
+                                "bytes_per_launch": per_launch}
+            line["config"]["nnz"] = nnz
+        elif tm["gemv_calls"]:
+            # streaming passes (A·x in f(x), Aᵀv in step!): each reads the local A once
+            line["hbm_gbs_streaming"] = (tm["gemv_calls"] * 8.0 * N_local * m) / (tm["gemv_ms"] * 1e-3) / 1e9
+            line["hbm_frac_streaming"] = line["hbm_gbs_streaming"] / HBM_PEAK_GBS
+        line["breakdown_ms_per_step"] = {k.replace("_ms", ""): tm[k] / steps for k in tm if k.endswith("_ms")}
+        line["objective_last"] = objs[-1]
+        if not args.no_cpu_baseline and args.config == "c3":
             env = dict(os.environ)
             cores = int(env.get("OMP_NUM_THREADS", "16"))
             env["OPENBLAS_NUM_THREADS"] = str(cores)
             try:
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--N", str(N),
-                                      "--m", str(m), "--Ns", str(args.cpu_Ns), "--ms", str(args.cpu_ms)],
+                                      "--m", str(m), "--Ns", str(args.cpu_Ns), "--ms", str(min(args.cpu_ms, m))],
                                      capture_output=True, text=True, env=env, timeout=300, check=True)
                 cb = json.loads(out.stdout.strip().splitlines()[-1])
                 line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}

@@ -88,7 +88,8 @@ typedef struct scs_synth {
   uint64_t seed;
   int kind;          /* 1: A ~ N(0,1)/sqrt(m); y ~ Bernoulli(sigmoid(A x_true)) in {0,1}
                         2: A ~ N(0,1)/sqrt(m); y ~ ±1 with P(+1) = sigmoid(A x_true)
-                        3: A ~ N(0,1);         y = A x_true + 0.1 eps              */
+                        3: A ~ N(0,1);         y = A x_true + 0.1 eps
+                        4: sparse A (scs_gen_sparse); x_true ~ U(-1.5,1.5), y = A x_true + 0.1 eps */
   double density;    /* fraction of nonzero entries of x_true             */
 } scs_synth;
 
@@ -127,6 +128,27 @@ int scs_gen_data(scs_ctx* ctx, const scs_synth* spec);
 /* Copy device A rows [r0, r0+nr) (column-major, lda_out) and y back.       */
 int scs_get_data(scs_ctx* ctx, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y);
 int scs_get_dims(scs_ctx* ctx, int64_t* N, int64_t* m, int64_t* N_global, int64_t* row0);
+
+/* ---- sparse A  (Problem(A::SparseMatrixCSC, y, ...); README.md:105 builds it
+ * with sprandn(N, m, 0.01) -- BASELINE configs[4]).  Held twice on the device:
+ * CSR for A*x and a CSC copy for Aᵀ*v, so both products are gathers with a
+ * fixed summation order (no atomics).  Indices are 0-based; the CSC copy
+ * describes the same local rows (rowidx in [0, N)).  val_f32 = 1 stores the
+ * values as fp32 (the fp32-value arm of the study; accumulation stays fp64).
+ * f, ∇f and ProxLQNSCORE run on sparse A; the Gram-based methods return
+ * SCS_ERR_ARG.                                                              */
+int scs_set_sparse(scs_ctx* ctx, int64_t N, int64_t m, int64_t nnz,
+                   const int64_t* rowptr, const int32_t* colidx, const double* val,
+                   const int64_t* colptr, const int32_t* rowidx, const double* valT,
+                   int val_f32, const double* y, int64_t N_global, int64_t row0);
+/* Synthetic sparse A (single context): k = round(density*m) nonzeros per row
+ * in a layered-bijection pattern (N a power of two, m | N; every column then
+ * holds k*N/m), values N(0,1)/sqrt(k); x_true ~ U(-1.5, 1.5) and
+ * y = A x_true + 0.1 eps (spec->kind must be 4; spec->density is ρ).        */
+int scs_gen_sparse(scs_ctx* ctx, const scs_synth* spec, int val_f32);
+int scs_get_nnz(scs_ctx* ctx, int64_t* nnz);
+/* CSR copy back to the host (values widened to fp64).                       */
+int scs_get_sparse(scs_ctx* ctx, int64_t* rowptr, int32_t* colidx, double* val);
 
 /* ---- problem / regularizer / smoother ----------------------------------- */
 int scs_set_loss(scs_ctx* ctx, int loss_kind, int ggn_kind, double scale);

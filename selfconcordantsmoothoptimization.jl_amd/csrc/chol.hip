@@ -27,66 +27,176 @@ constexpr int CLD = CB + 1;      // LDS row pitch (doubles) -> conflict-light co
 
 // Factor the diagonal block U_kk (upper) of G in place and write W_k = U_kk⁻¹
 // (upper, column-major 128 x 128).  info: first non-positive pivot (1-based,
-// global) or left untouched.
-__global__ __launch_bounds__(1024) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
-                                                         double* __restrict__ W, int* __restrict__ info) {
-  __shared__ __attribute__((aligned(16))) double sm[CB * CLD];   // column-major: a(r,c) = sm[c*CLD + r]
+// global); the caller then takes the LU path.
+//
+// Inner-blocked (b = 16) right-looking factorization of the LDS copy S:
+//   A  wave 0 factors the 16 x 16 diagonal sub-block in registers (lane =
+//      column c, rows g + 4q) with shuffles, and inverts it (D⁻¹);
+//   B  panel: S(o:o+16, c) = D⁻ᵀ S(o:o+16, c) for the columns to the right;
+//   C  trailing update of the upper triangle with 4 x 4 register tiles.
+// Then W = U⁻¹ block row by block row from the bottom:
+//   W(ii, c) = -D_ii⁻¹ Σ_{t > block ii} U(ii, t) W(t, c),
+// overwriting U's rows in LDS as they are consumed.  The reciprocal of each
+// pivot is formed once and multiplied in, as LAPACK dpotf2 does.
+constexpr int SB = 16;
+__global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
+                                                        double* __restrict__ W, int* __restrict__ info) {
+  __shared__ double su[CB * CLD];        // S(r, c) = su[c*CLD + r]
+  __shared__ double sdinv[SB * SB];      // D⁻¹(r, c) = sdinv[c*SB + r]
+  __shared__ double sT[(CB - SB) * SB];  // W phase: T(r, ci) = sT[ci*SB + r]
   double* blk = G + (int64_t)k * CB * ld + (int64_t)k * CB;
+  double* Wk = W + (int64_t)k * CB * CB;
   const int tid = threadIdx.x;
-  for (int e = tid; e < CB * CB; e += 1024) {
-    const int c = e / CB, r = e % CB;
-    sm[c * CLD + r] = (r <= c) ? blk[(int64_t)c * ld + r] : 0.0;
+  for (int e = tid; e < CB * CB; e += 256) {
+    const int c = e >> 7, r = e & 127;
+    su[c * CLD + r] = (r <= c) ? blk[(int64_t)c * ld + r] : 0.0;
   }
   __syncthreads();
-  // right-looking upper Cholesky: for j: u_jj = sqrt(a_jj); u_jc = a_jc / u_jj; a_ic -= u_ji u_jc (j < i <= c)
-  for (int j = 0; j < CB; ++j) {
-    const double ajj = sm[j * CLD + j];
-    const double d = sqrt(ajj);
-    const bool bad = !(ajj > 0.0);
-    __syncthreads();
-    if (bad) {
-      if (tid == 0 && *info == 0) *info = k * CB + j + 1;
-    }
-    for (int c = j + 1 + tid; c < CB; c += 1024) sm[c * CLD + j] = sm[c * CLD + j] / d;
-    if (tid == 0) sm[j * CLD + j] = d;
-    __syncthreads();
-    const int n = CB - 1 - j;  // trailing order
-    for (int e = tid; e < n * n; e += 1024) {
-      const int c = j + 1 + e / n, i = j + 1 + e % n;
-      if (i <= c) sm[c * CLD + i] -= sm[i * CLD + j] * sm[c * CLD + j];
-    }
-    __syncthreads();
-  }
-  for (int e = tid; e < CB * CB; e += 1024) {
-    const int c = e / CB, r = e % CB;
-    if (r <= c) blk[(int64_t)c * ld + r] = sm[c * CLD + r];
-  }
-  // W = U⁻¹ (upper).  Row by row from the bottom: W[i][c] = -(Σ_{i<t<=c} U[i][t] W[t][c]) / U[i][i]
-  // for c > i, W[i][i] = 1/U[i][i].  W's strictly-upper entries live transposed in the
-  // (unused) strictly-lower half of the LDS tile: W[i][c] -> sm[i*CLD + c]; the diagonal in wd.
-  __shared__ double wd[CB];
-  if (tid < CB) wd[tid] = 1.0 / sm[tid * CLD + tid];
-  __syncthreads();
-  {
-    const int c = tid >> 3, part = tid & 7;   // 8 threads per column
-    for (int i = CB - 2; i >= 0; --i) {
-      double s = 0.0;
-      if (c > i) {
-        for (int t = i + 1 + part; t <= c; t += 8) {
-          const double wtc = (t == c) ? wd[c] : sm[t * CLD + c];
-          s += sm[t * CLD + i] * wtc;
+
+  for (int kb = 0; kb < CB / SB; ++kb) {
+    const int o = kb * SB;
+    // ---- A: factor + invert the diagonal sub-block (wave 0)
+    if (tid < 64) {
+      const int c = tid & 15, g = tid >> 4;
+      double a[4], w[4], rinv[SB];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = su[(o + c) * CLD + o + g + 4 * q];
+#pragma unroll
+      for (int j = 0; j < SB; ++j) {
+        const int gj = j & 3, qj = j >> 2;
+        const double ajj = __shfl(a[qj], gj * 16 + j);
+        if (tid == 0 && !(ajj > 0.0) && *info == 0) *info = k * CB + o + j + 1;
+        const double d = sqrt(ajj);
+        const double r = 1.0 / d;
+        rinv[j] = r;
+        if (g == gj) a[qj] = (c > j) ? a[qj] * r : ((c == j) ? d : a[qj]);
+        const double ujc = __shfl(a[qj], gj * 16 + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double uji = __shfl(a[qj], gj * 16 + g + 4 * q);
+          if (g + 4 * q > j) a[q] -= uji * ujc;
         }
       }
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
-      if (c > i && part == 0) sm[i * CLD + c] = -s * wd[i];
-      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = (g + 4 * q == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = SB - 1; t >= 0; --t) {
+        const int gt = t & 3, qt = t >> 2;
+        if (g == gt) w[qt] *= rinv[t];
+        const double wtc = __shfl(w[qt], gt * 16 + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double dit = __shfl(a[q], g * 16 + t);
+          if (g + 4 * q < t) w[q] -= dit * wtc;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = g + 4 * q;
+        if (r <= c) su[(o + c) * CLD + o + r] = a[q];
+        sdinv[c * SB + r] = w[q];
+        Wk[(int64_t)(o + c) * CB + o + r] = w[q];
+      }
     }
+    __syncthreads();
+    const int np = CB - o - SB;  // columns right of the sub-block
+    if (np == 0) break;
+    // ---- B: panel  S(o + t, c) = Σ_{u <= t} D⁻¹(u, t) S(o + u, c)
+    {
+      const int ci = tid & 127, h = tid >> 7, c = o + SB + ci;
+      double X[SB], out[8];
+      if (ci < np) {
+#pragma unroll
+        for (int u = 0; u < SB; ++u) X[u] = su[c * CLD + o + u];
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+          const int t = 8 * h + tt;
+          double s = 0.0;
+#pragma unroll
+          for (int u = 0; u < SB; ++u) s += sdinv[t * SB + u] * X[u];
+          out[tt] = s;
+        }
+      }
+      __syncthreads();
+      if (ci < np) {
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) su[c * CLD + o + 8 * h + tt] = out[tt];
+      }
+    }
+    __syncthreads();
+    // ---- C: trailing update  S(i, c) -= Σ_t U(o + t, i) U(o + t, c),  o+16 <= i <= c
+    {
+      const int nt = np >> 2, ntiles = nt * (nt + 1) / 2;
+      for (int id = tid; id < ntiles; id += 256) {
+        int C = (int)((sqrtf(8.0f * id + 1.0f) - 1.0f) * 0.5f);
+        while (C * (C + 1) / 2 > id) --C;
+        while ((C + 1) * (C + 2) / 2 <= id) ++C;
+        const int I = id - C * (C + 1) / 2;
+        const int i0 = o + SB + 4 * I, c0 = o + SB + 4 * C;
+        double acc[4][4] = {};
+#pragma unroll
+        for (int t = 0; t < SB; ++t) {
+          double ui[4], uc[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            ui[q] = su[(i0 + q) * CLD + o + t];
+            uc[q] = su[(c0 + q) * CLD + o + t];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) acc[r][cc] += ui[r] * uc[cc];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+            if (i0 + r <= c0 + cc) su[(c0 + cc) * CLD + i0 + r] -= acc[r][cc];
+      }
+    }
+    __syncthreads();
   }
-  for (int e = tid; e < CB * CB; e += 1024) {
-    const int c = e / CB, r = e % CB;
-    W[(int64_t)k * CB * CB + (int64_t)c * CB + r] = (r < c) ? sm[r * CLD + c] : (r == c ? wd[c] : 0.0);
+  // ---- store U
+  for (int e = tid; e < CB * CB; e += 256) {
+    const int c = e >> 7, r = e & 127;
+    if (r <= c) blk[(int64_t)c * ld + r] = su[c * CLD + r];
+  }
+  __syncthreads();
+  // ---- W = U⁻¹, block rows from the bottom (the last diagonal block already is D⁻¹ in Wk)
+  for (int ii = CB / SB - 1; ii >= 0; --ii) {
+    const int o = ii * SB, np = CB - o - SB;
+    sdinv[tid] = Wk[(int64_t)(o + (tid >> 4)) * CB + o + (tid & 15)];
+    const int ci = tid & 127, h = tid >> 7, c = o + SB + ci;
+    if (ci < np) {
+      double T[8] = {};
+      for (int t = o + SB; t < CB; ++t) {
+        const double wtc = su[c * CLD + t];   // W(t, c) (rows below o+16 already hold W; 0 for t > c)
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) T[tt] += su[t * CLD + o + 8 * h + tt] * wtc;
+      }
+#pragma unroll
+      for (int tt = 0; tt < 8; ++tt) sT[ci * SB + 8 * h + tt] = T[tt];
+    }
+    __syncthreads();
+    if (ci < np) {
+#pragma unroll
+      for (int tt = 0; tt < 8; ++tt) {
+        const int rr = 8 * h + tt;
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < SB; ++u) s += sdinv[u * SB + rr] * sT[ci * SB + u];
+        su[c * CLD + o + rr] = -s;
+      }
+    }
+    {
+      const int cc = tid >> 4, rr = tid & 15;
+      su[(o + cc) * CLD + o + rr] = sdinv[cc * SB + rr];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < CB * CB; e += 256) {
+    const int c = e >> 7, r = e & 127;
+    Wk[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
   }
 }
 
@@ -164,7 +274,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
   if (mpad > m) hipLaunchKernelGGL(diag_pad_kernel, dim3((unsigned)ceil_div(mpad - m, 256)), dim3(256), 0, st, G, ld,
                                    m, mpad);
   for (int k = 0; k < nblk; ++k) {
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(1024), 0, st, G, ld, k, W, info);
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, G, ld, k, W, info);
     const int nb = nblk - k - 1;
     if (nb == 0) break;
     double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..) : 128 rows x nb*128 cols

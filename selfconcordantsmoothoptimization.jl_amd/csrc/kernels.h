@@ -90,4 +90,14 @@ hipError_t launch_gen_xtrue(double* x, int64_t m, uint64_t seed, double density,
 hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t row0, uint64_t seed,
                         hipStream_t st);
 
+// ---- sparse.hip (CSR / CSC gathers; out[r] = Σ_p val[p] x[idx[p]], p in [ptr[r], ptr[r+1]))
+hipError_t launch_spmv(const int64_t* ptr, const int* idx, const void* val, int f32, const double* x, int64_t nrows,
+                       double* out, hipStream_t st);
+size_t sparse_layer_map_bytes(int k);
+void sparse_layer_maps(uint64_t seed, int k, int64_t N, void* out_host);
+hipError_t launch_gen_sparse(int64_t N, int64_t m, int k, uint64_t seed, const void* Ldev, int f32, double scale,
+                             int64_t* rowptr, int* col, void* val, int64_t* colptr, int* row, void* valT,
+                             hipStream_t st);
+hipError_t launch_gen_uniform(double* x, int64_t m, uint64_t seed, double lo, double hi, hipStream_t st);
+
 }  // namespace scs

@@ -1,0 +1,81 @@
+// probe_chol: timing of the blocked Cholesky pieces (chol.hip) in isolation.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cmath>
+#include "common.h"
+#include "kernels.h"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+namespace scs {
+__global__ void chol_diag_kernel(double* G, int64_t ld, int k, double* W, int* info);
+}
+
+__global__ void spd_fill(double* G, int64_t n) {   // G = I*n + small symmetric noise (upper valid)
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n * n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = e / n, r = e % n;
+    const uint64_t h = (uint64_t)(r < c ? r * 1315423911ull + c : c * 1315423911ull + r) * 0x9E3779B97F4A7C15ull;
+    G[e] = (r == c) ? (double)n : ((double)((h >> 11) & 0xFFFF) / 65536.0 - 0.5);
+  }
+}
+
+__global__ void rowsum(const double* G, int64_t n, double* b) {   // b = G * ones (G symmetric, full)
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int64_t j = 0; j < n; ++j) s += G[j * n + i];
+  b[i] = s;
+}
+
+int main(int argc, char** argv) {
+  for (int64_t n : {(int64_t)8192, (int64_t)16384}) {
+    double *G, *G0, *W, *b, *y;
+    int* info;
+    CK(hipMalloc(&G, n * n * 8)); CK(hipMalloc(&G0, n * n * 8)); CK(hipMalloc(&W, n * 128 * 8));
+    CK(hipMalloc(&b, n * 8)); CK(hipMalloc(&y, n * 8)); CK(hipMalloc(&info, 4));
+    spd_fill<<<4096, 256>>>(G0, n);
+    const int nb = (int)(n / 128);
+    std::vector<int2> rl(nb), tr((size_t)nb * (nb + 1) / 2);
+    for (int j = 0; j < nb; ++j) rl[j] = make_int2(0, j);
+    scs::gram_tile_list_rowmajor(nb, tr.data());
+    int2 *drl, *dtr; double* wpm;
+    CK(hipMalloc(&drl, nb * 8)); CK(hipMalloc(&dtr, tr.size() * 8)); CK(hipMalloc(&wpm, 256 * 8));
+    CK(hipMemcpy(drl, rl.data(), nb * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dtr, tr.data(), tr.size() * 8, hipMemcpyHostToDevice));
+    std::vector<double> hw(256); for (int i = 0; i < 256; ++i) hw[i] = i < 128 ? 1.0 : -1.0;
+    CK(hipMemcpy(wpm, hw.data(), 256 * 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); float ms;
+    // diag kernel alone, 64 launches on distinct blocks of a fresh copy
+    CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
+    CK(hipMemset(info, 0, 4));
+    CK(hipEventRecord(e0));
+    for (int k = 0; k < 64; ++k) hipLaunchKernelGGL(scs::chol_diag_kernel, dim3(1), dim3(256), 0, 0, G, n, k, W, info);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("n=%ld diag kernel: %.1f us/launch\n", (long)n, ms * 1000 / 64);
+    // full factorization + solve
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
+      CK(hipMemset(info, 0, 4));
+      CK(hipEventRecord(e0));
+      CK(scs::chol_factor(G, n, n, n, W, wpm, drl, dtr, info, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      int hinfo; CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost));
+      printf("n=%ld factor: %.2f ms (info %d)\n", (long)n, ms, hinfo);
+      hipLaunchKernelGGL(rowsum, dim3((unsigned)(n / 256)), dim3(256), 0, 0, G0, n, b);
+      CK(hipEventRecord(e0));
+      CK(scs::chol_solve(G, n, n, W, b, y, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      std::vector<double> hx(n);
+      CK(hipMemcpy(hx.data(), b, n * 8, hipMemcpyDeviceToHost));
+      double err = 0.0;
+      for (int64_t i = 0; i < n; ++i) err = fmax(err, fabs(hx[i] - 1.0));
+      printf("n=%ld solve: %.2f ms  max|x-1| = %.3e\n", (long)n, ms, err);
+    }
+    CK(hipFree(G)); CK(hipFree(G0)); CK(hipFree(W)); CK(hipFree(b)); CK(hipFree(y)); CK(hipFree(info));
+    CK(hipFree(drl)); CK(hipFree(dtr)); CK(hipFree(wpm));
+  }
+  return 0;
+}

@@ -60,6 +60,13 @@ struct scs_ctx {
   bool generic = false;  // ProblemGeneric (no A)
   double* A = nullptr;
   double* y = nullptr;
+  // sparse A: CSR (rows) + CSC copy (columns), values fp64 or fp32
+  bool sparse = false;
+  int sp_f32 = 0;
+  int64_t nnz = 0;
+  int64_t *rowptr = nullptr, *colptr = nullptr;
+  int *colidx = nullptr, *rowidx = nullptr;
+  void *val = nullptr, *valT = nullptr;
 
   // problem
   int loss = 0, ggn = 0;
@@ -334,9 +341,9 @@ void alloc_mspace(scs_ctx* c) {
 
 void alloc_nspace(scs_ctx* c) {
   if (c->generic) return;
-  c->nsplit = gemv_n_splits(c->Npad, c->m);
+  c->nsplit = c->sparse ? 1 : gemv_n_splits(c->Npad, c->m);
   c->nval = epilogue_blocks(c->Npad);
-  c->nchunk = gemv_t_chunks(c->Npad);
+  c->nchunk = c->sparse ? 1 : gemv_t_chunks(c->Npad);
   dfree_t(c, c->zpart);
   dfree_t(c, c->z);
   dfree_t(c, c->gN);
@@ -407,6 +414,33 @@ double loss_scale_value(scs_ctx* c, double s) {
   }
 }
 
+// z-partials of A x into c->zpart (dense: `nsplit` column splits; sparse: one
+// CSR gather pass).  Returns the number of partials written.
+int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
+  if (c->sparse) {
+    HCK(launch_spmv(c->rowptr, c->colidx, c->val, c->sp_f32, xd, c->N, c->zpart, c->st));
+    return 1;
+  }
+  HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, nsplit, c->zpart, c->Npad, c->st));
+  return nsplit;
+}
+
+// out (device, m) = Aᵀ v over the local rows (dense: chunked column sums +
+// fixed-order finalize; sparse: one CSC gather pass)
+void matvec_t(scs_ctx* c, const double* v, double* out) {
+  if (c->sparse) {
+    HCK(launch_spmv(c->colptr, c->rowidx, c->valT, c->sp_f32, v, c->m, out, c->st));
+    return;
+  }
+  HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
+  HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, out, c->st));
+}
+
+void require_dense(scs_ctx* c, const char* what) {
+  if (c->sparse)
+    fail(c, SCS_ERR_ARG, "%s needs a dense A (sparse A supports f, ∇f and ProxLQNSCORE)", what);
+}
+
 // Forward pass at the device vector xd whose host copy is xh: z = A x (or the
 // cached z), then the epilogue with `flags`.  Always refreshes the f-value
 // cache; returns f(x) (global).
@@ -415,10 +449,10 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
   hipEvent_t e0;
   if (!cached) {
     tbegin(c, T_GEMV, &e0);
-    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, c->nsplit, c->zpart, c->Npad, c->st));
+    const int ns = matvec_n(c, xd, c->nsplit);
     tend(c, T_GEMV, e0);
     flags |= EPI_Z | EPI_VAL;
-    HCK(launch_epilogue(c->loss, c->ggn, flags, c->zpart, c->nsplit, c->Npad, c->y, c->N, c->Npad, c->scale, c->z,
+    HCK(launch_epilogue(c->loss, c->ggn, flags, c->zpart, ns, c->Npad, c->y, c->N, c->Npad, c->scale, c->z,
                         c->gN, c->hN, c->wN, c->vN, c->valpart, c->st));
     // loss sum -> scal[8] (reduce buffer slot 0 in multi-rank)
     double* dst = (c->nranks > 1) ? c->red : c->scal + 8;
@@ -442,8 +476,7 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
 void gemv_t_local(scs_ctx* c, const double* v, double* out) {
   hipEvent_t e0;
   tbegin(c, T_GEMV, &e0);
-  HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
-  HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, out, c->st));
+  matvec_t(c, v, out);
   tend(c, T_GEMV, e0);
 }
 
@@ -451,14 +484,11 @@ void gemv_t_local(scs_ctx* c, const double* v, double* out) {
 void gemv_t_global(scs_ctx* c, const double* v, double* out) {
   hipEvent_t e0;
   tbegin(c, T_GEMV, &e0);
-  HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
+  matvec_t(c, v, c->nranks > 1 ? c->red : out);
   tend(c, T_GEMV, e0);
   if (c->nranks > 1) {
-    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, c->red, c->st));
     allreduce(c, c->red, c->m);
     HCK(hipMemcpyAsync(out, c->red, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
-  } else {
-    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, out, c->st));
   }
 }
 
@@ -472,6 +502,7 @@ double eval_f_dev(scs_ctx* c, const double* xh, const double* xd) {
   }
   if (c->loss == SCS_LOSS_QUADRATIC) {
     // 1/2*(x'*(A*x)) + y'*x
+    require_dense(c, "the quadratic loss");
     HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, 1, c->zpart, c->Npad, c->st));
     HCK(launch_dot(xd, c->zpart, c->m, c->scal + 8, c->st));
     HCK(launch_dot(c->y, xd, c->m, c->scal + 9, c->st));
@@ -490,6 +521,7 @@ void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
   }
   if (c->loss == SCS_LOSS_QUADRATIC) {
     // 0.5*(A*x + Aᵀ*x) + y
+    require_dense(c, "the quadratic loss");
     HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, 1, c->zpart, c->Npad, c->st));
     gemv_t_global(c, xd, c->gtmp2);
     HCK(launch_axpby(c->zpart, 1.0, c->gtmp2, c->m, c->gtmp2, c->st));
@@ -587,6 +619,7 @@ void solve_system(scs_ctx* c, double* rhs) {
 // Gram of the local rows with weights w -> c->G (single rank) or the packed
 // reduce buffer (multi-rank; then all-reduced together with `vec`).
 void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
+  require_dense(c, "ProxNSCORE / ProxGGNSCORE (the Gram JᵀQJ)");
   ensure_gram(c);
   hipEvent_t e0;
   if (c->nranks > 1) {
@@ -635,6 +668,7 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
       HCK(launch_rosen(c->x, m, 2, nullptr, c->G, c->mpad, c->st));
       HCK(launch_rosen(c->x, m, 1, c->gtmp, nullptr, 0, c->st));
     } else if (c->loss == SCS_LOSS_QUADRATIC) {
+      require_dense(c, "the quadratic loss");
       HCK(launch_half_sym(c->A, c->Npad, m, c->G, c->mpad, c->st));
       grad_f_dev(c, xh, c->x, c->gtmp);
     } else {
@@ -829,6 +863,14 @@ static void set_dims(scs_ctx* c, int64_t N, int64_t m, int64_t Nglob, int64_t ro
 
 static void reset_data(scs_ctx* c) {
   dfree_t(c, c->A);
+  dfree_t(c, c->rowptr);
+  dfree_t(c, c->colptr);
+  dfree_t(c, c->colidx);
+  dfree_t(c, c->rowidx);
+  dfree(c, c->val);
+  dfree(c, c->valT);
+  c->sparse = false;
+  c->nnz = 0;
   dfree_t(c, c->y);
   dfree_t(c, c->G);
   dfree_t(c, c->Gc);
@@ -898,6 +940,7 @@ int scs_gen_data(scs_ctx* c, const scs_synth* s) {
 int scs_get_data(scs_ctx* c, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y) {
   return guarded(c, [&] {
     if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    if (c->sparse && A) fail(c, SCS_ERR_ARG, "sparse A: use scs_get_sparse");
     if (r0 < 0 || nr < 0 || r0 + nr > c->N) fail(c, SCS_ERR_ARG, "row range out of bounds");
     if (A && nr > 0)
       HCK(hipMemcpy2DAsync(A, sizeof(double) * lda_out, c->A + r0, sizeof(double) * c->Npad, sizeof(double) * nr,
@@ -913,6 +956,138 @@ int scs_get_dims(scs_ctx* c, int64_t* N, int64_t* m, int64_t* Ng, int64_t* r0) {
     if (m) *m = c->m;
     if (Ng) *Ng = c->Nglob;
     if (r0) *r0 = c->row0;
+  });
+}
+
+static void* dalloc_vals(scs_ctx* c, int64_t n, int f32) {
+  return f32 ? (void*)dalloc<float>(c, (size_t)n) : (void*)dalloc<double>(c, (size_t)n);
+}
+
+static void upload_vals(scs_ctx* c, void* dst, const double* src, int64_t n, int f32) {
+  if (!f32) {
+    HCK(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    sync(c);
+    return;
+  }
+  std::vector<float> h((size_t)n);
+  for (int64_t i = 0; i < n; ++i) h[i] = (float)src[i];
+  HCK(hipMemcpyAsync(dst, h.data(), sizeof(float) * n, hipMemcpyHostToDevice, c->st));
+  sync(c);
+}
+
+int scs_set_sparse(scs_ctx* c, int64_t N, int64_t m, int64_t nnz, const int64_t* rowptr, const int32_t* colidx,
+                   const double* val, const int64_t* colptr, const int32_t* rowidx, const double* valT, int f32,
+                   const double* y, int64_t Nglob, int64_t row0) {
+  return guarded(c, [&] {
+    if (nnz < 0 || !rowptr || !colptr || (nnz > 0 && (!colidx || !val || !rowidx || !valT)))
+      fail(c, SCS_ERR_ARG, "sparse A: null arrays");
+    if (rowptr[0] != 0 || rowptr[N] != nnz || colptr[0] != 0 || colptr[m] != nnz)
+      fail(c, SCS_ERR_ARG, "sparse A: rowptr/colptr must start at 0 and end at nnz");
+    for (int64_t i = 0; i < N; ++i)
+      if (rowptr[i + 1] < rowptr[i]) fail(c, SCS_ERR_ARG, "sparse A: rowptr not monotone at %lld", (long long)i);
+    for (int64_t j = 0; j < m; ++j)
+      if (colptr[j + 1] < colptr[j]) fail(c, SCS_ERR_ARG, "sparse A: colptr not monotone at %lld", (long long)j);
+    for (int64_t p = 0; p < nnz; ++p)
+      if (colidx[p] < 0 || colidx[p] >= m || rowidx[p] < 0 || rowidx[p] >= N)
+        fail(c, SCS_ERR_ARG, "sparse A: index out of range at %lld", (long long)p);
+    if (nnz > INT32_MAX * 64LL) fail(c, SCS_ERR_ARG, "sparse A: nnz too large");
+    HCK(hipSetDevice(c->dev));
+    reset_data(c);
+    set_dims(c, N, m, Nglob, row0);
+    c->generic = false;
+    c->sparse = true;
+    c->sp_f32 = f32 ? 1 : 0;
+    c->nnz = nnz;
+    c->rowptr = dalloc<int64_t>(c, N + 1);
+    c->colptr = dalloc<int64_t>(c, m + 1);
+    c->colidx = dalloc<int>(c, nnz);
+    c->rowidx = dalloc<int>(c, nnz);
+    c->val = dalloc_vals(c, nnz, c->sp_f32);
+    c->valT = dalloc_vals(c, nnz, c->sp_f32);
+    HCK(hipMemcpyAsync(c->rowptr, rowptr, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice, c->st));
+    HCK(hipMemcpyAsync(c->colptr, colptr, sizeof(int64_t) * (m + 1), hipMemcpyHostToDevice, c->st));
+    if (nnz > 0) {
+      HCK(hipMemcpyAsync(c->colidx, colidx, sizeof(int) * nnz, hipMemcpyHostToDevice, c->st));
+      HCK(hipMemcpyAsync(c->rowidx, rowidx, sizeof(int) * nnz, hipMemcpyHostToDevice, c->st));
+      upload_vals(c, c->val, val, nnz, c->sp_f32);
+      upload_vals(c, c->valT, valT, nnz, c->sp_f32);
+    }
+    c->y = dalloc<double>(c, c->Npad);
+    if (y && N > 0) h2d(c, c->y, y, N);
+    alloc_mspace(c);
+    alloc_nspace(c);
+    sync(c);
+    c->has_data = true;
+  });
+}
+
+int scs_gen_sparse(scs_ctx* c, const scs_synth* s, int f32) {
+  return guarded(c, [&] {
+    if (!s) fail(c, SCS_ERR_ARG, "null synth spec");
+    if (s->kind != 4) fail(c, SCS_ERR_ARG, "scs_gen_sparse: kind must be 4");
+    const int64_t N = s->N, m = s->m;
+    if (N <= 0 || (N & (N - 1)) != 0 || m <= 0 || N % m != 0)
+      fail(c, SCS_ERR_ARG, "scs_gen_sparse: N must be a power of two and a multiple of m");
+    if ((s->N_global > 0 && s->N_global != N) || s->row0 != 0)
+      fail(c, SCS_ERR_ARG, "scs_gen_sparse: single-context generator (shard with scs_set_sparse)");
+    const int k = (int)std::max<int64_t>(1, std::llround(s->density * (double)m));
+    if (k > m) fail(c, SCS_ERR_ARG, "scs_gen_sparse: density > 1");
+    const int64_t nnz = N * (int64_t)k;
+    HCK(hipSetDevice(c->dev));
+    reset_data(c);
+    set_dims(c, N, m, N, 0);
+    c->generic = false;
+    c->sparse = true;
+    c->sp_f32 = f32 ? 1 : 0;
+    c->nnz = nnz;
+    c->rowptr = dalloc<int64_t>(c, N + 1);
+    c->colptr = dalloc<int64_t>(c, m + 1);
+    c->colidx = dalloc<int>(c, nnz);
+    c->rowidx = dalloc<int>(c, nnz);
+    c->val = dalloc_vals(c, nnz, c->sp_f32);
+    c->valT = dalloc_vals(c, nnz, c->sp_f32);
+    c->y = dalloc<double>(c, c->Npad);
+    alloc_mspace(c);
+    alloc_nspace(c);
+    std::vector<char> maps(sparse_layer_map_bytes(k));
+    sparse_layer_maps(s->seed, k, N, maps.data());
+    void* dmaps = dalloc<char>(c, maps.size());
+    HCK(hipMemcpyAsync(dmaps, maps.data(), maps.size(), hipMemcpyHostToDevice, c->st));
+    HCK(launch_gen_sparse(N, m, k, s->seed, dmaps, c->sp_f32, 1.0 / std::sqrt((double)k), c->rowptr, c->colidx,
+                          c->val, c->colptr, c->rowidx, c->valT, c->st));
+    HCK(launch_gen_uniform(c->xn, m, s->seed, -1.5, 1.5, c->st));
+    matvec_n(c, c->xn, 1);
+    HCK(launch_gen_y(3, c->zpart, c->y, c->N, 0, s->seed, c->st));
+    sync(c);
+    dfree(c, dmaps);
+    c->has_data = true;
+  });
+}
+
+int scs_get_nnz(scs_ctx* c, int64_t* nnz) {
+  return guarded(c, [&] {
+    if (!c->has_data || !c->sparse) fail(c, SCS_ERR_STATE, "no sparse data");
+    *nnz = c->nnz;
+  });
+}
+
+int scs_get_sparse(scs_ctx* c, int64_t* rowptr, int32_t* colidx, double* val) {
+  return guarded(c, [&] {
+    if (!c->has_data || !c->sparse) fail(c, SCS_ERR_STATE, "no sparse data");
+    if (rowptr) HCK(hipMemcpyAsync(rowptr, c->rowptr, sizeof(int64_t) * (c->N + 1), hipMemcpyDeviceToHost, c->st));
+    if (colidx && c->nnz)
+      HCK(hipMemcpyAsync(colidx, c->colidx, sizeof(int) * c->nnz, hipMemcpyDeviceToHost, c->st));
+    if (val && c->nnz) {
+      if (c->sp_f32) {
+        std::vector<float> h((size_t)c->nnz);
+        HCK(hipMemcpyAsync(h.data(), c->val, sizeof(float) * c->nnz, hipMemcpyDeviceToHost, c->st));
+        sync(c);
+        for (int64_t p = 0; p < c->nnz; ++p) val[p] = h[p];
+      } else {
+        HCK(hipMemcpyAsync(val, c->val, sizeof(double) * c->nnz, hipMemcpyDeviceToHost, c->st));
+      }
+    }
+    sync(c);
   });
 }
 
@@ -1140,6 +1315,7 @@ int scs_prox_eval(scs_ctx* c, const double* z, const double* Hr, double lam, dou
 int scs_gram_eval(scs_ctx* c, const double* w, double* G, int64_t ldg) {
   return guarded(c, [&] {
     if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    require_dense(c, "scs_gram_eval");
     std::vector<double> wp(c->Npad, 0.0);
     std::memcpy(wp.data(), w, sizeof(double) * c->N);
     h2d(c, c->wN, wp.data(), c->Npad);
@@ -1162,8 +1338,7 @@ int scs_gemv_t_eval(scs_ctx* c, const double* v, double* out) {
     std::vector<double> vp(c->Npad, 0.0);
     std::memcpy(vp.data(), v, sizeof(double) * c->N);
     h2d(c, c->vN, vp.data(), c->Npad);
-    HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, c->vN, c->tpart, c->st));
-    HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, c->gtmp, c->st));
+    matvec_t(c, c->vN, c->gtmp);
     d2h(c, out, c->gtmp, c->m);
     sync(c);
   });
@@ -1173,8 +1348,8 @@ int scs_gemv_n_eval(scs_ctx* c, const double* x, double* out) {
   return guarded(c, [&] {
     if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
     h2d(c, c->xn, x, c->m);
-    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, c->xn, c->nsplit, c->zpart, c->Npad, c->st));
-    HCK(launch_epilogue(c->loss ? c->loss : SCS_LOSS_LEAST_SQUARES, SCS_GGN_NONE, EPI_Z, c->zpart, c->nsplit, c->Npad,
+    const int ns = matvec_n(c, c->xn, c->nsplit);
+    HCK(launch_epilogue(c->loss ? c->loss : SCS_LOSS_LEAST_SQUARES, SCS_GGN_NONE, EPI_Z, c->zpart, ns, c->Npad,
                         c->y, c->N, c->Npad, 1.0, c->z, nullptr, nullptr, nullptr, nullptr, c->valpart, c->st));
     d2h(c, out, c->z, c->N);
     sync(c);

@@ -40,6 +40,7 @@ lib = C.CDLL(LIB_PATH)
 
 c_dp = C.POINTER(C.c_double)
 c_i64p = C.POINTER(C.c_int64)
+c_i32p = C.POINTER(C.c_int32)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
 
 
@@ -69,6 +70,11 @@ _SIGS = {
     "scs_gen_data": (C.c_int, [C.c_void_p, C.POINTER(Synth)]),
     "scs_get_data": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_dp, C.c_int64, c_dp]),
     "scs_get_dims": (C.c_int, [C.c_void_p, c_i64p, c_i64p, c_i64p, c_i64p]),
+    "scs_set_sparse": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, c_i64p, c_i32p, c_dp, c_i64p, c_i32p,
+                                 c_dp, C.c_int, c_dp, C.c_int64, C.c_int64]),
+    "scs_gen_sparse": (C.c_int, [C.c_void_p, C.POINTER(Synth), C.c_int]),
+    "scs_get_nnz": (C.c_int, [C.c_void_p, c_i64p]),
+    "scs_get_sparse": (C.c_int, [C.c_void_p, c_i64p, c_i32p, c_dp]),
     "scs_set_loss": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double]),
     "scs_set_reg": (C.c_int, [C.c_void_p, C.c_int, c_dp, C.c_int, c_dp, c_dp, C.c_int64, c_i64p, C.c_int64]),
     "scs_set_smoother": (C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_double, c_dp, c_dp,

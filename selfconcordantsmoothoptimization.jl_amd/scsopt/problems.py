@@ -56,11 +56,15 @@ def _lam_tuple(lam):
     return v
 
 
+def _is_sparse(A):
+    return hasattr(A, "tocsr") and hasattr(A, "tocsc") and hasattr(A, "nnz")
+
+
 class Problem:
     """problems.jl:21-40 (data) / :5-19 (generic)."""
 
     def __init__(self, *args, L=None, sol=None, C_set=None, P=None, out_fn: Optional[OutFn] = None,
-                 name=None, device=0, comm=None, N_global=None, row0=0, _ctx=None):
+                 name=None, device=0, comm=None, N_global=None, row0=0, sparse_f32=False, _ctx=None):
         if len(args) == 5:
             A, y, x0, f, lam = args
         elif len(args) == 3:
@@ -89,6 +93,8 @@ class Problem:
             if self.generic:
                 self.N = 0
                 self.ctx.check(_lib.lib.scs_set_data(self.ctx.h, 0, self.m, None, 0, None, 0, 0))
+            elif _is_sparse(A):
+                self._set_sparse(A, y, N_global, row0, f32=bool(sparse_f32))
             else:
                 A = np.asarray(A, dtype=np.float64)
                 if A.ndim != 2 or A.shape[1] != self.m:
@@ -129,6 +135,55 @@ class Problem:
         spec = _lib.Synth(N_global=N, row0=r0, N=r1 - r0, m=m, seed=seed, kind=kind, density=density)
         ctx.check(_lib.lib.scs_gen_data(ctx.h, C.byref(spec)))
         return cls(x0, f, lam, out_fn=out_fn, device=device, comm=comm, _ctx=ctx, **kw)
+
+    @classmethod
+    def synthetic_sparse(cls, N, m, x0, f, lam, *, density=0.01, seed=1234, f32=False, device=0, **kw):
+        """Sparse A (the README's sprandn(N, m, ρ) problem class, BASELINE configs[4]) generated on
+        the device: k = round(ρ m) nonzeros per row, N(0,1)/sqrt(k) values, CSR + CSC copies;
+        x_true ~ U(-1.5, 1.5), y = A x_true + 0.1ε.  N must be a power of two and a multiple of m."""
+        ctx = _lib.Context(device)
+        spec = _lib.Synth(N_global=N, row0=0, N=N, m=m, seed=seed, kind=4, density=density)
+        ctx.check(_lib.lib.scs_gen_sparse(ctx.h, C.byref(spec), 1 if f32 else 0))
+        return cls(x0, f, lam, device=device, _ctx=ctx, **kw)
+
+    def _set_sparse(self, A, y, N_global, row0, f32):
+        csr = A.tocsr()
+        csc = A.tocsc()
+        if csr.shape[1] != self.m:
+            raise ValueError(f"A must be N x m with m = length(x0) = {self.m}")
+        self.N = int(csr.shape[0])
+        rowptr = np.ascontiguousarray(csr.indptr, dtype=np.int64)
+        colidx = np.ascontiguousarray(csr.indices, dtype=np.int32)
+        val = np.ascontiguousarray(csr.data, dtype=np.float64)
+        colptr = np.ascontiguousarray(csc.indptr, dtype=np.int64)
+        rowidx = np.ascontiguousarray(csc.indices, dtype=np.int32)
+        valT = np.ascontiguousarray(csc.data, dtype=np.float64)
+        yv = np.ascontiguousarray(np.asarray(y, dtype=np.float64).reshape(-1))
+        Ng = self.N if N_global is None else int(N_global)
+        i64, i32 = _lib.c_i64p, _lib.c_i32p
+        self.ctx.check(_lib.lib.scs_set_sparse(
+            self.ctx.h, self.N, self.m, int(val.shape[0]), rowptr.ctypes.data_as(i64), colidx.ctypes.data_as(i32),
+            dptr(val), colptr.ctypes.data_as(i64), rowidx.ctypes.data_as(i32), dptr(valT), 1 if f32 else 0,
+            dptr(yv), Ng, int(row0)))
+
+    @property
+    def nnz(self):
+        n = C.c_int64()
+        self.ctx.check(_lib.lib.scs_get_nnz(self.ctx.h, C.byref(n)))
+        return int(n.value)
+
+    def get_sparse(self):
+        """The device CSR copy of A as a scipy.sparse.csr_matrix (values widened to fp64), and y."""
+        import scipy.sparse as sp
+        nnz = self.nnz
+        rowptr = np.zeros(self.N + 1, dtype=np.int64)
+        colidx = np.zeros(max(nnz, 1), dtype=np.int32)
+        val = np.zeros(max(nnz, 1), dtype=np.float64)
+        self.ctx.check(_lib.lib.scs_get_sparse(self.ctx.h, rowptr.ctypes.data_as(_lib.c_i64p),
+                                               colidx.ctypes.data_as(_lib.c_i32p), dptr(val)))
+        y = np.zeros(self.N, dtype=np.float64)
+        self.ctx.check(_lib.lib.scs_get_data(self.ctx.h, 0, self.N, None, self.N, dptr(y)))
+        return sp.csr_matrix((val[:nnz], colidx[:nnz], rowptr), shape=(self.N, self.m)), y
 
     # device evaluation helpers ------------------------------------------------
     def fx(self, x):

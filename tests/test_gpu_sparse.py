@@ -1,0 +1,124 @@
+"""GPU parity of the sparse-A path (BASELINE configs[4]: box-constrained least squares with
+ProxLQNSCORE, the README's `sprandn(N, m, ρ)` problem class) against the oracle.
+
+The device holds A as CSR (A·x) plus a CSC copy (Aᵀ·v); both products are per-row / per-column
+gathers with a fixed summation order.  The oracle runs on the same matrix densified (sizes here
+are small), so the comparison isolates the summation order:
+  * A·x, Aᵀ·v: |err| <= 1e-13 · Σ|terms|;
+  * LQN trajectories: objective history rtol 1e-8, same length/termination, x rtol 1e-6;
+  * fp32-value arm: the device's fp32 values (read back widened) through the oracle -> the same
+    fp64 bars; fp32 vs fp64 arm on the same problem -> objective within 1e-5 relative (the
+    "tolerance study" row of SURVEY.md §8d C5).
+"""
+import numpy as np
+import pytest
+
+import scsopt
+import scsopt_oracle as O
+from scsopt import losses
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_products(p, A):
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal(A.shape[1])
+    v = rng.standard_normal(A.shape[0])
+    Ad = A.toarray() if hasattr(A, "toarray") else A
+    z = p.gemv_n(x)
+    np.testing.assert_allclose(z, Ad @ x, rtol=0, atol=1e-13 * float(np.max(np.abs(Ad) @ np.abs(x))) + 1e-300)
+    t = p.gemv_t(v)
+    np.testing.assert_allclose(t, Ad.T @ v, rtol=0, atol=1e-13 * float(np.max(np.abs(Ad).T @ np.abs(v))) + 1e-300)
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_generated_pattern_and_products(f32):
+    N, m, rho = 8192, 256, 0.05
+    k = round(rho * m)
+    p = scsopt.Problem.synthetic_sparse(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1e-4, density=rho,
+                                        seed=7, f32=f32)
+    assert p.nnz == N * k
+    A, y = p.get_sparse()
+    # every row holds k entries, every column k N / m (the layered-bijection construction)
+    assert np.all(np.diff(A.indptr) == k)
+    assert np.all(np.bincount(A.indices, minlength=m) == k * N // m)
+    vals = A.data
+    if f32:
+        assert np.array_equal(vals, vals.astype(np.float32).astype(np.float64))
+    # values N(0,1)/sqrt(k): loose moment check
+    assert abs(np.mean(vals)) < 0.02 / np.sqrt(k) * 10
+    assert abs(np.std(vals) * np.sqrt(k) - 1.0) < 0.02
+    _check_products(p, A)
+    # y = A x_true + 0.1 eps with x_true in [-1.5, 1.5]
+    assert np.all(np.isfinite(y)) and np.std(y) > 0.1
+
+
+def test_user_csr_input_and_edges():
+    """Problem(A::SparseMatrixCSC, ...) from host CSR/CSC, with empty rows/columns and duplicates summed."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(3)
+    N, m = 1000, 300
+    A = sp.random(N, m, density=0.03, random_state=4, format="coo", data_rvs=rng.standard_normal)
+    A = sp.coo_matrix((np.concatenate([A.data, [0.5, 0.25]]),
+                       (np.concatenate([A.row, [3, 3]]), np.concatenate([A.col, [7, 7]]))), shape=(N, m))
+    A = A.tocsr()
+    A[10, :] = 0.0          # an empty row
+    A[:, 20] = 0.0          # an empty column
+    A.eliminate_zeros()
+    y = rng.standard_normal(N)
+    x0 = rng.standard_normal(m)
+    ps = scsopt.Problem(A, y, x0, losses.least_squares(1.0 / N), 0.1)
+    pd = scsopt.Problem(A.toarray(), y, x0, losses.least_squares(1.0 / N), 0.1)
+    _check_products(ps, A)
+    assert ps.fx(x0) == pytest.approx(pd.fx(x0), rel=1e-13)
+    np.testing.assert_allclose(ps.gradx(x0), pd.gradx(x0), rtol=1e-12, atol=1e-15)
+    om = O.Problem(A.toarray(), y, x0, O.Loss("least_squares", 1.0 / N), 0.1)
+    assert ps.fx(x0) == pytest.approx(om.fx(x0), rel=1e-13)
+    # all-zero matrix
+    Z = sp.csr_matrix((N, m))
+    pz = scsopt.Problem(Z, y, x0, losses.least_squares(1.0 / N), 0.1)
+    np.testing.assert_array_equal(pz.gemv_n(x0), np.zeros(N))
+    assert pz.fx(x0) == pytest.approx(0.5 * np.dot(y, y) / N, rel=1e-13)
+
+
+def test_gram_methods_refuse_sparse():
+    N, m = 1024, 64
+    p = scsopt.Problem.synthetic_sparse(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1e-4, density=0.1)
+    with pytest.raises(scsopt.ScsError, match="dense A"):
+        scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=2, verbose=0)
+
+
+def _c5_pair(N=8192, m=512, rho=0.02, f32=False, max_epoch=25, mem=20):
+    x0 = np.random.default_rng(1234).standard_normal(m) * 0.5
+    lam, mu = 1e-4, 0.6
+    p = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), lam, density=rho, seed=2026,
+                                        f32=f32, C_set=[-1.0, 1.0])
+    A, y = p.get_sparse()
+    om = O.Problem(A.toarray(), y, x0, O.Loss("least_squares", 1.0 / N), lam, C_set=[-1.0, 1.0])
+    sol = scsopt.iterate(scsopt.ProxLQNSCORE(m=mem), p, "indbox", scsopt.PHuberSmootherIndBox(-1.0, 1.0, mu),
+                         max_epoch=max_epoch, verbose=0)
+    osol = O.iterate(O.ProxLQNSCORE(m=mem), om, "indbox", O.PHuberSmootherIndBox(-1.0, 1.0, mu),
+                     max_epoch=max_epoch)
+    return p, sol, osol
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_c5_lqn_box_ls_trajectory(f32):
+    """C5 in miniature: ProxLQNSCORE(mem = 20) + indbox + PHuberSmootherIndBox(μ = 0.6), λ = 1e-4."""
+    p, sol, osol = _c5_pair(f32=f32)
+    assert sol.epochs == osol.epochs
+    assert len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+    assert np.all(sol.x >= -1.0) and np.all(sol.x <= 1.0)
+    assert sol.obj[-1] < sol.obj[0]
+
+
+def test_c5_fp32_vs_fp64_arm():
+    """The tolerance study: the same problem with fp32-stored values stays within 1e-5 (relative) in
+    objective of the fp64 arm over the run."""
+    _, s64, _ = _c5_pair(f32=False, max_epoch=20)
+    _, s32, _ = _c5_pair(f32=True, max_epoch=20)
+    n = min(len(s64.obj), len(s32.obj))
+    np.testing.assert_allclose(s32.obj[:n], s64.obj[:n], rtol=1e-5)
+    np.testing.assert_allclose(s32.x, s64.x, atol=1e-3)
