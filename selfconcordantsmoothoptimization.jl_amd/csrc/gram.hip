@@ -51,14 +51,19 @@ __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
     asm volatile("" ::: "memory");                             \
   } while (0)
 
-template <bool NOLOAD>
-__global__ __launch_bounds__(256, 2) void gram_f64_kernel(
+// TI = 64-row wave groups along i: TI = 2 -> 128 x 128 tiles, 4 waves, 2 WG/CU;
+// TI = 4 -> 256 x 128 tiles, 8 waves, 1 WG/CU (25 % less operand traffic per flop).
+template <bool NOLOAD, int TI>
+__global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
     const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
     const double* __restrict__ w, int64_t k0, int64_t Nk, const int2* __restrict__ tiles, int ntiles,
     double* __restrict__ G, int64_t ldg, int flags) {
+  constexpr int GTI = 64 * TI;               // tile rows (A1 panel width)
+  constexpr int NT = 128 * TI;               // threads
+  constexpr int SB = GTI * GBK + GT * GBK;   // doubles per LDS stage
   const int packed = flags & GRAM_PACKED, accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
-  // All LDS in ONE array (cdna_hip_programming.md §5 item 4a): [buf][panel][128 x 16]
-  __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GT * GBK];
+  // All LDS in ONE array (cdna_hip_programming.md §5 item 4a): [buf][A1 panel GTI x 16 | A2 panel 128 x 16]
+  __shared__ __attribute__((aligned(16))) double lds[2 * SB];
 
   // XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle")
   const int orig = blockIdx.x;
@@ -69,33 +74,36 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const double* __restrict__ Ai = A1 + (int64_t)bi * GT * lda1;
+  const double* __restrict__ Ai = A1 + (int64_t)bi * GTI * lda1;
   const double* __restrict__ Aj = A2 + (int64_t)bj * GT * lda2;
 
-  // staging map: chunk q = tid + 256*i  ->  feature f = (tid>>3) + 32 i, chunk c = tid & 7
+  // staging map: chunk q = tid + NT*i  ->  feature f = (tid>>3) + (NT/8) i, chunk c = tid & 7
+  constexpr int FS = NT / 8;                 // features per staging sweep
+  constexpr int NA = GTI / FS, NB = GT / FS; // sweeps: A1 panel 4, A2 panel 4 (TI=2) or 2 (TI=4)
   const int sc = tid & 7;
   const int sf0 = tid >> 3;
-  v2d ra[4], rb[4], rw;
+  v2d ra[NA], rb[NB], rw;
 
   auto gload = [&](int64_t n0) {
     if (NOLOAD && n0 > k0) return;  // timing-only experiment: operands stay in registers
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t f = sf0 + 32 * i;
-      ra[i] = *(const v2d*)(Ai + f * lda1 + n0 + 2 * sc);
-      rb[i] = *(const v2d*)(Aj + f * lda2 + n0 + 2 * sc);
-    }
+    for (int i = 0; i < NA; ++i) ra[i] = *(const v2d*)(Ai + (int64_t)(sf0 + FS * i) * lda1 + n0 + 2 * sc);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(Aj + (int64_t)(sf0 + FS * i) * lda2 + n0 + 2 * sc);
     rw = *(const v2d*)(w + n0 + 2 * sc);
   };
   auto swrite = [&](int buf) {
-    double* la = lds + (buf * 2 + 0) * GT * GBK;
-    double* lb = lds + (buf * 2 + 1) * GT * GBK;
+    double* la = lds + buf * SB;
+    double* lb = la + GTI * GBK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = sf0 + 32 * i;
-      const int off = f * GBK + 2 * (sc ^ swz(f));
-      *(v2d*)(la + off) = ra[i];
-      *(v2d*)(lb + off) = rb[i] * rw;
+    for (int i = 0; i < NA; ++i) {
+      const int f = sf0 + FS * i;
+      *(v2d*)(la + f * GBK + 2 * (sc ^ swz(f))) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int f = sf0 + FS * i;
+      *(v2d*)(lb + f * GBK + 2 * (sc ^ swz(f))) = rb[i] * rw;
     }
   };
 
@@ -113,8 +121,8 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
   __syncthreads();
   for (int k = 0; k < nk; ++k) {
     if (k + 1 < nk) gload(k0 + (int64_t)(k + 1) * GBK);
-    const double* la = lds + ((k & 1) * 2 + 0) * GT * GBK;
-    const double* lb = lds + ((k & 1) * 2 + 1) * GT * GBK;
+    const double* la = lds + (k & 1) * SB;
+    const double* lb = la + GTI * GBK;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int pc = ((4 * p + g) ^ s) * 2;
@@ -152,9 +160,9 @@ __global__ __launch_bounds__(256, 2) void gram_f64_kernel(
         const int il = wr * 64 + 16 * ti + g + 4 * r;
         const int jl = wc * 64 + 16 * tj + fl;
         double* dst;
-        if (packed) dst = G + (int64_t)tix * GT * GT + jl * GT + il;
-        else if (upper) dst = G + ((int64_t)bi * GT + il) * ldg + (int64_t)bj * GT + jl;
-        else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GT + il;
+        if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
+        else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
+        else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
         if (accumulate) *dst += acc[ti][tj][r];
         else *dst = acc[ti][tj][r];
       }
@@ -315,6 +323,20 @@ void gram_tile_list(int nb, int2* out, int* ntiles) {
   *ntiles = t;
 }
 
+// Super-blocked list of 256 x 128 tiles (BI, bj) for the TI = 4 kernel: row block
+// BI covers 128-blocks 2BI, 2BI+1; every tile with bj <= 2BI+1 (the one above the
+// diagonal holds the mirror values, stored harmlessly below it).  nb even.
+void gram_tile_list_tall(int nb, int2* out, int* ntiles) {
+  const int nbi = nb / 2, SI = 4, SJ = 8;
+  int t = 0;
+  for (int sbi = 0; sbi < (nbi + SI - 1) / SI; ++sbi)
+    for (int sbj = 0; sbj <= sbi; ++sbj)
+      for (int I = sbi * SI; I < (sbi + 1) * SI && I < nbi; ++I)
+        for (int j = sbj * SJ; j < (sbj + 1) * SJ && j < nb; ++j)
+          if (j <= 2 * I + 1) out[t++] = make_int2(I, j);
+  *ntiles = t;
+}
+
 // Row-major lower-triangle order: the first nb'(nb'+1)/2 entries are the list for nb' <= nb.
 void gram_tile_list_rowmajor(int nb, int2* out) {
   int t = 0;
@@ -327,8 +349,13 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
                            hipStream_t st);
 
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,
-                       int ntiles, double* G, int64_t ldg, int packed, hipStream_t st) {
-  return gram_launch_gen(A, lda, A, lda, w, 0, Nk, tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER, st);
+                       int ntiles, double* G, int64_t ldg, int packed, int tall, hipStream_t st) {
+  if (!tall)
+    return gram_launch_gen(A, lda, A, lda, w, 0, Nk, tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER, st);
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
+                     tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER);
+  return hipGetLastError();
 }
 
 // General form: operand panels from two matrices, K range [k0, k1), flags GRAM_*.
@@ -336,7 +363,7 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                            hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles,
+  hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles,
                      ntiles, G, ldg, flags);
   return hipGetLastError();
 }
@@ -345,14 +372,20 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
-  if (noload == 2)
+  if (noload == 4)
+    hipLaunchKernelGGL((gram_f64_kernel<true, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags);
+  else if (noload == 3)
+    hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags);
+  else if (noload == 2)
     hipLaunchKernelGGL(gram_f64_pf2_kernel, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G, ldg,
                        0, accumulate);
   else if (noload)
-    hipLaunchKernelGGL(gram_f64_kernel<true>, dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
+    hipLaunchKernelGGL((gram_f64_kernel<true, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
                        ntiles, G, ldg, flags);
   else
-    hipLaunchKernelGGL(gram_f64_kernel<false>, dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
+    hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
                        ntiles, G, ldg, flags);
   return hipGetLastError();
 }

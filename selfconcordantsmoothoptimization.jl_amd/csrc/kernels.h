@@ -21,8 +21,11 @@ struct ProxArgsH {
 
 // ---- gram.hip
 void gram_tile_list(int nb, int2* out, int* ntiles);
+void gram_tile_list_tall(int nb, int2* out, int* ntiles);
+// tall = 1: 256 x 128 tiles from gram_tile_list_tall (nb even); packed slots are then
+// the 128 x 128 halves (2t, 2t+1) of launch tile t
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
-                       double* G, int64_t ldg, int packed, hipStream_t st);
+                       double* G, int64_t ldg, int packed, int tall, hipStream_t st);
 void gram_tile_list_rowmajor(int nb, int2* out);
 hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,

@@ -10,8 +10,9 @@
 
 namespace scs {
 void gram_tile_list(int nb, int2* out, int* ntiles);
+void gram_tile_list_tall(int nb, int2* out, int* ntiles);
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
-                       double* G, int64_t ldg, int packed, hipStream_t st);
+                       double* G, int64_t ldg, int packed, int tall, hipStream_t st);
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st);
 }
@@ -32,7 +33,7 @@ __global__ void fill_kernel(double* p, size_t n, uint64_t seed, double scale) {
   }
 }
 
-static int run(int64_t N, int64_t m, int reps, bool check) {
+static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
   const int64_t lda = N;
   double *A, *w, *G;
   CK(hipMalloc(&A, (size_t)lda * m * 8));
@@ -42,13 +43,14 @@ static int run(int64_t N, int64_t m, int reps, bool check) {
   fill_kernel<<<256, 256>>>(w, (size_t)N, 99, 1.0);
   CK(hipMemset(G, 0, (size_t)m * m * 8));
   const int nb = (int)(m / 128);
-  std::vector<int2> tl((size_t)nb * (nb + 1) / 2);
+  std::vector<int2> tl((size_t)nb * (nb + 1) / 2 + nb);
   int nt = 0;
-  scs::gram_tile_list(nb, tl.data(), &nt);
+  if (tall) scs::gram_tile_list_tall(nb, tl.data(), &nt);
+  else scs::gram_tile_list(nb, tl.data(), &nt);
   int2* dtl;
   CK(hipMalloc(&dtl, nt * sizeof(int2)));
   CK(hipMemcpy(dtl, tl.data(), nt * sizeof(int2), hipMemcpyHostToDevice));
-  CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, 0));
+  CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, tall, 0));
   CK(hipDeviceSynchronize());
   if (check) {
     std::vector<double> hA((size_t)lda * m), hw(N), hG((size_t)m * m);
@@ -66,20 +68,26 @@ static int run(int64_t N, int64_t m, int reps, bool check) {
         double e = fabs(hG[i * m + j] - s) / (sa > 0 ? sa : 1);  // upper triangle: (row j, col i)
         if (e > maxrel) maxrel = e;
       }
-    printf("CHECK N=%ld m=%ld max |G-ref|/sum|terms| = %.3e  %s\n", (long)N, (long)m, maxrel,
+    printf("CHECK tall=%d N=%ld m=%ld max |G-ref|/sum|terms| = %.3e  %s\n", tall, (long)N, (long)m, maxrel,
            maxrel < 1e-14 ? "PASS" : "FAIL");
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0));
-  for (int r = 0; r < reps; ++r) CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, 0));
+  for (int r = 0; r < reps; ++r) CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, tall, 0));
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= reps;
   const double alg = (double)N * m * (m + 1);   // symmetric Gram, algorithmic
-  if (getenv("GRAM_EXPERIMENTS")) {
+  if (getenv("GRAM_EXPERIMENTS") && tall) {
+    CK(hipEventRecord(e0));
+    CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 4, 0));
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float t; CK(hipEventElapsedTime(&t, e0, e1));
+    printf("EXP tall noload: %.3f ms  %.2f TF/s\n", t, alg / t / 1e9);
+  } else if (getenv("GRAM_EXPERIMENTS")) {
     // (a) operands held in registers after the first stage: compute + LDS + barrier ceiling
     CK(hipEventRecord(e0));
     CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 1, 0));
@@ -116,19 +124,25 @@ static int run(int64_t N, int64_t m, int reps, bool check) {
       printf("EXP kchunk %ld: %.3f ms  %.2f TF/s\n", (long)kc, t, alg / t / 1e9);
     }
   }
-  double exe = 2.0 * N * 128.0 * 128.0 * nt;  // executed incl. full diagonal tiles
-  printf("GRAM N=%ld m=%ld tiles=%d: %.3f ms/launch  alg %.2f TF/s  exec %.2f TF/s\n", (long)N, (long)m, nt, ms,
+  double exe = 2.0 * N * (tall ? 256.0 : 128.0) * 128.0 * nt;  // executed incl. full diagonal tiles
+  printf("GRAM tall=%d N=%ld m=%ld tiles=%d: %.3f ms/launch  alg %.2f TF/s  exec %.2f TF/s\n", tall, (long)N, (long)m,
+         nt, ms,
          alg / ms / 1e9, exe / ms / 1e9);
   CK(hipFree(A)); CK(hipFree(w)); CK(hipFree(G)); CK(hipFree(dtl));
   return 0;
 }
 
 int main(int argc, char** argv) {
-  if (argc >= 3) return run(atoll(argv[1]), atoll(argv[2]), argc > 3 ? atoi(argv[3]) : 3, false);
-  run(48, 256, 1, true);
-  run(1024, 384, 1, true);
-  run(4096, 1024, 1, true);
-  run(1 << 17, 8192, 3, false);
-  run(1 << 17, 16384, 2, false);
+  if (argc >= 3) {
+    run(atoll(argv[1]), atoll(argv[2]), argc > 3 ? atoi(argv[3]) : 3, false, 0);
+    return run(atoll(argv[1]), atoll(argv[2]), argc > 3 ? atoi(argv[3]) : 3, false, 1);
+  }
+  for (int tall = 0; tall < 2; ++tall) {
+    run(48, 256, 1, true, tall);
+    if (!tall) run(1024, 384, 1, true, tall);
+    run(4096, 1024, 1, true, tall);
+    run(1 << 17, 8192, 3, false, tall);
+    run(1 << 17, 16384, 2, false, tall);
+  }
   return 0;
 }

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -115,8 +116,11 @@ struct scs_ctx {
   double* tpart = nullptr;
   // Gram / solve
   double *G = nullptr, *Gc = nullptr;
-  int2* tiles = nullptr;
+  int2* tiles = nullptr;    // Gram launch list
   int ntiles = 0;
+  int tall = 0;             // 1: 256 x 128 launch tiles (nb even), packed slots = their 128 x 128 halves
+  int2* utiles = nullptr;   // 128 x 128 slot list (unpack)
+  int nslots = 0;
   double* W = nullptr;      // inverted diagonal blocks of the Cholesky factor [mpad/128][128*128]
   double* wpm = nullptr;    // [128 x +1.0, 128 x -1.0] Gram weights for the factorization
   double* ysol = nullptr;   // triangular-solve scratch (mpad)
@@ -368,12 +372,27 @@ void ensure_gram(scs_ctx* c) {
   c->G = dalloc<double>(c, (size_t)mp * mp);
   c->Gc = dalloc<double>(c, (size_t)mp * mp);
   const int nb = (int)(mp / 128);
-  std::vector<int2> tl((size_t)nb * (nb + 1) / 2);
+  std::vector<int2> tl((size_t)nb * (nb + 1) / 2 + nb), ul;
   int nt = 0;
-  gram_tile_list(nb, tl.data(), &nt);
+  const char* sq = std::getenv("SCS_GRAM_TALL");
+  c->tall = (nb % 2 == 0) && !(sq && sq[0] == '0');
+  if (c->tall) {
+    gram_tile_list_tall(nb, tl.data(), &nt);
+    ul.resize(2 * (size_t)nt);
+    for (int t = 0; t < nt; ++t) {
+      ul[2 * t] = make_int2(2 * tl[t].x, tl[t].y);
+      ul[2 * t + 1] = make_int2(2 * tl[t].x + 1, tl[t].y);
+    }
+  } else {
+    gram_tile_list(nb, tl.data(), &nt);
+    ul.assign(tl.begin(), tl.begin() + nt);
+  }
   c->tiles = dalloc<int2>(c, nt);
   HCK(hipMemcpyAsync(c->tiles, tl.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->st));
   c->ntiles = nt;
+  c->nslots = (int)ul.size();
+  c->utiles = dalloc<int2>(c, ul.size());
+  HCK(hipMemcpyAsync(c->utiles, ul.data(), sizeof(int2) * ul.size(), hipMemcpyHostToDevice, c->st));
   {
     const int nb2 = (int)(mp / 128);
     c->W = dalloc<double>(c, (size_t)mp * 128);
@@ -623,17 +642,17 @@ void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
   ensure_gram(c);
   hipEvent_t e0;
   if (c->nranks > 1) {
-    const int64_t tsz = (int64_t)c->ntiles * 128 * 128;
+    const int64_t tsz = (int64_t)c->nslots * 128 * 128;
     tbegin(c, T_GRAM, &e0);
-    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->red, c->mpad, 1, c->st));
+    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->red, c->mpad, 1, c->tall, c->st));
     tend(c, T_GRAM, e0);
     HCK(hipMemcpyAsync(c->red + tsz, vec_dev, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
     allreduce(c, c->red, tsz + c->m);
-    HCK(gram_unpack_launch(c->red, c->tiles, c->ntiles, c->G, c->mpad, c->st));
+    HCK(gram_unpack_launch(c->red, c->utiles, c->nslots, c->G, c->mpad, c->st));
     HCK(hipMemcpyAsync(vec_dev, c->red + tsz, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
   } else {
     tbegin(c, T_GRAM, &e0);
-    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->st));
+    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->tall, c->st));
     tend(c, T_GRAM, e0);
   }
 }
@@ -839,7 +858,7 @@ int scs_reduce_buffer_size(scs_ctx* c, int64_t* nd) {
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "reduce buffer size needs the data dimensions");
     const int64_t nb = c->mpad / 128;
-    const int64_t tsz = nb * (nb + 1) / 2 * 128 * 128;
+    const int64_t tsz = (nb * (nb + 1) / 2 + nb) * 128 * 128;   // 128 x 128 slots (tall lists add <= nb)
     *nd = std::max<int64_t>(tsz + c->mpad, c->mpad) + 64;
   });
 }
@@ -875,6 +894,7 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->G);
   dfree_t(c, c->Gc);
   dfree_t(c, c->tiles);
+  dfree_t(c, c->utiles);
   dfree_t(c, c->W);
   dfree_t(c, c->wpm);
   dfree_t(c, c->ysol);
@@ -883,7 +903,7 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->cinfo);
   dfree_t(c, c->dinfo);
   dfree_t(c, c->ipiv);
-  c->ntiles = 0;
+  c->ntiles = c->nslots = 0;
   invalidate_caches(c);
   c->has_data = false;
   c->reg_set = c->smooth_set = c->method_set = false;
@@ -1322,7 +1342,7 @@ int scs_gram_eval(scs_ctx* c, const double* w, double* G, int64_t ldg) {
     ensure_gram(c);
     hipEvent_t e0;
     tbegin(c, T_GRAM, &e0);
-    HCK(gram_launch(c->A, c->Npad, c->wN, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->st));
+    HCK(gram_launch(c->A, c->Npad, c->wN, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->tall, c->st));
     tend(c, T_GRAM, e0);
     HCK(launch_symmetrize(c->G, c->mpad, c->m, c->st));
     HCK(hipMemcpy2DAsync(G, sizeof(double) * ldg, c->G, sizeof(double) * c->mpad, sizeof(double) * c->m, c->m,
