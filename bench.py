@@ -217,6 +217,16 @@ def main():
             line["hbm_frac_streaming"] = line["hbm_gbs_streaming"] / HBM_PEAK_GBS
         line["breakdown_ms_per_step"] = {k.replace("_ms", ""): tm[k] / steps for k in tm if k.endswith("_ms")}
         line["objective_last"] = objs[-1]
+        if not args.no_cpu_baseline and args.config == "c5":
+            try:
+                out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline_lqn.py"), "--N", str(N),
+                                      "--m", str(m), "--rho", str(cfg["rho"]), "--mem", str(cfg["mem"])],
+                                     capture_output=True, text=True, timeout=300, check=True)
+                cb = json.loads(out.stdout.strip().splitlines()[-1])
+                line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+                line["cpu_baseline"]["t_iter_s"] = cb["t_iter_s"]
+            except Exception as e:  # the baseline is reported, never the target
+                line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
         if not args.no_cpu_baseline and args.config == "c3":
             env = dict(os.environ)
             cores = int(env.get("OMP_NUM_THREADS", "16"))

@@ -56,8 +56,13 @@ hipError_t launch_trial_point(const double* x, const double* d, double alpha, in
                               hipStream_t st);
 hipError_t launch_bb_step(const double* x, const double* xp, const double* g, const double* gp, int64_t m,
                           double* out, hipStream_t st);
+// m <= TWO_LOOP_SINGLE_MAX: one workgroup; above: TWO_LOOP_MAX_WG workgroups at most, one launch per
+// recursion step; work holds (k + 2) * TWO_LOOP_MAX_WG doubles
+constexpr int64_t TWO_LOOP_SINGLE_MAX = 16384;
+constexpr int TWO_LOOP_MAX_WG = 256;
 hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
-                           const double* g, int64_t m, double* q, double* d, double* ab, hipStream_t st);
+                           const double* g, int64_t m, double* q, double* d, double* ab, double* work,
+                           hipStream_t st);
 hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
                                double* Yslot, double* scal, hipStream_t st);
 hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st);

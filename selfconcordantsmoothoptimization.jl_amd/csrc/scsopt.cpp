@@ -105,7 +105,7 @@ struct scs_ctx {
   // m-space workspace
   double *x = nullptr, *xp = nullptr, *xn = nullptr, *dxv = nullptr, *gr = nullptr, *Hr = nullptr, *hinv = nullptr,
          *zb = nullptr, *d = nullptr, *gq = nullptr, *gqn = nullptr, *gtmp = nullptr, *gtmp2 = nullptr, *q = nullptr,
-         *ab = nullptr, *scal = nullptr, *gcache[2] = {nullptr, nullptr};
+         *ab = nullptr, *tlwork = nullptr, *scal = nullptr, *gcache[2] = {nullptr, nullptr};
   double* hscal = nullptr;  // pinned host scalars
   // N-space workspace
   int nsplit = 1;
@@ -732,7 +732,8 @@ void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, dou
     HCK(launch_neg(c->gq, m, c->d, c->st));
   } else {
     HCK(hipMemcpyAsync(c->d_order, c->ring.data(), sizeof(int) * k, hipMemcpyHostToDevice, c->st));
-    HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->st));
+    HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->tlwork,
+                        c->st));
   }
   double step = 0.0;
   const double* step_dev = nullptr;
@@ -1242,6 +1243,8 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
       dfree_t(c, c->Yv);
       dfree_t(c, c->d_order);
       dfree_t(c, c->ab);
+      dfree_t(c, c->tlwork);
+      c->tlwork = dalloc<double>(c, (size_t)(mem + 3) * TWO_LOOP_MAX_WG);
       c->S = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
       c->Yv = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
       c->d_order = dalloc<int>(c, mem + 1);

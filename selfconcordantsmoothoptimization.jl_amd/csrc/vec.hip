@@ -8,6 +8,9 @@
 // bitwise identical.  Expressions follow the reference's evaluation order
 // so that, on identical inputs, elementwise outputs match the oracle bit for
 // bit (IEEE +,-,*,/,sqrt); pow() may differ by <= 1-2 ulp from Julia's.
+#include <algorithm>
+#include <utility>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -340,6 +343,102 @@ __global__ __launch_bounds__(VB) void two_loop_kernel(const double* __restrict__
   for (int64_t i = threadIdx.x; i < m; i += VB) dout[i] = -q[i];
 }
 
+// Multi-workgroup two-loop for large m: the same recursion, with each dot
+// formed as fixed-order per-chunk partials that every workgroup sums in the
+// same order (so all of them agree on α, β bit for bit and runs repeat
+// exactly).  One launch per recursion step; each launch applies its axpy to
+// its chunk and immediately forms the next step's partial dot on the updated
+// chunk, so q / r are read once per step.  The chunk partition (not the
+// single-workgroup stride) sets the summation order of the dots.
+constexpr int TLB = 256;
+__device__ __forceinline__ double sum_parts(const double* __restrict__ p, int G) {
+  double s = 0.0;
+  for (int b = 0; b < G; ++b) s += p[b];
+  return s;
+}
+
+__global__ __launch_bounds__(TLB) void tl_init_kernel(const double* __restrict__ S, const double* __restrict__ Y,
+                                                      int64_t ld, const int* __restrict__ order, int k,
+                                                      const double* __restrict__ g, int64_t m, int64_t C,
+                                                      double* __restrict__ q, double* __restrict__ pys,
+                                                      double* __restrict__ psq) {
+  __shared__ double sh[TLB / 64];
+  const int G = gridDim.x, b = blockIdx.x;
+  const int64_t i0 = b * C, i1 = min(m, i0 + C);
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) q[i] = g[i];
+  for (int t = 0; t < k; ++t) {
+    const double* s = S + (int64_t)order[t] * ld;
+    const double* y = Y + (int64_t)order[t] * ld;
+    double v = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) v += y[i] * s[i];
+    v = block_sum<TLB>(v, sh);
+    if (threadIdx.x == 0) pys[t * G + b] = v;
+  }
+  const double* s = S + (int64_t)order[k - 1] * ld;
+  double v = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) v += s[i] * g[i];
+  v = block_sum<TLB>(v, sh);
+  if (threadIdx.x == 0) psq[b] = v;
+}
+
+// first loop, step t (newest -> oldest): q -= α_t y_t; partial s_{t-1}·q (or, at t = 0,
+// r = H0 q and the partial y_0·r of the second loop)
+__global__ __launch_bounds__(TLB) void tl_first_kernel(const double* __restrict__ S, const double* __restrict__ Y,
+                                                       int64_t ld, const int* __restrict__ order, int t, double H0,
+                                                       int64_t m, int64_t C, double* __restrict__ q,
+                                                       const double* __restrict__ pys,
+                                                       const double* __restrict__ pin, double* __restrict__ pout,
+                                                       double* __restrict__ ab) {
+  __shared__ double sh[TLB / 64];
+  const int G = gridDim.x, b = blockIdx.x;
+  const int64_t i0 = b * C, i1 = min(m, i0 + C);
+  const double ys = sum_parts(pys + t * G, G), sq = sum_parts(pin, G);
+  const double rho = 1.0 / ys;
+  const double al = rho * sq;
+  const double* y = Y + (int64_t)order[t] * ld;
+  const double* sn = (t > 0) ? S + (int64_t)order[t - 1] * ld : Y + (int64_t)order[0] * ld;
+  double v = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) {
+    double qi = q[i] - al * y[i];
+    if (t == 0) qi = H0 * qi;
+    q[i] = qi;
+    v += sn[i] * qi;
+  }
+  v = block_sum<TLB>(v, sh);
+  if (threadIdx.x == 0) {
+    pout[b] = v;
+    if (b == 0) { ab[2 * t] = al; ab[2 * t + 1] = rho; }
+  }
+}
+
+// second loop, step t (oldest -> newest): r += s_t (α_t − β_t); partial y_{t+1}·r, or d = −r at the end
+__global__ __launch_bounds__(TLB) void tl_second_kernel(const double* __restrict__ S, const double* __restrict__ Y,
+                                                        int64_t ld, const int* __restrict__ order, int t, int k,
+                                                        int64_t m, int64_t C, double* __restrict__ r,
+                                                        const double* __restrict__ pin, double* __restrict__ pout,
+                                                        const double* __restrict__ ab, double* __restrict__ dout) {
+  __shared__ double sh[TLB / 64];
+  const int G = gridDim.x, b = blockIdx.x;
+  const int64_t i0 = b * C, i1 = min(m, i0 + C);
+  const double yr = sum_parts(pin, G);
+  const double al = ab[2 * t], rho = ab[2 * t + 1];
+  const double beta = rho * yr;
+  const double* s = S + (int64_t)order[t] * ld;
+  const bool last = (t == k - 1);
+  const double* yn = last ? s : Y + (int64_t)order[t + 1] * ld;
+  double v = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) {
+    const double ri = r[i] + s[i] * (al - beta);
+    if (last) dout[i] = -ri;
+    else r[i] = ri;
+    v += yn[i] * ri;
+  }
+  if (!last) {
+    v = block_sum<TLB>(v, sh);
+    if (threadIdx.x == 0) pout[b] = v;
+  }
+}
+
 // L-BFGS memory update (prox-L-BFGS-SCORE.jl:148-162): γh = ∇q_new − ∇q,
 // store (δh, γh) into ring slot `slot` when δhᵀγh > 1e-10.  scal[0] = δhᵀγh,
 // scal[1] = γhᵀγh.  The host reads scal and advances the ring.
@@ -490,8 +589,26 @@ hipError_t launch_bb_step(const double* x, const double* xp, const double* g, co
   return hipGetLastError();
 }
 hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
-                           const double* g, int64_t m, double* q, double* d, double* ab, hipStream_t st) {
-  hipLaunchKernelGGL(two_loop_kernel, dim3(1), dim3(VB), 0, st, S, Y, ld, order, k, H0, g, m, q, d, ab);
+                           const double* g, int64_t m, double* q, double* d, double* ab, double* work,
+                           hipStream_t st) {
+  if (m <= TWO_LOOP_SINGLE_MAX || k < 1) {
+    hipLaunchKernelGGL(two_loop_kernel, dim3(1), dim3(VB), 0, st, S, Y, ld, order, k, H0, g, m, q, d, ab);
+    return hipGetLastError();
+  }
+  const int G = (int)std::min<int64_t>(TWO_LOOP_MAX_WG, ceil_div(m, 1024));
+  const int64_t C = ceil_div(m, G);
+  double* pys = work;               // [k][G]
+  double* pa = work + (int64_t)k * G;
+  double* pb = pa + G;
+  hipLaunchKernelGGL(tl_init_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, k, g, m, C, q, pys, pa);
+  for (int t = k - 1; t >= 0; --t) {
+    hipLaunchKernelGGL(tl_first_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, t, H0, m, C, q, pys, pa, pb, ab);
+    std::swap(pa, pb);
+  }
+  for (int t = 0; t < k; ++t) {
+    hipLaunchKernelGGL(tl_second_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, t, k, m, C, q, pa, pb, ab, d);
+    std::swap(pa, pb);
+  }
   return hipGetLastError();
 }
 hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,

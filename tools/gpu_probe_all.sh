@@ -11,7 +11,7 @@ rc=$?; echo "probe_gram c3 rc=$rc"; cat gpurun_out/probe_gram_c3.log
 timeout -k 10 120 ./build/probe_chol > gpurun_out/probe_chol.log 2>&1
 rc=$?; echo "probe_chol rc=$rc"; cat gpurun_out/probe_chol.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 900 python -m pytest tests -m gpu -q -ra -k "cholesky or lu_fallback or sparse or synthetic or gram or shard" > gpurun_out/pytest_sc.log 2>&1
+timeout -k 10 900 python -m pytest tests -m gpu -q -ra -k "cholesky or lu_fallback or sparse or synthetic or gram or shard or two_loop" > gpurun_out/pytest_sc.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_sc.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for c in c2 c5 c3; do
