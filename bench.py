@@ -196,18 +196,20 @@ def main():
                                 "kernel": "gram_f64_kernel", "avg_ms": gram_avg_ms, "launches": main_calls,
                                 "flops_per_launch": gram_flops}
         if tm["gemv_calls"] and cfg.get("sparse"):
-            # CSR (A·x, N rows) and CSC (Aᵀ·v, m columns) gathers, launched equally often: algorithmic
-            # bytes per launch = nnz·(value + 4 B index) + 8 B pointer + 8 B output per row (column)
-            # + the gathered vector read once (mean of the two launches)
+            # LDS-blocked CSR (A·x) and CSC (Aᵀ·v) passes, launched equally often.  Bytes each launch must
+            # move: nnz·(value + 2 B local index) + the per-block row pointers (8 B per row and block)
+            # + one partial per row and block + the gathered vector once (mean of the two launches)
             nnz = model.nnz
             vb = 4 if args.f32 else 8
-            csr = nnz * (vb + 4) + 8 * (N + 1) + 8 * N + 8 * m
-            csc = nnz * (vb + 4) + 8 * (m + 1) + 8 * m + 8 * N
+            nb_csr = -(-m // 16384)
+            nb_csc = -(-N // 16384)
+            csr = nnz * (vb + 2) + 8 * nb_csr * (N + 1) + 8 * nb_csr * N + 8 * m
+            csc = nnz * (vb + 2) + 8 * nb_csc * (m + 1) + 8 * nb_csc * m + 8 * N
             per_launch = 0.5 * (csr + csc)
             avg_ms = tm["gemv_ms"] / tm["gemv_calls"]
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "spmv_kernel",
+                                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "spmv_blk_kernel",
                                 "avg_ms": avg_ms, "launches_per_step": tm["gemv_calls"] / steps,
                                 "bytes_per_launch": per_launch}
             line["config"]["nnz"] = nnz

@@ -30,6 +30,9 @@
 // run of that list: the ~64 tiles co-resident on an XCD then read ~16
 // distinct column panels, which its 4 MiB L2 serves (speed only; results do
 // not depend on placement).
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 
 namespace scs {
@@ -57,7 +60,8 @@ template <bool NOLOAD, int TI>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
     const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
     const double* __restrict__ w, int64_t k0, int64_t Nk, const int2* __restrict__ tiles, int ntiles,
-    double* __restrict__ G, int64_t ldg, int flags) {
+    double* __restrict__ G, int64_t ldg, int flags, const int4* __restrict__ work, int seglen, int nsplit,
+    double* __restrict__ P) {
   constexpr int GTI = 64 * TI;               // tile rows (A1 panel width)
   constexpr int NT = 128 * TI;               // threads
   constexpr int SB = GTI * GBK + GT * GBK;   // doubles per LDS stage
@@ -67,10 +71,31 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
 
   // XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle")
   const int orig = blockIdx.x;
-  const int q8 = ntiles / 8, r8 = ntiles % 8, xcd = orig % 8;
-  const int tix = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int2 tl = tiles[tix];
-  const int bi = tl.x, bj = tl.y;
+  const int xcd = orig % 8;
+  int bi, bj, tix, part = -1;
+  if (work) {
+    // scheduled work list (gram_schedule): XCD x runs items [x*seglen, (x+1)*seglen) in order;
+    // item = (bi, bj, ks, idx): ks < 0 -> whole K, canonical tile idx; ks >= 0 -> K piece ks of
+    // nsplit, partial slot idx; bi < 0 -> padding
+    const int4 it = work[xcd * seglen + orig / 8];
+    if (it.x < 0) return;
+    bi = it.x;
+    bj = it.y;
+    tix = it.w;
+    if (it.z >= 0) {
+      const int64_t L = ((Nk - k0 + (int64_t)nsplit * GBK - 1) / ((int64_t)nsplit * GBK)) * GBK;
+      part = it.w;
+      k0 = k0 + it.z * L;
+      Nk = k0 + L < Nk ? k0 + L : Nk;
+      if (Nk < k0) Nk = k0;
+    }
+  } else {
+    const int q8 = ntiles / 8, r8 = ntiles % 8;
+    tix = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int2 tl = tiles[tix];
+    bi = tl.x;
+    bj = tl.y;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -116,8 +141,10 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
   const int fl = lane & 15, g = lane >> 4, s = swz(fl);
   const int nk = (int)((Nk - k0) / GBK);
 
-  gload(k0);
-  swrite(0);
+  if (nk > 0) {
+    gload(k0);
+    swrite(0);
+  }
   __syncthreads();
   for (int k = 0; k < nk; ++k) {
     if (k + 1 < nk) gload(k0 + (int64_t)(k + 1) * GBK);
@@ -160,6 +187,10 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
         const int il = wr * 64 + 16 * ti + g + 4 * r;
         const int jl = wc * 64 + 16 * tj + fl;
         double* dst;
+        if (part >= 0) {
+          P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
+          continue;
+        }
         if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
         else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
         else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
@@ -354,7 +385,7 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
     return gram_launch_gen(A, lda, A, lda, w, 0, Nk, tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER, st);
   if (ntiles <= 0) return hipSuccess;
   hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
-                     tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER);
+                     tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER, nullptr, 0, 0, nullptr);
   return hipGetLastError();
 }
 
@@ -364,7 +395,7 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
                            hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles,
-                     ntiles, G, ldg, flags);
+                     ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   return hipGetLastError();
 }
 
@@ -374,20 +405,107 @@ hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
   if (noload == 4)
     hipLaunchKernelGGL((gram_f64_kernel<true, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (noload == 3)
     hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (noload == 2)
     hipLaunchKernelGGL(gram_f64_pf2_kernel, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G, ldg,
                        0, accumulate);
   else if (noload)
     hipLaunchKernelGGL((gram_f64_kernel<true, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   return hipGetLastError();
+}
+
+// Combine K-split partials of the scheduled tail tiles in piece order and place
+// them like the main epilogue (upper triangle, or the packed slot of the
+// canonical tile index).  item = (bi, bj, canonical tix, first partial slot).
+template <int TI>
+__global__ void gram_combine_kernel(const double* __restrict__ P, const int4* __restrict__ items, int nsplit,
+                                    double* __restrict__ G, int64_t ldg, int packed) {
+  constexpr int GTI = 64 * TI;
+  const int4 it = items[blockIdx.y];
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < GTI * GT; e += gridDim.x * blockDim.x) {
+    const int jl = e / GTI, il = e % GTI;
+    double sum = 0.0;
+    for (int sp = 0; sp < nsplit; ++sp) sum += P[(int64_t)(it.w + sp) * GTI * GT + e];
+    if (packed)
+      G[((int64_t)it.z * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT)] = sum;
+    else
+      G[((int64_t)it.x * GTI + il) * ldg + (int64_t)it.y * GT + jl] = sum;
+  }
+}
+
+// Scheduled main Gram (gram_schedule's work list + tail combine).
+hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
+                             int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
+                             int tall, hipStream_t st) {
+  const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
+  if (tall)
+    hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
+                       Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  else
+    hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w, (int64_t)0,
+                       Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  if (ncomb > 0) {
+    if (tall)
+      hipLaunchKernelGGL(gram_combine_kernel<4>, dim3(16, ncomb), dim3(256), 0, st, P, comb, nsplit, G, ldg, packed);
+    else
+      hipLaunchKernelGGL(gram_combine_kernel<2>, dim3(16, ncomb), dim3(256), 0, st, P, comb, nsplit, G, ldg, packed);
+  }
+  return hipGetLastError();
+}
+
+// Host: build the scheduled work list from the canonical tile list.  The list is
+// cut into 8 contiguous XCD segments (XCD x = blocks orig % 8 == x, run in
+// orig order); in each segment the tiles that would form a partial last round
+// (fewer than 3/4 of the XCD's `slots` concurrent workgroups) are split into
+// nsplit K pieces, so the last round is full; segments are padded to equal
+// length with no-op items.  Returns seglen; fills work (8*seglen), comb
+// (combine items), *ncomb, *nsplit, *npart (partial slots).
+int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<int4>& work, std::vector<int4>& comb,
+                  int* nsplit, int* npart) {
+  const int q = ntiles / 8, r = ntiles % 8;
+  // per-XCD tail and a common split factor
+  int tail_max = 0;
+  for (int x = 0; x < 8; ++x) {
+    const int n = q + (x < r ? 1 : 0);
+    const int t = n % slots_per_xcd;
+    tail_max = std::max(tail_max, t);
+  }
+  int S = 1;
+  if (tail_max > 0 && 4 * tail_max < 3 * slots_per_xcd)
+    S = std::max(2, std::min(16, slots_per_xcd / tail_max));
+  std::vector<std::vector<int4>> seg(8);
+  comb.clear();
+  int pslot = 0, t0 = 0;
+  for (int x = 0; x < 8; ++x) {
+    const int n = q + (x < r ? 1 : 0);
+    const int tail = (S > 1) ? n % slots_per_xcd : 0;
+    for (int i = 0; i < n - tail; ++i) {
+      const int2 tl = tiles[t0 + i];
+      seg[x].push_back(make_int4(tl.x, tl.y, -1, t0 + i));
+    }
+    for (int i = n - tail; i < n; ++i) {
+      const int2 tl = tiles[t0 + i];
+      comb.push_back(make_int4(tl.x, tl.y, t0 + i, pslot));
+      for (int sp = 0; sp < S; ++sp) seg[x].push_back(make_int4(tl.x, tl.y, sp, pslot + sp));
+      pslot += S;
+    }
+    t0 += n;
+  }
+  size_t seglen = 0;
+  for (auto& v : seg) seglen = std::max(seglen, v.size());
+  work.assign(8 * seglen, make_int4(-1, -1, -1, -1));
+  for (int x = 0; x < 8; ++x)
+    for (size_t i = 0; i < seg[x].size(); ++i) work[x * seglen + i] = seg[x][i];
+  *nsplit = S;
+  *npart = pslot;
+  return (int)seglen;
 }
 
 hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <vector>
 #include "../../include/scsopt.h"
 
 namespace scs {
@@ -30,6 +32,13 @@ void gram_tile_list_rowmajor(int nb, int2* out);
 hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                            hipStream_t st);
+// Tail-balanced schedule of the main Gram (see gram.hip): work items (bi, bj, ks, idx),
+// combine items (bi, bj, tix, first partial slot)
+int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<int4>& work, std::vector<int4>& comb,
+                  int* nsplit, int* npart);
+hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
+                             int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
+                             int tall, hipStream_t st);
 hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,
                               hipStream_t st);
 
@@ -98,14 +107,23 @@ hipError_t launch_gen_xtrue(double* x, int64_t m, uint64_t seed, double density,
 hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t row0, uint64_t seed,
                         hipStream_t st);
 
-// ---- sparse.hip (CSR / CSC gathers; out[r] = Σ_p val[p] x[idx[p]], p in [ptr[r], ptr[r+1]))
-hipError_t launch_spmv(const int64_t* ptr, const int* idx, const void* val, int f32, const double* x, int64_t nrows,
-                       double* out, hipStream_t st);
+// ---- sparse.hip (LDS-blocked gathers; out[b*ldo + r] = Σ_{p in row r, block b} val[p] x[(b<<shift) + lidx[p]])
+int spmv_blk_shift(int64_t ncols);
+hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
+                           int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,
+                           hipStream_t st);
+hipError_t blk_count(const int64_t* ptr, const int* idx, int64_t nrows, int shift, int64_t* cnt, int64_t* first,
+                     hipStream_t st);
+hipError_t blk_scan(void* temp, size_t* temp_bytes, const int64_t* cnt, int64_t* bptr, int64_t n, hipStream_t st);
+hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int f32, int64_t nrows, int shift,
+                       const int64_t* bptr, const int64_t* first, uint16_t* lidx, void* bval, hipStream_t st);
 size_t sparse_layer_map_bytes(int k);
 void sparse_layer_maps(uint64_t seed, int k, int64_t N, void* out_host);
 hipError_t launch_gen_sparse(int64_t N, int64_t m, int k, uint64_t seed, const void* Ldev, int f32, double scale,
                              int64_t* rowptr, int* col, void* val, int64_t* colptr, int* row, void* valT,
                              hipStream_t st);
+hipError_t sort_segments(void* temp, size_t* temp_bytes, const int* kin, int* kout, const void* vin, void* vout,
+                         int f32, int64_t nnz, int64_t nseg, const int64_t* off, int end_bit, hipStream_t st);
 hipError_t launch_gen_uniform(double* x, int64_t m, uint64_t seed, double lo, double hi, hipStream_t st);
 
 }  // namespace scs

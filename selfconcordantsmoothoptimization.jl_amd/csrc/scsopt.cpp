@@ -68,6 +68,12 @@ struct scs_ctx {
   int64_t *rowptr = nullptr, *colptr = nullptr;
   int *colidx = nullptr, *rowidx = nullptr;
   void *val = nullptr, *valT = nullptr;
+  struct SpBlk {
+    int shift = 0, nblk = 0;
+    int64_t* ptr = nullptr;
+    uint16_t* lidx = nullptr;
+    void* val = nullptr;
+  } bcsr, bcsc;  // LDS-blocked copies used by the products (sparse.hip)
 
   // problem
   int loss = 0, ggn = 0;
@@ -121,6 +127,10 @@ struct scs_ctx {
   int tall = 0;             // 1: 256 x 128 launch tiles (nb even), packed slots = their 128 x 128 halves
   int2* utiles = nullptr;   // 128 x 128 slot list (unpack)
   int nslots = 0;
+  int4* gwork = nullptr;    // tail-balanced schedule (gram_schedule): work items, combine items, partials
+  int4* gcomb = nullptr;
+  int gseglen = 0, gncomb = 0, gnsplit = 1;
+  double* gpart = nullptr;
   double* W = nullptr;      // inverted diagonal blocks of the Cholesky factor [mpad/128][128*128]
   double* wpm = nullptr;    // [128 x +1.0, 128 x -1.0] Gram weights for the factorization
   double* ysol = nullptr;   // triangular-solve scratch (mpad)
@@ -345,9 +355,9 @@ void alloc_mspace(scs_ctx* c) {
 
 void alloc_nspace(scs_ctx* c) {
   if (c->generic) return;
-  c->nsplit = c->sparse ? 1 : gemv_n_splits(c->Npad, c->m);
+  c->nsplit = c->sparse ? c->bcsr.nblk : gemv_n_splits(c->Npad, c->m);
   c->nval = epilogue_blocks(c->Npad);
-  c->nchunk = c->sparse ? 1 : gemv_t_chunks(c->Npad);
+  c->nchunk = c->sparse ? c->bcsc.nblk : gemv_t_chunks(c->Npad);
   dfree_t(c, c->zpart);
   dfree_t(c, c->z);
   dfree_t(c, c->gN);
@@ -375,7 +385,10 @@ void ensure_gram(scs_ctx* c) {
   std::vector<int2> tl((size_t)nb * (nb + 1) / 2 + nb), ul;
   int nt = 0;
   const char* sq = std::getenv("SCS_GRAM_TALL");
-  c->tall = (nb % 2 == 0) && !(sq && sq[0] == '0');
+  // 256 x 128 tiles pay off once the Gram is large (C3, m = 16384: 59.7 vs 57.0 TF/s); at m = 8192
+  // the 128 x 128 tiles are ~1.5 % faster (profiles/r01/ab_gram.log)
+  c->tall = (nb % 2 == 0) && nb >= 96 && !(sq && sq[0] == '0');
+  if (sq && sq[0] == '1') c->tall = (nb % 2 == 0);
   if (c->tall) {
     gram_tile_list_tall(nb, tl.data(), &nt);
     ul.resize(2 * (size_t)nt);
@@ -391,6 +404,22 @@ void ensure_gram(scs_ctx* c) {
   HCK(hipMemcpyAsync(c->tiles, tl.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->st));
   c->ntiles = nt;
   c->nslots = (int)ul.size();
+  {
+    const char* ev = std::getenv("SCS_GRAM_SCHED");
+    if (!(ev && ev[0] == '0')) {
+      std::vector<int4> wk, cb;
+      int npart = 0;
+      c->gseglen = gram_schedule(tl.data(), nt, 32 * (c->tall ? 1 : 2), wk, cb, &c->gnsplit, &npart);
+      c->gncomb = (int)cb.size();
+      c->gwork = dalloc<int4>(c, wk.size());
+      HCK(hipMemcpyAsync(c->gwork, wk.data(), sizeof(int4) * wk.size(), hipMemcpyHostToDevice, c->st));
+      if (c->gncomb > 0) {
+        c->gcomb = dalloc<int4>(c, cb.size());
+        HCK(hipMemcpyAsync(c->gcomb, cb.data(), sizeof(int4) * cb.size(), hipMemcpyHostToDevice, c->st));
+        c->gpart = dalloc<double>(c, (size_t)npart * (c->tall ? 256 : 128) * 128);
+      }
+    }
+  }
   c->utiles = dalloc<int2>(c, ul.size());
   HCK(hipMemcpyAsync(c->utiles, ul.data(), sizeof(int2) * ul.size(), hipMemcpyHostToDevice, c->st));
   {
@@ -437,8 +466,9 @@ double loss_scale_value(scs_ctx* c, double s) {
 // CSR gather pass).  Returns the number of partials written.
 int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
   if (c->sparse) {
-    HCK(launch_spmv(c->rowptr, c->colidx, c->val, c->sp_f32, xd, c->N, c->zpart, c->st));
-    return 1;
+    const auto& B = c->bcsr;
+    HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, c->sp_f32, xd, c->N, c->m, B.shift, c->nnz, c->zpart, c->Npad, c->st));
+    return B.nblk;
   }
   HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, nsplit, c->zpart, c->Npad, c->st));
   return nsplit;
@@ -448,7 +478,9 @@ int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
 // fixed-order finalize; sparse: one CSC gather pass)
 void matvec_t(scs_ctx* c, const double* v, double* out) {
   if (c->sparse) {
-    HCK(launch_spmv(c->colptr, c->rowidx, c->valT, c->sp_f32, v, c->m, out, c->st));
+    const auto& B = c->bcsc;
+    HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, c->sp_f32, v, c->m, c->N, B.shift, c->nnz, c->tpart, c->mpad, c->st));
+    HCK(launch_gemv_t_finalize(c->tpart, B.nblk, c->mpad, c->m, out, c->st));
     return;
   }
   HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
@@ -635,6 +667,15 @@ void solve_system(scs_ctx* c, double* rhs) {
   tend(c, T_SOLVE, e0);
 }
 
+// the main Gram launch (scheduled when gram_schedule built a work list)
+void gram_main(scs_ctx* c, const double* w, double* out, int packed) {
+  if (c->gwork)
+    HCK(gram_launch_sched(c->A, c->Npad, w, c->Npad, c->gwork, c->gseglen, c->gnsplit, c->gcomb, c->gncomb, c->gpart,
+                          out, c->mpad, packed, c->tall, c->st));
+  else
+    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st));
+}
+
 // Gram of the local rows with weights w -> c->G (single rank) or the packed
 // reduce buffer (multi-rank; then all-reduced together with `vec`).
 void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
@@ -644,7 +685,7 @@ void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
   if (c->nranks > 1) {
     const int64_t tsz = (int64_t)c->nslots * 128 * 128;
     tbegin(c, T_GRAM, &e0);
-    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->red, c->mpad, 1, c->tall, c->st));
+    gram_main(c, w, c->red, 1);
     tend(c, T_GRAM, e0);
     HCK(hipMemcpyAsync(c->red + tsz, vec_dev, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
     allreduce(c, c->red, tsz + c->m);
@@ -652,7 +693,7 @@ void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
     HCK(hipMemcpyAsync(vec_dev, c->red + tsz, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
   } else {
     tbegin(c, T_GRAM, &e0);
-    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->tall, c->st));
+    gram_main(c, w, c->G, 0);
     tend(c, T_GRAM, e0);
   }
 }
@@ -889,6 +930,12 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->rowidx);
   dfree(c, c->val);
   dfree(c, c->valT);
+  for (auto* B : {&c->bcsr, &c->bcsc}) {
+    dfree_t(c, B->ptr);
+    dfree_t(c, B->lidx);
+    dfree(c, B->val);
+    B->nblk = B->shift = 0;
+  }
   c->sparse = false;
   c->nnz = 0;
   dfree_t(c, c->y);
@@ -896,6 +943,11 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->Gc);
   dfree_t(c, c->tiles);
   dfree_t(c, c->utiles);
+  dfree_t(c, c->gwork);
+  dfree_t(c, c->gcomb);
+  dfree_t(c, c->gpart);
+  c->gseglen = c->gncomb = 0;
+  c->gnsplit = 1;
   dfree_t(c, c->W);
   dfree_t(c, c->wpm);
   dfree_t(c, c->ysol);
@@ -996,6 +1048,50 @@ static void upload_vals(scs_ctx* c, void* dst, const double* src, int64_t n, int
   sync(c);
 }
 
+// Sort each row's entries by index (in place: the arrays are replaced by sorted
+// copies) and build the LDS-blocked copy B (sparse.hip).
+static void build_blocked(scs_ctx* c, int64_t nrows, int64_t ncols, int64_t* ptr, int*& idx, void*& val,
+                          scs_ctx::SpBlk& B) {
+  const int64_t nnz = c->nnz;
+  size_t tb = 0;
+  if (nnz > 0 && nrows > 0) {
+    int end_bit = 1;
+    while ((int64_t(1) << end_bit) < ncols) ++end_bit;
+    int* idx_s = dalloc<int>(c, nnz);
+    void* val_s = dalloc_vals(c, nnz, c->sp_f32);
+    HCK(sort_segments(nullptr, &tb, idx, idx_s, val, val_s, c->sp_f32, nnz, nrows, ptr, end_bit, c->st));
+    void* tmp = dalloc<char>(c, tb);
+    HCK(sort_segments(tmp, &tb, idx, idx_s, val, val_s, c->sp_f32, nnz, nrows, ptr, end_bit, c->st));
+    sync(c);
+    dfree(c, tmp);
+    dfree_t(c, idx);
+    dfree(c, val);
+    idx = idx_s;
+    val = val_s;
+  }
+  B.shift = spmv_blk_shift(ncols);
+  B.nblk = (int)ceil_div(ncols, int64_t(1) << B.shift);
+  const int64_t nk = (int64_t)B.nblk * nrows;
+  int64_t* cnt = dalloc<int64_t>(c, nk + 1);
+  int64_t* first = dalloc<int64_t>(c, nk + 1);
+  B.ptr = dalloc<int64_t>(c, nk + 1);
+  B.lidx = dalloc<uint16_t>(c, nnz);
+  B.val = dalloc_vals(c, nnz, c->sp_f32);
+  if (nrows > 0) {
+    HCK(blk_count(ptr, idx, nrows, B.shift, cnt, first, c->st));
+    tb = 0;
+    HCK(blk_scan(nullptr, &tb, cnt, B.ptr, nk + 1, c->st));
+    void* tmp = dalloc<char>(c, tb);
+    HCK(blk_scan(tmp, &tb, cnt, B.ptr, nk + 1, c->st));
+    HCK(blk_scatter(ptr, idx, val, c->sp_f32, nrows, B.shift, B.ptr, first, B.lidx, B.val, c->st));
+    sync(c);
+    dfree(c, tmp);
+  }
+  sync(c);
+  dfree_t(c, cnt);
+  dfree_t(c, first);
+}
+
 int scs_set_sparse(scs_ctx* c, int64_t N, int64_t m, int64_t nnz, const int64_t* rowptr, const int32_t* colidx,
                    const double* val, const int64_t* colptr, const int32_t* rowidx, const double* valT, int f32,
                    const double* y, int64_t Nglob, int64_t row0) {
@@ -1035,6 +1131,8 @@ int scs_set_sparse(scs_ctx* c, int64_t N, int64_t m, int64_t nnz, const int64_t*
     }
     c->y = dalloc<double>(c, c->Npad);
     if (y && N > 0) h2d(c, c->y, y, N);
+    build_blocked(c, N, m, c->rowptr, c->colidx, c->val, c->bcsr);
+    build_blocked(c, m, N, c->colptr, c->rowidx, c->valT, c->bcsc);
     alloc_mspace(c);
     alloc_nspace(c);
     sync(c);
@@ -1069,16 +1167,20 @@ int scs_gen_sparse(scs_ctx* c, const scs_synth* s, int f32) {
     c->valT = dalloc_vals(c, nnz, c->sp_f32);
     c->y = dalloc<double>(c, c->Npad);
     alloc_mspace(c);
-    alloc_nspace(c);
     std::vector<char> maps(sparse_layer_map_bytes(k));
     sparse_layer_maps(s->seed, k, N, maps.data());
     void* dmaps = dalloc<char>(c, maps.size());
     HCK(hipMemcpyAsync(dmaps, maps.data(), maps.size(), hipMemcpyHostToDevice, c->st));
     HCK(launch_gen_sparse(N, m, k, s->seed, dmaps, c->sp_f32, 1.0 / std::sqrt((double)k), c->rowptr, c->colidx,
                           c->val, c->colptr, c->rowidx, c->valT, c->st));
+    build_blocked(c, N, m, c->rowptr, c->colidx, c->val, c->bcsr);
+    build_blocked(c, m, N, c->colptr, c->rowidx, c->valT, c->bcsc);
+    alloc_nspace(c);
     HCK(launch_gen_uniform(c->xn, m, s->seed, -1.5, 1.5, c->st));
-    matvec_n(c, c->xn, 1);
-    HCK(launch_gen_y(3, c->zpart, c->y, c->N, 0, s->seed, c->st));
+    const int ns = matvec_n(c, c->xn, c->nsplit);
+    HCK(launch_epilogue(SCS_LOSS_LEAST_SQUARES, SCS_GGN_NONE, EPI_Z, c->zpart, ns, c->Npad, c->y, c->N, c->Npad, 1.0,
+                        c->z, nullptr, nullptr, nullptr, nullptr, c->valpart, c->st));
+    HCK(launch_gen_y(3, c->z, c->y, c->N, 0, s->seed, c->st));
     sync(c);
     dfree(c, dmaps);
     c->has_data = true;
@@ -1345,7 +1447,7 @@ int scs_gram_eval(scs_ctx* c, const double* w, double* G, int64_t ldg) {
     ensure_gram(c);
     hipEvent_t e0;
     tbegin(c, T_GRAM, &e0);
-    HCK(gram_launch(c->A, c->Npad, c->wN, c->Npad, c->tiles, c->ntiles, c->G, c->mpad, 0, c->tall, c->st));
+    gram_main(c, c->wN, c->G, 0);
     tend(c, T_GRAM, e0);
     HCK(launch_symmetrize(c->G, c->mpad, c->m, c->st));
     HCK(hipMemcpy2DAsync(G, sizeof(double) * ldg, c->G, sizeof(double) * c->mpad, sizeof(double) * c->m, c->m,

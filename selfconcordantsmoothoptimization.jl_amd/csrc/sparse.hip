@@ -6,7 +6,7 @@
 //   spmv_csr : one wave per row, lanes stride the row's nonzeros (coalesced
 //              value/index loads, x gathered from L2), fixed-order wave sum.
 //   spmv_csc : the same per column.
-// Both are HBM-bound: bytes per pass = nnz * (sizeof(val) + 4) + vectors.
+// Both run on an LDS-blocked copy (below): bytes per pass = nnz * (sizeof(val) + 2) + pointers + vectors.
 //
 // Synthetic pattern (scs_gen_sparse): k = round(ρ m) "layers"; layer s maps
 // row i to column ((a_s i + b_s) mod N) mod m with a_s odd, a bijection of
@@ -14,33 +14,170 @@
 // nonzeros and every column exactly k N / m, so both the CSR and the CSC
 // arrays are written in place from closed forms (no sort); the value of
 // (i, s) is a counter-RNG normal, identical in both copies.
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace scs {
 
-template <typename VT>
-__global__ __launch_bounds__(256) void spmv_kernel(const int64_t* __restrict__ ptr, const int* __restrict__ idx,
-                                                   const VT* __restrict__ val, const double* __restrict__ x,
-                                                   int64_t nrows, double* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= nrows) return;
-  const int64_t p0 = ptr[row], p1 = ptr[row + 1];
-  double acc = 0.0;
-  for (int64_t p = p0 + lane; p < p1; p += 64) acc += (double)val[p] * x[idx[p]];
-  acc = wave_sum(acc);
-  if (lane == 0) out[row] = acc;
+// ---- LDS-blocked layout ------------------------------------------------------
+// Gathering x[idx] straight from L2 costs one L2 request per nonzero (the
+// indices are scattered), which caps the pass far below HBM rate.  Instead each
+// direction is stored "blocked": the index range is cut into blocks of
+// BS = 2^shift (<= 16384, 128 KiB of fp64) and block b holds, for every row,
+// that row's entries whose index falls in b (16-bit local indices).  A
+// workgroup owns (a run of rows, one block): it stages the block's slice of the
+// gathered vector in LDS once and streams the rows' (value, local index)
+// pairs, so the gathers are LDS reads and HBM sees nnz * (sizeof(val) + 2) B.
+// Output: one partial per block, out[b * ldo + r]; the callers sum the blocks
+// in fixed order (epilogue z-splits / gemv_t_finalize), so results do not
+// depend on scheduling.
+constexpr int SPB_MAXSHIFT = 14;
+constexpr int SPB_THREADS = 1024;
+constexpr int SPB_ROWS = 1024;   // rows per workgroup
+
+template <typename VT, int U>
+__global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
+                                                               const uint16_t* __restrict__ lidx,
+                                                               const VT* __restrict__ val,
+                                                               const double* __restrict__ x, int64_t nrows,
+                                                               int64_t ncols, int shift, double* __restrict__ out,
+                                                               int64_t ldo) {
+  __shared__ double xs[1 << SPB_MAXSHIFT];
+  const int b = blockIdx.y;
+  const int64_t c0 = (int64_t)b << shift;
+  const int nb = (int)min((int64_t)1 << shift, ncols - c0);
+  for (int i = threadIdx.x; i < nb; i += SPB_THREADS) xs[i] = x[c0 + i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t* pb = ptr + (int64_t)b * nrows;
+  const int64_t r1 = min(nrows, (int64_t)(blockIdx.x + 1) * SPB_ROWS);
+  for (int64_t r = (int64_t)blockIdx.x * SPB_ROWS + wv; r < r1; r += SPB_THREADS / 64) {
+    const int64_t p0 = pb[r], p1 = pb[r + 1];
+    double acc = 0.0;
+    int64_t p = p0 + lane;
+    for (; p + 64 * (U - 1) < p1; p += 64 * U) {
+      int id[U];
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        id[u] = lidx[p + 64 * u];
+        v[u] = (double)val[p + 64 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += v[u] * xs[id[u]];
+    }
+    if (p0 < p1 && p - lane < p1) {
+      int id[U];
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = min(p + 64 * u, p1 - 1);
+        id[u] = lidx[q];
+        v[u] = (double)val[q];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (p + 64 * u < p1) acc += v[u] * xs[id[u]];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) out[(int64_t)b * ldo + r] = acc;
+  }
 }
 
-hipError_t launch_spmv(const int64_t* ptr, const int* idx, const void* val, int f32, const double* x, int64_t nrows,
-                       double* out, hipStream_t st) {
-  const unsigned grid = (unsigned)ceil_div(nrows, 4);
+int spmv_blk_shift(int64_t ncols) {
+  int s = 0;
+  while (s < SPB_MAXSHIFT && ((int64_t)1 << s) < ncols) ++s;
+  return s;
+}
+
+hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
+                           int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,
+                           hipStream_t st) {
+  if (nrows <= 0) return hipSuccess;
+  const int nblk = (int)ceil_div(ncols, (int64_t)1 << shift);
+  const dim3 grid((unsigned)ceil_div(nrows, SPB_ROWS), (unsigned)nblk);
+  const int64_t avg = nnz / (nrows * nblk);
+  if (f32) {
+    if (avg <= 64 * 4)
+      hipLaunchKernelGGL((spmv_blk_kernel<float, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
+                         x, nrows, ncols, shift, out, ldo);
+    else
+      hipLaunchKernelGGL((spmv_blk_kernel<float, 16>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
+                         x, nrows, ncols, shift, out, ldo);
+  } else {
+    if (avg <= 64 * 4)
+      hipLaunchKernelGGL((spmv_blk_kernel<double, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+                         (const double*)val, x, nrows, ncols, shift, out, ldo);
+    else
+      hipLaunchKernelGGL((spmv_blk_kernel<double, 16>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+                         (const double*)val, x, nrows, ncols, shift, out, ldo);
+  }
+  return hipGetLastError();
+}
+
+// ---- building the blocked layout from a row-sorted CSR (indices ascending per row)
+// cnt[b*nrows + r] = #entries of row r in block b; first[b*nrows + r] = position of the first one
+__global__ void blk_count_kernel(const int64_t* __restrict__ ptr, const int* __restrict__ idx, int64_t nrows,
+                                 int shift, int64_t* __restrict__ cnt, int64_t* __restrict__ first) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const int64_t p0 = ptr[r], p1 = ptr[r + 1];
+  for (int64_t p = p0 + lane; p < p1; p += 64) {
+    const int b = idx[p] >> shift;
+    if (p == p0 || (idx[p - 1] >> shift) != b) first[(int64_t)b * nrows + r] = p;
+    if (p == p1 - 1 || (idx[p + 1] >> shift) != b) {
+      // last of its block in this row: count = p - first + 1 (first is written by another lane
+      // of this wave in the same pass only if p - first < 64; recompute it here instead)
+      int64_t q = p;
+      while (q > p0 && (idx[q - 1] >> shift) == b) --q;
+      cnt[(int64_t)b * nrows + r] = p - q + 1;
+    }
+  }
+}
+
+template <typename VT>
+__global__ void blk_scatter_kernel(const int64_t* __restrict__ ptr, const int* __restrict__ idx,
+                                   const VT* __restrict__ val, int64_t nrows, int shift,
+                                   const int64_t* __restrict__ bptr, const int64_t* __restrict__ first,
+                                   uint16_t* __restrict__ lidx, VT* __restrict__ bval) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const int64_t p0 = ptr[r], p1 = ptr[r + 1];
+  const int mask = (1 << shift) - 1;
+  for (int64_t p = p0 + lane; p < p1; p += 64) {
+    const int c = idx[p];
+    const int64_t k = (int64_t)(c >> shift) * nrows + r;
+    const int64_t dst = bptr[k] + (p - first[k]);
+    lidx[dst] = (uint16_t)(c & mask);
+    bval[dst] = val[p];
+  }
+}
+
+hipError_t blk_count(const int64_t* ptr, const int* idx, int64_t nrows, int shift, int64_t* cnt, int64_t* first,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(blk_count_kernel, dim3((unsigned)ceil_div(nrows, 4)), dim3(256), 0, st, ptr, idx, nrows, shift,
+                     cnt, first);
+  return hipGetLastError();
+}
+
+hipError_t blk_scan(void* temp, size_t* temp_bytes, const int64_t* cnt, int64_t* bptr, int64_t n, hipStream_t st) {
+  return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, cnt, bptr, n, st);
+}
+
+hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int f32, int64_t nrows, int shift,
+                       const int64_t* bptr, const int64_t* first, uint16_t* lidx, void* bval, hipStream_t st) {
+  const dim3 grid((unsigned)ceil_div(nrows, 4));
   if (f32)
-    hipLaunchKernelGGL(spmv_kernel<float>, dim3(grid), dim3(256), 0, st, ptr, idx, (const float*)val, x, nrows, out);
+    hipLaunchKernelGGL(blk_scatter_kernel<float>, grid, dim3(256), 0, st, ptr, idx, (const float*)val, nrows, shift,
+                       bptr, first, lidx, (float*)bval);
   else
-    hipLaunchKernelGGL(spmv_kernel<double>, dim3(grid), dim3(256), 0, st, ptr, idx, (const double*)val, x, nrows,
-                       out);
+    hipLaunchKernelGGL(blk_scatter_kernel<double>, grid, dim3(256), 0, st, ptr, idx, (const double*)val, nrows,
+                       shift, bptr, first, lidx, (double*)bval);
   return hipGetLastError();
 }
 
@@ -140,6 +277,19 @@ hipError_t launch_gen_sparse(int64_t N, int64_t m, int k, uint64_t seed, const v
                        (double*)valT);
   }
   return hipGetLastError();
+}
+
+// Sort each segment's (index, value) pairs by index (segments = CSC columns).
+// With temp == nullptr only *temp_bytes is set.  Ascending row order per
+// column makes the concurrently running column waves sweep the gathered vector
+// in the same direction, so its lines are reused in L2 instead of re-fetched.
+hipError_t sort_segments(void* temp, size_t* temp_bytes, const int* kin, int* kout, const void* vin, void* vout,
+                         int f32, int64_t nnz, int64_t nseg, const int64_t* off, int end_bit, hipStream_t st) {
+  if (f32)
+    return hipcub::DeviceSegmentedRadixSort::SortPairs(temp, *temp_bytes, kin, kout, (const float*)vin, (float*)vout,
+                                                       (int)nnz, (int)nseg, off, off + 1, 0, end_bit, st);
+  return hipcub::DeviceSegmentedRadixSort::SortPairs(temp, *temp_bytes, kin, kout, (const double*)vin, (double*)vout,
+                                                     (int)nnz, (int)nseg, off, off + 1, 0, end_bit, st);
 }
 
 // x_true ~ U(-1.5, 1.5); y = A x_true + 0.1 ε computed by the caller

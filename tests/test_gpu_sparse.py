@@ -81,6 +81,23 @@ def test_user_csr_input_and_edges():
     assert pz.fx(x0) == pytest.approx(0.5 * np.dot(y, y) / N, rel=1e-13)
 
 
+@pytest.mark.parametrize("N,m,rho", [(40000, 20000, 2e-4), (65536, 256, 0.05)])
+def test_multiblock_products(N, m, rho):
+    """Index ranges above one 16384-wide LDS block in either direction (several blocked partials,
+    summed in fixed order): generated (power-of-two N) and user-provided unsorted CSR."""
+    import scipy.sparse as sp
+    if N & (N - 1) == 0:
+        p = scsopt.Problem.synthetic_sparse(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1e-4, density=rho)
+        A, _ = p.get_sparse()
+    else:
+        rng = np.random.default_rng(21)
+        C = sp.random(N, m, density=rho, random_state=22, format="coo", data_rvs=rng.standard_normal)
+        perm = rng.permutation(C.nnz)          # scrambled entry order (unsorted rows): the device sorts
+        A = sp.coo_matrix((C.data[perm], (C.row[perm], C.col[perm])), shape=C.shape)
+        p = scsopt.Problem(A, rng.standard_normal(N), np.zeros(m), losses.least_squares(1.0 / N), 0.1)
+    _check_products(p, A)
+
+
 def test_gram_methods_refuse_sparse():
     N, m = 1024, 64
     p = scsopt.Problem.synthetic_sparse(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1e-4, density=0.1)
