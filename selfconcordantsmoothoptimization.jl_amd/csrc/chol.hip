@@ -30,20 +30,92 @@ constexpr int CLD = CB + 1;      // LDS row pitch (doubles) -> conflict-light co
 // global); the caller then takes the LU path.
 //
 // Inner-blocked (b = 16) right-looking factorization of the LDS copy S:
-//   A  wave 0 factors the 16 x 16 diagonal sub-block in registers (lane =
-//      column c, rows g + 4q) with shuffles, and inverts it (D⁻¹);
-//   B  panel: S(o:o+16, c) = D⁻ᵀ S(o:o+16, c) for the columns to the right;
+//   A  wave 0 factors the 16 x 16 diagonal sub-block in registers (lane c =
+//      column c; row values broadcast with v_readlane), reciprocal pivots to LDS;
+//   B  panel: forward substitution Dᵀ P = S(o:o+16, c), one column per thread;
 //   C  trailing update of the upper triangle with 4 x 4 register tiles.
-// Then W = U⁻¹ block row by block row from the bottom:
-//   W(ii, c) = -D_ii⁻¹ Σ_{t > block ii} U(ii, t) W(t, c),
-// overwriting U's rows in LDS as they are consumed.  The reciprocal of each
-// pivot is formed once and multiplied in, as LAPACK dpotf2 does.
+// Then W = U⁻¹: the eight 16 x 16 diagonal inverses (two per wave, in
+// registers), and recursive doubling W12 = -W11 · (U12 · W22) at block sizes
+// 16 -> 32 -> 64 -> 128, as register-blocked LDS products (4 x S/16 outputs per
+// thread); the intermediate T = U12·W22 lives in the (unused) strictly-lower
+// triangle of S.  Only the factorization steps are a serial chain.
 constexpr int SB = 16;
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+#ifdef CHOL_PROF
+// probe_chol -DCHOL_PROF: thread 0 records s_memrealtime (100 MHz) at phase boundaries
+__device__ long long chol_prof[64];
+#define PROF_MARK(i) \
+  if (threadIdx.x == 0 && k == 0) chol_prof[i] = (long long)__builtin_amdgcn_s_memrealtime()
+#else
+#define PROF_MARK(i)
+#endif
+
+// one doubling level: for every pair (i0 = 2pS, j0 = i0 + S):
+//   step 1  T(r, c) = Σ_{t <= c} U(i0+r, j0+t) W(j0+t, j0+c)   -> S[j0 + r][i0 + c] (strictly lower)
+//   step 2  W(i0+r, j0+c) = -Σ_{t >= r} W(i0+r, i0+t) T(t, c)  -> S[i0 + r][j0 + c]
+template <int S>
+__device__ __forceinline__ void chol_inv_double(double* su, int tid) {
+  constexpr int MC = S / 16;                  // columns per thread (4 rows x MC)
+  constexpr int TPP = 256 / (CB / (2 * S));   // threads per pair
+  const int pair = tid / TPP, loc = tid % TPP;
+  const int rg = loc / 16, cg = loc % 16;
+  const int i0 = 2 * S * pair, j0 = i0 + S;
+  const int r0 = 4 * rg, c0 = cg * MC;
+  double acc[4][MC];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < MC; ++m) acc[q][m] = 0.0;
+#pragma unroll 4
+  for (int t = 0; t < S; ++t) {
+    double u[4], wv[MC];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u[q] = su[(j0 + t) * CLD + i0 + r0 + q];
+#pragma unroll
+    for (int m = 0; m < MC; ++m) wv[m] = (t <= c0 + m) ? su[(j0 + c0 + m) * CLD + j0 + t] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int m = 0; m < MC; ++m) acc[q][m] += u[q] * wv[m];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < MC; ++m) su[(i0 + c0 + m) * CLD + j0 + r0 + q] = acc[q][m];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < MC; ++m) acc[q][m] = 0.0;
+#pragma unroll 4
+  for (int t = 0; t < S; ++t) {
+    double wv[4], tv[MC];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wv[q] = (t >= r0 + q) ? su[(i0 + t) * CLD + i0 + r0 + q] : 0.0;
+#pragma unroll
+    for (int m = 0; m < MC; ++m) tv[m] = su[(i0 + c0 + m) * CLD + j0 + t];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int m = 0; m < MC; ++m) acc[q][m] += wv[q] * tv[m];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < MC; ++m) su[(j0 + c0 + m) * CLD + i0 + r0 + q] = -acc[q][m];
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
                                                         double* __restrict__ W, int* __restrict__ info) {
-  __shared__ double su[CB * CLD];        // S(r, c) = su[c*CLD + r]
-  __shared__ double sdinv[SB * SB];      // D⁻¹(r, c) = sdinv[c*SB + r]
-  __shared__ double sT[(CB - SB) * SB];  // W phase: T(r, ci) = sT[ci*SB + r]
+  __shared__ double su[CB * CLD];   // S(r, c) = su[c*CLD + r]
+  __shared__ double srinv[CB];      // 1 / U(j, j)
   double* blk = G + (int64_t)k * CB * ld + (int64_t)k * CB;
   double* Wk = W + (int64_t)k * CB * CB;
   const int tid = threadIdx.x;
@@ -53,77 +125,55 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ G, 
   }
   __syncthreads();
 
+  PROF_MARK(0);
   for (int kb = 0; kb < CB / SB; ++kb) {
     const int o = kb * SB;
-    // ---- A: factor + invert the diagonal sub-block (wave 0)
+    PROF_MARK(1 + 4 * kb);
+    // ---- A: factor the diagonal sub-block (wave 0; lanes 16..63 mirror lanes 0..15)
     if (tid < 64) {
-      const int c = tid & 15, g = tid >> 4;
-      double a[4], w[4], rinv[SB];
+      const int c = tid & 15;
+      double a[SB];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = su[(o + c) * CLD + o + g + 4 * q];
+      for (int i = 0; i < SB; ++i) a[i] = su[(o + c) * CLD + o + i];   // S(o+i, o+c); zero below the diagonal
 #pragma unroll
       for (int j = 0; j < SB; ++j) {
-        const int gj = j & 3, qj = j >> 2;
-        const double ajj = __shfl(a[qj], gj * 16 + j);
+        const double ajj = readlane_d(a[j], j);
         if (tid == 0 && !(ajj > 0.0) && *info == 0) *info = k * CB + o + j + 1;
         const double d = sqrt(ajj);
         const double r = 1.0 / d;
-        rinv[j] = r;
-        if (g == gj) a[qj] = (c > j) ? a[qj] * r : ((c == j) ? d : a[qj]);
-        const double ujc = __shfl(a[qj], gj * 16 + c);
+        if (tid == 0) srinv[o + j] = r;
+        a[j] = (c > j) ? a[j] * r : ((c == j) ? d : a[j]);    // row j of U: U(j, c)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const double uji = __shfl(a[qj], gj * 16 + g + 4 * q);
-          if (g + 4 * q > j) a[q] -= uji * ujc;
-        }
+        for (int i = j + 1; i < SB; ++i) a[i] -= readlane_d(a[j], i) * a[j];   // U(j, i) from lane i
       }
+      if (tid < SB) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = (g + 4 * q == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int t = SB - 1; t >= 0; --t) {
-        const int gt = t & 3, qt = t >> 2;
-        if (g == gt) w[qt] *= rinv[t];
-        const double wtc = __shfl(w[qt], gt * 16 + c);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const double dit = __shfl(a[q], g * 16 + t);
-          if (g + 4 * q < t) w[q] -= dit * wtc;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = g + 4 * q;
-        if (r <= c) su[(o + c) * CLD + o + r] = a[q];
-        sdinv[c * SB + r] = w[q];
-        Wk[(int64_t)(o + c) * CB + o + r] = w[q];
+        for (int i = 0; i < SB; ++i)
+          if (i <= c) su[(o + c) * CLD + o + i] = a[i];
       }
     }
     __syncthreads();
+    PROF_MARK(2 + 4 * kb);
     const int np = CB - o - SB;  // columns right of the sub-block
     if (np == 0) break;
-    // ---- B: panel  S(o + t, c) = Σ_{u <= t} D⁻¹(u, t) S(o + u, c)
-    {
-      const int ci = tid & 127, h = tid >> 7, c = o + SB + ci;
-      double X[SB], out[8];
-      if (ci < np) {
+    // ---- B: panel, forward substitution Dᵀ p = x per column (D(u, t) reads are wave-uniform)
+    if (tid < np) {
+      const int c = o + SB + tid;
+      double X[SB];
 #pragma unroll
-        for (int u = 0; u < SB; ++u) X[u] = su[c * CLD + o + u];
+      for (int u = 0; u < SB; ++u) X[u] = su[c * CLD + o + u];
 #pragma unroll
-        for (int tt = 0; tt < 8; ++tt) {
-          const int t = 8 * h + tt;
-          double s = 0.0;
+      for (int t = 0; t < SB; ++t) {
+        double sacc = X[t];
 #pragma unroll
-          for (int u = 0; u < SB; ++u) s += sdinv[t * SB + u] * X[u];
-          out[tt] = s;
-        }
+        for (int u = 0; u < t; ++u) sacc -= su[(o + t) * CLD + o + u] * X[u];
+        X[t] = sacc * srinv[o + t];
       }
-      __syncthreads();
-      if (ci < np) {
 #pragma unroll
-        for (int tt = 0; tt < 8; ++tt) su[c * CLD + o + 8 * h + tt] = out[tt];
-      }
+      for (int u = 0; u < SB; ++u) su[c * CLD + o + u] = X[u];
     }
     __syncthreads();
+    PROF_MARK(3 + 4 * kb);
     // ---- C: trailing update  S(i, c) -= Σ_t U(o + t, i) U(o + t, c),  o+16 <= i <= c
     {
       const int nt = np >> 2, ntiles = nt * (nt + 1) / 2;
@@ -156,48 +206,56 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ G, 
     }
     __syncthreads();
   }
+  PROF_MARK(33);
   // ---- store U
   for (int e = tid; e < CB * CB; e += 256) {
     const int c = e >> 7, r = e & 127;
     if (r <= c) blk[(int64_t)c * ld + r] = su[c * CLD + r];
   }
-  __syncthreads();
-  // ---- W = U⁻¹, block rows from the bottom (the last diagonal block already is D⁻¹ in Wk)
-  for (int ii = CB / SB - 1; ii >= 0; --ii) {
-    const int o = ii * SB, np = CB - o - SB;
-    sdinv[tid] = Wk[(int64_t)(o + (tid >> 4)) * CB + o + (tid & 15)];
-    const int ci = tid & 127, h = tid >> 7, c = o + SB + ci;
-    if (ci < np) {
-      double T[8] = {};
-      for (int t = o + SB; t < CB; ++t) {
-        const double wtc = su[c * CLD + t];   // W(t, c) (rows below o+16 already hold W; 0 for t > c)
+  // ---- diagonal 16 x 16 inverses: wave wv inverts blocks wv and wv + 4 (lane c = column c)
+  {
+    const int wv = tid >> 6, c = tid & 15;
+    double w0[SB], w1[SB];
 #pragma unroll
-        for (int tt = 0; tt < 8; ++tt) T[tt] += su[t * CLD + o + 8 * h + tt] * wtc;
+    for (int h = 0; h < 2; ++h) {
+      const int o = (wv + 4 * h) * SB;
+      double a[SB], w[SB];
+#pragma unroll
+      for (int i = 0; i < SB; ++i) {
+        a[i] = su[(o + c) * CLD + o + i];
+        w[i] = (i == c) ? 1.0 : 0.0;
       }
 #pragma unroll
-      for (int tt = 0; tt < 8; ++tt) sT[ci * SB + 8 * h + tt] = T[tt];
-    }
-    __syncthreads();
-    if (ci < np) {
+      for (int t = SB - 1; t >= 0; --t) {
+        w[t] *= srinv[o + t];
 #pragma unroll
-      for (int tt = 0; tt < 8; ++tt) {
-        const int rr = 8 * h + tt;
-        double s = 0.0;
+        for (int i = 0; i < t; ++i) w[i] -= readlane_d(a[i], t) * w[t];
+      }
 #pragma unroll
-        for (int u = 0; u < SB; ++u) s += sdinv[u * SB + rr] * sT[ci * SB + u];
-        su[c * CLD + o + rr] = -s;
+      for (int i = 0; i < SB; ++i) {
+        if (h == 0) w0[i] = w[i];
+        else w1[i] = w[i];
       }
     }
-    {
-      const int cc = tid >> 4, rr = tid & 15;
-      su[(o + cc) * CLD + o + rr] = sdinv[cc * SB + rr];
+    __syncthreads();   // every wave has read its U blocks
+    if ((tid & 63) < SB) {
+#pragma unroll
+      for (int i = 0; i < SB; ++i) {
+        if (i <= c) su[(wv * SB + c) * CLD + wv * SB + i] = w0[i];
+        if (i <= c) su[((wv + 4) * SB + c) * CLD + (wv + 4) * SB + i] = w1[i];
+      }
     }
     __syncthreads();
   }
+  PROF_MARK(34);
+  chol_inv_double<16>(su, tid);
+  chol_inv_double<32>(su, tid);
+  chol_inv_double<64>(su, tid);
   for (int e = tid; e < CB * CB; e += 256) {
     const int c = e >> 7, r = e & 127;
     Wk[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
   }
+  PROF_MARK(35);
 }
 
 // Forward solve Uᵀ y = b, block step k (all blocks recompute y_k = W_kᵀ b_k;

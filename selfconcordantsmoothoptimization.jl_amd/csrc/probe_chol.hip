@@ -12,6 +12,9 @@
 
 namespace scs {
 __global__ void chol_diag_kernel(double* G, int64_t ld, int k, double* W, int* info);
+#ifdef CHOL_PROF
+extern __device__ long long chol_prof[64];
+#endif
 }
 
 __global__ void spd_fill(double* G, int64_t n) {   // G = I*n + small symmetric noise (upper valid)
@@ -55,6 +58,23 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 64; ++k) hipLaunchKernelGGL(scs::chol_diag_kernel, dim3(1), dim3(256), 0, 0, G, n, k, W, info);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
     printf("n=%ld diag kernel: %.1f us/launch\n", (long)n, ms * 1000 / 64);
+#ifdef CHOL_PROF
+    {
+      long long hp[64];
+      CK(hipMemcpyFromSymbol(hp, HIP_SYMBOL(scs::chol_prof), sizeof(hp)));
+      // s_memtime runs at the 100 MHz constant clock on gfx950
+      printf("phase times (k=0 launch, us): ");
+      for (int kb = 0; kb < 8; ++kb) {
+        const long long a0 = hp[1 + 4 * kb], a1 = hp[2 + 4 * kb], a2 = hp[3 + 4 * kb];
+        const long long a3 = (kb < 7) ? hp[1 + 4 * (kb + 1)] : hp[33];
+        printf("[kb%d A %.2f B %.2f C %.2f] ", kb, (a1 - a0) / 100.0, kb < 7 ? (a2 - a1) / 100.0 : 0.0,
+               kb < 7 ? (a3 - a2) / 100.0 : 0.0);
+      }
+      printf("\n  load %.2f  factor %.2f  storeU+diaginv %.2f  doubling+storeW %.2f  total %.2f\n", (hp[1] - hp[0]) / 100.0,
+             (hp[33] - hp[1]) / 100.0, (hp[34] - hp[33]) / 100.0, (hp[35] - hp[34]) / 100.0,
+             (hp[35] - hp[0]) / 100.0);
+    }
+#endif
     // full factorization + solve
     for (int rep = 0; rep < 2; ++rep) {
       CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));

@@ -38,7 +38,12 @@ constexpr int SPB_MAXSHIFT = 14;
 constexpr int SPB_THREADS = 1024;
 constexpr int SPB_ROWS = 1024;   // rows per workgroup
 
-template <typename VT, int U>
+// One wave works on RW rows at a time (rows r, r + 16, ...): the RW rows' pointer
+// pairs, then all RW*U (index, value) loads are issued before any use, which
+// keeps RW*U*64 loads per wave in flight (the kernel runs at one workgroup per
+// CU because of the 128 KiB LDS slice).  Per row the summation order is the
+// same as one row at a time (lane-ascending p, then the wave butterfly).
+template <typename VT, int U, int RW>
 __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
                                                                const uint16_t* __restrict__ lidx,
                                                                const VT* __restrict__ val,
@@ -46,6 +51,7 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
                                                                int64_t ncols, int shift, double* __restrict__ out,
                                                                int64_t ldo) {
   __shared__ double xs[1 << SPB_MAXSHIFT];
+  constexpr int NW = SPB_THREADS / 64;
   const int b = blockIdx.y;
   const int64_t c0 = (int64_t)b << shift;
   const int nb = (int)min((int64_t)1 << shift, ncols - c0);
@@ -54,36 +60,63 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t* pb = ptr + (int64_t)b * nrows;
   const int64_t r1 = min(nrows, (int64_t)(blockIdx.x + 1) * SPB_ROWS);
-  for (int64_t r = (int64_t)blockIdx.x * SPB_ROWS + wv; r < r1; r += SPB_THREADS / 64) {
-    const int64_t p0 = pb[r], p1 = pb[r + 1];
-    double acc = 0.0;
-    int64_t p = p0 + lane;
-    for (; p + 64 * (U - 1) < p1; p += 64 * U) {
-      int id[U];
-      double v[U];
+  for (int64_t rb = (int64_t)blockIdx.x * SPB_ROWS + wv; rb < r1; rb += NW * RW) {
+    int64_t p0[RW], p1[RW], p[RW];
+    double acc[RW];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        id[u] = lidx[p + 64 * u];
-        v[u] = (double)val[p + 64 * u];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc += v[u] * xs[id[u]];
+    for (int j = 0; j < RW; ++j) {
+      const int64_t r = rb + (int64_t)j * NW;
+      p0[j] = (r < r1) ? pb[r] : 0;
+      p1[j] = (r < r1) ? pb[r + 1] : 0;
+      p[j] = p0[j] + lane;
+      acc[j] = 0.0;
     }
-    if (p0 < p1 && p - lane < p1) {
-      int id[U];
-      double v[U];
+    // full rounds while every row of the group still has one
+    bool more = true;
+    while (more) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t q = min(p + 64 * u, p1 - 1);
-        id[u] = lidx[q];
-        v[u] = (double)val[q];
+      for (int j = 0; j < RW; ++j) more = more && (p[j] + 64 * (U - 1) < p1[j]);
+      if (!more) break;
+      int id[RW][U];
+      double v[RW][U];
+#pragma unroll
+      for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          id[j][u] = lidx[p[j] + 64 * u];
+          v[j][u] = (double)val[p[j] + 64 * u];
+        }
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[j] += v[j][u] * xs[id[j][u]];
+        p[j] += 64 * U;
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (p + 64 * u < p1) acc += v[u] * xs[id[u]];
     }
-    acc = wave_sum(acc);
-    if (lane == 0) out[(int64_t)b * ldo + r] = acc;
+    // remaining rounds, row by row (clamped addresses, masked terms)
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      while (p0[j] < p1[j] && p[j] - lane < p1[j]) {
+        int id[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t q = min(p[j] + 64 * u, p1[j] - 1);
+          id[u] = lidx[q];
+          v[u] = (double)val[q];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (p[j] + 64 * u < p1[j]) acc[j] += v[u] * xs[id[u]];
+        p[j] += 64 * U;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      const double a = wave_sum(acc[j]);
+      const int64_t r = rb + (int64_t)j * NW;
+      if (lane == 0 && r < r1) out[(int64_t)b * ldo + r] = a;
+    }
   }
 }
 
@@ -102,17 +135,17 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
   const int64_t avg = nnz / (nrows * nblk);
   if (f32) {
     if (avg <= 64 * 4)
-      hipLaunchKernelGGL((spmv_blk_kernel<float, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
+      hipLaunchKernelGGL((spmv_blk_kernel<float, 4, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
                          x, nrows, ncols, shift, out, ldo);
     else
-      hipLaunchKernelGGL((spmv_blk_kernel<float, 16>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
+      hipLaunchKernelGGL((spmv_blk_kernel<float, 16, 1>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
                          x, nrows, ncols, shift, out, ldo);
   } else {
     if (avg <= 64 * 4)
-      hipLaunchKernelGGL((spmv_blk_kernel<double, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+      hipLaunchKernelGGL((spmv_blk_kernel<double, 4, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
                          (const double*)val, x, nrows, ncols, shift, out, ldo);
     else
-      hipLaunchKernelGGL((spmv_blk_kernel<double, 16>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+      hipLaunchKernelGGL((spmv_blk_kernel<double, 16, 1>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
                          (const double*)val, x, nrows, ncols, shift, out, ldo);
   }
   return hipGetLastError();
