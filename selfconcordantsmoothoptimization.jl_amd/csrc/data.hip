@@ -105,6 +105,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(int loss, int ggn, int fl
       if (flags & EPI_GRAD) gout[n] = 0.0;
       if (flags & EPI_HESS) hout[n] = 0.0;
       if (flags & EPI_GGN) { wout[n] = 0.0; vout[n] = 0.0; }
+      if (flags & EPI_SQR) { gout[n] = 0.0; hout[n] = 0.0; }
       continue;
     }
     const double yn = y[n];
@@ -133,17 +134,25 @@ __global__ __launch_bounds__(256) void epilogue_kernel(int loss, int ggn, int fl
       if (flags & EPI_HESS) hout[n] = c;
     }
     if (flags & EPI_GGN) {
+      double s, r, q;
       if (ggn == SCS_GGN_SIGMOID_CE) {
         const double e = exp(-z);
         const double yh = 1.0 / (1.0 + e);
-        const double s = e / ((1.0 + e) * (1.0 + e));
-        const double r = -c * (yn / yh - (1.0 - yn) / (1.0 - yh));
-        const double q = c * (yn / (yh * yh) + (1.0 - yn) / ((1.0 - yh) * (1.0 - yh)));
+        s = e / ((1.0 + e) * (1.0 + e));
+        r = -c * (yn / yh - (1.0 - yn) / (1.0 - yh));
+        q = c * (yn / (yh * yh) + (1.0 - yn) / ((1.0 - yh) * (1.0 - yh)));
+      } else {  // SCS_GGN_LINEAR_LS
+        s = 1.0;
+        r = (z - yn) * c;
+        q = c;
+      }
+      if (flags & EPI_SQR) {   // sample-space branch: the factors themselves
+        gout[n] = s;
+        hout[n] = q;
+        wout[n] = r;
+      } else {
         wout[n] = s * s * q;
         vout[n] = s * r;
-      } else {  // SCS_GGN_LINEAR_LS
-        wout[n] = 1.0 * 1.0 * c;
-        vout[n] = 1.0 * ((z - yn) * c);
       }
     }
   }
@@ -168,6 +177,30 @@ __global__ __launch_bounds__(1024) void sum_partials_kernel(const double* __rest
   for (int i = threadIdx.x; i < n; i += 1024) acc += part[i];
   const double s = block_sum<1024>(acc, sh);
   if (threadIdx.x == 0) out[0] = s;
+}
+
+// At (n-major: At[n*ldt + f] = A[f*lda + n]) for the sample-space Gram A diag(h) Aᵀ; zero padded
+__global__ void transpose_kernel(const double* __restrict__ A, int64_t lda, int64_t N, int64_t m, double* __restrict__ At,
+                                 int64_t ldt, int64_t nt) {
+  __shared__ double tile[32][33];
+  const int64_t f0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  for (int j = ty; j < 32; j += 8) {
+    const int64_t f = f0 + j, n = n0 + tx;
+    tile[j][tx] = (f < m && n < N) ? A[f * lda + n] : 0.0;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int64_t n = n0 + j, f = f0 + tx;
+    if (n < nt && f < ldt) At[n * ldt + f] = tile[tx][j];
+  }
+}
+
+hipError_t launch_transpose(const double* A, int64_t lda, int64_t N, int64_t m, double* At, int64_t ldt, int64_t nt,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)ceil_div(ldt, 32), (unsigned)ceil_div(nt, 32)), dim3(256), 0,
+                     st, A, lda, N, m, At, ldt, nt);
+  return hipGetLastError();
 }
 
 hipError_t launch_sum_partials(const double* part, int n, double* out, hipStream_t st) {

@@ -86,7 +86,8 @@ hipError_t launch_gemv_n(const double* A, int64_t lda, int64_t Npad, int64_t m, 
                          double* part, int64_t ldo, hipStream_t st);
 // loss epilogue over samples: sums the z-partials, writes z / coefficient vectors and
 // per-block loss partials.  Returns the number of value partials written.
-enum { EPI_Z = 1, EPI_VAL = 2, EPI_GRAD = 4, EPI_HESS = 8, EPI_GGN = 16 };
+// EPI_SQR (with EPI_GGN): write s -> g, q -> h, r -> w instead of s²q / s·r (GGN sample-space branch)
+enum { EPI_Z = 1, EPI_VAL = 2, EPI_GRAD = 4, EPI_HESS = 8, EPI_GGN = 16, EPI_SQR = 32 };
 int epilogue_blocks(int64_t Npad);
 hipError_t launch_epilogue(int loss, int ggn, int flags, const double* zpart, int nsplit, int64_t ldz,
                            const double* y, int64_t N, int64_t Npad, double c, double* z, double* g, double* h,
@@ -100,6 +101,18 @@ hipError_t launch_gemv_t(const double* A, int64_t lda, int64_t Npad, int64_t m, 
 // out[j] = Σ_chunk part[chunk][j] (+ lam*add[j] if add)
 hipError_t launch_gemv_t_finalize(const double* part, int nchunk, int64_t mpad, int64_t m, double* out,
                                   hipStream_t st);
+hipError_t launch_transpose(const double* A, int64_t lda, int64_t N, int64_t m, double* At, int64_t ldt, int64_t nt,
+                            hipStream_t st);
+// GGN sample-space branch (vec.hip)
+hipError_t launch_ggn_sample_prep(const double* Hr, const double* gr, double lam, int64_t m, int64_t mpad,
+                                  double* hvec, double* hg, hipStream_t st);
+hipError_t launch_ggn_sample_assemble(const double* P, int64_t ldp, const double* s, const double* q,
+                                      const double* r, const double* u, const double* kNN, int64_t N, double* M,
+                                      double* b, hipStream_t st);
+hipError_t launch_ggn_sample_scale(const double* s, const double* B, int64_t N, int64_t Npad, double* v,
+                                   hipStream_t st);
+hipError_t launch_ggn_sample_direction(const double* hvec, const double* t, const double* hg, const double* B,
+                                       int64_t N, int64_t m, double* d, hipStream_t st);
 // synthetic data
 hipError_t launch_gen_A(double* A, int64_t lda, int64_t N, int64_t m, int64_t row0, uint64_t seed, double scale,
                         hipStream_t st);

@@ -138,6 +138,12 @@ struct scs_ctx {
   int2* trilist = nullptr;  // row-major lower tiles
   int* cinfo = nullptr;
   rocblas_handle blas = nullptr;
+  // GGN sample-space branch (N + 1 <= m): Aᵀ copy, sample Gram, (N+1)² system
+  double *At = nullptr, *Ps = nullptr, *Ms = nullptr, *bS = nullptr, *uN = nullptr, *hvec = nullptr, *hg = nullptr;
+  int64_t NpS = 0;
+  int2* stiles = nullptr;
+  int nstiles = 0;
+  rocblas_int *ipivS = nullptr, *dinfoS = nullptr;
   rocblas_int* dinfo = nullptr;
   rocblas_int* ipiv = nullptr;
   bool lu_fallback_used = false;
@@ -637,6 +643,12 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
 // pivoting (the reference's `\`, prox-N-SCORE.jl:204) from the saved copy when
 // a pivot is not positive (e.g. the indefinite Q of a CE loss on ±1 labels,
 // test/test_algs.jl:10).
+void ensure_blas(scs_ctx* c) {
+  if (c->blas) return;
+  RCK(rocblas_create_handle(&c->blas));
+  RCK(rocblas_set_stream(c->blas, c->st));
+}
+
 void solve_system(scs_ctx* c, double* rhs) {
   const int64_t m = c->m, ld = c->mpad;
   hipEvent_t e0;
@@ -651,10 +663,7 @@ void solve_system(scs_ctx* c, double* rhs) {
     HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, c->st));
     c->lu_fallback_used = false;
   } else {
-    if (!c->blas) {
-      RCK(rocblas_create_handle(&c->blas));
-      RCK(rocblas_set_stream(c->blas, c->st));
-    }
+    ensure_blas(c);
     HCK(launch_symmetrize(c->Gc, ld, m, c->st));
     RCK(rocsolver_dgetrf(c->blas, (rocblas_int)m, (rocblas_int)m, c->Gc, (rocblas_int)ld, c->ipiv, c->dinfo));
     HCK(hipMemcpyAsync(&info, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
@@ -717,10 +726,68 @@ double step_size_newton(scs_ctx* c, int64_t iter, bool* needs_ls) {
   fail(c, SCS_ERR_REF, "Please, choose ss_type in [1, 2, 3].");
 }
 
+// ggn_score_step's sample-space branch (prox-GGN-SCORE.jl:124-127, N + 1 <= m) -> c->d
+void ggn_sample_direction(scs_ctx* c, const double* xh) {
+  const int64_t N = c->N, m = c->m;
+  if (c->nranks > 1)
+    fail(c, SCS_ERR_ARG, "ProxGGNSCORE sample-space branch (N + 1 <= m) runs on one rank (its system is N x N)");
+  require_dense(c, "ProxGGNSCORE");
+  ensure_blas(c);
+  if (!c->At) {
+    c->NpS = round_up(N, 128);
+    c->At = dalloc<double>(c, (size_t)c->NpS * c->mpad);
+    HCK(launch_transpose(c->A, c->Npad, N, m, c->At, c->mpad, c->NpS, c->st));
+    c->Ps = dalloc<double>(c, (size_t)c->NpS * c->NpS);
+    c->Ms = dalloc<double>(c, (size_t)(N + 1) * (N + 1));
+    c->bS = dalloc<double>(c, N + 1);
+    c->uN = dalloc<double>(c, c->Npad);
+    c->hvec = dalloc<double>(c, c->mpad);
+    c->hg = dalloc<double>(c, c->mpad);
+    c->ipivS = dalloc<rocblas_int>(c, N + 1);
+    c->dinfoS = dalloc<rocblas_int>(c, 1);
+    const int nb = (int)(c->NpS / 128);
+    std::vector<int2> tl((size_t)nb * (nb + 1) / 2);
+    int nt = 0;
+    gram_tile_list(nb, tl.data(), &nt);
+    c->stiles = dalloc<int2>(c, nt);
+    HCK(hipMemcpyAsync(c->stiles, tl.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->st));
+    c->nstiles = nt;
+  }
+  // s, q, r (prox-GGN-SCORE.jl:44-56) -> gN, hN, wN
+  forward(c, xh, c->x, EPI_GGN | EPI_SQR);
+  HCK(launch_ggn_sample_prep(c->Hr, c->gr, c->lam, m, c->mpad, c->hvec, c->hg, c->st));
+  hipEvent_t e0;
+  tbegin(c, T_GRAM, &e0);
+  HCK(gram_launch_gen(c->At, c->mpad, c->At, c->mpad, c->hvec, 0, c->mpad, c->stiles, c->nstiles, c->Ps, c->NpS,
+                      /*GRAM_UPPER*/ 4, c->st));
+  tend(c, T_GRAM, e0);
+  HCK(launch_symmetrize(c->Ps, c->NpS, N, c->st));
+  const int ns = matvec_n(c, c->hg, c->nsplit);   // u = A (h∘λgr)
+  HCK(launch_epilogue(SCS_LOSS_LEAST_SQUARES, SCS_GGN_NONE, EPI_Z, c->zpart, ns, c->Npad, c->y, N, c->Npad, 1.0,
+                      c->uN, nullptr, nullptr, nullptr, nullptr, c->valpart, c->st));
+  HCK(launch_ggn_sample_assemble(c->Ps, c->NpS, c->gN, c->hN, c->wN, c->uN, nullptr, N, c->Ms, c->bS, c->st));
+  tbegin(c, T_SOLVE, &e0);
+  const rocblas_int n1 = (rocblas_int)(N + 1);
+  RCK(rocsolver_dgetrf(c->blas, n1, n1, c->Ms, n1, c->ipivS, c->dinfoS));
+  int info = 0;
+  HCK(hipMemcpyAsync(&info, c->dinfoS, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
+  RCK(rocsolver_dgetrs(c->blas, rocblas_operation_none, n1, 1, c->Ms, n1, c->ipivS, c->bS, n1));
+  tend(c, T_SOLVE, e0);
+  HCK(launch_ggn_sample_scale(c->gN, c->bS, N, c->Npad, c->vN, c->st));
+  gemv_t_local(c, c->vN, c->gtmp);   // Aᵀ(s∘B)
+  HCK(launch_ggn_sample_direction(c->hvec, c->gtmp, c->hg, c->bS, N, m, c->d, c->st));
+}
+
 // ProxNSCORE / ProxGGNSCORE step
 void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, double* dx, double* pri) {
   const int64_t m = c->m;
   HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
+  const bool sample_space = (c->method == SCS_PROX_GGNSCORE) && (c->Nglob + 1 <= m) && c->ggn != SCS_GGN_NONE;
+  if (sample_space) {
+    ggn_sample_direction(c, xh);
+  } else {
   ensure_gram(c);
   if (c->method == SCS_PROX_NSCORE) {
     // H = hess_fx, ∇q = grad_fx + λ gr  (prox-N-SCORE.jl:183-204)
@@ -749,6 +816,7 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
   HCK(launch_diag_add(c->G, c->mpad, m, c->lam, c->Hr, c->st));
   solve_system(c, c->gq);
   HCK(launch_neg(c->gq, m, c->d, c->st));  // d = -sol
+  }
   bool ls = false;
   double step = step_size_newton(c, iter, &ls);
   if (ls) step = line_search(c, xh, c->x, c->d);
@@ -943,6 +1011,12 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->Gc);
   dfree_t(c, c->tiles);
   dfree_t(c, c->utiles);
+  for (double** v : {&c->At, &c->Ps, &c->Ms, &c->bS, &c->uN, &c->hvec, &c->hg}) dfree_t(c, *v);
+  dfree_t(c, c->stiles);
+  dfree_t(c, c->ipivS);
+  dfree_t(c, c->dinfoS);
+  c->NpS = 0;
+  c->nstiles = 0;
   dfree_t(c, c->gwork);
   dfree_t(c, c->gcomb);
   dfree_t(c, c->gpart);
@@ -1332,9 +1406,9 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
     if (method < SCS_PROX_NSCORE || method > SCS_PROX_LQNSCORE) fail(c, SCS_ERR_ARG, "unknown method %d", method);
     if (method == SCS_PROX_GGNSCORE && (c->generic || c->loss == SCS_LOSS_QUADRATIC))
       fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs a data problem with an out_fn (GGN kind)");
-    if (method == SCS_PROX_GGNSCORE && c->N + 1 <= c->m)
-      fail(c, SCS_ERR_ARG, "ProxGGNSCORE sample-space branch (N+1 <= m, prox-GGN-SCORE.jl:124-127) is not "
-                           "implemented on the device yet");
+    if (method == SCS_PROX_GGNSCORE && c->Nglob + 1 <= c->m && c->nranks > 1)
+      fail(c, SCS_ERR_ARG, "ProxGGNSCORE sample-space branch (N+1 <= m, prox-GGN-SCORE.jl:124-127) runs on one "
+                           "rank (its system is N x N)");
     c->method = method;
     c->ss_type = ss_type;
     c->use_prox = use_prox;

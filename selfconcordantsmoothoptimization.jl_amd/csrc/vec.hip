@@ -17,6 +17,7 @@
 namespace scs {
 
 constexpr int VB = 1024;  // single-workgroup kernels: 16 waves
+static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 // ---------------------------------------------------------------------------
 // Smoothers  (phuber-smooth.jl, exponential-smooth.jl)
@@ -461,6 +462,76 @@ __global__ __launch_bounds__(VB) void lbfgs_update_kernel(const double* __restri
   if (threadIdx.x == 0) { scal[0] = dg; scal[1] = gg; }
 }
 
+// ---------------------------------------------------------------------------
+// ProxGGNSCORE sample-space branch (ggn_score_step, prox-GGN-SCORE.jl:124-127,
+// taken when N + 1 <= m):  Jt = [Jᵀ  λgr] (m x (N+1)), J = diag(s) A,
+//   M = I + Q̃ (Jtᵀ H⁻¹ Jt),  Q̃ = diag(q, 0),   M B = [r; 1],   d = -H⁻¹ Jt B.
+// With P = A diag(h) Aᵀ (h = 1/Hr, the MFMA Gram on Aᵀ) and u = A (h∘λgr):
+//   M[i][j] = δij + q_i s_i s_j P_ij,  M[i][N] = q_i s_i u_i,  M[N][·] = e_N.
+// ---------------------------------------------------------------------------
+__global__ void ggn_sample_prep_kernel(const double* __restrict__ Hr, const double* __restrict__ gr, double lam,
+                                       int64_t m, int64_t mpad, double* __restrict__ hvec, double* __restrict__ hg) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f >= mpad) return;
+  const double h = (f < m) ? 1.0 / Hr[f] : 0.0;   // Hdiag_inv = 1 ./ Hr_diag (prox-GGN-SCORE.jl:64)
+  hvec[f] = h;
+  hg[f] = (f < m) ? h * (lam * gr[f]) : 0.0;
+}
+
+__global__ void ggn_sample_assemble_kernel(const double* __restrict__ P, int64_t ldp, const double* __restrict__ s,
+                                           const double* __restrict__ q, const double* __restrict__ r,
+                                           const double* __restrict__ u, const double* __restrict__ kNN, int64_t N,
+                                           double* __restrict__ M, double* __restrict__ b) {
+  const int64_t ld = N + 1;
+  const int64_t j = blockIdx.y;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ld; i += (int64_t)gridDim.x * blockDim.x) {
+    double v;
+    if (i == N) v = (j == N) ? 1.0 : 0.0;
+    else if (j < N) v = (i == j ? 1.0 : 0.0) + q[i] * (s[i] * s[j] * P[j * ldp + i]);
+    else v = q[i] * (s[i] * u[i]);
+    M[j * ld + i] = v;
+    if (j == 0) b[i] = (i < N) ? r[i] : 1.0;
+  }
+  (void)kNN;   // Q̃[N][N] = 0: the λgr·H⁻¹·λgr entry only reaches M through a zero row
+}
+
+__global__ void ggn_sample_scale_kernel(const double* __restrict__ s, const double* __restrict__ B, int64_t N,
+                                        int64_t Npad, double* __restrict__ v) {
+  const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (n < Npad) v[n] = (n < N) ? s[n] * B[n] : 0.0;
+}
+
+// d = -(H⁻¹ (Jᵀ... )): d_f = -h_f (t_f + λgr_f B_N), t = Aᵀ(s∘B)
+__global__ void ggn_sample_direction_kernel(const double* __restrict__ hvec, const double* __restrict__ t,
+                                            const double* __restrict__ hg, const double* __restrict__ B, int64_t N,
+                                            int64_t m, double* __restrict__ d) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f < m) d[f] = -(hvec[f] * t[f] + hg[f] * B[N]);
+}
+
+hipError_t launch_ggn_sample_prep(const double* Hr, const double* gr, double lam, int64_t m, int64_t mpad,
+                                  double* hvec, double* hg, hipStream_t st) {
+  hipLaunchKernelGGL(ggn_sample_prep_kernel, dim3(nblk(mpad, 256)), dim3(256), 0, st, Hr, gr, lam, m, mpad, hvec, hg);
+  return hipGetLastError();
+}
+hipError_t launch_ggn_sample_assemble(const double* P, int64_t ldp, const double* s, const double* q,
+                                      const double* r, const double* u, const double* kNN, int64_t N, double* M,
+                                      double* b, hipStream_t st) {
+  hipLaunchKernelGGL(ggn_sample_assemble_kernel, dim3((unsigned)ceil_div(N + 1, 256), (unsigned)(N + 1)), dim3(256),
+                     0, st, P, ldp, s, q, r, u, kNN, N, M, b);
+  return hipGetLastError();
+}
+hipError_t launch_ggn_sample_scale(const double* s, const double* B, int64_t N, int64_t Npad, double* v,
+                                   hipStream_t st) {
+  hipLaunchKernelGGL(ggn_sample_scale_kernel, dim3(nblk(Npad, 256)), dim3(256), 0, st, s, B, N, Npad, v);
+  return hipGetLastError();
+}
+hipError_t launch_ggn_sample_direction(const double* hvec, const double* t, const double* hg, const double* B,
+                                       int64_t N, int64_t m, double* d, hipStream_t st) {
+  hipLaunchKernelGGL(ggn_sample_direction_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, hvec, t, hg, B, N, m, d);
+  return hipGetLastError();
+}
+
 // G[i,i] += λ·Hr[i]   (H + λ.*Diagonal(Hr), prox-N-SCORE.jl:177,204; prox-GGN-SCORE.jl:129)
 __global__ void diag_add_kernel(double* __restrict__ G, int64_t ldg, int64_t m, double lam,
                                 const double* __restrict__ Hr) {
@@ -529,7 +600,6 @@ __global__ __launch_bounds__(VB) void rosen_kernel(const double* __restrict__ x,
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,
                            const double* wel, double* gr, double* Hr, hipStream_t st) {

@@ -361,3 +361,27 @@ def test_lqn_large_m_multiblock_two_loop():
     assert len(sol.obj) == len(osol.obj)
     np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
     np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("loss", ["logistic_ce", "least_squares"])
+def test_ggn_sample_space_branch(loss):
+    """ggn_score_step's N + 1 <= m branch (prox-GGN-SCORE.jl:124-127): the (N+1) x (N+1) system
+    I + Q̃ Jtᵀ H⁻¹ Jt on the device (sample Gram on Aᵀ by MFMA, LU) against the oracle's QR."""
+    N, m = 300, 1000
+    x0 = np.random.default_rng(31).standard_normal(m) * 0.3
+    if loss == "logistic_ce":
+        f, out, kind = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N), 1
+        of = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+        reg, lam = "l1", 1e-3
+    else:
+        f, out, kind = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N), 3
+        of = O.Loss("least_squares", 1.0 / N, ggn="linear_ls")
+        reg, lam = "l2", 1e-3
+    p = scsopt.Problem.synthetic(N, m, x0, f, lam, kind=kind, seed=33, out_fn=out)
+    A, y = p.get_data()
+    om = O.Problem(A, y, x0, of, lam)
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, reg, scsopt.PHuberSmootherL1L2(1.0), max_epoch=8, verbose=0)
+    osol = O.iterate(O.ProxGGNSCORE(), om, reg, O.PHuberSmootherL1L2(1.0), max_epoch=8)
+    assert len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
