@@ -60,6 +60,15 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 }
 
 __host__ __device__ __forceinline__ int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---- device layout of A: panel-blocked ("tiled") ------------------------------
+// Block (panel p = j / 128, stage s = n / 16) holds [128 features][16 samples]
+// contiguously (16 KiB); blocks of one panel follow each other in stage order.
+// S = N_pad / 16 stages.  Every 16-sample K step of the Gram then reads two
+// contiguous 16 KiB blocks instead of 256 scattered 128-B column pieces.
+__host__ __device__ __forceinline__ int64_t tiled_off(int64_t S, int64_t n, int64_t j) {
+  return (((j >> 7) * S + (n >> 4)) * 128 + (j & 127)) * 16 + (n & 15);
+}
 __host__ __device__ __forceinline__ int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 
 }  // namespace scs

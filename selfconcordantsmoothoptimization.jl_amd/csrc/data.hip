@@ -7,7 +7,8 @@
 //                    GGN (w = s²q, v = s·r) of the selected loss kind)
 //   Aᵀ*v            gemv_t   (HBM-bound: reads A once; v staged in LDS)
 //
-// A is column-major with lda = Npad (Npad % 16 == 0, zero rows beyond N).
+// A is panel-blocked (common.h tiled_off; S = Npad / 16 stages, m_pad % 128 == 0,
+// zero rows beyond N and zero columns beyond m).
 #include "common.h"
 #include "kernels.h"
 
@@ -22,59 +23,61 @@ constexpr int GN_ROWS = 512;
 int gemv_n_splits(int64_t Npad, int64_t m) {
   const int64_t rb = ceil_div(Npad, GN_ROWS);
   int64_t s = ceil_div(2048, rb);
-  const int64_t smax = ceil_div(m, 256);
+  const int64_t smax = ceil_div(m, 128);   // splits are whole panels
   if (s > smax) s = smax;
   if (s < 1) s = 1;
   return (int)s;
 }
 
-__global__ __launch_bounds__(256) void gemv_n_kernel(const double* __restrict__ A, int64_t lda, int64_t Npad,
-                                                     int64_t m, const double* __restrict__ x, int64_t cps,
+// thread = 2 consecutive samples (one v2d of a block row); a wave covers 8
+// stages, so each load instruction reads 8 full 128-B lines.  Columns [c0, c1)
+// are whole panels; x must be zero beyond m (callers pass m_pad-sized x).
+__global__ __launch_bounds__(256) void gemv_n_kernel(const double* __restrict__ A, int64_t S, int64_t Npad,
+                                                     int64_t mpad, const double* __restrict__ x, int64_t cps,
                                                      double* __restrict__ part, int64_t ldo) {
   const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
   if (r >= Npad) return;
   const int64_t c0 = (int64_t)blockIdx.y * cps;
-  const int64_t c1 = (c0 + cps < m) ? c0 + cps : m;
+  const int64_t c1 = (c0 + cps < mpad) ? c0 + cps : mpad;
   v2d acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
-  const double* p = A + c0 * lda + r;
-  int64_t j = c0;
-  for (; j + 8 <= c1; j += 8) {
-    const v2d a0 = *(const v2d*)(p);
-    const v2d a1 = *(const v2d*)(p + lda);
-    const v2d a2 = *(const v2d*)(p + 2 * lda);
-    const v2d a3 = *(const v2d*)(p + 3 * lda);
-    const v2d a4 = *(const v2d*)(p + 4 * lda);
-    const v2d a5 = *(const v2d*)(p + 5 * lda);
-    const v2d a6 = *(const v2d*)(p + 6 * lda);
-    const v2d a7 = *(const v2d*)(p + 7 * lda);
-    acc0 += a0 * x[j];
-    acc1 += a1 * x[j + 1];
-    acc0 += a2 * x[j + 2];
-    acc1 += a3 * x[j + 3];
-    acc0 += a4 * x[j + 4];
-    acc1 += a5 * x[j + 5];
-    acc0 += a6 * x[j + 6];
-    acc1 += a7 * x[j + 7];
-    p += 8 * lda;
-  }
-  for (; j < c1; ++j) {
-    acc0 += *(const v2d*)(p) * x[j];
-    p += lda;
+  for (int64_t pc = c0; pc < c1; pc += 128) {
+    const double* p = A + tiled_off(S, r, pc);
+    const double* xp = x + pc;
+#pragma unroll 4
+    for (int f = 0; f < 128; f += 8) {
+      const v2d a0 = *(const v2d*)(p + 16 * (f + 0));
+      const v2d a1 = *(const v2d*)(p + 16 * (f + 1));
+      const v2d a2 = *(const v2d*)(p + 16 * (f + 2));
+      const v2d a3 = *(const v2d*)(p + 16 * (f + 3));
+      const v2d a4 = *(const v2d*)(p + 16 * (f + 4));
+      const v2d a5 = *(const v2d*)(p + 16 * (f + 5));
+      const v2d a6 = *(const v2d*)(p + 16 * (f + 6));
+      const v2d a7 = *(const v2d*)(p + 16 * (f + 7));
+      acc0 += a0 * xp[f];
+      acc1 += a1 * xp[f + 1];
+      acc0 += a2 * xp[f + 2];
+      acc1 += a3 * xp[f + 3];
+      acc0 += a4 * xp[f + 4];
+      acc1 += a5 * xp[f + 5];
+      acc0 += a6 * xp[f + 6];
+      acc1 += a7 * xp[f + 7];
+    }
   }
   *(v2d*)(part + (int64_t)blockIdx.y * ldo + r) = acc0 + acc1;
 }
 
-hipError_t launch_gemv_n(const double* A, int64_t lda, int64_t Npad, int64_t m, const double* x, int nsplit,
+hipError_t launch_gemv_n(const double* A, int64_t S, int64_t Npad, int64_t mpad, const double* x, int nsplit,
                          double* part, int64_t ldo, hipStream_t st) {
-  int64_t cps = ceil_div(m, nsplit);
-  const int ns = (int)ceil_div(m, cps);
+  const int64_t np = mpad / 128;
+  const int64_t pps = ceil_div(np, nsplit);   // panels per split
+  const int ns = (int)ceil_div(np, pps);
   // unused trailing splits (if any) are zeroed so the epilogue can sum nsplit slices
   if (ns < nsplit) {
     hipError_t e = hipMemsetAsync(part + (int64_t)ns * ldo, 0, sizeof(double) * ldo * (nsplit - ns), st);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(gemv_n_kernel, dim3((unsigned)ceil_div(Npad, GN_ROWS), (unsigned)ns), dim3(256), 0, st, A, lda,
-                     Npad, m, x, cps, part, ldo);
+  hipLaunchKernelGGL(gemv_n_kernel, dim3((unsigned)ceil_div(Npad, GN_ROWS), (unsigned)ns), dim3(256), 0, st, A, S,
+                     Npad, mpad, x, pps * 128, part, ldo);
   return hipGetLastError();
 }
 
@@ -180,14 +183,15 @@ __global__ __launch_bounds__(1024) void sum_partials_kernel(const double* __rest
 }
 
 // At (n-major: At[n*ldt + f] = A[f*lda + n]) for the sample-space Gram A diag(h) Aᵀ; zero padded
-__global__ void transpose_kernel(const double* __restrict__ A, int64_t lda, int64_t N, int64_t m, double* __restrict__ At,
-                                 int64_t ldt, int64_t nt) {
+__global__ void transpose_kernel(const double* __restrict__ A, int64_t Npad, int64_t N, int64_t m,
+                                 double* __restrict__ At, int64_t ldt, int64_t nt) {
+  const int64_t S = Npad / 16;
   __shared__ double tile[32][33];
   const int64_t f0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
   for (int j = ty; j < 32; j += 8) {
     const int64_t f = f0 + j, n = n0 + tx;
-    tile[j][tx] = (f < m && n < N) ? A[f * lda + n] : 0.0;
+    tile[j][tx] = (f < m && n < N) ? A[tiled_off(S, n, f)] : 0.0;
   }
   __syncthreads();
   for (int j = ty; j < 32; j += 8) {
@@ -196,10 +200,29 @@ __global__ void transpose_kernel(const double* __restrict__ A, int64_t lda, int6
   }
 }
 
-hipError_t launch_transpose(const double* A, int64_t lda, int64_t N, int64_t m, double* At, int64_t ldt, int64_t nt,
-                            hipStream_t st) {
+hipError_t launch_transpose(const double* A, int64_t Npad, int64_t N, int64_t m, double* At, int64_t ldt,
+                            int64_t nt, hipStream_t st) {
   hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)ceil_div(ldt, 32), (unsigned)ceil_div(nt, 32)), dim3(256), 0,
-                     st, A, lda, N, m, At, ldt, nt);
+                     st, A, Npad, N, m, At, ldt, nt);
+  return hipGetLastError();
+}
+
+// panel p of A: column-major buffer C (Npad x 128, ld Npad) <-> the tiled blocks of panel p
+__global__ void retile_kernel(double* __restrict__ C, double* __restrict__ A, int64_t Npad, int64_t p, int to_tiled) {
+  const int64_t S = Npad / 16;
+  double* blk = A + p * S * 128 * 16;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < Npad * 128;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    // e walks the tiled panel contiguously: e = (s*128 + f)*16 + ks
+    const int64_t ks = e & 15, f = (e >> 4) & 127, s = e >> 11;
+    const int64_t n = s * 16 + ks;
+    if (to_tiled) blk[e] = C[f * Npad + n];
+    else C[f * Npad + n] = blk[e];
+  }
+}
+
+hipError_t launch_retile(double* C, double* A, int64_t Npad, int64_t p, int to_tiled, hipStream_t st) {
+  hipLaunchKernelGGL(retile_kernel, dim3(1024), dim3(256), 0, st, C, A, Npad, p, to_tiled);
   return hipGetLastError();
 }
 
@@ -216,7 +239,7 @@ constexpr int GT_ROWS = 4096;
 
 int gemv_t_chunks(int64_t Npad) { return (int)ceil_div(Npad, GT_ROWS); }
 
-__global__ __launch_bounds__(256) void gemv_t_kernel(const double* __restrict__ A, int64_t lda, int64_t Npad,
+__global__ __launch_bounds__(256) void gemv_t_kernel(const double* __restrict__ A, int64_t S, int64_t Npad,
                                                      int64_t m, const double* __restrict__ v,
                                                      double* __restrict__ part, int64_t ldp) {
   __shared__ v2d vs[GT_ROWS / 2];
@@ -231,12 +254,14 @@ __global__ __launch_bounds__(256) void gemv_t_kernel(const double* __restrict__ 
     const int64_t j = jbase + cc;
     if (j >= m) break;
     v2d acc[4] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-    const double* p0 = A + j * lda + r0;
+    // columns j..j+3 share a panel (j % 4 == 0): rows of one stage are 16 contiguous samples
+    const double* p0 = A + tiled_off(S, r0, j);
     for (int i = lane; i < nh; i += 64) {
       const v2d vv = vs[i];
+      const double* pi = p0 + (int64_t)(i >> 3) * (128 * 16) + 2 * (i & 7);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (j + q < m) acc[q] += *(const v2d*)(p0 + q * lda + 2 * i) * vv;
+        if (j + q < m) acc[q] += *(const v2d*)(pi + 16 * q) * vv;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -246,10 +271,10 @@ __global__ __launch_bounds__(256) void gemv_t_kernel(const double* __restrict__ 
   }
 }
 
-hipError_t launch_gemv_t(const double* A, int64_t lda, int64_t Npad, int64_t m, int64_t mpad, const double* v,
+hipError_t launch_gemv_t(const double* A, int64_t S, int64_t Npad, int64_t m, int64_t mpad, const double* v,
                          double* part, hipStream_t st) {
   hipLaunchKernelGGL(gemv_t_kernel, dim3((unsigned)gemv_t_chunks(Npad), (unsigned)ceil_div(m, 64)), dim3(256), 0, st,
-                     A, lda, Npad, m, v, part, mpad);
+                     A, S, Npad, m, v, part, mpad);
   return hipGetLastError();
 }
 
@@ -289,21 +314,23 @@ __device__ __forceinline__ double gauss(uint64_t seed, uint64_t idx) {
   return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
 }
 
-__global__ void gen_A_kernel(double* __restrict__ A, int64_t lda, int64_t N, int64_t m, int64_t row0,
+// grid.y = m_pad columns; columns >= m (and rows >= N) are zero
+__global__ void gen_A_kernel(double* __restrict__ A, int64_t Npad, int64_t N, int64_t m, int64_t row0,
                              uint64_t seed, double scale) {
   const int64_t j = blockIdx.y;
-  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < lda; n += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t S = Npad / 16;
+  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < Npad; n += (int64_t)gridDim.x * blockDim.x) {
     double v = 0.0;
     if (n < N && j < m) v = scale * gauss(seed, (uint64_t)(row0 + n) * (uint64_t)m + (uint64_t)j);
-    A[j * lda + n] = v;
+    A[tiled_off(S, n, j)] = v;
   }
 }
 
-hipError_t launch_gen_A(double* A, int64_t lda, int64_t N, int64_t m, int64_t row0, uint64_t seed, double scale,
-                        hipStream_t st) {
-  int64_t gx = ceil_div(lda, 256);
+hipError_t launch_gen_A(double* A, int64_t Npad, int64_t N, int64_t m, int64_t mpad, int64_t row0, uint64_t seed,
+                        double scale, hipStream_t st) {
+  int64_t gx = ceil_div(Npad, 256);
   if (gx > 64) gx = 64;
-  hipLaunchKernelGGL(gen_A_kernel, dim3((unsigned)gx, (unsigned)m), dim3(256), 0, st, A, lda, N, m, row0, seed,
+  hipLaunchKernelGGL(gen_A_kernel, dim3((unsigned)gx, (unsigned)mpad), dim3(256), 0, st, A, Npad, N, m, row0, seed,
                      scale);
   return hipGetLastError();
 }

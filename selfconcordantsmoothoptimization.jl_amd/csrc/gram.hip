@@ -31,6 +31,7 @@
 // distinct column panels, which its 4 MiB L2 serves (speed only; results do
 // not depend on placement).
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -56,7 +57,8 @@ __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
 
 // TI = 64-row wave groups along i: TI = 2 -> 128 x 128 tiles, 4 waves, 2 WG/CU;
 // TI = 4 -> 256 x 128 tiles, 8 waves, 1 WG/CU (25 % less operand traffic per flop).
-template <bool NOLOAD, int TI>
+// TILED: operands are the panel-blocked A (common.h tiled_off), lda1/lda2 = S stages.
+template <bool NOLOAD, int TI, bool TILED = false>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
     const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
     const double* __restrict__ w, int64_t k0, int64_t Nk, const int2* __restrict__ tiles, int ntiles,
@@ -111,10 +113,20 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
 
   auto gload = [&](int64_t n0) {
     if (NOLOAD && n0 > k0) return;  // timing-only experiment: operands stay in registers
+    if (TILED) {
+      const int64_t so = (n0 >> 4) * (GT * GBK);
 #pragma unroll
-    for (int i = 0; i < NA; ++i) ra[i] = *(const v2d*)(Ai + (int64_t)(sf0 + FS * i) * lda1 + n0 + 2 * sc);
+      for (int i = 0; i < NA; ++i)
+        ra[i] = *(const v2d*)(A1 + tiled_off(lda1, 2 * sc, (int64_t)bi * GTI + sf0 + FS * i) + so);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(Aj + (int64_t)(sf0 + FS * i) * lda2 + n0 + 2 * sc);
+      for (int i = 0; i < NB; ++i)
+        rb[i] = *(const v2d*)(A2 + tiled_off(lda2, 2 * sc, (int64_t)bj * GT + sf0 + FS * i) + so);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) ra[i] = *(const v2d*)(Ai + (int64_t)(sf0 + FS * i) * lda1 + n0 + 2 * sc);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(Aj + (int64_t)(sf0 + FS * i) * lda2 + n0 + 2 * sc);
+    }
     rw = *(const v2d*)(w + n0 + 2 * sc);
   };
   auto swrite = [&](int buf) {
@@ -191,6 +203,157 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
           P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
           continue;
         }
+        if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
+        else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
+        else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
+        if (accumulate) *dst += acc[ti][tj][r];
+        else *dst = acc[ti][tj][r];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA variant of the 256 x 128 tile (8 waves, one workgroup per CU).
+// Operands go global -> LDS with global_load_lds_dwordx4 (no VGPR staging)
+// into a 3-deep ring of 16-sample stages (48 KiB each); per stage every wave
+// issues 6 DMA instructions (1 KiB = 8 feature rows each).  The LDS image is
+// lane-linear, so the XOR swizzle moves to the per-lane SOURCE address (lane
+// L of an instruction fills row 8i + L/8, slot L%8 with global chunk
+// slot ^ swz(row); cdna_hip_programming.md §5.4 rule 21) and the fragment
+// reads are unchanged.  w is staged by wave 0 in 1 KiB blocks (8 stages) and
+// applied to the B fragments in registers (the same products b·w the register
+// path stores).  Iteration k: counted s_waitcnt vmcnt(6) (stage k landed, stage
+// k+1 stays in flight) + raw s_barrier, then the DMA of stage k+2 into the
+// buffer read in iteration k-1, then the MFMAs on stage k.
+constexpr int GL_STAGES = 3;
+constexpr int GL_SA = 256 * GBK;
+constexpr int GL_SS = GL_SA + GT * GBK;
+constexpr int GL_W = 128;
+
+__device__ __forceinline__ void glds16(const double* src, double* dst) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// TILED: A is stored panel-blocked, block (panel p, stage s) = [128 features][16 samples]
+// contiguous (16 KiB) at ((p * lda + s) * 128) * 16 doubles, lda = number of 16-sample stages.
+template <bool TILED>
+__global__ __launch_bounds__(512, 1) void gram_glds_kernel(
+    const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
+    const double* __restrict__ w, int64_t k0, int64_t Nk, const int2* __restrict__ tiles, int ntiles,
+    double* __restrict__ G, int64_t ldg, int flags, const int4* __restrict__ work, int seglen, int nsplit,
+    double* __restrict__ P) {
+  constexpr int GTI = 256;
+  const int packed = flags & GRAM_PACKED, accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
+  __shared__ __attribute__((aligned(16))) double lds[GL_STAGES * GL_SS + 2 * GL_W];
+
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8;
+  int bi, bj, tix, part = -1;
+  if (work) {
+    const int4 it = work[xcd * seglen + orig / 8];
+    if (it.x < 0) return;
+    bi = it.x;
+    bj = it.y;
+    tix = it.w;
+    if (it.z >= 0) {
+      const int64_t L = ((Nk - k0 + (int64_t)nsplit * GBK - 1) / ((int64_t)nsplit * GBK)) * GBK;
+      part = it.w;
+      k0 = k0 + it.z * L;
+      Nk = k0 + L < Nk ? k0 + L : Nk;
+      if (Nk < k0) Nk = k0;
+    }
+  } else {
+    const int q8 = ntiles / 8, r8 = ntiles % 8;
+    tix = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int2 tl = tiles[tix];
+    bi = tl.x;
+    bj = tl.y;
+  }
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  // this wave's 6 DMA instructions per stage: j = 6 wv + i; j < 32 -> A1 rows 8j.., else A2 rows 8(j-32)..
+  const double* src[6];
+  int dsto[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int j = 6 * wv + i;
+    const bool isA = j < 32;
+    const int f = 8 * (isA ? j : j - 32) + (lane >> 3);
+    const int slot = lane & 7;
+    const int cch = slot ^ swz(f);
+    if (TILED) {
+      const int64_t pnl = isA ? 2 * (int64_t)bi + (f >> 7) : (int64_t)bj;
+      src[i] = (isA ? A1 : A2) + (pnl * (isA ? lda1 : lda2) * GT + (f & 127)) * GBK + 2 * cch;
+    } else {
+      src[i] = isA ? A1 + ((int64_t)bi * GTI + f) * lda1 + 2 * cch : A2 + ((int64_t)bj * GT + f) * lda2 + 2 * cch;
+    }
+    dsto[i] = isA ? 8 * j * GBK : GL_SA + 8 * (j - 32) * GBK;
+  }
+  const int nk = (int)((Nk - k0) / GBK);
+  auto issue = [&](int st) {
+    const int64_t n0 = k0 + (int64_t)st * GBK;
+    double* base = lds + (st % GL_STAGES) * GL_SS;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) glds16(src[i] + (TILED ? (n0 / GBK) * (GT * GBK) : n0), base + dsto[i]);
+    if (wv == 0 && (st & 7) == 0) {
+      const int64_t nw = n0 + 2 * lane < Nk - 1 ? n0 + 2 * lane : Nk - 2;   // clamp past the K range (unused)
+      glds16(w + nw, lds + GL_STAGES * GL_SS + ((st >> 3) & 1) * GL_W);
+    }
+  };
+
+  v4d acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
+  const int fl = lane & 15, g = lane >> 4, sw = swz(fl);
+
+  if (nk > 0) issue(0);
+  if (nk > 1) issue(1);
+  for (int k = 0; k < nk; ++k) {
+    if (k + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + 2 < nk) issue(k + 2);
+    const double* la = lds + (k % GL_STAGES) * GL_SS;
+    const double* lb = la + GL_SA;
+    const double* lw = lds + GL_STAGES * GL_SS + ((k >> 3) & 1) * GL_W + (k & 7) * GBK;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int c = 4 * p + g;
+      const int pc = (c ^ sw) * 2;
+      v2d a[4], b[4];
+      const v2d wv2 = *(const v2d*)(lw + 2 * c);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a[t] = *(const v2d*)(la + (wr * 64 + 16 * t + fl) * GBK + pc);
+        b[t] = *(const v2d*)(lb + (wc * 64 + 16 * t + fl) * GBK + pc) * wv2;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < 4; ++tj)
+            acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int il = wr * 64 + 16 * ti + g + 4 * r;
+        const int jl = wc * 64 + 16 * tj + fl;
+        if (part >= 0) {
+          P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
+          continue;
+        }
+        double* dst;
         if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
         else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
         else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
@@ -381,11 +544,14 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,
                        int ntiles, double* G, int64_t ldg, int packed, int tall, hipStream_t st) {
-  if (!tall)
-    return gram_launch_gen(A, lda, A, lda, w, 0, Nk, tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER, st);
   if (ntiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
-                     tiles, ntiles, G, ldg, packed ? GRAM_PACKED : GRAM_UPPER, nullptr, 0, 0, nullptr);
+  const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
+  if (!tall)
+    hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w,
+                       (int64_t)0, Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else
+    hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
+                       tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   return hipGetLastError();
 }
 
@@ -403,7 +569,13 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
-  if (noload == 4)
+  if (noload == 5)   // timing experiment: the same kernel on a panel-blocked (tiled) A, lda = stages
+    hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(ntiles), dim3(512), 0, st, A, (k1 - k0) / GBK, A,
+                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 6)
+    hipLaunchKernelGGL(gram_glds_kernel<false>, dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 4)
     hipLaunchKernelGGL((gram_f64_kernel<true, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, k0, k1, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (noload == 3)
@@ -445,12 +617,19 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
                              int tall, hipStream_t st) {
   const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
-  if (tall)
-    hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
-                       Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  static const bool use_glds = [] {
+    const char* e = getenv("SCS_GRAM_GLDS");
+    return !(e && e[0] == '0');
+  }();
+  if (tall && use_glds)
+    hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
+                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  else if (tall)
+    hipLaunchKernelGGL((gram_f64_kernel<false, 4, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w,
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   else
-    hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w, (int64_t)0,
-                       Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+    hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w,
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   if (ncomb > 0) {
     if (tall)
       hipLaunchKernelGGL(gram_combine_kernel<4>, dim3(16, ncomb), dim3(256), 0, st, P, comb, nsplit, G, ldg, packed);

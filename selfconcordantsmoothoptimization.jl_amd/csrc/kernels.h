@@ -24,8 +24,9 @@ struct ProxArgsH {
 // ---- gram.hip
 void gram_tile_list(int nb, int2* out, int* ntiles);
 void gram_tile_list_tall(int nb, int2* out, int* ntiles);
-// tall = 1: 256 x 128 tiles from gram_tile_list_tall (nb even); packed slots are then
-// the 128 x 128 halves (2t, 2t+1) of launch tile t
+// Main Gram on the panel-blocked A (lda = S = Npad / 16).  tall = 1: 256 x 128 tiles from
+// gram_tile_list_tall (nb even); packed slots are then the 128 x 128 halves (2t, 2t+1) of
+// launch tile t.  gram_launch_gen operates on column-major operands (the Cholesky updates).
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
                        double* G, int64_t ldg, int packed, int tall, hipStream_t st);
 void gram_tile_list_rowmajor(int nb, int2* out);
@@ -76,13 +77,14 @@ hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const dou
                                double* Yslot, double* scal, hipStream_t st);
 hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st);
 hipError_t launch_symmetrize(double* G, int64_t ldg, int64_t m, hipStream_t st);
-hipError_t launch_half_sym(const double* A, int64_t lda, int64_t m, double* G, int64_t ldg, hipStream_t st);
+hipError_t launch_half_sym(const double* A, int64_t S, int64_t m, double* G, int64_t ldg, hipStream_t st);
 hipError_t launch_rosen(const double* x, int64_t m, int what, double* out, double* G, int64_t ldg, hipStream_t st);
 
 // ---- data.hip
 // z-partials: out[split][ldo] ; returns the number of splits used
 int gemv_n_splits(int64_t Npad, int64_t m);
-hipError_t launch_gemv_n(const double* A, int64_t lda, int64_t Npad, int64_t m, const double* x, int nsplit,
+// A is panel-blocked (common.h tiled_off), S = Npad / 16; x has m_pad entries (zero beyond m)
+hipError_t launch_gemv_n(const double* A, int64_t S, int64_t Npad, int64_t mpad, const double* x, int nsplit,
                          double* part, int64_t ldo, hipStream_t st);
 // loss epilogue over samples: sums the z-partials, writes z / coefficient vectors and
 // per-block loss partials.  Returns the number of value partials written.
@@ -96,13 +98,15 @@ hipError_t launch_epilogue(int loss, int ggn, int flags, const double* zpart, in
 hipError_t launch_sum_partials(const double* part, int n, double* out, hipStream_t st);
 // Aᵀ v (column partial sums over row chunks, then a fixed-order finalize)
 int gemv_t_chunks(int64_t Npad);
-hipError_t launch_gemv_t(const double* A, int64_t lda, int64_t Npad, int64_t m, int64_t mpad, const double* v,
+hipError_t launch_gemv_t(const double* A, int64_t S, int64_t Npad, int64_t m, int64_t mpad, const double* v,
                          double* part, hipStream_t st);
+// panel p: column-major Npad x 128 buffer C <-> tiled A (to_tiled = 1: C -> A)
+hipError_t launch_retile(double* C, double* A, int64_t Npad, int64_t p, int to_tiled, hipStream_t st);
 // out[j] = Σ_chunk part[chunk][j] (+ lam*add[j] if add)
 hipError_t launch_gemv_t_finalize(const double* part, int nchunk, int64_t mpad, int64_t m, double* out,
                                   hipStream_t st);
-hipError_t launch_transpose(const double* A, int64_t lda, int64_t N, int64_t m, double* At, int64_t ldt, int64_t nt,
-                            hipStream_t st);
+hipError_t launch_transpose(const double* A, int64_t Npad, int64_t N, int64_t m, double* At, int64_t ldt,
+                            int64_t nt, hipStream_t st);
 // GGN sample-space branch (vec.hip)
 hipError_t launch_ggn_sample_prep(const double* Hr, const double* gr, double lam, int64_t m, int64_t mpad,
                                   double* hvec, double* hg, hipStream_t st);
@@ -114,8 +118,8 @@ hipError_t launch_ggn_sample_scale(const double* s, const double* B, int64_t N, 
 hipError_t launch_ggn_sample_direction(const double* hvec, const double* t, const double* hg, const double* B,
                                        int64_t N, int64_t m, double* d, hipStream_t st);
 // synthetic data
-hipError_t launch_gen_A(double* A, int64_t lda, int64_t N, int64_t m, int64_t row0, uint64_t seed, double scale,
-                        hipStream_t st);
+hipError_t launch_gen_A(double* A, int64_t Npad, int64_t N, int64_t m, int64_t mpad, int64_t row0, uint64_t seed,
+                        double scale, hipStream_t st);
 hipError_t launch_gen_xtrue(double* x, int64_t m, uint64_t seed, double density, hipStream_t st);
 hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t row0, uint64_t seed,
                         hipStream_t st);

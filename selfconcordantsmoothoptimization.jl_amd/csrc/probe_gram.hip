@@ -11,7 +11,7 @@
 namespace scs {
 void gram_tile_list(int nb, int2* out, int* ntiles);
 void gram_tile_list_tall(int nb, int2* out, int* ntiles);
-hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
+hipError_t gram_launch(const double* A, int64_t S, const double* w, int64_t Nk, const int2* tiles, int ntiles,
                        double* G, int64_t ldg, int packed, int tall, hipStream_t st);
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st);
@@ -50,7 +50,8 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
   int2* dtl;
   CK(hipMalloc(&dtl, nt * sizeof(int2)));
   CK(hipMemcpy(dtl, tl.data(), nt * sizeof(int2), hipMemcpyHostToDevice));
-  CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, tall, 0));
+  // gram_launch reads the panel-blocked layout (S = N/16 stages); the fill is layout-agnostic
+  CK(scs::gram_launch(A, N / 16, w, N, dtl, nt, G, m, 0, tall, 0));
   CK(hipDeviceSynchronize());
   if (check) {
     std::vector<double> hA((size_t)lda * m), hw(N), hG((size_t)m * m);
@@ -62,7 +63,7 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
       for (int64_t i = j; i < m; ++i) {
         double s = 0, sa = 0;
         for (int64_t n = 0; n < N; ++n) {
-          double t = hA[i * lda + n] * hw[n] * hA[j * lda + n];
+          double t = hA[scs::tiled_off(N / 16, n, i)] * hw[n] * hA[scs::tiled_off(N / 16, n, j)];
           s += t; sa += fabs(t);
         }
         double e = fabs(hG[i * m + j] - s) / (sa > 0 ? sa : 1);  // upper triangle: (row j, col i)
@@ -74,7 +75,7 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0));
-  for (int r = 0; r < reps; ++r) CK(scs::gram_launch(A, lda, w, N, dtl, nt, G, m, 0, tall, 0));
+  for (int r = 0; r < reps; ++r) CK(scs::gram_launch(A, N / 16, w, N, dtl, nt, G, m, 0, tall, 0));
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -87,6 +88,13 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float t; CK(hipEventElapsedTime(&t, e0, e1));
     printf("EXP tall noload: %.3f ms  %.2f TF/s\n", t, alg / t / 1e9);
+    for (int v : {6, 5, 6, 5}) {   // glds column-major vs glds panel-blocked (same bytes, contiguous 16 KiB blocks)
+      CK(hipEventRecord(e0));
+      CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, v, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      printf("EXP %s: %.3f ms  %.2f TF/s\n", v == 5 ? "glds tiled-A" : "glds col-major", t, alg / t / 1e9);
+    }
   } else if (getenv("GRAM_EXPERIMENTS")) {
     // (a) operands held in registers after the first stage: compute + LDS + barrier ceiling
     CK(hipEventRecord(e0));

@@ -57,6 +57,7 @@ struct scs_ctx {
 
   // data
   int64_t N = 0, Npad = 0, m = 0, mpad = 0, Nglob = 0, row0 = 0;
+  int64_t nstage = 0;  // Npad / 16: stages of the panel-blocked A (common.h tiled_off)
   bool has_data = false;
   bool generic = false;  // ProblemGeneric (no A)
   double* A = nullptr;
@@ -476,7 +477,7 @@ int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
     HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, c->sp_f32, xd, c->N, c->m, B.shift, c->nnz, c->zpart, c->Npad, c->st));
     return B.nblk;
   }
-  HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, nsplit, c->zpart, c->Npad, c->st));
+  HCK(launch_gemv_n(c->A, c->nstage, c->Npad, c->mpad, xd, nsplit, c->zpart, c->Npad, c->st));
   return nsplit;
 }
 
@@ -489,7 +490,7 @@ void matvec_t(scs_ctx* c, const double* v, double* out) {
     HCK(launch_gemv_t_finalize(c->tpart, B.nblk, c->mpad, c->m, out, c->st));
     return;
   }
-  HCK(launch_gemv_t(c->A, c->Npad, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
+  HCK(launch_gemv_t(c->A, c->nstage, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
   HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, out, c->st));
 }
 
@@ -560,7 +561,7 @@ double eval_f_dev(scs_ctx* c, const double* xh, const double* xd) {
   if (c->loss == SCS_LOSS_QUADRATIC) {
     // 1/2*(x'*(A*x)) + y'*x
     require_dense(c, "the quadratic loss");
-    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, 1, c->zpart, c->Npad, c->st));
+    HCK(launch_gemv_n(c->A, c->nstage, c->Npad, c->mpad, xd, 1, c->zpart, c->Npad, c->st));
     HCK(launch_dot(xd, c->zpart, c->m, c->scal + 8, c->st));
     HCK(launch_dot(c->y, xd, c->m, c->scal + 9, c->st));
     d2h(c, c->hscal + 8, c->scal + 8, 2);
@@ -579,7 +580,7 @@ void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
   if (c->loss == SCS_LOSS_QUADRATIC) {
     // 0.5*(A*x + Aᵀ*x) + y
     require_dense(c, "the quadratic loss");
-    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, xd, 1, c->zpart, c->Npad, c->st));
+    HCK(launch_gemv_n(c->A, c->nstage, c->Npad, c->mpad, xd, 1, c->zpart, c->Npad, c->st));
     gemv_t_global(c, xd, c->gtmp2);
     HCK(launch_axpby(c->zpart, 1.0, c->gtmp2, c->m, c->gtmp2, c->st));
     HCK(launch_axpby(c->y, 0.5, c->gtmp2, c->m, out, c->st));  // y + 0.5*(Ax + Aᵀx)
@@ -679,10 +680,10 @@ void solve_system(scs_ctx* c, double* rhs) {
 // the main Gram launch (scheduled when gram_schedule built a work list)
 void gram_main(scs_ctx* c, const double* w, double* out, int packed) {
   if (c->gwork)
-    HCK(gram_launch_sched(c->A, c->Npad, w, c->Npad, c->gwork, c->gseglen, c->gnsplit, c->gcomb, c->gncomb, c->gpart,
+    HCK(gram_launch_sched(c->A, c->nstage, w, c->Npad, c->gwork, c->gseglen, c->gnsplit, c->gcomb, c->gncomb, c->gpart,
                           out, c->mpad, packed, c->tall, c->st));
   else
-    HCK(gram_launch(c->A, c->Npad, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st));
+    HCK(gram_launch(c->A, c->nstage, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st));
 }
 
 // Gram of the local rows with weights w -> c->G (single rank) or the packed
@@ -796,7 +797,7 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
       HCK(launch_rosen(c->x, m, 1, c->gtmp, nullptr, 0, c->st));
     } else if (c->loss == SCS_LOSS_QUADRATIC) {
       require_dense(c, "the quadratic loss");
-      HCK(launch_half_sym(c->A, c->Npad, m, c->G, c->mpad, c->st));
+      HCK(launch_half_sym(c->A, c->nstage, m, c->G, c->mpad, c->st));
       grad_f_dev(c, xh, c->x, c->gtmp);
     } else {
       forward(c, xh, c->x, EPI_GRAD | EPI_HESS);
@@ -986,6 +987,7 @@ static void set_dims(scs_ctx* c, int64_t N, int64_t m, int64_t Nglob, int64_t ro
   c->m = m;
   c->Npad = std::max<int64_t>(round_up(std::max<int64_t>(N, 1), 16), 16);
   c->mpad = round_up(m, 128);
+  c->nstage = c->Npad / 16;
   c->Nglob = Nglob > 0 ? Nglob : N;
   c->row0 = row0;
 }
@@ -1048,8 +1050,18 @@ int scs_set_data(scs_ctx* c, int64_t N, int64_t m, const double* A, int64_t lda,
       c->A = dalloc<double>(c, (size_t)c->Npad * c->mpad);
       c->y = dalloc<double>(c, c->Npad);
       if (N > 0) {
-        HCK(hipMemcpy2DAsync(c->A, sizeof(double) * c->Npad, A, sizeof(double) * lda, sizeof(double) * N, m,
-                             hipMemcpyHostToDevice, c->st));
+        // panel by panel: host columns -> column-major staging buffer -> panel-blocked A
+        double* C = dalloc<double>(c, (size_t)c->Npad * 128);
+        for (int64_t p = 0; p < c->mpad / 128; ++p) {
+          const int64_t j0 = p * 128, nc = std::min<int64_t>(128, m - j0);
+          HCK(hipMemsetAsync(C, 0, sizeof(double) * c->Npad * 128, c->st));
+          if (nc > 0)
+            HCK(hipMemcpy2DAsync(C, sizeof(double) * c->Npad, A + j0 * lda, sizeof(double) * lda, sizeof(double) * N,
+                                 nc, hipMemcpyHostToDevice, c->st));
+          HCK(launch_retile(C, c->A, c->Npad, p, 1, c->st));
+        }
+        sync(c);
+        dfree_t(c, C);
         if (y) h2d(c, c->y, y, N);
       }
     }
@@ -1072,12 +1084,9 @@ int scs_gen_data(scs_ctx* c, const scs_synth* s) {
     alloc_mspace(c);
     alloc_nspace(c);
     const double scale = (s->kind == 3) ? 1.0 : 1.0 / std::sqrt((double)s->m);
-    HCK(launch_gen_A(c->A, c->Npad, c->N, c->mpad, c->row0, s->seed, scale, c->st));
-    // the padded columns beyond m must be zero: generate with m columns of data
-    if (c->mpad > c->m)
-      HCK(hipMemsetAsync(c->A + c->m * c->Npad, 0, sizeof(double) * c->Npad * (c->mpad - c->m), c->st));
+    HCK(launch_gen_A(c->A, c->Npad, c->N, c->m, c->mpad, c->row0, s->seed, scale, c->st));
     HCK(launch_gen_xtrue(c->xn, c->m, s->seed, s->density, c->st));
-    HCK(launch_gemv_n(c->A, c->Npad, c->Npad, c->m, c->xn, 1, c->zpart, c->Npad, c->st));
+    HCK(launch_gemv_n(c->A, c->nstage, c->Npad, c->mpad, c->xn, 1, c->zpart, c->Npad, c->st));
     HCK(launch_gen_y(s->kind, c->zpart, c->y, c->N, c->row0, s->seed, c->st));
     sync(c);
     c->has_data = true;
@@ -1089,9 +1098,18 @@ int scs_get_data(scs_ctx* c, int64_t r0, int64_t nr, double* A, int64_t lda_out,
     if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
     if (c->sparse && A) fail(c, SCS_ERR_ARG, "sparse A: use scs_get_sparse");
     if (r0 < 0 || nr < 0 || r0 + nr > c->N) fail(c, SCS_ERR_ARG, "row range out of bounds");
-    if (A && nr > 0)
-      HCK(hipMemcpy2DAsync(A, sizeof(double) * lda_out, c->A + r0, sizeof(double) * c->Npad, sizeof(double) * nr,
-                           c->m, hipMemcpyDeviceToHost, c->st));
+    if (A && nr > 0) {
+      double* C = dalloc<double>(c, (size_t)c->Npad * 128);
+      for (int64_t p = 0; p < c->mpad / 128; ++p) {
+        const int64_t j0 = p * 128, nc = std::min<int64_t>(128, c->m - j0);
+        if (nc <= 0) break;
+        HCK(launch_retile(C, c->A, c->Npad, p, 0, c->st));
+        HCK(hipMemcpy2DAsync(A + j0 * lda_out, sizeof(double) * lda_out, C + r0, sizeof(double) * c->Npad,
+                             sizeof(double) * nr, nc, hipMemcpyDeviceToHost, c->st));
+      }
+      sync(c);
+      dfree_t(c, C);
+    }
     if (y && nr > 0) d2h(c, y, c->y + r0, nr);
     sync(c);
   });

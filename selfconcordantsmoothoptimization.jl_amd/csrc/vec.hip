@@ -547,12 +547,12 @@ __global__ void symmetrize_kernel(double* __restrict__ G, int64_t ldg, int64_t m
     G[i * ldg + j] = G[j * ldg + i];
 }
 
-// G = 0.5*(A + Aᵀ) for the quadratic loss (Hessian of 1/2 x'Ax, m x m A)
-__global__ void half_sym_kernel(const double* __restrict__ A, int64_t lda, int64_t m, double* __restrict__ G,
+// G = 0.5*(A + Aᵀ) for the quadratic loss (Hessian of 1/2 x'Ax, m x m A; A panel-blocked, S stages)
+__global__ void half_sym_kernel(const double* __restrict__ A, int64_t S, int64_t m, double* __restrict__ G,
                                 int64_t ldg) {
   const int64_t j = blockIdx.y;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
-    G[j * ldg + i] = 0.5 * (A[j * lda + i] + A[i * lda + j]);
+    G[j * ldg + i] = 0.5 * (A[tiled_off(S, i, j)] + A[tiled_off(S, j, i)]);
 }
 
 // ---------------------------------------------------------------------------
@@ -694,8 +694,8 @@ hipError_t launch_symmetrize(double* G, int64_t ldg, int64_t m, hipStream_t st) 
   hipLaunchKernelGGL(symmetrize_kernel, dim3(4, (unsigned)m), dim3(256), 0, st, G, ldg, m);
   return hipGetLastError();
 }
-hipError_t launch_half_sym(const double* A, int64_t lda, int64_t m, double* G, int64_t ldg, hipStream_t st) {
-  hipLaunchKernelGGL(half_sym_kernel, dim3(4, (unsigned)m), dim3(256), 0, st, A, lda, m, G, ldg);
+hipError_t launch_half_sym(const double* A, int64_t S, int64_t m, double* G, int64_t ldg, hipStream_t st) {
+  hipLaunchKernelGGL(half_sym_kernel, dim3(4, (unsigned)m), dim3(256), 0, st, A, S, m, G, ldg);
   return hipGetLastError();
 }
 hipError_t launch_rosen(const double* x, int64_t m, int what, double* out, double* G, int64_t ldg,

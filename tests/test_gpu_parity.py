@@ -385,3 +385,18 @@ def test_ggn_sample_space_branch(loss):
     assert len(sol.obj) == len(osol.obj)
     np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
     np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+
+
+def test_gram_tall_tiles_and_ksplit(monkeypatch):
+    """The 256 x 128 tile kernel (LDS-DMA ring) under the tail-balanced schedule (K-split
+    partials + fixed-order combine), forced at a small size (default: m >= 12288)."""
+    monkeypatch.setenv("SCS_GRAM_TALL", "1")
+    N, m = 4096 + 48, 1024
+    rng = np.random.default_rng(41)
+    A = rng.standard_normal((N, m))
+    w = rng.standard_normal(N)
+    p = scsopt.Problem(A, np.zeros(N), np.zeros(m), losses.least_squares(), 1.0)
+    G = p.gram(w)
+    terms = np.abs(A).T @ (np.abs(w)[:, None] * np.abs(A))
+    ref = A.T @ (w[:, None] * A)
+    assert np.all(np.abs(G - ref) <= 1e-13 * terms + 1e-300)
