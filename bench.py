@@ -184,16 +184,17 @@ def main():
             gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])   # launches are timed under "solve"
             gram_flops = float(N_local) * m * (m + 1)   # algorithmic symmetric Gram per launch
             achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
-            traffic = None
-            pmc = os.path.join(ROOT, "profiles", "r01_gram_pmc.json")
+            traffic, kname = None, ("gram_glds_kernel" if m >= 12288 and (m // 128) % 2 == 0 else "gram_f64_kernel")
+            pmc = os.path.join(ROOT, "profiles", "r01_gram_pmc.json")   # tools/gpu_prof_c3.sh + tools/pmc_summary.py
             if os.path.exists(pmc) and world == 1:
                 with open(pmc) as f:
                     pm = json.load(f)
                 if pm.get("N") == N and pm.get("m") == m:
                     traffic = pm.get("hbm_bytes_per_launch")
+                    kname = pm.get("kernel", kname)
             line["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                                 "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                                "kernel": "gram_f64_kernel", "avg_ms": gram_avg_ms, "launches": main_calls,
+                                "kernel": kname, "avg_ms": gram_avg_ms, "launches": main_calls,
                                 "flops_per_launch": gram_flops}
         if tm["gemv_calls"] and cfg.get("sparse"):
             # LDS-blocked CSR (A·x) and CSC (Aᵀ·v) passes, launched equally often.  Bytes each launch must
