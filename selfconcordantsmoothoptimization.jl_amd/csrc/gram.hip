@@ -235,7 +235,14 @@ __device__ __forceinline__ void glds16(const double* src, double* dst) {
 
 // TILED: A is stored panel-blocked, block (panel p, stage s) = [128 features][16 samples]
 // contiguous (16 KiB) at ((p * lda + s) * 128) * 16 doubles, lda = number of 16-sample stages.
-template <bool TILED>
+// PIPE (1, 2 = no-load timing build): fragment reads software-pipelined across the
+// barrier.  Each stage's MFMAs run in two halves (samples 0-7 / 8-15 of the stage);
+// iteration k: ds_read F(k,1) | MFMA F(k,0) | wait stage k+1 + barrier | DMA stage
+// k+3 into the slot of stage k | ds_read F(k+1,0) | MFMA F(k,1).  No MFMA then
+// waits on LDS latency after a barrier (both waves of a SIMD leave it together and
+// would otherwise stall on their first fragments at the same time).  Same stages
+// in flight (2) as the plain loop; w is applied to B in registers at use.
+template <bool TILED, int PIPE = 0>
 __global__ __launch_bounds__(512, 1) void gram_glds_kernel(
     const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
     const double* __restrict__ w, int64_t k0, int64_t Nk, const int2* __restrict__ tiles, int ntiles,
@@ -295,7 +302,7 @@ __global__ __launch_bounds__(512, 1) void gram_glds_kernel(
     double* base = lds + (st % GL_STAGES) * GL_SS;
 #pragma unroll
     for (int i = 0; i < 6; ++i) glds16(src[i] + (TILED ? (n0 / GBK) * (GT * GBK) : n0), base + dsto[i]);
-    if (wv == 0 && (st & 7) == 0) {
+    if (__builtin_amdgcn_readfirstlane(wv) == 0 && (st & 7) == 0) {
       const int64_t nw = n0 + 2 * lane < Nk - 1 ? n0 + 2 * lane : Nk - 2;   // clamp past the K range (unused)
       glds16(w + nw, lds + GL_STAGES * GL_SS + ((st >> 3) & 1) * GL_W);
     }
@@ -308,6 +315,79 @@ __global__ __launch_bounds__(512, 1) void gram_glds_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
   const int fl = lane & 15, g = lane >> 4, sw = swz(fl);
 
+  if (PIPE) {
+    // fragment set: A rows (4 v2d), raw B rows (4 v2d), w pair of this lane group
+    struct Frag { v2d a[4], b[4], w; };
+    auto fread = [&](int st, int p, Frag& F) {
+      const double* la = lds + (st % GL_STAGES) * GL_SS;
+      const double* lb = la + GL_SA;
+      const double* lw = lds + GL_STAGES * GL_SS + ((st >> 3) & 1) * GL_W + (st & 7) * GBK;
+      const int c = 4 * p + g;
+      const int pc = (c ^ sw) * 2;
+      F.w = *(const v2d*)(lw + 2 * c);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        F.a[t] = *(const v2d*)(la + (wr * 64 + 16 * t + fl) * GBK + pc);
+        F.b[t] = *(const v2d*)(lb + (wc * 64 + 16 * t + fl) * GBK + pc);
+      }
+    };
+    auto mm = [&](const Frag& F) {
+      v2d b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) b[t] = F.b[t] * F.w;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < 4; ++tj)
+            acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(F.a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
+    };
+    const bool live = PIPE == 1;
+    // waits are __builtin_amdgcn_s_waitcnt (gfx9 encoding: vmcnt[3:0] | expcnt<<4 | lgkmcnt<<8 |
+    // vmcnt[5:4]<<14), visible to the compiler's waitcnt pass, unlike inline asm
+    Frag X, Y;
+    if (nk > 0) {
+      issue(0);
+      if (nk > 1) issue(1);
+      if (nk > 2) issue(2);
+      if (nk > 2) __builtin_amdgcn_s_waitcnt(0x0F7C);   // vmcnt(12)
+      else if (nk > 1) __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6)
+      else __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      fread(0, 0, X);
+    }
+    // one iteration; has1/2/3 = stages k+1/k+2/k+3 exist (compile-time true in the
+    // steady-state loop, so its body has no branches for the waitcnt pass to merge over)
+    auto body = [&](int k, bool has1, bool has2, bool has3) {
+      // X was read during the previous mm(Y) (32 MFMAs ago): retire it explicitly so the Y reads
+      // below do not push the LDS queue past lgkmcnt's 4-bit range (which would make the
+      // compiler wait for Y too before mm(X))
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+      fread(k, 1, Y);
+      __builtin_amdgcn_sched_barrier(0);   // issue all fragment reads before the MFMAs
+      mm(X);
+      __builtin_amdgcn_sched_barrier(0);   // keep mm(X) above the barrier (MFMAs are not memory ops)
+      if (has1) {
+        if (has2) __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (has3 && live) issue(k + 3);
+      if (has1) fread(k + 1, 0, X);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(Y);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    int k = 0;
+    for (; k + 3 < nk; ++k) body(k, true, true, true);
+    for (; k < nk; ++k) body(k, k + 1 < nk, k + 2 < nk, false);
+  } else {
   if (nk > 0) issue(0);
   if (nk > 1) issue(1);
   for (int k = 0; k < nk; ++k) {
@@ -339,6 +419,7 @@ __global__ __launch_bounds__(512, 1) void gram_glds_kernel(
           for (int tj = 0; tj < 4; ++tj)
             acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
     }
+  }
   }
 
 #pragma unroll
@@ -550,7 +631,7 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else
-    hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
+    hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   return hipGetLastError();
 }
@@ -569,7 +650,11 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
-  if (noload == 5)   // timing experiment: the same kernel on a panel-blocked (tiled) A, lda = stages
+  if (noload == 7 || noload == 8)   // pipelined fragment reads (8: no-load ceiling), panel-blocked A
+    hipLaunchKernelGGL((noload == 7 ? gram_glds_kernel<true, 1> : gram_glds_kernel<true, 2>), dim3(ntiles), dim3(512),
+                       0, st, A, (k1 - k0) / GBK, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr,
+                       0, 0, nullptr);
+  else if (noload == 5)   // timing experiment: the same kernel on a panel-blocked (tiled) A, lda = stages
     hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(ntiles), dim3(512), 0, st, A, (k1 - k0) / GBK, A,
                        (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (noload == 6)
@@ -617,11 +702,16 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
                              int tall, hipStream_t st) {
   const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
-  static const bool use_glds = [] {
+  // SCS_GRAM_GLDS (A/B switch): 0 = register-staged kernel, 1 = LDS-DMA plain loop,
+  // unset/2 = LDS-DMA with pipelined fragment reads (default)
+  static const int glds = [] {
     const char* e = getenv("SCS_GRAM_GLDS");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 2;
   }();
-  if (tall && use_glds)
+  if (tall && glds == 2)
+    hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
+                       Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  else if (tall && glds == 1)
     hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   else if (tall)

@@ -71,6 +71,18 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
       }
     printf("CHECK tall=%d N=%ld m=%ld max |G-ref|/sum|terms| = %.3e  %s\n", tall, (long)N, (long)m, maxrel,
            maxrel < 1e-14 ? "PASS" : "FAIL");
+    if (tall) {   // gram_launch runs the pipelined variant: same MFMA order as the plain loop -> bitwise identical
+      double* G2;
+      CK(hipMalloc(&G2, (size_t)m * m * 8));
+      CK(hipMemcpy(G2, G, (size_t)m * m * 8, hipMemcpyDeviceToDevice));
+      CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G2, m, 0, 5, 0));   // plain LDS-DMA loop
+      std::vector<double> hG2((size_t)m * m);
+      CK(hipMemcpy(hG2.data(), G2, hG2.size() * 8, hipMemcpyDeviceToHost));
+      size_t ndiff = 0;
+      for (size_t e = 0; e < hG2.size(); ++e) ndiff += hG2[e] != hG[e];
+      printf("CHECK pipe N=%ld m=%ld bitwise diffs vs plain: %zu  %s\n", (long)N, (long)m, ndiff, ndiff ? "FAIL" : "PASS");
+      CK(hipFree(G2));
+    }
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -88,12 +100,13 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float t; CK(hipEventElapsedTime(&t, e0, e1));
     printf("EXP tall noload: %.3f ms  %.2f TF/s\n", t, alg / t / 1e9);
-    for (int v : {6, 5, 6, 5}) {   // glds column-major vs glds panel-blocked (same bytes, contiguous 16 KiB blocks)
+    for (int v : {5, 7, 8, 5, 7}) {   // glds panel-blocked: plain loop / pipelined fragments / pipelined no-load
       CK(hipEventRecord(e0));
       CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, v, 0));
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       CK(hipEventElapsedTime(&t, e0, e1));
-      printf("EXP %s: %.3f ms  %.2f TF/s\n", v == 5 ? "glds tiled-A" : "glds col-major", t, alg / t / 1e9);
+      printf("EXP %s: %.3f ms  %.2f TF/s\n", v == 5 ? "glds tiled-A" : v == 7 ? "glds pipe" : "glds pipe noload", t,
+             alg / t / 1e9);
     }
   } else if (getenv("GRAM_EXPERIMENTS")) {
     // (a) operands held in registers after the first stage: compute + LDS + barrier ceiling

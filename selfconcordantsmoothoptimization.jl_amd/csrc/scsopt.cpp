@@ -392,9 +392,9 @@ void ensure_gram(scs_ctx* c) {
   std::vector<int2> tl((size_t)nb * (nb + 1) / 2 + nb), ul;
   int nt = 0;
   const char* sq = std::getenv("SCS_GRAM_TALL");
-  // 256 x 128 tiles pay off once the Gram is large (C3, m = 16384: 59.7 vs 57.0 TF/s); at m = 8192
-  // the 128 x 128 tiles are ~1.5 % faster (profiles/r01/ab_gram.log)
-  c->tall = (nb % 2 == 0) && nb >= 96 && !(sq && sq[0] == '0');
+  // 256 x 128 tiles (LDS-DMA kernel with pipelined fragment reads) from m = 8192 on: C3 67.1 TF/s,
+  // C2 65.2 vs 63.2 TF/s with the 128 x 128 register-staged tiles (profiles/r01/ab_gram_pipe.log)
+  c->tall = (nb % 2 == 0) && nb >= 64 && !(sq && sq[0] == '0');
   if (sq && sq[0] == '1') c->tall = (nb % 2 == 0);
   if (c->tall) {
     gram_tile_list_tall(nb, tl.data(), &nt);
