@@ -17,6 +17,9 @@
 //
 // Layout: G is m_pad x m_pad, ld = m_pad, m_pad % 128 == 0; the padded tail of
 // the diagonal is set to 1 by the caller (block-diag(A, I)).
+#include <cstdlib>
+#include <vector>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -59,70 +62,135 @@ __device__ long long chol_prof[64];
 // one doubling level: for every pair (i0 = 2pS, j0 = i0 + S):
 //   step 1  T(r, c) = Σ_{t <= c} U(i0+r, j0+t) W(j0+t, j0+c)   -> S[j0 + r][i0 + c] (strictly lower)
 //   step 2  W(i0+r, j0+c) = -Σ_{t >= r} W(i0+r, i0+t) T(t, c)  -> S[i0 + r][j0 + c]
+constexpr int DNT = 256;          // threads of chol_diag_kernel (4 waves; 512 spills: measured slower)
+constexpr int RQ = 1024 / DNT;    // rows per thread in the doubling products
+
 template <int S>
 __device__ __forceinline__ void chol_inv_double(double* su, int tid) {
-  constexpr int MC = S / 16;                  // columns per thread (4 rows x MC)
-  constexpr int TPP = 256 / (CB / (2 * S));   // threads per pair
+  constexpr int MC = S / 16;                  // columns per thread (RQ rows x MC)
+  constexpr int TPP = DNT / (CB / (2 * S));   // threads per pair
   const int pair = tid / TPP, loc = tid % TPP;
   const int rg = loc / 16, cg = loc % 16;
   const int i0 = 2 * S * pair, j0 = i0 + S;
-  const int r0 = 4 * rg, c0 = cg * MC;
-  double acc[4][MC];
+  const int r0 = RQ * rg, c0 = cg * MC;
+  double acc[RQ][MC];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < RQ; ++q)
 #pragma unroll
     for (int m = 0; m < MC; ++m) acc[q][m] = 0.0;
 #pragma unroll 4
   for (int t = 0; t < S; ++t) {
-    double u[4], wv[MC];
+    double u[RQ], wv[MC];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) u[q] = su[(j0 + t) * CLD + i0 + r0 + q];
+    for (int q = 0; q < RQ; ++q) u[q] = su[(j0 + t) * CLD + i0 + r0 + q];
 #pragma unroll
     for (int m = 0; m < MC; ++m) wv[m] = (t <= c0 + m) ? su[(j0 + c0 + m) * CLD + j0 + t] : 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < RQ; ++q)
 #pragma unroll
       for (int m = 0; m < MC; ++m) acc[q][m] += u[q] * wv[m];
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < RQ; ++q)
 #pragma unroll
     for (int m = 0; m < MC; ++m) su[(i0 + c0 + m) * CLD + j0 + r0 + q] = acc[q][m];
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < RQ; ++q)
 #pragma unroll
     for (int m = 0; m < MC; ++m) acc[q][m] = 0.0;
 #pragma unroll 4
   for (int t = 0; t < S; ++t) {
-    double wv[4], tv[MC];
+    double wv[RQ], tv[MC];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wv[q] = (t >= r0 + q) ? su[(i0 + t) * CLD + i0 + r0 + q] : 0.0;
+    for (int q = 0; q < RQ; ++q) wv[q] = (t >= r0 + q) ? su[(i0 + t) * CLD + i0 + r0 + q] : 0.0;
 #pragma unroll
     for (int m = 0; m < MC; ++m) tv[m] = su[(i0 + c0 + m) * CLD + j0 + t];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < RQ; ++q)
 #pragma unroll
       for (int m = 0; m < MC; ++m) acc[q][m] += wv[q] * tv[m];
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < RQ; ++q)
 #pragma unroll
     for (int m = 0; m < MC; ++m) su[(j0 + c0 + m) * CLD + i0 + r0 + q] = -acc[q][m];
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
+// The same doubling level on MFMA: S x S products as 16 x 16 output tiles (S/4 MFMAs
+// each), (pair, tile) items round-robin over the waves.  Fragment maps as in phase C;
+// the triangular operands are masked per lane (W22: k <= j; W11: k >= i).
+template <int S>
+__device__ __forceinline__ void chol_inv_double_mfma(double* su, int tid) {
+  constexpr int NP = CB / (2 * S), NT16 = (S / 16) * (S / 16);
+  const int wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  for (int it = wv; it < NP * NT16; it += DNT / 64) {   // step 1: T = U12 · W22 -> strictly lower
+    const int pair = it / NT16, tt = it % NT16;
+    const int i0 = 2 * S * pair, j0 = i0 + S;
+    const int ti = 16 * (tt / (S / 16)), tj = 16 * (tt % (S / 16));
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t0 = 0; t0 < S; t0 += 4) {
+      const int k = t0 + lk;
+      const double a = su[(j0 + k) * CLD + i0 + ti + li];
+      const double b = (k <= tj + li) ? su[(j0 + tj + li) * CLD + j0 + k] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) su[(i0 + tj + li) * CLD + j0 + ti + lk + 4 * r] = acc[r];
+  }
+  __syncthreads();
+  for (int it = wv; it < NP * NT16; it += DNT / 64) {   // step 2: W12 = -W11 · T
+    const int pair = it / NT16, tt = it % NT16;
+    const int i0 = 2 * S * pair, j0 = i0 + S;
+    const int ti = 16 * (tt / (S / 16)), tj = 16 * (tt % (S / 16));
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t0 = 0; t0 < S; t0 += 4) {
+      const int k = t0 + lk;
+      const double a = (k >= ti + li) ? su[(i0 + k) * CLD + i0 + ti + li] : 0.0;
+      const double b = su[(i0 + tj + li) * CLD + j0 + k];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) su[(j0 + tj + li) * CLD + i0 + ti + lk + 4 * r] = -acc[r];
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
                                                         double* __restrict__ W, int* __restrict__ info) {
   __shared__ double su[CB * CLD];   // S(r, c) = su[c*CLD + r]
   __shared__ double srinv[CB];      // 1 / U(j, j)
+  __shared__ double swinv[CB / SB][SB * SB];   // inverses of the 16 x 16 diagonal blocks (col-major)
   double* blk = G + (int64_t)k * CB * ld + (int64_t)k * CB;
   double* Wk = W + (int64_t)k * CB * CB;
   const int tid = threadIdx.x;
-  for (int e = tid; e < CB * CB; e += 256) {
+  for (int e = tid; e < CB * CB; e += DNT) {
     const int c = e >> 7, r = e & 127;
     su[c * CLD + r] = (r <= c) ? blk[(int64_t)c * ld + r] : 0.0;
   }
+  // inverse of the (final) 16 x 16 diagonal block kb by one wave (lane c = column c)
+  auto inv16 = [&](int kb) {
+    const int o = kb * SB, c = tid & 15;
+    double a[SB], w[SB];
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      a[i] = su[(o + c) * CLD + o + i];
+      w[i] = (i == c) ? 1.0 : 0.0;
+    }
+#pragma unroll
+    for (int t = SB - 1; t >= 0; --t) {
+      w[t] *= srinv[o + t];
+#pragma unroll
+      for (int i = 0; i < t; ++i) w[i] -= readlane_d(a[i], t) * w[t];
+    }
+    if ((tid & 63) < SB) {
+#pragma unroll
+      for (int i = 0; i < SB; ++i) swinv[kb][c * SB + i] = (i <= c) ? w[i] : 0.0;
+    }
+  };
   __syncthreads();
 
   PROF_MARK(0);
@@ -139,8 +207,13 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ G, 
       for (int j = 0; j < SB; ++j) {
         const double ajj = readlane_d(a[j], j);
         if (tid == 0 && !(ajj > 0.0) && *info == 0) *info = k * CB + o + j + 1;
-        const double d = sqrt(ajj);
-        const double r = 1.0 / d;
+        // 1/sqrt(ajj): v_rsq_f64 + two Newton steps (6 dependent FMAs instead of the
+        // sqrt + divide sequences on this serial chain); d = ajj * r
+        double r = __builtin_amdgcn_rsq(ajj);
+        const double hj = 0.5 * ajj;
+#pragma unroll
+        for (int it = 0; it < 2; ++it) r = fma(r, fma(-hj * r, r, 0.5), r);
+        const double d = ajj * r;
         if (tid == 0) srinv[o + j] = r;
         a[j] = (c > j) ? a[j] * r : ((c == j) ? d : a[j]);    // row j of U: U(j, c)
 #pragma unroll
@@ -174,151 +247,59 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ G, 
     }
     __syncthreads();
     PROF_MARK(3 + 4 * kb);
-    // ---- C: trailing update  S(i, c) -= Σ_t U(o + t, i) U(o + t, c),  o+16 <= i <= c
+    // ---- C: trailing update  S(i, c) -= Σ_t U(o + t, i) U(o + t, c),  o+16 <= i <= c, on MFMA:
+    // 16 x 16 upper tiles (I <= C) round-robin over the waves, 4 x v_mfma_f64_16x16x4 each
+    // (A[i][k] = U(o+t0+k, i0+i), B[k][j] = U(o+t0+k, c0+j); lane l feeds i|j = l&15, k = l>>4;
+    // D row = (l>>4) + 4r, col = l&15).  Diagonal tiles update only i <= c: phase A reads the
+    // zeros below the diagonal.
     {
-      const int nt = np >> 2, ntiles = nt * (nt + 1) / 2;
-      for (int id = tid; id < ntiles; id += 256) {
-        int C = (int)((sqrtf(8.0f * id + 1.0f) - 1.0f) * 0.5f);
-        while (C * (C + 1) / 2 > id) --C;
+      const int n16 = np >> 4, ntl = n16 * (n16 + 1) / 2;
+      const int wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+      for (int id = wv; id < ntl; id += DNT / 64) {
+        int C = 0;
         while ((C + 1) * (C + 2) / 2 <= id) ++C;
         const int I = id - C * (C + 1) / 2;
-        const int i0 = o + SB + 4 * I, c0 = o + SB + 4 * C;
-        double acc[4][4] = {};
+        const int i0 = o + SB + 16 * I, c0 = o + SB + 16 * C;
+        v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int t = 0; t < SB; ++t) {
-          double ui[4], uc[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            ui[q] = su[(i0 + q) * CLD + o + t];
-            uc[q] = su[(c0 + q) * CLD + o + t];
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) acc[r][cc] += ui[r] * uc[cc];
+        for (int t0 = 0; t0 < SB; t0 += 4) {
+          const double a = su[(i0 + li) * CLD + o + t0 + lk];
+          const double b = su[(c0 + li) * CLD + o + t0 + lk];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc)
-            if (i0 + r <= c0 + cc) su[(c0 + cc) * CLD + i0 + r] -= acc[r][cc];
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + lk + 4 * r, c = c0 + li;
+          if (i <= c) su[c * CLD + i] -= acc[r];
+        }
       }
     }
     __syncthreads();
   }
   PROF_MARK(33);
   // ---- store U
-  for (int e = tid; e < CB * CB; e += 256) {
+  for (int e = tid; e < CB * CB; e += DNT) {
     const int c = e >> 7, r = e & 127;
     if (r <= c) blk[(int64_t)c * ld + r] = su[c * CLD + r];
   }
-  // ---- diagonal 16 x 16 inverses: wave wv inverts blocks wv and wv + 4 (lane c = column c)
-  {
-    const int wv = tid >> 6, c = tid & 15;
-    double w0[SB], w1[SB];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int o = (wv + 4 * h) * SB;
-      double a[SB], w[SB];
-#pragma unroll
-      for (int i = 0; i < SB; ++i) {
-        a[i] = su[(o + c) * CLD + o + i];
-        w[i] = (i == c) ? 1.0 : 0.0;
-      }
-#pragma unroll
-      for (int t = SB - 1; t >= 0; --t) {
-        w[t] *= srinv[o + t];
-#pragma unroll
-        for (int i = 0; i < t; ++i) w[i] -= readlane_d(a[i], t) * w[t];
-      }
-#pragma unroll
-      for (int i = 0; i < SB; ++i) {
-        if (h == 0) w0[i] = w[i];
-        else w1[i] = w[i];
-      }
-    }
-    __syncthreads();   // every wave has read its U blocks
-    if ((tid & 63) < SB) {
-#pragma unroll
-      for (int i = 0; i < SB; ++i) {
-        if (i <= c) su[(wv * SB + c) * CLD + wv * SB + i] = w0[i];
-        if (i <= c) su[((wv + 4) * SB + c) * CLD + (wv + 4) * SB + i] = w1[i];
-      }
-    }
-    __syncthreads();
+  // (running inv16 beside phase B on the idle last wave measured slower: B waits for it)
+  for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) inv16(kb);
+  __syncthreads();   // storeU has read the diagonal blocks; swinv complete
+  // ---- diagonal 16 x 16 inverses into the diagonal blocks of S (start of the doubling)
+  for (int e = tid; e < CB * SB; e += DNT) {
+    const int kb = e >> 8, c = (e >> 4) & 15, i = e & 15;
+    if (i <= c) su[(kb * SB + c) * CLD + kb * SB + i] = swinv[kb][c * SB + i];
   }
+  __syncthreads();
   PROF_MARK(34);
-  chol_inv_double<16>(su, tid);
-  chol_inv_double<32>(su, tid);
-  chol_inv_double<64>(su, tid);
-  for (int e = tid; e < CB * CB; e += 256) {
+  chol_inv_double_mfma<16>(su, tid);
+  chol_inv_double_mfma<32>(su, tid);
+  chol_inv_double_mfma<64>(su, tid);
+  for (int e = tid; e < CB * CB; e += DNT) {
     const int c = e >> 7, r = e & 127;
     Wk[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
   }
   PROF_MARK(35);
-}
-
-// Forward solve Uᵀ y = b, block step k (all blocks recompute y_k = W_kᵀ b_k;
-// block 0 stores it, the others update b_j -= U_kjᵀ y_k for j > k).
-__global__ __launch_bounds__(256) void chol_fwd_step_kernel(const double* __restrict__ G, int64_t ld, int k,
-                                                            int nblk, const double* __restrict__ W,
-                                                            double* __restrict__ b, double* __restrict__ y) {
-  __shared__ double yk[CB];
-  __shared__ double bk[CB];
-  const int tid = threadIdx.x;
-  if (tid < CB) bk[tid] = b[(int64_t)k * CB + tid];
-  __syncthreads();
-  const double* Wk = W + (int64_t)k * CB * CB;
-  if (tid < CB) {  // y_k[t] = Σ_{u<=t} W[u][t] b_k[u]
-    double s = 0.0;
-    for (int u = 0; u <= tid; ++u) s += Wk[(int64_t)tid * CB + u] * bk[u];
-    yk[tid] = s;
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    if (tid < CB) y[(int64_t)k * CB + tid] = yk[tid];
-    return;
-  }
-  // columns of the row panel handled by this block: 64 per block, 16 per wave
-  const int lane = tid & 63, wid = tid >> 6;
-  const int64_t c0 = (int64_t)(k + 1) * CB + (int64_t)(blockIdx.x - 1) * 64 + wid * 16;
-  const double ya = yk[2 * lane], yb = yk[2 * lane + 1];
-  for (int q = 0; q < 16; ++q) {
-    const int64_t c = c0 + q;
-    if (c >= (int64_t)nblk * CB) break;
-    const v2d u = *(const v2d*)(G + c * ld + (int64_t)k * CB + 2 * lane);
-    const double s = wave_sum(u[0] * ya + u[1] * yb);
-    if (lane == 0) b[c] -= s;
-  }
-}
-
-// Backward solve U x = y, block step k (descending): x_k = W_k y_k; rows above
-// the block: y_r -= Σ_t U[r][k*128+t] x_k[t].
-__global__ __launch_bounds__(256) void chol_bwd_step_kernel(const double* __restrict__ G, int64_t ld, int k,
-                                                            const double* __restrict__ W, double* __restrict__ y,
-                                                            double* __restrict__ x) {
-  __shared__ double xk[CB];
-  __shared__ double ykk[CB];
-  const int tid = threadIdx.x;
-  if (tid < CB) ykk[tid] = y[(int64_t)k * CB + tid];
-  __syncthreads();
-  const double* Wk = W + (int64_t)k * CB * CB;
-  if (tid < CB) {  // x_k[t] = Σ_{u>=t} W[t][u] y_k[u]
-    double s = 0.0;
-    for (int u = tid; u < CB; ++u) s += Wk[(int64_t)u * CB + tid] * ykk[u];
-    xk[tid] = s;
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    if (tid < CB) x[(int64_t)k * CB + tid] = xk[tid];
-    return;
-  }
-  const int64_t r = (int64_t)(blockIdx.x - 1) * 256 + tid;
-  if (r >= (int64_t)k * CB) return;
-  double s = 0.0;
-  const double* col = G + (int64_t)k * CB * ld + r;
-  for (int t = 0; t < CB; ++t) s += col[(int64_t)t * ld] * xk[t];
-  y[r] -= s;
 }
 
 __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, int64_t mpad) {
@@ -326,42 +307,277 @@ __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, i
   if (i < mpad) G[i * ld + i] = 1.0;
 }
 
-hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const double* wpm,
-                       const int2* rowlist, const int2* trilist, int* info, hipStream_t st) {
+// ---------------------------------------------------------------------------
+// Two-level blocked factorization.  Outer blocks of OB (default 8) inner 128-blocks:
+//   A  inner factor of the outer diagonal block (the single-level loop below, restricted
+//      to the block: chol_diag_kernel + panel solve + trailing update with K = 128);
+//   B  forward solve of the outer row strip X = U_D⁻ᵀ R (rows of the block, all columns to
+//      its right), recursively: X1 = solve(D11, R1); R2 -= U12ᵀ X1 (one Gram launch over
+//      an (rows of R2) x (strip columns) rectangle, K = rows of X1); X2 = solve(D22, R2);
+//      leaves are the in-place W_kᵀ multiplies;
+//   C  trailing update of everything right of / below the block with K = OB·128:
+//      A_rest -= Xᵀ X (upper store).
+// Moving the bulk of the m³/3 flops into C with K = 1024 instead of 128 cuts the
+// read-modify-write of the trailing matrix 8x (the single-level update is HBM-bound on
+// that C tile traffic: 2·128 KiB per 4.2 MFLOP tile).
+hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
+  a->nblk = nblk;
+  std::vector<double> hw((size_t)CB + mpad, -1.0);
+  for (int i = 0; i < CB; ++i) hw[i] = 1.0;
+  std::vector<int2> rl;
+  for (int R = 1; R <= 4; ++R)
+    for (int j = 0; j < nblk; ++j)
+      for (int i = 0; i < R; ++i) rl.push_back(make_int2(i, j));   // bj-major: first R*C = R x C rectangle
+  hipError_t e = hipMalloc(&a->w, sizeof(double) * hw.size());
+  if (e == hipSuccess) e = hipMalloc(&a->rect, sizeof(int2) * rl.size());
+  if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return e;
+}
+
+void chol_aux_free(CholAux* a) {
+  if (a->w) (void)hipFree(a->w);
+  if (a->rect) (void)hipFree(a->rect);
+  a->w = nullptr;
+  a->rect = nullptr;
+}
+
+static const int2* rect_list(const CholAux* a, int R) { return a->rect + (int64_t)a->nblk * (R - 1) * R / 2; }
+
+static int outer_block() {
+  static const int ob = [] {
+    const char* e = getenv("SCS_CHOL_OB");
+    const int v = e ? atoi(e) : 8;
+    return v < 1 ? 1 : v;
+  }();
+  return ob;
+}
+
+// forward solve of the strip rows [lo, hi) (inner blocks) x nc columns starting at block c0
+static hipError_t strip_solve(double* G, int64_t ld, const double* W, const CholAux* a, int lo, int hi, int c0, int nc,
+                              hipStream_t st) {
+  if (hi - lo == 1) {
+    double* R = G + (int64_t)c0 * CB * ld + (int64_t)lo * CB;
+    return gram_launch_gen(W + (int64_t)lo * CB * CB, CB, R, ld, a->w, 0, CB, rect_list(a, 1), nc, R, ld, 0, st);
+  }
+  const int mid = (lo + hi) / 2;
+  hipError_t e = strip_solve(G, ld, W, a, lo, mid, c0, nc, st);
+  if (e != hipSuccess) return e;
+  // R2 -= U12ᵀ X1: A1 = U[lo:mid, mid:hi] (panels mid.., rows from lo), A2 = X1 (panels c0.., rows from lo)
+  const double* U12 = G + (int64_t)mid * CB * ld + (int64_t)lo * CB;
+  const double* X1 = G + (int64_t)c0 * CB * ld + (int64_t)lo * CB;
+  double* R2 = G + (int64_t)c0 * CB * ld + (int64_t)mid * CB;
+  e = gram_launch_gen(U12, ld, X1, ld, a->w + CB, 0, (int64_t)(mid - lo) * CB, rect_list(a, hi - mid), (hi - mid) * nc,
+                      R2, ld, /*GRAM_ACCUMULATE*/ 2, st);
+  if (e != hipSuccess) return e;
+  return strip_solve(G, ld, W, a, mid, hi, c0, nc, st);
+}
+
+hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* a,
+                       const int2* trilist, int* info, hipStream_t st) {
+  const int nblk = (int)(mpad / CB);
+  const int OB = outer_block();
   if (mpad > m) hipLaunchKernelGGL(diag_pad_kernel, dim3((unsigned)ceil_div(mpad - m, 256)), dim3(256), 0, st, G, ld,
                                    m, mpad);
-  for (int k = 0; k < nblk; ++k) {
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, G, ld, k, W, info);
-    const int nb = nblk - k - 1;
-    if (nb == 0) break;
-    double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..) : 128 rows x nb*128 cols
-    // panel solve in place: U_kj = W_kᵀ A_kj  (P = W_k, tiles (0, j))
-    hipError_t e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, wpm, 0, CB, rowlist, nb, rowpanel,
-                                   ld, 0, st);
+  for (int i0 = 0; i0 < nblk; i0 += OB) {
+    const int i1 = i0 + OB < nblk ? i0 + OB : nblk;
+    // A: inner factor of the outer diagonal block
+    for (int k = i0; k < i1; ++k) {
+      hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+      const int nb = i1 - k - 1;
+      if (nb == 0) break;
+      double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..i1-1)
+      hipError_t e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb,
+                                     rowpanel, ld, 0, st);
+      if (e != hipSuccess) return e;
+      double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
+      e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld,
+                          /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+      if (e != hipSuccess) return e;
+    }
+    const int nc = nblk - i1;
+    if (nc == 0) break;
+    // B: strip solve, C: trailing update with K = (i1 - i0)·128
+    hipError_t e = strip_solve(G, ld, W, a, i0, i1, i1, nc, st);
     if (e != hipSuccess) return e;
-    // trailing update (upper): A_(k+1..) -= U_kᵀ U_k
-    double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
-    e = gram_launch_gen(rowpanel, ld, rowpanel, ld, wpm + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld,
-                        /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+    const double* X = G + (int64_t)i1 * CB * ld;
+    double* trail = G + (int64_t)i1 * CB * ld + (int64_t)i1 * CB;
+    e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, nc * (nc + 1) / 2, trail,
+                        ld, 2 | 4, st);
     if (e != hipSuccess) return e;
   }
   return hipGetLastError();
 }
 
-// Solve G x = b given the factor; b (length mpad, zero-padded) is overwritten
-// by x; y is scratch (mpad).
+// ---------------------------------------------------------------------------
+// Triangular solves, two-level: per outer block one single-workgroup kernel runs the
+// (≤ OB) serial 128-block steps with the block's right-hand side in LDS, and one
+// many-workgroup kernel applies the block's contribution to the rest of the vector
+// (a (OB·128) x rest transposed GEMV).  2 launches per outer block instead of
+// 2 per 128-block, and the W_k products are coalesced.
+constexpr int SOLVE_NT = 1024;
+constexpr int SOLVE_MAXB = 16;   // max inner blocks per outer block held in LDS
+
+// Uᵀ y = b restricted to rows [i0, i1) (inner blocks): b is already reduced by the
+// contributions of earlier outer blocks.  Writes y[i0..i1).
+__global__ __launch_bounds__(SOLVE_NT) void chol_fwd_inner_kernel(const double* __restrict__ G, int64_t ld,
+                                                                   const double* __restrict__ W, int i0, int i1,
+                                                                   const double* __restrict__ b,
+                                                                   double* __restrict__ y) {
+  __shared__ double bs[SOLVE_MAXB * CB];
+  __shared__ double yk[CB];
+  const int tid = threadIdx.x;
+  const int nr = (i1 - i0) * CB;
+  for (int r = tid; r < nr; r += SOLVE_NT) bs[r] = b[(int64_t)i0 * CB + r];
+  __syncthreads();
+  for (int k = i0; k < i1; ++k) {
+    const int ko = (k - i0) * CB;
+    {  // y_k[t] = Σ_u W(u, t) b_k(u): 8 threads per output t, 16 contiguous u each (column t of W)
+      const int t = tid >> 3, p = tid & 7;
+      const double* col = W + (int64_t)k * CB * CB + (int64_t)t * CB + 16 * p;
+      double sacc = 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) sacc += col[u] * bs[ko + 16 * p + u];
+      sacc += __shfl_xor(sacc, 1, 64);
+      sacc += __shfl_xor(sacc, 2, 64);
+      sacc += __shfl_xor(sacc, 4, 64);
+      if (p == 0) yk[t] = sacc;
+    }
+    __syncthreads();
+    if (tid < CB) y[(int64_t)k * CB + tid] = yk[tid];
+    // b_j -= U_kjᵀ y_k for the columns of the later blocks of this outer block
+    const int ncol = (i1 - k - 1) * CB;
+    for (int cb = 0; cb < ncol; cb += SOLVE_NT / 8) {
+      const int cl = cb + (tid >> 3), p = tid & 7;
+      double sacc = 0.0;
+      if (cl < ncol) {
+        const double* col = G + (int64_t)((k + 1) * CB + cl) * ld + (int64_t)k * CB + 16 * p;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sacc += col[u] * yk[16 * p + u];
+      }
+      sacc += __shfl_xor(sacc, 1, 64);
+      sacc += __shfl_xor(sacc, 2, 64);
+      sacc += __shfl_xor(sacc, 4, 64);
+      if (p == 0 && cl < ncol) bs[ko + CB + cl] -= sacc;
+    }
+    __syncthreads();
+  }
+}
+
+// b[c] -= Σ_{r in rows [r0, r1)} U(r, c) y(r) for columns c in [c0, c0 + nc): one wave per column
+// (contiguous rows), fixed-order wave reduction.
+__global__ __launch_bounds__(256) void chol_fwd_update_kernel(const double* __restrict__ G, int64_t ld, int64_t r0,
+                                                              int64_t r1, const double* __restrict__ y, int64_t c0,
+                                                              int64_t nc, double* __restrict__ b) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nc) return;
+  const double* col = G + (c0 + c) * ld;
+  double sacc = 0.0;
+  for (int64_t r = r0 + 2 * lane; r < r1; r += 128) {
+    const v2d u = *(const v2d*)(col + r);
+    const v2d yy = *(const v2d*)(y + r);
+    sacc += u[0] * yy[0] + u[1] * yy[1];
+  }
+  sacc = wave_sum(sacc);
+  if (lane == 0) b[c0 + c] -= sacc;
+}
+
+// U x = y restricted to rows [i0, i1), descending; y already reduced by the later outer
+// blocks.  Writes x[i0..i1).
+__global__ __launch_bounds__(SOLVE_NT) void chol_bwd_inner_kernel(const double* __restrict__ G, int64_t ld,
+                                                                   const double* __restrict__ W, int i0, int i1,
+                                                                   const double* __restrict__ yv,
+                                                                   double* __restrict__ x) {
+  __shared__ double ys[SOLVE_MAXB * CB];
+  __shared__ double part[8][CB];
+  __shared__ double xk[CB];
+  const int tid = threadIdx.x;
+  const int nr = (i1 - i0) * CB;
+  for (int r = tid; r < nr; r += SOLVE_NT) ys[r] = yv[(int64_t)i0 * CB + r];
+  __syncthreads();
+  for (int k = i1 - 1; k >= i0; --k) {
+    const int ko = (k - i0) * CB;
+    {  // x_k[t] = Σ_{u} W(t, u) y_k(u): thread (p, t), u in [16p, 16p+16), coalesced over t
+      const int t = tid & 127, p = tid >> 7;
+      const double* Wk = W + (int64_t)k * CB * CB;
+      double sacc = 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) sacc += Wk[(int64_t)(16 * p + u) * CB + t] * ys[ko + 16 * p + u];
+      part[p][t] = sacc;
+    }
+    __syncthreads();
+    if (tid < CB) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) sacc += part[p][tid];
+      xk[tid] = sacc;
+      x[(int64_t)k * CB + tid] = sacc;
+    }
+    __syncthreads();
+    // y_r -= Σ_t U(r, k·128 + t) x_k(t) for the rows of the earlier blocks of this outer block
+    const int nrow = ko;
+    for (int r = tid; r < nrow; r += SOLVE_NT) {
+      const double* row = G + (int64_t)k * CB * ld + (int64_t)i0 * CB + r;
+      double sacc = 0.0;
+#pragma unroll 8
+      for (int t = 0; t < CB; ++t) sacc += row[(int64_t)t * ld] * xk[t];
+      ys[r] -= sacc;
+    }
+    __syncthreads();
+  }
+}
+
+// y[r] -= Σ_{c in [c0, c1)} U(r, c) x(c) for rows r in [0, nr): 64 rows per workgroup,
+// 4 waves split the column range, partials summed in wave order.
+__global__ __launch_bounds__(256) void chol_bwd_update_kernel(const double* __restrict__ G, int64_t ld, int64_t c0,
+                                                              int64_t c1, const double* __restrict__ x, int64_t nr,
+                                                              double* __restrict__ y) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t len = (c1 - c0 + 3) / 4;
+  const int64_t ca = c0 + wv * len, cz = ca + len < c1 ? ca + len : c1;
+  double sacc = 0.0;
+  if (r < nr)
+    for (int64_t c = ca; c < cz; ++c) sacc += G[c * ld + r] * x[c];
+  part[wv][lane] = sacc;
+  __syncthreads();
+  if (wv == 0 && r < nr) y[r] -= ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
+// Solve G x = b given the factor; b (length mpad, zero-padded) is overwritten by x; y is
+// scratch (mpad).
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
                       hipStream_t st) {
   const int nblk = (int)(mpad / CB);
-  for (int k = 0; k < nblk; ++k) {
-    const int ncols = (nblk - k - 1) * CB;
-    const int grid = 1 + (int)ceil_div(ncols, 64);
-    hipLaunchKernelGGL(chol_fwd_step_kernel, dim3(grid), dim3(256), 0, st, G, ld, k, nblk, W, b, y);
+  // one 128-block per outer step measured fastest for the solves (m = 16384: 4.2 ms vs 6.6 ms
+  // with 8); SCS_SOLVE_OB overrides (A/B)
+  static const int sob = [] {
+    const char* e = getenv("SCS_SOLVE_OB");
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : (v > SOLVE_MAXB ? SOLVE_MAXB : v);
+  }();
+  const int OB = sob;
+  for (int i0 = 0; i0 < nblk; i0 += OB) {
+    const int i1 = i0 + OB < nblk ? i0 + OB : nblk;
+    hipLaunchKernelGGL(chol_fwd_inner_kernel, dim3(1), dim3(SOLVE_NT), 0, st, G, ld, W, i0, i1, b, y);
+    const int64_t nc = (int64_t)(nblk - i1) * CB;
+    if (nc > 0)
+      hipLaunchKernelGGL(chol_fwd_update_kernel, dim3((unsigned)ceil_div(nc, 4)), dim3(256), 0, st, G, ld,
+                         (int64_t)i0 * CB, (int64_t)i1 * CB, y, (int64_t)i1 * CB, nc, b);
   }
-  for (int k = nblk - 1; k >= 0; --k) {
-    const int grid = 1 + (int)ceil_div((int64_t)k * CB, 256);
-    hipLaunchKernelGGL(chol_bwd_step_kernel, dim3(grid), dim3(256), 0, st, G, ld, k, W, y, b);
+  // backward: outer blocks in descending order; the x of block [i0, i1) goes to b
+  const int nout = (nblk + OB - 1) / OB;
+  for (int q = nout - 1; q >= 0; --q) {
+    const int i0 = q * OB, i1 = i0 + OB < nblk ? i0 + OB : nblk;
+    hipLaunchKernelGGL(chol_bwd_inner_kernel, dim3(1), dim3(SOLVE_NT), 0, st, G, ld, W, i0, i1, y, b);
+    const int64_t nr = (int64_t)i0 * CB;
+    if (nr > 0)
+      hipLaunchKernelGGL(chol_bwd_update_kernel, dim3((unsigned)ceil_div(nr, 64)), dim3(256), 0, st, G, ld,
+                         (int64_t)i0 * CB, (int64_t)i1 * CB, b, nr, y);
   }
   return hipGetLastError();
 }

@@ -44,8 +44,15 @@ hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, do
                               hipStream_t st);
 
 // ---- chol.hip (upper Cholesky on MFMA; W holds the inverted diagonal blocks)
-hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const double* wpm,
-                       const int2* rowlist, const int2* trilist, int* info, hipStream_t st);
+struct CholAux {             // device constants of the two-level factorization (chol_aux_init)
+  double* w = nullptr;       // [128 x +1.0 | mpad x -1.0] Gram weights (panel solve | block updates)
+  int2* rect = nullptr;      // R x nblk rectangle tile lists, R = 1..4 (bj-major)
+  int nblk = 0;
+};
+hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);
+void chol_aux_free(CholAux* a);
+hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* aux,
+                       const int2* trilist, int* info, hipStream_t st);
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
                       hipStream_t st);
 

@@ -50,6 +50,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dtr, tr.data(), tr.size() * 8, hipMemcpyHostToDevice));
     std::vector<double> hw(256); for (int i = 0; i < 256; ++i) hw[i] = i < 128 ? 1.0 : -1.0;
     CK(hipMemcpy(wpm, hw.data(), 256 * 8, hipMemcpyHostToDevice));
+    scs::CholAux aux;
+    CK(scs::chol_aux_init(&aux, n, 0));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); float ms;
     // diag kernel alone, 64 launches on distinct blocks of a fresh copy
     CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
@@ -80,7 +82,7 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
       CK(hipMemset(info, 0, 4));
       CK(hipEventRecord(e0));
-      CK(scs::chol_factor(G, n, n, n, W, wpm, drl, dtr, info, 0));
+      CK(scs::chol_factor(G, n, n, n, W, &aux, dtr, info, 0));
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
       int hinfo; CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost));
       printf("n=%ld factor: %.2f ms (info %d)\n", (long)n, ms, hinfo);
@@ -96,6 +98,7 @@ int main(int argc, char** argv) {
     }
     CK(hipFree(G)); CK(hipFree(G0)); CK(hipFree(W)); CK(hipFree(b)); CK(hipFree(y)); CK(hipFree(info));
     CK(hipFree(drl)); CK(hipFree(dtr)); CK(hipFree(wpm));
+    scs::chol_aux_free(&aux);
   }
   return 0;
 }

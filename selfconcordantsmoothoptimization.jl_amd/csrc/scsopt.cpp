@@ -133,11 +133,10 @@ struct scs_ctx {
   int gseglen = 0, gncomb = 0, gnsplit = 1;
   double* gpart = nullptr;
   double* W = nullptr;      // inverted diagonal blocks of the Cholesky factor [mpad/128][128*128]
-  double* wpm = nullptr;    // [128 x +1.0, 128 x -1.0] Gram weights for the factorization
   double* ysol = nullptr;   // triangular-solve scratch (mpad)
-  int2* rowlist = nullptr;  // (0, j) tiles
   int2* trilist = nullptr;  // row-major lower tiles
   int* cinfo = nullptr;
+  CholAux caux;             // two-level factorization constants (chol.hip)
   rocblas_handle blas = nullptr;
   // GGN sample-space branch (N + 1 <= m): Aᵀ copy, sample Gram, (N+1)² system
   double *At = nullptr, *Ps = nullptr, *Ms = nullptr, *bS = nullptr, *uN = nullptr, *hvec = nullptr, *hg = nullptr;
@@ -433,18 +432,12 @@ void ensure_gram(scs_ctx* c) {
     const int nb2 = (int)(mp / 128);
     c->W = dalloc<double>(c, (size_t)mp * 128);
     c->ysol = dalloc<double>(c, mp);
-    c->wpm = dalloc<double>(c, 256);
-    std::vector<double> hw(256);
-    for (int i = 0; i < 256; ++i) hw[i] = i < 128 ? 1.0 : -1.0;
-    h2d(c, c->wpm, hw.data(), 256);
-    std::vector<int2> rl(nb2), tr((size_t)nb2 * (nb2 + 1) / 2);
-    for (int j = 0; j < nb2; ++j) rl[j] = make_int2(0, j);
+    std::vector<int2> tr((size_t)nb2 * (nb2 + 1) / 2);
     gram_tile_list_rowmajor(nb2, tr.data());
-    c->rowlist = dalloc<int2>(c, nb2);
     c->trilist = dalloc<int2>(c, tr.size());
-    HCK(hipMemcpyAsync(c->rowlist, rl.data(), sizeof(int2) * nb2, hipMemcpyHostToDevice, c->st));
     HCK(hipMemcpyAsync(c->trilist, tr.data(), sizeof(int2) * tr.size(), hipMemcpyHostToDevice, c->st));
     c->cinfo = dalloc<int>(c, 1);
+    HCK(chol_aux_init(&c->caux, mp, c->st));
   }
   c->dinfo = dalloc<rocblas_int>(c, 1);
   c->ipiv = dalloc<rocblas_int>(c, mp);
@@ -656,7 +649,7 @@ void solve_system(scs_ctx* c, double* rhs) {
   tbegin(c, T_SOLVE, &e0);
   HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
   HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
-  HCK(chol_factor(c->G, ld, m, ld, c->W, c->wpm, c->rowlist, c->trilist, c->cinfo, c->st));
+  HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
   int info = 0;
   HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
@@ -1025,11 +1018,10 @@ static void reset_data(scs_ctx* c) {
   c->gseglen = c->gncomb = 0;
   c->gnsplit = 1;
   dfree_t(c, c->W);
-  dfree_t(c, c->wpm);
   dfree_t(c, c->ysol);
-  dfree_t(c, c->rowlist);
   dfree_t(c, c->trilist);
   dfree_t(c, c->cinfo);
+  chol_aux_free(&c->caux);
   dfree_t(c, c->dinfo);
   dfree_t(c, c->ipiv);
   c->ntiles = c->nslots = 0;
