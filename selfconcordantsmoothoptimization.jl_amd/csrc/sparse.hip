@@ -38,11 +38,13 @@ constexpr int SPB_MAXSHIFT = 14;
 constexpr int SPB_THREADS = 1024;
 constexpr int SPB_ROWS = 1024;   // rows per workgroup
 
-// One wave works on RW rows at a time (rows r, r + 16, ...): the RW rows' pointer
-// pairs, then all RW*U (index, value) loads are issued before any use, which
-// keeps RW*U*64 loads per wave in flight (the kernel runs at one workgroup per
-// CU because of the 128 KiB LDS slice).  Per row the summation order is the
-// same as one row at a time (lane-ascending p, then the wave butterfly).
+// One wave works on RW rows at a time (of its 64 contiguous rows): all RW*U (index,
+// value) loads of a round are issued before any use,
+// masked per lane (clamped addresses), so a row segment of up to 64*U entries --
+// the common case: ~164 per (row, block) at C5 in both directions -- costs one
+// round with RW*U*64 loads per wave in flight (the kernel runs at one workgroup per
+// CU because of the 128 KiB LDS slice).  Per row the summation order is fixed
+// (lane-ascending p, then the wave butterfly).
 template <typename VT, int U, int RW>
 __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
                                                                const uint16_t* __restrict__ lidx,
@@ -51,71 +53,76 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
                                                                int64_t ncols, int shift, double* __restrict__ out,
                                                                int64_t ldo) {
   __shared__ double xs[1 << SPB_MAXSHIFT];
-  constexpr int NW = SPB_THREADS / 64;
   const int b = blockIdx.y;
   const int64_t c0 = (int64_t)b << shift;
   const int nb = (int)min((int64_t)1 << shift, ncols - c0);
-  for (int i = threadIdx.x; i < nb; i += SPB_THREADS) xs[i] = x[c0 + i];
+  // stage the slice: all loads of a thread in flight before the LDS stores (a plain
+  // load->store loop serializes 16 L2 round trips while every wave waits at the barrier)
+  {
+    constexpr int PER = (1 << SPB_MAXSHIFT) / SPB_THREADS;
+    double t[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * SPB_THREADS;
+      t[k] = (i < nb) ? x[c0 + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) xs[threadIdx.x + k * SPB_THREADS] = t[k];
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t* pb = ptr + (int64_t)b * nrows;
   const int64_t r1 = min(nrows, (int64_t)(blockIdx.x + 1) * SPB_ROWS);
-  for (int64_t rb = (int64_t)blockIdx.x * SPB_ROWS + wv; rb < r1; rb += NW * RW) {
-    int64_t p0[RW], p1[RW], p[RW];
+  // each wave owns 64 contiguous rows: their pointer pairs are loaded once (lane k: row
+  // rw0 + k, coalesced) and broadcast per round with readlane, so a round waits on one
+  // memory latency (its data loads), not two
+  const int64_t rw0 = (int64_t)blockIdx.x * SPB_ROWS + (int64_t)wv * 64;
+  const int64_t myr = rw0 + lane;
+  const int64_t mp0 = (myr < r1) ? pb[myr] : 0, mp1 = (myr < r1) ? pb[myr + 1] : 0;
+  const int nrw = (int)max((int64_t)0, min((int64_t)64, r1 - rw0));
+  for (int k0 = 0; k0 < nrw; k0 += RW) {
+    // per row: wave-uniform base pointers (SGPRs) + 32-bit lane offsets, so 24 loads in
+    // flight do not need 24 64-bit address pairs
+    const uint16_t* li[RW];
+    const VT* va[RW];
+    int len[RW];
     double acc[RW];
+    int rem = 0;   // longest segment of the group (wave-uniform)
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
-      const int64_t r = rb + (int64_t)j * NW;
-      p0[j] = (r < r1) ? pb[r] : 0;
-      p1[j] = (r < r1) ? pb[r + 1] : 0;
-      p[j] = p0[j] + lane;
+      const int k = k0 + j;   // rows past nrw have mp0 = mp1 = 0 -> empty
+      const int64_t a0 = ((int64_t)__builtin_amdgcn_readlane((int)(mp0 >> 32), k) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)mp0, k);
+      const int64_t a1 = ((int64_t)__builtin_amdgcn_readlane((int)(mp1 >> 32), k) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)mp1, k);
+      len[j] = (int)(a1 - a0);
+      li[j] = len[j] > 0 ? lidx + a0 : lidx;   // empty rows read element 0 (masked)
+      va[j] = len[j] > 0 ? val + a0 : val;
       acc[j] = 0.0;
+      rem = max(rem, len[j]);
     }
-    // full rounds while every row of the group still has one
-    bool more = true;
-    while (more) {
-#pragma unroll
-      for (int j = 0; j < RW; ++j) more = more && (p[j] + 64 * (U - 1) < p1[j]);
-      if (!more) break;
+    for (int o = lane; o - lane < rem; o += 64 * U) {
       int id[RW][U];
       double v[RW][U];
 #pragma unroll
       for (int j = 0; j < RW; ++j)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          id[j][u] = lidx[p[j] + 64 * u];
-          v[j][u] = (double)val[p[j] + 64 * u];
+          const int q = max(min(o + 64 * u, len[j] - 1), 0);
+          id[j][u] = li[j][q];
+          v[j][u] = (double)va[j][q];
         }
 #pragma unroll
-      for (int j = 0; j < RW; ++j) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc[j] += v[j][u] * xs[id[j][u]];
-        p[j] += 64 * U;
-      }
-    }
-    // remaining rounds, row by row (clamped addresses, masked terms)
-#pragma unroll
-    for (int j = 0; j < RW; ++j) {
-      while (p0[j] < p1[j] && p[j] - lane < p1[j]) {
-        int id[U];
-        double v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int64_t q = min(p[j] + 64 * u, p1[j] - 1);
-          id[u] = lidx[q];
-          v[u] = (double)val[q];
-        }
+      for (int j = 0; j < RW; ++j)
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (p[j] + 64 * u < p1[j]) acc[j] += v[u] * xs[id[u]];
-        p[j] += 64 * U;
-      }
+          if (o + 64 * u < len[j]) acc[j] += v[j][u] * xs[id[j][u]];
     }
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
       const double a = wave_sum(acc[j]);
-      const int64_t r = rb + (int64_t)j * NW;
-      if (lane == 0 && r < r1) out[(int64_t)b * ldo + r] = a;
+      const int k = k0 + j;
+      if (lane == 0 && k < nrw) out[(int64_t)b * ldo + rw0 + k] = a;
     }
   }
 }
@@ -133,19 +140,21 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
   const int nblk = (int)ceil_div(ncols, (int64_t)1 << shift);
   const dim3 grid((unsigned)ceil_div(nrows, SPB_ROWS), (unsigned)nblk);
   const int64_t avg = nnz / (nrows * nblk);
+  // short segments (C5: ~164 entries per row and block): 3 x 64 slots, 8 rows per round;
+  // long ones: 8 x 64 slots, 2 rows
   if (f32) {
-    if (avg <= 64 * 4)
-      hipLaunchKernelGGL((spmv_blk_kernel<float, 4, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
+    if (avg <= 64 * 3)
+      hipLaunchKernelGGL((spmv_blk_kernel<float, 3, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
                          x, nrows, ncols, shift, out, ldo);
     else
-      hipLaunchKernelGGL((spmv_blk_kernel<float, 16, 1>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
+      hipLaunchKernelGGL((spmv_blk_kernel<float, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
                          x, nrows, ncols, shift, out, ldo);
   } else {
-    if (avg <= 64 * 4)
-      hipLaunchKernelGGL((spmv_blk_kernel<double, 4, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+    if (avg <= 64 * 3)
+      hipLaunchKernelGGL((spmv_blk_kernel<double, 3, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
                          (const double*)val, x, nrows, ncols, shift, out, ldo);
     else
-      hipLaunchKernelGGL((spmv_blk_kernel<double, 16, 1>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+      hipLaunchKernelGGL((spmv_blk_kernel<double, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
                          (const double*)val, x, nrows, ncols, shift, out, ldo);
   }
   return hipGetLastError();
