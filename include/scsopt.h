@@ -183,6 +183,29 @@ int scs_eval_reg(scs_ctx* ctx, const double* x, double* gval);
 int scs_step(scs_ctx* ctx, const double* x, const double* x_prev, int64_t iter,
              double* x_new, double* dx, double* pri_res_norm);
 
+/* ---- loop level  (iterate!(method, model, reg_name, hμ; max_epoch, x_tol,
+ * f_tol) -> Solution, iterate.jl:56-76 / optim_loop! :100-267) ------------ */
+/* History arrays of a Solution (iterate.jl:3-32), caller-owned, capacity
+ * max_epoch + 1 each (times may be NULL).  pri_res_norm[0] is the
+ * reference's `nothing` (NaN).                                              */
+typedef struct scs_history {
+  double* obj;
+  double* fval;
+  double* pri_res_norm;
+  double* rel;      /* rel_error: max(‖x − x*‖ / max(‖x*‖, 1), x_tol), or the
+                       mean_square_error for reg "gl" (rel_kind = 1)       */
+  double* objrel;   /* f_rel_error: max(|obj − obj*| / |obj*|, f_tol)       */
+  double* times;    /* seconds since the start, millisecond resolution       */
+} scs_history;
+/* Full-batch optim_loop! on the device: init! + per epoch f(x) + get_reg(x)
+ * + step!, the reference's termination tests and history pushes.  x_star is
+ * model.x (the comparison solution).  Outputs: final x, *n_hist entries,
+ * *epochs (Solution.epochs).  Metrics / test data / verbose printing stay in
+ * the host loop (scsopt.iterate).  Requires scs_method_init.                */
+int scs_iterate(scs_ctx* ctx, const double* x0, const double* x_star, int64_t max_epoch, double x_tol,
+                double f_tol, int rel_kind, double* x_out, const scs_history* hist, int64_t* n_hist,
+                int64_t* epochs);
+
 /* ---- kernel-level entry points (parity tests) --------------------------- */
 /* hμ.grad(Cmat, x), hμ.hess(Cmat, x)                                       */
 int scs_smoother_eval(scs_ctx* ctx, const double* x, double* gr, double* Hr);

@@ -13,11 +13,13 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -1493,6 +1495,123 @@ int scs_step(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, do
       step_newton(c, x, iter, xnew_h.data(), dx, pri);
     std::memcpy(x_new, xnew_h.data(), sizeof(double) * c->m);
     tend(c, T_STEP, e0);
+    if (c->timing) tresolve(c);
+  });
+}
+
+// optim_loop! (iterate.jl:100-267), full-batch, in C++ around the same device calls the
+// per-call entry points make (f(x) + get_reg(x) + step! per epoch), so a caller pays one
+// ABI crossing per solve instead of three per epoch.  Histories follow iterate.jl exactly:
+// one push per epoch (the pre-step values), the duplicated entry at max_epoch
+// (:219-231) or the post-step entry on termination (:235-247); pri_res_norm[0] is
+// `nothing` (NaN here).  Termination uses the pre-step f_rel_error (:234, :257).
+int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_epoch, double x_tol, double f_tol,
+                int rel_kind, double* x_out, const scs_history* h, int64_t* n_hist, int64_t* epochs_out) {
+  return guarded(c, [&] {
+    require_ready(c, true);
+    if (!x0 || !x_star || !x_out || !h || !n_hist || !epochs_out) fail(c, SCS_ERR_ARG, "scs_iterate: null argument");
+    if (max_epoch < 1) fail(c, SCS_ERR_ARG, "scs_iterate: max_epoch must be >= 1");
+    HCK(hipSetDevice(c->dev));
+    const int64_t m = c->m;
+    auto nrm = [&](const double* a, const double* b) {   // ‖a − b‖ (b may be null)
+      double s2 = 0.0;
+      for (int64_t i = 0; i < m; ++i) {
+        const double d = b ? a[i] - b[i] : a[i];
+        s2 += d * d;
+      }
+      return std::sqrt(s2);
+    };
+    auto jmax = [](double a, double b) {   // Julia max: NaN propagates, -0.0 < +0.0
+      if (std::isnan(a)) return a;
+      if (std::isnan(b)) return b;
+      return (b < a || (std::signbit(b) && !std::signbit(a))) ? a : b;
+    };
+    auto f_of = [&](const double* xx) {
+      h2d(c, c->xn, xx, m);
+      return eval_f_dev(c, xx, c->xn);
+    };
+    auto reg_of = [&](const double* xx) {
+      h2d(c, c->xn, xx, m);
+      return eval_reg_dev(c, c->xn);
+    };
+    const double nstar = nrm(x_star, nullptr);
+    auto rel_of = [&](const double* xx) {
+      if (rel_kind == 1) {   // mean_square_error (utils.jl:3-5), the "gl" rel_error
+        double s2 = 0.0;
+        for (int64_t i = 0; i < m; ++i) s2 += (x_star[i] - xx[i]) * (x_star[i] - xx[i]);
+        return s2 / (double)m;
+      }
+      return jmax(nrm(xx, x_star) / jmax(nstar, 1.0), x_tol);
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    auto now = [&] {   // Dates.now() differences: millisecond resolution
+      const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      return std::floor(sec * 1000.0) / 1000.0;
+    };
+    const double obj_star = f_of(x_star) + reg_of(x_star);
+    auto frel_of = [&](double ob) { return jmax(std::fabs(ob - obj_star) / std::fabs(obj_star), f_tol); };
+    int64_t nh = 0;
+    auto push = [&](double ob, double fv, double pr, double rl, double fr, double dt) {
+      h->obj[nh] = ob;
+      h->fval[nh] = fv;
+      h->pri_res_norm[nh] = pr;
+      h->rel[nh] = rl;
+      h->objrel[nh] = fr;
+      if (h->times) h->times[nh] = dt;
+      ++nh;
+    };
+    // init!(method, x): reset the method state (prox-L-BFGS-SCORE.jl:31-36)
+    c->ring.clear();
+    c->spare = 0;
+    c->H0 = 1.0;
+    invalidate_caches(c);
+    std::vector<double> x(x0, x0 + m), x_prev = x, x_new(m);
+    double pri = std::numeric_limits<double>::quiet_NaN();
+    int64_t epochs = 0;
+    for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
+      double dt = now();
+      double fval = f_of(x.data());
+      double obj = fval + reg_of(x.data());
+      double rel = rel_of(x.data());
+      double frel = frel_of(obj);
+      push(obj, fval, pri, rel, frel, dt);
+      if (epoch == max_epoch) {
+        dt = now();
+        fval = f_of(x.data());
+        obj = fval + reg_of(x.data());
+        rel = rel_of(x.data());
+        push(obj, fval, pri, rel, frel_of(obj), dt);
+      }
+      hipEvent_t e0;
+      tbegin(c, T_STEP, &e0);
+      h2d(c, c->x, x.data(), m);
+      h2d(c, c->xp, x_prev.data(), m);
+      if (c->method == SCS_PROX_LQNSCORE)
+        step_lqn(c, x.data(), x_prev.data(), epoch, x_new.data(), nullptr, &pri);
+      else
+        step_newton(c, x.data(), epoch, x_new.data(), nullptr, &pri);
+      tend(c, T_STEP, e0);
+      const double nx = nrm(x.data(), nullptr);
+      if (nrm(x_new.data(), x.data()) < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol) {
+        if (epoch != max_epoch) {   // iterate.jl:235-247
+          dt = now();
+          fval = f_of(x_new.data());
+          obj = fval + reg_of(x_new.data());
+          rel = rel_of(x_new.data());
+          push(obj, fval, pri, rel, frel_of(obj), dt);
+        }
+        ++epochs;
+      }
+      x_prev.swap(x);
+      x = x_new;
+      if (nrm(x.data(), x_prev.data()) < x_tol * std::max(nrm(x_prev.data(), nullptr), 1.0) || frel <= f_tol ||
+          pri < x_tol)
+        break;   // iterate.jl:257-259
+      ++epochs;
+    }
+    std::memcpy(x_out, x.data(), sizeof(double) * m);
+    *n_hist = nh;
+    *epochs_out = epochs;
     if (c->timing) tresolve(c);
   });
 }

@@ -127,4 +127,28 @@ function step!(method::ProximalMethod, model::DeviceProblem, reg_name, hμ, As, 
     return return_dx ? (x_new, dx, pri[]) : (x_new, pri[])
 end
 
+# iterate!(method, model::DeviceProblem, reg_name, hμ; max_epoch, x_tol, f_tol): optim_loop!
+# (iterate.jl:100-267) as ONE ccall (scs_iterate) -- no per-epoch host round trips.  Returns the
+# reference's Solution (iterate.jl:3-32); pri_res_norm[1] is `nothing` as in the reference.
+function iterate_device!(method::ProximalMethod, model::DeviceProblem, reg_name::String, hμ;
+                         α=nothing, max_epoch=1000, x_tol=1e-10, f_tol=1e-10)
+    α === nothing || (model.L = 1 / α)                 # iterate.jl:113-115
+    configure!(model, reg_name, hμ)
+    init_device!(method, model)
+    cap = max_epoch + 1
+    obj, fval, pri, rel, objrel, tms = (Vector{Float64}(undef, cap) for _ in 1:6)
+    hist = (pointer(obj), pointer(fval), pointer(pri), pointer(rel), pointer(objrel), pointer(tms))
+    x_out = similar(model.x0); nh = Ref{Int64}(0); ep = Ref{Int64}(0)
+    GC.@preserve obj fval pri rel objrel tms begin
+        chk(ccall((:scs_iterate, lib), Cint,
+                  (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Cint, Ptr{Float64},
+                   Ref{NTuple{6,Ptr{Float64}}}, Ref{Int64}, Ref{Int64}),
+                  model.ctx, model.x0, model.x, max_epoch, x_tol, f_tol, reg_name == "gl" ? 1 : 0, x_out,
+                  hist, nh, ep), model.ctx)
+    end
+    n = nh[]
+    pris = Any[isnan(pri[i]) && i == 1 ? nothing : pri[i] for i in 1:n]
+    return Solution(x_out, obj[1:n], fval[1:n], pris, [], rel[1:n], objrel[1:n], Dict(), tms[1:n], ep[], model)
+end
+
 end # module

@@ -57,6 +57,12 @@ class Timing(C.Structure):
                 ("reduce_ms", C.c_double), ("reduce_calls", C.c_int64)]
 
 
+class History(C.Structure):
+    _fields_ = [("obj", C.POINTER(C.c_double)), ("fval", C.POINTER(C.c_double)),
+                ("pri_res_norm", C.POINTER(C.c_double)), ("rel", C.POINTER(C.c_double)),
+                ("objrel", C.POINTER(C.c_double)), ("times", C.POINTER(C.c_double))]
+
+
 _SIGS = {
     "scs_version": (C.c_char_p, []),
     "scs_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
@@ -85,6 +91,8 @@ _SIGS = {
     "scs_eval_grad": (C.c_int, [C.c_void_p, c_dp, c_dp]),
     "scs_eval_reg": (C.c_int, [C.c_void_p, c_dp, c_dp]),
     "scs_step": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, c_dp, c_dp, c_dp]),
+    "scs_iterate": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, C.c_double, C.c_double, C.c_int, c_dp,
+                              C.POINTER(History), c_i64p, c_i64p]),
     "scs_smoother_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, c_dp]),
     "scs_prox_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_double, C.c_double, c_dp]),
     "scs_gram_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64]),

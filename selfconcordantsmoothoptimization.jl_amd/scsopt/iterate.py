@@ -80,14 +80,54 @@ def init_method(method, model):
 
 def iterate(method: ProximalMethod, model, reg_name, hmu, *, metrics=None, alpha=None, batch_size=None,
             slice_samples=False, shuffle_batch=True, max_epoch=1000, comm_rounds=100, local_max_iter=None,
-            x_tol=1e-10, f_tol=1e-10, verbose=1):
-    """iterate!(method, model, reg_name, hμ; kwargs...) (iterate.jl:56-76)."""
+            x_tol=1e-10, f_tol=1e-10, verbose=1, device_loop=None):
+    """iterate!(method, model, reg_name, hμ; kwargs...) (iterate.jl:56-76).
+
+    device_loop: run optim_loop! inside libscsopt (scs_iterate: one ABI call per solve);
+    the default (None) does so whenever nothing needs the host per epoch (no metrics,
+    verbose <= 1).  False forces the host restatement below (same device calls)."""
     if local_max_iter is not None:
         max_epoch = 1
     if batch_size is not None or slice_samples:
         raise NotImplementedError("minibatch / slice_samples paths are not on the device yet (SURVEY §8f rank 3)")
+    if device_loop is None:
+        device_loop = not metrics and verbose <= 1
+    if device_loop:
+        if metrics or verbose > 1:
+            raise ValueError("device_loop runs without per-epoch metrics / printing")
+        return device_optim_loop(method, model, reg_name, hmu, alpha=alpha, max_epoch=max_epoch, x_tol=x_tol,
+                                 f_tol=f_tol, verbose=verbose)
     return optim_loop(method, model, reg_name, hmu, metrics=metrics, alpha=alpha, max_epoch=max_epoch,
                       x_tol=x_tol, f_tol=f_tol, verbose=verbose)
+
+
+def device_optim_loop(method, model, reg_name, hmu, *, alpha=None, max_epoch=1000, x_tol=1e-10, f_tol=1e-10,
+                      verbose=1):
+    """optim_loop! (iterate.jl:100-267) as one scs_iterate call; same Solution as optim_loop."""
+    implemented = []
+    method.set_name(implemented)
+    if alpha is not None:
+        model.L = 1 / alpha                                   # iterate.jl:113-115
+    if method.name in implemented and method.ss_type == 1 and model.L is None and verbose > 0:
+        print("[ Info: Neither L nor α is set for the problem... Now fixing α = 0.5...", file=sys.stderr)
+    model.configure(reg_name, hmu)
+    init_method(method, model)
+    m = model.m
+    cap = int(max_epoch) + 1
+    hist = {k: np.empty(cap) for k in ("obj", "fval", "pri_res_norm", "rel", "objrel", "times")}
+    h = _lib.History(*(dptr(hist[k]) for k in ("obj", "fval", "pri_res_norm", "rel", "objrel", "times")))
+    x0 = np.ascontiguousarray(model.x0, dtype=np.float64)
+    xs = np.ascontiguousarray(model.x, dtype=np.float64)
+    x_out = np.empty(m)
+    nh, ep = C.c_int64(), C.c_int64()
+    model.ctx.check(_lib.lib.scs_iterate(model.ctx.h, dptr(x0), dptr(xs), int(max_epoch), float(x_tol), float(f_tol),
+                                         1 if reg_name == "gl" else 0, dptr(x_out), C.byref(h), C.byref(nh),
+                                         C.byref(ep)))
+    n = int(nh.value)
+    pris = [None if (i == 0 and math.isnan(v)) else float(v) for i, v in enumerate(hist["pri_res_norm"][:n])]
+    as_list = lambda k: [float(v) for v in hist[k][:n]]   # noqa: E731
+    return Solution(x_out, as_list("obj"), as_list("fval"), pris, [], as_list("rel"), as_list("objrel"), {},
+                    as_list("times"), int(ep.value), model)
 
 
 def _show(opt_verbose, label, tag, epoch, obj, fval, pri, rel, dt):

@@ -290,6 +290,34 @@ def test_group_lasso_ggn():
     np.testing.assert_allclose(sol.rel, osol.rel, rtol=1e-6)
 
 
+@pytest.mark.parametrize("method,reg,kw", [("ggn", "l1", {}), ("nscore", "l1", {}), ("lqn", "l1", {"m": 5}),
+                                           ("lqn", "indbox", {"m": 5, "ss_type": 2})])
+def test_device_loop_matches_host_loop(method, reg, kw):
+    """scs_iterate (optim_loop! in libscsopt) == the host restatement over the same device calls:
+    identical objective / fval / pri_res_norm histories and epochs (same kernels, same order),
+    rel_error to rounding of the host norm; plus a terminating run (x_tol hit before max_epoch)."""
+    N, m = 2048, 192
+    x0 = np.random.default_rng(5).standard_normal(m) * 0.3
+    if method == "ggn":
+        f, out, kind, meth = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N), 1, scsopt.ProxGGNSCORE
+    elif method == "nscore":
+        f, out, kind, meth = losses.logistic_margin(1.0 / N), None, 2, scsopt.ProxNSCORE
+    else:
+        f, out, kind, meth = losses.least_squares(1.0 / N), None, 3, scsopt.ProxLQNSCORE
+    C_set = [-1.0, 1.0] if reg == "indbox" else None
+    p = scsopt.Problem.synthetic(N, m, x0, f, 1e-3, kind=kind, seed=7, out_fn=out, C_set=C_set)
+    hm = scsopt.PHuberSmootherIndBox(-1.0, 1.0, 0.5) if reg == "indbox" else scsopt.PHuberSmootherL1L2(1.0)
+    for max_epoch, x_tol in ((9, 1e-10), (200, 1e-6)):
+        a = scsopt.iterate(meth(**kw), p, reg, hm, max_epoch=max_epoch, x_tol=x_tol, verbose=0, device_loop=True)
+        b = scsopt.iterate(meth(**kw), p, reg, hm, max_epoch=max_epoch, x_tol=x_tol, verbose=0, device_loop=False)
+        assert a.epochs == b.epochs and len(a.obj) == len(b.obj)
+        assert a.obj == b.obj and a.fval == b.fval and a.pri_res_norm == b.pri_res_norm
+        assert np.array_equal(bits(a.x), bits(b.x))
+        np.testing.assert_allclose(a.rel, b.rel, rtol=1e-13)
+        np.testing.assert_allclose(a.objrel, b.objrel, rtol=1e-12)
+        assert len(a.times) == len(a.obj) and a.metricvals == {}
+
+
 def test_determinism():
     _, _, s1, _ = _synthetic_pair("ggn", N=2048, m=128, max_epoch=4)
     _, _, s2, _ = _synthetic_pair("ggn", N=2048, m=128, max_epoch=4)
