@@ -63,7 +63,11 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_matches_single_process():
+@pytest.mark.parametrize("tall", ["0", "1"])
+def test_two_rank_shard_matches_single_process(tall, monkeypatch):
+    """tall = "1" forces the 256 x 128 LDS-DMA Gram kernel (the C3/C2 kernel) at this small m, so the
+    packed multi-rank slots of its tile halves (gram_unpack) are exercised too."""
+    monkeypatch.setenv("SCS_GRAM_TALL", tall)
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
