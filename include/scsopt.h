@@ -58,12 +58,15 @@ enum scs_ggn_kind {
  * prox-operators.jl:68-79).                                                 */
 enum scs_reg_kind { SCS_REG_L1 = 1, SCS_REG_L2 = 2, SCS_REG_INDBOX = 3, SCS_REG_GL = 4 };
 
-/* Smoother types (phuber-smooth.jl, exponential-smooth.jl).                 */
+/* Smoother types (src/regularizers/: the *-smooth.jl files).                 */
 enum scs_smoother_kind {
   SCS_SMOOTH_PHUBER_L1L2 = 1,   /* PHuberSmootherL1L2(μ)          phuber-smooth.jl:27   */
   SCS_SMOOTH_PHUBER_INDBOX = 2, /* PHuberSmootherIndBox(lb,ub,μ)  phuber-smooth.jl:59   */
   SCS_SMOOTH_PHUBER_GL = 3,     /* PHuberSmootherGL(μ, problem)   phuber-smooth.jl:137  */
-  SCS_SMOOTH_EXP_INDBOX = 4     /* ExponentialSmootherIndBox      exponential-smooth.jl:28 */
+  SCS_SMOOTH_EXP_INDBOX = 4,    /* ExponentialSmootherIndBox      exponential-smooth.jl:28 */
+  SCS_SMOOTH_LOGEXP_INDBOX = 5, /* LogExpSmootherIndBox(lb,ub,μ)  log-exp-smooth.jl:28 */
+  SCS_SMOOTH_OSBA_L1L2 = 6,     /* OsBaSmootherL1L2(μ)            ostrovskii-bach-smooth.jl:27 */
+  SCS_SMOOTH_OSBA_GL = 7        /* OsBaSmootherGL(μ, problem)     ostrovskii-bach-smooth.jl:59 */
 };
 
 /* ProximalMethod subtypes (src/algorithms/prox-*-SCORE.jl).                 */

@@ -1388,14 +1388,16 @@ int scs_set_smoother(scs_ctx* c, int kind, double mu, double Mh, double nu, cons
                      int64_t nbound) {
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the smoother");
-    if (kind < SCS_SMOOTH_PHUBER_L1L2 || kind > SCS_SMOOTH_EXP_INDBOX) fail(c, SCS_ERR_ARG, "unknown smoother %d", kind);
-    if (kind == SCS_SMOOTH_PHUBER_INDBOX || kind == SCS_SMOOTH_EXP_INDBOX) {
+    if (kind < SCS_SMOOTH_PHUBER_L1L2 || kind > SCS_SMOOTH_OSBA_GL) fail(c, SCS_ERR_ARG, "unknown smoother %d", kind);
+    if (kind == SCS_SMOOTH_PHUBER_INDBOX || kind == SCS_SMOOTH_EXP_INDBOX || kind == SCS_SMOOTH_LOGEXP_INDBOX) {
       if (!lb || !ub || (nbound != 1 && nbound != c->m))
         fail(c, SCS_ERR_REF, "Lengths of the bounds do not match that of the variable.");
       c->slb = upload_bounds(c, c->slb, lb, nbound, true, true);
       c->sub = upload_bounds(c, c->sub, ub, nbound, true, false);
     }
-    if (kind == SCS_SMOOTH_PHUBER_GL && !c->wel) fail(c, SCS_ERR_STATE, "PHuberSmootherGL needs the gl groups (scs_set_reg)");
+    if ((kind == SCS_SMOOTH_PHUBER_GL || kind == SCS_SMOOTH_OSBA_GL) && !c->wel)
+      fail(c, SCS_ERR_STATE, "%s needs the gl groups (scs_set_reg)",
+           kind == SCS_SMOOTH_PHUBER_GL ? "PHuberSmootherGL" : "OsBaSmootherGL");
     c->smooth = kind;
     c->mu = mu;
     c->Mh = Mh;

@@ -8,6 +8,10 @@
 // bitwise identical.  Expressions follow the reference's evaluation order
 // so that, on identical inputs, elementwise outputs match the oracle bit for
 // bit (IEEE +,-,*,/,sqrt); pow() may differ by <= 1-2 ulp from Julia's.
+// Julia evaluates a*b + c with two roundings (no @muladd / @fastmath on the reference path), and
+// hipcc contracts to FMA by default: keep the roundings separate in these elementwise semantics
+// kernels (it decides exact zeros, e.g. the 0/0 = NaN of the Ostrovskii-Bach gradient at x = 0).
+#pragma clang fp contract(off)
 #include <algorithm>
 #include <utility>
 
@@ -31,6 +35,27 @@ __device__ __forceinline__ double huber_hess_d(double x, double mu) {   // phube
 __device__ __forceinline__ double pseudo_huber_d(double x, double mu) { // phuber-smooth.jl:28-30
   const double v = mu * mu + x * x;
   return (mu * mu - mu * sqrt(v) + x * x) * pow(v, -0.5);
+}
+
+// Ostrovskii & Bach (ostrovskii-bach-smooth.jl:28-36), λ = 1.  Julia literal powers: x^2,
+// μ^3 are products; x^5 is the accurate Float64^Int power (pow here); (·)^(-1//2) is pow(·,-0.5).
+// x = 0 gives 0/0 = NaN, propagated as the reference does.
+__device__ __forceinline__ double osba_val_d(double x, double mu) {   // ostrovskii-bach-smooth.jl:28-30
+  const double s = sqrt(mu * mu + 4.0 * (x * x));
+  return (((s / 2.0 - mu / 2.0) + mu * log((2.0 * x - s + mu) / x) / 2.0) - 0.6931471805599453 * mu) +
+         mu * log((s - mu + 2.0 * x) / x) / 2.0;
+}
+__device__ __forceinline__ double osba_grad_d(double x, double mu) {   // ostrovskii-bach-smooth.jl:31-33
+  const double x2 = x * x, mu2 = mu * mu;
+  const double s = sqrt(mu2 + 4.0 * x2);
+  const double A = ((-(mu2 * mu) + mu2 * s) - 4.0 * x2 * mu) + 2.0 * x2 * s;
+  const double B = (mu * s + mu2) + 4.0 * x2;
+  const double C = 4.0 * mu2 * (x2 * x) + 16.0 * pow(x, 5.0);
+  return A * B / C;
+}
+__device__ __forceinline__ double osba_hess_d(double x, double mu) {   // ostrovskii-bach-smooth.jl:34-36
+  const double v = mu * mu + 4.0 * (x * x);
+  return (sqrt(v) - mu) * mu / (x * x) * pow(v, -0.5) / 2.0;
 }
 
 __global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64_t m, double mu,
@@ -63,6 +88,17 @@ __global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64
     } else {
       h = __builtin_nan("");  // NaN x: the reference leaves the entry undefined
     }
+  } else if (kind == SCS_SMOOTH_LOGEXP_INDBOX) {   // log-exp-smooth.jl:45-61 (both ifelse arms, then +)
+    const double ai = a[i], bi = b[i];
+    const double g1 = (xi <= ai + mu) ? (xi - ai - 2.0 * mu) / mu : ((xi >= bi - mu) ? (xi - bi + 2.0 * mu) / mu : 0.0);
+    const double g2 = (xi < ai) ? mu / (ai - xi) : ((xi > bi) ? -mu / (bi - xi) : 0.0);
+    g = g1 + g2;
+    const double h1 = (xi <= ai + mu) ? 1.0 / mu : ((xi >= bi - mu) ? 1.0 / mu : 0.0);
+    const double h2 = (xi < ai) ? mu / ((ai - xi) * (ai - xi)) : ((xi > bi) ? mu / ((bi - xi) * (bi - xi)) : 0.0);
+    h = h1 + h2;
+  } else if (kind == SCS_SMOOTH_OSBA_L1L2) {   // ostrovskii-bach-smooth.jl:27
+    g = osba_grad_d(xi, mu);
+    h = osba_hess_d(xi, mu);
   } else {  // SCS_SMOOTH_EXP_INDBOX (exponential-smooth.jl:41-50)
     const double e = exp((-xi + a[i]) / mu);
     g = -e;
@@ -75,24 +111,30 @@ __global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64
 // PHuberSmootherGL grad/hess (phuber-smooth.jl:150-164).  Cmat for a
 // contiguous partition is diag(group weight); the Hessian carries the global
 // dot(Dg, Dg).  Single workgroup: the dot is one fixed-order reduction.
+// OSBA = true: OsBaSmootherGL (ostrovskii-bach-smooth.jl:73-87), the same composition with the
+// Ostrovskii-Bach value / grad / hess.
+template <bool OSBA>
 __global__ __launch_bounds__(VB) void smooth_gl_kernel(const double* __restrict__ x, int64_t m, double mu,
                                                        const double* __restrict__ wel,
                                                        double* __restrict__ gr, double* __restrict__ Hr) {
   __shared__ double sh[VB / 64];
+  auto val = [&](double v) { return OSBA ? osba_val_d(v, mu) : pseudo_huber_d(v, mu); };
+  auto grd = [&](double v) { return OSBA ? osba_grad_d(v, mu) : huber_grad_d(v, mu); };
+  auto hes = [&](double v) { return OSBA ? osba_hess_d(v, mu) : huber_hess_d(v, mu); };
   double part = 0.0;
   for (int64_t i = threadIdx.x; i < m; i += VB) {
-    const double Dg = huber_grad_d(x[i], mu);
+    const double Dg = grd(x[i]);
     part += Dg * Dg;
   }
   const double dd = block_sum<VB>(part, sh);
   for (int64_t i = threadIdx.x; i < m; i += VB) {
     const double xi = x[i];
-    const double g = pseudo_huber_d(xi, mu);
-    const double Dg = huber_grad_d(xi, mu);
-    const double DDg = huber_hess_d(xi, mu);
+    const double g = val(xi);
+    const double Dg = grd(xi);
+    const double DDg = hes(xi);
     const double Cg = wel[i] * g;
-    gr[i] = huber_grad_d(Cg, mu) * Dg;
-    Hr[i] = huber_hess_d(Cg, mu) * dd + huber_grad_d(Cg, mu) * DDg;
+    gr[i] = grd(Cg) * Dg;
+    Hr[i] = hes(Cg) * dd + grd(Cg) * DDg;
   }
 }
 
@@ -604,7 +646,9 @@ __global__ __launch_bounds__(VB) void rosen_kernel(const double* __restrict__ x,
 hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,
                            const double* wel, double* gr, double* Hr, hipStream_t st) {
   if (kind == SCS_SMOOTH_PHUBER_GL)
-    hipLaunchKernelGGL(smooth_gl_kernel, dim3(1), dim3(VB), 0, st, x, m, mu, wel, gr, Hr);
+    hipLaunchKernelGGL(smooth_gl_kernel<false>, dim3(1), dim3(VB), 0, st, x, m, mu, wel, gr, Hr);
+  else if (kind == SCS_SMOOTH_OSBA_GL)
+    hipLaunchKernelGGL(smooth_gl_kernel<true>, dim3(1), dim3(VB), 0, st, x, m, mu, wel, gr, Hr);
   else
     hipLaunchKernelGGL(smooth_elem_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, kind, x, m, mu, a, b, gr, Hr);
   return hipGetLastError();

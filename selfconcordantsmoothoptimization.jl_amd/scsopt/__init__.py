@@ -13,9 +13,10 @@ from ._lib import ScsError, ScsReferenceError, version
 from .iterate import Solution, iterate, optim_loop, step
 from .methods import ProximalMethod, ProxGGNSCORE, ProxLQNSCORE, ProxNSCORE
 from .problems import Problem, get_P
-from .smoothers import (ExponentialSmootherIndBox, PHuberSmootherGL, PHuberSmootherIndBox, PHuberSmootherL1L2,
-                        Smoother)
+from .smoothers import (ExponentialSmootherIndBox, LogExpSmootherIndBox, OsBaSmootherGL, OsBaSmootherL1L2,
+                        PHuberSmootherGL, PHuberSmootherIndBox, PHuberSmootherL1L2, Smoother)
 
 __all__ = ["Problem", "get_P", "iterate", "optim_loop", "step", "Solution", "ProximalMethod", "ProxNSCORE",
            "ProxGGNSCORE", "ProxLQNSCORE", "PHuberSmootherL1L2", "PHuberSmootherIndBox", "PHuberSmootherGL",
-           "ExponentialSmootherIndBox", "Smoother", "losses", "shard", "ScsError", "ScsReferenceError", "version"]
+           "ExponentialSmootherIndBox", "LogExpSmootherIndBox", "OsBaSmootherL1L2", "OsBaSmootherGL", "Smoother",
+           "losses", "shard", "ScsError", "ScsReferenceError", "version"]

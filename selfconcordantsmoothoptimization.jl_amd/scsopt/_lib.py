@@ -20,7 +20,8 @@ SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS
 LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5}
 GGN = {None: 0, "sigmoid_ce": 1, "linear_ls": 2}
 REG = {"l1": 1, "l2": 2, "indbox": 3, "gl": 4}
-SMOOTH = {"phuber_l1l2": 1, "phuber_indbox": 2, "phuber_gl": 3, "exp_indbox": 4}
+SMOOTH = {"phuber_l1l2": 1, "phuber_indbox": 2, "phuber_gl": 3, "exp_indbox": 4, "logexp_indbox": 5, "osba_l1l2": 6,
+          "osba_gl": 7}
 METHOD = {"nscore": 1, "ggnscore": 2, "lqnscore": 3}
 
 # One HIP runtime per process: torch's wheel bundles ROCm libraries whose NEEDED

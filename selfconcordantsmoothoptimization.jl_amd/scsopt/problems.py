@@ -235,7 +235,7 @@ class Problem:
                                             ng))
         slb = sub = None
         snb = 0
-        if hmu.kind in ("phuber_indbox", "exp_indbox"):
+        if hmu.kind in ("phuber_indbox", "exp_indbox", "logexp_indbox"):
             slb, sub = bounds_array(hmu.lb, self.m), bounds_array(hmu.ub, self.m)
             if slb.size != sub.size:
                 slb = np.broadcast_to(slb, (self.m,)).copy()

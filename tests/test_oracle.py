@@ -129,3 +129,45 @@ def test_golden_kernel_vectors(golden):
     p = k["prox_in"]
     out = O.prox_l1(np.array(p["z"]), 1.0 / np.array(p["Hr"]), p["lam"], p["alpha"])
     np.testing.assert_array_equal(out, np.array(k["prox_l1"]))
+
+
+@pytest.mark.parametrize("mu", [0.3, 1.0])
+def test_new_smoothers_derivative_consistency(mu):
+    """LogExp indbox / Ostrovskii-Bach restatements (log-exp-smooth.jl:36-61,
+    ostrovskii-bach-smooth.jl:28-36): central differences of val reproduce grad, of grad reproduce
+    hess (away from the branch points; the reference ships no vectors for these smoothers, so this
+    pins the restatement against its own value functions)."""
+    x = np.linspace(-3.0, 3.0, 61)
+    x = x[np.abs(x) > 0.04]
+    h = 1e-6
+    # Ostrovskii-Bach (l1 smoothing)
+    g_fd = (O.osba_val(x + h, mu) - O.osba_val(x - h, mu)) / (2 * h)
+    np.testing.assert_allclose(O.osba_grad(x, mu), g_fd, rtol=1e-6, atol=1e-8)
+    H_fd = (O.osba_grad(x + h, mu) - O.osba_grad(x - h, mu)) / (2 * h)
+    np.testing.assert_allclose(O.osba_hess(x, mu), H_fd, rtol=1e-5, atol=1e-7)
+    assert np.isnan(O.osba_grad(np.array([0.0]), mu)[0])          # 0/0 at x = 0, as in Julia
+    # LogExp indbox on [-1, 1]: both pieces, away from x = a, a + μ, b - μ, b
+    lb, ub = -1.0, 1.0
+    kinks = np.array([lb, lb + mu, ub - mu, ub])
+    xs = np.linspace(-0.999, 0.999, 200)
+    xs = xs[np.min(np.abs(xs[:, None] - kinks[None, :]), axis=1) > 1e-3]
+    g_fd = (O.logexp_val_indbox(xs + h, mu, lb, ub) - O.logexp_val_indbox(xs - h, mu, lb, ub)) / (2 * h)
+    np.testing.assert_allclose(O.logexp_grad_indbox(xs, mu, lb, ub), g_fd, rtol=1e-6, atol=1e-8)
+    H_fd = (O.logexp_grad_indbox(xs + h, mu, lb, ub) - O.logexp_grad_indbox(xs - h, mu, lb, ub)) / (2 * h)
+    np.testing.assert_allclose(O.logexp_hess_indbox(xs, mu, lb, ub), H_fd, rtol=1e-5, atol=1e-7)
+    # outside the box: the barrier part μ/(a-x), μ/(a-x)^2
+    xo = np.array([-1.5, 1.5])
+    np.testing.assert_allclose(O.logexp_grad_indbox(xo, mu, lb, ub),
+                               [(-1.5 + 1 - 2 * mu) / mu + mu / 0.5, (1.5 - 1 + 2 * mu) / mu - mu / -0.5])
+
+
+def test_new_smoother_constants():
+    """Mh / ν of the added smoothers (log-exp-smooth.jl:25-26, ostrovskii-bach-smooth.jl:3-4) and
+    the get_Mg branch they select (smoothing.jl:12-25: ν = 3 -> n^0 μ^-0.5 Mh; ν = 2 -> n^0.5 μ^-1 Mh)."""
+    import scsopt
+    h = scsopt.OsBaSmootherL1L2(0.5)
+    assert (h.Mh, h.ν) == (2 * np.sqrt(2), 3.0)
+    assert O.get_Mg(h.Mh, h.ν, 0.5, 1000) == pytest.approx(2 * np.sqrt(2) * 0.5 ** -0.5)
+    h = scsopt.LogExpSmootherIndBox(-1.0, 1.0, 0.5)
+    assert (h.Mh, h.ν) == (1.0, 2.0)
+    assert O.get_Mg(h.Mh, h.ν, 0.5, 100) == pytest.approx(10.0 * 0.5 ** -1.0)
