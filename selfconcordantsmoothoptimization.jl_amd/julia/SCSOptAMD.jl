@@ -105,6 +105,9 @@ function smoother_kind(hμ)
     T <: PHuberSmootherIndBox && return (2, Float64.(vcat(hμ.lb)), Float64.(vcat(hμ.ub)))
     T <: PHuberSmootherGL && return (3, Float64[], Float64[])
     T <: ExponentialSmootherIndBox && return (4, Float64.(vcat(hμ.lb)), Float64.(vcat(hμ.ub)))
+    T <: LogExpSmootherIndBox && return (5, Float64.(vcat(hμ.lb)), Float64.(vcat(hμ.ub)))
+    T <: OsBaSmootherL1L2 && return (6, Float64[], Float64[])
+    T <: OsBaSmootherGL && return (7, Float64[], Float64[])
     error("smoother $(T) has no device implementation")
 end
 
