@@ -180,6 +180,18 @@ int scs_eval_f(scs_ctx* ctx, const double* x, double* fval);
 int scs_eval_grad(scs_ctx* ctx, const double* x, double* g);
 /* get_reg(model, x, reg_name) (regularizers.jl:4-31).                      */
 int scs_eval_reg(scs_ctx* ctx, const double* x, double* gval);
+/* Minibatches: the collected DataLoader batch list of optim_loop!
+ * (iterate.jl:124-146; utils.jl:18-25 get_data_loader / get_loader_subset).
+ * Batch b is the local rows rows[offsets[b] .. offsets[b+1]) (0-based, any
+ * order -- a shuffled loader's permutation is the caller's), gathered on the
+ * device as the As, ys its step! sees (iterate.jl:205-207).  scs_iterate runs
+ * the inner `for (i, sample) in enumerate(data)` loop over the registered
+ * list; scs_select_batch(b) makes batch b the As, ys of the following scs_step
+ * calls (b = -1: the full data).  f / get_reg / the histories always use the
+ * full data (iterate.jl:168).  nbatch = 0 clears the list.  Dense A, one
+ * rank.                                                                     */
+int scs_set_batches(scs_ctx* ctx, const int64_t* rows, const int64_t* offsets, int64_t nbatch);
+int scs_select_batch(scs_ctx* ctx, int64_t b);
 /* step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter;
  *       return_dx) (prox-N-SCORE.jl:34, prox-GGN-SCORE.jl:34,
  * prox-L-BFGS-SCORE.jl:69).  dx may be NULL.                               */
@@ -189,8 +201,10 @@ int scs_step(scs_ctx* ctx, const double* x, const double* x_prev, int64_t iter,
 /* ---- loop level  (iterate!(method, model, reg_name, hμ; max_epoch, x_tol,
  * f_tol) -> Solution, iterate.jl:56-76 / optim_loop! :100-267) ------------ */
 /* History arrays of a Solution (iterate.jl:3-32), caller-owned, capacity
- * max_epoch + 1 each (times may be NULL).  pri_res_norm[0] is the
- * reference's `nothing` (NaN).                                              */
+ * 2 * max_epoch + 1 each (times may be NULL): an epoch pushes its start entry
+ * (:214) and, when a step stops on f_rel_error <= f_tol but the refreshed
+ * f_rel_error no longer passes the test at :257, a terminate entry (:246)
+ * too.  pri_res_norm[0] is the reference's `nothing` (NaN).                  */
 typedef struct scs_history {
   double* obj;
   double* fval;
@@ -200,8 +214,9 @@ typedef struct scs_history {
   double* objrel;   /* f_rel_error: max(|obj − obj*| / |obj*|, f_tol)       */
   double* times;    /* seconds since the start, millisecond resolution       */
 } scs_history;
-/* Full-batch optim_loop! on the device: init! + per epoch f(x) + get_reg(x)
- * + step!, the reference's termination tests and history pushes.  x_star is
+/* optim_loop! on the device: init! + per epoch f(x) + get_reg(x) + one step!
+ * per batch (the full batch, or the scs_set_batches list in order), the
+ * reference's termination tests and history pushes.  x_star is
  * model.x (the comparison solution).  Outputs: final x, *n_hist entries,
  * *epochs (Solution.epochs).  Metrics / test data / verbose printing stay in
  * the host loop (scsopt.iterate).  Requires scs_method_init.                */

@@ -9,6 +9,8 @@
 //
 // A is panel-blocked (common.h tiled_off; S = Npad / 16 stages, m_pad % 128 == 0,
 // zero rows beyond N and zero columns beyond m).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -204,6 +206,31 @@ hipError_t launch_transpose(const double* A, int64_t Npad, int64_t N, int64_t m,
                             int64_t nt, hipStream_t st) {
   hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)ceil_div(ldt, 32), (unsigned)ceil_div(nt, 32)), dim3(256), 0,
                      st, A, Npad, N, m, At, ldt, nt);
+  return hipGetLastError();
+}
+
+// Minibatch gather (iterate.jl:141-145, 205-207: the DataLoader batch As, ys of a step!):
+// rows[0..n) of the panel-blocked A (Npad rows) -> a panel-blocked batch Ab (Npad_b rows,
+// zero padding), y -> yb.  Threads walk the OUTPUT layout, so the writes are coalesced.
+__global__ void gather_rows_kernel(const double* __restrict__ A, int64_t Npad, const double* __restrict__ y,
+                                   const int64_t* __restrict__ rows, int64_t n, int64_t Npad_b, int64_t mpad,
+                                   double* __restrict__ Ab, double* __restrict__ yb) {
+  const int64_t S = Npad / 16, Sb = Npad_b / 16;
+  const int64_t total = Npad_b * mpad;
+  for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < total; o += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = o & 15, f = (o >> 4) & 127, ps = o >> 11;   // ((p*Sb + s)*128 + f)*16 + t
+    const int64_t s = ps % Sb, p = ps / Sb;
+    const int64_t r = s * 16 + t, j = p * 128 + f;
+    Ab[o] = (r < n) ? A[tiled_off(S, rows[r], j)] : 0.0;
+    if (j == 0) yb[r] = (r < n) ? y[rows[r]] : 0.0;
+  }
+}
+
+hipError_t launch_gather_rows(const double* A, int64_t Npad, const double* y, const int64_t* rows, int64_t n,
+                              int64_t Npad_b, int64_t mpad, double* Ab, double* yb, hipStream_t st) {
+  const int64_t total = Npad_b * mpad;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(total, 256), 65536);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid), dim3(256), 0, st, A, Npad, y, rows, n, Npad_b, mpad, Ab, yb);
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/scsopt.h"
@@ -40,6 +41,23 @@ enum { T_GRAM = 0, T_GEMV, T_SOLVE, T_STEP, T_REDUCE, T_N };
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+};
+
+// The N-dependent state of a context: the data rows with their sample-space workspace and the
+// GGN sample-space caches.  A minibatch (scs_set_batch) is a second view swapped in for the
+// duration of scs_step (the As, ys handed to step!, iterate.jl:205-207).
+struct NView {
+  double* A = nullptr;
+  double* y = nullptr;
+  int64_t N = 0, Npad = 0, nstage = 0, Nglob = 0;
+  int nsplit = 1, nval = 1, nchunk = 1;
+  double *zpart = nullptr, *z = nullptr, *gN = nullptr, *hN = nullptr, *wN = nullptr, *vN = nullptr,
+         *valpart = nullptr, *tpart = nullptr;
+  double *At = nullptr, *Ps = nullptr, *Ms = nullptr, *bS = nullptr, *uN = nullptr, *hvec = nullptr, *hg = nullptr;
+  int64_t NpS = 0;
+  int2* stiles = nullptr;
+  int nstiles = 0;
+  rocblas_int *ipivS = nullptr, *dinfoS = nullptr;
 };
 
 }  // namespace
@@ -148,6 +166,14 @@ struct scs_ctx {
   rocblas_int *ipivS = nullptr, *dinfoS = nullptr;
   rocblas_int* dinfo = nullptr;
   rocblas_int* ipiv = nullptr;
+  // minibatches (scs_set_batches / scs_select_batch): the collected DataLoader batch list of
+  // iterate.jl:141-146 as one device row list; each distinct batch size owns a gathered view
+  // (NView) that is swapped in for the steps on that batch
+  int64_t* brows = nullptr;
+  std::vector<int64_t> boff;   // batch b = brows[boff[b] .. boff[b + 1])
+  std::vector<NView> bpool;    // gathered views, one per distinct batch size
+  std::vector<int64_t> bheld;  // the batch each pool view currently holds (-1: none)
+  int bview = -1;              // the selected batch's pool view (-1: the full data)
   bool lu_fallback_used = false;
 
   // caches (CSE of identical evaluations; keyed by the host x content)
@@ -455,6 +481,105 @@ void invalidate_caches(scs_ctx* c) {
 // f / ∇f building blocks
 // ---------------------------------------------------------------------------
 // finalize a loss sum: the per-kind constant of f (see epilogue_kernel)
+// exchange the context's N-dependent fields with v (the full data <-> a minibatch)
+void swap_view(scs_ctx* c, NView& v) {
+  std::swap(c->A, v.A);
+  std::swap(c->y, v.y);
+  std::swap(c->N, v.N);
+  std::swap(c->Npad, v.Npad);
+  std::swap(c->nstage, v.nstage);
+  std::swap(c->Nglob, v.Nglob);
+  std::swap(c->nsplit, v.nsplit);
+  std::swap(c->nval, v.nval);
+  std::swap(c->nchunk, v.nchunk);
+  for (auto pr : {std::make_pair(&c->zpart, &v.zpart), std::make_pair(&c->z, &v.z), std::make_pair(&c->gN, &v.gN),
+                  std::make_pair(&c->hN, &v.hN), std::make_pair(&c->wN, &v.wN), std::make_pair(&c->vN, &v.vN),
+                  std::make_pair(&c->valpart, &v.valpart), std::make_pair(&c->tpart, &v.tpart),
+                  std::make_pair(&c->At, &v.At), std::make_pair(&c->Ps, &v.Ps), std::make_pair(&c->Ms, &v.Ms),
+                  std::make_pair(&c->bS, &v.bS), std::make_pair(&c->uN, &v.uN), std::make_pair(&c->hvec, &v.hvec),
+                  std::make_pair(&c->hg, &v.hg)})
+    std::swap(*pr.first, *pr.second);
+  std::swap(c->NpS, v.NpS);
+  std::swap(c->stiles, v.stiles);
+  std::swap(c->nstiles, v.nstiles);
+  std::swap(c->ipivS, v.ipivS);
+  std::swap(c->dinfoS, v.dinfoS);
+}
+
+void free_view(scs_ctx* c, NView& v) {
+  for (double** p : {&v.A, &v.y, &v.zpart, &v.z, &v.gN, &v.hN, &v.wN, &v.vN, &v.valpart, &v.tpart, &v.At, &v.Ps,
+                     &v.Ms, &v.bS, &v.uN, &v.hvec, &v.hg})
+    dfree_t(c, *p);
+  dfree_t(c, v.stiles);
+  dfree_t(c, v.ipivS);
+  dfree_t(c, v.dinfoS);
+  v = NView();
+}
+
+// scs_step on the selected minibatch view: swapped in (and the data-keyed caches dropped) for
+// the call, swapped back even when the step fails
+struct BatchScope {
+  scs_ctx* c;
+  int k;
+  explicit BatchScope(scs_ctx* cc) : c(cc), k(cc->bview) {
+    if (k >= 0) {
+      swap_view(c, c->bpool[k]);
+      invalidate_caches(c);
+    }
+  }
+  ~BatchScope() {
+    if (k >= 0) {
+      swap_view(c, c->bpool[k]);
+      invalidate_caches(c);
+    }
+  }
+};
+
+void clear_batches(scs_ctx* c) {
+  for (NView& v : c->bpool) free_view(c, v);
+  c->bpool.clear();
+  c->bheld.clear();
+  c->boff.clear();
+  dfree_t(c, c->brows);
+  c->bview = -1;
+}
+
+// select batch b (-1: the full data) for the following steps: its size's pool view is
+// allocated on first use (A / y rows + the sample-space workspace sized by its own Npad)
+// and re-gathered only when it holds another batch
+void select_batch(scs_ctx* c, int64_t b) {
+  c->bview = -1;
+  if (b < 0) return;
+  // f(A, y, x) = 1/2 x'(A x) + y'x reads A as an m x m operator, not as samples
+  if (c->loss == SCS_LOSS_QUADRATIC) fail(c, SCS_ERR_ARG, "the quadratic loss has no samples to batch");
+  const int64_t n = c->boff[b + 1] - c->boff[b];
+  int k = -1;
+  for (int i = 0; i < (int)c->bpool.size(); ++i)
+    if (c->bpool[i].N == n) k = i;
+  if (k < 0) {
+    NView v;
+    v.N = v.Nglob = n;
+    v.Npad = round_up(n, 16);
+    v.nstage = v.Npad / 16;
+    v.A = dalloc<double>(c, (size_t)v.Npad * c->mpad);
+    v.y = dalloc<double>(c, v.Npad);
+    swap_view(c, v);
+    alloc_nspace(c);
+    swap_view(c, v);
+    c->bpool.push_back(v);
+    c->bheld.push_back(-1);
+    k = (int)c->bpool.size() - 1;
+  }
+  if (c->bheld[k] != b) {
+    NView& v = c->bpool[k];
+    HCK(launch_gather_rows(c->A, c->Npad, c->y, c->brows + c->boff[b], n, v.Npad, c->mpad, v.A, v.y, c->st));
+    // the view's GGN sample-space Aᵀ copy (built once per A, ggn_sample_step) follows its rows
+    if (v.At) HCK(launch_transpose(v.A, v.Npad, n, c->m, v.At, c->mpad, v.NpS, c->st));
+    c->bheld[k] = b;
+  }
+  c->bview = k;
+}
+
 double loss_scale_value(scs_ctx* c, double s) {
   switch (c->loss) {
     case SCS_LOSS_LOGISTIC_MARGIN: return c->scale * s;
@@ -1024,6 +1149,7 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->trilist);
   dfree_t(c, c->cinfo);
   chol_aux_free(&c->caux);
+  clear_batches(c);
   dfree_t(c, c->dinfo);
   dfree_t(c, c->ipiv);
   c->ntiles = c->nslots = 0;
@@ -1481,6 +1607,41 @@ int scs_eval_reg(scs_ctx* c, const double* x, double* gval) {
   });
 }
 
+int scs_set_batches(scs_ctx* c, const int64_t* rows, const int64_t* offsets, int64_t nbatch) {
+  return guarded(c, [&] {
+    HCK(hipSetDevice(c->dev));
+    sync(c);
+    clear_batches(c);
+    invalidate_caches(c);
+    if (nbatch == 0) return;
+    if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
+    if (c->generic) fail(c, SCS_ERR_ARG, "a ProblemGeneric has no samples to batch");
+    if (c->sparse) fail(c, SCS_ERR_ARG, "minibatches of a sparse A are not supported");
+    if (c->nranks > 1) fail(c, SCS_ERR_ARG, "minibatches run on one rank");
+    if (nbatch < 0 || !rows || !offsets || offsets[0] != 0) fail(c, SCS_ERR_ARG, "scs_set_batches: bad batch list");
+    for (int64_t b = 0; b < nbatch; ++b)
+      if (offsets[b + 1] <= offsets[b]) fail(c, SCS_ERR_ARG, "scs_set_batches: batch %lld is empty", (long long)b);
+    const int64_t tot = offsets[nbatch];
+    for (int64_t i = 0; i < tot; ++i)
+      if (rows[i] < 0 || rows[i] >= c->N)
+        fail(c, SCS_ERR_ARG, "scs_set_batches: row %lld out of range", (long long)rows[i]);
+    c->brows = dalloc<int64_t>(c, tot);
+    HCK(hipMemcpyAsync(c->brows, rows, sizeof(int64_t) * tot, hipMemcpyHostToDevice, c->st));
+    c->boff.assign(offsets, offsets + nbatch + 1);
+    sync(c);
+  });
+}
+
+int scs_select_batch(scs_ctx* c, int64_t b) {
+  return guarded(c, [&] {
+    const int64_t nb = c->boff.empty() ? 0 : (int64_t)c->boff.size() - 1;
+    if (b < -1 || b >= nb) fail(c, SCS_ERR_ARG, "scs_select_batch: batch %lld of %lld", (long long)b, (long long)nb);
+    HCK(hipSetDevice(c->dev));
+    select_batch(c, b);
+    sync(c);
+  });
+}
+
 int scs_step(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, double* x_new, double* dx,
              double* pri) {
   return guarded(c, [&] {
@@ -1488,6 +1649,7 @@ int scs_step(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, do
     HCK(hipSetDevice(c->dev));
     hipEvent_t e0;
     tbegin(c, T_STEP, &e0);
+    BatchScope bs(c);
     h2d(c, c->x, x, c->m);
     h2d(c, c->xp, x_prev ? x_prev : x, c->m);
     std::vector<double> xnew_h(c->m);
@@ -1570,6 +1732,13 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     std::vector<double> x(x0, x0 + m), x_prev = x, x_new(m);
     double pri = std::numeric_limits<double>::quiet_NaN();
     int64_t epochs = 0;
+    // the collected batches (iterate.jl:146): the registered list, else the one full batch
+    const int64_t nb = c->boff.empty() ? 0 : (int64_t)c->boff.size() - 1;
+    const int64_t iend = std::max<int64_t>(nb, 1);
+    struct Unselect {
+      scs_ctx* c;
+      ~Unselect() { c->bview = -1; }
+    } unselect{c};
     for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
       double dt = now();
       double fval = f_of(x.data());
@@ -1577,35 +1746,46 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
       double rel = rel_of(x.data());
       double frel = frel_of(obj);
       push(obj, fval, pri, rel, frel, dt);
-      if (epoch == max_epoch) {
-        dt = now();
-        fval = f_of(x.data());
-        obj = fval + reg_of(x.data());
-        rel = rel_of(x.data());
-        push(obj, fval, pri, rel, frel_of(obj), dt);
-      }
-      hipEvent_t e0;
-      tbegin(c, T_STEP, &e0);
-      h2d(c, c->x, x.data(), m);
-      h2d(c, c->xp, x_prev.data(), m);
-      if (c->method == SCS_PROX_LQNSCORE)
-        step_lqn(c, x.data(), x_prev.data(), epoch, x_new.data(), nullptr, &pri);
-      else
-        step_newton(c, x.data(), epoch, x_new.data(), nullptr, &pri);
-      tend(c, T_STEP, e0);
-      const double nx = nrm(x.data(), nullptr);
-      if (nrm(x_new.data(), x.data()) < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol) {
-        if (epoch != max_epoch) {   // iterate.jl:235-247
+      for (int64_t i = 1; i <= iend; ++i) {   // for (i, sample) in enumerate(data) (iterate.jl:204-255)
+        if (epoch == max_epoch && i == iend) {   // iterate.jl:219-231 (x as of this batch)
+          dt = now();
+          fval = f_of(x.data());
+          obj = fval + reg_of(x.data());
+          rel = rel_of(x.data());
+          frel = frel_of(obj);
+          push(obj, fval, pri, rel, frel, dt);
+        }
+        hipEvent_t e0;
+        tbegin(c, T_STEP, &e0);
+        select_batch(c, nb > 0 ? i - 1 : -1);
+        {
+          BatchScope bs(c);
+          h2d(c, c->x, x.data(), m);
+          h2d(c, c->xp, x_prev.data(), m);
+          if (c->method == SCS_PROX_LQNSCORE)
+            step_lqn(c, x.data(), x_prev.data(), epoch, x_new.data(), nullptr, &pri);
+          else
+            step_newton(c, x.data(), epoch, x_new.data(), nullptr, &pri);
+        }
+        c->bview = -1;
+        tend(c, T_STEP, e0);
+        const double nx = nrm(x.data(), nullptr);
+        const bool stop = nrm(x_new.data(), x.data()) < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol;
+        if (stop && epoch != max_epoch) {   // iterate.jl:235-247 (f_rel_error is refreshed for the test at :257)
           dt = now();
           fval = f_of(x_new.data());
           obj = fval + reg_of(x_new.data());
           rel = rel_of(x_new.data());
-          push(obj, fval, pri, rel, frel_of(obj), dt);
+          frel = frel_of(obj);
+          push(obj, fval, pri, rel, frel, dt);
         }
-        ++epochs;
+        x_prev.swap(x);
+        x = x_new;
+        if (stop) {
+          ++epochs;
+          break;
+        }
       }
-      x_prev.swap(x);
-      x = x_new;
       if (nrm(x.data(), x_prev.data()) < x_tol * std::max(nrm(x_prev.data(), nullptr), 1.0) || frel <= f_tol ||
           pri < x_tol)
         break;   // iterate.jl:257-259

@@ -8,6 +8,7 @@
 # package `scsopt` (same ABI, same call sequence).
 module SCSOptAMD
 
+using Random
 using SelfConcordantSmoothOptimization
 import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel
 
@@ -123,6 +124,10 @@ end
 # step! on a DeviceProblem: the whole per-iteration work runs in libscsopt.
 function step!(method::ProximalMethod, model::DeviceProblem, reg_name, hμ, As, x, x_prev, ys, Cmat, iter;
                ∇fx=nothing, return_dx=false)
+    # the device holds the rows: a minibatch As from the reference's loader cannot be mapped back
+    # to them, so minibatches go through iterate_device!(...; batch_size) (scs_set_batches)
+    As === nothing || size(As, 1) == size(model.A, 1) ||
+        error("minibatch As on a DeviceProblem: use iterate_device!(...; batch_size, shuffle_batch)")
     x_new = similar(x); dx = similar(x); pri = Ref{Float64}(0.0)
     chk(ccall((:scs_step, lib), Cint,
               (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Ref{Float64}),
@@ -130,15 +135,56 @@ function step!(method::ProximalMethod, model::DeviceProblem, reg_name, hμ, As, 
     return return_dx ? (x_new, dx, pri[]) : (x_new, pri[])
 end
 
-# iterate!(method, model::DeviceProblem, reg_name, hμ; max_epoch, x_tol, f_tol): optim_loop!
-# (iterate.jl:100-267) as ONE ccall (scs_iterate) -- no per-epoch host round trips.  Returns the
-# reference's Solution (iterate.jl:3-32); pri_res_norm[1] is `nothing` as in the reference.
+# The collected loader batches of optim_loop! (iterate.jl:124-146, utils.jl:14-25) as 0-based
+# row lists: ceil(N/b) consecutive runs of the (randperm-shuffled) sample order, the last one
+# partial; slice_samples keeps only sample 1 (max_iter stays 1); local_max_iter truncates.
+# `nothing` = the one full batch.
+function loader_batches(N::Int, batch_size, slice_samples::Bool, shuffle_batch::Bool, local_max_iter)
+    batch_size !== nothing && slice_samples && (slice_samples = false)
+    max_iter = batch_size !== nothing ? Int(ceil(N / batch_size)) : 1
+    iend = (local_max_iter !== nothing && Int(floor(local_max_iter)) > 0) ?
+           min(Int(floor(local_max_iter)), max_iter) : max_iter
+    slice_samples && return [Int64[i - 1] for i in 1:min(iend, N)]
+    batch_size === nothing && return nothing
+    order = shuffle_batch ? randperm(N) .- 1 : collect(0:N-1)
+    return [Int64.(order[(i-1)*batch_size+1:min(i * batch_size, N)]) for i in 1:iend]
+end
+
+function set_batches!(model::DeviceProblem, batches)
+    if batches === nothing || isempty(batches)
+        chk(ccall((:scs_set_batches, lib), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Int64),
+                  model.ctx, C_NULL, C_NULL, 0), model.ctx)
+        return
+    end
+    rows = reduce(vcat, batches)
+    offs = Int64[0; cumsum(length.(batches))]
+    chk(ccall((:scs_set_batches, lib), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Int64),
+              model.ctx, rows, offs, length(batches)), model.ctx)
+end
+
+# iterate!(method, model::DeviceProblem, reg_name, hμ; max_epoch, x_tol, f_tol, batch_size, ...):
+# optim_loop! (iterate.jl:100-267) as ONE ccall (scs_iterate) -- no per-epoch host round trips;
+# minibatches are gathered on the device from the registered row lists (scs_set_batches).
+# Returns the reference's Solution (iterate.jl:3-32); pri_res_norm[1] is `nothing` as there.
 function iterate_device!(method::ProximalMethod, model::DeviceProblem, reg_name::String, hμ;
-                         α=nothing, max_epoch=1000, x_tol=1e-10, f_tol=1e-10)
+                         α=nothing, batch_size=nothing, slice_samples=false, shuffle_batch=true,
+                         max_epoch=1000, local_max_iter=nothing, x_tol=1e-10, f_tol=1e-10)
+    local_max_iter === nothing || (max_epoch = 1)      # iterate.jl:66
     α === nothing || (model.L = 1 / α)                 # iterate.jl:113-115
+    batches = (batch_size !== nothing || slice_samples) ?
+              loader_batches(size(model.A, 1), batch_size, slice_samples, shuffle_batch, local_max_iter) : nothing
+    set_batches!(model, batches)
+    try
+        return iterate_registered!(method, model, reg_name, hμ, max_epoch, x_tol, f_tol)
+    finally
+        batches === nothing || set_batches!(model, nothing)
+    end
+end
+
+function iterate_registered!(method, model, reg_name, hμ, max_epoch, x_tol, f_tol)
     configure!(model, reg_name, hμ)
     init_device!(method, model)
-    cap = max_epoch + 1
+    cap = 2 * max_epoch + 1                           # scsopt.h: up to two pushes per epoch
     obj, fval, pri, rel, objrel, tms = (Vector{Float64}(undef, cap) for _ in 1:6)
     hist = (pointer(obj), pointer(fval), pointer(pri), pointer(rel), pointer(objrel), pointer(tms))
     x_out = similar(model.x0); nh = Ref{Int64}(0); ep = Ref{Int64}(0)

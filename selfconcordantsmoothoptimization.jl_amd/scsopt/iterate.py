@@ -57,15 +57,23 @@ def _norm(v):
     return float(np.linalg.norm(v))
 
 
-def step(method, model, reg_name, hmu, x, x_prev, iter_, return_dx=False):
-    """step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter; return_dx)."""
+def step(method, model, reg_name, hmu, x, x_prev, iter_, return_dx=False, batch=None):
+    """step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter; return_dx).
+
+    As, ys: the full data, or registered batch `batch` (Problem.set_batches)."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     x_prev = np.ascontiguousarray(x_prev, dtype=np.float64)
     x_new = np.empty_like(x)
     dx = np.empty_like(x) if return_dx else None
     pri = C.c_double()
-    model.ctx.check(_lib.lib.scs_step(model.ctx.h, dptr(x), dptr(x_prev), int(iter_), dptr(x_new), dptr(dx),
-                                      C.byref(pri)))
+    if batch is not None:
+        model.select_batch(batch)
+    try:
+        model.ctx.check(_lib.lib.scs_step(model.ctx.h, dptr(x), dptr(x_prev), int(iter_), dptr(x_new), dptr(dx),
+                                          C.byref(pri)))
+    finally:
+        if batch is not None:
+            model.select_batch(-1)
     if return_dx:
         return x_new, dx, pri.value
     return x_new, pri.value
@@ -78,27 +86,71 @@ def init_method(method, model):
                                              int(mem)))
 
 
+def loader_batches(N, batch_size=None, slice_samples=False, shuffle_batch=True, local_max_iter=None, perm=None,
+                   rng=None):
+    """The collected batch list of optim_loop! (iterate.jl:124-146; utils.jl:14-25) as
+    0-based row-index arrays, or None for the single full batch.
+
+    * batch_size b: DataLoader(batchsize=b, shuffle=shuffle_batch) -> ceil(N/b) batches of
+      consecutive rows of the (shuffled) order, the last one partial; collected once, so the
+      same batches run every epoch.  The shuffle permutation is `perm` when given, else drawn
+      from `rng` (numpy; Julia's global RNG stream is not reproducible here).
+    * slice_samples (ignored when batch_size is set, :131-134): one-sample batches -- and since
+      max_iter stays 1 (:127), only the first sample is ever used.
+    * local_max_iter: only the first min(floor(local_max_iter), max_iter) batches (:124,128).
+    """
+    if batch_size is not None and slice_samples:
+        log.info("Cannot use both batch_size and slice_samples=true... Now setting slice_samples=false...")
+        slice_samples = False
+    max_iter = int(math.ceil(N / batch_size)) if batch_size is not None else 1
+    iend = max_iter
+    if local_max_iter is not None and int(math.floor(local_max_iter)) > 0:
+        iend = min(int(math.floor(local_max_iter)), max_iter)
+    if slice_samples:
+        return [np.arange(i, i + 1, dtype=np.int64) for i in range(min(iend, N))]
+    if batch_size is None:
+        return None
+    b = int(batch_size)
+    if b < 1:
+        raise ValueError("batch_size must be >= 1")
+    if shuffle_batch:
+        order = np.asarray(perm, dtype=np.int64) if perm is not None else \
+            (rng if rng is not None else np.random.default_rng()).permutation(N).astype(np.int64)
+        if sorted(order.tolist()) != list(range(N)):
+            raise ValueError("perm must be a permutation of 0..N-1")
+    else:
+        order = np.arange(N, dtype=np.int64)
+    return [order[i * b:min((i + 1) * b, N)] for i in range(iend)]
+
+
 def iterate(method: ProximalMethod, model, reg_name, hmu, *, metrics=None, alpha=None, batch_size=None,
             slice_samples=False, shuffle_batch=True, max_epoch=1000, comm_rounds=100, local_max_iter=None,
-            x_tol=1e-10, f_tol=1e-10, verbose=1, device_loop=None):
+            x_tol=1e-10, f_tol=1e-10, verbose=1, device_loop=None, batch_perm=None, rng=None):
     """iterate!(method, model, reg_name, hμ; kwargs...) (iterate.jl:56-76).
 
     device_loop: run optim_loop! inside libscsopt (scs_iterate: one ABI call per solve);
     the default (None) does so whenever nothing needs the host per epoch (no metrics,
-    verbose <= 1).  False forces the host restatement below (same device calls)."""
+    verbose <= 1).  False forces the host restatement below (same device calls).
+    batch_perm / rng: the shuffled loader's permutation (see loader_batches)."""
     if local_max_iter is not None:
         max_epoch = 1
-    if batch_size is not None or slice_samples:
-        raise NotImplementedError("minibatch / slice_samples paths are not on the device yet (SURVEY §8f rank 3)")
+    batches = None
+    if getattr(model, "N", 0) and (batch_size is not None or slice_samples):
+        batches = loader_batches(model.N, batch_size, slice_samples, shuffle_batch, local_max_iter, batch_perm, rng)
     if device_loop is None:
         device_loop = not metrics and verbose <= 1
-    if device_loop:
-        if metrics or verbose > 1:
-            raise ValueError("device_loop runs without per-epoch metrics / printing")
-        return device_optim_loop(method, model, reg_name, hmu, alpha=alpha, max_epoch=max_epoch, x_tol=x_tol,
-                                 f_tol=f_tol, verbose=verbose)
-    return optim_loop(method, model, reg_name, hmu, metrics=metrics, alpha=alpha, max_epoch=max_epoch,
-                      x_tol=x_tol, f_tol=f_tol, verbose=verbose)
+    if device_loop and (metrics or verbose > 1):
+        raise ValueError("device_loop runs without per-epoch metrics / printing")
+    model.set_batches(batches)
+    try:
+        if device_loop:
+            return device_optim_loop(method, model, reg_name, hmu, alpha=alpha, max_epoch=max_epoch, x_tol=x_tol,
+                                     f_tol=f_tol, verbose=verbose)
+        return optim_loop(method, model, reg_name, hmu, metrics=metrics, alpha=alpha, max_epoch=max_epoch,
+                          x_tol=x_tol, f_tol=f_tol, verbose=verbose, nbatch=len(batches) if batches else 0)
+    finally:
+        if batches:
+            model.set_batches(None)
 
 
 def device_optim_loop(method, model, reg_name, hmu, *, alpha=None, max_epoch=1000, x_tol=1e-10, f_tol=1e-10,
@@ -113,7 +165,7 @@ def device_optim_loop(method, model, reg_name, hmu, *, alpha=None, max_epoch=100
     model.configure(reg_name, hmu)
     init_method(method, model)
     m = model.m
-    cap = int(max_epoch) + 1
+    cap = 2 * int(max_epoch) + 1                       # scsopt.h: up to two pushes per epoch
     hist = {k: np.empty(cap) for k in ("obj", "fval", "pri_res_norm", "rel", "objrel", "times")}
     h = _lib.History(*(dptr(hist[k]) for k in ("obj", "fval", "pri_res_norm", "rel", "objrel", "times")))
     x0 = np.ascontiguousarray(model.x0, dtype=np.float64)
@@ -138,8 +190,9 @@ def _show(opt_verbose, label, tag, epoch, obj, fval, pri, rel, dt):
 
 
 def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_epoch=1000, x_tol=1e-10,
-               f_tol=1e-10, verbose=1):
-    """optim_loop! (iterate.jl:100-267) for the full-batch case."""
+               f_tol=1e-10, verbose=1, nbatch=0):
+    """optim_loop! (iterate.jl:100-267); nbatch > 0: the registered batches in order
+    (Problem.set_batches), else the one full batch."""
     implemented = []
     method.set_name(implemented)
     if alpha is not None:
@@ -179,6 +232,7 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
         for k in metric_vals:
             metric_vals[k].append(metrics[k](model, xx))
 
+    iend = max(nbatch, 1)
     for epoch_t in range(1, max_epoch + 1):
         dt = now()
         fval = f(x)
@@ -187,28 +241,29 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
         f_rel_error = frel_of(obj)
         _show(verbose, method.label, "epoch", epoch_t - 1, obj, fval, pri, rel_error, dt)
         push(obj, fval, pri, rel_error, f_rel_error, dt, x)
-        if epoch_t == max_epoch:                              # iterate.jl:219-231
-            dt = now()
-            fval = f(x)
-            obj = fval + greg(x)
-            rel_error = rel_of(x)
-            _show(verbose, method.label, "max_epoch", epoch_t, obj, fval, pri, rel_error, dt)
-            f_rel_error = frel_of(obj)
-            push(obj, fval, pri, rel_error, f_rel_error, dt, x)
-        x_new, pri = step(method, model, reg_name, hmu, x, x_prev, epoch_t)
-        if _norm(x_new - x) < x_tol * max(_norm(x), 1.0) or f_rel_error <= f_tol or pri < x_tol:
-            if epoch_t != max_epoch:                          # iterate.jl:235-247
+        for i in range(1, iend + 1):                          # iterate.jl:204-255
+            if epoch_t == max_epoch and i == iend:            # iterate.jl:219-231
                 dt = now()
-                fval = f(x_new)
-                obj = fval + greg(x_new)
-                rel_error = rel_of(x_new)
-                _show(verbose, method.label, "terminate_epoch", epoch_t, obj, fval, pri, rel_error, dt)
+                fval = f(x)
+                obj = fval + greg(x)
+                rel_error = rel_of(x)
+                _show(verbose, method.label, "max_epoch", epoch_t, obj, fval, pri, rel_error, dt)
                 f_rel_error = frel_of(obj)
-                push(obj, fval, pri, rel_error, f_rel_error, dt, x_new)
-            x_prev = x
-            x = x_new
-            epochs += 1
-        else:
+                push(obj, fval, pri, rel_error, f_rel_error, dt, x)
+            x_new, pri = step(method, model, reg_name, hmu, x, x_prev, epoch_t, batch=(i - 1) if nbatch else None)
+            if _norm(x_new - x) < x_tol * max(_norm(x), 1.0) or f_rel_error <= f_tol or pri < x_tol:
+                if epoch_t != max_epoch:                      # iterate.jl:235-247
+                    dt = now()
+                    fval = f(x_new)
+                    obj = fval + greg(x_new)
+                    rel_error = rel_of(x_new)
+                    _show(verbose, method.label, "terminate_epoch", epoch_t, obj, fval, pri, rel_error, dt)
+                    f_rel_error = frel_of(obj)
+                    push(obj, fval, pri, rel_error, f_rel_error, dt, x_new)
+                x_prev = x
+                x = x_new
+                epochs += 1
+                break
             x_prev = x
             x = x_new
         if _norm(x - x_prev) < x_tol * max(_norm(x_prev), 1.0) or f_rel_error <= f_tol or pri < x_tol:

@@ -253,6 +253,24 @@ class Problem:
         self.ctx.check(_lib.lib.scs_eval_reg(self.ctx.h, dptr(x), C.byref(out)))
         return out.value
 
+    def set_batches(self, batches=None):
+        """Register the collected loader batches (iterate.jl:141-146): a list of local row-index
+        arrays (0-based), gathered on the device as the As, ys of their step! calls
+        (iterate.jl:205-207).  None / [] clears the list.  f / get_reg stay on the full data."""
+        if not batches:
+            self.ctx.check(_lib.lib.scs_set_batches(self.ctx.h, None, None, 0))
+            return
+        rs = [np.asarray(b, dtype=np.int64).reshape(-1) for b in batches]
+        rows = np.ascontiguousarray(np.concatenate(rs))
+        off = np.zeros(len(rs) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([r.size for r in rs])
+        self.ctx.check(_lib.lib.scs_set_batches(self.ctx.h, rows.ctypes.data_as(_lib.c_i64p),
+                                                off.ctypes.data_as(_lib.c_i64p), len(rs)))
+
+    def select_batch(self, b=-1):
+        """The registered batch the following step! calls see as As, ys (-1: the full data)."""
+        self.ctx.check(_lib.lib.scs_select_batch(self.ctx.h, int(b)))
+
     def _smoother_eval(self, hmu, x):
         x = np.ascontiguousarray(x, dtype=np.float64)
         gr = np.empty(self.m)

@@ -171,3 +171,48 @@ def test_new_smoother_constants():
     h = scsopt.LogExpSmootherIndBox(-1.0, 1.0, 0.5)
     assert (h.Mh, h.ν) == (1.0, 2.0)
     assert O.get_Mg(h.Mh, h.ν, 0.5, 100) == pytest.approx(10.0 * 0.5 ** -1.0)
+
+
+def test_loader_batches_semantics():
+    """iterate.jl:124-146 / utils.jl:14-25: ceil(N/b) batches with a partial last one, batch_size
+    wins over slice_samples, slice_samples keeps only the first sample (max_iter stays 1),
+    local_max_iter truncates; the product's host restatement builds the identical list."""
+    from scsopt.iterate import loader_batches as host_batches
+    perm = np.random.default_rng(0).permutation(10)
+    cases = [dict(batch_size=4, shuffle_batch=False), dict(batch_size=4, shuffle_batch=True, perm=perm),
+             dict(batch_size=10), dict(batch_size=3, local_max_iter=2.9), dict(slice_samples=True),
+             dict(batch_size=5, slice_samples=True, shuffle_batch=False), dict()]
+    for kw in cases:
+        kw.setdefault("perm", perm)
+        ob = O.loader_batches(10, **kw)
+        hb = host_batches(10, **kw)
+        if ob is None:
+            assert hb is None
+            continue
+        assert [list(b) for b in ob] == [list(b) for b in hb], kw
+    b = O.loader_batches(10, 4, shuffle_batch=False)
+    assert [len(t) for t in b] == [4, 4, 2] and list(np.concatenate(b)) == list(range(10))
+    assert [list(t) for t in O.loader_batches(10, slice_samples=True)] == [[0]]
+    assert len(O.loader_batches(10, 3, shuffle_batch=False, local_max_iter=2.9)) == 2
+    assert O.loader_batches(10) is None
+    assert [list(t) for t in O.loader_batches(10, 5, slice_samples=True, shuffle_batch=False)] == \
+        [[0, 1, 2, 3, 4], [5, 6, 7, 8, 9]]
+
+
+@pytest.mark.parametrize("meth", [O.ProxNSCORE, O.ProxGGNSCORE, O.ProxLQNSCORE])
+def test_batched_loop_semantics(meth):
+    """One unshuffled full batch == the full-batch loop (bitwise); two batches per epoch keep the
+    history rules (one push per epoch + the max_epoch entry, iterate.jl:219-231, taken before the
+    epoch's last batch) and step on each batch's rows."""
+    model = logistic_model()
+    full = O.iterate(meth(), model, "l1", O.PHuberSmootherL1L2(1))
+    one = O.iterate(meth(), logistic_model(), "l1", O.PHuberSmootherL1L2(1),
+                    batches=O.loader_batches(5, 5, shuffle_batch=False))
+    assert full.obj == one.obj and np.array_equal(full.x, one.x) and full.epochs == one.epochs
+    small = lambda: O.Problem(np.array(LOGI_A), np.array(LOGI_Y, float), X0,  # noqa: E731
+                              O.Loss("logistic_margin", 1 / 5, ggn="sigmoid_ce"), 0.1)
+    two = O.iterate(meth(), small(), "l1", O.PHuberSmootherL1L2(1), max_epoch=4, x_tol=0.0, f_tol=0.0,
+                    batches=O.loader_batches(5, 3, shuffle_batch=False))
+    assert len(two.obj) == 5 and two.epochs == 4   # the max_epoch entry is taken before the last batch
+    assert not np.array_equal(two.x, O.iterate(meth(), small(), "l1", O.PHuberSmootherL1L2(1),
+                                               max_epoch=4, x_tol=0.0, f_tol=0.0).x)
