@@ -158,10 +158,16 @@ int scs_set_loss(scs_ctx* ctx, int loss_kind, int ggn_kind, double scale);
 /* λ: nlam = 1 (scalar) or 2 ([λ1, λ2] for "gl").  Box (indbox): lb/ub are
  * nbound = 1 scalars or nbound = m vectors (C_set).  Groups (gl): ind is the
  * 3 x ngroups Int matrix of get_P (column-major, 1-based start, end, weight;
- * prox-reg-utils.jl:27-62); groups must tile 1..m contiguously.            */
+ * prox-reg-utils.jl:27-62); the ranges must partition 1..m (any order) --
+ * what get_Cmat (prox-reg-utils.jl:121-142) and the GL smoothers accept.    */
 int scs_set_reg(scs_ctx* ctx, int reg_kind, const double* lam, int nlam,
                 const double* lb, const double* ub, int64_t nbound,
                 const int64_t* ind, int64_t ngroups);
+/* G of get_P(n, G, ind) (1-based, a permutation of 1..m): get_reg's group
+ * term reads P.matrix*x = x[G] (prox-reg-utils.jl:31, regularizers.jl:24-27);
+ * the prox (ProxL2) and the GL smoothers (Cmat) index x directly, as in the
+ * reference.  Call after scs_set_reg(gl); the default is G = 1:m.           */
+int scs_set_group_map(scs_ctx* ctx, const int64_t* G, int64_t ntotal);
 /* Mh/nu as in the smoother struct (e.g. 2.0/2.6 for pseudo-Huber).  lb/ub
  * (indbox smoothers) follow bounds_sanity_check (prox-reg-utils.jl:144-158). */
 int scs_set_smoother(scs_ctx* ctx, int kind, double mu, double Mh, double nu,

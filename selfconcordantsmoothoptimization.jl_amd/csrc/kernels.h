@@ -19,6 +19,7 @@ struct ProxArgsH {
   const int* gend = nullptr;
   const double* gw = nullptr;
   int ngroups = 0;
+  const int* gmap = nullptr;
 };
 
 // ---- gram.hip
@@ -83,6 +84,8 @@ hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const i
 hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
                                double* Yslot, double* scal, hipStream_t st);
 hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st);
+hipError_t launch_nonfinite(const double* G, int64_t ldg, int64_t m, const double* rhs, int* flag, hipStream_t st);
+hipError_t launch_fill(double* a, int64_t n, double v, hipStream_t st);
 hipError_t launch_symmetrize(double* G, int64_t ldg, int64_t m, hipStream_t st);
 hipError_t launch_half_sym(const double* A, int64_t S, int64_t m, double* G, int64_t ldg, hipStream_t st);
 hipError_t launch_rosen(const double* x, int64_t m, int what, double* out, double* G, int64_t ldg, hipStream_t st);

@@ -111,6 +111,7 @@ struct scs_ctx {
   int* gend = nullptr;
   double* gw = nullptr;
   double* wel = nullptr;  // per-element group weight (Cmat diagonal)
+  int* gmap = nullptr;    // get_P's G, 0-based (null: identity)
   int smooth = 0;
   double mu = 1.0, Mh = 2.0, nu = 2.6;
   bool smooth_set = false;
@@ -347,6 +348,7 @@ ProxArgsH prox_args(scs_ctx* c) {
   P.gend = c->gend;
   P.gw = c->gw;
   P.ngroups = c->ngroups;
+  P.gmap = c->gmap;
   return P;
 }
 
@@ -786,6 +788,18 @@ void solve_system(scs_ctx* c, double* rhs) {
   } else {
     ensure_blas(c);
     HCK(launch_symmetrize(c->Gc, ld, m, c->st));
+    // a NaN / Inf in the system (a smoother's NaN, Appendix A) is no SingularException in the
+    // reference: LAPACK getrf only flags exact zero pivots, and the solve comes out NaN
+    HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+    HCK(launch_nonfinite(c->Gc, ld, m, rhs, c->cinfo, c->st));
+    HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    if (info != 0) {
+      HCK(launch_fill(rhs, m, std::numeric_limits<double>::quiet_NaN(), c->st));
+      c->lu_fallback_used = true;
+      tend(c, T_SOLVE, e0);
+      return;
+    }
     RCK(rocsolver_dgetrf(c->blas, (rocblas_int)m, (rocblas_int)m, c->Gc, (rocblas_int)ld, c->ipiv, c->dinfo));
     HCK(hipMemcpyAsync(&info, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
     sync(c);
@@ -889,12 +903,21 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
   HCK(launch_ggn_sample_assemble(c->Ps, c->NpS, c->gN, c->hN, c->wN, c->uN, nullptr, N, c->Ms, c->bS, c->st));
   tbegin(c, T_SOLVE, &e0);
   const rocblas_int n1 = (rocblas_int)(N + 1);
-  RCK(rocsolver_dgetrf(c->blas, n1, n1, c->Ms, n1, c->ipivS, c->dinfoS));
   int info = 0;
+  // NaN / Inf in the system: the reference's qr(...) \ b comes out NaN (no SingularException)
+  HCK(hipMemsetAsync(c->dinfoS, 0, sizeof(int), c->st));
+  HCK(launch_nonfinite(c->Ms, n1, n1, c->bS, c->dinfoS, c->st));
   HCK(hipMemcpyAsync(&info, c->dinfoS, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
-  if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
-  RCK(rocsolver_dgetrs(c->blas, rocblas_operation_none, n1, 1, c->Ms, n1, c->ipivS, c->bS, n1));
+  if (info != 0) {
+    HCK(launch_fill(c->bS, n1, std::numeric_limits<double>::quiet_NaN(), c->st));
+  } else {
+    RCK(rocsolver_dgetrf(c->blas, n1, n1, c->Ms, n1, c->ipivS, c->dinfoS));
+    HCK(hipMemcpyAsync(&info, c->dinfoS, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
+    RCK(rocsolver_dgetrs(c->blas, rocblas_operation_none, n1, 1, c->Ms, n1, c->ipivS, c->bS, n1));
+  }
   tend(c, T_SOLVE, e0);
   HCK(launch_ggn_sample_scale(c->gN, c->bS, N, c->Npad, c->vN, c->st));
   gemv_t_local(c, c->vN, c->gtmp);   // Aᵀ(s∘B)
@@ -1478,19 +1501,26 @@ int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* 
       if (!ind || ngroups < 1) fail(c, SCS_ERR_ARG, "gl needs the group index matrix");
       std::vector<int> hs(ngroups), he(ngroups);
       std::vector<double> hw(ngroups), wel(c->mpad, 0.0);
-      int64_t expect = 1;
+      // get_Cmat (prox-reg-utils.jl:121-142) needs the ranges to cover 1..n exactly once, in any
+      // order (a gap leaves a zero column index, an overlap makes Cmat longer than x)
+      std::vector<char> seen(c->m, 0);
       for (int64_t g = 0; g < ngroups; ++g) {
         const int64_t s = ind[3 * g], e = ind[3 * g + 1], w = ind[3 * g + 2];
-        if (s != expect || e < s || e > c->m)
-          fail(c, SCS_ERR_ARG, "groups must tile 1..m contiguously (group %lld = %lld:%lld)", (long long)g + 1,
-               (long long)s, (long long)e);
-        expect = e + 1;
+        if (s < 1 || e < s || e > c->m)
+          fail(c, SCS_ERR_ARG, "group %lld = %lld:%lld is outside 1..%lld", (long long)g + 1, (long long)s,
+               (long long)e, (long long)c->m);
+        for (int64_t k = s - 1; k < e; ++k) {
+          if (seen[k]) fail(c, SCS_ERR_ARG, "groups overlap at %lld: they must partition 1..m", (long long)k + 1);
+          seen[k] = 1;
+          wel[k] = (double)w;
+        }
         hs[g] = (int)(s - 1);
         he[g] = (int)(e - 1);
         hw[g] = (double)w;
-        for (int64_t k = s - 1; k < e; ++k) wel[k] = (double)w;
       }
-      if (expect != c->m + 1) fail(c, SCS_ERR_ARG, "groups must tile 1..m (covered 1..%lld)", (long long)expect - 1);
+      for (int64_t k = 0; k < c->m; ++k)
+        if (!seen[k]) fail(c, SCS_ERR_ARG, "groups must partition 1..m (%lld is in no group)", (long long)k + 1);
+      dfree_t(c, c->gmap);
       dfree_t(c, c->gstart);
       dfree_t(c, c->gend);
       dfree_t(c, c->gw);
@@ -1507,6 +1537,29 @@ int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* 
       sync(c);
     }
     c->reg_set = true;
+  });
+}
+
+int scs_set_group_map(scs_ctx* c, const int64_t* G, int64_t ntotal) {
+  return guarded(c, [&] {
+    if (!c->reg_set || c->reg != SCS_REG_GL) fail(c, SCS_ERR_STATE, "scs_set_group_map needs reg gl set first");
+    if (!G || ntotal != c->m)
+      fail(c, SCS_ERR_ARG, "G must select every variable once (length %lld, m = %lld)", (long long)ntotal,
+           (long long)c->m);
+    std::vector<int> h(ntotal);
+    std::vector<char> seen(c->m, 0);
+    bool ident = true;
+    for (int64_t k = 0; k < ntotal; ++k) {
+      if (G[k] < 1 || G[k] > c->m || seen[G[k] - 1]) fail(c, SCS_ERR_ARG, "G must be a permutation of 1..m");
+      seen[G[k] - 1] = 1;
+      h[k] = (int)(G[k] - 1);
+      ident = ident && (G[k] == k + 1);
+    }
+    dfree_t(c, c->gmap);
+    if (ident) return;
+    c->gmap = dalloc<int>(c, ntotal);
+    HCK(hipMemcpyAsync(c->gmap, h.data(), sizeof(int) * ntotal, hipMemcpyHostToDevice, c->st));
+    sync(c);
   });
 }
 

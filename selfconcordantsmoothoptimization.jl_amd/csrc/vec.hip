@@ -161,10 +161,11 @@ struct ProxArgs {
   double lam2;        // λ2 (gl)
   const double* lb;   // C_set lower (length m, raw, may be -Inf)
   const double* ub;
-  const int* gstart;  // gl groups (0-based, contiguous partition)
+  const int* gstart;  // gl groups (0-based ranges partitioning 0..m-1, any order)
   const int* gend;
   const double* gw;   // group weights (Int in the reference)
   int ngroups;
+  const int* gmap;    // get_P's G (0-based) for P.matrix*x = x[G] in get_reg; null = identity
 };
 
 // Elementwise prox + the gl group pass, inside one workgroup.
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(VB) void prox_only_kernel(ProxArgs P, const double*
   prox_block(P, z, hinv, step, m, out);
 }
 
-// get_reg (regularizers.jl:4-31); gl with G = identity selector.
+// get_reg (regularizers.jl:4-31); gl: λ2·fz(P.matrix*x) + λ1·Σ|x| with (P.matrix*x)_k = x[G[k]].
 __global__ __launch_bounds__(VB) void reg_value_kernel(ProxArgs P, const double* __restrict__ x, int64_t m,
                                                        double* __restrict__ out) {
   __shared__ double sh[VB / 64];
@@ -278,7 +279,10 @@ __global__ __launch_bounds__(VB) void reg_value_kernel(ProxArgs P, const double*
     double fz = 0.0;
     for (int g = 0; g < P.ngroups; ++g) {
       double nrm2 = 0.0;
-      for (int k = P.gstart[g]; k <= P.gend[g]; ++k) nrm2 += x[k] * x[k];
+      for (int k = P.gstart[g]; k <= P.gend[g]; ++k) {
+        const double v = P.gmap ? x[P.gmap[k]] : x[k];
+        nrm2 += v * v;
+      }
       fz += P.gw[g] * sqrt(nrm2);
     }
     gsum[0] = fz;
@@ -657,7 +661,7 @@ hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, cons
 hipError_t launch_score_tail(const double* x, const double* d, const double* gr, const double* Hr, int64_t m,
                              double lam, double Mg, double step_host, const double* step_dev, const ProxArgsH& Ph,
                              double* hinv, double* zbuf, double* x_new, double* dx, double* scal, hipStream_t st) {
-  ProxArgs P{Ph.reg, Ph.use_prox, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups};
+  ProxArgs P{Ph.reg, Ph.use_prox, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
   hipLaunchKernelGGL(score_tail_kernel, dim3(1), dim3(VB), 0, st, x, d, gr, Hr, m, lam, Mg, step_host, step_dev, P,
                      hinv, zbuf, x_new, dx, scal);
   return hipGetLastError();
@@ -665,13 +669,13 @@ hipError_t launch_score_tail(const double* x, const double* d, const double* gr,
 
 hipError_t launch_prox_only(const ProxArgsH& Ph, const double* z, const double* Hr, double step, int64_t m,
                             double* hinv, double* out, hipStream_t st) {
-  ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups};
+  ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
   hipLaunchKernelGGL(prox_only_kernel, dim3(1), dim3(VB), 0, st, P, z, Hr, step, m, hinv, out);
   return hipGetLastError();
 }
 
 hipError_t launch_reg_value(const ProxArgsH& Ph, const double* x, int64_t m, double* out, hipStream_t st) {
-  ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups};
+  ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
   hipLaunchKernelGGL(reg_value_kernel, dim3(1), dim3(VB), 0, st, P, x, m, out);
   return hipGetLastError();
 }
@@ -734,6 +738,32 @@ hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const 
   hipLaunchKernelGGL(diag_add_kernel, dim3(nblk(m, 256)), dim3(256), 0, st, G, ldg, m, lam, Hr);
   return hipGetLastError();
 }
+// flag[0] |= 1 when an m x m system (ld ldg) or its right-hand side holds a NaN / Inf
+__global__ void nonfinite_kernel(const double* __restrict__ G, int64_t ldg, int64_t m, const double* __restrict__ rhs,
+                                 int* __restrict__ flag) {
+  const int64_t j = blockIdx.y;
+  bool bad = false;
+  for (int64_t i = threadIdx.x; i < m; i += blockDim.x) bad |= !isfinite(G[j * ldg + i]);
+  if (j == 0)
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) bad |= !isfinite(rhs[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+__global__ void fill_kernel(double* __restrict__ a, int64_t n, double v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    a[i] = v;
+}
+
+hipError_t launch_nonfinite(const double* G, int64_t ldg, int64_t m, const double* rhs, int* flag, hipStream_t st) {
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(1, (unsigned)m), dim3(256), 0, st, G, ldg, m, rhs, flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill(double* a, int64_t n, double v, hipStream_t st) {
+  hipLaunchKernelGGL(fill_kernel, dim3((unsigned)nblk(n, 256)), dim3(256), 0, st, a, n, v);
+  return hipGetLastError();
+}
+
 hipError_t launch_symmetrize(double* G, int64_t ldg, int64_t m, hipStream_t st) {
   hipLaunchKernelGGL(symmetrize_kernel, dim3(4, (unsigned)m), dim3(256), 0, st, G, ldg, m);
   return hipGetLastError();

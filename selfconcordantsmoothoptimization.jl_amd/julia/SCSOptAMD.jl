@@ -89,6 +89,11 @@ function configure!(model::DeviceProblem, reg_name::String, hμ)
     chk(ccall((:scs_set_reg, lib), Cint,
               (Ptr{Cvoid}, Cint, Ptr{Float64}, Cint, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Int64}, Int64),
               model.ctx, REG[reg_name], lam, length(lam), lb, ub, nb, ind, ng), model.ctx)
+    if reg_name == "gl"                                  # P.matrix*x = x[G] in get_reg
+        G = Int64.(model.P.G)
+        chk(ccall((:scs_set_group_map, lib), Cint, (Ptr{Cvoid}, Ptr{Int64}, Int64), model.ctx, G, length(G)),
+            model.ctx)
+    end
     kind, slb, sub = smoother_kind(hμ)
     chk(ccall((:scs_set_smoother, lib), Cint,
               (Ptr{Cvoid}, Cint, Float64, Float64, Float64, Ptr{Float64}, Ptr{Float64}, Int64),

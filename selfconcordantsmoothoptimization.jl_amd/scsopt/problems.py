@@ -24,8 +24,10 @@ from .smoothers import Smoother, bounds_array
 @dataclass
 class GetP:
     """get_P(n, G, ind) (prox-reg-utils.jl:9-62): group structure for "gl".
-    ind is 3 x grpNUM (1-based start, end; Int weight); G maps the selected
-    entries to variables (identity for contiguous, non-overlapping groups)."""
+    ind is 3 x grpNUM (1-based start, end; Int weight), its ranges partitioning
+    1..n; G (1-based) maps the entries of P.matrix*x to variables -- a
+    permutation of 1..n, read by get_reg only (the prox and the GL smoothers
+    index x directly, as in the reference)."""
     n: int
     G: np.ndarray
     ind: np.ndarray
@@ -38,8 +40,10 @@ class GetP:
         self.grpNUM = int(self.ind.shape[1])
         self.grpSIZES = self.ind[1] - self.ind[0] + 1
         self.ntotal = int(self.grpSIZES.sum())
-        if not np.array_equal(self.G, np.arange(1, self.n + 1)) or self.ntotal != self.n:
-            raise NotImplementedError("device gl path supports contiguous groups tiling 1..n (G = 1:n)")
+        if self.ntotal != self.n or self.G.shape != (self.n,) or \
+                not np.array_equal(np.sort(self.G), np.arange(1, self.n + 1)):
+            # get_Cmat / the GL smoothers raise DimensionMismatch for ntotal != n in the reference
+            raise ValueError("gl groups must partition 1..n and G must be a permutation of 1..n")
 
 
 def get_P(n, G, ind):
@@ -233,6 +237,9 @@ class Problem:
         self.ctx.check(_lib.lib.scs_set_reg(self.ctx.h, REG[reg_name], dptr(lam), lam.size, dptr(lb), dptr(ub),
                                             nb, ind.ctypes.data_as(_lib.c_i64p) if ind is not None else None,
                                             ng))
+        if reg_name == "gl":
+            G = np.ascontiguousarray(self.P.G, dtype=np.int64)
+            self.ctx.check(_lib.lib.scs_set_group_map(self.ctx.h, G.ctypes.data_as(_lib.c_i64p), int(G.size)))
         slb = sub = None
         snb = 0
         if hmu.kind in ("phuber_indbox", "exp_indbox", "logexp_indbox"):

@@ -78,5 +78,9 @@ def test_get_P_validates_partition():
     import scsopt
     P = scsopt.get_P(6, np.arange(1, 7), np.array([[1, 4], [3, 6], [1, 2]]))
     assert P.grpNUM == 2 and list(P.grpSIZES) == [3, 3]
-    with pytest.raises(NotImplementedError):
+    P = scsopt.get_P(6, np.array([6, 2, 3, 1, 4, 5]), np.array([[4, 1], [6, 3], [2, 1]]))   # any order, permuted G
+    assert P.grpNUM == 2 and P.ntotal == 6
+    with pytest.raises(ValueError):   # G not a permutation
         scsopt.get_P(6, np.array([1, 2, 3, 3, 4, 5]), np.array([[1, 4], [3, 6], [1, 1]]))
+    with pytest.raises(ValueError):   # ntotal != n: the reference's Cmat / smoothers raise DimensionMismatch
+        scsopt.get_P(6, np.arange(1, 7), np.array([[1, 3], [4, 6], [1, 1]]))

@@ -302,6 +302,38 @@ def test_group_lasso_ggn():
     np.testing.assert_allclose(sol.rel, osol.rel, rtol=1e-6)
 
 
+@pytest.mark.parametrize("smoother", ["phuber", "osba"])
+def test_group_lasso_general_groups(smoother):
+    """get_P with unequal groups listed out of order, Int weights 1..3 and a permuted G: get_reg
+    reads x[G] (prox-reg-utils.jl:31), the prox and the GL smoothers index x directly
+    (prox-reg-utils.jl:84-99, :121-142).  ProxNSCORE trajectory vs the oracle."""
+    N, m = 1024, 96
+    rng = np.random.default_rng(21)
+    cuts = [0, 7, 20, 21, 40, 64, 80, 96]
+    groups = [(cuts[i] + 1, cuts[i + 1], 1 + i % 3) for i in range(len(cuts) - 1)]
+    order = rng.permutation(len(groups))
+    ind = np.array([[groups[g][0] for g in order], [groups[g][1] for g in order], [groups[g][2] for g in order]])
+    G = rng.permutation(m) + 1
+    x0 = rng.standard_normal(m)
+    lam = [1e-4, 0.02]
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), lam, kind=3, seed=12)
+    p.P = scsopt.get_P(m, G, ind)
+    A, y = p.get_data()
+    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), lam, P=O.GroupP(m, ind, G))
+    if smoother == "phuber":
+        hm, ohm = scsopt.PHuberSmootherGL(0.05, p), O.PHuberSmootherGL(0.05, om)
+    else:
+        hm, ohm = scsopt.OsBaSmootherGL(0.05, p), O.OsBaSmootherGL(0.05, om)
+    p.configure("gl", hm)
+    for x in (x0, rng.standard_normal(m)):
+        assert p.get_reg(x) == pytest.approx(O.get_reg(om, x, "gl"), rel=1e-15)
+    sol = scsopt.iterate(scsopt.ProxNSCORE(), p, "gl", hm, max_epoch=8, verbose=0)
+    osol = O.iterate(O.ProxNSCORE(), om, "gl", ohm, max_epoch=8)
+    assert len(sol.obj) == len(osol.obj) and sol.epochs == osol.epochs
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+
+
 @pytest.mark.parametrize("method,reg,kw", [("ggn", "l1", {}), ("nscore", "l1", {}), ("lqn", "l1", {"m": 5}),
                                            ("lqn", "indbox", {"m": 5, "ss_type": 2})])
 def test_device_loop_matches_host_loop(method, reg, kw):
