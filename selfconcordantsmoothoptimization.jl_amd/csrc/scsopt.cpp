@@ -95,6 +95,7 @@ struct scs_ctx {
     uint16_t* lidx = nullptr;
     void* val = nullptr;
   } bcsr, bcsc;  // LDS-blocked copies used by the products (sparse.hip)
+  double* Ad = nullptr;  // dense panel-blocked mirror of a sparse A (Gram-based methods only)
 
   // problem
   int loss = 0, ggn = 0;
@@ -812,18 +813,38 @@ void solve_system(scs_ctx* c, double* rhs) {
 }
 
 // the main Gram launch (scheduled when gram_schedule built a work list)
+// the panel-blocked A the Gram kernels read: A itself, or for a sparse A its dense mirror, built
+// once (Jt*Q*Jt' of a SparseMatrixCSC, prox-GGN-SCORE.jl:129 / hess_fx, prox-N-SCORE.jl:55; the
+// products Ax, Aᵀv keep running on the sparse copies)
+const double* dense_A(scs_ctx* c) {
+  if (!c->sparse) return c->A;
+  if (c->Ad) return c->Ad;
+  const size_t bytes = (size_t)c->Npad * c->mpad * sizeof(double);
+  size_t fr = 0, tot = 0;
+  HCK(hipMemGetInfo(&fr, &tot));
+  if (bytes + (size_t)c->mpad * c->mpad * 16 > fr)
+    fail(c, SCS_ERR_ARG,
+         "ProxNSCORE / ProxGGNSCORE on a sparse A form the Gram on a dense mirror of A (%.1f GiB) plus the "
+         "m x m system; the device has %.1f GiB free",
+         bytes / 1073741824.0, fr / 1073741824.0);
+  c->Ad = dalloc<double>(c, bytes / sizeof(double));
+  HCK(hipMemsetAsync(c->Ad, 0, bytes, c->st));
+  HCK(launch_densify(c->rowptr, c->colidx, c->val, c->sp_f32, c->N, c->Npad, c->Ad, c->st));
+  return c->Ad;
+}
+
 void gram_main(scs_ctx* c, const double* w, double* out, int packed) {
+  const double* A = dense_A(c);
   if (c->gwork)
-    HCK(gram_launch_sched(c->A, c->nstage, w, c->Npad, c->gwork, c->gseglen, c->gnsplit, c->gcomb, c->gncomb, c->gpart,
+    HCK(gram_launch_sched(A, c->nstage, w, c->Npad, c->gwork, c->gseglen, c->gnsplit, c->gcomb, c->gncomb, c->gpart,
                           out, c->mpad, packed, c->tall, c->st));
   else
-    HCK(gram_launch(c->A, c->nstage, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st));
+    HCK(gram_launch(A, c->nstage, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st));
 }
 
 // Gram of the local rows with weights w -> c->G (single rank) or the packed
 // reduce buffer (multi-rank; then all-reduced together with `vec`).
 void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
-  require_dense(c, "ProxNSCORE / ProxGGNSCORE (the Gram JᵀQJ)");
   ensure_gram(c);
   hipEvent_t e0;
   if (c->nranks > 1) {
@@ -866,12 +887,12 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
   const int64_t N = c->N, m = c->m;
   if (c->nranks > 1)
     fail(c, SCS_ERR_ARG, "ProxGGNSCORE sample-space branch (N + 1 <= m) runs on one rank (its system is N x N)");
-  require_dense(c, "ProxGGNSCORE");
   ensure_blas(c);
   if (!c->At) {
+    const double* A = dense_A(c);
     c->NpS = round_up(N, 128);
     c->At = dalloc<double>(c, (size_t)c->NpS * c->mpad);
-    HCK(launch_transpose(c->A, c->Npad, N, m, c->At, c->mpad, c->NpS, c->st));
+    HCK(launch_transpose(A, c->Npad, N, m, c->At, c->mpad, c->NpS, c->st));
     c->Ps = dalloc<double>(c, (size_t)c->NpS * c->NpS);
     c->Ms = dalloc<double>(c, (size_t)(N + 1) * (N + 1));
     c->bS = dalloc<double>(c, N + 1);
@@ -1150,6 +1171,7 @@ static void reset_data(scs_ctx* c) {
     B->nblk = B->shift = 0;
   }
   c->sparse = false;
+  dfree_t(c, c->Ad);
   c->nnz = 0;
   dfree_t(c, c->y);
   dfree_t(c, c->G);
@@ -1878,7 +1900,6 @@ int scs_prox_eval(scs_ctx* c, const double* z, const double* Hr, double lam, dou
 int scs_gram_eval(scs_ctx* c, const double* w, double* G, int64_t ldg) {
   return guarded(c, [&] {
     if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
-    require_dense(c, "scs_gram_eval");
     std::vector<double> wp(c->Npad, 0.0);
     std::memcpy(wp.data(), w, sizeof(double) * c->N);
     h2d(c, c->wN, wp.data(), c->Npad);

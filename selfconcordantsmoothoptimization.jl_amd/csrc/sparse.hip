@@ -14,6 +14,8 @@
 // nonzeros and every column exactly k N / m, so both the CSR and the CSC
 // arrays are written in place from closed forms (no sort); the value of
 // (i, s) is a counter-RNG normal, identical in both copies.
+#include <algorithm>
+
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
@@ -332,6 +334,28 @@ hipError_t sort_segments(void* temp, size_t* temp_bytes, const int* kin, int* ko
                                                        (int)nnz, (int)nseg, off, off + 1, 0, end_bit, st);
   return hipcub::DeviceSegmentedRadixSort::SortPairs(temp, *temp_bytes, kin, kout, (const double*)vin, (double*)vout,
                                                      (int)nnz, (int)nseg, off, off + 1, 0, end_bit, st);
+}
+
+// Dense panel-blocked mirror of a CSR A (common.h tiled_off; Ad zeroed by the caller) for the
+// Gram-based methods (Jt*Q*Jt' of a SparseMatrixCSC, prox-GGN-SCORE.jl:129).  One thread per
+// row walks its entries in CSR order, so duplicates are summed race-free.
+template <typename V>
+__global__ void densify_kernel(const int64_t* __restrict__ rowptr, const int* __restrict__ col,
+                               const V* __restrict__ val, int64_t N, int64_t S, double* __restrict__ Ad) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t p = rowptr[r]; p < rowptr[r + 1]; ++p) Ad[tiled_off(S, r, col[p])] += (double)val[p];
+}
+
+hipError_t launch_densify(const int64_t* rowptr, const int* col, const void* val, int f32, int64_t N, int64_t Npad,
+                          double* Ad, hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(std::max<int64_t>(N, 1), 256), 16384);
+  if (f32)
+    hipLaunchKernelGGL(densify_kernel<float>, dim3(grid), dim3(256), 0, st, rowptr, col, (const float*)val, N,
+                       Npad / 16, Ad);
+  else
+    hipLaunchKernelGGL(densify_kernel<double>, dim3(grid), dim3(256), 0, st, rowptr, col, (const double*)val, N,
+                       Npad / 16, Ad);
+  return hipGetLastError();
 }
 
 // x_true ~ U(-1.5, 1.5); y = A x_true + 0.1 ε computed by the caller

@@ -98,11 +98,47 @@ def test_multiblock_products(N, m, rho):
     _check_products(p, A)
 
 
-def test_gram_methods_refuse_sparse():
-    N, m = 1024, 64
-    p = scsopt.Problem.synthetic_sparse(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1e-4, density=0.1)
-    with pytest.raises(scsopt.ScsError, match="dense A"):
-        scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=2, verbose=0)
+@pytest.mark.parametrize("case", ["nscore_ls_f32", "ggn_logistic", "ggn_sample_space", "nscore_logistic"])
+def test_gram_methods_on_sparse(case):
+    """ProxNSCORE / ProxGGNSCORE on a sparse A (Jt*Q*Jt' of a SparseMatrixCSC): the Gram runs on a
+    dense mirror built on the device from the CSR (duplicates summed), the products on the sparse
+    copies; trajectories vs the oracle on the densified matrix at the trajectory bar."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(41)
+    if case == "nscore_ls_f32":
+        N, m = 4096, 128
+        x0 = rng.standard_normal(m) * 0.5
+        p = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), 1e-3, density=0.05, seed=5,
+                                            f32=True)
+        A, y = p.get_sparse()
+        of = O.Loss("least_squares", 1.0 / N)
+        meth, ometh = scsopt.ProxNSCORE(), O.ProxNSCORE()
+    else:
+        N, m = (96, 256) if case == "ggn_sample_space" else (3000, 160)
+        C = sp.random(N, m, density=0.05, random_state=7, format="coo")
+        rows = np.concatenate([C.row, C.row[:50]])             # duplicates (summed) + unsorted entries
+        cols = np.concatenate([C.col, C.col[:50]])
+        vals = np.concatenate([C.data, rng.standard_normal(50)]) * 2.0
+        perm = rng.permutation(rows.size)
+        A = sp.coo_matrix((vals[perm], (rows[perm], cols[perm])), shape=(N, m))
+        y = (rng.random(N) < 0.5).astype(float)
+        x0 = rng.standard_normal(m) * 0.3
+        if case == "nscore_logistic":
+            y = 2 * y - 1
+            f, out, of = losses.logistic_margin(1.0 / N), None, O.Loss("logistic_margin", 1.0 / N)
+            meth, ometh = scsopt.ProxNSCORE(), O.ProxNSCORE()
+        else:
+            f, out = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N)
+            of = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+            meth, ometh = scsopt.ProxGGNSCORE(), O.ProxGGNSCORE()
+        p = scsopt.Problem(A, y, x0, f, 1e-3, out_fn=out)
+    Ad = A.toarray() if hasattr(A, "toarray") else A
+    om = O.Problem(Ad, y, x0, of, 1e-3)
+    sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=8, verbose=0)
+    osol = O.iterate(ometh, om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=8)
+    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
 
 
 def _c5_pair(N=8192, m=512, rho=0.02, f32=False, max_epoch=25, mem=20):
