@@ -163,6 +163,14 @@ int scs_set_loss(scs_ctx* ctx, int loss_kind, int ggn_kind, double scale);
 int scs_set_reg(scs_ctx* ctx, int reg_kind, const double* lam, int nlam,
                 const double* lb, const double* ub, int64_t nbound,
                 const int64_t* ind, int64_t ngroups);
+/* Opt-in: reuse AᵀQA across steps when it does not depend on x -- least
+ * squares under ProxNSCORE (hess_fx = c·AᵀA) or under ProxGGNSCORE with the
+ * linear out_fn (J = A, Q = c·I).  The reference recomputes it every step
+ * (prox-GGN-SCORE.jl:129, prox-N-SCORE.jl:55) and that stays the default;
+ * with the cache on, later steps copy the (all-reduced) Gram of the first and
+ * only the gradient is all-reduced.  Bit-identical results.  Costs one more
+ * m_pad² fp64 buffer.                                                        */
+int scs_set_gram_cache(scs_ctx* ctx, int on);
 /* G of get_P(n, G, ind) (1-based, a permutation of 1..m): get_reg's group
  * term reads P.matrix*x = x[G] (prox-reg-utils.jl:31, regularizers.jl:24-27);
  * the prox (ProxL2) and the GL smoothers (Cmat) index x directly, as in the

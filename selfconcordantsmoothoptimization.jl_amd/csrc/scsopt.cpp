@@ -96,6 +96,11 @@ struct scs_ctx {
     void* val = nullptr;
   } bcsr, bcsc;  // LDS-blocked copies used by the products (sparse.hip)
   double* Ad = nullptr;  // dense panel-blocked mirror of a sparse A (Gram-based methods only)
+  // x-independent Gram reuse (scs_set_gram_cache): Gk holds AᵀQA of data generation gk_gen;
+  // data_gen moves on every change of the rows or the loss (new data, batch view swaps)
+  int gram_cache = 0;
+  double* Gk = nullptr;
+  uint64_t data_gen = 1, gk_gen = 0;
 
   // problem
   int loss = 0, ggn = 0;
@@ -486,6 +491,7 @@ void invalidate_caches(scs_ctx* c) {
 // finalize a loss sum: the per-kind constant of f (see epilogue_kernel)
 // exchange the context's N-dependent fields with v (the full data <-> a minibatch)
 void swap_view(scs_ctx* c, NView& v) {
+  ++c->data_gen;
   std::swap(c->A, v.A);
   std::swap(c->y, v.y);
   std::swap(c->N, v.N);
@@ -844,9 +850,28 @@ void gram_main(scs_ctx* c, const double* w, double* out, int packed) {
 
 // Gram of the local rows with weights w -> c->G (single rank) or the packed
 // reduce buffer (multi-rank; then all-reduced together with `vec`).
+// AᵀQA does not depend on x: least squares under ProxNSCORE (hess_fx = c·AᵀA) or under
+// ProxGGNSCORE with the linear out_fn (J = A, Q = c·I); the reference still recomputes it every
+// step (prox-GGN-SCORE.jl:129), which stays the default
+bool gram_x_independent(const scs_ctx* c) {
+  if (c->loss != SCS_LOSS_LEAST_SQUARES) return false;
+  return c->method == SCS_PROX_NSCORE || (c->method == SCS_PROX_GGNSCORE && c->ggn == SCS_GGN_LINEAR_LS);
+}
+
 void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
   ensure_gram(c);
   hipEvent_t e0;
+  const bool cacheable = c->gram_cache && gram_x_independent(c);
+  const size_t gbytes = sizeof(double) * (size_t)c->mpad * c->mpad;
+  if (cacheable && c->Gk && c->gk_gen == c->data_gen) {   // the reduced Gram of an earlier step
+    HCK(hipMemcpyAsync(c->G, c->Gk, gbytes, hipMemcpyDeviceToDevice, c->st));
+    if (c->nranks > 1) {
+      HCK(hipMemcpyAsync(c->red, vec_dev, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+      allreduce(c, c->red, c->m);
+      HCK(hipMemcpyAsync(vec_dev, c->red, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+    }
+    return;
+  }
   if (c->nranks > 1) {
     const int64_t tsz = (int64_t)c->nslots * 128 * 128;
     tbegin(c, T_GRAM, &e0);
@@ -860,6 +885,11 @@ void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
     tbegin(c, T_GRAM, &e0);
     gram_main(c, w, c->G, 0);
     tend(c, T_GRAM, e0);
+  }
+  if (cacheable) {
+    if (!c->Gk) c->Gk = dalloc<double>(c, (size_t)c->mpad * c->mpad);
+    HCK(hipMemcpyAsync(c->Gk, c->G, gbytes, hipMemcpyDeviceToDevice, c->st));
+    c->gk_gen = c->data_gen;
   }
 }
 
@@ -1172,6 +1202,8 @@ static void reset_data(scs_ctx* c) {
   }
   c->sparse = false;
   dfree_t(c, c->Ad);
+  dfree_t(c, c->Gk);
+  ++c->data_gen;
   c->nnz = 0;
   dfree_t(c, c->y);
   dfree_t(c, c->G);
@@ -1481,6 +1513,7 @@ int scs_set_loss(scs_ctx* c, int loss, int ggn, double scale) {
     c->ggn = ggn;
     c->scale = scale;
     c->loss_set = true;
+    ++c->data_gen;
     invalidate_caches(c);
   });
 }
@@ -1559,6 +1592,14 @@ int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* 
       sync(c);
     }
     c->reg_set = true;
+  });
+}
+
+int scs_set_gram_cache(scs_ctx* c, int on) {
+  return guarded(c, [&] {
+    c->gram_cache = on ? 1 : 0;
+    ++c->data_gen;
+    if (!on) dfree_t(c, c->Gk);
   });
 }
 

@@ -260,6 +260,12 @@ class Problem:
         self.ctx.check(_lib.lib.scs_eval_reg(self.ctx.h, dptr(x), C.byref(out)))
         return out.value
 
+    def set_gram_cache(self, on=True):
+        """Opt-in reuse of AᵀQA across steps when it is x-independent (least squares under
+        ProxNSCORE, or ProxGGNSCORE with the linear out_fn); the reference recomputes it every
+        step (prox-GGN-SCORE.jl:129), which stays the default.  Results are bit-identical."""
+        self.ctx.check(_lib.lib.scs_set_gram_cache(self.ctx.h, int(bool(on))))
+
     def set_batches(self, batches=None):
         """Register the collected loader batches (iterate.jl:141-146): a list of local row-index
         arrays (0-based), gathered on the device as the As, ys of their step! calls

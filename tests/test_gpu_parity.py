@@ -334,6 +334,36 @@ def test_group_lasso_general_groups(smoother):
     np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("case", ["nscore_ls", "ggn_ls_gl", "ggn_ls_batches"])
+def test_gram_cache_bit_identical(case):
+    """scs_set_gram_cache: AᵀQA of least squares is x-independent, so reusing it changes nothing --
+    identical histories and x bits vs the reference's recompute-every-step; minibatches (a different
+    A per step) must not reuse another batch's Gram."""
+    N, m, gs = 2048, 128, 16
+    x0 = np.random.default_rng(9).standard_normal(m)
+    out = None if case == "nscore_ls" else losses.linear_ls(1.0 / N)
+    lam = 1e-3 if case != "ggn_ls_gl" else [1e-8, 0.05]
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), lam, kind=3, seed=8, out_fn=out)
+    reg, hm = "l1", scsopt.PHuberSmootherL1L2(1.0)
+    if case == "ggn_ls_gl":
+        ng = m // gs
+        p.P = scsopt.get_P(m, np.arange(1, m + 1),
+                           np.array([[1 + gs * g for g in range(ng)], [gs + gs * g for g in range(ng)], [1] * ng]))
+        reg, hm = "gl", scsopt.PHuberSmootherGL(1e-2, p)
+    meth = scsopt.ProxNSCORE if case == "nscore_ls" else scsopt.ProxGGNSCORE
+    kw = dict(max_epoch=7, verbose=0)
+    if case == "ggn_ls_batches":
+        kw.update(batch_size=700, batch_perm=np.random.default_rng(2).permutation(N))
+    ref = scsopt.iterate(meth(), p, reg, hm, **kw)
+    p.set_gram_cache(True)
+    try:
+        got = scsopt.iterate(meth(), p, reg, hm, **kw)
+    finally:
+        p.set_gram_cache(False)
+    assert got.obj == ref.obj and got.pri_res_norm == ref.pri_res_norm and got.epochs == ref.epochs
+    assert np.array_equal(bits(got.x), bits(ref.x))
+
+
 @pytest.mark.parametrize("method,reg,kw", [("ggn", "l1", {}), ("nscore", "l1", {}), ("lqn", "l1", {"m": 5}),
                                            ("lqn", "indbox", {"m": 5, "ss_type": 2})])
 def test_device_loop_matches_host_loop(method, reg, kw):

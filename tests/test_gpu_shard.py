@@ -37,10 +37,15 @@ def _run(method, comm=None):
     elif method == "nscore":
         f, out, kind = losses.logistic_margin(1.0 / N), None, 2
         meth = scsopt.ProxNSCORE()
+    elif method == "ggn_ls_cached":
+        f, out, kind = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N), 3
+        meth = scsopt.ProxGGNSCORE()
     else:
         f, out, kind = losses.least_squares(1.0 / N), None, 3
         meth = scsopt.ProxLQNSCORE(m=5)
     p = scsopt.Problem.synthetic(N, M, x0, f, 2e-3, kind=kind, seed=11, out_fn=out, comm=comm)
+    if method == "ggn_ls_cached" and comm is not None:   # sharded: Gram reused, only ∇f all-reduced
+        p.set_gram_cache(True)
     sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=6, verbose=0)
     return {"obj": list(sol.obj), "x": sol.x.copy(), "epochs": sol.epochs}
 
@@ -56,7 +61,7 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = {}
-    for method in ("ggn", "nscore", "lqn"):
+    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached"):
         comm = shard.Comm(device=torch.device("cuda", 0))
         res[method] = _run(method, comm)
     out[rank] = res
@@ -72,7 +77,7 @@ def test_two_rank_shard_matches_single_process(tall, monkeypatch):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    for method in ("ggn", "nscore", "lqn"):
+    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached"):
         full = _run(method)
         r0, r1 = out[0][method], out[1][method]
         assert r0["epochs"] == r1["epochs"] == full["epochs"]
