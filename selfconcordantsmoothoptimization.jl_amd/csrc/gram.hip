@@ -623,13 +623,246 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                            hipStream_t st);
 
+// ---------------------------------------------------------------------------
+// Interleaved-schedule Gram tiles on the panel-blocked A (4 waves, 2 x 2).
+//   TI = 2: 128 x 128 tile, 4 waves, <= 256 VGPRs -> 2 workgroups / CU;
+//   TI = 4: 256 x 128 tile, 8 waves, one workgroup per CU, 25 % less operand
+//           traffic per flop.  Each wave holds 64 x 64 (16 accumulators).
+// One LDS buffer per workgroup (the A1 and A2 stage blocks); the next stage waits
+// in registers.  Iteration k (stage k in LDS, its p = 0 fragments F0 already in
+// registers, stage k+1 in registers R):
+//   phase 1 : the p = 0 MFMAs, the p = 1 fragment reads F1 interleaved;
+//             lgkmcnt(0) + barrier (every wave is done reading stage k)
+//   phase 2a: R -> LDS (A2 rows scaled by w), the global loads of stage k+2 into
+//             R, interleaved with 3/4 of the p = 1 MFMAs; lgkmcnt(0) + barrier
+//   phase 2b: the F0 reads of stage k+1 interleaved with the last 1/4.
+// No phase waits on LDS latency (measured: the no-load build of this structure
+// runs at ~97 % of the fp64 MFMA peak per round, one or two waves per SIMD), the
+// global loads have a whole iteration to land, and the MFMA order per
+// accumulator is the plain loop's (p, u) order: G is bitwise identical to
+// gram_f64_kernel / gram_glds_kernel of the same tile height.
+template <int PIPE, int TI = 2>
+__global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
+    const double* __restrict__ A, int64_t S, const double* __restrict__ w, int64_t k0, int64_t Nk,
+    const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int flags,
+    const int4* __restrict__ work, int seglen, int nsplit, double* __restrict__ P) {
+  constexpr int GTI = 64 * TI;        // tile rows (A1 features)
+  constexpr int NT = 128 * TI;        // threads
+  constexpr int FS = NT / 8;          // features per staging sweep
+  constexpr int NTI = 4;              // 16-row MFMA tiles per wave along i
+  constexpr int NA = GTI / FS;        // A1 staging chunks per thread per stage (4)
+  constexpr int NB = GT / FS;         // A2 staging chunks per thread per stage (4 or 2)
+  constexpr int NMM = 2 * NTI * 4;    // MFMAs per fragment set (2 u x NTI x 4)
+  constexpr int NRD = NTI + 4;        // ds_read_b128 per fragment set
+  constexpr int TAIL = NMM / 4;       // MFMAs left for phase 2b
+  const int packed = flags & GRAM_PACKED, accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
+  // PIPE 4/5 (timing builds, TI = 2): LDS padding -> one workgroup (one wave per SIMD) per CU
+  __shared__ __attribute__((aligned(16))) double lds[(PIPE >= 4 ? 5 * GT * GBK : (GTI + GT) * GBK)];
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8;
+  int bi, bj, tix, part = -1;
+  if (work) {
+    const int4 it = work[xcd * seglen + orig / 8];
+    if (it.x < 0) return;
+    bi = it.x;
+    bj = it.y;
+    tix = it.w;
+    if (it.z >= 0) {
+      const int64_t L = ((Nk - k0 + (int64_t)nsplit * GBK - 1) / ((int64_t)nsplit * GBK)) * GBK;
+      part = it.w;
+      k0 = k0 + it.z * L;
+      Nk = k0 + L < Nk ? k0 + L : Nk;
+      if (Nk < k0) Nk = k0;
+    }
+  } else {
+    const int q8 = ntiles / 8, r8 = ntiles % 8;
+    tix = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int2 tl = tiles[tix];
+    bi = tl.x;
+    bj = tl.y;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int sc = tid & 7, sf0 = tid >> 3;
+  if (PIPE >= 4 && tid == 0) lds[4 * GT * GBK] = 0.0;   // keep the padding allocated
+  const int64_t st0 = k0 / GBK;
+  // this thread's 16-B chunks of a stage: feature sf0 + FS i of the A1 rows (panel
+  // (GTI/128) bi + f/128) and of the A2 rows (panel bj), samples 2 sc, 2 sc + 1.
+  // S < 0 (layout experiment, TI = 2): stage-major blocks, block (p, s) at s * (-S) + p
+  const int64_t pstr = S > 0 ? S : 1, sstr = S > 0 ? 1 : -S;
+  const double* srcA = A + ((int64_t)bi * (GTI / GT) * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
+  const double* srcB = A + ((int64_t)bj * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
+  const double* srcW = w + k0 + 2 * sc;
+  double* la = lds;
+  double* lb = lds + GTI * GBK;
+  int woff[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int f = sf0 + FS * i;
+    woff[i] = f * GBK + 2 * (sc ^ swz(f));
+  }
+  v2d ra[NA], rb[NB], rw;
+  auto gload = [&](int64_t st) {
+    if ((PIPE == 3 || PIPE == 5) && st >= 2) return;   // timing builds: no global loads after the prologue
+    const int64_t so = st * sstr * GT * GBK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int f = FS * i;   // + sf0 (in srcA): the panel of f is f / 128 (FS divides 128)
+      ra[i] = *(const v2d*)(srcA + so + (f >> 7) * pstr * GT * GBK + (f & 127) * GBK);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + so + FS * GBK * i);
+    rw = *(const v2d*)(srcW + st * GBK);
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) *(v2d*)(la + woff[i]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) *(v2d*)(lb + woff[i]) = rb[i] * rw;
+  };
+  const int fl = lane & 15, g = lane >> 4, s = swz(fl);
+  struct Frag {
+    v2d a[NTI], b[4];
+  };
+  auto fread = [&](int p, Frag& F) {
+    const int pc = ((4 * p + g) ^ s) * 2;
+#pragma unroll
+    for (int t = 0; t < NTI; ++t) F.a[t] = *(const v2d*)(la + (wr * 64 + 16 * t + fl) * GBK + pc);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) F.b[t] = *(const v2d*)(lb + (wc * 64 + 16 * t + fl) * GBK + pc);
+  };
+  v4d acc[NTI][4];
+#pragma unroll
+  for (int i = 0; i < NTI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
+  // MFMAs n in [n0, n1) of a fragment set, n = 4 NTI u + 4 ti + tj (the plain loop's order)
+  auto mm = [&](const Frag& F, int n0, int n1) {
+#pragma unroll
+    for (int n = n0; n < n1; ++n) {
+      const int u = n / (4 * NTI), ti = (n / 4) % NTI, tj = n & 3;
+      acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(F.a[ti][u], F.b[tj][u], acc[ti][tj], 0, 0, 0);
+    }
+  };
+  auto barrier = [&]() {   // also a scheduling fence: nothing (e.g. the w products) crosses a phase
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS traffic is done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int nk = (int)((Nk - k0) / GBK);
+  Frag F0, F1;
+  if (nk > 0) {
+    gload(0);
+    swrite();
+    if (nk > 1) gload(1);
+    barrier();
+    fread(0, F0);
+  }
+  auto body = [&](int k, bool has1, bool has2) {
+    // phase 1
+    __builtin_amdgcn_sched_barrier(0);
+    fread(1, F1);
+    mm(F0, 0, NMM);
+    if (PIPE) {
+#pragma unroll
+      for (int i = 0; i < NRD; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NMM / NRD, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           // DS read
+      }
+    }
+    barrier();
+    // phase 2a
+    if (has1) swrite();
+    if (has2) gload(k + 2);
+    mm(F1, 0, NMM - TAIL);
+    if (PIPE) {
+      if (has1) {
+#pragma unroll
+        for (int i = 0; i < NA + NB; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, (NMM - TAIL) / (NA + NB), 0);   // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                         // DS write
+          if (has2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);               // VMEM read
+        }
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NMM, 0);
+    }
+    // phase 2b
+    if (has1) {
+      barrier();
+      fread(0, F0);
+    }
+    mm(F1, NMM - TAIL, NMM);
+    if (PIPE && has1) {
+#pragma unroll
+      for (int i = 0; i < NRD; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, TAIL / NRD > 0 ? TAIL / NRD : 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+  };
+  int k = 0;
+  for (; k + 2 < nk; ++k) body(k, true, true);
+  if (k + 1 < nk) {
+    body(k, true, false);
+    ++k;
+  }
+  if (k < nk) body(k, false, false);
+
+  // epilogue (the C/D map of gram_f64_kernel): element (il, jl) of the GTI x 128 tile
+#pragma unroll
+  for (int ti = 0; ti < NTI; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int il = wr * 64 + 16 * ti + g + 4 * r;
+        const int jl = wc * 64 + 16 * tj + fl;
+        double* dst;
+        if (part >= 0) {
+          P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
+          continue;
+        }
+        if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
+        else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
+        else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
+        if (accumulate) *dst += acc[ti][tj][r];
+        else *dst = acc[ti][tj][r];
+      }
+}
+
+// Main-Gram kernel selection (A/B switches, read once):
+//   SCS_GRAM_SIA  (128 x 128 tiles): unset/1 = interleaved-schedule kernel, 2 = same kernel with
+//                 the compiler's schedule, 0 = register-staged gram_f64_kernel;
+//   SCS_GRAM_GLDS (256 x 128 tiles): unset/3 = interleaved-schedule kernel, 2 = LDS-DMA ring with
+//                 pipelined fragment reads, 1 = LDS-DMA plain loop, 0 = register-staged.
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+int gram_sia_mode() {
+  static const int v = env_int("SCS_GRAM_SIA", 1);
+  return v;
+}
+int gram_tall_mode() {
+  static const int v = env_int("SCS_GRAM_GLDS", 3);
+  return v;
+}
+
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,
                        int ntiles, double* G, int64_t ldg, int packed, int tall, hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
-  if (!tall)
+  if (!tall && gram_sia_mode() == 0)
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (!tall)
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (gram_tall_mode() == 3)
+    hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -749,7 +982,25 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
-  if (noload == 7 || noload == 8)   // pipelined fragment reads (8: no-load ceiling), panel-blocked A
+  if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
+    hipLaunchKernelGGL((noload == 16 ? gram_sia_kernel<1, 4> : gram_sia_kernel<3, 4>), dim3(ntiles), dim3(512), 0,
+                       st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 14 || noload == 15)   // one workgroup per CU (LDS padding): loaded / no-load
+    hipLaunchKernelGGL((noload == 14 ? gram_sia_kernel<4> : gram_sia_kernel<5>), dim3(ntiles), dim3(256), 0, st, A,
+                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 13)   // layout experiment: stage-major panel blocks (S passed negated: -number of panels)
+    hipLaunchKernelGGL((gram_sia_kernel<1>), dim3(ntiles), dim3(256), 0, st, A, -(int64_t)(ldg / GT), w, k0, k1,
+                       tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 12)
+    hipLaunchKernelGGL((gram_sia_kernel<3>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 9 || noload == 10)
+    hipLaunchKernelGGL((noload == 9 ? gram_sia_kernel<1> : gram_sia_kernel<0>), dim3(ntiles), dim3(256), 0, st, A,
+                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 11)
+    hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, A,
+                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else if (noload == 7 || noload == 8)   // pipelined fragment reads (8: no-load ceiling), panel-blocked A
     hipLaunchKernelGGL((noload == 7 ? gram_glds_kernel<true, 1> : gram_glds_kernel<true, 2>), dim3(ntiles), dim3(512),
                        0, st, A, (k1 - k0) / GBK, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr,
                        0, 0, nullptr);
@@ -801,13 +1052,11 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
                              int tall, hipStream_t st) {
   const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
-  // SCS_GRAM_GLDS (A/B switch): 0 = register-staged kernel, 1 = LDS-DMA plain loop,
-  // unset/2 = LDS-DMA with pipelined fragment reads (default)
-  static const int glds = [] {
-    const char* e = getenv("SCS_GRAM_GLDS");
-    return e ? atoi(e) : 2;
-  }();
-  if (tall && glds == 2)
+  const int glds = gram_tall_mode();
+  if (tall && glds == 3)
+    hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk,
+                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  else if (tall && glds == 2)
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
                        Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   else if (tall && glds == 1)
@@ -816,6 +1065,12 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
   else if (tall)
     hipLaunchKernelGGL((gram_f64_kernel<false, 4, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  else if (gram_sia_mode() == 1)
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr,
+                       0, G, ldg, flags, work, seglen, nsplit, P);
+  else if (gram_sia_mode() == 2)
+    hipLaunchKernelGGL((gram_sia_kernel<0>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr, 0,
+                       G, ldg, flags, work, seglen, nsplit, P);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);

@@ -86,6 +86,62 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  if (getenv("GRAM_ONLY")) {   // one launch of one experiment kernel (for rocprofv3 --pmc passes)
+    if (tall) return 0;
+    CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, atoi(getenv("GRAM_ONLY")), 0));
+    CK(hipDeviceSynchronize());
+    return 0;
+  }
+  if (getenv("GRAM_SIA") && tall) {
+    // 256 x 128 interleaved kernel (16; 17 = no-load build) vs the LDS-DMA pipelined kernel (7)
+    const double alg0 = (double)N * m * (m + 1);
+    std::vector<double> ref((size_t)m * m), got((size_t)m * m);
+    CK(hipMemset(G, 0, (size_t)m * m * 8));
+    CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 7, 0));
+    CK(hipMemcpy(ref.data(), G, ref.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemset(G, 0, (size_t)m * m * 8));
+    CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 16, 0));
+    CK(hipMemcpy(got.data(), G, got.size() * 8, hipMemcpyDeviceToHost));
+    size_t nd = 0;
+    for (size_t e = 0; e < got.size(); ++e) nd += got[e] != ref[e];
+    printf("CHECK sia-tall N=%ld m=%ld bitwise diffs vs glds pipe: %zu  %s\n", (long)N, (long)m, nd, nd ? "FAIL" : "PASS");
+    for (int v : {7, 16, 17}) {
+      float t;
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, v, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      t /= reps;
+      printf("SIA-TALL kernel %d N=%ld m=%ld: %.3f ms  %.2f TF/s\n", v, (long)N, (long)m, t, alg0 / t / 1e9);
+    }
+  }
+  if (getenv("GRAM_SIA") && !tall) {
+    // interleaved-schedule kernel (9: sched_group_barrier patterns, 10: compiler schedule) vs the
+    // register-staged 128 x 128 kernel on the same panel-blocked A (11): bitwise, then timing
+    const double alg0 = (double)N * m * (m + 1);
+    std::vector<double> ref((size_t)m * m), got((size_t)m * m);
+    CK(hipMemset(G, 0, (size_t)m * m * 8));
+    CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, 11, 0));
+    CK(hipMemcpy(ref.data(), G, ref.size() * 8, hipMemcpyDeviceToHost));
+    for (int v : {9, 10}) {
+      CK(hipMemset(G, 0, (size_t)m * m * 8));
+      CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, v, 0));
+      CK(hipMemcpy(got.data(), G, got.size() * 8, hipMemcpyDeviceToHost));
+      size_t nd = 0;
+      for (size_t e = 0; e < got.size(); ++e) nd += got[e] != ref[e];
+      printf("CHECK sia%d N=%ld m=%ld bitwise diffs vs register kernel: %zu  %s\n", v, (long)N, (long)m, nd,
+             nd ? "FAIL" : "PASS");
+    }
+    for (int v : {9, 12}) {
+      float t;
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, v, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      t /= reps;
+      printf("SIA kernel %d N=%ld m=%ld: %.3f ms  %.2f TF/s\n", v, (long)N, (long)m, t, alg0 / t / 1e9);
+    }
+  }
   CK(hipEventRecord(e0));
   for (int r = 0; r < reps; ++r) CK(scs::gram_launch(A, N / 16, w, N, dtl, nt, G, m, 0, tall, 0));
   CK(hipEventRecord(e1));
