@@ -641,7 +641,9 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 // global loads have a whole iteration to land, and the MFMA order per
 // accumulator is the plain loop's (p, u) order: G is bitwise identical to
 // gram_f64_kernel / gram_glds_kernel of the same tile height.
-template <int PIPE, int TI = 2>
+// CM: column-major operands (the Cholesky's trailing updates, gen form with A1 == A2),
+// S = leading dimension; stage k of feature f is the 16 samples at f * S + k0 + 16 k.
+template <int PIPE, int TI = 2, bool CM = false>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     const double* __restrict__ A, int64_t S, const double* __restrict__ w, int64_t k0, int64_t Nk,
     const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int flags,
@@ -690,8 +692,10 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   // (GTI/128) bi + f/128) and of the A2 rows (panel bj), samples 2 sc, 2 sc + 1.
   // S < 0 (layout experiment, TI = 2): stage-major blocks, block (p, s) at s * (-S) + p
   const int64_t pstr = S > 0 ? S : 1, sstr = S > 0 ? 1 : -S;
-  const double* srcA = A + ((int64_t)bi * (GTI / GT) * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
-  const double* srcB = A + ((int64_t)bj * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
+  const double* srcA = CM ? A + ((int64_t)bi * GTI + sf0) * S + k0 + 2 * sc
+                          : A + ((int64_t)bi * (GTI / GT) * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
+  const double* srcB = CM ? A + ((int64_t)bj * GT + sf0) * S + k0 + 2 * sc
+                          : A + ((int64_t)bj * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
   const double* srcW = w + k0 + 2 * sc;
   double* la = lds;
   double* lb = lds + GTI * GBK;
@@ -704,14 +708,21 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   v2d ra[NA], rb[NB], rw;
   auto gload = [&](int64_t st) {
     if ((PIPE == 3 || PIPE == 5) && st >= 2) return;   // timing builds: no global loads after the prologue
-    const int64_t so = st * sstr * GT * GBK;
+    if (CM) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int f = FS * i;   // + sf0 (in srcA): the panel of f is f / 128 (FS divides 128)
-      ra[i] = *(const v2d*)(srcA + so + (f >> 7) * pstr * GT * GBK + (f & 127) * GBK);
+      for (int i = 0; i < NA; ++i) ra[i] = *(const v2d*)(srcA + st * GBK + (int64_t)FS * i * S);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + st * GBK + (int64_t)FS * i * S);
+    } else {
+      const int64_t so = st * sstr * GT * GBK;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int f = FS * i;   // + sf0 (in srcA): the panel of f is f / 128 (FS divides 128)
+        ra[i] = *(const v2d*)(srcA + so + (f >> 7) * pstr * GT * GBK + (f & 127) * GBK);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + so + FS * GBK * i);
     }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + so + FS * GBK * i);
     rw = *(const v2d*)(srcW + st * GBK);
   };
   auto swrite = [&]() {
@@ -973,8 +984,12 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
                        ldg, flags);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles,
-                     ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)   // the Cholesky's trailing updates
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  else
+    hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1,
+                       tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   return hipGetLastError();
 }
 

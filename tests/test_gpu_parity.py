@@ -531,3 +531,42 @@ def test_gram_tall_tiles_and_ksplit(monkeypatch):
     terms = np.abs(A).T @ (np.abs(w)[:, None] * np.abs(A))
     ref = A.T @ (w[:, None] * A)
     assert np.all(np.abs(G - ref) <= 1e-13 * terms + 1e-300)
+
+
+_GRAM_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import scsopt
+from scsopt import losses
+out = {}
+for tall, (N, m) in (("1", (4096 + 48, 1024)), ("0", (2000, 384))):
+    import os
+    os.environ["SCS_GRAM_TALL"] = tall
+    rng = np.random.default_rng(7)
+    A = rng.standard_normal((N, m)); w = rng.standard_normal(N)
+    p = scsopt.Problem(A, np.zeros(N), np.zeros(m), losses.least_squares(), 1.0)
+    out[tall] = p.gram(w)
+np.savez(sys.argv[2], **out)
+"""
+
+
+def test_interleaved_gram_bitwise_vs_previous_kernels(tmp_path):
+    """The interleaved-schedule Gram kernels (defaults) reproduce the previous kernels bit for bit:
+    the same sizes through the LDS-DMA 256 x 128 kernel (SCS_GRAM_GLDS=2) and the register-staged
+    128 x 128 kernel (SCS_GRAM_SIA=0) in a child process (the switches are read once per process),
+    tail-balanced schedule included."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "selfconcordantsmoothoptimization.jl_amd")
+    outs = {}
+    for tag, env in (("new", {}), ("old", {"SCS_GRAM_GLDS": "2", "SCS_GRAM_SIA": "0"})):
+        f = tmp_path / f"{tag}.npz"
+        e = dict(os.environ, **env)
+        e.pop("SCS_GRAM_TALL", None)
+        subprocess.run([sys.executable, "-c", _GRAM_CHILD, pkg, str(f)], env=e, check=True, timeout=120)
+        outs[tag] = np.load(f)
+    for k in ("1", "0"):
+        lo = np.tril_indices(outs["new"][k].shape[0])
+        assert np.array_equal(bits(outs["new"][k][lo]), bits(outs["old"][k][lo])), k
