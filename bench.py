@@ -244,13 +244,16 @@ def main():
                 line["cpu_baseline"]["t_iter_s"] = cb["t_iter_s"]
             except Exception as e:  # the baseline is reported, never the target
                 line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
-        if not args.no_cpu_baseline and args.config == "c3":
+        if not args.no_cpu_baseline and args.config in ("c2", "c3", "c4"):
             env = dict(os.environ)
             cores = int(env.get("OMP_NUM_THREADS", "16"))
             env["OPENBLAS_NUM_THREADS"] = str(cores)
             try:
+                meth = {"c2": "nscore", "c3": "ggn", "c4": "ggn_ls"}[args.config]
+                Ns = args.cpu_Ns if m <= 16384 else 256   # bounded sample (the dgemm is Ns·m² flops)
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--N", str(N),
-                                      "--m", str(m), "--Ns", str(args.cpu_Ns), "--ms", str(min(args.cpu_ms, m))],
+                                      "--m", str(m), "--Ns", str(Ns), "--ms", str(min(args.cpu_ms, m)),
+                                      "--method", meth],
                                      capture_output=True, text=True, env=env, timeout=300, check=True)
                 cb = json.loads(out.stdout.strip().splitlines()[-1])
                 line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}

@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--Ns", type=int, default=2048)
     ap.add_argument("--ms", type=int, default=0, help="QR timed at ms and scaled by (m/ms)^3 (0: full m)")
     ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--method", default="ggn", choices=["ggn", "ggn_ls", "nscore"],
+                    help="ggn: C3 (CE + sigmoid out_fn, QR); ggn_ls: C4 (least squares, J = A, QR); "
+                         "nscore: C2 (logistic margin, hess_fx Gram, LU)")
     a = ap.parse_args()
     import scipy.linalg.lapack as lapack
 
@@ -62,14 +65,49 @@ def main():
         Je = Jt @ r
         return f, JQJ, Je
 
+    def sample_nscore():
+        # prox-N-SCORE.jl:51-70 with closed-form callbacks: f pass, grad_fx, hess_fx = Aᵀ diag(h) A
+        ys = 2 * y - 1
+        z = A @ x                                                    # f(x) pass
+        f = c * np.sum(np.log1p(np.exp(-ys * z)))
+        z = A @ x                                                    # grad_fx
+        e = np.exp(-ys * z)
+        g = A.T @ (c * (-ys * e / (1.0 + e)))
+        z = A @ x                                                    # hess_fx
+        e = np.exp(-ys * z)
+        h = c * e / ((1.0 + e) * (1.0 + e))
+        H = A.T @ (h[:, None] * A)                                    # full dgemm
+        return f, g, H
+
+    def sample_ggn_ls():
+        # prox-GGN-SCORE.jl:44-56,121-130 with out_fn = A*x, least squares: J = A (copy), Q = c I
+        z = A @ x                                                    # f(x) pass
+        f = 0.5 * c * np.sum((z - y) ** 2)
+        z = A @ x                                                    # out_fn
+        r = c * (z - y)
+        Jt = np.ascontiguousarray(A.T)                                # jac_yx + hcat copy
+        JtQ = Jt * c
+        JQJ = JtQ @ Jt.T
+        Je = Jt @ r
+        return f, JQJ, Je
+
+    if a.method == "nscore":
+        sample_part = sample_nscore  # noqa: F811
+    elif a.method == "ggn_ls":
+        sample_part = sample_ggn_ls  # noqa: F811
+
     def solve_part(msz):
         M = rng.standard_normal((msz, msz)) / np.sqrt(msz)
         M = np.asfortranarray(M @ M.T + np.eye(msz))
         b = rng.standard_normal(msz)
         t0 = time.perf_counter()
-        qr, tau, work, info = lapack.dgeqrf(M, overwrite_a=True)
-        qtb, work, info = lapack.dormqr("L", "T", qr, tau, b, max(1, msz * 64))
-        d, info = lapack.dtrtrs(qr, qtb, lower=0)
+        if a.method == "nscore":   # `\` on a dense Matrix: dgetrf + dgetrs (prox-N-SCORE.jl:70)
+            lu, piv, info = lapack.dgetrf(M, overwrite_a=True)
+            d, info = lapack.dgetrs(lu, piv, b)
+        else:                      # qr(JQJ) \ Je: dgeqrf + dormqr + dtrtrs (prox-GGN-SCORE.jl:131)
+            qr, tau, work, info = lapack.dgeqrf(M, overwrite_a=True)
+            qtb, work, info = lapack.dormqr("L", "T", qr, tau, b, max(1, msz * 64))
+            d, info = lapack.dtrtrs(qr, qtb, lower=0)
         return time.perf_counter() - t0
 
     sample_part()  # warm-up (page-in, threads)
@@ -87,8 +125,10 @@ def main():
     print(json.dumps({
         "value": 1.0 / t_iter, "unit": "iterations/s", "cores": threads, "kind": "port",
         "t_iter_s": t_iter, "t_sample_s": t_sample, "t_qr_s": t_qr, "qr_m": msz,
-        "sample": f"oracle port (NumPy/OpenBLAS, reference BLAS call structure) of one ProxGGNSCORE epoch: "
-                  f"sample part on {Ns} of {N} rows x m={m} scaled x{N // Ns}, dgeqrf/dormqr/dtrtrs solve at "
+        "sample": f"oracle port (NumPy/OpenBLAS, reference BLAS call structure) of one "
+                  f"{'ProxNSCORE' if a.method == 'nscore' else 'ProxGGNSCORE'} epoch ({a.method}): "
+                  f"sample part on {Ns} of {N} rows x m={m} scaled x{N / Ns:.0f}, "
+                  f"{'dgetrf/dgetrs' if a.method == 'nscore' else 'dgeqrf/dormqr/dtrtrs'} solve at "
                   f"m={msz}" + (f" scaled x{(m / msz) ** 3:.0f}" if msz != m else ""),
     }))
 
