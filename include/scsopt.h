@@ -138,8 +138,9 @@ int scs_get_dims(scs_ctx* ctx, int64_t* N, int64_t* m, int64_t* N_global, int64_
  * fixed summation order (no atomics).  Indices are 0-based; the CSC copy
  * describes the same local rows (rowidx in [0, N)).  val_f32 = 1 stores the
  * values as fp32 (the fp32-value arm of the study; accumulation stays fp64).
- * f, ∇f and ProxLQNSCORE run on sparse A; the Gram-based methods return
- * SCS_ERR_ARG.                                                              */
+ * All methods run on sparse A: the products stay sparse; ProxNSCORE /
+ * ProxGGNSCORE form their Gram on a dense device mirror of A, built once and
+ * refused (SCS_ERR_ARG) when it does not fit in device memory.               */
 int scs_set_sparse(scs_ctx* ctx, int64_t N, int64_t m, int64_t nnz,
                    const int64_t* rowptr, const int32_t* colidx, const double* val,
                    const int64_t* colptr, const int32_t* rowidx, const double* valT,
