@@ -350,7 +350,9 @@ static int outer_block() {
   static const int ob = [] {
     const char* e = getenv("SCS_CHOL_OB");
     const int v = e ? atoi(e) : 8;
-    return v < 1 ? 1 : v;
+    // the strip-solve recursion needs rectangle lists of up to OB/2 block rows (chol_aux_init
+    // builds R <= 4), so OB is capped at 8
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
   }();
   return ob;
 }
