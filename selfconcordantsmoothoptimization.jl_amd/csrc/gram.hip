@@ -656,7 +656,7 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   constexpr int NB = GT / FS;         // A2 staging chunks per thread per stage (4 or 2)
   constexpr int NMM = 2 * NTI * 4;    // MFMAs per fragment set (2 u x NTI x 4)
   constexpr int NRD = NTI + 4;        // ds_read_b128 per fragment set
-  constexpr int TAIL = NMM / 4;       // MFMAs left for phase 2b
+  constexpr int TAIL = PIPE == 7 ? NMM / 8 : (PIPE == 8 ? 3 * NMM / 8 : NMM / 4);   // MFMAs left for phase 2b
   const int packed = flags & GRAM_PACKED, accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
   // PIPE 4/5 (timing builds, TI = 2): LDS padding -> one workgroup (one wave per SIMD) per CU
   __shared__ __attribute__((aligned(16))) double lds[(PIPE >= 4 ? 5 * GT * GBK : (GTI + GT) * GBK)];
@@ -757,9 +757,11 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   };
   auto barrier = [&]() {   // also a scheduling fence: nothing (e.g. the w products) crosses a phase
     __builtin_amdgcn_sched_barrier(0);
+    if (PIPE == 6) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS traffic is done
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (PIPE == 6) __builtin_amdgcn_s_setprio(3);
     __builtin_amdgcn_sched_barrier(0);
   };
   const int nk = (int)((Nk - k0) / GBK);
@@ -997,7 +999,12 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
-  if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
+  if (noload >= 18 && noload <= 20)   // 256 x 128 interleaved schedule variants: setprio / tail 1/8 / tail 3/8
+    hipLaunchKernelGGL((noload == 18 ? gram_sia_kernel<6, 4> : noload == 19 ? gram_sia_kernel<7, 4>
+                                                                              : gram_sia_kernel<8, 4>),
+                       dim3(ntiles), dim3(512), 0, st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags,
+                       nullptr, 0, 0, nullptr);
+  else if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
     hipLaunchKernelGGL((noload == 16 ? gram_sia_kernel<1, 4> : gram_sia_kernel<3, 4>), dim3(ntiles), dim3(512), 0,
                        st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (noload == 14 || noload == 15)   // one workgroup per CU (LDS padding): loaded / no-load

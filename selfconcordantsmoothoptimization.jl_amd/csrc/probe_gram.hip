@@ -105,7 +105,7 @@ static int run(int64_t N, int64_t m, int reps, bool check, int tall) {
     size_t nd = 0;
     for (size_t e = 0; e < got.size(); ++e) nd += got[e] != ref[e];
     printf("CHECK sia-tall N=%ld m=%ld bitwise diffs vs glds pipe: %zu  %s\n", (long)N, (long)m, nd, nd ? "FAIL" : "PASS");
-    for (int v : {7, 16, 17}) {
+    for (int v : {16, 18, 19, 20, 16}) {
       float t;
       CK(hipEventRecord(e0));
       for (int r = 0; r < reps; ++r) CK(scs::gram_launch_ex(A, lda, w, 0, N, dtl, nt, G, m, 0, v, 0));
