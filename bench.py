@@ -234,6 +234,14 @@ def main():
             line["config"]["gram_cache"] = True
         line["breakdown_ms_per_step"] = {k.replace("_ms", ""): tm[k] / steps for k in tm if k.endswith("_ms")}
         line["objective_last"] = objs[-1]
+        if not args.no_cpu_baseline and args.config == "c1":
+            try:
+                out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline_c1.py")],
+                                     capture_output=True, text=True, timeout=120, check=True)
+                cb = json.loads(out.stdout.strip().splitlines()[-1])
+                line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+            except Exception as e:  # the baseline is reported, never the target
+                line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
         if not args.no_cpu_baseline and args.config == "c5":
             try:
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline_lqn.py"), "--N", str(N),
