@@ -203,8 +203,8 @@ int scs_eval_reg(scs_ctx* ctx, const double* x, double* gval);
  * the inner `for (i, sample) in enumerate(data)` loop over the registered
  * list; scs_select_batch(b) makes batch b the As, ys of the following scs_step
  * calls (b = -1: the full data).  f / get_reg / the histories always use the
- * full data (iterate.jl:168).  nbatch = 0 clears the list.  Dense A, one
- * rank.                                                                     */
+ * full data (iterate.jl:168).  nbatch = 0 clears the list.  One rank; a
+ * sparse A's batches are gathered dense (the reference's Matrix(As')).                                                                          */
 int scs_set_batches(scs_ctx* ctx, const int64_t* rows, const int64_t* offsets, int64_t nbatch);
 int scs_select_batch(scs_ctx* ctx, int64_t b);
 /* step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter;

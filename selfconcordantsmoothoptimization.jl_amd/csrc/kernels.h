@@ -117,6 +117,8 @@ hipError_t launch_gemv_t_finalize(const double* part, int nchunk, int64_t mpad, 
                                   hipStream_t st);
 hipError_t launch_densify(const int64_t* rowptr, const int* col, const void* val, int f32, int64_t N, int64_t Npad,
                           double* Ad, hipStream_t st);
+hipError_t launch_densify_rows(const int64_t* rowptr, const int* col, const void* val, int f32, const int64_t* rows,
+                               int64_t n, int64_t Npad_b, const double* y, double* Ab, double* yb, hipStream_t st);
 hipError_t launch_gather_rows(const double* A, int64_t Npad, const double* y, const int64_t* rows, int64_t n,
                               int64_t Npad_b, int64_t mpad, double* Ab, double* yb, hipStream_t st);
 hipError_t launch_transpose(const double* A, int64_t Npad, int64_t N, int64_t m, double* At, int64_t ldt,

@@ -58,6 +58,7 @@ struct NView {
   int2* stiles = nullptr;
   int nstiles = 0;
   rocblas_int *ipivS = nullptr, *dinfoS = nullptr;
+  bool sparse = false;   // a batch view is always dense (Matrix(As'), iterate.jl:207)
 };
 
 }  // namespace
@@ -492,6 +493,7 @@ void invalidate_caches(scs_ctx* c) {
 // exchange the context's N-dependent fields with v (the full data <-> a minibatch)
 void swap_view(scs_ctx* c, NView& v) {
   ++c->data_gen;
+  std::swap(c->sparse, v.sparse);
   std::swap(c->A, v.A);
   std::swap(c->y, v.y);
   std::swap(c->N, v.N);
@@ -581,7 +583,13 @@ void select_batch(scs_ctx* c, int64_t b) {
   }
   if (c->bheld[k] != b) {
     NView& v = c->bpool[k];
-    HCK(launch_gather_rows(c->A, c->Npad, c->y, c->brows + c->boff[b], n, v.Npad, c->mpad, v.A, v.y, c->st));
+    if (c->sparse) {   // CSR rows -> the dense batch (the reference's Matrix(As') of a sparse A)
+      HCK(hipMemsetAsync(v.A, 0, sizeof(double) * (size_t)v.Npad * c->mpad, c->st));
+      HCK(launch_densify_rows(c->rowptr, c->colidx, c->val, c->sp_f32, c->brows + c->boff[b], n, v.Npad, c->y,
+                              v.A, v.y, c->st));
+    } else {
+      HCK(launch_gather_rows(c->A, c->Npad, c->y, c->brows + c->boff[b], n, v.Npad, c->mpad, v.A, v.y, c->st));
+    }
     // the view's GGN sample-space Aᵀ copy (built once per A, ggn_sample_step) follows its rows
     if (v.At) HCK(launch_transpose(v.A, v.Npad, n, c->m, v.At, c->mpad, v.NpS, c->st));
     c->bheld[k] = b;
@@ -1732,7 +1740,6 @@ int scs_set_batches(scs_ctx* c, const int64_t* rows, const int64_t* offsets, int
     if (nbatch == 0) return;
     if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
     if (c->generic) fail(c, SCS_ERR_ARG, "a ProblemGeneric has no samples to batch");
-    if (c->sparse) fail(c, SCS_ERR_ARG, "minibatches of a sparse A are not supported");
     if (c->nranks > 1) fail(c, SCS_ERR_ARG, "minibatches run on one rank");
     if (nbatch < 0 || !rows || !offsets || offsets[0] != 0) fail(c, SCS_ERR_ARG, "scs_set_batches: bad batch list");
     for (int64_t b = 0; b < nbatch; ++b)

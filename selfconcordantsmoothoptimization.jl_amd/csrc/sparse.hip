@@ -358,6 +358,36 @@ hipError_t launch_densify(const int64_t* rowptr, const int* col, const void* val
   return hipGetLastError();
 }
 
+// Minibatch of a sparse A: CSR rows rows[0..n) -> dense panel-blocked batch Ab (Npad_b rows,
+// zeroed by the caller), y -> yb.  One thread per batch row, entries in CSR order.
+template <typename V>
+__global__ void densify_rows_kernel(const int64_t* __restrict__ rowptr, const int* __restrict__ col,
+                                    const V* __restrict__ val, const int64_t* __restrict__ rows, int64_t n,
+                                    int64_t Npad_b, const double* __restrict__ y, double* __restrict__ Ab,
+                                    double* __restrict__ yb) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < Npad_b; r += (int64_t)gridDim.x * blockDim.x) {
+    if (r >= n) {
+      yb[r] = 0.0;
+      continue;
+    }
+    const int64_t src = rows[r];
+    yb[r] = y[src];
+    for (int64_t p = rowptr[src]; p < rowptr[src + 1]; ++p) Ab[tiled_off(Npad_b / 16, r, col[p])] += (double)val[p];
+  }
+}
+
+hipError_t launch_densify_rows(const int64_t* rowptr, const int* col, const void* val, int f32, const int64_t* rows,
+                               int64_t n, int64_t Npad_b, const double* y, double* Ab, double* yb, hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(std::max<int64_t>(Npad_b, 1), 256), 16384);
+  if (f32)
+    hipLaunchKernelGGL(densify_rows_kernel<float>, dim3(grid), dim3(256), 0, st, rowptr, col, (const float*)val, rows,
+                       n, Npad_b, y, Ab, yb);
+  else
+    hipLaunchKernelGGL(densify_rows_kernel<double>, dim3(grid), dim3(256), 0, st, rowptr, col, (const double*)val,
+                       rows, n, Npad_b, y, Ab, yb);
+  return hipGetLastError();
+}
+
 // x_true ~ U(-1.5, 1.5); y = A x_true + 0.1 ε computed by the caller
 __global__ void gen_uniform_kernel(double* __restrict__ x, int64_t m, uint64_t seed, double lo, double hi) {
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;

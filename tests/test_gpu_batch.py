@@ -128,3 +128,33 @@ def test_batch_errors():
     q.set_batches([np.array([0, 1])])
     with pytest.raises(scsopt.ScsError, match="quadratic"):
         q.select_batch(0)
+
+
+@pytest.mark.parametrize("method", ["lqn", "ggn"])
+def test_sparse_minibatches_gathered_dense(method):
+    """Batches of a sparse A are the reference's Matrix(As') (iterate.jl:207): the CSR rows of each
+    batch are gathered into a dense view on the device; trajectory vs the oracle on the dense A."""
+    import scipy.sparse as sp
+    N, m = 1500, 96
+    rng = np.random.default_rng(17)
+    A = sp.random(N, m, density=0.08, random_state=3, format="csr") * 3.0
+    x0 = rng.standard_normal(m) * 0.3
+    if method == "lqn":
+        y = rng.standard_normal(N)
+        f, out, of = losses.least_squares(1.0 / N), None, O.Loss("least_squares", 1.0 / N)
+        meth, ometh, reg = scsopt.ProxLQNSCORE(m=5), O.ProxLQNSCORE(m=5), "l1"
+    else:
+        y = (rng.random(N) < 0.5).astype(float)
+        f, out = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N)
+        of = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+        meth, ometh, reg = scsopt.ProxGGNSCORE(), O.ProxGGNSCORE(), "l1"
+    p = scsopt.Problem(A, y, x0, f, 1e-3, out_fn=out)
+    om = O.Problem(A.toarray(), y, x0, of, 1e-3)
+    perm = np.random.default_rng(4).permutation(N)
+    s = scsopt.iterate(meth, p, reg, scsopt.PHuberSmootherL1L2(1.0), batch_size=400, batch_perm=perm, max_epoch=5,
+                       verbose=0)
+    o = O.iterate(ometh, om, reg, O.PHuberSmootherL1L2(1.0), max_epoch=5,
+                  batches=O.loader_batches(N, 400, perm=perm))
+    assert s.epochs == o.epochs and len(s.obj) == len(o.obj)
+    np.testing.assert_allclose(s.obj, o.obj, rtol=1e-8)
+    np.testing.assert_allclose(s.x, o.x, rtol=1e-6, atol=1e-9)
