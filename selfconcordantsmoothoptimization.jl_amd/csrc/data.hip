@@ -221,8 +221,9 @@ __global__ void gather_rows_kernel(const double* __restrict__ A, int64_t Npad, c
     const int64_t t = o & 15, f = (o >> 4) & 127, ps = o >> 11;   // ((p*Sb + s)*128 + f)*16 + t
     const int64_t s = ps % Sb, p = ps / Sb;
     const int64_t r = s * 16 + t, j = p * 128 + f;
-    Ab[o] = (r < n) ? A[tiled_off(S, rows[r], j)] : 0.0;
-    if (j == 0) yb[r] = (r < n) ? y[rows[r]] : 0.0;
+    const int64_t src = (r < n) ? rows[r] : -1;   // -1: a zero row (rows held by other ranks)
+    Ab[o] = (src >= 0) ? A[tiled_off(S, src, j)] : 0.0;
+    if (j == 0) yb[r] = (src >= 0) ? y[src] : 0.0;
   }
 }
 

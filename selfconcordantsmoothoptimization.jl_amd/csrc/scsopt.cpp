@@ -182,6 +182,9 @@ struct scs_ctx {
   std::vector<NView> bpool;    // gathered views, one per distinct batch size
   std::vector<int64_t> bheld;  // the batch each pool view currently holds (-1: none)
   int bview = -1;              // the selected batch's pool view (-1: the full data)
+  // all ranks' rows (GGN sample-space branch with N_global + 1 <= m on several ranks)
+  NView gview;
+  bool gview_ok = false;
   bool lu_fallback_used = false;
 
   // caches (CSE of identical evaluations; keyed by the host x content)
@@ -921,10 +924,59 @@ double step_size_newton(scs_ctx* c, int64_t iter, bool* needs_ls) {
 }
 
 // ggn_score_step's sample-space branch (prox-GGN-SCORE.jl:124-127, N + 1 <= m) -> c->d
+void ggn_sample_direction(scs_ctx* c, const double* xh);
+
+// The sample-space branch across ranks: its (N+1) x (N+1) system couples every pair of
+// samples, so the ranks' rows are all-gathered once (each rank writes its rows into the
+// zeroed reduce buffer at their global positions; the sum is the full A and y, at most
+// N_global·m <= m² doubles -- the size of the feature branch's Gram exchange) and every
+// rank runs the single-rank branch on that view, redundantly, as it does the m x m solve.
+void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
+  if (c->sparse) fail(c, SCS_ERR_ARG, "the sharded GGN sample-space branch needs a dense A");
+  if (!c->gview_ok) {
+    const int64_t Ng = c->Nglob, Npg = round_up(std::max<int64_t>(Ng, 1), 16);
+    if (Npg * c->mpad + Npg > c->red_cap) fail(c, SCS_ERR_COMM, "reduce buffer too small for the row all-gather");
+    std::vector<int64_t> rows(Ng, -1);
+    for (int64_t r = 0; r < c->N; ++r) rows[c->row0 + r] = r;
+    int64_t* drows = dalloc<int64_t>(c, Ng);
+    HCK(hipMemcpyAsync(drows, rows.data(), sizeof(int64_t) * Ng, hipMemcpyHostToDevice, c->st));
+    HCK(launch_gather_rows(c->A, c->Npad, c->y, drows, Ng, Npg, c->mpad, c->red, c->red + Npg * c->mpad, c->st));
+    allreduce(c, c->red, Npg * c->mpad + Npg);
+    NView& v = c->gview;
+    v.N = v.Nglob = Ng;
+    v.Npad = Npg;
+    v.nstage = Npg / 16;
+    v.A = dalloc<double>(c, (size_t)Npg * c->mpad);
+    v.y = dalloc<double>(c, Npg);
+    HCK(hipMemcpyAsync(v.A, c->red, sizeof(double) * Npg * c->mpad, hipMemcpyDeviceToDevice, c->st));
+    HCK(hipMemcpyAsync(v.y, c->red + Npg * c->mpad, sizeof(double) * Npg, hipMemcpyDeviceToDevice, c->st));
+    sync(c);
+    dfree_t(c, drows);
+    swap_view(c, v);
+    alloc_nspace(c);
+    swap_view(c, v);
+    c->gview_ok = true;
+  }
+  struct Scope {   // the gathered rows on one logical rank, restored even when the step fails
+    scs_ctx* c;
+    int nr;
+    explicit Scope(scs_ctx* cc) : c(cc), nr(cc->nranks) {
+      swap_view(c, c->gview);
+      c->nranks = 1;
+      invalidate_caches(c);
+    }
+    ~Scope() {
+      swap_view(c, c->gview);
+      c->nranks = nr;
+      invalidate_caches(c);
+    }
+  } scope(c);
+  ggn_sample_direction(c, xh);
+}
+
 void ggn_sample_direction(scs_ctx* c, const double* xh) {
   const int64_t N = c->N, m = c->m;
-  if (c->nranks > 1)
-    fail(c, SCS_ERR_ARG, "ProxGGNSCORE sample-space branch (N + 1 <= m) runs on one rank (its system is N x N)");
+  if (c->nranks > 1) return ggn_sample_direction_sharded(c, xh);
   ensure_blas(c);
   if (!c->At) {
     const double* A = dense_A(c);
@@ -1172,7 +1224,12 @@ int scs_reduce_buffer_size(scs_ctx* c, int64_t* nd) {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "reduce buffer size needs the data dimensions");
     const int64_t nb = c->mpad / 128;
     const int64_t tsz = (nb * (nb + 1) / 2 + nb) * 128 * 128;   // 128 x 128 slots (tall lists add <= nb)
-    *nd = std::max<int64_t>(tsz + c->mpad, c->mpad) + 64;
+    int64_t need = std::max<int64_t>(tsz + c->mpad, c->mpad);
+    if (c->Nglob + 1 <= c->m) {   // GGN sample-space branch across ranks: all-gather of A and y
+      const int64_t Ng = round_up(std::max<int64_t>(c->Nglob, 1), 16);
+      need = std::max<int64_t>(need, Ng * c->mpad + Ng);
+    }
+    *nd = need + 64;
   });
 }
 
@@ -1235,6 +1292,8 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->cinfo);
   chol_aux_free(&c->caux);
   clear_batches(c);
+  free_view(c, c->gview);
+  c->gview_ok = false;
   dfree_t(c, c->dinfo);
   dfree_t(c, c->ipiv);
   c->ntiles = c->nslots = 0;
@@ -1670,9 +1729,6 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
     if (method < SCS_PROX_NSCORE || method > SCS_PROX_LQNSCORE) fail(c, SCS_ERR_ARG, "unknown method %d", method);
     if (method == SCS_PROX_GGNSCORE && (c->generic || c->loss == SCS_LOSS_QUADRATIC))
       fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs a data problem with an out_fn (GGN kind)");
-    if (method == SCS_PROX_GGNSCORE && c->Nglob + 1 <= c->m && c->nranks > 1)
-      fail(c, SCS_ERR_ARG, "ProxGGNSCORE sample-space branch (N+1 <= m, prox-GGN-SCORE.jl:124-127) runs on one "
-                           "rank (its system is N x N)");
     c->method = method;
     c->ss_type = ss_type;
     c->use_prox = use_prox;

@@ -17,6 +17,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 N, M = 3001, 192
+NS = 151          # sample-space case: N + 1 <= M
 
 
 def _free_port():
@@ -37,6 +38,12 @@ def _run(method, comm=None):
     elif method == "nscore":
         f, out, kind = losses.logistic_margin(1.0 / N), None, 2
         meth = scsopt.ProxNSCORE()
+    elif method == "ggn_sample":   # N + 1 <= m: the sharded sample-space branch (row all-gather)
+        f, out, kind = losses.logistic_ce(1.0 / NS), losses.sigmoid_ce(1.0 / NS), 1
+        meth = scsopt.ProxGGNSCORE()
+        p = scsopt.Problem.synthetic(NS, M, x0, f, 2e-3, kind=kind, seed=13, out_fn=out, comm=comm)
+        sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=6, verbose=0)
+        return {"obj": list(sol.obj), "x": sol.x.copy(), "epochs": sol.epochs}
     elif method == "ggn_ls_cached":
         f, out, kind = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N), 3
         meth = scsopt.ProxGGNSCORE()
@@ -61,7 +68,7 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = {}
-    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached"):
+    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample"):
         comm = shard.Comm(device=torch.device("cuda", 0))
         res[method] = _run(method, comm)
     out[rank] = res
@@ -77,7 +84,7 @@ def test_two_rank_shard_matches_single_process(tall, monkeypatch):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached"):
+    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample"):
         full = _run(method)
         r0, r1 = out[0][method], out[1][method]
         assert r0["epochs"] == r1["epochs"] == full["epochs"]
