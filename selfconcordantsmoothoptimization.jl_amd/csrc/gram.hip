@@ -443,135 +443,6 @@ __global__ __launch_bounds__(512, 1) void gram_glds_kernel(
       }
 }
 
-// Variant: global loads issued two stages ahead (two register staging sets,
-// loop unrolled by 2 so every set index is static).
-__global__ __launch_bounds__(256, 2) void gram_f64_pf2_kernel(
-    const double* __restrict__ A, int64_t lda, const double* __restrict__ w, int64_t k0, int64_t Nk,
-    const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int packed, int accumulate) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GT * GBK];
-  const int orig = blockIdx.x;
-  const int q8 = ntiles / 8, r8 = ntiles % 8, xcd = orig % 8;
-  const int tix = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int2 tl = tiles[tix];
-  const int bi = tl.x, bj = tl.y;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const double* __restrict__ Ai = A + (int64_t)bi * GT * lda;
-  const double* __restrict__ Aj = A + (int64_t)bj * GT * lda;
-  const int sc = tid & 7;
-  const int sf0 = tid >> 3;
-  v2d ra0[4], rb0[4], rw0, ra1[4], rb1[4], rw1;
-  const int nk = (int)((Nk - k0) / GBK);
-
-  // buffer loads: wave-uniform descriptors (panel bases), one 32-bit per-lane offset,
-  // the feature-group / sample offsets in soffset (cdna_hip_programming.md T8/T20)
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ai, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Aj, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rWv = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, 0x7fffffff, 0x00020000);
-  const int voff = (int)(((int64_t)sf0 * lda + 2 * sc) * 8);
-  const int wvoff = 2 * sc * 8;
-  const int fstride = (int)(32 * lda * 8);
-#define GLOAD(RA, RB, RW, n0)                                                                              \
-  do {                                                                                                     \
-    const int nb_ = (int)((n0) * 8);                                                                       \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                        \
-      RA[i] = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rA, voff, nb_ + i * fstride, 0)); \
-      RB[i] = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rB, voff, nb_ + i * fstride, 0)); \
-    }                                                                                                      \
-    RW = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rWv, wvoff, nb_, 0));               \
-    __builtin_amdgcn_sched_barrier(0); /* keep each set's loads contiguous in issue order */               \
-  } while (0)
-#define SWRITE(RA, RB, RW, buf)                                            \
-  do {                                                                     \
-    double* la_ = lds + ((buf) * 2 + 0) * GT * GBK;                        \
-    double* lb_ = lds + ((buf) * 2 + 1) * GT * GBK;                        \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                        \
-      const int f = sf0 + 32 * i;                                          \
-      const int off = f * GBK + 2 * (sc ^ swz(f));                         \
-      *(v2d*)(la_ + off) = RA[i];                                          \
-      *(v2d*)(lb_ + off) = RB[i] * RW;                                     \
-    }                                                                      \
-  } while (0)
-
-  v4d acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
-  const int fl = lane & 15, g = lane >> 4, s = swz(fl);
-
-  auto compute = [&](int buf) {
-    const double* la = lds + (buf * 2 + 0) * GT * GBK;
-    const double* lb = lds + (buf * 2 + 1) * GT * GBK;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int pc = ((4 * p + g) ^ s) * 2;
-      v2d a[4], b[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        a[t] = *(const v2d*)(la + (wr * 64 + 16 * t + fl) * GBK + pc);
-        b[t] = *(const v2d*)(lb + (wc * 64 + 16 * t + fl) * GBK + pc);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int ti = 0; ti < 4; ++ti)
-#pragma unroll
-          for (int tj = 0; tj < 4; ++tj)
-            acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
-    }
-  };
-
-  // prologue: stage 0 -> LDS buf 0, stage 1 in flight (set 1)
-  GLOAD(ra0, rb0, rw0, k0);
-  if (nk > 1) GLOAD(ra1, rb1, rw1, k0 + GBK);
-  SWRITE(ra0, rb0, rw0, 0);
-  LDS_BARRIER();
-  int k = 0;
-  for (; k + 2 <= nk; k += 2) {
-    // even step: compute buf0 (stage k); set0 <- stage k+2; buf1 <- set1 (stage k+1)
-    if (k + 2 < nk) GLOAD(ra0, rb0, rw0, k0 + (int64_t)(k + 2) * GBK);
-    compute(0);
-    SWRITE(ra1, rb1, rw1, 1);
-    LDS_BARRIER();
-    // odd step: compute buf1 (stage k+1); set1 <- stage k+3; buf0 <- set0 (stage k+2)
-    if (k + 3 < nk) GLOAD(ra1, rb1, rw1, k0 + (int64_t)(k + 3) * GBK);
-    compute(1);
-    if (k + 2 < nk) SWRITE(ra0, rb0, rw0, 0);
-    LDS_BARRIER();
-  }
-  if (k < nk) compute(0);  // odd stage count: last stage sits in buf 0
-#undef GLOAD
-#undef SWRITE
-
-  if (packed) {
-    double* Gt = G + (int64_t)tix * GT * GT;
-#pragma unroll
-    for (int ti = 0; ti < 4; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < 4; ++tj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wr * 64 + 16 * ti + g + 4 * r;
-          const int col = wc * 64 + 16 * tj + fl;
-          if (accumulate) Gt[col * GT + row] += acc[ti][tj][r];
-          else Gt[col * GT + row] = acc[ti][tj][r];
-        }
-  } else {
-#pragma unroll
-    for (int ti = 0; ti < 4; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < 4; ++tj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = (int64_t)bi * GT + wr * 64 + 16 * ti + g + 4 * r;
-          const int64_t col = (int64_t)bj * GT + wc * 64 + 16 * tj + fl;
-          if (accumulate) G[col * ldg + row] += acc[ti][tj][r];
-          else G[col * ldg + row] = acc[ti][tj][r];
-        }
-  }
-}
-
 // Scatter packed tiles (list order) into the upper triangle of a column-major
 // m_pad x m_pad matrix (same placement as GRAM_UPPER).
 __global__ void gram_unpack_kernel(const double* __restrict__ P, const int2* __restrict__ tiles,
@@ -656,10 +527,9 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   constexpr int NB = GT / FS;         // A2 staging chunks per thread per stage (4 or 2)
   constexpr int NMM = 2 * NTI * 4;    // MFMAs per fragment set (2 u x NTI x 4)
   constexpr int NRD = NTI + 4;        // ds_read_b128 per fragment set
-  constexpr int TAIL = PIPE == 7 ? NMM / 8 : (PIPE == 8 ? 3 * NMM / 8 : NMM / 4);   // MFMAs left for phase 2b
+  constexpr int TAIL = NMM / 4;       // MFMAs left for phase 2b (1/8 and 3/8 measured within noise)
   const int packed = flags & GRAM_PACKED, accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
-  // PIPE 4/5 (timing builds, TI = 2): LDS padding -> one workgroup (one wave per SIMD) per CU
-  __shared__ __attribute__((aligned(16))) double lds[(PIPE >= 4 ? 5 * GT * GBK : (GTI + GT) * GBK)];
+  __shared__ __attribute__((aligned(16))) double lds[(GTI + GT) * GBK];
   const int orig = blockIdx.x;
   const int xcd = orig % 8;
   int bi, bj, tix, part = -1;
@@ -686,16 +556,13 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int sc = tid & 7, sf0 = tid >> 3;
-  if (PIPE >= 4 && tid == 0) lds[4 * GT * GBK] = 0.0;   // keep the padding allocated
   const int64_t st0 = k0 / GBK;
   // this thread's 16-B chunks of a stage: feature sf0 + FS i of the A1 rows (panel
   // (GTI/128) bi + f/128) and of the A2 rows (panel bj), samples 2 sc, 2 sc + 1.
-  // S < 0 (layout experiment, TI = 2): stage-major blocks, block (p, s) at s * (-S) + p
-  const int64_t pstr = S > 0 ? S : 1, sstr = S > 0 ? 1 : -S;
   const double* srcA = CM ? A + ((int64_t)bi * GTI + sf0) * S + k0 + 2 * sc
-                          : A + ((int64_t)bi * (GTI / GT) * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
+                          : A + ((int64_t)bi * (GTI / GT) * S + st0) * GT * GBK + sf0 * GBK + 2 * sc;
   const double* srcB = CM ? A + ((int64_t)bj * GT + sf0) * S + k0 + 2 * sc
-                          : A + ((int64_t)bj * pstr + st0 * sstr) * GT * GBK + sf0 * GBK + 2 * sc;
+                          : A + ((int64_t)bj * S + st0) * GT * GBK + sf0 * GBK + 2 * sc;
   const double* srcW = w + k0 + 2 * sc;
   double* la = lds;
   double* lb = lds + GTI * GBK;
@@ -707,18 +574,18 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   }
   v2d ra[NA], rb[NB], rw;
   auto gload = [&](int64_t st) {
-    if ((PIPE == 3 || PIPE == 5) && st >= 2) return;   // timing builds: no global loads after the prologue
+    if (PIPE == 3 && st >= 2) return;   // timing build: no global loads after the prologue
     if (CM) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) ra[i] = *(const v2d*)(srcA + st * GBK + (int64_t)FS * i * S);
 #pragma unroll
       for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + st * GBK + (int64_t)FS * i * S);
     } else {
-      const int64_t so = st * sstr * GT * GBK;
+      const int64_t so = st * GT * GBK;
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int f = FS * i;   // + sf0 (in srcA): the panel of f is f / 128 (FS divides 128)
-        ra[i] = *(const v2d*)(srcA + so + (f >> 7) * pstr * GT * GBK + (f & 127) * GBK);
+        ra[i] = *(const v2d*)(srcA + so + (f >> 7) * S * GT * GBK + (f & 127) * GBK);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + so + FS * GBK * i);
@@ -757,11 +624,9 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   };
   auto barrier = [&]() {   // also a scheduling fence: nothing (e.g. the w products) crosses a phase
     __builtin_amdgcn_sched_barrier(0);
-    if (PIPE == 6) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS traffic is done
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (PIPE == 6) __builtin_amdgcn_s_setprio(3);
     __builtin_amdgcn_sched_barrier(0);
   };
   const int nk = (int)((Nk - k0) / GBK);
@@ -999,20 +864,9 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st) {
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
-  if (noload >= 18 && noload <= 20)   // 256 x 128 interleaved schedule variants: setprio / tail 1/8 / tail 3/8
-    hipLaunchKernelGGL((noload == 18 ? gram_sia_kernel<6, 4> : noload == 19 ? gram_sia_kernel<7, 4>
-                                                                              : gram_sia_kernel<8, 4>),
-                       dim3(ntiles), dim3(512), 0, st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags,
-                       nullptr, 0, 0, nullptr);
-  else if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
+  if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
     hipLaunchKernelGGL((noload == 16 ? gram_sia_kernel<1, 4> : gram_sia_kernel<3, 4>), dim3(ntiles), dim3(512), 0,
                        st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
-  else if (noload == 14 || noload == 15)   // one workgroup per CU (LDS padding): loaded / no-load
-    hipLaunchKernelGGL((noload == 14 ? gram_sia_kernel<4> : gram_sia_kernel<5>), dim3(ntiles), dim3(256), 0, st, A,
-                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
-  else if (noload == 13)   // layout experiment: stage-major panel blocks (S passed negated: -number of panels)
-    hipLaunchKernelGGL((gram_sia_kernel<1>), dim3(ntiles), dim3(256), 0, st, A, -(int64_t)(ldg / GT), w, k0, k1,
-                       tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (noload == 12)
     hipLaunchKernelGGL((gram_sia_kernel<3>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, w, k0, k1, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -1038,9 +892,6 @@ hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t
   else if (noload == 3)
     hipLaunchKernelGGL((gram_f64_kernel<false, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, k0, k1, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
-  else if (noload == 2)
-    hipLaunchKernelGGL(gram_f64_pf2_kernel, dim3(ntiles), dim3(256), 0, st, A, lda, w, k0, k1, tiles, ntiles, G, ldg,
-                       0, accumulate);
   else if (noload)
     hipLaunchKernelGGL((gram_f64_kernel<true, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w, k0, k1, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
