@@ -234,7 +234,8 @@ def main():
             line["config"]["gram_cache"] = True
         line["breakdown_ms_per_step"] = {k.replace("_ms", ""): tm[k] / steps for k in tm if k.endswith("_ms")}
         line["objective_last"] = objs[-1]
-        if not args.no_cpu_baseline and args.config == "c1":
+        do_cpu = not args.no_cpu_baseline and world == 1   # the CPU baseline: rank 0 at N = 1 only
+        if do_cpu and args.config == "c1":
             try:
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline_c1.py")],
                                      capture_output=True, text=True, timeout=120, check=True)
@@ -242,7 +243,7 @@ def main():
                 line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
             except Exception as e:  # the baseline is reported, never the target
                 line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
-        if not args.no_cpu_baseline and args.config == "c5":
+        if do_cpu and args.config == "c5":
             try:
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline_lqn.py"), "--N", str(N),
                                       "--m", str(m), "--rho", str(cfg["rho"]), "--mem", str(cfg["mem"])],
@@ -252,7 +253,7 @@ def main():
                 line["cpu_baseline"]["t_iter_s"] = cb["t_iter_s"]
             except Exception as e:  # the baseline is reported, never the target
                 line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
-        if not args.no_cpu_baseline and args.config in ("c2", "c3", "c4"):
+        if do_cpu and args.config in ("c2", "c3", "c4"):
             env = dict(os.environ)
             cores = int(env.get("OMP_NUM_THREADS", "16"))
             env["OPENBLAS_NUM_THREADS"] = str(cores)
