@@ -65,7 +65,8 @@ hipError_t launch_score_tail(const double* x, const double* d, const double* gr,
                              double* hinv, double* zbuf, double* x_new, double* dx, double* scal, hipStream_t st);
 hipError_t launch_prox_only(const ProxArgsH& P, const double* z, const double* Hr, double step, int64_t m,
                             double* hinv, double* out, hipStream_t st);
-hipError_t launch_reg_value(const ProxArgsH& P, const double* x, int64_t m, double* out, hipStream_t st);
+hipError_t launch_reg_value(const ProxArgsH& P, const double* x, int64_t m, double* out, double* part,
+                            hipStream_t st);
 hipError_t launch_dot(const double* a, const double* b, int64_t m, double* out, hipStream_t st);
 hipError_t launch_axpby(const double* a, double lam, const double* b, int64_t m, double* out, hipStream_t st);
 hipError_t launch_sub(const double* a, const double* b, int64_t m, double* out, hipStream_t st);
@@ -82,7 +83,7 @@ hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const i
                            const double* g, int64_t m, double* q, double* d, double* ab, double* work,
                            hipStream_t st);
 hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
-                               double* Yslot, double* scal, hipStream_t st);
+                               double* Yslot, double* scal, double* part, hipStream_t st);
 hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st);
 hipError_t launch_nonfinite(const double* G, int64_t ldg, int64_t m, const double* rhs, int* flag, hipStream_t st);
 hipError_t launch_fill(double* a, int64_t n, double v, hipStream_t st);

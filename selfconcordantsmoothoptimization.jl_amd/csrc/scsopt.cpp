@@ -395,7 +395,7 @@ void alloc_mspace(scs_ctx* c) {
     *v = dalloc<double>(c, mp);
   }
   dfree_t(c, c->scal);
-  c->scal = dalloc<double>(c, 64);
+  c->scal = dalloc<double>(c, 64 + 3 * 256);   // scalars + the multi-workgroup tail / get_reg partials
   if (!c->hscal) HCK(hipHostMalloc((void**)&c->hscal, 64 * sizeof(double), hipHostMallocDefault));
 }
 
@@ -748,7 +748,7 @@ void grad_q_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
 }
 
 double eval_reg_dev(scs_ctx* c, const double* xd) {
-  HCK(launch_reg_value(prox_args(c), xd, c->m, c->scal + 10, c->st));
+  HCK(launch_reg_value(prox_args(c), xd, c->m, c->scal + 10, c->scal + 64 + 2 * 256, c->st));
   d2h(c, c->hscal + 10, c->scal + 10, 1);
   sync(c);
   return c->hscal[10];
@@ -1134,7 +1134,7 @@ void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, dou
   grad_q_dev(c, x_new, c->xn, c->gqn);
   const int slot = c->spare;
   HCK(launch_lbfgs_update(c->q, c->gqn, c->gq, m, c->S + (int64_t)slot * c->mpad, c->Yv + (int64_t)slot * c->mpad,
-                          c->scal + 16, c->st));
+                          c->scal + 16, c->scal + 64, c->st));
   d2h(c, c->hscal + 16, c->scal + 16, 2);
   sync(c);
   const double dg = c->hscal[16], gg = c->hscal[17];

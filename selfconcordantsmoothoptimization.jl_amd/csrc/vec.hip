@@ -247,6 +247,83 @@ __global__ __launch_bounds__(VB) void score_tail_kernel(
   }
 }
 
+// Multi-workgroup SCORE tail (large m, elementwise prox: l1 / l2 / indbox, or no prox): the
+// same arithmetic as score_tail_kernel with the two norms reduced over TAIL_G workgroups --
+// per-block partials in `part`, summed by every block in the same fixed order, so all blocks
+// agree bitwise on η, α.  (gl keeps the one-workgroup kernel: its group pass is sequential.)
+constexpr int TAIL_G = 256, TAIL_T = 256;
+
+__device__ __forceinline__ double fixed_sum(const double* __restrict__ part, int n, double* sh) {
+  // one wave: lane-strided partial sums, then the wave butterfly (fixed order)
+  if (threadIdx.x < 64) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += 64) v += part[i];
+    v = wave_sum(v);
+    if (threadIdx.x == 0) sh[0] = v;
+  }
+  __syncthreads();
+  const double r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(TAIL_T) void tail_eta_kernel(const double* __restrict__ gr, const double* __restrict__ Hr,
+                                                          int64_t m, double lam, double* __restrict__ hinv,
+                                                          double* __restrict__ part) {
+  __shared__ double sh[TAIL_T / 64];
+  double p = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)TAIL_G * TAIL_T) {
+    const double hi = 1.0 / Hr[i];
+    hinv[i] = hi;
+    const double lgr = lam * gr[i];
+    p += lgr * (hi * lgr);
+  }
+  const double s = block_sum<TAIL_T>(p, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(TAIL_T) void tail_apply_kernel(
+    const double* __restrict__ x, const double* __restrict__ d, int64_t m, double Mg, double step_host,
+    const double* __restrict__ step_dev, ProxArgs P, const double* __restrict__ hinv, double* __restrict__ zbuf,
+    double* __restrict__ x_new, double* __restrict__ dx, double* __restrict__ part, double* __restrict__ scal) {
+  __shared__ double sh[TAIL_T / 64];
+  const double step = step_dev ? *step_dev : step_host;
+  const double eta = sqrt(fixed_sum(part, TAIL_G, sh));
+  const double alpha = step / (1.0 + Mg * eta);
+  const double safe_alpha = jl_min(1.0, alpha);
+  double p = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)TAIL_G * TAIL_T) {
+    const double dxi = safe_alpha * d[i];
+    dx[i] = dxi;
+    const double z = x[i] + dxi;
+    zbuf[i] = z;
+    double xn = z;
+    if (P.use_prox) {
+      if (P.reg == SCS_REG_L1) xn = prox_l1_d(z, hinv[i], P.lam, step);
+      else if (P.reg == SCS_REG_L2) xn = prox_l2_d(z, hinv[i], P.lam, step);
+      else xn = prox_box_d(z, P.lb[i], P.ub[i]);
+    }
+    x_new[i] = xn;
+    const double r = P.use_prox ? (xn - x[i]) : dxi;
+    p += r * r;
+  }
+  const double s = block_sum<TAIL_T>(p, sh);
+  if (threadIdx.x == 0) {
+    part[TAIL_G + blockIdx.x] = s;
+    if (blockIdx.x == 0) {
+      scal[1] = eta;
+      scal[2] = alpha;
+      scal[3] = step;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void tail_pri_kernel(const double* __restrict__ part, double* __restrict__ scal) {
+  __shared__ double sh[1];
+  const double s = fixed_sum(part + TAIL_G, TAIL_G, sh);
+  if (threadIdx.x == 0) scal[0] = sqrt(s);
+}
+
 // prox only (kernel-level parity entry point)
 __global__ __launch_bounds__(VB) void prox_only_kernel(ProxArgs P, const double* __restrict__ z,
                                                        const double* __restrict__ Hr, double step, int64_t m,
@@ -662,6 +739,16 @@ hipError_t launch_score_tail(const double* x, const double* d, const double* gr,
                              double lam, double Mg, double step_host, const double* step_dev, const ProxArgsH& Ph,
                              double* hinv, double* zbuf, double* x_new, double* dx, double* scal, hipStream_t st) {
   ProxArgs P{Ph.reg, Ph.use_prox, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
+  // one workgroup is ~130 us at m = 65536 (C5); the multi-workgroup form ~10 us.  Partials live
+  // in scal[64 .. 64 + 2 TAIL_G) (alloc_mspace).
+  if (m >= 16384 && !(Ph.use_prox && Ph.reg == SCS_REG_GL)) {
+    double* part = scal + 64;
+    hipLaunchKernelGGL(tail_eta_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, gr, Hr, m, lam, hinv, part);
+    hipLaunchKernelGGL(tail_apply_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, x, d, m, Mg, step_host, step_dev, P,
+                       hinv, zbuf, x_new, dx, part, scal);
+    hipLaunchKernelGGL(tail_pri_kernel, dim3(1), dim3(64), 0, st, part, scal);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(score_tail_kernel, dim3(1), dim3(VB), 0, st, x, d, gr, Hr, m, lam, Mg, step_host, step_dev, P,
                      hinv, zbuf, x_new, dx, scal);
   return hipGetLastError();
@@ -674,8 +761,34 @@ hipError_t launch_prox_only(const ProxArgsH& Ph, const double* z, const double* 
   return hipGetLastError();
 }
 
-hipError_t launch_reg_value(const ProxArgsH& Ph, const double* x, int64_t m, double* out, hipStream_t st) {
+// get_reg for l1 / l2 / indbox over TAIL_G workgroups (partials, then a fixed-order sum)
+__global__ __launch_bounds__(TAIL_T) void reg_part_kernel(ProxArgs P, const double* __restrict__ x, int64_t m,
+                                                          double* __restrict__ part) {
+  __shared__ double sh[TAIL_T / 64];
+  double p = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)TAIL_G * TAIL_T) {
+    if (P.reg == SCS_REG_INDBOX) p += (x[i] < P.lb[i] || x[i] > P.ub[i]) ? 1.0 : 0.0;
+    else p += (P.reg == SCS_REG_L2) ? x[i] * x[i] : fabs(x[i]);
+  }
+  const double s = block_sum<TAIL_T>(p, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(64) void reg_final_kernel(ProxArgs P, const double* __restrict__ part,
+                                                       double* __restrict__ out) {
+  __shared__ double sh[1];
+  const double s = fixed_sum(part, TAIL_G, sh);
+  if (threadIdx.x == 0) out[0] = (P.reg == SCS_REG_INDBOX) ? (s > 0 ? __builtin_inf() : 0.0) : P.lam * s;
+}
+
+hipError_t launch_reg_value(const ProxArgsH& Ph, const double* x, int64_t m, double* out, double* part,
+                            hipStream_t st) {
   ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
+  if (m >= 16384 && Ph.reg != SCS_REG_GL && part) {
+    hipLaunchKernelGGL(reg_part_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, P, x, m, part);
+    hipLaunchKernelGGL(reg_final_kernel, dim3(1), dim3(64), 0, st, P, part, out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(reg_value_kernel, dim3(1), dim3(VB), 0, st, P, x, m, out);
   return hipGetLastError();
 }
@@ -729,8 +842,49 @@ hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const i
   }
   return hipGetLastError();
 }
+// the same update over TAIL_G workgroups (large m): per-block partial dots, fixed-order sums
+__global__ __launch_bounds__(TAIL_T) void lbfgs_update_part_kernel(const double* __restrict__ dh,
+                                                                   const double* __restrict__ gq_new,
+                                                                   const double* __restrict__ gq, int64_t m,
+                                                                   double* __restrict__ Sslot,
+                                                                   double* __restrict__ Yslot,
+                                                                   double* __restrict__ part) {
+  __shared__ double sh[TAIL_T / 64];
+  double dg = 0.0, gg = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)TAIL_G * TAIL_T) {
+    const double gh = gq_new[i] - gq[i];
+    Yslot[i] = gh;
+    Sslot[i] = dh[i];
+    dg += dh[i] * gh;
+    gg += gh * gh;
+  }
+  dg = block_sum<TAIL_T>(dg, sh);
+  gg = block_sum<TAIL_T>(gg, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = dg;
+    part[TAIL_G + blockIdx.x] = gg;
+  }
+}
+
+__global__ __launch_bounds__(64) void lbfgs_update_final_kernel(const double* __restrict__ part,
+                                                                double* __restrict__ scal) {
+  __shared__ double sh[1];
+  const double dg = fixed_sum(part, TAIL_G, sh);
+  const double gg = fixed_sum(part + TAIL_G, TAIL_G, sh);
+  if (threadIdx.x == 0) {
+    scal[0] = dg;
+    scal[1] = gg;
+  }
+}
+
 hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
-                               double* Yslot, double* scal, hipStream_t st) {
+                               double* Yslot, double* scal, double* part, hipStream_t st) {
+  if (m >= 16384 && part) {
+    hipLaunchKernelGGL(lbfgs_update_part_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, dh, gq_new, gq, m, Sslot, Yslot,
+                       part);
+    hipLaunchKernelGGL(lbfgs_update_final_kernel, dim3(1), dim3(64), 0, st, part, scal);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(lbfgs_update_kernel, dim3(1), dim3(VB), 0, st, dh, gq_new, gq, m, Sslot, Yslot, scal);
   return hipGetLastError();
 }

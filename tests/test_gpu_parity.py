@@ -477,18 +477,25 @@ def test_indefinite_system_lu_fallback():
     np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
 
 
-def test_lqn_large_m_multiblock_two_loop():
-    """m above the single-workgroup two-loop limit (16384): the multi-workgroup recursion
-    (one launch per step, fixed-order chunk partials) against the oracle."""
+@pytest.mark.parametrize("reg", ["l1", "l2", "indbox"])
+def test_lqn_large_m_multiblock_two_loop(reg):
+    """m above the single-workgroup limits (16384): the multi-workgroup two-loop recursion, SCORE
+    tail (η, prox, pri_res_norm), get_reg and L-BFGS memory update (fixed-order partials) against
+    the oracle, for each elementwise prox."""
     N, m = 256, 20000
     rng = np.random.default_rng(12)
     A = rng.standard_normal((N, m)) / np.sqrt(m)
     y = rng.standard_normal(N)
     x0 = rng.standard_normal(m) * 0.1
-    p = scsopt.Problem(A, y, x0, losses.least_squares(1.0 / N), 1e-4)
-    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), 1e-4)
-    sol = scsopt.iterate(scsopt.ProxLQNSCORE(m=6), p, "l1", scsopt.PHuberSmootherL1L2(0.5), max_epoch=10, verbose=0)
-    osol = O.iterate(O.ProxLQNSCORE(m=6), om, "l1", O.PHuberSmootherL1L2(0.5), max_epoch=10)
+    C_set = [-0.05, 0.05] if reg == "indbox" else None
+    p = scsopt.Problem(A, y, x0, losses.least_squares(1.0 / N), 1e-4, C_set=C_set)
+    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), 1e-4, C_set=C_set)
+    if reg == "indbox":
+        hm, ohm = scsopt.PHuberSmootherIndBox(-0.05, 0.05, 0.5), O.PHuberSmootherIndBox(-0.05, 0.05, 0.5)
+    else:
+        hm, ohm = scsopt.PHuberSmootherL1L2(0.5), O.PHuberSmootherL1L2(0.5)
+    sol = scsopt.iterate(scsopt.ProxLQNSCORE(m=6), p, reg, hm, max_epoch=10, verbose=0)
+    osol = O.iterate(O.ProxLQNSCORE(m=6), om, reg, ohm, max_epoch=10)
     assert len(sol.obj) == len(osol.obj)
     np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
     np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
