@@ -12,7 +12,7 @@ using Random
 using SelfConcordantSmoothOptimization
 import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel
 
-export DeviceProblem, configure!
+export DeviceProblem, configure!, iterate_device!, set_gram_cache!
 
 const lib = joinpath(@__DIR__, "..", "scsopt", "libscsopt.so")
 
@@ -116,6 +116,11 @@ function smoother_kind(hμ)
     T <: OsBaSmootherGL && return (7, Float64[], Float64[])
     error("smoother $(T) has no device implementation")
 end
+
+# Opt-in reuse of the x-independent AᵀQA of least squares across steps (scs_set_gram_cache);
+# the reference recomputes it every step (prox-GGN-SCORE.jl:129) and that stays the default.
+set_gram_cache!(model::DeviceProblem, on::Bool=true) =
+    chk(ccall((:scs_set_gram_cache, lib), Cint, (Ptr{Cvoid}, Cint), model.ctx, on ? 1 : 0), model.ctx)
 
 method_code(m) = m isa ProxNSCORE ? 1 : m isa ProxGGNSCORE ? 2 : m isa ProxLQNSCORE ? 3 : error("unknown method")
 
