@@ -102,6 +102,7 @@ struct scs_ctx {
   int gram_cache = 0;
   double* Gk = nullptr;
   uint64_t data_gen = 1, gk_gen = 0;
+  bool g_from_cache = false;   // this step's G was copied from Gk (solve_system)
 
   // problem
   int loss = 0, ggn = 0;
@@ -794,7 +795,9 @@ void solve_system(scs_ctx* c, double* rhs) {
   const int64_t m = c->m, ld = c->mpad;
   hipEvent_t e0;
   tbegin(c, T_SOLVE, &e0);
-  HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+  // the LU fallback needs the system the in-place factor destroys: copied up front, or -- when
+  // this step's Gram came from the cache -- rebuilt from it only if the factor fails
+  if (!c->g_from_cache) HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
   HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
   HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
   int info = 0;
@@ -805,6 +808,10 @@ void solve_system(scs_ctx* c, double* rhs) {
     c->lu_fallback_used = false;
   } else {
     ensure_blas(c);
+    if (c->g_from_cache) {
+      HCK(hipMemcpyAsync(c->Gc, c->Gk, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+      HCK(launch_diag_add(c->Gc, c->mpad, m, c->lam, c->Hr, c->st));
+    }
     HCK(launch_symmetrize(c->Gc, ld, m, c->st));
     // a NaN / Inf in the system (a smoother's NaN, Appendix A) is no SingularException in the
     // reference: LAPACK getrf only flags exact zero pivots, and the solve comes out NaN
@@ -875,6 +882,7 @@ void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
   const bool cacheable = c->gram_cache && gram_x_independent(c);
   const size_t gbytes = sizeof(double) * (size_t)c->mpad * c->mpad;
   if (cacheable && c->Gk && c->gk_gen == c->data_gen) {   // the reduced Gram of an earlier step
+    c->g_from_cache = true;
     HCK(hipMemcpyAsync(c->G, c->Gk, gbytes, hipMemcpyDeviceToDevice, c->st));
     if (c->nranks > 1) {
       HCK(hipMemcpyAsync(c->red, vec_dev, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
@@ -1038,6 +1046,7 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
 // ProxNSCORE / ProxGGNSCORE step
 void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, double* dx, double* pri) {
   const int64_t m = c->m;
+  c->g_from_cache = false;
   HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
   const bool sample_space = (c->method == SCS_PROX_GGNSCORE) && (c->Nglob + 1 <= m) && c->ggn != SCS_GGN_NONE;
   if (sample_space) {

@@ -351,17 +351,28 @@ __global__ __launch_bounds__(VB) void reg_value_kernel(ProxArgs P, const double*
     if (threadIdx.x == 0) out[0] = P.lam * s;
     return;
   }
-  // fz (prox-reg-utils.jl:101-110): sequential over groups, twonorm sequential
-  if (threadIdx.x == 0) {
-    double fz = 0.0;
-    for (int g = 0; g < P.ngroups; ++g) {
+  // fz (prox-reg-utils.jl:101-110): the group terms w_g·‖(Px)_g‖ (twonorm sequential within a
+  // group) one thread per group, then their sum in group order by one thread -- the
+  // reference's own order, so the value is the same as the sequential loop's bit for bit
+  constexpr int GL_LDS = 4096;
+  __shared__ double gterm[GL_LDS];
+  double fz = 0.0;
+  for (int g0 = 0; g0 < P.ngroups; g0 += GL_LDS) {
+    const int ng = min(GL_LDS, P.ngroups - g0);
+    for (int g = threadIdx.x; g < ng; g += VB) {
       double nrm2 = 0.0;
-      for (int k = P.gstart[g]; k <= P.gend[g]; ++k) {
+      for (int k = P.gstart[g0 + g]; k <= P.gend[g0 + g]; ++k) {
         const double v = P.gmap ? x[P.gmap[k]] : x[k];
         nrm2 += v * v;
       }
-      fz += P.gw[g] * sqrt(nrm2);
+      gterm[g] = P.gw[g0 + g] * sqrt(nrm2);
     }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int g = 0; g < ng; ++g) fz += gterm[g];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
     gsum[0] = fz;
     out[0] = P.lam2 * fz + P.lam * s;
   }
