@@ -188,7 +188,7 @@ def main():
             gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])   # launches are timed under "solve"
             gram_flops = float(N_local) * m * (m + 1)   # algorithmic symmetric Gram per launch
             achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
-            traffic, kname = None, ("gram_sia_kernel<1, 4>" if m >= 8192 and (m // 128) % 2 == 0 else "gram_sia_kernel<1, 2>")
+            traffic, kname = None, ("gram_sia_kernel<1, 4>" if m >= 12288 and (m // 128) % 2 == 0 else "gram_sia_kernel<1, 2>")
             pmc = os.path.join(ROOT, "profiles", "r01_gram_pmc.json")   # tools/gpu_prof_c3.sh + tools/pmc_summary.py
             if os.path.exists(pmc) and world == 1:
                 with open(pmc) as f:

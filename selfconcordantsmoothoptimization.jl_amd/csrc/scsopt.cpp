@@ -432,9 +432,9 @@ void ensure_gram(scs_ctx* c) {
   std::vector<int2> tl((size_t)nb * (nb + 1) / 2 + nb), ul;
   int nt = 0;
   const char* sq = std::getenv("SCS_GRAM_TALL");
-  // 256 x 128 tiles (LDS-DMA kernel with pipelined fragment reads) from m = 8192 on: C3 67.1 TF/s,
-  // C2 65.2 vs 63.2 TF/s with the 128 x 128 register-staged tiles (profiles/r01/ab_gram_pipe.log)
-  c->tall = (nb % 2 == 0) && nb >= 64 && !(sq && sq[0] == '0');
+  // 256 x 128 tiles from m = 12288 on (interleaved kernels: C3 73-74 TF/s; at m = 8192 the 128 x 128
+  // tiles with 2 workgroups / CU are ~1 % faster, 72.5 vs 71.6 TF/s at C2)
+  c->tall = (nb % 2 == 0) && nb >= 96 && !(sq && sq[0] == '0');
   if (sq && sq[0] == '1') c->tall = (nb % 2 == 0);
   if (c->tall) {
     gram_tile_list_tall(nb, tl.data(), &nt);
