@@ -75,20 +75,22 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("tall", ["0", "1"])
-def test_two_rank_shard_matches_single_process(tall, monkeypatch):
-    """tall = "1" forces the 256 x 128 LDS-DMA Gram kernel (the C3/C2 kernel) at this small m, so the
-    packed multi-rank slots of its tile halves (gram_unpack) are exercised too."""
+@pytest.mark.parametrize("world,tall", [(2, "0"), (2, "1"), (4, "1")])
+def test_two_rank_shard_matches_single_process(world, tall, monkeypatch):
+    """tall = "1" forces the 256 x 128 Gram kernel (the C3 kernel) at this small m, so the packed
+    multi-rank slots of its tile halves (gram_unpack) are exercised too; world = 4 splits the 3001
+    rows unevenly (751/750/750/750) and the 151-row sample-space case into 38/38/38/37."""
     monkeypatch.setenv("SCS_GRAM_TALL", tall)
-    world = 2
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for method in ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample"):
         full = _run(method)
-        r0, r1 = out[0][method], out[1][method]
-        assert r0["epochs"] == r1["epochs"] == full["epochs"]
-        assert r0["obj"] == r1["obj"]                       # identical bits on both ranks
-        assert np.array_equal(r0["x"], r1["x"])
+        r0 = out[0][method]
+        for r in range(1, world):
+            rr = out[r][method]
+            assert rr["epochs"] == r0["epochs"] == full["epochs"]
+            assert rr["obj"] == r0["obj"]                   # identical bits on every rank
+            assert np.array_equal(rr["x"], r0["x"])
         np.testing.assert_allclose(r0["obj"], full["obj"], rtol=1e-10)
         np.testing.assert_allclose(r0["x"], full["x"], rtol=1e-8, atol=1e-12)
