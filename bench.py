@@ -213,8 +213,13 @@ def main():
             per_launch = 0.5 * (csr + csc)
             avg_ms = tm["gemv_ms"] / tm["gemv_calls"]
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "r01_c5_spmv_pmc.json")   # tools/pmc_summary_spmv.py
+            if os.path.exists(pmc) and world == 1 and not args.f32 and N == 1 << 20 and m == 1 << 16:
+                with open(pmc) as f:
+                    traffic = json.load(f).get("hbm_bytes_per_launch")
             line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "spmv_blk_kernel",
+                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "spmv_blk_kernel",
                                 "avg_ms": avg_ms, "launches_per_step": tm["gemv_calls"] / steps,
                                 "bytes_per_launch": per_launch}
             line["config"]["nnz"] = nnz
