@@ -188,7 +188,11 @@ def main():
             gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])   # launches are timed under "solve"
             gram_flops = float(N_local) * m * (m + 1)   # algorithmic symmetric Gram per launch
             achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
-            traffic, kname = None, ("gram_sia_kernel<1, 4>" if m >= 12288 and (m // 128) % 2 == 0 else "gram_sia_kernel<1, 2>")
+            tall = m >= 12288 and (m // 128) % 2 == 0   # 256 x 128 tiles, Aᵀv fused (gram.hip gram_fuse_ok)
+            fuse = tall and os.environ.get("SCS_GRAM_FUSE", "1") != "0" and not args.gram_cache
+            traffic = None
+            kname = ("gram_sia_kernel<1, 4, false, true>" if fuse else "gram_sia_kernel<1, 4>") if tall \
+                else "gram_sia_kernel<1, 2>"
             pmc = os.path.join(ROOT, "profiles", "r01_gram_pmc.json")   # tools/gpu_prof_c3.sh + tools/pmc_summary.py
             if os.path.exists(pmc) and world == 1:
                 with open(pmc) as f:

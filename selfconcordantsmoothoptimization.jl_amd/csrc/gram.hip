@@ -32,6 +32,7 @@
 // not depend on placement).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -514,11 +515,20 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 // gram_f64_kernel / gram_glds_kernel of the same tile height.
 // CM: column-major operands (the Cholesky's trailing updates, gen form with A1 == A2),
 // S = leading dimension; stage k of feature f is the 16 samples at f * S + k0 + 16 k.
-template <int PIPE, int TI = 2, bool CM = false>
+// AV: the same pass also forms Aᵀv (the Jᵀr / ∇f product of the step, SURVEY §8d "one fused
+// Gram + Aᵀv pass"): the tile whose row block holds its column panel (bi = bj GT / GTI, one
+// per panel in both tile lists) accumulates its raw A2 registers times v while staging them,
+// so Aᵀv costs no HBM pass of its own.  Per thread a running fma over its samples in stage
+// order, then a fixed 8-lane butterfly; piece p of a K-split tile writes row p of VP (row
+// stride vps, features of panel bj), summed in piece order by gram_vfinal_kernel.  G is
+// unchanged bit for bit (the MFMA stream is the same).
+template <int PIPE, int TI = 2, bool CM = false, bool AV = false>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     const double* __restrict__ A, int64_t S, const double* __restrict__ w, int64_t k0, int64_t Nk,
     const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int flags,
-    const int4* __restrict__ work, int seglen, int nsplit, double* __restrict__ P) {
+    const int4* __restrict__ work, int seglen, int nsplit, double* __restrict__ P,
+    const double* __restrict__ v, double* __restrict__ VP, int64_t vps) {
+  static_assert(!(AV && CM), "the fused Aᵀv runs on the panel-blocked A only");
   constexpr int GTI = 64 * TI;        // tile rows (A1 features)
   constexpr int NT = 128 * TI;        // threads
   constexpr int FS = NT / 8;          // features per staging sweep
@@ -532,7 +542,7 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   __shared__ __attribute__((aligned(16))) double lds[(GTI + GT) * GBK];
   const int orig = blockIdx.x;
   const int xcd = orig % 8;
-  int bi, bj, tix, part = -1;
+  int bi, bj, tix, part = -1, piece = 0;
   if (work) {
     const int4 it = work[xcd * seglen + orig / 8];
     if (it.x < 0) return;
@@ -540,6 +550,7 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     bj = it.y;
     tix = it.w;
     if (it.z >= 0) {
+      piece = it.z;
       const int64_t L = ((Nk - k0 + (int64_t)nsplit * GBK - 1) / ((int64_t)nsplit * GBK)) * GBK;
       part = it.w;
       k0 = k0 + it.z * L;
@@ -564,6 +575,7 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   const double* srcB = CM ? A + ((int64_t)bj * GT + sf0) * S + k0 + 2 * sc
                           : A + ((int64_t)bj * S + st0) * GT * GBK + sf0 * GBK + 2 * sc;
   const double* srcW = w + k0 + 2 * sc;
+  const double* srcV = AV ? v + k0 + 2 * sc : nullptr;
   double* la = lds;
   double* lb = lds + GTI * GBK;
   int woff[NA];
@@ -572,8 +584,14 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     const int f = sf0 + FS * i;
     woff[i] = f * GBK + 2 * (sc ^ swz(f));
   }
-  v2d ra[NA], rb[NB], rw;
-  auto gload = [&](int64_t st) {
+  v2d ra[NA], rb[NB], rw, rv;
+  double av[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) av[i] = 0.0;
+  // fa: std::bool_constant -- the designated tiles of an AV launch run the loop with the Aᵀv
+  // products (FA), every other tile the plain loop (no extra loads or VALU)
+  auto gload = [&](int64_t st, auto fa) {
+    constexpr bool FA = decltype(fa)::value;
     if (PIPE == 3 && st >= 2) return;   // timing build: no global loads after the prologue
     if (CM) {
 #pragma unroll
@@ -591,12 +609,18 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
       for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + so + FS * GBK * i);
     }
     rw = *(const v2d*)(srcW + st * GBK);
+    if (FA) rv = *(const v2d*)(srcV + st * GBK);
   };
-  auto swrite = [&]() {
+  auto swrite = [&](auto fa) {
+    constexpr bool FA = decltype(fa)::value;
 #pragma unroll
     for (int i = 0; i < NA; ++i) *(v2d*)(la + woff[i]) = ra[i];
 #pragma unroll
     for (int i = 0; i < NB; ++i) *(v2d*)(lb + woff[i]) = rb[i] * rw;
+    if (FA) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) av[i] = __builtin_fma(rb[i][1], rv[1], __builtin_fma(rb[i][0], rv[0], av[i]));
+    }
   };
   const int fl = lane & 15, g = lane >> 4, s = swz(fl);
   struct Frag {
@@ -631,62 +655,82 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   };
   const int nk = (int)((Nk - k0) / GBK);
   Frag F0, F1;
-  if (nk > 0) {
-    gload(0);
-    swrite();
-    if (nk > 1) gload(1);
-    barrier();
-    fread(0, F0);
-  }
-  auto body = [&](int k, bool has1, bool has2) {
-    // phase 1
-    __builtin_amdgcn_sched_barrier(0);
-    fread(1, F1);
-    mm(F0, 0, NMM);
-    if (PIPE) {
-#pragma unroll
-      for (int i = 0; i < NRD; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, NMM / NRD, 0);   // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           // DS read
-      }
-    }
-    barrier();
-    // phase 2a
-    if (has1) swrite();
-    if (has2) gload(k + 2);
-    mm(F1, 0, NMM - TAIL);
-    if (PIPE) {
-      if (has1) {
-#pragma unroll
-        for (int i = 0; i < NA + NB; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, (NMM - TAIL) / (NA + NB), 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                         // DS write
-          if (has2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);               // VMEM read
-        }
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, NMM, 0);
-    }
-    // phase 2b
-    if (has1) {
+  auto run = [&](auto fa) {
+    if (nk > 0) {
+      gload(0, fa);
+      swrite(fa);
+      if (nk > 1) gload(1, fa);
       barrier();
       fread(0, F0);
     }
-    mm(F1, NMM - TAIL, NMM);
-    if (PIPE && has1) {
+    auto body = [&](int k, bool has1, bool has2) {
+      // phase 1
+      __builtin_amdgcn_sched_barrier(0);
+      fread(1, F1);
+      mm(F0, 0, NMM);
+      if (PIPE) {
 #pragma unroll
-      for (int i = 0; i < NRD; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, TAIL / NRD > 0 ? TAIL / NRD : 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int i = 0; i < NRD; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, NMM / NRD, 0);   // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           // DS read
+        }
       }
+      barrier();
+      // phase 2a
+      if (has1) swrite(fa);
+      if (has2) gload(k + 2, fa);
+      mm(F1, 0, NMM - TAIL);
+      if (PIPE) {
+        if (has1) {
+#pragma unroll
+          for (int i = 0; i < NA + NB; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, (NMM - TAIL) / (NA + NB), 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                         // DS write
+            if (has2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);               // VMEM read
+          }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NMM, 0);
+      }
+      // phase 2b
+      if (has1) {
+        barrier();
+        fread(0, F0);
+      }
+      mm(F1, NMM - TAIL, NMM);
+      if (PIPE && has1) {
+#pragma unroll
+        for (int i = 0; i < NRD; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, TAIL / NRD > 0 ? TAIL / NRD : 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+    };
+    int k = 0;
+    for (; k + 2 < nk; ++k) body(k, true, true);
+    if (k + 1 < nk) {
+      body(k, true, false);
+      ++k;
     }
+    if (k < nk) body(k, false, false);
   };
-  int k = 0;
-  for (; k + 2 < nk; ++k) body(k, true, true);
-  if (k + 1 < nk) {
-    body(k, true, false);
-    ++k;
+  const bool dav = AV && (int64_t)bj * GT / GTI == bi;   // this tile owns panel bj's Aᵀv rows
+  if constexpr (AV) {
+    if (dav) run(std::true_type{});
+    else run(std::false_type{});
+  } else {
+    run(std::false_type{});
   }
-  if (k < nk) body(k, false, false);
+
+  if (dav) {   // lanes 8q .. 8q+7 share a feature
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      double t = av[i];
+      t += __shfl_xor(t, 1);
+      t += __shfl_xor(t, 2);
+      t += __shfl_xor(t, 4);
+      if (sc == 0) VP[(int64_t)piece * vps + (int64_t)bj * GT + sf0 + FS * i] = t;
+    }
+  }
 
   // epilogue (the C/D map of gram_f64_kernel): element (il, jl) of the GTI x 128 tile
 #pragma unroll
@@ -728,19 +772,55 @@ int gram_tall_mode() {
   return v;
 }
 
+// The fused Aᵀv (AV kernels) rides on the default interleaved kernels.  Default: the 256 x 128
+// kernel only (C3: the separate 24 ms pass goes, the Gram grows by ~7 ms); on 128 x 128 tiles the
+// designated tiles' longer loop costs more than the pass (C2: 111.0 vs 110.4 ms per step), so
+// SCS_GRAM_FUSE=2 enables it there too, 0 turns it off (read per call; the tests' references).
+int gram_fuse_ok(int tall) {
+  const char* e = getenv("SCS_GRAM_FUSE");
+  const int mode = e ? atoi(e) : 1;
+  if (mode == 0 || (!tall && mode < 2)) return 0;
+  return tall ? gram_tall_mode() == 3 : gram_sia_mode() == 1;
+}
+
+__global__ void gram_vfinal_kernel(const double* __restrict__ VP, int npiece, int64_t vps, int64_t m,
+                                   double* __restrict__ out) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m) return;
+  double s = VP[f];
+  for (int p = 1; p < npiece; ++p) s += VP[(int64_t)p * vps + f];
+  out[f] = s;
+}
+
+hipError_t gram_vfinal_launch(const double* VP, int npiece, int64_t vps, int64_t m, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(gram_vfinal_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, VP, npiece, vps, m, out);
+  return hipGetLastError();
+}
+
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,
-                       int ntiles, double* G, int64_t ldg, int packed, int tall, hipStream_t st) {
+                       int ntiles, double* G, int64_t ldg, int packed, int tall, hipStream_t st, const double* v,
+                       double* VP, int64_t vps) {
   if (ntiles <= 0) return hipSuccess;
   const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
+  if (v) {
+    if (!gram_fuse_ok(tall)) return hipErrorInvalidValue;
+    if (tall)
+      hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0,
+                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps);
+    else
+      hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0,
+                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps);
+    return hipGetLastError();
+  }
   if (!tall && gram_sia_mode() == 0)
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (!tall)
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
   else if (gram_tall_mode() == 3)
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
   else
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -853,7 +933,7 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
   }
   if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)   // the Cholesky's trailing updates
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -866,13 +946,13 @@ hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
   if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
     hipLaunchKernelGGL((noload == 16 ? gram_sia_kernel<1, 4> : gram_sia_kernel<3, 4>), dim3(ntiles), dim3(512), 0,
-                       st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+                       st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
   else if (noload == 12)
     hipLaunchKernelGGL((gram_sia_kernel<3>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
   else if (noload == 9 || noload == 10)
     hipLaunchKernelGGL((noload == 9 ? gram_sia_kernel<1> : gram_sia_kernel<0>), dim3(ntiles), dim3(256), 0, st, A,
-                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
   else if (noload == 11)
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, A,
                        (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -923,12 +1003,19 @@ __global__ void gram_combine_kernel(const double* __restrict__ P, const int4* __
 // Scheduled main Gram (gram_schedule's work list + tail combine).
 hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
-                             int tall, hipStream_t st) {
+                             int tall, hipStream_t st, const double* v, double* VP, int64_t vps) {
   const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
   const int glds = gram_tall_mode();
-  if (tall && glds == 3)
+  if (v && !gram_fuse_ok(tall)) return hipErrorInvalidValue;
+  if (v && tall)
+    hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w,
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps);
+  else if (v)
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w,
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps);
+  else if (tall && glds == 3)
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk,
-                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
   else if (tall && glds == 2)
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
                        Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
@@ -940,10 +1027,10 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   else if (gram_sia_mode() == 1)
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr,
-                       0, G, ldg, flags, work, seglen, nsplit, P);
+                       0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
   else if (gram_sia_mode() == 2)
     hipLaunchKernelGGL((gram_sia_kernel<0>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr, 0,
-                       G, ldg, flags, work, seglen, nsplit, P);
+                       G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);

@@ -28,8 +28,14 @@ void gram_tile_list_tall(int nb, int2* out, int* ntiles);
 // Main Gram on the panel-blocked A (lda = S = Npad / 16).  tall = 1: 256 x 128 tiles from
 // gram_tile_list_tall (nb even); packed slots are then the 128 x 128 halves (2t, 2t+1) of
 // launch tile t.  gram_launch_gen operates on column-major operands (the Cholesky updates).
+// v != nullptr: the same launch also forms Aᵀv (fused, gram_fuse_ok kernels only) into VP: one row
+// (stride vps >= mpad) per K piece (nsplit rows for the scheduled launch, zeroed beforehand when
+// nsplit > 1), reduced by gram_vfinal_launch.
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
-                       double* G, int64_t ldg, int packed, int tall, hipStream_t st);
+                       double* G, int64_t ldg, int packed, int tall, hipStream_t st, const double* v = nullptr,
+                       double* VP = nullptr, int64_t vps = 0);
+int gram_fuse_ok(int tall);
+hipError_t gram_vfinal_launch(const double* VP, int npiece, int64_t vps, int64_t m, double* out, hipStream_t st);
 void gram_tile_list_rowmajor(int nb, int2* out);
 hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
@@ -40,7 +46,8 @@ int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<
                   int* nsplit, int* npart);
 hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
-                             int tall, hipStream_t st);
+                             int tall, hipStream_t st, const double* v = nullptr, double* VP = nullptr,
+                             int64_t vps = 0);
 hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,
                               hipStream_t st);
 

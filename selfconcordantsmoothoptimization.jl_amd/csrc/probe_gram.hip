@@ -12,7 +12,8 @@ namespace scs {
 void gram_tile_list(int nb, int2* out, int* ntiles);
 void gram_tile_list_tall(int nb, int2* out, int* ntiles);
 hipError_t gram_launch(const double* A, int64_t S, const double* w, int64_t Nk, const int2* tiles, int ntiles,
-                       double* G, int64_t ldg, int packed, int tall, hipStream_t st);
+                       double* G, int64_t ldg, int packed, int tall, hipStream_t st, const double* v = nullptr,
+                       double* VP = nullptr, int64_t vps = 0);
 hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t k0, int64_t k1, const int2* tiles,
                           int ntiles, double* G, int64_t ldg, int accumulate, int noload, hipStream_t st);
 }

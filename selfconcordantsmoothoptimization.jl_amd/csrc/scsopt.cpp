@@ -161,6 +161,7 @@ struct scs_ctx {
   int4* gcomb = nullptr;
   int gseglen = 0, gncomb = 0, gnsplit = 1;
   double* gpart = nullptr;
+  double* vpart = nullptr;   // fused Aᵀv partials: max(gnsplit, 1) rows of mpad
   double* W = nullptr;      // inverted diagonal blocks of the Cholesky factor [mpad/128][128*128]
   double* ysol = nullptr;   // triangular-solve scratch (mpad)
   int2* trilist = nullptr;  // row-major lower tiles
@@ -467,6 +468,7 @@ void ensure_gram(scs_ctx* c) {
       }
     }
   }
+  c->vpart = dalloc<double>(c, (size_t)std::max(c->gnsplit, 1) * mp);
   c->utiles = dalloc<int2>(c, ul.size());
   HCK(hipMemcpyAsync(c->utiles, ul.data(), sizeof(int2) * ul.size(), hipMemcpyHostToDevice, c->st));
   {
@@ -857,13 +859,19 @@ const double* dense_A(scs_ctx* c) {
   return c->Ad;
 }
 
-void gram_main(scs_ctx* c, const double* w, double* out, int packed) {
+// v != nullptr: the same launch forms Aᵀv of the local rows into vout (fused, gram_fuse_ok)
+void gram_main(scs_ctx* c, const double* w, double* out, int packed, const double* v = nullptr,
+               double* vout = nullptr) {
   const double* A = dense_A(c);
+  const int npiece = (v && c->gwork) ? std::max(c->gnsplit, 1) : 1;
+  if (v && npiece > 1) HCK(hipMemsetAsync(c->vpart, 0, sizeof(double) * npiece * c->mpad, c->st));
   if (c->gwork)
     HCK(gram_launch_sched(A, c->nstage, w, c->Npad, c->gwork, c->gseglen, c->gnsplit, c->gcomb, c->gncomb, c->gpart,
-                          out, c->mpad, packed, c->tall, c->st));
+                          out, c->mpad, packed, c->tall, c->st, v, c->vpart, c->mpad));
   else
-    HCK(gram_launch(A, c->nstage, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st));
+    HCK(gram_launch(A, c->nstage, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st, v, c->vpart,
+                    c->mpad));
+  if (v) HCK(gram_vfinal_launch(c->vpart, npiece, c->mpad, c->m, vout, c->st));
 }
 
 // Gram of the local rows with weights w -> c->G (single rank) or the packed
@@ -876,11 +884,16 @@ bool gram_x_independent(const scs_ctx* c) {
   return c->method == SCS_PROX_NSCORE || (c->method == SCS_PROX_GGNSCORE && c->ggn == SCS_GGN_LINEAR_LS);
 }
 
-void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
+// vec_dev = Aᵀv of the local rows (then reduced with the Gram): formed inside the Gram launch
+// (gram_sia_kernel AV) unless the Gram is served from the cache (a cached run never fuses, so
+// its steps all take the same separate Aᵀv pass) or SCS_GRAM_FUSE=0
+void gram_and_reduce(scs_ctx* c, const double* w, const double* v, double* vec_dev) {
   ensure_gram(c);
   hipEvent_t e0;
   const bool cacheable = c->gram_cache && gram_x_independent(c);
   const size_t gbytes = sizeof(double) * (size_t)c->mpad * c->mpad;
+  const bool fuse = !cacheable && gram_fuse_ok(c->tall);
+  if (!fuse) gemv_t_local(c, v, vec_dev);
   if (cacheable && c->Gk && c->gk_gen == c->data_gen) {   // the reduced Gram of an earlier step
     c->g_from_cache = true;
     HCK(hipMemcpyAsync(c->G, c->Gk, gbytes, hipMemcpyDeviceToDevice, c->st));
@@ -894,7 +907,7 @@ void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
   if (c->nranks > 1) {
     const int64_t tsz = (int64_t)c->nslots * 128 * 128;
     tbegin(c, T_GRAM, &e0);
-    gram_main(c, w, c->red, 1);
+    gram_main(c, w, c->red, 1, fuse ? v : nullptr, vec_dev);
     tend(c, T_GRAM, e0);
     HCK(hipMemcpyAsync(c->red + tsz, vec_dev, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
     allreduce(c, c->red, tsz + c->m);
@@ -902,7 +915,7 @@ void gram_and_reduce(scs_ctx* c, const double* w, double* vec_dev) {
     HCK(hipMemcpyAsync(vec_dev, c->red + tsz, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
   } else {
     tbegin(c, T_GRAM, &e0);
-    gram_main(c, w, c->G, 0);
+    gram_main(c, w, c->G, 0, fuse ? v : nullptr, vec_dev);
     tend(c, T_GRAM, e0);
   }
   if (cacheable) {
@@ -1064,16 +1077,14 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
       grad_f_dev(c, xh, c->x, c->gtmp);
     } else {
       forward(c, xh, c->x, EPI_GRAD | EPI_HESS);
-      // local Aᵀg (not yet reduced); reduced together with the Gram
-      gemv_t_local(c, c->gN, c->gtmp);
-      gram_and_reduce(c, c->hN, c->gtmp);
+      // local Aᵀg (not yet reduced; fused into the Gram pass); reduced together with the Gram
+      gram_and_reduce(c, c->hN, c->gN, c->gtmp);
     }
   } else {
     if (c->ggn == SCS_GGN_NONE) fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs an out_fn / GGN loss kind");
     // J, residual, Q (prox-GGN-SCORE.jl:44-56) -> w = s²q, v = s·r
     forward(c, xh, c->x, EPI_GGN);
-    gemv_t_local(c, c->vN, c->gtmp);
-    gram_and_reduce(c, c->wN, c->gtmp);
+    gram_and_reduce(c, c->wN, c->vN, c->gtmp);   // Gram + Jᵀr in one pass over A
   }
   // rhs = ∇f + λ gr (NSCORE) | Jᵀr + λ gr (GGN: Jt*[r;1], prox-GGN-SCORE.jl:121-130)
   HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
@@ -1293,6 +1304,7 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->gwork);
   dfree_t(c, c->gcomb);
   dfree_t(c, c->gpart);
+  dfree_t(c, c->vpart);
   c->gseglen = c->gncomb = 0;
   c->gnsplit = 1;
   dfree_t(c, c->W);

@@ -335,10 +335,12 @@ def test_group_lasso_general_groups(smoother):
 
 
 @pytest.mark.parametrize("case", ["nscore_ls", "ggn_ls_gl", "ggn_ls_batches"])
-def test_gram_cache_bit_identical(case):
+def test_gram_cache_bit_identical(case, monkeypatch):
     """scs_set_gram_cache: AᵀQA of least squares is x-independent, so reusing it changes nothing --
     identical histories and x bits vs the reference's recompute-every-step; minibatches (a different
-    A per step) must not reuse another batch's Gram."""
+    A per step) must not reuse another batch's Gram.  A cached run forms Aᵀv in its own pass, so the
+    recompute reference runs with the Gram-fused Aᵀv off (SCS_GRAM_FUSE=0, read per call)."""
+    monkeypatch.setenv("SCS_GRAM_FUSE", "0")
     N, m, gs = 2048, 128, 16
     x0 = np.random.default_rng(9).standard_normal(m)
     out = None if case == "nscore_ls" else losses.linear_ls(1.0 / N)
@@ -577,3 +579,35 @@ def test_interleaved_gram_bitwise_vs_previous_kernels(tmp_path):
     for k in ("1", "0"):
         lo = np.tril_indices(outs["new"][k].shape[0])
         assert np.array_equal(bits(outs["new"][k][lo]), bits(outs["old"][k][lo])), k
+
+
+@pytest.mark.parametrize("method,m,tall", [("ggn", 192, "0"), ("nscore", 192, "0"), ("ggn", 256, "1"),
+                                           ("nscore", 512, "1")])
+def test_fused_gram_atv_matches_separate_pass(method, m, tall, monkeypatch):
+    """The Gram launch's fused Aᵀv (gram_sia_kernel AV: Jᵀr for GGN, ∇f for NSCORE) == the separate
+    gemv_t pass to rounding, over 128 x 128 and 256 x 128 tiles with K-split tail pieces (the tail
+    schedule splits at these sizes), and both stay on the oracle's trajectory."""
+    monkeypatch.setenv("SCS_GRAM_TALL", tall)
+    monkeypatch.setenv("SCS_GRAM_FUSE", "2")   # fused on 128 x 128 tiles too (default: 256 x 128 only)
+    N = 3001
+    x0 = np.random.default_rng(21).standard_normal(m) * 0.5
+    if method == "ggn":
+        f, out, kind, of = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N), 1, \
+            O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+        M, OM = scsopt.ProxGGNSCORE, O.ProxGGNSCORE
+    else:
+        f, out, kind, of = losses.logistic_margin(1.0 / N), None, 2, O.Loss("logistic_margin", 1.0 / N)
+        M, OM = scsopt.ProxNSCORE, O.ProxNSCORE
+    p = scsopt.Problem.synthetic(N, m, x0, f, 2e-3, kind=kind, seed=17, out_fn=out)
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    fused = scsopt.iterate(M(), p, "l1", hm, max_epoch=6, verbose=0)
+    monkeypatch.setenv("SCS_GRAM_FUSE", "0")
+    sep = scsopt.iterate(M(), p, "l1", hm, max_epoch=6, verbose=0)
+    assert fused.epochs == sep.epochs
+    np.testing.assert_allclose(fused.obj, sep.obj, rtol=1e-12)
+    np.testing.assert_allclose(fused.x, sep.x, rtol=1e-9, atol=1e-13)
+    A, y = p.get_data()
+    osol = O.iterate(OM(), O.Problem(A, y, x0, of, 2e-3), "l1", O.PHuberSmootherL1L2(1.0), max_epoch=6)
+    assert fused.epochs == osol.epochs
+    np.testing.assert_allclose(fused.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(fused.x, osol.x, rtol=1e-6, atol=1e-9)
