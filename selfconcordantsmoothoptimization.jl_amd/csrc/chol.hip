@@ -320,28 +320,48 @@ __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, i
 // Moving the bulk of the m³/3 flops into C with K = 1024 instead of 128 cuts the
 // read-modify-write of the trailing matrix 8x (the single-level update is HBM-bound on
 // that C tile traffic: 2·128 KiB per 4.2 MFLOP tile).
+static int outer_block();
+
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
+  const int OB = outer_block();
   a->nblk = nblk;
   std::vector<double> hw((size_t)CB + mpad, -1.0);
   for (int i = 0; i < CB; ++i) hw[i] = 1.0;
-  std::vector<int2> rl;
+  std::vector<int2> rl, sl;
   for (int R = 1; R <= 4; ++R)
     for (int j = 0; j < nblk; ++j)
       for (int i = 0; i < R; ++i) rl.push_back(make_int2(i, j));   // bj-major: first R*C = R x C rectangle
+  // pairs (i >= j) with j < OB, row-major: the first sum_{i<n} min(i+1, OB) entries cover the
+  // first OB block columns of an n x n lower triangle
+  for (int i = 0; i < nblk; ++i)
+    for (int j = 0; j <= i && j < OB; ++j) sl.push_back(make_int2(i, j));
   hipError_t e = hipMalloc(&a->w, sizeof(double) * hw.size());
   if (e == hipSuccess) e = hipMalloc(&a->rect, sizeof(int2) * rl.size());
+  if (e == hipSuccess) e = hipMalloc(&a->strip, sizeof(int2) * sl.size());
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(a->strip, sl.data(), sizeof(int2) * sl.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&a->st2, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev1, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev2, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   return e;
 }
 
 void chol_aux_free(CholAux* a) {
+  if (a->st2) (void)hipStreamSynchronize(a->st2);
   if (a->w) (void)hipFree(a->w);
   if (a->rect) (void)hipFree(a->rect);
+  if (a->strip) (void)hipFree(a->strip);
+  if (a->ev1) (void)hipEventDestroy(a->ev1);
+  if (a->ev2) (void)hipEventDestroy(a->ev2);
+  if (a->st2) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
+  a->strip = nullptr;
+  a->ev1 = a->ev2 = nullptr;
+  a->st2 = nullptr;
 }
 
 static const int2* rect_list(const CholAux* a, int R) { return a->rect + (int64_t)a->nblk * (R - 1) * R / 2; }
@@ -377,10 +397,24 @@ static hipError_t strip_solve(double* G, int64_t ld, const double* W, const Chol
   return strip_solve(G, ld, W, a, mid, hi, c0, nc, st);
 }
 
+// Lookahead (default; SCS_CHOL_LA=0 off): the trailing update C of outer block t is cut into
+//   C1 = the next outer block's strip (block pairs whose smaller index is in block t+1), on st;
+//   C2 = everything right of / below that strip, on st2,
+// so block t+1's serial diagonal steps (A, 128 chol_diag_kernel launches of one workgroup
+// each over the whole factor) and strip solve (B) run while C2_t fills the machine.
+// Every element still receives its updates in block order (C1_{t+1} waits for C2_t, which
+// also covers strip t+2's rows), so U is bit-identical to the serial order.
+static bool chol_lookahead() {
+  const char* e = getenv("SCS_CHOL_LA");
+  return !(e && e[0] == '0');
+}
+
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* a,
                        const int2* trilist, int* info, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
   const int OB = outer_block();
+  const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
+  bool c2_pending = false;
   if (mpad > m) hipLaunchKernelGGL(diag_pad_kernel, dim3((unsigned)ceil_div(mpad - m, 256)), dim3(256), 0, st, G, ld,
                                    m, mpad);
   for (int i0 = 0; i0 < nblk; i0 += OB) {
@@ -406,8 +440,42 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (e != hipSuccess) return e;
     const double* X = G + (int64_t)i1 * CB * ld;
     double* trail = G + (int64_t)i1 * CB * ld + (int64_t)i1 * CB;
-    e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, nc * (nc + 1) / 2, trail,
-                        ld, 2 | 4, st);
+    const int nc2 = nc - OB;   // block pairs both beyond the next outer block
+    if (!la || nc2 <= 0) {
+      if (c2_pending) {
+        e = hipStreamWaitEvent(st, a->ev2, 0);
+        if (e != hipSuccess) return e;
+        c2_pending = false;
+      }
+      e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, nc * (nc + 1) / 2,
+                          trail, ld, 2 | 4, st);
+      if (e != hipSuccess) return e;
+      continue;
+    }
+    // C1: the next block's strip, after C2 of the previous block (same elements, block order)
+    if (c2_pending) {
+      e = hipStreamWaitEvent(st, a->ev2, 0);
+      if (e != hipSuccess) return e;
+    }
+    const int n1 = (OB * (OB + 1)) / 2 + (nc - OB) * OB;   // sum_{i<nc} min(i+1, OB)
+    e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, a->strip, n1, trail, ld, 2 | 4, st);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(a->ev1, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(a->st2, a->ev1, 0);
+    if (e != hipSuccess) return e;
+    // C2 on st2, overlapping the next block's A and B on st
+    const int i2 = i1 + OB;
+    const double* X2 = G + (int64_t)i2 * CB * ld;
+    double* trail2 = G + (int64_t)i2 * CB * ld + (int64_t)i2 * CB;
+    e = gram_launch_gen(X2, ld, X2, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, nc2 * (nc2 + 1) / 2,
+                        trail2, ld, 2 | 4, a->st2);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(a->ev2, a->st2);
+    if (e != hipSuccess) return e;
+    c2_pending = true;
+  }
+  if (c2_pending) {
+    hipError_t e = hipStreamWaitEvent(st, a->ev2, 0);
     if (e != hipSuccess) return e;
   }
   return hipGetLastError();

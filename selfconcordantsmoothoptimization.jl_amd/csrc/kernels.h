@@ -55,6 +55,9 @@ hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, do
 struct CholAux {             // device constants of the two-level factorization (chol_aux_init)
   double* w = nullptr;       // [128 x +1.0 | mpad x -1.0] Gram weights (panel solve | block updates)
   int2* rect = nullptr;      // R x nblk rectangle tile lists, R = 1..4 (bj-major)
+  int2* strip = nullptr;     // lookahead: the next outer block's strip of a trailing update
+  hipStream_t st2 = nullptr; // lookahead: the rest of each trailing update runs here
+  hipEvent_t ev1 = nullptr, ev2 = nullptr;
   int nblk = 0;
 };
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);

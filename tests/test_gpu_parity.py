@@ -611,3 +611,20 @@ def test_fused_gram_atv_matches_separate_pass(method, m, tall, monkeypatch):
     assert fused.epochs == osol.epochs
     np.testing.assert_allclose(fused.obj, osol.obj, rtol=1e-8, atol=0)
     np.testing.assert_allclose(fused.x, osol.x, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("m", [2304, 3200])
+def test_cholesky_lookahead_bit_identical(m, monkeypatch):
+    """The factor's lookahead (next outer block's diagonal steps overlapping the rest of the trailing
+    update on a second stream) keeps every element's update order, so the ProxNSCORE trajectory is
+    bit-identical to the serial order (SCS_CHOL_LA=0); m = 2304 / 3200: 18 / 25 inner blocks, i.e.
+    2-3 outer blocks with a lookahead split and a short last block."""
+    N = 4000
+    x0 = np.random.default_rng(31).standard_normal(m) * 0.3
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=23)
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    la = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=4, verbose=0)
+    monkeypatch.setenv("SCS_CHOL_LA", "0")
+    ser = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=4, verbose=0)
+    assert la.obj == ser.obj and la.pri_res_norm == ser.pri_res_norm and la.epochs == ser.epochs
+    assert np.array_equal(bits(la.x), bits(ser.x))
