@@ -152,8 +152,9 @@ def main():
     steps, warmup = args.steps, args.warmup
     if cfg["loss"] == "rosenbrock" and steps < 50:
         steps = 50                               # microsecond-scale steps: time a meaningful batch
-    if cfg.get("sparse") and steps < 20:
-        steps = 20                               # millisecond-scale steps: amortize iterate!'s f(x*) once
+    if cfg.get("sparse"):
+        steps = max(steps, 50)                   # millisecond-scale steps: amortize iterate!'s f(x*) once
+        warmup = max(warmup, 5)                  # and let the clocks settle (1 warm-up step: +-5 % box to box)
     ctx.check(scsopt._lib.lib.scs_timing_enable(ctx.h, 1))
     if warmup > 0:
         run_iterate(warmup)
