@@ -1877,34 +1877,45 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     if (max_epoch < 1) fail(c, SCS_ERR_ARG, "scs_iterate: max_epoch must be >= 1");
     HCK(hipSetDevice(c->dev));
     const int64_t m = c->m;
-    auto nrm = [&](const double* a, const double* b) {   // ‖a − b‖ (b may be null)
-      double s2 = 0.0;
-      for (int64_t i = 0; i < m; ++i) {
-        const double d = b ? a[i] - b[i] : a[i];
-        s2 += d * d;
+    // Σ (a − b)² (b may be null) in a fixed order: eight interleaved partial sums (vectorized;
+    // the one-accumulator loop was ~90 us per call at m = 65536, three calls per epoch, on the
+    // C5 step's critical path), then a fixed tree and the tail.  Julia's norm is BLAS nrm2, a
+    // different order again; termination compares at x_tol, not ulps.
+    auto sumsq = [&](const double* a, const double* b) {
+      double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      int64_t i = 0;
+      if (b) {
+        for (; i + 8 <= m; i += 8)
+          for (int l = 0; l < 8; ++l) {
+            const double d = a[i + l] - b[i + l];
+            acc[l] += d * d;
+          }
+      } else {
+        for (; i + 8 <= m; i += 8)
+          for (int l = 0; l < 8; ++l) acc[l] += a[i + l] * a[i + l];
       }
-      return std::sqrt(s2);
+      double t = 0.0;
+      for (; i < m; ++i) {
+        const double d = b ? a[i] - b[i] : a[i];
+        t += d * d;
+      }
+      return (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]))) + t;
     };
+    auto nrm = [&](const double* a, const double* b) { return std::sqrt(sumsq(a, b)); };   // ‖a − b‖
     auto jmax = [](double a, double b) {   // Julia max: NaN propagates, -0.0 < +0.0
       if (std::isnan(a)) return a;
       if (std::isnan(b)) return b;
       return (b < a || (std::signbit(b) && !std::signbit(a))) ? a : b;
     };
-    auto f_of = [&](const double* xx) {
+    // f(x) + get_reg(x) with one upload of x (c->xn holds it for both)
+    auto fobj_of = [&](const double* xx, double* fv) {
       h2d(c, c->xn, xx, m);
-      return eval_f_dev(c, xx, c->xn);
-    };
-    auto reg_of = [&](const double* xx) {
-      h2d(c, c->xn, xx, m);
-      return eval_reg_dev(c, c->xn);
+      *fv = eval_f_dev(c, xx, c->xn);
+      return *fv + eval_reg_dev(c, c->xn);
     };
     const double nstar = nrm(x_star, nullptr);
     auto rel_of = [&](const double* xx) {
-      if (rel_kind == 1) {   // mean_square_error (utils.jl:3-5), the "gl" rel_error
-        double s2 = 0.0;
-        for (int64_t i = 0; i < m; ++i) s2 += (x_star[i] - xx[i]) * (x_star[i] - xx[i]);
-        return s2 / (double)m;
-      }
+      if (rel_kind == 1) return sumsq(x_star, xx) / (double)m;   // mean_square_error (utils.jl:3-5), the "gl" rel_error
       return jmax(nrm(xx, x_star) / jmax(nstar, 1.0), x_tol);
     };
     const auto t0 = std::chrono::steady_clock::now();
@@ -1912,7 +1923,8 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
       const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       return std::floor(sec * 1000.0) / 1000.0;
     };
-    const double obj_star = f_of(x_star) + reg_of(x_star);
+    double fstar = 0.0;
+    const double obj_star = fobj_of(x_star, &fstar);
     auto frel_of = [&](double ob) { return jmax(std::fabs(ob - obj_star) / std::fabs(obj_star), f_tol); };
     int64_t nh = 0;
     auto push = [&](double ob, double fv, double pr, double rl, double fr, double dt) {
@@ -1929,7 +1941,20 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     c->spare = 0;
     c->H0 = 1.0;
     invalidate_caches(c);
-    std::vector<double> x(x0, x0 + m), x_prev = x, x_new(m);
+    // x, x_prev, x_new in pinned host memory: their per-epoch uploads / the x_new download are
+    // DMA transfers instead of staged pageable copies (the arrays are only touched after syncs)
+    struct Pinned {
+      double* p = nullptr;
+      ~Pinned() {
+        if (p) (void)hipHostFree(p);
+      }
+    } pin;
+    HCK(hipHostMalloc((void**)&pin.p, sizeof(double) * 3 * std::max<int64_t>(m, 1), hipHostMallocDefault));
+    double* x = pin.p;
+    double* x_prev = pin.p + m;
+    double* x_new = pin.p + 2 * m;
+    std::memcpy(x, x0, sizeof(double) * m);
+    std::memcpy(x_prev, x0, sizeof(double) * m);
     double pri = std::numeric_limits<double>::quiet_NaN();
     int64_t epochs = 0;
     // the collected batches (iterate.jl:146): the registered list, else the one full batch
@@ -1941,17 +1966,16 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     } unselect{c};
     for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
       double dt = now();
-      double fval = f_of(x.data());
-      double obj = fval + reg_of(x.data());
-      double rel = rel_of(x.data());
+      double fval = 0.0;
+      double obj = fobj_of(x, &fval);
+      double rel = rel_of(x);
       double frel = frel_of(obj);
       push(obj, fval, pri, rel, frel, dt);
       for (int64_t i = 1; i <= iend; ++i) {   // for (i, sample) in enumerate(data) (iterate.jl:204-255)
         if (epoch == max_epoch && i == iend) {   // iterate.jl:219-231 (x as of this batch)
           dt = now();
-          fval = f_of(x.data());
-          obj = fval + reg_of(x.data());
-          rel = rel_of(x.data());
+          obj = fobj_of(x, &fval);
+          rel = rel_of(x);
           frel = frel_of(obj);
           push(obj, fval, pri, rel, frel, dt);
         }
@@ -1960,38 +1984,37 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         select_batch(c, nb > 0 ? i - 1 : -1);
         {
           BatchScope bs(c);
-          h2d(c, c->x, x.data(), m);
-          h2d(c, c->xp, x_prev.data(), m);
+          h2d(c, c->x, x, m);
+          h2d(c, c->xp, x_prev, m);
           if (c->method == SCS_PROX_LQNSCORE)
-            step_lqn(c, x.data(), x_prev.data(), epoch, x_new.data(), nullptr, &pri);
+            step_lqn(c, x, x_prev, epoch, x_new, nullptr, &pri);
           else
-            step_newton(c, x.data(), epoch, x_new.data(), nullptr, &pri);
+            step_newton(c, x, epoch, x_new, nullptr, &pri);
         }
         c->bview = -1;
         tend(c, T_STEP, e0);
-        const double nx = nrm(x.data(), nullptr);
-        const bool stop = nrm(x_new.data(), x.data()) < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol;
+        const double nx = nrm(x, nullptr);
+        const bool stop = nrm(x_new, x) < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol;
         if (stop && epoch != max_epoch) {   // iterate.jl:235-247 (f_rel_error is refreshed for the test at :257)
           dt = now();
-          fval = f_of(x_new.data());
-          obj = fval + reg_of(x_new.data());
-          rel = rel_of(x_new.data());
+          obj = fobj_of(x_new, &fval);
+          rel = rel_of(x_new);
           frel = frel_of(obj);
           push(obj, fval, pri, rel, frel, dt);
         }
-        x_prev.swap(x);
-        x = x_new;
+        std::swap(x_prev, x);
+        std::memcpy(x, x_new, sizeof(double) * m);
         if (stop) {
           ++epochs;
           break;
         }
       }
-      if (nrm(x.data(), x_prev.data()) < x_tol * std::max(nrm(x_prev.data(), nullptr), 1.0) || frel <= f_tol ||
+      if (nrm(x, x_prev) < x_tol * std::max(nrm(x_prev, nullptr), 1.0) || frel <= f_tol ||
           pri < x_tol)
         break;   // iterate.jl:257-259
       ++epochs;
     }
-    std::memcpy(x_out, x.data(), sizeof(double) * m);
+    std::memcpy(x_out, x, sizeof(double) * m);
     *n_hist = nh;
     *epochs_out = epochs;
     if (c->timing) tresolve(c);
