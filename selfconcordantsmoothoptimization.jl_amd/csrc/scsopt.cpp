@@ -195,6 +195,15 @@ struct scs_ctx {
   double zfval = 0.0;  // f(x) for zkey (global, scaled)
   std::vector<double> gkey[2];
   bool gvalid[2] = {false, false};
+  // scs_iterate's host vectors carry version tags (bumped on every write), so the f / ∇q caches
+  // compare a tag instead of m doubles and keep no copy; untagged pointers (the per-call ABI)
+  // use the content keys above.  A key's tag is 0 for a content key.
+  struct XTag {
+    const double* p = nullptr;
+    uint64_t v = 0;
+  } xtags[3];
+  uint64_t xtag_next = 1;
+  uint64_t ztag = 0, gtag[2] = {0, 0};
   int gnext = 0;
 
   // timing
@@ -346,6 +355,25 @@ double jl_min_h(double x, double y) {
 
 bool same_x(const std::vector<double>& key, const double* x, int64_t m) {
   return (int64_t)key.size() == m && std::memcmp(key.data(), x, sizeof(double) * m) == 0;
+}
+
+uint64_t xtag_of(const scs_ctx* c, const double* x) {
+  for (const auto& t : c->xtags)
+    if (t.p && t.p == x) return t.v;
+  return 0;
+}
+// cache key (content `key` or tag `ktag`) matches the host vector x
+bool key_hit(const scs_ctx* c, const std::vector<double>& key, uint64_t ktag, const double* x) {
+  const uint64_t t = xtag_of(c, x);
+  if (t) return ktag == t;
+  return ktag == 0 && same_x(key, x, c->m);
+}
+void key_set(const scs_ctx* c, std::vector<double>& key, uint64_t& ktag, const double* x) {
+  ktag = xtag_of(c, x);
+  if (ktag)
+    key.clear();
+  else
+    key.assign(x, x + c->m);
 }
 
 ProxArgsH prox_args(scs_ctx* c) {
@@ -646,7 +674,7 @@ void require_dense(scs_ctx* c, const char* what) {
 // cached z), then the epilogue with `flags`.  Always refreshes the f-value
 // cache; returns f(x) (global).
 double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
-  const bool cached = c->zvalid && same_x(c->zkey, xh, c->m);
+  const bool cached = c->zvalid && key_hit(c, c->zkey, c->ztag, xh);
   hipEvent_t e0;
   if (!cached) {
     tbegin(c, T_GEMV, &e0);
@@ -663,7 +691,7 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
     d2h(c, c->hscal + 8, c->scal + 8, 1);
     sync(c);
     c->zfval = loss_scale_value(c, c->hscal[8]);
-    c->zkey.assign(xh, xh + c->m);
+    key_set(c, c->zkey, c->ztag, xh);
     c->zvalid = true;
   } else if (flags & ~(EPI_VAL | EPI_Z)) {
     flags &= ~(EPI_Z | EPI_VAL);
@@ -736,7 +764,7 @@ void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
 // ∇q(x) = ∇f(x) + λ hμ.grad(x) -> out (device); uses the 2-slot cache.
 void grad_q_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
   for (int s = 0; s < 2; ++s)
-    if (c->gvalid[s] && same_x(c->gkey[s], xh, c->m)) {
+    if (c->gvalid[s] && key_hit(c, c->gkey[s], c->gtag[s], xh)) {
       HCK(hipMemcpyAsync(out, c->gcache[s], sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
       return;
     }
@@ -746,7 +774,7 @@ void grad_q_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
   const int s = c->gnext;
   c->gnext ^= 1;
   HCK(hipMemcpyAsync(c->gcache[s], out, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
-  c->gkey[s].assign(xh, xh + c->m);
+  key_set(c, c->gkey[s], c->gtag[s], xh);
   c->gvalid[s] = true;
 }
 
@@ -1908,8 +1936,15 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
       return (b < a || (std::signbit(b) && !std::signbit(a))) ? a : b;
     };
     // f(x) + get_reg(x) with one upload of x (c->xn holds it for both)
+    // the tagged host vector the device buffers c->x / c->xn hold (0: unknown), so a vector
+    // already on the device is not uploaded again (x = the last step's x_new = c->xn)
+    uint64_t dev_x = 0, dev_xn = 0;
     auto fobj_of = [&](const double* xx, double* fv) {
-      h2d(c, c->xn, xx, m);
+      const uint64_t t = xtag_of(c, xx);
+      if (!(t && t == dev_xn)) {
+        h2d(c, c->xn, xx, m);
+        dev_xn = t;
+      }
       *fv = eval_f_dev(c, xx, c->xn);
       return *fv + eval_reg_dev(c, c->xn);
     };
@@ -1955,6 +1990,22 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     double* x_new = pin.p + 2 * m;
     std::memcpy(x, x0, sizeof(double) * m);
     std::memcpy(x_prev, x0, sizeof(double) * m);
+    // version tags of the three buffers for the f / ∇q caches (unregistered on exit)
+    struct Untag {
+      scs_ctx* c;
+      ~Untag() {
+        for (auto& t : c->xtags) t = scs_ctx::XTag{};
+      }
+    } untag{c};
+    auto tag_slot = [&](const double* p) -> scs_ctx::XTag& {
+      for (auto& t : c->xtags)
+        if (t.p == p) return t;
+      fail(c, SCS_ERR_STATE, "scs_iterate: untracked buffer");
+      return c->xtags[0];
+    };
+    c->xtags[0] = {x, c->xtag_next};
+    c->xtags[1] = {x_prev, c->xtag_next++};   // same content as x
+    c->xtags[2] = {x_new, c->xtag_next++};
     double pri = std::numeric_limits<double>::quiet_NaN();
     int64_t epochs = 0;
     // the collected batches (iterate.jl:146): the registered list, else the one full batch
@@ -1984,12 +2035,23 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         select_batch(c, nb > 0 ? i - 1 : -1);
         {
           BatchScope bs(c);
-          h2d(c, c->x, x, m);
-          h2d(c, c->xp, x_prev, m);
+          const uint64_t tx = xtag_of(c, x), tp = xtag_of(c, x_prev);
+          const size_t vb = sizeof(double) * m;
+          if (nb == 0 && tp && tp == dev_x)   // x_prev = the previous step's x, still in c->x
+            HCK(hipMemcpyAsync(c->xp, c->x, vb, hipMemcpyDeviceToDevice, c->st));
+          else
+            h2d(c, c->xp, x_prev, m);
+          if (nb == 0 && tx && tx == dev_xn)
+            HCK(hipMemcpyAsync(c->x, c->xn, vb, hipMemcpyDeviceToDevice, c->st));
+          else
+            h2d(c, c->x, x, m);
+          dev_x = tx;
+          tag_slot(x_new).v = c->xtag_next++;   // the step writes x_new
           if (c->method == SCS_PROX_LQNSCORE)
             step_lqn(c, x, x_prev, epoch, x_new, nullptr, &pri);
           else
             step_newton(c, x, epoch, x_new, nullptr, &pri);
+          dev_xn = xtag_of(c, x_new);   // the step's tail wrote x_new to c->xn (and downloaded it)
         }
         c->bview = -1;
         tend(c, T_STEP, e0);
@@ -2004,6 +2066,7 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         }
         std::swap(x_prev, x);
         std::memcpy(x, x_new, sizeof(double) * m);
+        tag_slot(x).v = tag_slot(x_new).v;   // same content
         if (stop) {
           ++epochs;
           break;
