@@ -2015,6 +2015,7 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
       scs_ctx* c;
       ~Unselect() { c->bview = -1; }
     } unselect{c};
+    double last_nx = 0.0, last_ndx = 0.0;
     for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
       double dt = now();
       double fval = 0.0;
@@ -2056,7 +2057,10 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         c->bview = -1;
         tend(c, T_STEP, e0);
         const double nx = nrm(x, nullptr);
-        const bool stop = nrm(x_new, x) < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol;
+        const double ndx = nrm(x_new, x);
+        last_nx = nx;     // the epoch-end test (:257) reads the same pair after the swap
+        last_ndx = ndx;
+        const bool stop = ndx < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol;
         if (stop && epoch != max_epoch) {   // iterate.jl:235-247 (f_rel_error is refreshed for the test at :257)
           dt = now();
           obj = fobj_of(x_new, &fval);
@@ -2072,7 +2076,8 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
           break;
         }
       }
-      if (nrm(x, x_prev) < x_tol * std::max(nrm(x_prev, nullptr), 1.0) || frel <= f_tol ||
+      // ‖x − x_prev‖, ‖x_prev‖ = the last inner step's ‖x_new − x‖, ‖x‖ (same operands, same order)
+      if (last_ndx < x_tol * std::max(last_nx, 1.0) || frel <= f_tol ||
           pri < x_tol)
         break;   // iterate.jl:257-259
       ++epochs;
