@@ -193,6 +193,7 @@ struct scs_ctx {
   std::vector<double> zkey;
   bool zvalid = false;
   double zfval = 0.0;  // f(x) for zkey (global, scaled)
+  bool zf_pending = false;   // zfval still in flight to hscal[8] (forward with need_val = false)
   std::vector<double> gkey[2];
   bool gvalid[2] = {false, false};
   // scs_iterate's host vectors carry version tags (bumped on every write), so the f / ∇q caches
@@ -673,7 +674,7 @@ void require_dense(scs_ctx* c, const char* what) {
 // Forward pass at the device vector xd whose host copy is xh: z = A x (or the
 // cached z), then the epilogue with `flags`.  Always refreshes the f-value
 // cache; returns f(x) (global).
-double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
+double forward(scs_ctx* c, const double* xh, const double* xd, int flags, bool need_val = true) {
   const bool cached = c->zvalid && key_hit(c, c->zkey, c->ztag, xh);
   hipEvent_t e0;
   if (!cached) {
@@ -689,14 +690,18 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags) {
     allreduce(c, c->red, 1);
     if (c->nranks > 1) HCK(hipMemcpyAsync(c->scal + 8, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
     d2h(c, c->hscal + 8, c->scal + 8, 1);
-    sync(c);
-    c->zfval = loss_scale_value(c, c->hscal[8]);
+    c->zf_pending = true;   // read at the next use: no host round trip when the caller only needs z
     key_set(c, c->zkey, c->ztag, xh);
     c->zvalid = true;
   } else if (flags & ~(EPI_VAL | EPI_Z)) {
     flags &= ~(EPI_Z | EPI_VAL);
     HCK(launch_epilogue(c->loss, c->ggn, flags, c->z, 1, c->Npad, c->y, c->N, c->Npad, c->scale, c->z, c->gN, c->hN,
                         c->wN, c->vN, c->valpart, c->st));
+  }
+  if (need_val && c->zf_pending) {
+    sync(c);
+    c->zfval = loss_scale_value(c, c->hscal[8]);
+    c->zf_pending = false;
   }
   return c->zfval;
 }
@@ -757,7 +762,7 @@ void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
     HCK(launch_axpby(c->y, 0.5, c->gtmp2, c->m, out, c->st));  // y + 0.5*(Ax + Aᵀx)
     return;
   }
-  forward(c, xh, xd, EPI_GRAD);
+  forward(c, xh, xd, EPI_GRAD, false);
   gemv_t_global(c, c->gN, out);
 }
 
@@ -1049,7 +1054,7 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
     c->nstiles = nt;
   }
   // s, q, r (prox-GGN-SCORE.jl:44-56) -> gN, hN, wN
-  forward(c, xh, c->x, EPI_GGN | EPI_SQR);
+  forward(c, xh, c->x, EPI_GGN | EPI_SQR, false);
   HCK(launch_ggn_sample_prep(c->Hr, c->gr, c->lam, m, c->mpad, c->hvec, c->hg, c->st));
   hipEvent_t e0;
   tbegin(c, T_GRAM, &e0);
@@ -1104,14 +1109,14 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
       HCK(launch_half_sym(c->A, c->nstage, m, c->G, c->mpad, c->st));
       grad_f_dev(c, xh, c->x, c->gtmp);
     } else {
-      forward(c, xh, c->x, EPI_GRAD | EPI_HESS);
+      forward(c, xh, c->x, EPI_GRAD | EPI_HESS, false);
       // local Aᵀg (not yet reduced; fused into the Gram pass); reduced together with the Gram
       gram_and_reduce(c, c->hN, c->gN, c->gtmp);
     }
   } else {
     if (c->ggn == SCS_GGN_NONE) fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs an out_fn / GGN loss kind");
     // J, residual, Q (prox-GGN-SCORE.jl:44-56) -> w = s²q, v = s·r
-    forward(c, xh, c->x, EPI_GGN);
+    forward(c, xh, c->x, EPI_GGN, false);
     gram_and_reduce(c, c->wN, c->vN, c->gtmp);   // Gram + Jᵀr in one pass over A
   }
   // rhs = ∇f + λ gr (NSCORE) | Jᵀr + λ gr (GGN: Jt*[r;1], prox-GGN-SCORE.jl:121-130)
