@@ -22,6 +22,7 @@ logistic N=100k m=8k (configs[1]), c4 ProxGGNSCORE sparse-group lasso N=4M m=32k
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -194,13 +195,16 @@ def main():
             traffic = None
             kname = ("gram_sia_kernel<1, 4, false, true>" if fuse else "gram_sia_kernel<1, 4>") if tall \
                 else "gram_sia_kernel<1, 2>"
-            pmc = os.path.join(ROOT, "profiles", "r01_gram_pmc.json")   # tools/gpu_prof_c3.sh + tools/pmc_summary.py
-            if os.path.exists(pmc) and world == 1:
+            # PMC summaries (tools/gpu_prof_c3.sh, tools/gpu_pmc_c2.sh + tools/pmc_summary.py), one per (N, m)
+            for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_gram_pmc*.json"))):
+                if world != 1 or args.gram_cache:
+                    break
                 with open(pmc) as f:
                     pm = json.load(f)
                 if pm.get("N") == N and pm.get("m") == m:
                     traffic = pm.get("hbm_bytes_per_launch")
                     kname = pm.get("kernel", kname)
+                    break
             line["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                                 "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                                 "kernel": kname, "avg_ms": gram_avg_ms, "launches": main_calls,

@@ -11,7 +11,8 @@ import csv
 import json
 import os
 
-KERNELS = ("gram_sia_kernel<1, 4, false, true>", "gram_sia_kernel<1, 4>", "gram_sia_kernel<1, 2>", "gram_glds_kernel", "gram_f64_kernel<false, 4, true>", "gram_f64_kernel<false, 2, true>")
+KERNELS = ("gram_sia_kernel<1, 4, false, true>", "gram_sia_kernel<1, 4>", "gram_sia_kernel<1, 2>",
+           "gram_sia_kernel<1, 2, false, false>", "gram_sia_kernel<1, 4, false, false>", "gram_glds_kernel", "gram_f64_kernel<false, 4, true>", "gram_f64_kernel<false, 2, true>")
 
 
 def load(d, name):
