@@ -34,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd")
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix, AMD spec; 64 cycles/MFMA confirmed by PMC
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "t_iter_s", "reps", "stat", "threads_note")
 METRIC = "iterate!() iterations/sec + achieved HBM GB/s, ProxGGNSCORE n=1M m=16k"
 
 CONFIGS = {
@@ -91,6 +92,63 @@ def build_problem(cfg, N, m, comm, local, f32=False):
     return model, hmu, meth
 
 
+def sampled_gram_check(model, m, seed=7, ncols=8):
+    """Full-size parity property of the dominant kernel: the production Gram launch (with the Aᵀv
+    fused where a step fuses it) against host fp64 dot products of columns read back from the
+    device, for all pairs of `ncols` random columns and their Aᵀv entries; bound 1e-11·Σ|terms|
+    (summation order differs; a wrong tile / weight / panel is an O(1) error)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    N = model.N
+    cols = np.sort(rng.choice(m, ncols, replace=False))
+    w = rng.random(N) + 0.5
+    v = rng.standard_normal(N)
+    pairs = [(int(i), int(j)) for a, i in enumerate(cols) for j in cols[a:]]
+    g, atv, fused = model.gram_atv_sample(w, v, pairs)
+    Ac = model.get_columns(cols)
+    col = {int(c): k for k, c in enumerate(cols)}
+    worst = 0.0
+    for (i, j), gv in zip(pairs, g):
+        a, b = Ac[:, col[i]], Ac[:, col[j]]
+        ref = float((a * w) @ b)
+        worst = max(worst, abs(gv - ref) / (1e-11 * float(np.abs(a * w * b).sum()) + 1e-300))
+    ref_atv = Ac.T @ v
+    bound = 1e-11 * (np.abs(Ac).T @ np.abs(v))
+    worst_v = float(np.max(np.abs(atv[cols] - ref_atv) / (bound + 1e-300)))
+    return {"gram_entries": len(pairs), "atv_entries": int(ncols), "fused_atv": fused,
+            "max_err_over_bound": max(worst, worst_v), "bound": "1e-11 * sum|terms| (host fp64 dots)",
+            "pass": bool(worst <= 1.0 and worst_v <= 1.0)}
+
+
+def host_info():
+    """The GPU box's host as the CPU baseline saw it."""
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    info["model"] = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return info
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: the process's CPU share on the GPU box (OMP_NUM_THREADS, set to
+    16 per GPU there; nproc / os.cpu_count() report the whole machine), capped by the affinity mask."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    return max(1, n)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +162,7 @@ def main():
                     help="c4: reuse the x-independent AᵀQA of least squares across steps (scs_set_gram_cache; "
                          "reported separately -- the reference recomputes it every step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the sampled full-size Gram / Aᵀv check")
     ap.add_argument("--cpu-Ns", type=int, default=2048)
     ap.add_argument("--cpu-ms", type=int, default=4096)
     args = ap.parse_args()
@@ -172,6 +231,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    check = None
+    if rank == 0 and not cfg.get("sparse") and cfg["loss"] != "rosenbrock" and not args.no_check:
+        check = sampled_gram_check(model, m)
+
     if rank == 0:
         ms_step = 1e3 * dt / steps
         value = steps / dt
@@ -195,15 +258,16 @@ def main():
             traffic = None
             kname = ("gram_sia_kernel<1, 4, false, true>" if fuse else "gram_sia_kernel<1, 4>") if tall \
                 else "gram_sia_kernel<1, 2>"
-            # PMC summaries (tools/gpu_prof_c3.sh, tools/gpu_pmc_c2.sh + tools/pmc_summary.py), one per (N, m)
-            for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_gram_pmc*.json"))):
+            # PMC summaries (tools/gpu_prof_c3.sh, tools/gpu_pmc_c2.sh + tools/pmc_summary.py), one per (N, m):
+            # their bytes are used only when they were measured on the kernel this run launched
+            for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_gram_pmc*.json")), reverse=True):
                 if world != 1 or args.gram_cache:
                     break
                 with open(pmc) as f:
                     pm = json.load(f)
-                if pm.get("N") == N and pm.get("m") == m:
+                if pm.get("N") == N and pm.get("m") == m and pm.get("kernel", "").split("::")[-1] == kname:
                     traffic = pm.get("hbm_bytes_per_launch")
-                    kname = pm.get("kernel", kname)
+                    line["roofline_traffic_source"] = os.path.relpath(pmc, ROOT)
                     break
             line["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                                 "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
@@ -248,13 +312,15 @@ def main():
             line["config"]["gram_cache"] = True
         line["breakdown_ms_per_step"] = {k.replace("_ms", ""): tm[k] / steps for k in tm if k.endswith("_ms")}
         line["objective_last"] = objs[-1]
+        if check is not None:
+            line["parity_check"] = check
         do_cpu = not args.no_cpu_baseline and world == 1   # the CPU baseline: rank 0 at N = 1 only
         if do_cpu and args.config == "c1":
             try:
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline_c1.py")],
                                      capture_output=True, text=True, timeout=120, check=True)
                 cb = json.loads(out.stdout.strip().splitlines()[-1])
-                line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+                line["cpu_baseline"] = {k: cb[k] for k in CPU_KEYS if k in cb}
             except Exception as e:  # the baseline is reported, never the target
                 line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
         if do_cpu and args.config == "c5":
@@ -263,27 +329,30 @@ def main():
                                       "--m", str(m), "--rho", str(cfg["rho"]), "--mem", str(cfg["mem"])],
                                      capture_output=True, text=True, timeout=300, check=True)
                 cb = json.loads(out.stdout.strip().splitlines()[-1])
-                line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
-                line["cpu_baseline"]["t_iter_s"] = cb["t_iter_s"]
+                line["cpu_baseline"] = {k: cb[k] for k in CPU_KEYS if k in cb}
             except Exception as e:  # the baseline is reported, never the target
                 line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
         if do_cpu and args.config in ("c2", "c3", "c4"):
             env = dict(os.environ)
-            cores = int(env.get("OMP_NUM_THREADS", "16"))
+            cores = cpu_threads()
             env["OPENBLAS_NUM_THREADS"] = str(cores)
+            env["OMP_NUM_THREADS"] = str(cores)
             try:
                 meth = {"c2": "nscore", "c3": "ggn", "c4": "ggn_ls"}[args.config]
                 Ns = args.cpu_Ns if m <= 16384 else 256   # bounded sample (the dgemm is Ns·m² flops)
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--N", str(N),
                                       "--m", str(m), "--Ns", str(Ns), "--ms", str(min(args.cpu_ms, m)),
-                                      "--method", meth],
+                                      "--method", meth, "--reps", "3"],
                                      capture_output=True, text=True, env=env, timeout=300, check=True)
                 cb = json.loads(out.stdout.strip().splitlines()[-1])
-                line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
-                line["cpu_baseline"]["t_iter_s"] = cb["t_iter_s"]
+                line["cpu_baseline"] = {k: cb[k] for k in CPU_KEYS if k in cb}
             except Exception as e:  # the baseline is reported, never the target
                 line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
+        if isinstance(line.get("cpu_baseline"), dict):
+            line["cpu_baseline"]["host"] = host_info()
         print(json.dumps(line))
+        if check is not None and not check["pass"]:
+            raise SystemExit("sampled full-size Gram / Aᵀv check FAILED: " + json.dumps(check))
     if world > 1:
         dist.destroy_process_group()
 

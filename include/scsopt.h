@@ -252,6 +252,24 @@ int scs_gemv_t_eval(scs_ctx* ctx, const double* v, double* out);
 /* out = A x (local rows)                                                   */
 int scs_gemv_n_eval(scs_ctx* ctx, const double* x, double* out);
 
+/* The m x m system of ProxNSCORE / ProxGGNSCORE, (Aᵀ diag(w) A + diag(dvec)) x = rhs
+ * ((H + λ·Diagonal(Hr)) \ ∇q, prox-N-SCORE.jl:69-70; qr(JQJ) \ Je, prox-GGN-SCORE.jl:129-131),
+ * through the step's own path: MFMA Gram, then the hand-written Cholesky with the LU
+ * fallback (mode 0) or the hand-written LU alone (mode 1).  *used_lu = 1 when the LU ran.  */
+int scs_solve_eval(scs_ctx* ctx, const double* w, const double* dvec, const double* rhs, int mode,
+                   double* x, int* used_lu);
+/* Julia's `A \ b` for a dense square Matrix (LAPACK getrf + getrs) by the hand-written
+ * blocked LU: A is row-major n x n; ipiv receives getrf's pivot rows (0-based), info its
+ * first zero pivot (1-based; x is then not written).  Needs a context only.               */
+int scs_lu_eval(scs_ctx* ctx, int64_t n, const double* A, const double* b, double* x, int32_t* ipiv,
+                int* info);
+/* Columns cols[0..ncols) of the local (dense) A, column-major N x ncols.                 */
+int scs_get_columns(scs_ctx* ctx, const int64_t* cols, int64_t ncols, double* out);
+/* The production Gram launch for weights w, with Aᵀv formed in the same pass where a step
+ * fuses it (*fused = 1): entries G(ij[2k], ij[2k+1]) for k < n, and Aᵀv (m).              */
+int scs_gram_atv_eval(scs_ctx* ctx, const double* w, const double* v, const int64_t* ij, int64_t n,
+                      double* gvals, double* atv, int* fused);
+
 /* ---- timing ------------------------------------------------------------- */
 int scs_timing_enable(scs_ctx* ctx, int on);
 int scs_timing_get(scs_ctx* ctx, scs_timing* out);

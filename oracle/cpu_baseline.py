@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--m", type=int, default=1 << 14)
     ap.add_argument("--Ns", type=int, default=2048)
     ap.add_argument("--ms", type=int, default=0, help="QR timed at ms and scaled by (m/ms)^3 (0: full m)")
-    ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--method", default="ggn", choices=["ggn", "ggn_ls", "nscore"],
                     help="ggn: C3 (CE + sigmoid out_fn, QR); ggn_ls: C4 (least squares, J = A, QR); "
                          "nscore: C2 (logistic margin, hess_fx Gram, LU)")
@@ -116,15 +116,15 @@ def main():
         t0 = time.perf_counter()
         sample_part()
         ts.append(time.perf_counter() - t0)
-    t_sample = min(ts)
+    t_sample = float(np.median(ts))
     msz = a.ms if a.ms else m
-    t_qr = solve_part(msz)
+    t_qr = float(np.median([solve_part(msz) for _ in range(a.reps)]))
     t_qr_full = t_qr * (m / msz) ** 3
     t_iter = t_sample * (N / Ns) + t_qr_full
     threads = int(os.environ.get("OPENBLAS_NUM_THREADS", os.environ.get("OMP_NUM_THREADS", os.cpu_count())))
     print(json.dumps({
         "value": 1.0 / t_iter, "unit": "iterations/s", "cores": threads, "kind": "port",
-        "t_iter_s": t_iter, "t_sample_s": t_sample, "t_qr_s": t_qr, "qr_m": msz,
+        "t_iter_s": t_iter, "t_sample_s": t_sample, "t_qr_s": t_qr, "qr_m": msz, "reps": a.reps, "stat": "median",
         "sample": f"oracle port (NumPy/OpenBLAS, reference BLAS call structure) of one "
                   f"{'ProxNSCORE' if a.method == 'nscore' else 'ProxGGNSCORE'} epoch ({a.method}): "
                   f"sample part on {Ns} of {N} rows x m={m} scaled x{N / Ns:.0f}, "

@@ -90,11 +90,13 @@ def main():
         t0 = time.perf_counter()
         vector_part()
         tv.append(time.perf_counter() - t0)
-    t_sparse, t_vec = min(ts), min(tv)
+    t_sparse, t_vec = float(np.median(ts)), float(np.median(tv))
     t_iter = t_sparse * (N / Ns) + t_vec
     print(json.dumps({
         "value": 1.0 / t_iter, "unit": "iterations/s", "cores": 1, "kind": "port",
-        "t_iter_s": t_iter, "t_sparse_sample_s": t_sparse, "t_vector_s": t_vec,
+        "t_iter_s": t_iter, "t_sparse_sample_s": t_sparse, "t_vector_s": t_vec, "reps": a.reps, "stat": "median",
+        "threads_note": "1 thread: the reference's SparseMatrixCSC products (SparseArrays mul!) are single-threaded, "
+                        "and SciPy's CSR/CSC matvec holds the GIL (measured: 8 threads over row chunks = 1.0x)",
         "sample": f"oracle port (SciPy CSR, single thread, reference call structure: 3 A*x + 2 Aᵀ*r per epoch) "
                   f"of one ProxLQNSCORE(mem={a.mem}) epoch: sparse products on {Ns} of {N} rows "
                   f"(rho={a.rho}, nnz {Ns * k}) scaled x{N // Ns}, two-loop/smoother/prox at full m={m}",

@@ -391,4 +391,33 @@ hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t
   return hipGetLastError();
 }
 
+// out[k][n] = A(n, cols[k]) for n < N (column-major N x ncols): selected columns of the
+// panel-blocked A back in the host layout (bench.py's sampled Gram / Aᵀv check)
+__global__ void get_columns_kernel(const double* __restrict__ A, int64_t S, const int64_t* __restrict__ cols,
+                                   int64_t N, double* __restrict__ out) {
+  const int64_t k = blockIdx.y, j = cols[k];
+  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < N; n += (int64_t)gridDim.x * blockDim.x)
+    out[k * N + n] = A[tiled_off(S, n, j)];
+}
+
+hipError_t launch_get_columns(const double* A, int64_t S, const int64_t* cols, int64_t ncols, int64_t N, double* out,
+                              hipStream_t st) {
+  if (ncols <= 0 || N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(get_columns_kernel, dim3(256, (unsigned)ncols), dim3(256), 0, st, A, S, cols, N, out);
+  return hipGetLastError();
+}
+
+// out[k] = G[ij[k].y * ld + ij[k].x]
+__global__ void gather_entries_kernel(const double* __restrict__ G, int64_t ld, const int2* __restrict__ ij, int n,
+                                      double* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[k] = G[(int64_t)ij[k].y * ld + ij[k].x];
+}
+
+hipError_t launch_gather_entries(const double* G, int64_t ld, const int2* ij, int n, double* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_entries_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, G, ld, ij, n, out);
+  return hipGetLastError();
+}
+
 }  // namespace scs

@@ -67,6 +67,32 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
                       hipStream_t st);
 
+// ---- lu.hip (blocked LU with partial pivoting, row-major, in place; lu_solve after lu_factor)
+struct LUAux {
+  int64_t npad = 0;          // capacity (lu_aux_init)
+  double* cand = nullptr;    // [2][256] per-workgroup pivot candidates |a| of the next column
+  int* candi = nullptr;      // [2][256] their rows
+  double* candrow = nullptr; // [2][256][128] their panel rows
+  double* rowj = nullptr;    // [2][128] copy of row j (the row the pivot row displaces)
+  int* ipiv = nullptr;       // [npad] pivot row of each column (0-based, absolute)
+  int2* pairs = nullptr;     // [nblk][256] composed row moves of each block (dst, src)
+  int* npairs = nullptr;     // [nblk]
+  double* Linv = nullptr;    // [nblk][128 x 128] row-major L11⁻¹
+  double* Uinv = nullptr;    // [nblk][128 x 128] row-major U11⁻¹
+  double* T = nullptr;       // [npad][128] A12ᵀ staging
+  double* UT = nullptr;      // [npad][128] U12 as K-contiguous columns
+  double* w = nullptr;       // [128 x +1 | 128 x -1]
+  int2* sq = nullptr;        // square-shell tile list (trailing updates)
+  int2* row1 = nullptr;      // (0, j) tile list (TRSM)
+};
+hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st);
+void lu_aux_free(LUAux* a);
+// A: npad x npad row-major (row stride ld), rows/cols [n, npad) zero; *info must be 0 on
+// entry and receives the first zero pivot (1-based) -- the factorization still completes.
+hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st);
+// b (npad, zero-padded) <- A⁻¹ b
+hipError_t lu_solve(const double* A, int64_t ld, int64_t npad, const LUAux* a, double* b, hipStream_t st);
+
 // ---- vec.hip
 hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,
                            const double* wel, double* gr, double* Hr, hipStream_t st);
@@ -134,12 +160,17 @@ hipError_t launch_gather_rows(const double* A, int64_t Npad, const double* y, co
                               int64_t Npad_b, int64_t mpad, double* Ab, double* yb, hipStream_t st);
 hipError_t launch_transpose(const double* A, int64_t Npad, int64_t N, int64_t m, double* At, int64_t ldt,
                             int64_t nt, hipStream_t st);
+// selected columns of the panel-blocked A -> column-major N x ncols (cols on the device)
+hipError_t launch_get_columns(const double* A, int64_t S, const int64_t* cols, int64_t ncols, int64_t N, double* out,
+                              hipStream_t st);
+// out[k] = G(ij[k].x, ij[k].y) of a column-major matrix
+hipError_t launch_gather_entries(const double* G, int64_t ld, const int2* ij, int n, double* out, hipStream_t st);
 // GGN sample-space branch (vec.hip)
 hipError_t launch_ggn_sample_prep(const double* Hr, const double* gr, double lam, int64_t m, int64_t mpad,
                                   double* hvec, double* hg, hipStream_t st);
 hipError_t launch_ggn_sample_assemble(const double* P, int64_t ldp, const double* s, const double* q,
                                       const double* r, const double* u, const double* kNN, int64_t N, double* M,
-                                      double* b, hipStream_t st);
+                                      int64_t ldm, double* b, hipStream_t st);
 hipError_t launch_ggn_sample_scale(const double* s, const double* B, int64_t N, int64_t Npad, double* v,
                                    hipStream_t st);
 hipError_t launch_ggn_sample_direction(const double* hvec, const double* t, const double* hg, const double* B,

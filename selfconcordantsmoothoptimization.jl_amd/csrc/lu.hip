@@ -1,0 +1,545 @@
+// Blocked LU with partial pivoting (GEPP), in place, ROW-major, for the systems the
+// reference solves with a general factorization:
+//   * `(H + λ·Diagonal(Hr)) \ ∇q` (prox-N-SCORE.jl:70, Julia `\` on a dense Matrix = LAPACK
+//     getrf/getrs) when the hand-written Cholesky (chol.hip) meets a non-positive pivot --
+//     the indefinite Q of a cross-entropy GGN on ±1 labels (test/test_algs.jl:10) and the
+//     NSCORE box QP;
+//   * the GGN sample-space system `qr(I + Q'(Jt'H⁻¹)Jt) \ [r; 1]` (prox-GGN-SCORE.jl:124-127),
+//     non-symmetric, (N+1) x (N+1).
+// Pivots follow LAPACK getf2: the first row of maximal |a| in the column; a zero pivot
+// is recorded (info, 1-based) and its column is neither swapped nor scaled.
+//
+// Why row-major: a row interchange then moves contiguous bytes, the panel rows are 1 KiB
+// contiguous pieces (the panel is factored in place, no copy), and the L21 rows are
+// directly the "contiguous K" operand of the MFMA Gram kernels (gram.hip):
+//   panel      128 launches of lu_panel_step_kernel (one per column: the argmax of the
+//              column needs every row of the panel, so each column step is one grid-wide
+//              hand-off -- a kernel boundary here, cheaper than an in-launch grid barrier,
+//              MI355X_MICROARCH.md "boundary" vs "barrier-xcd");
+//   swaps      the block's 128 interchanges composed into <= 256 (dst, src) row moves
+//              (lu_perm_kernel) and applied to the columns right of the panel in one pass;
+//   inverses   L11⁻¹ (unit lower) and U11⁻¹ of the diagonal block (lu_diag_inv_kernel);
+//   TRSM       U12 = L11⁻¹ A12 = Gram(L11⁻¹ rows, A12ᵀ) on MFMA (A12ᵀ staged by a transpose);
+//   update     A22 -= L21 U12 = Gram(L21 rows, U12ᵀ, w = -1), accumulate, row-major store.
+// The column interchanges of later blocks are NOT applied to the L columns of earlier
+// blocks; lu_solve applies each block's interchanges to b just before that block's
+// forward step (the order getrf's left swaps would have produced).
+//
+// Layout: A is npad x npad, row stride ld >= npad, npad % 128 == 0.  Rows/columns
+// [n, npad) must be zero on entry; lu_factor puts ones on their diagonal (block-diag(A, I)).
+#include <climits>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace scs {
+
+constexpr int LB = 128;           // block / panel width
+constexpr int LU_MAXWG = 256;     // workgroups of a panel step at most
+constexpr int LU_NT = 256;        // panel step: 32 rows x 8 lanes (16 columns each) per pass
+constexpr int LU_MAXPAIRS = 2 * LB;
+
+__device__ __forceinline__ bool lu_better(double v1, int i1, double v2, int i2) {
+  return v1 > v2 || (v1 == v2 && i1 < i2);
+}
+
+// (v, i) argmax over the workgroup (larger |a|, then smaller row); every thread gets the result.
+// sv / si hold LU_NT / 64 entries.
+__device__ __forceinline__ void lu_block_argmax(double& v, int& i, int& w, double* sv, int* si, int* sw) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(v, o, 64);
+    const int i2 = __shfl_xor(i, o, 64);
+    const int w2 = __shfl_xor(w, o, 64);
+    if (lu_better(v2, i2, v, i)) {
+      v = v2;
+      i = i2;
+      w = w2;
+    }
+  }
+  const int wv = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sv[wv] = v;
+    si[wv] = i;
+    sw[wv] = w;
+  }
+  __syncthreads();
+  v = sv[0];
+  i = si[0];
+  w = sw[0];
+#pragma unroll
+  for (int k = 1; k < LU_NT / 64; ++k)
+    if (lu_better(sv[k], si[k], v, i)) {
+      v = sv[k];
+      i = si[k];
+      w = sw[k];
+    }
+}
+
+template <int NV>
+__device__ __forceinline__ double sel(const double (&v)[NV], int k) {
+  double r = 0.0;
+#pragma unroll
+  for (int t = 0; t < NV; ++t) r = (t == k) ? v[t] : r;
+  return r;
+}
+
+// One column step j of the panel (columns c0 .. c0+127, rows r0 .. r0+h-1 = local 0 .. h-1).
+// Workgroup g owns local rows [g·R, g·R + R).
+//   1. pivot: the best of the per-workgroup candidates of column j (written by step j-1 into
+//      slot j&1): row p, pivot row u = that candidate's full panel row (a copy: no race with
+//      this launch's stores);
+//   2. row j <- u, row p <- the previous row j (rowj copy), every row i > j:
+//      l = a_ij / u_j (column j <- l), a_ic -= l·u_c for c > j;
+//   3. candidates of column j+1 over this workgroup's rows > j (post-update) -> slot (j+1)&1,
+//      with the row's full copy; the owner of row j+1 also copies it to rowj.
+// j = -1: only step 3 for column 0.
+__global__ __launch_bounds__(LU_NT) void lu_panel_step_kernel(double* A, int64_t ld, int64_t r0, int64_t c0,
+                                                              int64_t h, int R, int j, double* cand, int* candi,
+                                                              double* candrow, double* rowj, int* ipiv, int* info) {
+  __shared__ double sv[LU_NT / 64];
+  __shared__ int si[LU_NT / 64], sw[LU_NT / 64];
+  const int tid = threadIdx.x, g = blockIdx.x, nwg = gridDim.x;
+  const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
+  const int par = j & 1, npar = (j + 1) & 1;
+  int p = j;
+  double piv = 0.0, rp = 0.0;
+  bool scale = false;
+  const double* urow = nullptr;
+  if (j >= 0) {
+    double v = -1.0;
+    int i = INT_MAX, w = -1;
+    if (tid < nwg) {
+      v = cand[par * LU_MAXWG + tid];
+      i = candi[par * LU_MAXWG + tid];
+      w = tid;
+      if (!(v >= 0.0)) {   // no candidate (or NaN): never wins
+        v = -1.0;
+        i = INT_MAX;
+      }
+    }
+    lu_block_argmax(v, i, w, sv, si, sw);
+    if (v < 0.0) {   // no valid candidate anywhere (NaN column): keep row j
+      p = j;
+      urow = rowj + par * LB;
+    } else {
+      p = i;
+      urow = candrow + ((int64_t)par * LU_MAXWG + w) * LB;
+    }
+    piv = urow[j];
+    scale = (piv != 0.0);
+    if (!scale) {   // getf2: zero pivot -> no interchange, no scaling (the column below is zero)
+      p = j;
+      urow = rowj + par * LB;
+      piv = urow[j];
+    }
+    rp = 1.0 / piv;
+    if (g == 0 && tid == 0) {
+      ipiv[r0 + j] = (int)(r0 + p);
+      if (!scale && *info == 0) *info = (int)(r0 + j + 1);
+    }
+  }
+  const int jn = j + 1;
+  double u[16];
+  const bool need_u = (j >= 0) && (cq + 15 > j);
+  if (need_u) {
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(u + c) = *(const v2d*)(urow + cq + c);
+  }
+  double bv = -1.0;
+  int bi = INT_MAX;
+  const int npass = R / 32;
+  for (int pass = 0; pass < npass; ++pass) {
+    const int64_t i = (int64_t)g * R + pass * 32 + rr;
+    if (i >= h || i < j) continue;
+    double* row = A + (r0 + i) * ld + c0;
+    if (j < 0) {   // column-0 candidates
+      if (q == 0) {
+        const double a = fabs(row[0]);
+        if (lu_better(a, (int)i, bv, bi)) {
+          bv = a;
+          bi = (int)i;
+        }
+      }
+      continue;
+    }
+    const bool top = (i == j) && (p != j);
+    const bool bot = (i == p) && (p != j);
+    if (i == j) {   // the pivot row: U(j, :) = u
+      if (top) {
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) *(v2d*)(row + cq + c) = *(const v2d*)(urow + cq + c);
+      }
+      continue;
+    }
+    const double* src = bot ? (rowj + par * LB) : row;
+    if (!(bot || cq + 15 >= j)) continue;   // columns < j of an unmoved row are final
+    double v[16];
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(v + c) = *(const v2d*)(src + cq + c);
+    const double x = src[j];
+    const double l = scale ? (fabs(piv) >= 2.2250738585072014e-308 ? x * rp : x / piv) : x;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int col = cq + c;
+      if (col > j) v[c] -= l * u[c];
+      else if (col == j) v[c] = l;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(row + cq + c) = *(const v2d*)(v + c);
+    if (jn < LB && q == (jn >> 4)) {
+      const double a = fabs(sel(v, jn & 15));
+      if (lu_better(a, (int)i, bv, bi)) {
+        bv = a;
+        bi = (int)i;
+      }
+    }
+  }
+  if (jn >= LB) return;
+  int bw = g;
+  lu_block_argmax(bv, bi, bw, sv, si, sw);   // (its __syncthreads also orders this workgroup's row stores)
+  if (tid == 0) {
+    cand[npar * LU_MAXWG + g] = (bi == INT_MAX) ? -1.0 : bv;
+    candi[npar * LU_MAXWG + g] = bi;
+  }
+  if (bi != INT_MAX && tid < LB) candrow[((int64_t)npar * LU_MAXWG + g) * LB + tid] = A[(r0 + bi) * ld + c0 + tid];
+  if ((int64_t)g * R <= jn && jn < (int64_t)g * R + R && tid < LB) rowj[npar * LB + tid] = A[(r0 + jn) * ld + c0 + tid];
+}
+
+// Compose block k's 128 interchanges (rows r0+s <-> ipiv[r0+s], in order) into row moves
+// "row dst <- previous row src" (<= 256 of them).  One wave.
+__global__ __launch_bounds__(64) void lu_perm_kernel(const int* __restrict__ ipiv, int r0, int2* __restrict__ pairs,
+                                                     int* __restrict__ npairs) {
+  __shared__ int top[LB];         // content of rows r0 .. r0+127
+  __shared__ int brow[LB], bval[LB];   // touched rows below the block: (row, content)
+  __shared__ int nb;
+  const int lane = threadIdx.x;
+  for (int t = lane; t < LB; t += 64) top[t] = r0 + t;
+  if (lane == 0) nb = 0;
+  __syncthreads();
+  for (int s = 0; s < LB; ++s) {
+    const int pr = ipiv[r0 + s];
+    if (pr == r0 + s) continue;
+    if (pr < r0 + LB) {
+      if (lane == 0) {
+        const int t = top[s];
+        top[s] = top[pr - r0];
+        top[pr - r0] = t;
+      }
+    } else {
+      int slot = -1;
+      for (int b = lane; b < nb; b += 64)
+        if (brow[b] == pr) slot = b;
+      // rows are unique in the list: at most one lane matches
+      const unsigned long long hit = __ballot(slot >= 0);
+      const int found = hit ? __shfl(slot, __ffsll((long long)hit) - 1, 64) : -1;
+      if (lane == 0) {
+        int sl;
+        if (found >= 0) {
+          sl = found;
+        } else {
+          sl = nb;
+          brow[sl] = pr;
+          bval[sl] = pr;
+          nb = nb + 1;
+        }
+        const int t = top[s];
+        top[s] = bval[sl];
+        bval[sl] = t;
+      }
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    int n = 0;
+    for (int t = 0; t < LB; ++t)
+      if (top[t] != r0 + t) pairs[n++] = make_int2(r0 + t, top[t]);
+    for (int b = 0; b < nb; ++b)
+      if (bval[b] != brow[b]) pairs[n++] = make_int2(brow[b], bval[b]);
+    *npairs = n;
+  }
+}
+
+// Apply the row moves to columns [c_lo, c_lo + w): all sources read before any store.
+constexpr int SW_COLS = 64;
+__global__ __launch_bounds__(256) void lu_swap_cols_kernel(double* A, int64_t ld, int64_t c_lo, int64_t w,
+                                                           const int2* __restrict__ pairs,
+                                                           const int* __restrict__ npairs) {
+  __shared__ double buf[LU_MAXPAIRS * SW_COLS];
+  const int np = *npairs;
+  if (np == 0) return;
+  const int col = threadIdx.x & (SW_COLS - 1), kg = threadIdx.x / SW_COLS;
+  const int64_t c = c_lo + (int64_t)blockIdx.x * SW_COLS + col;
+  const bool ok = (int64_t)blockIdx.x * SW_COLS + col < w;
+  for (int k = kg; k < np; k += 256 / SW_COLS)
+    if (ok) buf[k * SW_COLS + col] = A[(int64_t)pairs[k].y * ld + c];
+  __syncthreads();
+  for (int k = kg; k < np; k += 256 / SW_COLS)
+    if (ok) A[(int64_t)pairs[k].x * ld + c] = buf[k * SW_COLS + col];
+}
+
+// L11⁻¹ (block 0) and U11⁻¹ (block 1) of the factored 128 x 128 diagonal block, row-major.
+// X in registers (8 x 8 per thread: rows 8·(tid>>4), columns 8·(tid&15)); one row of X is
+// broadcast through LDS per elimination step.
+__global__ __launch_bounds__(256) void lu_diag_inv_kernel(const double* __restrict__ A, int64_t ld, int64_t r0,
+                                                          double* __restrict__ Linv, double* __restrict__ Uinv) {
+  constexpr int SP = LB + 1;
+  __shared__ double S[LB * SP];
+  __shared__ double rb[2][LB];
+  const int tid = threadIdx.x, ti = tid >> 4, tc = tid & 15;
+  for (int e = tid; e < LB * LB; e += 256) {
+    const int i = e >> 7, c = e & 127;
+    S[i * SP + c] = A[(r0 + i) * ld + r0 + c];
+  }
+  double X[8][8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) X[r][c] = (8 * ti + r == 8 * tc + c) ? 1.0 : 0.0;
+  __syncthreads();
+  const bool lower = blockIdx.x == 0;
+  for (int s = 0; s < LB; ++s) {
+    const int k = lower ? s : LB - 1 - s;
+    const int b = s & 1;
+    if (ti == (k >> 3)) {
+      const double dinv = lower ? 1.0 : 1.0 / S[k * SP + k];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        double xv = 0.0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) xv = (r == (k & 7)) ? X[r][c] : xv;
+        xv *= dinv;
+        rb[b][8 * tc + c] = xv;
+        if (!lower) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+            if (r == (k & 7)) X[r][c] = xv;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = 8 * ti + r;
+      if (lower ? (i > k) : (i < k)) {
+        const double f = S[i * SP + k];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) X[r][c] -= f * rb[b][8 * tc + c];
+      }
+    }
+  }
+  double* out = lower ? Linv : Uinv;
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) out[(8 * ti + r) * LB + 8 * tc + c] = X[r][c];
+}
+
+// T[j][k] = A(r0 + k, c_lo + j): the block row's 128 rows as columns (K-contiguous operand)
+__global__ __launch_bounds__(256) void lu_transpose_kernel(const double* __restrict__ A, int64_t ld, int64_t r0,
+                                                           int64_t c_lo, int64_t w, double* __restrict__ T) {
+  __shared__ double t[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * 64, k0 = (int64_t)blockIdx.y * 64;
+  for (int kk = ty; kk < 64; kk += 4) t[kk][tx] = (j0 + tx < w) ? A[(r0 + k0 + kk) * ld + c_lo + j0 + tx] : 0.0;
+  __syncthreads();
+  for (int jj = ty; jj < 64; jj += 4)
+    if (j0 + jj < w) T[(j0 + jj) * LB + k0 + tx] = t[tx][jj];
+}
+
+__global__ void lu_pad_kernel(double* A, int64_t ld, int64_t n, int64_t npad) {
+  const int64_t i = n + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < npad) A[i * ld + i] = 1.0;
+}
+
+// ---- solve -------------------------------------------------------------------------
+// forward block k: apply the block's row moves to b, then b_k <- L11⁻¹ b_k
+__global__ __launch_bounds__(256) void lu_fwd_block_kernel(const int2* __restrict__ pairs,
+                                                           const int* __restrict__ npairs,
+                                                           const double* __restrict__ Linv, int64_t r0, double* b) {
+  __shared__ double bs[LB];
+  __shared__ double part[2][LB];
+  const int tid = threadIdx.x, np = *npairs;
+  double v = 0.0;
+  if (tid < np) v = b[pairs[tid].y];
+  __syncthreads();
+  if (tid < np) b[pairs[tid].x] = v;
+  __syncthreads();
+  if (tid < LB) bs[tid] = b[r0 + tid];
+  __syncthreads();
+  {  // y_i = Σ_c Linv(i, c) b_c: two threads per row, 64 columns each
+    const int i = tid >> 1, h = tid & 1;
+    const double* lr = Linv + (int64_t)i * LB + 64 * h;
+    double s = 0.0;
+    for (int c = 0; c < 64; c += 2) {
+      const v2d a = *(const v2d*)(lr + c);
+      s += a[0] * bs[64 * h + c] + a[1] * bs[64 * h + c + 1];
+    }
+    part[h][i] = s;
+  }
+  __syncthreads();
+  if (tid < LB) b[r0 + tid] = part[0][tid] + part[1][tid];
+}
+
+// backward block k: b_k <- U11⁻¹ b_k
+__global__ __launch_bounds__(256) void lu_bwd_block_kernel(const double* __restrict__ Uinv, int64_t r0, double* b) {
+  __shared__ double bs[LB];
+  __shared__ double part[2][LB];
+  const int tid = threadIdx.x;
+  if (tid < LB) bs[tid] = b[r0 + tid];
+  __syncthreads();
+  {
+    const int i = tid >> 1, h = tid & 1;
+    const double* ur = Uinv + (int64_t)i * LB + 64 * h;
+    double s = 0.0;
+    for (int c = 0; c < 64; c += 2) {
+      const v2d a = *(const v2d*)(ur + c);
+      s += a[0] * bs[64 * h + c] + a[1] * bs[64 * h + c + 1];
+    }
+    part[h][i] = s;
+  }
+  __syncthreads();
+  if (tid < LB) b[r0 + tid] = part[0][tid] + part[1][tid];
+}
+
+// b[r] -= Σ_t A(r, c0 + t) b[c0 + t] for rows r in [rlo, rlo + nr): 8 lanes per row (16 columns
+// each), fixed-order butterfly over the 8 lanes.
+__global__ __launch_bounds__(256) void lu_rank_update_kernel(const double* __restrict__ A, int64_t ld, int64_t rlo,
+                                                             int64_t nr, int64_t c0, double* b) {
+  __shared__ double xs[LB];
+  const int tid = threadIdx.x;
+  if (tid < LB) xs[tid] = b[c0 + tid];
+  __syncthreads();
+  const int q = tid & 7;
+  const int64_t r = (int64_t)blockIdx.x * 32 + (tid >> 3);
+  double s = 0.0;
+  if (r < nr) {
+    const double* row = A + (rlo + r) * ld + c0 + 16 * q;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) {
+      const v2d a = *(const v2d*)(row + c);
+      s += a[0] * xs[16 * q + c] + a[1] * xs[16 * q + c + 1];
+    }
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (r < nr && q == 0) b[rlo + r] -= s;
+}
+
+// ---------------------------------------------------------------------------
+hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
+  if (a->npad >= npad) return hipSuccess;
+  lu_aux_free(a);
+  const int nblk = (int)(npad / LB);
+  std::vector<double> hw(2 * LB);
+  for (int i = 0; i < LB; ++i) {
+    hw[i] = 1.0;
+    hw[LB + i] = -1.0;
+  }
+  // square-shell order: the first t² entries are the t x t leading block
+  std::vector<int2> sq;
+  sq.reserve((size_t)nblk * nblk);
+  for (int s = 0; s < nblk; ++s) {
+    for (int j = 0; j <= s; ++j) sq.push_back(make_int2(s, j));
+    for (int i = 0; i < s; ++i) sq.push_back(make_int2(i, s));
+  }
+  std::vector<int2> row1(nblk);
+  for (int j = 0; j < nblk; ++j) row1[j] = make_int2(0, j);
+  hipError_t e = hipSuccess;
+  auto al = [&](void** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(p, bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(*p, 0, bytes, st);
+  };
+  al((void**)&a->cand, sizeof(double) * 2 * LU_MAXWG);
+  al((void**)&a->candi, sizeof(int) * 2 * LU_MAXWG);
+  al((void**)&a->candrow, sizeof(double) * 2 * LU_MAXWG * LB);
+  al((void**)&a->rowj, sizeof(double) * 2 * LB);
+  al((void**)&a->ipiv, sizeof(int) * npad);
+  al((void**)&a->pairs, sizeof(int2) * (size_t)nblk * LU_MAXPAIRS);
+  al((void**)&a->npairs, sizeof(int) * nblk);
+  al((void**)&a->Linv, sizeof(double) * (size_t)nblk * LB * LB);
+  al((void**)&a->Uinv, sizeof(double) * (size_t)nblk * LB * LB);
+  al((void**)&a->T, sizeof(double) * (size_t)npad * LB);
+  al((void**)&a->UT, sizeof(double) * (size_t)npad * LB);
+  al((void**)&a->w, sizeof(double) * 2 * LB);
+  al((void**)&a->sq, sizeof(int2) * sq.size());
+  al((void**)&a->row1, sizeof(int2) * row1.size());
+  if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(a->sq, sq.data(), sizeof(int2) * sq.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(a->row1, row1.data(), sizeof(int2) * row1.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) a->npad = npad;
+  return e;
+}
+
+void lu_aux_free(LUAux* a) {
+  void* ps[] = {a->cand, a->candi, a->candrow, a->rowj, a->ipiv, a->pairs, a->npairs, a->Linv,
+                a->Uinv, a->T,    a->UT,    a->w,       a->sq,   a->row1};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  *a = LUAux();
+}
+
+hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st) {
+  if (npad % LB != 0 || npad > a->npad || ld < npad) return hipErrorInvalidValue;
+  const int nblk = (int)(npad / LB);
+  if (npad > n)
+    hipLaunchKernelGGL(lu_pad_kernel, dim3((unsigned)ceil_div(npad - n, 256)), dim3(256), 0, st, A, ld, n, npad);
+  for (int k = 0; k < nblk; ++k) {
+    const int64_t r0 = (int64_t)k * LB, c0 = r0, h = npad - r0;
+    const int R = 32 * (int)ceil_div(h, 32 * LU_MAXWG);
+    const int nwg = (int)ceil_div(h, R);
+    for (int j = -1; j < LB; ++j)
+      hipLaunchKernelGGL(lu_panel_step_kernel, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
+                         a->candi, a->candrow, a->rowj, a->ipiv, info);
+    int2* pairs = a->pairs + (int64_t)k * LU_MAXPAIRS;
+    hipLaunchKernelGGL(lu_perm_kernel, dim3(1), dim3(64), 0, st, a->ipiv, (int)r0, pairs, a->npairs + k);
+    hipLaunchKernelGGL(lu_diag_inv_kernel, dim3(2), dim3(256), 0, st, A, ld, r0, a->Linv + (int64_t)k * LB * LB,
+                       a->Uinv + (int64_t)k * LB * LB);
+    const int64_t w = npad - c0 - LB;   // columns right of the panel
+    if (w == 0) break;
+    hipLaunchKernelGGL(lu_swap_cols_kernel, dim3((unsigned)ceil_div(w, SW_COLS)), dim3(256), 0, st, A, ld, c0 + LB, w,
+                       pairs, a->npairs + k);
+    // TRSM: U12 = L11⁻¹ A12 (row-major into A) and U12ᵀ-as-columns into UT
+    hipLaunchKernelGGL(lu_transpose_kernel, dim3((unsigned)ceil_div(w, 64), LB / 64), dim3(256), 0, st, A, ld, r0,
+                       c0 + LB, w, a->T);
+    const int nc = (int)(w / LB);
+    const double* Lk = a->Linv + (int64_t)k * LB * LB;
+    hipError_t e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nc, A + r0 * ld + c0 + LB, ld,
+                                   /*GRAM_UPPER*/ 4, st);
+    if (e == hipSuccess) e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nc, a->UT, LB, 0, st);
+    // A22 -= L21 U12
+    if (e == hipSuccess)
+      e = gram_launch_gen(A + (r0 + LB) * ld + c0, ld, a->UT, LB, a->w + LB, 0, LB, a->sq, nc * nc,
+                          A + (r0 + LB) * ld + c0 + LB, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipGetLastError();
+}
+
+hipError_t lu_solve(const double* A, int64_t ld, int64_t npad, const LUAux* a, double* b, hipStream_t st) {
+  const int nblk = (int)(npad / LB);
+  for (int k = 0; k < nblk; ++k) {
+    const int64_t r0 = (int64_t)k * LB;
+    hipLaunchKernelGGL(lu_fwd_block_kernel, dim3(1), dim3(256), 0, st, a->pairs + (int64_t)k * LU_MAXPAIRS,
+                       a->npairs + k, a->Linv + (int64_t)k * LB * LB, r0, b);
+    const int64_t nr = npad - r0 - LB;
+    if (nr > 0)
+      hipLaunchKernelGGL(lu_rank_update_kernel, dim3((unsigned)ceil_div(nr, 32)), dim3(256), 0, st, A, ld, r0 + LB, nr,
+                         r0, b);
+  }
+  for (int k = nblk - 1; k >= 0; --k) {
+    const int64_t r0 = (int64_t)k * LB;
+    hipLaunchKernelGGL(lu_bwd_block_kernel, dim3(1), dim3(256), 0, st, a->Uinv + (int64_t)k * LB * LB, r0, b);
+    if (r0 > 0)
+      hipLaunchKernelGGL(lu_rank_update_kernel, dim3((unsigned)ceil_div(r0, 32)), dim3(256), 0, st, A, ld, (int64_t)0,
+                         r0, r0, b);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace scs

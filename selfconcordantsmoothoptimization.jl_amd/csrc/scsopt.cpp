@@ -9,8 +9,6 @@
 //   linesearch / inv_BB_step  utils.jl:27-48           -> line_search / bb kernel
 //   get_Mg                    smoothing.jl:12-25        -> get_Mg
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <chrono>
@@ -37,6 +35,7 @@ struct Pending {
   hipEvent_t e0, e1;
 };
 enum { T_GRAM = 0, T_GEMV, T_SOLVE, T_STEP, T_REDUCE, T_N };
+constexpr int ZF_SLOT = 24;   // scal / hscal slot of the deferred f(x) (forward with need_val = false)
 
 struct DevBuf {
   void* p = nullptr;
@@ -57,7 +56,7 @@ struct NView {
   int64_t NpS = 0;
   int2* stiles = nullptr;
   int nstiles = 0;
-  rocblas_int *ipivS = nullptr, *dinfoS = nullptr;
+  int64_t n1pad = 0;     // row stride of Ms: round_up(N + 1, 128) (lu.hip)
   bool sparse = false;   // a batch view is always dense (Matrix(As'), iterate.jl:207)
 };
 
@@ -167,15 +166,13 @@ struct scs_ctx {
   int2* trilist = nullptr;  // row-major lower tiles
   int* cinfo = nullptr;
   CholAux caux;             // two-level factorization constants (chol.hip)
-  rocblas_handle blas = nullptr;
+  LUAux lu;                 // blocked LU (lu.hip): the non-SPD fallback and the GGN sample-space system
   // GGN sample-space branch (N + 1 <= m): Aᵀ copy, sample Gram, (N+1)² system
   double *At = nullptr, *Ps = nullptr, *Ms = nullptr, *bS = nullptr, *uN = nullptr, *hvec = nullptr, *hg = nullptr;
   int64_t NpS = 0;
   int2* stiles = nullptr;
   int nstiles = 0;
-  rocblas_int *ipivS = nullptr, *dinfoS = nullptr;
-  rocblas_int* dinfo = nullptr;
-  rocblas_int* ipiv = nullptr;
+  int64_t n1pad = 0;
   // minibatches (scs_set_batches / scs_select_batch): the collected DataLoader batch list of
   // iterate.jl:141-146 as one device row list; each distinct batch size owns a gathered view
   // (NView) that is swapped in for the steps on that batch
@@ -241,15 +238,6 @@ void set_err(scs_ctx* c, const char* fmt, ...) {
       set_err(c, "HIP error '%s' at %s:%d (%s)", hipGetErrorString(e__), __FILE__, __LINE__, #expr); \
       throw Fail{SCS_ERR_HIP};                                                                         \
     }                                                                                                  \
-  } while (0)
-
-#define RCK(expr)                                                                              \
-  do {                                                                                         \
-    rocblas_status s__ = (expr);                                                               \
-    if (s__ != rocblas_status_success) {                                                       \
-      set_err(c, "rocBLAS/rocSOLVER status %d at %s:%d (%s)", (int)s__, __FILE__, __LINE__, #expr); \
-      throw Fail{SCS_ERR_HIP};                                                                 \
-    }                                                                                          \
   } while (0)
 
 [[noreturn]] void fail(scs_ctx* c, int code, const char* fmt, ...) {
@@ -363,13 +351,20 @@ uint64_t xtag_of(const scs_ctx* c, const double* x) {
     if (t.p && t.p == x) return t.v;
   return 0;
 }
-// cache key (content `key` or tag `ktag`) matches the host vector x
+// cache key (content `key` or tag `ktag`) matches the host vector x; x = nullptr: a device-only
+// vector (a line-search trial point) that never hits and is keyed by a fresh tag
 bool key_hit(const scs_ctx* c, const std::vector<double>& key, uint64_t ktag, const double* x) {
+  if (!x) return false;
   const uint64_t t = xtag_of(c, x);
   if (t) return ktag == t;
   return ktag == 0 && same_x(key, x, c->m);
 }
-void key_set(const scs_ctx* c, std::vector<double>& key, uint64_t& ktag, const double* x) {
+void key_set(scs_ctx* c, std::vector<double>& key, uint64_t& ktag, const double* x) {
+  if (!x) {
+    key.clear();
+    ktag = c->xtag_next++;
+    return;
+  }
   ktag = xtag_of(c, x);
   if (ktag)
     key.clear();
@@ -425,6 +420,8 @@ void alloc_mspace(scs_ctx* c) {
     dfree_t(c, *v);
     *v = dalloc<double>(c, mp);
   }
+  dfree_t(c, c->cinfo);
+  c->cinfo = dalloc<int>(c, 1);   // factorization info (Cholesky pivot check, LU zero pivot, NaN scan)
   dfree_t(c, c->scal);
   c->scal = dalloc<double>(c, 64 + 3 * 256);   // scalars + the multi-workgroup tail / get_reg partials
   if (!c->hscal) HCK(hipHostMalloc((void**)&c->hscal, 64 * sizeof(double), hipHostMallocDefault));
@@ -508,16 +505,14 @@ void ensure_gram(scs_ctx* c) {
     gram_tile_list_rowmajor(nb2, tr.data());
     c->trilist = dalloc<int2>(c, tr.size());
     HCK(hipMemcpyAsync(c->trilist, tr.data(), sizeof(int2) * tr.size(), hipMemcpyHostToDevice, c->st));
-    c->cinfo = dalloc<int>(c, 1);
     HCK(chol_aux_init(&c->caux, mp, c->st));
   }
-  c->dinfo = dalloc<rocblas_int>(c, 1);
-  c->ipiv = dalloc<rocblas_int>(c, mp);
   sync(c);
 }
 
 void invalidate_caches(scs_ctx* c) {
   c->zvalid = false;
+  c->zf_pending = false;
   c->gvalid[0] = c->gvalid[1] = false;
 }
 
@@ -548,8 +543,7 @@ void swap_view(scs_ctx* c, NView& v) {
   std::swap(c->NpS, v.NpS);
   std::swap(c->stiles, v.stiles);
   std::swap(c->nstiles, v.nstiles);
-  std::swap(c->ipivS, v.ipivS);
-  std::swap(c->dinfoS, v.dinfoS);
+  std::swap(c->n1pad, v.n1pad);
 }
 
 void free_view(scs_ctx* c, NView& v) {
@@ -557,8 +551,6 @@ void free_view(scs_ctx* c, NView& v) {
                      &v.Ms, &v.bS, &v.uN, &v.hvec, &v.hg})
     dfree_t(c, *p);
   dfree_t(c, v.stiles);
-  dfree_t(c, v.ipivS);
-  dfree_t(c, v.dinfoS);
   v = NView();
 }
 
@@ -684,13 +676,14 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags, bool n
     flags |= EPI_Z | EPI_VAL;
     HCK(launch_epilogue(c->loss, c->ggn, flags, c->zpart, ns, c->Npad, c->y, c->N, c->Npad, c->scale, c->z,
                         c->gN, c->hN, c->wN, c->vN, c->valpart, c->st));
-    // loss sum -> scal[8] (reduce buffer slot 0 in multi-rank)
-    double* dst = (c->nranks > 1) ? c->red : c->scal + 8;
+    // loss sum -> scal[ZF_SLOT] (reduce buffer slot 0 in multi-rank); a slot of its own: the value
+    // stays in flight until the next use (no host round trip when the caller only needs z)
+    double* dst = (c->nranks > 1) ? c->red : c->scal + ZF_SLOT;
     HCK(launch_sum_partials(c->valpart, c->nval, dst, c->st));
     allreduce(c, c->red, 1);
-    if (c->nranks > 1) HCK(hipMemcpyAsync(c->scal + 8, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
-    d2h(c, c->hscal + 8, c->scal + 8, 1);
-    c->zf_pending = true;   // read at the next use: no host round trip when the caller only needs z
+    if (c->nranks > 1) HCK(hipMemcpyAsync(c->scal + ZF_SLOT, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+    d2h(c, c->hscal + ZF_SLOT, c->scal + ZF_SLOT, 1);
+    c->zf_pending = true;
     key_set(c, c->zkey, c->ztag, xh);
     c->zvalid = true;
   } else if (flags & ~(EPI_VAL | EPI_Z)) {
@@ -700,7 +693,7 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags, bool n
   }
   if (need_val && c->zf_pending) {
     sync(c);
-    c->zfval = loss_scale_value(c, c->hscal[8]);
+    c->zfval = loss_scale_value(c, c->hscal[ZF_SLOT]);
     c->zf_pending = false;
   }
   return c->zfval;
@@ -800,15 +793,11 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
   d2h(c, c->hscal + 11, c->scal + 11, 1);
   sync(c);
   const double gd = c->hscal[11];
-  std::vector<double> xt(c->m);
   double alpha = 1.0;
   for (int trial = 0; trial < 100000; ++trial) {
-    HCK(launch_trial_point(xd, dd, alpha, c->m, c->zb, c->st));
-    d2h(c, xt.data(), c->zb, c->m);
-    sync(c);
-    // trial point evaluated at a scratch copy (keeps xd / caches intact)
-    HCK(hipMemcpyAsync(c->gtmp2, c->zb, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
-    const double ft = eval_f_dev(c, xt.data(), c->gtmp2) + eval_reg_dev(c, c->gtmp2);
+    // the trial point lives on the device only (no host copy: it is keyed by a fresh tag)
+    HCK(launch_trial_point(xd, dd, alpha, c->m, c->gtmp2, c->st));
+    const double ft = eval_f_dev(c, nullptr, c->gtmp2) + eval_reg_dev(c, c->gtmp2);
     if (!(ft > f0 + 1e-4 * alpha * gd)) return alpha;
     alpha = 0.5 * alpha;
   }
@@ -816,58 +805,55 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
 }
 
 // solve (G + λ diag Hr) sol = rhs in place (rhs -> sol, length m_pad, zero-padded).
-// Hand-written blocked Cholesky on MFMA (chol.hip) first; LU with partial
-// pivoting (the reference's `\`, prox-N-SCORE.jl:204) from the saved copy when
+// Hand-written blocked Cholesky on MFMA (chol.hip) first; the hand-written blocked LU with
+// partial pivoting (lu.hip; the reference's `\`, prox-N-SCORE.jl:70) from the saved copy when
 // a pivot is not positive (e.g. the indefinite Q of a CE loss on ±1 labels,
-// test/test_algs.jl:10).
-void ensure_blas(scs_ctx* c) {
-  if (c->blas) return;
-  RCK(rocblas_create_handle(&c->blas));
-  RCK(rocblas_set_stream(c->blas, c->st));
-}
-
-void solve_system(scs_ctx* c, double* rhs) {
+// test/test_algs.jl:10), or always with force_lu (scs_solve_eval).
+void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
   const int64_t m = c->m, ld = c->mpad;
   hipEvent_t e0;
   tbegin(c, T_SOLVE, &e0);
   // the LU fallback needs the system the in-place factor destroys: copied up front, or -- when
   // this step's Gram came from the cache -- rebuilt from it only if the factor fails
   if (!c->g_from_cache) HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
-  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
-  HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
   int info = 0;
-  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
-  sync(c);
-  if (info == 0) {
-    HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, c->st));
-    c->lu_fallback_used = false;
-  } else {
-    ensure_blas(c);
-    if (c->g_from_cache) {
-      HCK(hipMemcpyAsync(c->Gc, c->Gk, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
-      HCK(launch_diag_add(c->Gc, c->mpad, m, c->lam, c->Hr, c->st));
-    }
-    HCK(launch_symmetrize(c->Gc, ld, m, c->st));
-    // a NaN / Inf in the system (a smoother's NaN, Appendix A) is no SingularException in the
-    // reference: LAPACK getrf only flags exact zero pivots, and the solve comes out NaN
+  if (!force_lu) {
     HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
-    HCK(launch_nonfinite(c->Gc, ld, m, rhs, c->cinfo, c->st));
+    HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
     HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
     sync(c);
-    if (info != 0) {
-      HCK(launch_fill(rhs, m, std::numeric_limits<double>::quiet_NaN(), c->st));
-      c->lu_fallback_used = true;
+    if (info == 0) {
+      HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, c->st));
+      c->lu_fallback_used = false;
       tend(c, T_SOLVE, e0);
       return;
     }
-    RCK(rocsolver_dgetrf(c->blas, (rocblas_int)m, (rocblas_int)m, c->Gc, (rocblas_int)ld, c->ipiv, c->dinfo));
-    HCK(hipMemcpyAsync(&info, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
-    sync(c);
-    if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
-    RCK(rocsolver_dgetrs(c->blas, rocblas_operation_none, (rocblas_int)m, 1, c->Gc, (rocblas_int)ld, c->ipiv, rhs,
-                         (rocblas_int)m));
-    c->lu_fallback_used = true;
   }
+  if (c->g_from_cache) {
+    HCK(hipMemcpyAsync(c->Gc, c->Gk, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+    HCK(launch_diag_add(c->Gc, c->mpad, m, c->lam, c->Hr, c->st));
+  }
+  // the full symmetric matrix: its column-major storage is also the row-major one lu.hip factors
+  HCK(launch_symmetrize(c->Gc, ld, m, c->st));
+  // a NaN / Inf in the system (a smoother's NaN, Appendix A) is no SingularException in the
+  // reference: LAPACK getrf only flags exact zero pivots, and the solve comes out NaN
+  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+  HCK(launch_nonfinite(c->Gc, ld, m, rhs, c->cinfo, c->st));
+  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  c->lu_fallback_used = true;
+  if (info != 0) {
+    HCK(launch_fill(rhs, m, std::numeric_limits<double>::quiet_NaN(), c->st));
+    tend(c, T_SOLVE, e0);
+    return;
+  }
+  HCK(lu_aux_init(&c->lu, ld, c->st));
+  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+  HCK(lu_factor(c->Gc, ld, m, ld, &c->lu, c->cinfo, c->st));
+  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
+  HCK(lu_solve(c->Gc, ld, ld, &c->lu, rhs, c->st));
   tend(c, T_SOLVE, e0);
 }
 
@@ -1031,20 +1017,18 @@ void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
 void ggn_sample_direction(scs_ctx* c, const double* xh) {
   const int64_t N = c->N, m = c->m;
   if (c->nranks > 1) return ggn_sample_direction_sharded(c, xh);
-  ensure_blas(c);
   if (!c->At) {
     const double* A = dense_A(c);
     c->NpS = round_up(N, 128);
     c->At = dalloc<double>(c, (size_t)c->NpS * c->mpad);
     HCK(launch_transpose(A, c->Npad, N, m, c->At, c->mpad, c->NpS, c->st));
     c->Ps = dalloc<double>(c, (size_t)c->NpS * c->NpS);
-    c->Ms = dalloc<double>(c, (size_t)(N + 1) * (N + 1));
-    c->bS = dalloc<double>(c, N + 1);
+    c->n1pad = round_up(N + 1, 128);   // row-major, zero padding (lu.hip)
+    c->Ms = dalloc<double>(c, (size_t)c->n1pad * c->n1pad);
+    c->bS = dalloc<double>(c, c->n1pad);
     c->uN = dalloc<double>(c, c->Npad);
     c->hvec = dalloc<double>(c, c->mpad);
     c->hg = dalloc<double>(c, c->mpad);
-    c->ipivS = dalloc<rocblas_int>(c, N + 1);
-    c->dinfoS = dalloc<rocblas_int>(c, 1);
     const int nb = (int)(c->NpS / 128);
     std::vector<int2> tl((size_t)nb * (nb + 1) / 2);
     int nt = 0;
@@ -1065,23 +1049,25 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
   const int ns = matvec_n(c, c->hg, c->nsplit);   // u = A (h∘λgr)
   HCK(launch_epilogue(SCS_LOSS_LEAST_SQUARES, SCS_GGN_NONE, EPI_Z, c->zpart, ns, c->Npad, c->y, N, c->Npad, 1.0,
                       c->uN, nullptr, nullptr, nullptr, nullptr, c->valpart, c->st));
-  HCK(launch_ggn_sample_assemble(c->Ps, c->NpS, c->gN, c->hN, c->wN, c->uN, nullptr, N, c->Ms, c->bS, c->st));
+  HCK(launch_ggn_sample_assemble(c->Ps, c->NpS, c->gN, c->hN, c->wN, c->uN, nullptr, N, c->Ms, c->n1pad, c->bS,
+                                      c->st));
   tbegin(c, T_SOLVE, &e0);
-  const rocblas_int n1 = (rocblas_int)(N + 1);
+  const int64_t n1 = N + 1, np1 = c->n1pad;
   int info = 0;
   // NaN / Inf in the system: the reference's qr(...) \ b comes out NaN (no SingularException)
-  HCK(hipMemsetAsync(c->dinfoS, 0, sizeof(int), c->st));
-  HCK(launch_nonfinite(c->Ms, n1, n1, c->bS, c->dinfoS, c->st));
-  HCK(hipMemcpyAsync(&info, c->dinfoS, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+  HCK(launch_nonfinite(c->Ms, np1, n1, c->bS, c->cinfo, c->st));
+  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
   if (info != 0) {
     HCK(launch_fill(c->bS, n1, std::numeric_limits<double>::quiet_NaN(), c->st));
   } else {
-    RCK(rocsolver_dgetrf(c->blas, n1, n1, c->Ms, n1, c->ipivS, c->dinfoS));
-    HCK(hipMemcpyAsync(&info, c->dinfoS, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    HCK(lu_aux_init(&c->lu, np1, c->st));
+    HCK(lu_factor(c->Ms, np1, n1, np1, &c->lu, c->cinfo, c->st));
+    HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
     sync(c);
     if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
-    RCK(rocsolver_dgetrs(c->blas, rocblas_operation_none, n1, 1, c->Ms, n1, c->ipivS, c->bS, n1));
+    HCK(lu_solve(c->Ms, np1, np1, &c->lu, c->bS, c->st));
   }
   tend(c, T_SOLVE, e0);
   HCK(launch_ggn_sample_scale(c->gN, c->bS, N, c->Npad, c->vN, c->st));
@@ -1249,7 +1235,7 @@ int scs_destroy(scs_ctx* c) {
   }
   for (auto& a : c->allocs) (void)hipFree(a.p);
   if (c->hscal) (void)hipHostFree(c->hscal);
-  if (c->blas) (void)rocblas_destroy_handle(c->blas);
+  lu_aux_free(&c->lu);
   if (c->own_stream) (void)hipStreamDestroy(c->st);
   delete c;
   return SCS_OK;
@@ -1330,8 +1316,7 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->utiles);
   for (double** v : {&c->At, &c->Ps, &c->Ms, &c->bS, &c->uN, &c->hvec, &c->hg}) dfree_t(c, *v);
   dfree_t(c, c->stiles);
-  dfree_t(c, c->ipivS);
-  dfree_t(c, c->dinfoS);
+  c->n1pad = 0;
   c->NpS = 0;
   c->nstiles = 0;
   dfree_t(c, c->gwork);
@@ -1348,8 +1333,6 @@ static void reset_data(scs_ctx* c) {
   clear_batches(c);
   free_view(c, c->gview);
   c->gview_ok = false;
-  dfree_t(c, c->dinfo);
-  dfree_t(c, c->ipiv);
   c->ntiles = c->nslots = 0;
   invalidate_caches(c);
   c->has_data = false;
@@ -2133,6 +2116,133 @@ int scs_gram_eval(scs_ctx* c, const double* w, double* G, int64_t ldg) {
     HCK(hipMemcpy2DAsync(G, sizeof(double) * ldg, c->G, sizeof(double) * c->mpad, sizeof(double) * c->m, c->m,
                          hipMemcpyDeviceToHost, c->st));
     sync(c);
+    if (c->timing) tresolve(c);
+  });
+}
+
+// The m x m system of ProxNSCORE / ProxGGNSCORE from given weights: (Aᵀ diag(w) A + diag(dvec)) x = rhs,
+// through the production path (Gram, then solve_system: Cholesky with the LU fallback, or the LU
+// alone with mode 1).  G is the step's scratch, so nothing else changes.
+int scs_solve_eval(scs_ctx* c, const double* w, const double* dvec, const double* rhs, int mode, double* x,
+                   int* used_lu) {
+  return guarded(c, [&] {
+    if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    if (c->nranks > 1) fail(c, SCS_ERR_ARG, "scs_solve_eval runs on one rank");
+    if (!w || !dvec || !rhs || !x) fail(c, SCS_ERR_ARG, "scs_solve_eval: null argument");
+    HCK(hipSetDevice(c->dev));
+    std::vector<double> wp(c->Npad, 0.0), v(c->mpad, 0.0);
+    std::memcpy(wp.data(), w, sizeof(double) * c->N);
+    h2d(c, c->wN, wp.data(), c->Npad);
+    ensure_gram(c);
+    hipEvent_t e0;
+    tbegin(c, T_GRAM, &e0);
+    gram_main(c, c->wN, c->G, 0);
+    tend(c, T_GRAM, e0);
+    std::memcpy(v.data(), dvec, sizeof(double) * c->m);
+    h2d(c, c->gtmp2, v.data(), c->mpad);
+    HCK(launch_diag_add(c->G, c->mpad, c->m, 1.0, c->gtmp2, c->st));
+    std::memcpy(v.data(), rhs, sizeof(double) * c->m);
+    h2d(c, c->gq, v.data(), c->mpad);
+    sync(c);
+    c->g_from_cache = false;
+    solve_system(c, c->gq, mode == 1);
+    d2h(c, x, c->gq, c->m);
+    sync(c);
+    if (used_lu) *used_lu = c->lu_fallback_used ? 1 : 0;
+    invalidate_caches(c);
+    if (c->timing) tresolve(c);
+  });
+}
+
+// A x = b for a host row-major n x n A by the hand-written LU (getrf + getrs semantics); ipiv
+// (0-based, LAPACK order) and info (first zero pivot, 1-based) as dgetrf reports them.  Needs a
+// context only (no data).
+int scs_lu_eval(scs_ctx* c, int64_t n, const double* A, const double* b, double* x, int32_t* ipiv, int* info) {
+  return guarded(c, [&] {
+    if (n < 1 || !A || !b || !x) fail(c, SCS_ERR_ARG, "scs_lu_eval: bad arguments");
+    HCK(hipSetDevice(c->dev));
+    const int64_t np = round_up(n, 128);
+    double* M = dalloc<double>(c, (size_t)np * np);
+    double* bb = dalloc<double>(c, np);
+    int* dinfo = dalloc<int>(c, 1);
+    HCK(hipMemcpy2DAsync(M, sizeof(double) * np, A, sizeof(double) * n, sizeof(double) * n, n, hipMemcpyHostToDevice,
+                         c->st));
+    HCK(hipMemcpyAsync(bb, b, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    HCK(lu_aux_init(&c->lu, np, c->st));
+    hipEvent_t e0;
+    tbegin(c, T_SOLVE, &e0);
+    HCK(lu_factor(M, np, n, np, &c->lu, dinfo, c->st));
+    int hinfo = 0;
+    HCK(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    if (hinfo == 0) HCK(lu_solve(M, np, np, &c->lu, bb, c->st));
+    tend(c, T_SOLVE, e0);
+    HCK(hipMemcpyAsync(x, bb, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
+    if (ipiv) HCK(hipMemcpyAsync(ipiv, c->lu.ipiv, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    if (info) *info = hinfo;
+    dfree_t(c, M);
+    dfree_t(c, bb);
+    dfree_t(c, dinfo);
+    if (c->timing) tresolve(c);
+  });
+}
+
+// Columns cols[0..ncols) of the local A, column-major N x ncols (ld = N).
+int scs_get_columns(scs_ctx* c, const int64_t* cols, int64_t ncols, double* out) {
+  return guarded(c, [&] {
+    if (!c->has_data || c->generic || c->sparse) fail(c, SCS_ERR_STATE, "scs_get_columns needs a dense A");
+    for (int64_t k = 0; k < ncols; ++k)
+      if (cols[k] < 0 || cols[k] >= c->m) fail(c, SCS_ERR_ARG, "column %lld out of range", (long long)cols[k]);
+    HCK(hipSetDevice(c->dev));
+    int64_t* dc = dalloc<int64_t>(c, ncols);
+    double* dout = dalloc<double>(c, (size_t)ncols * c->N);
+    HCK(hipMemcpyAsync(dc, cols, sizeof(int64_t) * ncols, hipMemcpyHostToDevice, c->st));
+    HCK(launch_get_columns(c->A, c->nstage, dc, ncols, c->N, dout, c->st));
+    HCK(hipMemcpyAsync(out, dout, sizeof(double) * ncols * c->N, hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    dfree_t(c, dc);
+    dfree_t(c, dout);
+  });
+}
+
+// The production Gram launch with weights w and -- where the step fuses it (256 x 128 tiles) --
+// Aᵀv in the same pass: entries G(i_k, j_k) (ij = n pairs, 0-based) and Aᵀv (m) to the host.
+int scs_gram_atv_eval(scs_ctx* c, const double* w, const double* v, const int64_t* ij, int64_t n, double* gvals,
+                      double* atv, int* fused) {
+  return guarded(c, [&] {
+    if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
+    if (n < 0 || (n > 0 && (!ij || !gvals))) fail(c, SCS_ERR_ARG, "scs_gram_atv_eval: bad sample list");
+    HCK(hipSetDevice(c->dev));
+    std::vector<double> wp(c->Npad, 0.0);
+    std::memcpy(wp.data(), w, sizeof(double) * c->N);
+    h2d(c, c->wN, wp.data(), c->Npad);
+    std::memcpy(wp.data(), v, sizeof(double) * c->N);
+    h2d(c, c->vN, wp.data(), c->Npad);
+    ensure_gram(c);
+    const bool fuse = gram_fuse_ok(c->tall) != 0;
+    hipEvent_t e0;
+    tbegin(c, T_GRAM, &e0);
+    gram_main(c, c->wN, c->G, 0, fuse ? c->vN : nullptr, c->gtmp);
+    tend(c, T_GRAM, e0);
+    if (!fuse) gemv_t_local(c, c->vN, c->gtmp);
+    std::vector<int2> hij((size_t)std::max<int64_t>(n, 1));
+    for (int64_t k = 0; k < n; ++k) {
+      const int64_t i = ij[2 * k], j = ij[2 * k + 1];
+      if (i < 0 || j < 0 || i >= c->m || j >= c->m) fail(c, SCS_ERR_ARG, "sample %lld out of range", (long long)k);
+      hij[k] = make_int2((int)std::min(i, j), (int)std::max(i, j));   // the upper triangle holds G
+    }
+    int2* dij = dalloc<int2>(c, hij.size());
+    double* dv = dalloc<double>(c, hij.size());
+    HCK(hipMemcpyAsync(dij, hij.data(), sizeof(int2) * n, hipMemcpyHostToDevice, c->st));
+    HCK(launch_gather_entries(c->G, c->mpad, dij, (int)n, dv, c->st));
+    if (n > 0) d2h(c, gvals, dv, n);
+    if (atv) d2h(c, atv, c->gtmp, c->m);
+    sync(c);
+    dfree_t(c, dij);
+    dfree_t(c, dv);
+    if (fused) *fused = fuse ? 1 : 0;
+    invalidate_caches(c);
     if (c->timing) tresolve(c);
   });
 }

@@ -615,17 +615,17 @@ __global__ void ggn_sample_prep_kernel(const double* __restrict__ Hr, const doub
 __global__ void ggn_sample_assemble_kernel(const double* __restrict__ P, int64_t ldp, const double* __restrict__ s,
                                            const double* __restrict__ q, const double* __restrict__ r,
                                            const double* __restrict__ u, const double* __restrict__ kNN, int64_t N,
-                                           double* __restrict__ M, double* __restrict__ b) {
-  const int64_t ld = N + 1;
-  const int64_t j = blockIdx.y;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ld; i += (int64_t)gridDim.x * blockDim.x) {
+                                           double* __restrict__ M, int64_t ldm, double* __restrict__ b) {
+  // M row-major (the LU's layout, lu.hip), row i = blockIdx.y; P is symmetric (P_ij = P_ji bitwise)
+  const int64_t i = blockIdx.y;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j <= N; j += (int64_t)gridDim.x * blockDim.x) {
     double v;
     if (i == N) v = (j == N) ? 1.0 : 0.0;
-    else if (j < N) v = (i == j ? 1.0 : 0.0) + q[i] * (s[i] * s[j] * P[j * ldp + i]);
+    else if (j < N) v = (i == j ? 1.0 : 0.0) + q[i] * (s[i] * s[j] * P[i * ldp + j]);
     else v = q[i] * (s[i] * u[i]);
-    M[j * ld + i] = v;
-    if (j == 0) b[i] = (i < N) ? r[i] : 1.0;
+    M[i * ldm + j] = v;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) b[i] = (i < N) ? r[i] : 1.0;
   (void)kNN;   // Q̃[N][N] = 0: the λgr·H⁻¹·λgr entry only reaches M through a zero row
 }
 
@@ -650,9 +650,9 @@ hipError_t launch_ggn_sample_prep(const double* Hr, const double* gr, double lam
 }
 hipError_t launch_ggn_sample_assemble(const double* P, int64_t ldp, const double* s, const double* q,
                                       const double* r, const double* u, const double* kNN, int64_t N, double* M,
-                                      double* b, hipStream_t st) {
+                                      int64_t ldm, double* b, hipStream_t st) {
   hipLaunchKernelGGL(ggn_sample_assemble_kernel, dim3((unsigned)ceil_div(N + 1, 256), (unsigned)(N + 1)), dim3(256),
-                     0, st, P, ldp, s, q, r, u, kNN, N, M, b);
+                     0, st, P, ldp, s, q, r, u, kNN, N, M, ldm, b);
   return hipGetLastError();
 }
 hipError_t launch_ggn_sample_scale(const double* s, const double* B, int64_t N, int64_t Npad, double* v,

@@ -10,7 +10,7 @@ module SCSOptAMD
 
 using Random
 using SelfConcordantSmoothOptimization
-import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel
+import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel, is_interval_set
 
 export DeviceProblem, configure!, iterate_device!, set_gram_cache!
 
@@ -82,7 +82,7 @@ function configure!(model::DeviceProblem, reg_name::String, hμ)
     lb = ub = Float64[]; nb = 0
     ind = Int64[]; ng = 0
     if reg_name == "indbox"
-        lb = Float64.(vcat(model.C_set[1])); ub = Float64.(vcat(model.C_set[2])); nb = length(lb)
+        lb, ub = cset_bounds(model.C_set); nb = length(lb)
     elseif reg_name == "gl"
         ind = Int64.(vec(model.P.ind)); ng = size(model.P.ind, 2)     # column-major 3 x G, 1-based
     end
@@ -94,7 +94,7 @@ function configure!(model::DeviceProblem, reg_name::String, hμ)
         chk(ccall((:scs_set_group_map, lib), Cint, (Ptr{Cvoid}, Ptr{Int64}, Int64), model.ctx, G, length(G)),
             model.ctx)
     end
-    kind, slb, sub = smoother_kind(hμ)
+    kind, slb, sub = smoother_kind(hμ, model)
     chk(ccall((:scs_set_smoother, lib), Cint,
               (Ptr{Cvoid}, Cint, Float64, Float64, Float64, Ptr{Float64}, Ptr{Float64}, Int64),
               model.ctx, kind, hμ.μ, hμ.Mh, hμ.ν, slb, sub, length(slb)), model.ctx)
@@ -103,15 +103,39 @@ function configure!(model::DeviceProblem, reg_name::String, hμ)
     return model
 end
 
-# smoother struct -> (kind, lb, ub); the IndBox smoothers' bounds live in their closures,
-# so callers pass them through `hμ.lb/hμ.ub` when wrapping (PHuberSmootherIndBox(lb, ub, μ)).
-function smoother_kind(hμ)
+# C_set -> (lb, ub) exactly as prox_step(::scaled_proximal_indbox) reads it
+# (prox-operators.jl:34-46): an interval, a tuple of intervals, or a (lb, ub) pair / vector.
+function cset_bounds(C_set)
+    C_set === nothing && error("indbox needs model.C_set")
+    if is_interval_set(C_set)
+        lb, ub = C_set isa Tuple ? ([minimum.(C_set)...], [maximum.(C_set)...]) : (minimum(C_set), maximum(C_set))
+    else
+        lb, ub = C_set[1], C_set[2]
+    end
+    return Float64.(vcat(lb)), Float64.(vcat(ub))
+end
+
+# The IndBox smoothers keep their bounds only in the closures they build
+# (phuber-smooth.jl:59-65, exponential-smooth.jl:28-34, log-exp-smooth.jl:28-34:
+# `grad = (Cmat,x) -> huber_grad_indbox(x; μ=mu, lb=lb, ub=ub)`), so the captured `lb` / `ub`
+# are read off the closure object (a closure's captures are its fields); model.C_set is the
+# fallback for a hand-built smoother whose closure captured other names.
+function indbox_bounds(hμ, model)
+    g = hμ.grad
+    if hasfield(typeof(g), :lb) && hasfield(typeof(g), :ub)
+        return Float64.(vcat(getfield(g, :lb))), Float64.(vcat(getfield(g, :ub)))
+    end
+    return cset_bounds(model.C_set)
+end
+
+# smoother struct -> (kind, lb, ub)
+function smoother_kind(hμ, model)
     T = typeof(hμ)
     T <: PHuberSmootherL1L2 && return (1, Float64[], Float64[])
-    T <: PHuberSmootherIndBox && return (2, Float64.(vcat(hμ.lb)), Float64.(vcat(hμ.ub)))
+    T <: PHuberSmootherIndBox && return (2, indbox_bounds(hμ, model)...)
     T <: PHuberSmootherGL && return (3, Float64[], Float64[])
-    T <: ExponentialSmootherIndBox && return (4, Float64.(vcat(hμ.lb)), Float64.(vcat(hμ.ub)))
-    T <: LogExpSmootherIndBox && return (5, Float64.(vcat(hμ.lb)), Float64.(vcat(hμ.ub)))
+    T <: ExponentialSmootherIndBox && return (4, indbox_bounds(hμ, model)...)
+    T <: LogExpSmootherIndBox && return (5, indbox_bounds(hμ, model)...)
     T <: OsBaSmootherL1L2 && return (6, Float64[], Float64[])
     T <: OsBaSmootherGL && return (7, Float64[], Float64[])
     error("smoother $(T) has no device implementation")

@@ -12,7 +12,7 @@ from . import _lib, losses, shard
 from ._lib import ScsError, ScsReferenceError, version
 from .iterate import Solution, iterate, optim_loop, step
 from .methods import ProximalMethod, ProxGGNSCORE, ProxLQNSCORE, ProxNSCORE
-from .problems import Problem, get_P
+from .problems import Problem, get_P, lu_solve
 from .smoothers import (ExponentialSmootherIndBox, LogExpSmootherIndBox, OsBaSmootherGL, OsBaSmootherL1L2,
                         PHuberSmootherGL, PHuberSmootherIndBox, PHuberSmootherL1L2, Smoother)
 

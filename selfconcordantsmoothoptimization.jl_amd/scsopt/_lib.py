@@ -28,8 +28,8 @@ METHOD = {"nscore": 1, "ggnscore": 2, "lqnscore": 3}
 # names ("libamdhip64.so") differ from the SONAMEs ("libamdhip64.so.7"), so if
 # libscsopt pulled /opt/rocm's copies in first, importing torch afterwards would
 # load a second runtime and crash.  Importing torch first makes libscsopt's
-# NEEDED entries resolve to the already-loaded (torch-bundled) runtime, rocBLAS
-# and rocSOLVER.  torch is plumbing only (streams, torch.distributed).
+# NEEDED entries resolve to the already-loaded (torch-bundled) HIP runtime.  torch is
+# plumbing only (streams, torch.distributed).
 import torch  # noqa: E402,F401  (must precede the CDLL below)
 
 if not os.path.exists(LIB_PATH):
@@ -103,6 +103,10 @@ _SIGS = {
     "scs_gram_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64]),
     "scs_gemv_t_eval": (C.c_int, [C.c_void_p, c_dp, c_dp]),
     "scs_gemv_n_eval": (C.c_int, [C.c_void_p, c_dp, c_dp]),
+    "scs_solve_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, c_dp, C.c_int, c_dp, C.POINTER(C.c_int)]),
+    "scs_lu_eval": (C.c_int, [C.c_void_p, C.c_int64, c_dp, c_dp, c_dp, c_i32p, C.POINTER(C.c_int)]),
+    "scs_get_columns": (C.c_int, [C.c_void_p, c_i64p, C.c_int64, c_dp]),
+    "scs_gram_atv_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, c_i64p, C.c_int64, c_dp, c_dp, C.POINTER(C.c_int)]),
     "scs_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_timing_get": (C.c_int, [C.c_void_p, C.POINTER(Timing)]),
     "scs_timing_reset": (C.c_int, [C.c_void_p]),

@@ -316,3 +316,53 @@ class Problem:
         out = np.empty(self.N)
         self.ctx.check(_lib.lib.scs_gemv_n_eval(self.ctx.h, dptr(x), dptr(out)))
         return out
+
+    def solve_eval(self, w, dvec, rhs, mode=0):
+        """(Aᵀ diag(w) A + diag(dvec)) \\ rhs through the step's solve path (mode 0: Cholesky with
+        the LU fallback; 1: the LU).  Returns (x, used_lu)."""
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        dvec = np.ascontiguousarray(dvec, dtype=np.float64)
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64)
+        x = np.empty(self.m)
+        used = C.c_int()
+        self.ctx.check(_lib.lib.scs_solve_eval(self.ctx.h, dptr(w), dptr(dvec), dptr(rhs), int(mode), dptr(x),
+                                               C.byref(used)))
+        return x, bool(used.value)
+
+    def get_columns(self, cols):
+        """Columns of the local A (N x len(cols), float64)."""
+        cols = np.ascontiguousarray(cols, dtype=np.int64)
+        out = np.empty((cols.size, self.N))
+        self.ctx.check(_lib.lib.scs_get_columns(self.ctx.h, cols.ctypes.data_as(_lib.c_i64p), cols.size, dptr(out)))
+        return out.T
+
+    def gram_atv_sample(self, w, v, pairs):
+        """The production Gram launch (Aᵀv fused where a step fuses it): G entries at pairs (k x 2),
+        Aᵀv, and whether the pass was fused."""
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        ij = np.ascontiguousarray(np.asarray(pairs, dtype=np.int64).reshape(-1, 2))
+        g = np.empty(ij.shape[0])
+        atv = np.empty(self.m)
+        fused = C.c_int()
+        self.ctx.check(_lib.lib.scs_gram_atv_eval(self.ctx.h, dptr(w), dptr(v), ij.ctypes.data_as(_lib.c_i64p),
+                                                  ij.shape[0], dptr(g), dptr(atv), C.byref(fused)))
+        return g, atv, bool(fused.value)
+
+
+def lu_solve(A, b, device=0, ctx=None):
+    """Julia's `A \\ b` for a dense square matrix (getrf + getrs) on the device: the hand-written
+    blocked LU with partial pivoting (lu.hip).  Returns (x, ipiv (0-based), info)."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
+    n = A.shape[0]
+    if A.shape != (n, n) or b.shape != (n,):
+        raise ValueError("A must be n x n and b of length n")
+    ctx = ctx or _lib.Context(device)
+    x = np.zeros(n)
+    ipiv = np.zeros(n, dtype=np.int32)
+    info = C.c_int()
+    ctx.check(_lib.lib.scs_lu_eval(ctx.h, n, dptr(A), dptr(b), dptr(x), ipiv.ctypes.data_as(_lib.c_i32p),
+                                   C.byref(info)))
+    return x, ipiv, int(info.value)
+

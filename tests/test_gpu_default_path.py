@@ -1,0 +1,135 @@
+"""Parity at the shapes the headline numbers are quoted on, with NO env overrides.
+
+The other GPU tests force each kernel variant at small sizes (SCS_GRAM_TALL=1, SCS_GRAM_FUSE=2,
+m <= 3200 ...).  These run the library's default choices at the BASELINE shapes (SURVEY.md §8:
+C2 m = 8192, C3 m = 16384, C4 m = 32768, C5 m = 65536), against the oracle:
+
+  * C3 shape: ProxGGNSCORE logistic + l1, m = 16384, N = 20480 (N + 1 > m: the feature branch):
+    256 x 128 Gram tiles with the Aᵀv fused into the Gram pass, the tail-balanced K-split
+    schedule, the 256-workgroup SCORE tail (m >= 16384) and the two-level Cholesky (128 inner
+    blocks = 16 outer blocks of 8) with its second-stream lookahead -- 3 epochs at rtol 1e-8;
+  * C2 shape: ProxNSCORE logistic (margin) + l1, m = 8192 (128 x 128 tiles, 8 outer blocks);
+  * C4 shape: the m = 32768 Cholesky solve (256 inner blocks) by its backward error, with the
+    residual formed by the independent streaming GEMV kernels; the m = 32768 LU likewise;
+  * C5 shape: ProxLQNSCORE(mem 20) box least squares on a sparse A with m = 65536 (4 LDS column
+    blocks of the CSR product, the multi-workgroup two-loop / tail / L-BFGS update) and
+    N = 2^17 (8 row blocks of the CSC product), 10 epochs at rtol 1e-8.
+
+The oracle runs its literal restatement except for FAST_LINALG (dsyrk Gram, LU in place of the
+QR: the same systems, equal to O(cond·eps) -- oracle/scsopt_oracle.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import scsopt
+import scsopt_oracle as O
+from scsopt import losses
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def clean_env(monkeypatch):
+    for k in list(os.environ):
+        if k.startswith("SCS_"):
+            monkeypatch.delenv(k)
+    monkeypatch.setattr(O, "FAST_LINALG", True)
+
+
+def _lam_rule(p, m):
+    """BASELINE's λ = 0.1·‖∇f(0)‖∞ (bench.py)."""
+    return 0.1 * float(np.max(np.abs(p.gradx(np.zeros(m)))))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("shape", ["c3", "c2"])
+def test_default_path_newton_methods(shape, clean_env):
+    if shape == "c3":
+        N, m, kind = 20480, 16384, 1
+        f, out = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N)
+        of = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+        meth, ometh = scsopt.ProxGGNSCORE(), O.ProxGGNSCORE()
+    else:
+        N, m, kind = 12288, 8192, 2
+        f, out = losses.logistic_margin(1.0 / N), None
+        of = O.Loss("logistic_margin", 1.0 / N)
+        meth, ometh = scsopt.ProxNSCORE(), O.ProxNSCORE()
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    p = scsopt.Problem.synthetic(N, m, x0, f, 1.0, kind=kind, seed=2026, out_fn=out)
+    lam = _lam_rule(p, m)
+    p.λ = lam
+    A, y = p.get_data()
+    if shape == "c3":   # the configuration under test really is the fused 256 x 128 launch
+        rng = np.random.default_rng(5)
+        cols = rng.choice(m, 6, replace=False)
+        w, v = rng.random(N), rng.standard_normal(N)
+        pairs = [(i, j) for i in cols for j in cols]
+        g, atv, fused = p.gram_atv_sample(w, v, pairs)
+        assert fused
+        for (i, j), gv in zip(pairs, g):
+            terms = float(np.abs(A[:, i] * w * A[:, j]).sum())
+            assert abs(gv - float((A[:, i] * w) @ A[:, j])) <= 1e-13 * terms
+        bound = 1e-13 * (np.abs(A[:, cols]).T @ np.abs(v))
+        assert np.all(np.abs(atv[cols] - A[:, cols].T @ v) <= bound)
+    om = O.Problem(A, y, x0, of, lam)
+    sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=3, x_tol=0.0, f_tol=0.0,
+                         verbose=0)
+    osol = O.iterate(ometh, om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=3, x_tol=0.0, f_tol=0.0)
+    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.fval, osol.fval, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+    assert sol.obj[-1] < sol.obj[0]
+
+
+def _gemv_residual(p, w, d, x, rhs):
+    """(Aᵀ diag(w) A + diag d) x - rhs through the streaming GEMV kernels (not the Gram)."""
+    return p.gemv_t(w * p.gemv_n(x)) + d * x - rhs
+
+
+def _norm2_est(p, w, d, m, iters=12):
+    v = np.random.default_rng(0).standard_normal(m)
+    for _ in range(iters):
+        v = p.gemv_t(w * p.gemv_n(v)) + d * v
+        v /= np.linalg.norm(v)
+    return float(np.linalg.norm(p.gemv_t(w * p.gemv_n(v)) + d * v))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_c4_shape_solve_backward_error(mode, clean_env):
+    """m = 32768: the two-level Cholesky (mode 0, 256 inner blocks, lookahead) and the blocked LU
+    (mode 1) on (Aᵀ diag(w) A + diag d), N = m + 4096: ||r|| <= 1e-12 ||G|| ||x||."""
+    N, m = 32768 + 4096, 32768
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=11)
+    rng = np.random.default_rng(12)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-2
+    rhs = rng.standard_normal(m)
+    x, used_lu = p.solve_eval(w, d, rhs, mode=mode)
+    assert used_lu == (mode == 1)
+    r = _gemv_residual(p, w, d, x, rhs)
+    gn = _norm2_est(p, w, d, m)
+    assert np.linalg.norm(r) <= 1e-12 * gn * np.linalg.norm(x), (np.linalg.norm(r), gn, np.linalg.norm(x))
+
+
+@pytest.mark.timeout(600)
+def test_c5_shape_lqn_sparse(clean_env):
+    """C5 with N = 2^17 (m = 2^16 as configured): ProxLQNSCORE(mem 20) + indbox + PHuberSmootherIndBox(0.6)."""
+    N, m, rho = 1 << 17, 1 << 16, 0.01
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    lam, mu = 1e-4, 0.6
+    p = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), lam, density=rho, seed=2026,
+                                        C_set=[-1.0, 1.0])
+    A, y = p.get_sparse()
+    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), lam, C_set=[-1.0, 1.0])
+    sol = scsopt.iterate(scsopt.ProxLQNSCORE(m=20), p, "indbox", scsopt.PHuberSmootherIndBox(-1.0, 1.0, mu),
+                         max_epoch=10, x_tol=0.0, f_tol=0.0, verbose=0)
+    osol = O.iterate(O.ProxLQNSCORE(m=20), om, "indbox", O.PHuberSmootherIndBox(-1.0, 1.0, mu), max_epoch=10,
+                     x_tol=0.0, f_tol=0.0)
+    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+    assert np.all(sol.x >= -1.0) and np.all(sol.x <= 1.0)

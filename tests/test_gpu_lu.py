@@ -1,0 +1,104 @@
+"""GPU parity of the hand-written blocked LU with partial pivoting (csrc/lu.hip).
+
+The reference's `\\` on a dense Matrix is LAPACK getrf + getrs (prox-N-SCORE.jl:70; the NSCORE
+/ GGN non-SPD fallback) and its sample-space `qr(...) \\ b` (prox-GGN-SCORE.jl:126) solves the
+same non-symmetric system.  Pins:
+  * pivot rows equal to LAPACK dgetrf's (scipy.linalg.lapack.dgetrf, 0-based) on matrices
+    without near-ties, ties broken towards the first row as getf2's idamax does;
+  * info = the first exactly-zero pivot (1-based), as dgetrf reports it;
+  * the solution against LAPACK's getrs to 1e-14·cond(A) (max norm, relative to max |x|), and a
+    backward error ||Ax - b|| / (||A|| ||x||) <= 1e-13 at every size.
+"""
+import time
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+from scipy.linalg import lapack
+
+import scsopt
+from scsopt import losses
+
+pytestmark = pytest.mark.gpu
+
+
+def _bwd(A, x, b):
+    return float(np.linalg.norm(A @ x - b, np.inf) / (np.linalg.norm(A, np.inf) * np.linalg.norm(x, np.inf)))
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 127, 128, 129, 300, 1000, 2176])
+def test_lu_matches_lapack_getrf(n):
+    rng = np.random.default_rng(n)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    x, ipiv, info = scsopt.lu_solve(A, b)
+    lu, piv, linfo = lapack.dgetrf(A)
+    assert info == linfo == 0
+    assert np.array_equal(ipiv, piv), np.nonzero(ipiv != piv)[0][:10]
+    xr = sla.lu_solve((lu, piv), b)
+    # forward error: both are backward stable, so they agree to ~ cond(A)·eps
+    kappa = float(np.linalg.cond(A, np.inf)) if n > 1 else 1.0
+    assert np.max(np.abs(x - xr)) <= 1e-14 * kappa * float(np.abs(xr).max())
+    assert _bwd(A, x, b) <= 1e-13
+
+
+def test_lu_pivoting_cases():
+    """Zero diagonal (a swap is forced), equal magnitudes (first row wins), and a permutation."""
+    cases = [np.array([[0.0, 1.0], [1.0, 0.0]]),
+             np.array([[1.0, 2.0], [-1.0, 3.0]]),
+             np.array([[2.0, 1.0, 1.0], [-2.0, 3.0, 1.0], [2.0, 0.0, 5.0]]),
+             np.eye(200)[np.random.default_rng(1).permutation(200)] * 3.0]
+    for A in cases:
+        b = np.arange(1.0, A.shape[0] + 1.0)
+        x, ipiv, info = scsopt.lu_solve(A, b)
+        _, piv, linfo = lapack.dgetrf(A)
+        assert info == linfo == 0
+        assert np.array_equal(ipiv, piv)
+        np.testing.assert_allclose(A @ x, b, rtol=1e-14, atol=1e-14)
+
+
+@pytest.mark.parametrize("n,zcol", [(6, 3), (300, 0), (300, 299), (700, 150)])
+def test_lu_singular_info(n, zcol):
+    """A zero column: dgetrf's info is the 1-based index of the first zero pivot."""
+    rng = np.random.default_rng(n + zcol)
+    A = rng.standard_normal((n, n))
+    A[:, zcol] = 0.0
+    _, ipiv, info = scsopt.lu_solve(A, np.ones(n))
+    _, piv, linfo = lapack.dgetrf(A)
+    assert info == linfo == zcol + 1
+    assert np.array_equal(ipiv[:zcol], piv[:zcol])
+
+
+@pytest.mark.parametrize("n", [4096, 8192])
+def test_lu_large_backward_error(n, capsys):
+    """Full-size factorization (64 blocks at n = 8192, the C2 m): backward error and time."""
+    rng = np.random.default_rng(7)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    ctx = scsopt._lib.Context(0)
+    scsopt.lu_solve(A[:256, :256], b[:256], ctx=ctx)   # warm-up (code objects, aux buffers)
+    t0 = time.perf_counter()
+    x, ipiv, info = scsopt.lu_solve(A, b, ctx=ctx)
+    dt = time.perf_counter() - t0
+    assert info == 0
+    assert _bwd(A, x, b) <= 1e-13
+    with capsys.disabled():
+        print(f"\n[lu] n={n}: factor+solve+transfers {dt * 1e3:.1f} ms, backward error {_bwd(A, x, b):.2e}")
+
+
+def test_solve_eval_lu_vs_cholesky():
+    """The step's m x m system, (Aᵀ diag(w) A + diag(d)) x = rhs: Cholesky path vs forced LU vs host."""
+    N, m = 1500, 1000
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=3)
+    A, _ = p.get_data()
+    rng = np.random.default_rng(2)
+    w = rng.random(N) + 0.1
+    d = rng.random(m) + 0.5
+    rhs = rng.standard_normal(m)
+    xc, used_c = p.solve_eval(w, d, rhs, mode=0)
+    xl, used_l = p.solve_eval(w, d, rhs, mode=1)
+    assert not used_c and used_l
+    G = A.T @ (w[:, None] * A) + np.diag(d)
+    xr = np.linalg.solve(G, rhs)
+    np.testing.assert_allclose(xc, xr, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(xl, xr, rtol=1e-9, atol=1e-12)
