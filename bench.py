@@ -163,6 +163,10 @@ def main():
                          "reported separately -- the reference recomputes it every step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the sampled full-size Gram / Aᵀv check")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"],
+                    help="row-shard exchange: libscsopt's own RCCL communicator or a torch.distributed callback")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the exchange path (packed Gram -> all-reduce -> unpack) at one rank too")
     ap.add_argument("--cpu-Ns", type=int, default=2048)
     ap.add_argument("--cpu-ms", type=int, default=4096)
     args = ap.parse_args()
@@ -179,10 +183,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     comm = None
-    if world > 1:
+    if world > 1 or args.force_comm:
+        # one process per GPU; the row-sharded exchange runs on libscsopt's own RCCL communicator
+        # (--comm rccl) or through torch.distributed.all_reduce (--comm torch); torch.distributed
+        # itself only carries the communicator's unique id and the timing barrier / max
         torch.cuda.set_device(local)
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        comm = shard.Comm(device=torch.device("cuda", local))
+        comm = shard.Comm(device=torch.device("cuda", local), native=(args.comm == "rccl"),
+                          force=args.force_comm)
     N = args.N or cfg["N"]
     m = args.m or cfg["m"]
     if cfg.get("sparse") and world > 1:
@@ -198,7 +208,7 @@ def main():
     ctx = model.ctx
 
     def barrier():
-        if world > 1:
+        if comm is not None:
             dist.barrier()
         torch.cuda.synchronize()
         ctx.check(scsopt._lib.lib.scs_sync(ctx.h))
@@ -226,7 +236,7 @@ def main():
     dt = time.perf_counter() - t0
     objs = sol.obj
     tm = ctx.timing()
-    if world > 1:
+    if comm is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", local))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -246,7 +256,9 @@ def main():
             "dtype": ("f64 (fp32-stored A values)" if args.f32 else "f64"), "data": "synthetic (on-device counter RNG: A ~ N(0,1)/sqrt(m), y from a sparse x_true)",
             "config": {"workload": cfg["workload"], "N": N, "m": m, "lambda": model.λ, "mu": hmu.mu,
                        "method": type(method).__name__, "ss_type": method.ss_type,
-                       "parallelism": f"row-shard x{world}"},
+                       "parallelism": f"row-shard x{world}",
+                       "exchange": (("rccl (libscsopt)" if args.comm == "rccl" else "torch.distributed callback")
+                                    + (" forced at one rank" if world == 1 else "")) if comm is not None else None},
         }
         if tm["gram_calls"]:
             main_calls = steps                      # one Gram per GGN/NSCORE step; the solver's own
@@ -353,7 +365,7 @@ def main():
         print(json.dumps(line))
         if check is not None and not check["pass"]:
             raise SystemExit("sampled full-size Gram / Aᵀv check FAILED: " + json.dumps(check))
-    if world > 1:
+    if comm is not None:
         dist.destroy_process_group()
 
 

@@ -115,7 +115,19 @@ const char* scs_last_error(const scs_ctx* ctx);
 int scs_get_stream(scs_ctx* ctx, void** stream);
 
 /* ---- row sharding ------------------------------------------------------- */
+/* Two ways to run the exchange step (one in-place fp64 sum per step):
+ *  (a) libscsopt's own RCCL communicator (the default of the Python and Julia hosts on GPUs):
+ *      rank 0 calls scs_rccl_unique_id, the caller hands the 128 opaque bytes to every rank
+ *      (MPI, torch.distributed, a file ...), and every rank calls scs_set_comm_rccl -- a
+ *      collective call.  The context then calls ncclAllReduce itself, on its stream, in place
+ *      in its reduce buffer (allocated by the library unless one is registered);
+ *  (b) an all-reduce callback (scs_set_comm), e.g. torch.distributed with gloo for CPU tests. */
 int scs_set_comm(scs_ctx* ctx, int rank, int nranks, scs_allreduce_fn fn, void* user);
+int scs_rccl_unique_id(void* id /* 128 bytes */);
+int scs_set_comm_rccl(scs_ctx* ctx, int rank, int nranks, const void* id /* 128 bytes */);
+/* Run the exchange path (packed Gram tiles -> all-reduce -> unpack) even at one rank, so the
+ * communicator is exercised on a one-GPU host (results are unchanged).                        */
+int scs_set_comm_force(scs_ctx* ctx, int on);
 /* Device buffer (>= scs_reduce_buffer_size() doubles) owned by the caller,
  * used as the in-place all-reduce payload.                                  */
 int scs_reduce_buffer_size(scs_ctx* ctx, int64_t* ndoubles);

@@ -9,6 +9,7 @@
 //   linesearch / inv_BB_step  utils.jl:27-48           -> line_search / bb kernel
 //   get_Mg                    smoothing.jl:12-25        -> get_Mg
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -68,12 +69,16 @@ struct scs_ctx {
   bool own_stream = false;
   std::string err;
 
-  // row sharding
+  // row sharding: the exchange runs through libscsopt's own RCCL communicator (rccl) or the
+  // caller's all-reduce callback (ar); comm_force runs the exchange path at one rank too
   int rank = 0, nranks = 1;
   scs_allreduce_fn ar = nullptr;
   void* ar_user = nullptr;
+  ncclComm_t rccl = nullptr;
+  bool comm_force = false;
   double* red = nullptr;
   int64_t red_cap = 0;
+  bool own_red = false;   // red allocated by the library (no scs_set_reduce_buffer)
 
   // data
   int64_t N = 0, Npad = 0, m = 0, mpad = 0, Nglob = 0, row0 = 0;
@@ -396,16 +401,47 @@ void require_ready(scs_ctx* c, bool need_method) {
   if (need_method && !c->method_set) fail(c, SCS_ERR_STATE, "no method: call scs_method_init first");
 }
 
+// the exchange step is active: several ranks, or one rank with the exchange forced
+bool sharded(const scs_ctx* c) { return c->nranks > 1 || c->comm_force; }
+
+// doubles of the in-place all-reduce payload: packed Gram tiles ‖ Aᵀv (GGN / NSCORE), the
+// m-vector (LQN), or the all-gather of the rows for the sharded GGN sample-space branch
+int64_t reduce_buffer_doubles(const scs_ctx* c) {
+  const int64_t nb = c->mpad / 128;
+  const int64_t tsz = (nb * (nb + 1) / 2 + nb) * 128 * 128;   // 128 x 128 slots (tall lists add <= nb)
+  int64_t need = std::max<int64_t>(tsz + c->mpad, c->mpad);
+  if (c->Nglob + 1 <= c->m) {   // GGN sample-space branch across ranks: all-gather of A and y
+    const int64_t Ng = round_up(std::max<int64_t>(c->Nglob, 1), 16);
+    need = std::max<int64_t>(need, Ng * c->mpad + Ng);
+  }
+  return need + 64;
+}
+
+// the payload buffer: the caller's (scs_set_reduce_buffer) or one the library owns
+void ensure_red(scs_ctx* c) {
+  if (c->red || !sharded(c)) return;
+  if (!c->has_data) fail(c, SCS_ERR_STATE, "the reduce buffer needs the data dimensions");
+  const int64_t need = reduce_buffer_doubles(c);
+  c->red = dalloc<double>(c, need);
+  c->red_cap = need;
+  c->own_red = true;
+}
+
 void allreduce(scs_ctx* c, double* buf, int64_t count) {
-  if (c->nranks <= 1) return;
-  if (!c->ar) fail(c, SCS_ERR_COMM, "multi-rank context without an all-reduce callback");
+  if (!sharded(c)) return;
   if (buf != c->red) fail(c, SCS_ERR_COMM, "internal: all-reduce payload must live in the reduce buffer");
   if (count > c->red_cap) fail(c, SCS_ERR_COMM, "reduce buffer too small (%lld < %lld doubles)",
                                (long long)c->red_cap, (long long)count);
   hipEvent_t e0;
   tbegin(c, T_REDUCE, &e0);
-  int rc = c->ar(buf, count, (void*)c->st, c->ar_user);
-  if (rc != 0) fail(c, SCS_ERR_COMM, "all-reduce callback returned %d", rc);
+  if (c->rccl) {   // in place, on the context stream (one fp64 sum per exchange)
+    const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->rccl, c->st);
+    if (r != ncclSuccess) fail(c, SCS_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+  } else {
+    if (!c->ar) fail(c, SCS_ERR_COMM, "multi-rank context without a communicator");
+    int rc = c->ar(buf, count, (void*)c->st, c->ar_user);
+    if (rc != 0) fail(c, SCS_ERR_COMM, "all-reduce callback returned %d", rc);
+  }
   tend(c, T_REDUCE, e0);
 }
 
@@ -678,10 +714,11 @@ double forward(scs_ctx* c, const double* xh, const double* xd, int flags, bool n
                         c->gN, c->hN, c->wN, c->vN, c->valpart, c->st));
     // loss sum -> scal[ZF_SLOT] (reduce buffer slot 0 in multi-rank); a slot of its own: the value
     // stays in flight until the next use (no host round trip when the caller only needs z)
-    double* dst = (c->nranks > 1) ? c->red : c->scal + ZF_SLOT;
+    ensure_red(c);
+    double* dst = sharded(c) ? c->red : c->scal + ZF_SLOT;
     HCK(launch_sum_partials(c->valpart, c->nval, dst, c->st));
     allreduce(c, c->red, 1);
-    if (c->nranks > 1) HCK(hipMemcpyAsync(c->scal + ZF_SLOT, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+    if (sharded(c)) HCK(hipMemcpyAsync(c->scal + ZF_SLOT, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
     d2h(c, c->hscal + ZF_SLOT, c->scal + ZF_SLOT, 1);
     c->zf_pending = true;
     key_set(c, c->zkey, c->ztag, xh);
@@ -711,9 +748,10 @@ void gemv_t_local(scs_ctx* c, const double* v, double* out) {
 void gemv_t_global(scs_ctx* c, const double* v, double* out) {
   hipEvent_t e0;
   tbegin(c, T_GEMV, &e0);
-  matvec_t(c, v, c->nranks > 1 ? c->red : out);
+  ensure_red(c);
+  matvec_t(c, v, sharded(c) ? c->red : out);
   tend(c, T_GEMV, e0);
-  if (c->nranks > 1) {
+  if (sharded(c)) {
     allreduce(c, c->red, c->m);
     HCK(hipMemcpyAsync(out, c->red, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
   }
@@ -908,6 +946,7 @@ bool gram_x_independent(const scs_ctx* c) {
 // its steps all take the same separate Aᵀv pass) or SCS_GRAM_FUSE=0
 void gram_and_reduce(scs_ctx* c, const double* w, const double* v, double* vec_dev) {
   ensure_gram(c);
+  ensure_red(c);
   hipEvent_t e0;
   const bool cacheable = c->gram_cache && gram_x_independent(c);
   const size_t gbytes = sizeof(double) * (size_t)c->mpad * c->mpad;
@@ -916,14 +955,14 @@ void gram_and_reduce(scs_ctx* c, const double* w, const double* v, double* vec_d
   if (cacheable && c->Gk && c->gk_gen == c->data_gen) {   // the reduced Gram of an earlier step
     c->g_from_cache = true;
     HCK(hipMemcpyAsync(c->G, c->Gk, gbytes, hipMemcpyDeviceToDevice, c->st));
-    if (c->nranks > 1) {
+    if (sharded(c)) {
       HCK(hipMemcpyAsync(c->red, vec_dev, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
       allreduce(c, c->red, c->m);
       HCK(hipMemcpyAsync(vec_dev, c->red, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
     }
     return;
   }
-  if (c->nranks > 1) {
+  if (sharded(c)) {
     const int64_t tsz = (int64_t)c->nslots * 128 * 128;
     tbegin(c, T_GRAM, &e0);
     gram_main(c, w, c->red, 1, fuse ? v : nullptr, vec_dev);
@@ -973,6 +1012,7 @@ void ggn_sample_direction(scs_ctx* c, const double* xh);
 // rank runs the single-rank branch on that view, redundantly, as it does the m x m solve.
 void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
   if (c->sparse) fail(c, SCS_ERR_ARG, "the sharded GGN sample-space branch needs a dense A");
+  ensure_red(c);
   if (!c->gview_ok) {
     const int64_t Ng = c->Nglob, Npg = round_up(std::max<int64_t>(Ng, 1), 16);
     if (Npg * c->mpad + Npg > c->red_cap) fail(c, SCS_ERR_COMM, "reduce buffer too small for the row all-gather");
@@ -1000,14 +1040,17 @@ void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
   struct Scope {   // the gathered rows on one logical rank, restored even when the step fails
     scs_ctx* c;
     int nr;
-    explicit Scope(scs_ctx* cc) : c(cc), nr(cc->nranks) {
+    bool force;
+    explicit Scope(scs_ctx* cc) : c(cc), nr(cc->nranks), force(cc->comm_force) {
       swap_view(c, c->gview);
       c->nranks = 1;
+      c->comm_force = false;
       invalidate_caches(c);
     }
     ~Scope() {
       swap_view(c, c->gview);
       c->nranks = nr;
+      c->comm_force = force;
       invalidate_caches(c);
     }
   } scope(c);
@@ -1016,7 +1059,7 @@ void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
 
 void ggn_sample_direction(scs_ctx* c, const double* xh) {
   const int64_t N = c->N, m = c->m;
-  if (c->nranks > 1) return ggn_sample_direction_sharded(c, xh);
+  if (sharded(c)) return ggn_sample_direction_sharded(c, xh);
   if (!c->At) {
     const double* A = dense_A(c);
     c->NpS = round_up(N, 128);
@@ -1233,6 +1276,7 @@ int scs_destroy(scs_ctx* c) {
     (void)hipEventDestroy(p.e0);
     (void)hipEventDestroy(p.e1);
   }
+  if (c->rccl) (void)ncclCommDestroy(c->rccl);
   for (auto& a : c->allocs) (void)hipFree(a.p);
   if (c->hscal) (void)hipHostFree(c->hscal);
   lu_aux_free(&c->lu);
@@ -1251,6 +1295,10 @@ int scs_set_comm(scs_ctx* c, int rank, int nranks, scs_allreduce_fn fn, void* us
   return guarded(c, [&] {
     if (nranks < 1 || rank < 0 || rank >= nranks) fail(c, SCS_ERR_ARG, "bad rank/nranks %d/%d", rank, nranks);
     if (nranks > 1 && !fn) fail(c, SCS_ERR_ARG, "nranks > 1 needs an all-reduce callback");
+    if (c->rccl) {
+      (void)ncclCommDestroy(c->rccl);
+      c->rccl = nullptr;
+    }
     c->rank = rank;
     c->nranks = nranks;
     c->ar = fn;
@@ -1258,22 +1306,57 @@ int scs_set_comm(scs_ctx* c, int rank, int nranks, scs_allreduce_fn fn, void* us
   });
 }
 
+int scs_rccl_unique_id(void* id) {
+  if (!id) return SCS_ERR_ARG;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return SCS_ERR_COMM;
+  std::memcpy(id, &u, sizeof(u));
+  return SCS_OK;
+}
+
+int scs_set_comm_rccl(scs_ctx* c, int rank, int nranks, const void* id) {
+  return guarded(c, [&] {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !id)
+      fail(c, SCS_ERR_ARG, "bad rank/nranks %d/%d or null id", rank, nranks);
+    HCK(hipSetDevice(c->dev));
+    sync(c);
+    if (c->rccl) {
+      (void)ncclCommDestroy(c->rccl);
+      c->rccl = nullptr;
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank);   // collective over the ranks
+    if (r != ncclSuccess) fail(c, SCS_ERR_COMM, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
+    c->rccl = comm;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->ar = nullptr;
+    c->ar_user = nullptr;
+  });
+}
+
+int scs_set_comm_force(scs_ctx* c, int on) {
+  return guarded(c, [&] {
+    if (on && !c->rccl && !c->ar) fail(c, SCS_ERR_STATE, "scs_set_comm_force needs a communicator");
+    c->comm_force = on != 0;
+  });
+}
+
 int scs_reduce_buffer_size(scs_ctx* c, int64_t* nd) {
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "reduce buffer size needs the data dimensions");
-    const int64_t nb = c->mpad / 128;
-    const int64_t tsz = (nb * (nb + 1) / 2 + nb) * 128 * 128;   // 128 x 128 slots (tall lists add <= nb)
-    int64_t need = std::max<int64_t>(tsz + c->mpad, c->mpad);
-    if (c->Nglob + 1 <= c->m) {   // GGN sample-space branch across ranks: all-gather of A and y
-      const int64_t Ng = round_up(std::max<int64_t>(c->Nglob, 1), 16);
-      need = std::max<int64_t>(need, Ng * c->mpad + Ng);
-    }
-    *nd = need + 64;
+    *nd = reduce_buffer_doubles(c);
   });
 }
 
 int scs_set_reduce_buffer(scs_ctx* c, void* p, int64_t nd) {
   return guarded(c, [&] {
+    if (c->own_red) {
+      dfree_t(c, c->red);
+      c->own_red = false;
+    }
     c->red = (double*)p;
     c->red_cap = nd;
   });
@@ -1291,6 +1374,11 @@ static void set_dims(scs_ctx* c, int64_t N, int64_t m, int64_t Nglob, int64_t ro
 }
 
 static void reset_data(scs_ctx* c) {
+  if (c->own_red) {   // sized by the old dimensions
+    dfree_t(c, c->red);
+    c->red_cap = 0;
+    c->own_red = false;
+  }
   dfree_t(c, c->A);
   dfree_t(c, c->rowptr);
   dfree_t(c, c->colptr);

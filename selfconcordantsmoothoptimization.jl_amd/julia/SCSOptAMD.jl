@@ -9,10 +9,12 @@
 module SCSOptAMD
 
 using Random
+using SparseArrays
 using SelfConcordantSmoothOptimization
 import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel, is_interval_set
 
-export DeviceProblem, configure!, iterate_device!, set_gram_cache!
+export DeviceProblem, configure!, iterate_device!, set_gram_cache!, rccl_unique_id, set_comm_rccl!,
+       set_comm_callback!
 
 const lib = joinpath(@__DIR__, "..", "scsopt", "libscsopt.so")
 
@@ -49,23 +51,101 @@ mutable struct DeviceProblem <: ProxModel
     name
 end
 
-function DeviceProblem(A::Matrix{Float64}, y::AbstractVector, x0::Vector{Float64}, loss::Symbol, λ;
-                       out_fn::Union{Symbol,Nothing}=nothing, scale::Float64=1.0 / size(A, 1),
-                       L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0)
+function create_ctx(device::Integer)
     ctx = Ref{Ptr{Cvoid}}(C_NULL)
     rc = ccall((:scs_create, lib), Cint, (Cint, Ptr{Cvoid}, Ref{Ptr{Cvoid}}), device, C_NULL, ctx)
     rc == 0 || error("scs_create failed ($rc)")
+    return ctx[]
+end
+
+function finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
+    chk(ccall((:scs_set_loss, lib), Cint, (Ptr{Cvoid}, Cint, Cint, Float64), ctx, LOSS[loss], GGN[out_fn], scale), ctx)
+    model = DeviceProblem(ctx, A, yv, x0, nothing, λ, nothing, nothing, L, sol, C_set, P, out_fn,
+                          nothing, nothing, nothing, nothing, nothing, nothing)
+    model.f = (A_, y_, x) -> devf(model, x)        # optim_loop! calls model.f(model.A, model.y, x)
+    finalizer(m_ -> ccall((:scs_destroy, lib), Cint, (Ptr{Cvoid},), m_.ctx), model)
+    return model
+end
+
+# Problem(A, y, x0, f, λ; ...) (problems.jl:61-81) with A on the device.  Row sharding: pass
+# the local rows with N_global / row0, and attach a communicator (set_comm_rccl! /
+# set_comm_callback!) before the first step.
+function DeviceProblem(A::Matrix{Float64}, y::AbstractVector, x0::Vector{Float64}, loss::Symbol, λ;
+                       out_fn::Union{Symbol,Nothing}=nothing, scale::Float64=1.0 / size(A, 1),
+                       L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0,
+                       N_global::Integer=size(A, 1), row0::Integer=0)
+    ctx = create_ctx(device)
     N, m = size(A)
     yv = Vector{Float64}(y)
     chk(ccall((:scs_set_data, lib), Cint,
               (Ptr{Cvoid}, Int64, Int64, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Int64),
-              ctx[], N, m, A, N, yv, N, 0), ctx[])
-    chk(ccall((:scs_set_loss, lib), Cint, (Ptr{Cvoid}, Cint, Cint, Float64), ctx[], LOSS[loss], GGN[out_fn], scale),
-        ctx[])
-    model = DeviceProblem(ctx[], A, yv, x0, nothing, λ, nothing, nothing, L, sol, C_set, P, out_fn,
-                          nothing, nothing, nothing, nothing, nothing, nothing)
-    model.f = (A_, y_, x) -> devf(model, x)        # optim_loop! calls model.f(model.A, model.y, x)
-    finalizer(m_ -> ccall((:scs_destroy, lib), Cint, (Ptr{Cvoid},), m_.ctx), model)
+              ctx, N, m, A, N, yv, N_global, row0), ctx)
+    return finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
+end
+
+# A::SparseMatrixCSC (README.md:105 builds it with sprandn): its CSC arrays are the column copy;
+# the row copy is the CSC of the transpose.  0-based indices on the C side.
+function DeviceProblem(A::SparseMatrixCSC{Float64}, y::AbstractVector, x0::Vector{Float64}, loss::Symbol, λ;
+                       out_fn::Union{Symbol,Nothing}=nothing, scale::Float64=1.0 / size(A, 1),
+                       L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0,
+                       val_f32::Bool=false, N_global::Integer=size(A, 1), row0::Integer=0)
+    ctx = create_ctx(device)
+    N, m = size(A)
+    yv = Vector{Float64}(y)
+    At = SparseMatrixCSC(transpose(A))
+    rowptr = Int64.(At.colptr .- 1); colidx = Int32.(At.rowval .- 1); val = Vector{Float64}(At.nzval)
+    colptr = Int64.(A.colptr .- 1);  rowidx = Int32.(A.rowval .- 1);  valT = Vector{Float64}(A.nzval)
+    chk(ccall((:scs_set_sparse, lib), Cint,
+              (Ptr{Cvoid}, Int64, Int64, Int64, Ptr{Int64}, Ptr{Int32}, Ptr{Float64}, Ptr{Int64}, Ptr{Int32},
+               Ptr{Float64}, Cint, Ptr{Float64}, Int64, Int64),
+              ctx, N, m, nnz(A), rowptr, colidx, val, colptr, rowidx, valT, val_f32 ? 1 : 0, yv, N_global, row0),
+        ctx)
+    return finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
+end
+
+# ---- row sharding (SURVEY.md §8e): one process per GPU, A's rows split across them ---------
+# libscsopt's own RCCL communicator: rank 0 draws the id, the caller hands the 128 bytes to
+# every rank (MPI.jl's Bcast!, a shared file ...), every rank then calls set_comm_rccl!.
+function rccl_unique_id()
+    id = zeros(UInt8, 128)
+    rc = ccall((:scs_rccl_unique_id, lib), Cint, (Ptr{Cvoid},), id)
+    rc == 0 || error("scs_rccl_unique_id failed ($rc)")
+    return id
+end
+
+function set_comm_rccl!(model::DeviceProblem, rank::Integer, nranks::Integer, id::Vector{UInt8})
+    length(id) == 128 || error("an RCCL unique id is 128 bytes")
+    chk(ccall((:scs_set_comm_rccl, lib), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{Cvoid}), model.ctx, rank, nranks, id),
+        model.ctx)
+    return model
+end
+
+# Or any all-reduce the host owns: `sum!(buf::Ptr{Float64}, count::Int64, stream::Ptr{Cvoid})`
+# sums `count` doubles in place across ranks on the device (e.g. an RCCL call through
+# AMDGPU.jl); the payload lives in a device buffer of reduce_buffer_size doubles registered here.
+const CALLBACKS = Dict{Ptr{Cvoid},Any}()
+
+function allreduce_trampoline(buf::Ptr{Cvoid}, count::Int64, stream::Ptr{Cvoid}, user::Ptr{Cvoid})::Cint
+    try
+        CALLBACKS[user](Ptr{Float64}(buf), count, stream)
+        return Cint(0)
+    catch
+        return Cint(1)
+    end
+end
+
+function set_comm_callback!(model::DeviceProblem, rank::Integer, nranks::Integer, sum!::Function,
+                            dev_buf::Ptr{Cvoid}=C_NULL)
+    CALLBACKS[model.ctx] = sum!
+    fn = @cfunction(allreduce_trampoline, Cint, (Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}))
+    chk(ccall((:scs_set_comm, lib), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{Cvoid}, Ptr{Cvoid}),
+              model.ctx, rank, nranks, fn, model.ctx), model.ctx)
+    if dev_buf != C_NULL
+        n = Ref{Int64}(0)
+        chk(ccall((:scs_reduce_buffer_size, lib), Cint, (Ptr{Cvoid}, Ref{Int64}), model.ctx, n), model.ctx)
+        chk(ccall((:scs_set_reduce_buffer, lib), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Int64), model.ctx, dev_buf, n[]),
+            model.ctx)
+    end
     return model
 end
 

@@ -28,8 +28,8 @@ METHOD = {"nscore": 1, "ggnscore": 2, "lqnscore": 3}
 # names ("libamdhip64.so") differ from the SONAMEs ("libamdhip64.so.7"), so if
 # libscsopt pulled /opt/rocm's copies in first, importing torch afterwards would
 # load a second runtime and crash.  Importing torch first makes libscsopt's
-# NEEDED entries resolve to the already-loaded (torch-bundled) HIP runtime.  torch is
-# plumbing only (streams, torch.distributed).
+# NEEDED entries resolve to the already-loaded (torch-bundled) HIP runtime and RCCL
+# (same SONAMEs).  torch is plumbing only (streams, torch.distributed).
 import torch  # noqa: E402,F401  (must precede the CDLL below)
 
 if not os.path.exists(LIB_PATH):
@@ -71,6 +71,9 @@ _SIGS = {
     "scs_last_error": (C.c_char_p, [C.c_void_p]),
     "scs_get_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "scs_set_comm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, C.c_void_p]),
+    "scs_rccl_unique_id": (C.c_int, [C.c_void_p]),
+    "scs_set_comm_rccl": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "scs_set_comm_force": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_reduce_buffer_size": (C.c_int, [C.c_void_p, c_i64p]),
     "scs_set_reduce_buffer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
     "scs_set_data": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_dp, C.c_int64, c_dp, C.c_int64, C.c_int64]),

@@ -91,7 +91,7 @@ class Problem:
         self.comm = comm
         self.generic = A is None and _ctx is None
         self.ctx = _ctx if _ctx is not None else _lib.Context(device)
-        if comm is not None and comm.world > 1:
+        if comm is not None and comm.active and _ctx is None:
             comm.attach(self.ctx)
         if _ctx is None:
             if self.generic:
@@ -114,7 +114,7 @@ class Problem:
             N = C.c_int64()
             self.ctx.check(_lib.lib.scs_get_dims(self.ctx.h, C.byref(N), None, None, None))
             self.N = int(N.value)
-        if comm is not None and comm.world > 1:
+        if comm is not None and comm.active:
             comm.bind_buffer(self.ctx)
         ggn = ggn_kind(out_fn)
         if out_fn is not None and f.kind in ("quadratic", "rosenbrock"):
@@ -134,7 +134,7 @@ class Problem:
         rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
         r0, r1 = row_range(N, world, rank)
         ctx = _lib.Context(device)
-        if comm is not None and world > 1:
+        if comm is not None and comm.active:
             comm.attach(ctx)
         spec = _lib.Synth(N_global=N, row0=r0, N=r1 - r0, m=m, seed=seed, kind=kind, density=density)
         ctx.check(_lib.lib.scs_gen_data(ctx.h, C.byref(spec)))

@@ -5,9 +5,13 @@ A (and of y), generated or uploaded in place; x and every length-m vector are
 replicated.  The only exchange of an iteration is one in-place fp64 sum
 (SURVEY.md §8e): [packed lower-triangular Gram tiles ‖ Aᵀv] for
 ProxGGNSCORE / ProxNSCORE, the length-m gradient for ProxLQNSCORE, and one
-scalar per objective evaluation.  libscsopt calls back into ``Comm`` at
-those points; the sum itself is ``torch.distributed.all_reduce`` (RCCL over
-xGMI with the "nccl" backend on MI355X, gloo on CPU).
+scalar per objective evaluation.  On GPUs (``native=True``, the default with the
+"nccl" backend) libscsopt runs the sum itself: an RCCL communicator of its own
+(scs_set_comm_rccl; torch.distributed only carries the 128-byte unique id) calls
+ncclAllReduce on the context stream, in place, over xGMI.  Otherwise libscsopt
+calls back into ``Comm`` at those points and the sum is
+``torch.distributed.all_reduce`` (gloo on CPU).  ``force=True`` runs the exchange
+path at one rank too, so a one-GPU host exercises the communicator.
 """
 from __future__ import annotations
 
@@ -33,25 +37,51 @@ def allreduce_inplace(t, group=None):
 class Comm:
     """Binds a libscsopt context to a torch.distributed process group."""
 
-    def __init__(self, rank=None, world=None, group=None, device=None):
+    def __init__(self, rank=None, world=None, group=None, device=None, native=None, force=False):
         import torch.distributed as dist
         self.rank = dist.get_rank(group) if rank is None else int(rank)
         self.world = dist.get_world_size(group) if world is None else int(world)
         self.group = group
         self.device = device
+        if native is None:
+            native = dist.get_backend(group) == "nccl"
+        self.native = bool(native)
+        self.force = bool(force)
         self.buf = None
         self._cb = None
         self._ctx = None
 
+    @property
+    def active(self):
+        return self.world > 1 or self.force
+
     def attach(self, ctx):
         from . import _lib
         self._ctx = ctx
-        self._cb = _lib.ALLREDUCE_FN(self._callback)
-        ctx._keep.append(self._cb)
-        ctx.check(_lib.lib.scs_set_comm(ctx.h, self.rank, self.world, self._cb, None))
+        if self.native:
+            import torch.distributed as dist
+            uid = C.create_string_buffer(128)
+            if self.rank == 0:
+                rc = _lib.lib.scs_rccl_unique_id(uid)
+                if rc != _lib.SCS_OK:
+                    raise _lib.ScsError(rc, "scs_rccl_unique_id failed")
+            box = [uid.raw if self.rank == 0 else None]
+            dist.broadcast_object_list(box, src=0, group=self.group)
+            uid = C.create_string_buffer(box[0], 128)
+            ctx._keep.append(uid)
+            ctx.check(_lib.lib.scs_set_comm_rccl(ctx.h, self.rank, self.world, uid))
+        else:
+            self._cb = _lib.ALLREDUCE_FN(self._callback)
+            ctx._keep.append(self._cb)
+            ctx.check(_lib.lib.scs_set_comm(ctx.h, self.rank, self.world, self._cb, None))
+        if self.force:
+            ctx.check(_lib.lib.scs_set_comm_force(ctx.h, 1))
 
     def bind_buffer(self, ctx):
-        """Allocate the all-reduce payload buffer (torch-owned device memory) once the dims are known."""
+        """Allocate the all-reduce payload buffer (torch-owned device memory) once the dims are known;
+        the native RCCL path lets libscsopt own it."""
+        if self.native:
+            return
         import torch
         from . import _lib
         n = C.c_int64()

@@ -1,0 +1,124 @@
+"""CPU: the Julia `ccall` binding (julia/SCSOptAMD.jl) against the C ABI (include/scsopt.h).
+
+Julia is absent here and on the GPU box, so the binding is never executed; this test pins what
+can be checked without it: every `ccall((:scs_*, lib), Ret, (Args...), ...)` names a function the
+header declares, with the same number of arguments and Julia types that match the C prototype
+(Ptr{Float64} <-> double*, Int64 <-> int64_t, Cint <-> int, Ref{T} <-> T*, Ptr{Cvoid} <-> any
+pointer, the 6-pointer scs_history struct as Ref{NTuple{6,Ptr{Float64}}}), and that the binding
+reads the IndBox smoothers' bounds the way the reference builds them (closure captures,
+phuber-smooth.jl:59-65), not from fields the reference structs do not have.
+"""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JL = os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd", "julia", "SCSOptAMD.jl")
+HDR = os.path.join(ROOT, "include", "scsopt.h")
+
+
+def _split_top(s, sep=","):
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch in "({[":
+            depth += 1
+        elif ch in ")}]":
+            depth -= 1
+        if ch == sep and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _header_protos():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"(const char\s*\*|int)\s+(scs_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.S):
+        ret, name, args = m.group(1), m.group(2), " ".join(m.group(3).split())
+        params = [] if args in ("", "void") else [a.strip() for a in args.split(",")]
+        types = []
+        for p in params:
+            p = re.sub(r"\s*\w+\s*\[\d+\]$", " *", p)          # T id[128] -> T *
+            p = re.sub(r"\b\w+\s*(\*?)$", r"\1", p) if not p.endswith("*") else p
+            types.append(" ".join(p.replace("*", " * ").split()))
+        protos[name] = (ret.replace(" ", ""), types)
+    return protos
+
+
+def _julia_ccalls():
+    src = open(JL).read()
+    calls = []
+    for m in re.finditer(r"ccall\(\(:(\w+),\s*lib\),", src):
+        i = m.end()
+        depth, j = 1, i
+        while depth:
+            if src[j] == "(":
+                depth += 1
+            elif src[j] == ")":
+                depth -= 1
+            j += 1
+        parts = _split_top(src[i:j - 1])
+        ret, argt = parts[0], parts[1]
+        assert argt.startswith("(") and argt.endswith(")"), (m.group(1), argt)
+        inner = argt[1:-1].strip().rstrip(",")
+        calls.append((m.group(1), ret, _split_top(inner) if inner else []))
+    return calls
+
+
+C_SCALARS = {"Cint": {"int"}, "Int64": {"int64_t"}, "Float64": {"double"}, "UInt64": {"uint64_t"},
+             "Cuint": {"unsigned"}, "Int32": {"int32_t"}}
+C_POINTEE = {"Float64": "double", "Int64": "int64_t", "Int32": "int32_t", "Cint": "int", "UInt8": "unsigned char"}
+
+
+def _compatible(jt, ct):
+    ct_base = ct.replace("const ", "").strip()
+    if ct_base == "scs_allreduce_fn":                 # function pointer typedef (a @cfunction)
+        return jt == "Ptr{Cvoid}"
+    is_ptr = ct_base.endswith("*")
+    if jt in C_SCALARS:
+        return (not is_ptr) and ct_base in C_SCALARS[jt]
+    if not is_ptr:
+        return False
+    pointee = ct_base[:-1].strip()
+    m = re.fullmatch(r"(Ptr|Ref)\{(.+)\}", jt)
+    if not m:
+        return False
+    inner = m.group(2)
+    if inner == "Cvoid":
+        return True                                   # void* / scs_ctx* / struct pointers
+    if inner == "Ptr{Cvoid}":
+        return pointee.endswith("*")                  # scs_ctx** / void**
+    if inner.startswith("NTuple{6,Ptr{Float64}}"):
+        return pointee == "scs_history"
+    return C_POINTEE.get(inner) == pointee
+
+
+def test_every_ccall_matches_the_header():
+    protos = _header_protos()
+    calls = _julia_ccalls()
+    assert len(calls) >= 15
+    seen = set()
+    for name, ret, args in calls:
+        assert name in protos, f"{name} is not declared in scsopt.h"
+        cret, ctypes = protos[name]
+        assert (ret == "Cstring") == (cret == "constchar*"), (name, ret, cret)
+        assert len(args) == len(ctypes), (name, args, ctypes)
+        for a, ct in zip(args, ctypes):
+            assert _compatible(a, ct), (name, a, ct)
+        seen.add(name)
+    # the binding covers the step / loop / comm / sparse entry points a maintainer needs
+    for need in ("scs_create", "scs_set_data", "scs_set_sparse", "scs_set_loss", "scs_set_reg", "scs_set_smoother",
+                 "scs_method_init", "scs_step", "scs_iterate", "scs_set_comm", "scs_set_reduce_buffer",
+                 "scs_reduce_buffer_size", "scs_eval_f"):
+        assert need in seen, need
+
+
+def test_indbox_bounds_come_from_the_closures():
+    src = open(JL).read()
+    assert "hμ.lb" not in src and "hμ.ub" not in src        # no such fields (phuber-smooth.jl:38-58)
+    assert "getfield(g, :lb)" in src and "getfield(g, :ub)" in src
+    assert "is_interval_set" in src                         # C_set forms of prox-operators.jl:34-46
