@@ -87,7 +87,10 @@ hipError_t launch_gemv_n(const double* A, int64_t S, int64_t Npad, int64_t mpad,
 // Loss epilogue  (closed forms; see oracle/scsopt_oracle.py Loss for the
 // reference expressions they restate, test/test_algs.jl:9-11)
 // ---------------------------------------------------------------------------
-constexpr int EPI_PER_BLOCK = 2048;
+// one sample per thread: the z-split partial loads of a sample are independent, so a block's
+// loads are all in flight at once (2048 samples per block, 8 sequential per thread, made the
+// C5 epilogue latency-bound: 26 us at N = 2^20)
+constexpr int EPI_PER_BLOCK = 256;
 
 int epilogue_blocks(int64_t Npad) { return (int)ceil_div(Npad, EPI_PER_BLOCK); }
 
@@ -306,19 +309,32 @@ hipError_t launch_gemv_t(const double* A, int64_t S, int64_t Npad, int64_t m, in
   return hipGetLastError();
 }
 
-__global__ void gemv_t_finalize_kernel(const double* __restrict__ part, int nchunk, int64_t ldp, int64_t m,
-                                       double* __restrict__ out) {
-  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+// out[j] = Σ_c part[c][j]: two columns per thread (16-B loads), four interleaved accumulators
+// combined in a fixed order, so 4 loads per thread are in flight (one accumulator chain made the
+// 64-chunk C5 finalize latency-bound: 27 us for 33.5 MB)
+__global__ __launch_bounds__(128) void gemv_t_finalize_kernel(const double* __restrict__ part, int nchunk,
+                                                              int64_t ldp, int64_t m, double* __restrict__ out) {
+  const int64_t j = 2 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x);
   if (j >= m) return;
-  double s = 0.0;
-  for (int c = 0; c < nchunk; ++c) s += part[(int64_t)c * ldp + j];
-  out[j] = s;
+  v2d s0 = {0.0, 0.0}, s1 = {0.0, 0.0}, s2 = {0.0, 0.0}, s3 = {0.0, 0.0};
+  int c = 0;
+  for (; c + 4 <= nchunk; c += 4) {
+    s0 += *(const v2d*)(part + (int64_t)c * ldp + j);
+    s1 += *(const v2d*)(part + (int64_t)(c + 1) * ldp + j);
+    s2 += *(const v2d*)(part + (int64_t)(c + 2) * ldp + j);
+    s3 += *(const v2d*)(part + (int64_t)(c + 3) * ldp + j);
+  }
+  for (; c < nchunk; ++c) s0 += *(const v2d*)(part + (int64_t)c * ldp + j);
+  const v2d s = (s0 + s1) + (s2 + s3);
+  out[j] = s[0];
+  if (j + 1 < m) out[j + 1] = s[1];
 }
 
 hipError_t launch_gemv_t_finalize(const double* part, int nchunk, int64_t mpad, int64_t m, double* out,
                                   hipStream_t st) {
-  hipLaunchKernelGGL(gemv_t_finalize_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, st, part, nchunk, mpad,
-                     m, out);
+  // ldp = mpad (even, >= m + 1 when m is odd): the pair loads stay inside each partial row
+  hipLaunchKernelGGL(gemv_t_finalize_kernel, dim3((unsigned)ceil_div(ceil_div(m, 2), 128)), dim3(128), 0, st, part,
+                     nchunk, mpad, m, out);
   return hipGetLastError();
 }
 

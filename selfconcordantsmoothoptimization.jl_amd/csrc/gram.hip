@@ -801,7 +801,8 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
                        int ntiles, double* G, int64_t ldg, int packed, int tall, hipStream_t st, const double* v,
                        double* VP, int64_t vps) {
   if (ntiles <= 0) return hipSuccess;
-  const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
+  // packed: bit 0 = packed slots (else the upper triangle), bit 1 = accumulate into G
+  const int flags = ((packed & 1) ? GRAM_PACKED : GRAM_UPPER) | ((packed & 2) ? GRAM_ACCUMULATE : 0);
   if (v) {
     if (!gram_fuse_ok(tall)) return hipErrorInvalidValue;
     if (tall)
@@ -993,10 +994,10 @@ __global__ void gram_combine_kernel(const double* __restrict__ P, const int4* __
     const int jl = e / GTI, il = e % GTI;
     double sum = 0.0;
     for (int sp = 0; sp < nsplit; ++sp) sum += P[(int64_t)(it.w + sp) * GTI * GT + e];
-    if (packed)
-      G[((int64_t)it.z * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT)] = sum;
-    else
-      G[((int64_t)it.x * GTI + il) * ldg + (int64_t)it.y * GT + jl] = sum;
+    double* dst = (packed & 1) ? G + ((int64_t)it.z * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT)
+                               : G + ((int64_t)it.x * GTI + il) * ldg + (int64_t)it.y * GT + jl;
+    if (packed & 2) *dst += sum;
+    else *dst = sum;
   }
 }
 
@@ -1004,7 +1005,8 @@ __global__ void gram_combine_kernel(const double* __restrict__ P, const int4* __
 hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
                              int tall, hipStream_t st, const double* v, double* VP, int64_t vps) {
-  const int flags = packed ? GRAM_PACKED : GRAM_UPPER;
+  // packed: bit 0 = packed slots (else the upper triangle), bit 1 = accumulate into G
+  const int flags = ((packed & 1) ? GRAM_PACKED : GRAM_UPPER) | ((packed & 2) ? GRAM_ACCUMULATE : 0);
   const int glds = gram_tall_mode();
   if (v && !gram_fuse_ok(tall)) return hipErrorInvalidValue;
   if (v && tall)

@@ -25,7 +25,8 @@ struct ProxArgsH {
 // ---- gram.hip
 void gram_tile_list(int nb, int2* out, int* ntiles);
 void gram_tile_list_tall(int nb, int2* out, int* ntiles);
-// Main Gram on the panel-blocked A (lda = S = Npad / 16).  tall = 1: 256 x 128 tiles from
+// Main Gram on the panel-blocked A (lda = S = Npad / 16); `packed` bit 0 = packed slots (else the
+// upper triangle), bit 1 = accumulate into G.  tall = 1: 256 x 128 tiles from
 // gram_tile_list_tall (nb even); packed slots are then the 128 x 128 halves (2t, 2t+1) of
 // launch tile t.  gram_launch_gen operates on column-major operands (the Cholesky updates).
 // v != nullptr: the same launch also forms Aᵀv (fused, gram_fuse_ok kernels only) into VP: one row
@@ -104,6 +105,9 @@ hipError_t launch_prox_only(const ProxArgsH& P, const double* z, const double* H
 hipError_t launch_reg_value(const ProxArgsH& P, const double* x, int64_t m, double* out, double* part,
                             hipStream_t st);
 hipError_t launch_dot(const double* a, const double* b, int64_t m, double* out, hipStream_t st);
+// out[0..3) = Σ(x − xs)², Σx², Σ(xn − x)² (xs / xn may be null); part: 3 x 256 doubles
+hipError_t launch_norms3(const double* x, const double* xs, const double* xn, int64_t m, double* out, double* part,
+                         hipStream_t st);
 hipError_t launch_axpby(const double* a, double lam, const double* b, int64_t m, double* out, hipStream_t st);
 hipError_t launch_sub(const double* a, const double* b, int64_t m, double* out, hipStream_t st);
 hipError_t launch_neg(const double* a, int64_t m, double* out, hipStream_t st);
@@ -154,6 +158,9 @@ hipError_t launch_gemv_t_finalize(const double* part, int nchunk, int64_t mpad, 
                                   hipStream_t st);
 hipError_t launch_densify(const int64_t* rowptr, const int* col, const void* val, int f32, int64_t N, int64_t Npad,
                           double* Ad, hipStream_t st);
+// CSR rows [r0, r0 + n) into a zeroed panel-blocked slot of Npad_b rows (zero = 1: clear them again)
+hipError_t launch_densify_range(const int64_t* rowptr, const int* col, const void* val, int f32, int64_t r0,
+                                int64_t n, int64_t Npad_b, int zero, double* Ab, hipStream_t st);
 hipError_t launch_densify_rows(const int64_t* rowptr, const int* col, const void* val, int f32, const int64_t* rows,
                                int64_t n, int64_t Npad_b, const double* y, double* Ab, double* yb, hipStream_t st);
 hipError_t launch_gather_rows(const double* A, int64_t Npad, const double* y, const int64_t* rows, int64_t n,

@@ -37,6 +37,8 @@ struct Pending {
 };
 enum { T_GRAM = 0, T_GEMV, T_SOLVE, T_STEP, T_REDUCE, T_N };
 constexpr int ZF_SLOT = 24;   // scal / hscal slot of the deferred f(x) (forward with need_val = false)
+// scs_iterate's device-resident loop: f(x) and get_reg(x) of the epoch's x, the norms (3 slots)
+constexpr int FX_SLOT = 25, RX_SLOT = 26, NRM_SLOT = 28, LOOP_SLOTS = 32;
 
 struct DevBuf {
   void* p = nullptr;
@@ -101,6 +103,12 @@ struct scs_ctx {
     void* val = nullptr;
   } bcsr, bcsc;  // LDS-blocked copies used by the products (sparse.hip)
   double* Ad = nullptr;  // dense panel-blocked mirror of a sparse A (Gram-based methods only)
+  // ... or, when the mirror does not fit under the cap, a ring of two R-row dense slots the Gram
+  // streams through chunk by chunk (gram_main_stream)
+  int sp_mode = 0;              // 0: undecided, 1: mirror, 2: stream
+  double* ringA = nullptr;
+  int64_t ring_rows = 0;
+  int64_t ring_r0[2] = {-1, -1}, ring_n[2] = {0, 0};
   // x-independent Gram reuse (scs_set_gram_cache): Gk holds AᵀQA of data generation gk_gen;
   // data_gen moves on every change of the rows or the loss (new data, batch view swaps)
   int gram_cache = 0;
@@ -140,6 +148,9 @@ struct scs_ctx {
   std::vector<int> ring;  // physical slots, oldest -> newest
   int spare = 0;
   int* d_order = nullptr;
+  int* hring = nullptr;       // pinned copy of the ring order (asynchronous upload)
+  bool lbfgs_pending = false; // scs_iterate's device loop: the memory update's dg/gg are read at the epoch end
+  int lbfgs_slot = 0;
   double H0 = 1.0;
 
   // m-space workspace
@@ -147,6 +158,8 @@ struct scs_ctx {
          *zb = nullptr, *d = nullptr, *gq = nullptr, *gqn = nullptr, *gtmp = nullptr, *gtmp2 = nullptr, *q = nullptr,
          *ab = nullptr, *tlwork = nullptr, *scal = nullptr, *gcache[2] = {nullptr, nullptr};
   double* hscal = nullptr;  // pinned host scalars
+  double* xstar = nullptr;  // model.x on the device (scs_iterate's rel_error)
+  bool dev_loop = false;    // scs_iterate's device-resident loop: steps leave x_new / pri on the device
   // N-space workspace
   int nsplit = 1;
   double *zpart = nullptr, *z = nullptr, *gN = nullptr, *hN = nullptr, *wN = nullptr, *vN = nullptr,
@@ -459,7 +472,11 @@ void alloc_mspace(scs_ctx* c) {
   dfree_t(c, c->cinfo);
   c->cinfo = dalloc<int>(c, 1);   // factorization info (Cholesky pivot check, LU zero pivot, NaN scan)
   dfree_t(c, c->scal);
-  c->scal = dalloc<double>(c, 64 + 3 * 256);   // scalars + the multi-workgroup tail / get_reg partials
+  // scalars + the partials of the multi-workgroup tail / L-BFGS update (64..), get_reg (64 + 2·256)
+  // and the loop norms (64 + 3·256)
+  c->scal = dalloc<double>(c, 64 + 6 * 256);
+  dfree_t(c, c->xstar);
+  c->xstar = dalloc<double>(c, mp);
   if (!c->hscal) HCK(hipHostMalloc((void**)&c->hscal, 64 * sizeof(double), hipHostMallocDefault));
 }
 
@@ -907,7 +924,7 @@ const double* dense_A(scs_ctx* c) {
   HCK(hipMemGetInfo(&fr, &tot));
   if (bytes + (size_t)c->mpad * c->mpad * 16 > fr)
     fail(c, SCS_ERR_ARG,
-         "ProxNSCORE / ProxGGNSCORE on a sparse A form the Gram on a dense mirror of A (%.1f GiB) plus the "
+         "the GGN sample-space branch on a sparse A forms Aᵀ from a dense mirror of A (%.1f GiB) plus the "
          "m x m system; the device has %.1f GiB free",
          bytes / 1073741824.0, fr / 1073741824.0);
   c->Ad = dalloc<double>(c, bytes / sizeof(double));
@@ -916,9 +933,70 @@ const double* dense_A(scs_ctx* c) {
   return c->Ad;
 }
 
+// How the Gram of a sparse A gets its dense operand tiles: a mirror of all of A when it fits
+// under the cap (SCS_SPARSE_MIRROR_MAX_GB, default: the free device memory less the m x m
+// system and 4 GiB), else the streaming ring (memory O(nnz + R·m + m²) for any N).
+bool sparse_streams(scs_ctx* c) {
+  if (!c->sparse) return false;
+  if (c->sp_mode == 0) {
+    const double bytes = (double)c->Npad * c->mpad * sizeof(double);
+    size_t fr = 0, tot = 0;
+    HCK(hipMemGetInfo(&fr, &tot));
+    double cap = (double)fr - (double)c->mpad * c->mpad * 24 - 4.0 * 1073741824.0;
+    if (const char* e = std::getenv("SCS_SPARSE_MIRROR_MAX_GB")) cap = std::atof(e) * 1073741824.0;
+    c->sp_mode = (bytes <= cap) ? 1 : 2;
+  }
+  return c->sp_mode == 2;
+}
+
+// Streaming sparse Gram (Jt*Q*Jt' of a SparseMatrixCSC, prox-GGN-SCORE.jl:114,129 / a hess_fx Gram):
+// rows are densified R at a time into one of two panel-blocked ring slots (the CSR scatter is
+// O(nnz), the slot's previous chunk is cleared by scattering zeros at its own positions) and the
+// production Gram launch accumulates each chunk's Aᵀ diag(w) A into G -- the MFMA tiles are the
+// dense kernel's, K split into N/R chunks.
+void gram_main_stream(scs_ctx* c, const double* w, double* out, int packed) {
+  if (!c->ringA) {
+    int64_t R = 0;
+    if (const char* e = std::getenv("SCS_SPARSE_CHUNK_ROWS")) R = round_up(std::max<int64_t>(16, std::atoll(e)), 16);
+    if (R == 0) {   // two slots within min(16 GiB, a quarter of the free memory)
+      size_t fr = 0, tot = 0;
+      HCK(hipMemGetInfo(&fr, &tot));
+      const double budget = std::min(16.0 * 1073741824.0, 0.25 * (double)fr);
+      R = std::max<int64_t>(2048, (int64_t)(budget / (2.0 * c->mpad * sizeof(double))) / 2048 * 2048);
+    }
+    c->ring_rows = std::min(R, c->Npad);
+    c->ringA = dalloc<double>(c, (size_t)2 * c->ring_rows * c->mpad);
+    c->ring_r0[0] = c->ring_r0[1] = -1;
+  }
+  const int64_t R = c->ring_rows;
+  const int64_t nchunk = ceil_div(std::max<int64_t>(c->N, 1), R);
+  for (int64_t k = 0; k < nchunk; ++k) {
+    const int s = (int)(k & 1);
+    double* slot = c->ringA + (size_t)s * R * c->mpad;
+    const int64_t r0 = k * R, n = std::min(R, c->N - r0);
+    if (c->ring_r0[s] >= 0)
+      HCK(launch_densify_range(c->rowptr, c->colidx, c->val, c->sp_f32, c->ring_r0[s], c->ring_n[s], R, 1, slot, c->st));
+    HCK(launch_densify_range(c->rowptr, c->colidx, c->val, c->sp_f32, r0, n, R, 0, slot, c->st));
+    c->ring_r0[s] = r0;
+    c->ring_n[s] = n;
+    const int mode = packed | (k > 0 ? 2 : 0);
+    const int64_t nk = round_up(std::max<int64_t>(n, 1), 16);   // w + r0 + nk <= w + Npad
+    if (c->gwork)
+      HCK(gram_launch_sched(slot, R / 16, w + r0, nk, c->gwork, c->gseglen, c->gnsplit, c->gcomb, c->gncomb, c->gpart,
+                            out, c->mpad, mode, c->tall, c->st));
+    else
+      HCK(gram_launch(slot, R / 16, w + r0, nk, c->tiles, c->ntiles, out, c->mpad, mode, c->tall, c->st));
+  }
+}
+
 // v != nullptr: the same launch forms Aᵀv of the local rows into vout (fused, gram_fuse_ok)
 void gram_main(scs_ctx* c, const double* w, double* out, int packed, const double* v = nullptr,
                double* vout = nullptr) {
+  if (sparse_streams(c)) {
+    if (v) fail(c, SCS_ERR_ARG, "internal: the streaming sparse Gram forms no Aᵀv");
+    gram_main_stream(c, w, out, packed);
+    return;
+  }
   const double* A = dense_A(c);
   const int npiece = (v && c->gwork) ? std::max(c->gnsplit, 1) : 1;
   if (v && npiece > 1) HCK(hipMemsetAsync(c->vpart, 0, sizeof(double) * npiece * c->mpad, c->st));
@@ -950,7 +1028,8 @@ void gram_and_reduce(scs_ctx* c, const double* w, const double* v, double* vec_d
   hipEvent_t e0;
   const bool cacheable = c->gram_cache && gram_x_independent(c);
   const size_t gbytes = sizeof(double) * (size_t)c->mpad * c->mpad;
-  const bool fuse = !cacheable && gram_fuse_ok(c->tall);
+  // sparse A: Aᵀv from the CSC copy (a streaming Gram has no whole-A pass to ride on)
+  const bool fuse = !cacheable && !c->sparse && gram_fuse_ok(c->tall);
   if (!fuse) gemv_t_local(c, v, vec_dev);
   if (cacheable && c->Gk && c->gk_gen == c->data_gen) {   // the reduced Gram of an earlier step
     c->g_from_cache = true;
@@ -1160,6 +1239,7 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
   const double Mg = get_Mg(c, c->Mh, c->nu, c->mu, m);
   HCK(launch_score_tail(c->x, c->d, c->gr, c->Hr, m, c->lam, Mg, step, nullptr, prox_args(c), c->hinv, c->zb, c->xn,
                         c->dxv, c->scal, c->st));
+  if (c->dev_loop) return;   // x_new stays in c->xn, pri_res_norm in scal[0]
   d2h(c, x_new, c->xn, m);
   if (dx) d2h(c, dx, c->dxv, m);
   d2h(c, c->hscal, c->scal, 4);
@@ -1167,17 +1247,53 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
   *pri = c->hscal[0];
 }
 
+// L-BFGS memory update decision (prox-L-BFGS-SCORE.jl:154-162) from the device's δhᵀγh, γhᵀγh:
+// accept the pair written to `slot` when δhᵀγh > 1e-10 (absolute), FIFO capped at mem
+void lbfgs_accept(scs_ctx* c, int slot, double dg, double gg) {
+  if (!(dg > 1e-10)) return;
+  if ((int)c->ring.size() == c->mem) {
+    c->spare = c->ring.front();
+    c->ring.erase(c->ring.begin());
+  } else {
+    // the next unused physical slot becomes the spare
+    std::vector<bool> used(c->mem + 1, false);
+    for (int r : c->ring) used[r] = true;
+    used[slot] = true;
+    for (int i = 0; i <= c->mem; ++i)
+      if (!used[i]) {
+        c->spare = i;
+        break;
+      }
+  }
+  c->ring.push_back(slot);
+  c->H0 = dg / gg;
+}
+
+// a memory update left in flight by the device loop: its dg / gg are in hscal[16..17] once the
+// epoch-end copy has landed (scs_iterate syncs before calling this)
+void lbfgs_settle(scs_ctx* c, bool synced) {
+  if (!c->lbfgs_pending) return;
+  if (!synced) {
+    d2h(c, c->hscal + 16, c->scal + 16, 2);
+    sync(c);
+  }
+  c->lbfgs_pending = false;
+  lbfgs_accept(c, c->lbfgs_slot, c->hscal[16], c->hscal[17]);
+}
+
 // ProxLQNSCORE step (prox-L-BFGS-SCORE.jl:69-169)
 void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, double* x_new, double* dx,
               double* pri) {
   const int64_t m = c->m;
+  lbfgs_settle(c, false);
   HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
   grad_q_dev(c, xh, c->x, c->gq);  // ∇q = grad_f(x) + λgr
   const int k = (int)c->ring.size();
   if (iter == 1 || k == 0) {
     HCK(launch_neg(c->gq, m, c->d, c->st));
   } else {
-    HCK(hipMemcpyAsync(c->d_order, c->ring.data(), sizeof(int) * k, hipMemcpyHostToDevice, c->st));
+    std::memcpy(c->hring, c->ring.data(), sizeof(int) * k);   // pinned: a truly asynchronous upload
+    HCK(hipMemcpyAsync(c->d_order, c->hring, sizeof(int) * k, hipMemcpyHostToDevice, c->st));
     HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->tlwork,
                         c->st));
   }
@@ -1203,38 +1319,27 @@ void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, dou
   const double Mg = get_Mg(c, c->Mh, c->nu, c->mu, m);
   HCK(launch_score_tail(c->x, c->d, c->gr, c->Hr, m, c->lam, Mg, step, step_dev, prox_args(c), c->hinv, c->zb, c->xn,
                         c->dxv, c->scal, c->st));
-  d2h(c, x_new, c->xn, m);
-  if (dx) d2h(c, dx, c->dxv, m);
-  d2h(c, c->hscal, c->scal, 4);
-  sync(c);
-  *pri = c->hscal[0];
-  // δh = x_new − x (prox) | dx ; ∇q_new = grad_f(x_new) + λ gr(x_new)
-  const double* dh = c->use_prox ? c->zb : c->dxv;
-  if (c->use_prox) HCK(launch_sub(c->xn, c->x, m, c->zb, c->st));
-  // keep δh safe from grad_q_dev's scratch use of zb
-  HCK(hipMemcpyAsync(c->q, dh, sizeof(double) * m, hipMemcpyDeviceToDevice, c->st));
+  if (!c->dev_loop) {
+    d2h(c, x_new, c->xn, m);
+    if (dx) d2h(c, dx, c->dxv, m);
+    d2h(c, c->hscal, c->scal, 4);
+    sync(c);
+    *pri = c->hscal[0];
+  }
+  // δh = x_new − x (prox) | dx (into q / dxv: grad_q_dev's smoother scratch is zb, hinv);
+  // ∇q_new = grad_f(x_new) + λ gr(x_new)
+  const double* dh = c->dxv;
+  if (c->use_prox) {
+    HCK(launch_sub(c->xn, c->x, m, c->q, c->st));
+    dh = c->q;
+  }
   grad_q_dev(c, x_new, c->xn, c->gqn);
   const int slot = c->spare;
-  HCK(launch_lbfgs_update(c->q, c->gqn, c->gq, m, c->S + (int64_t)slot * c->mpad, c->Yv + (int64_t)slot * c->mpad,
+  HCK(launch_lbfgs_update(dh, c->gqn, c->gq, m, c->S + (int64_t)slot * c->mpad, c->Yv + (int64_t)slot * c->mpad,
                           c->scal + 16, c->scal + 64, c->st));
-  d2h(c, c->hscal + 16, c->scal + 16, 2);
-  sync(c);
-  const double dg = c->hscal[16], gg = c->hscal[17];
-  if (dg > 1e-10) {  // prox-L-BFGS-SCORE.jl:154-162
-    if ((int)c->ring.size() == c->mem) {
-      c->spare = c->ring.front();
-      c->ring.erase(c->ring.begin());
-    } else {
-      // the next unused physical slot becomes the spare
-      std::vector<bool> used(c->mem + 1, false);
-      for (int r : c->ring) used[r] = true;
-      used[slot] = true;
-      for (int i = 0; i <= c->mem; ++i)
-        if (!used[i]) { c->spare = i; break; }
-    }
-    c->ring.push_back(slot);
-    c->H0 = dg / gg;
-  }
+  c->lbfgs_pending = true;
+  c->lbfgs_slot = slot;
+  if (!c->dev_loop) lbfgs_settle(c, false);
 }
 
 }  // namespace
@@ -1279,6 +1384,7 @@ int scs_destroy(scs_ctx* c) {
   if (c->rccl) (void)ncclCommDestroy(c->rccl);
   for (auto& a : c->allocs) (void)hipFree(a.p);
   if (c->hscal) (void)hipHostFree(c->hscal);
+  if (c->hring) (void)hipHostFree(c->hring);
   lu_aux_free(&c->lu);
   if (c->own_stream) (void)hipStreamDestroy(c->st);
   delete c;
@@ -1394,6 +1500,10 @@ static void reset_data(scs_ctx* c) {
   }
   c->sparse = false;
   dfree_t(c, c->Ad);
+  dfree_t(c, c->ringA);
+  c->sp_mode = 0;
+  c->ring_rows = 0;
+  c->ring_r0[0] = c->ring_r0[1] = -1;
   dfree_t(c, c->Gk);
   ++c->data_gen;
   c->nnz = 0;
@@ -1869,6 +1979,9 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
       c->S = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
       c->Yv = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
       c->d_order = dalloc<int>(c, mem + 1);
+      if (c->hring) (void)hipHostFree(c->hring);
+      c->hring = nullptr;
+      HCK(hipHostMalloc((void**)&c->hring, sizeof(int) * (mem + 1), hipHostMallocDefault));
       c->ab = dalloc<double>(c, 2 * (mem + 1));
       sync(c);
     }
@@ -1876,6 +1989,7 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
     c->ring.clear();
     c->spare = 0;
     c->H0 = 1.0;
+    c->lbfgs_pending = false;
     c->method_set = true;
     invalidate_caches(c);
   });
@@ -2051,6 +2165,7 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     c->ring.clear();
     c->spare = 0;
     c->H0 = 1.0;
+    c->lbfgs_pending = false;
     invalidate_caches(c);
     // x, x_prev, x_new in pinned host memory: their per-epoch uploads / the x_new download are
     // DMA transfers instead of staged pageable copies (the arrays are only touched after syncs)
@@ -2092,6 +2207,82 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
       ~Unselect() { c->bview = -1; }
     } unselect{c};
     double last_nx = 0.0, last_ndx = 0.0;
+    // Device-resident loop (the full batch of a data loss): x, x_prev, x_new never leave the
+    // device; get_reg(x), f(x), rel_error and the two norms of the termination test are reduced
+    // on the device and read back with pri_res_norm (and L-BFGS's δhᵀγh) in ONE copy + sync at the
+    // end of each epoch -- the GPU only idles for that hand-off.  Same kernels, same order as the
+    // per-call path, so the histories equal the host loop's (the norms differ in summation order
+    // only; test_device_loop_matches_host_loop).
+    const bool dev_ok = nb == 0 && !c->generic && c->loss != SCS_LOSS_QUADRATIC && c->loss != SCS_LOSS_ROSENBROCK;
+    if (dev_ok) {
+      struct DevLoop {
+        scs_ctx* c;
+        explicit DevLoop(scs_ctx* cc) : c(cc) { c->dev_loop = true; }
+        ~DevLoop() { c->dev_loop = false; }
+      } devloop(c);
+      h2d(c, c->xstar, x_star, m);
+      h2d(c, c->x, x0, m);
+      HCK(hipMemcpyAsync(c->xp, c->x, sizeof(double) * m, hipMemcpyDeviceToDevice, c->st));
+      double* hs = c->hscal;
+      auto rel_from = [&](double ss) {
+        if (rel_kind == 1) return ss / (double)m;
+        return jmax(std::sqrt(ss) / jmax(nstar, 1.0), x_tol);
+      };
+      for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
+        double dt = now();
+        // f(x): the z of x is cached (the previous step's ∇q(x_new) / the Newton step's forward)
+        // except at epoch 1; its value is copied out of the deferred slot before the step's
+        // forward at x_new reuses it
+        forward(c, x, c->x, 0, false);
+        HCK(hipMemcpyAsync(c->scal + FX_SLOT, c->scal + ZF_SLOT, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+        HCK(launch_reg_value(prox_args(c), c->x, m, c->scal + RX_SLOT, c->scal + 64 + 2 * 256, c->st));
+        hipEvent_t e0;
+        tbegin(c, T_STEP, &e0);
+        tag_slot(x_new).v = c->xtag_next++;   // the step writes x_new (c->xn)
+        if (c->method == SCS_PROX_LQNSCORE)
+          step_lqn(c, x, x_prev, epoch, x_new, nullptr, &pri);
+        else
+          step_newton(c, x, epoch, x_new, nullptr, &pri);
+        tend(c, T_STEP, e0);
+        HCK(launch_norms3(c->x, c->xstar, c->xn, m, c->scal + NRM_SLOT, c->scal + 64 + 3 * 256, c->st));
+        d2h(c, hs, c->scal, LOOP_SLOTS);
+        sync(c);
+        lbfgs_settle(c, true);
+        const double fval = loss_scale_value(c, hs[FX_SLOT]);
+        const double obj = fval + hs[RX_SLOT];
+        const double rel = rel_from(hs[NRM_SLOT]);
+        const double frel = frel_of(obj);
+        push(obj, fval, pri, rel, frel, dt);
+        if (epoch == max_epoch) push(obj, fval, pri, rel, frel, now());   // iterate.jl:219-231
+        pri = hs[0];
+        const double nx = std::sqrt(hs[NRM_SLOT + 1]), ndx = std::sqrt(hs[NRM_SLOT + 2]);
+        const bool stop = ndx < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol;
+        if (stop && epoch != max_epoch) {   // iterate.jl:235-247: stats of x_new
+          dt = now();
+          double fv = eval_f_dev(c, x_new, c->xn);
+          const double ob = fv + eval_reg_dev(c, c->xn);
+          HCK(launch_norms3(c->xn, c->xstar, nullptr, m, c->scal + NRM_SLOT, c->scal + 64 + 3 * 256, c->st));
+          d2h(c, hs + NRM_SLOT, c->scal + NRM_SLOT, 1);
+          sync(c);
+          push(ob, fv, pri, rel_from(hs[NRM_SLOT]), frel_of(ob), dt);
+        }
+        // x_prev <- x, x <- x_new: rotate the device buffers and the host identities' tags
+        std::swap(x_prev, x);
+        tag_slot(x).v = tag_slot(x_new).v;
+        double* t = c->xp;
+        c->xp = c->x;
+        c->x = c->xn;
+        c->xn = t;
+        ++epochs;
+        if (stop) break;
+      }
+      d2h(c, x_out, c->x, m);
+      sync(c);
+      *n_hist = nh;
+      *epochs_out = epochs;
+      if (c->timing) tresolve(c);
+      return;
+    }
     for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
       double dt = now();
       double fval = 0.0;
@@ -2308,7 +2499,7 @@ int scs_gram_atv_eval(scs_ctx* c, const double* w, const double* v, const int64_
     std::memcpy(wp.data(), v, sizeof(double) * c->N);
     h2d(c, c->vN, wp.data(), c->Npad);
     ensure_gram(c);
-    const bool fuse = gram_fuse_ok(c->tall) != 0;
+    const bool fuse = gram_fuse_ok(c->tall) != 0 && !c->sparse;
     hipEvent_t e0;
     tbegin(c, T_GRAM, &e0);
     gram_main(c, c->wN, c->G, 0, fuse ? c->vN : nullptr, c->gtmp);

@@ -372,6 +372,34 @@ hipError_t launch_densify(const int64_t* rowptr, const int* col, const void* val
   return hipGetLastError();
 }
 
+// Streaming sparse Gram (scsopt.cpp gram_main): CSR rows [r0, r0 + n) -> the panel-blocked slot Ab
+// (S stages), entries summed in CSR order (duplicates race-free); zero = 1 writes zeros at the
+// same positions instead, which clears a slot for its next chunk (the slot is otherwise zero).
+template <typename V>
+__global__ void densify_range_kernel(const int64_t* __restrict__ rowptr, const int* __restrict__ col,
+                                     const V* __restrict__ val, int64_t r0, int64_t n, int64_t S, int zero,
+                                     double* __restrict__ Ab) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t p = rowptr[r0 + r]; p < rowptr[r0 + r + 1]; ++p) {
+      double* dst = Ab + tiled_off(S, r, col[p]);
+      if (zero) *dst = 0.0;
+      else *dst += (double)val[p];
+    }
+}
+
+hipError_t launch_densify_range(const int64_t* rowptr, const int* col, const void* val, int f32, int64_t r0,
+                                int64_t n, int64_t Npad_b, int zero, double* Ab, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), 16384);
+  if (f32)
+    hipLaunchKernelGGL(densify_range_kernel<float>, dim3(grid), dim3(256), 0, st, rowptr, col, (const float*)val, r0,
+                       n, Npad_b / 16, zero, Ab);
+  else
+    hipLaunchKernelGGL(densify_range_kernel<double>, dim3(grid), dim3(256), 0, st, rowptr, col, (const double*)val,
+                       r0, n, Npad_b / 16, zero, Ab);
+  return hipGetLastError();
+}
+
 // Minibatch of a sparse A: CSR rows rows[0..n) -> dense panel-blocked batch Ab (Npad_b rows,
 // zeroed by the caller), y -> yb.  One thread per batch row, entries in CSR order.
 template <typename V>

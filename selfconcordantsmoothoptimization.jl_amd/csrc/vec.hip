@@ -804,6 +804,56 @@ hipError_t launch_reg_value(const ProxArgsH& Ph, const double* x, int64_t m, dou
   return hipGetLastError();
 }
 
+// optim_loop!'s vector norms on the device (iterate.jl:192-197, :234): out = [Σ(x − xs)², Σx², Σ(xn − x)²]
+// over G <= TAIL_G workgroups, fixed-order partial sums (xs / xn may be null: that sum is 0)
+__global__ __launch_bounds__(TAIL_T) void norms_part_kernel(const double* __restrict__ x, const double* __restrict__ xs,
+                                                            const double* __restrict__ xn, int64_t m,
+                                                            double* __restrict__ part) {
+  __shared__ double sh[TAIL_T / 64];
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)gridDim.x * TAIL_T) {
+    const double xi = x[i];
+    if (xs) {
+      const double t = xs[i] - xi;
+      a += t * t;
+    }
+    b += xi * xi;
+    if (xn) {
+      const double t = xn[i] - xi;
+      c += t * t;
+    }
+  }
+  a = block_sum<TAIL_T>(a, sh);
+  b = block_sum<TAIL_T>(b, sh);
+  c = block_sum<TAIL_T>(c, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = a;
+    part[TAIL_G + blockIdx.x] = b;
+    part[2 * TAIL_G + blockIdx.x] = c;
+  }
+}
+
+__global__ __launch_bounds__(64) void norms_final_kernel(const double* __restrict__ part, int G,
+                                                         double* __restrict__ out) {
+  __shared__ double sh[1];
+  const double a = fixed_sum(part, G, sh);
+  const double b = fixed_sum(part + TAIL_G, G, sh);
+  const double c = fixed_sum(part + 2 * TAIL_G, G, sh);
+  if (threadIdx.x == 0) {
+    out[0] = a;
+    out[1] = b;
+    out[2] = c;
+  }
+}
+
+hipError_t launch_norms3(const double* x, const double* xs, const double* xn, int64_t m, double* out, double* part,
+                         hipStream_t st) {
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(TAIL_G, ceil_div(m, 4 * TAIL_T)));
+  hipLaunchKernelGGL(norms_part_kernel, dim3(G), dim3(TAIL_T), 0, st, x, xs, xn, m, part);
+  hipLaunchKernelGGL(norms_final_kernel, dim3(1), dim3(64), 0, st, part, G, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_dot(const double* a, const double* b, int64_t m, double* out, hipStream_t st) {
   hipLaunchKernelGGL(dot_kernel, dim3(1), dim3(VB), 0, st, a, b, m, out);
   return hipGetLastError();

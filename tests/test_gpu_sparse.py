@@ -175,3 +175,39 @@ def test_c5_fp32_vs_fp64_arm():
     n = min(len(s64.obj), len(s32.obj))
     np.testing.assert_allclose(s32.obj[:n], s64.obj[:n], rtol=1e-5)
     np.testing.assert_allclose(s32.x, s64.x, atol=1e-3)
+
+
+@pytest.mark.parametrize("case,tall", [("ggn_logistic", "0"), ("nscore_logistic", "0"), ("ggn_logistic", "1")])
+def test_streaming_sparse_gram(case, tall, monkeypatch):
+    """§8f rank 3: a sparse A whose dense mirror is refused (SCS_SPARSE_MIRROR_MAX_GB=0) -- the Gram
+    streams the CSR through a ring of two 1024-row dense slots (SCS_SPARSE_CHUNK_ROWS), accumulating
+    N / 1024 chunk launches of the production kernel (scheduled K-split tail + combine included).
+    Trajectory vs the oracle (rtol 1e-8) and vs the mirror path (rtol 1e-12)."""
+    import scipy.sparse as sp
+    monkeypatch.setenv("SCS_GRAM_TALL", tall)
+    rng = np.random.default_rng(43)
+    N, m = 3000 + 37, (256 if tall == "1" else 160)
+    A = sp.random(N, m, density=0.04, random_state=9, format="csr", data_rvs=rng.standard_normal)
+    y = (rng.random(N) < 0.5).astype(float)
+    x0 = rng.standard_normal(m) * 0.3
+    if case == "nscore_logistic":
+        y = 2 * y - 1
+        f, out, of = losses.logistic_margin(1.0 / N), None, O.Loss("logistic_margin", 1.0 / N)
+        mk, omk = scsopt.ProxNSCORE, O.ProxNSCORE
+    else:
+        f, out = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N)
+        of = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+        mk, omk = scsopt.ProxGGNSCORE, O.ProxGGNSCORE
+    runs = {}
+    for mode, cap in (("stream", "0"), ("mirror", "1000")):
+        monkeypatch.setenv("SCS_SPARSE_MIRROR_MAX_GB", cap)
+        monkeypatch.setenv("SCS_SPARSE_CHUNK_ROWS", "1024")
+        p = scsopt.Problem(A, y, x0, f, 1e-3, out_fn=out)
+        runs[mode] = scsopt.iterate(mk(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=6, verbose=0)
+    osol = O.iterate(omk(), O.Problem(A.toarray(), y, x0, of, 1e-3), "l1", O.PHuberSmootherL1L2(1.0), max_epoch=6)
+    st, mi = runs["stream"], runs["mirror"]
+    assert st.epochs == osol.epochs == mi.epochs and len(st.obj) == len(osol.obj)
+    np.testing.assert_allclose(st.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(st.x, osol.x, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(st.obj, mi.obj, rtol=1e-12, atol=0)
+
