@@ -105,6 +105,19 @@ hipError_t launch_prox_only(const ProxArgsH& P, const double* z, const double* H
 hipError_t launch_reg_value(const ProxArgsH& P, const double* x, int64_t m, double* out, double* part,
                             hipStream_t st);
 hipError_t launch_dot(const double* a, const double* b, int64_t m, double* out, hipStream_t st);
+// fused ProxLQNSCORE epoch passes (vec.hip): R = LQ_NPART x 256 partials
+enum { LQ_DG = 0, LQ_GG, LQ_ETA, LQ_REG, LQ_NA, LQ_NB, LQ_NC, LQ_PRI, LQ_NPART };
+constexpr int LQ_G = 256;
+hipError_t launch_lqn_eta(const double* gr, const double* Hr, int64_t m, double lam, double* hinv, double* R,
+                          hipStream_t st);
+hipError_t launch_lqn_tail(const double* x, const double* d, int neg, int64_t m, double Mg, double step,
+                           const ProxArgsH& P, const double* hinv, double* x_new, double* dx, double* dh, double* R,
+                           double* scal, hipStream_t st);
+hipError_t launch_lqn_post(const double* tpart, int nchunk, int64_t ldp, int64_t m, double lam, int skind, double mu,
+                           const double* sa, const double* sb, const ProxArgsH& P, const double* xs, const double* x,
+                           const double* xn, const double* gq, const double* dh, double* gqn, double* Sslot,
+                           double* Yslot, double* gr, double* Hr, double* hinv, double* R, double* scal, int rx_slot,
+                           int nrm_slot, hipStream_t st);
 // out[0..3) = Σ(x − xs)², Σx², Σ(xn − x)² (xs / xn may be null); part: 3 x 256 doubles
 hipError_t launch_norms3(const double* x, const double* xs, const double* xn, int64_t m, double* out, double* part,
                          hipStream_t st);

@@ -159,6 +159,7 @@ struct scs_ctx {
          *ab = nullptr, *tlwork = nullptr, *scal = nullptr, *gcache[2] = {nullptr, nullptr};
   double* hscal = nullptr;  // pinned host scalars
   double* xstar = nullptr;  // model.x on the device (scs_iterate's rel_error)
+  double* lqR = nullptr;    // fused ProxLQNSCORE epoch: LQ_NPART x 256 partial sums
   bool dev_loop = false;    // scs_iterate's device-resident loop: steps leave x_new / pri on the device
   // N-space workspace
   int nsplit = 1;
@@ -477,6 +478,8 @@ void alloc_mspace(scs_ctx* c) {
   c->scal = dalloc<double>(c, 64 + 6 * 256);
   dfree_t(c, c->xstar);
   c->xstar = dalloc<double>(c, mp);
+  dfree_t(c, c->lqR);
+  c->lqR = dalloc<double>(c, (size_t)LQ_NPART * LQ_G);
   if (!c->hscal) HCK(hipHostMalloc((void**)&c->hscal, 64 * sizeof(double), hipHostMallocDefault));
 }
 
@@ -698,17 +701,22 @@ int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
   return nsplit;
 }
 
-// out (device, m) = Aᵀ v over the local rows (dense: chunked column sums +
-// fixed-order finalize; sparse: one CSC gather pass)
-void matvec_t(scs_ctx* c, const double* v, double* out) {
+// the partial rows of Aᵀ v over the local rows into c->tpart (stride mpad); returns their count
+int matvec_t_part(scs_ctx* c, const double* v) {
   if (c->sparse) {
     const auto& B = c->bcsc;
     HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, c->sp_f32, v, c->m, c->N, B.shift, c->nnz, c->tpart, c->mpad, c->st));
-    HCK(launch_gemv_t_finalize(c->tpart, B.nblk, c->mpad, c->m, out, c->st));
-    return;
+    return B.nblk;
   }
   HCK(launch_gemv_t(c->A, c->nstage, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
-  HCK(launch_gemv_t_finalize(c->tpart, c->nchunk, c->mpad, c->m, out, c->st));
+  return c->nchunk;
+}
+
+// out (device, m) = Aᵀ v over the local rows (dense: chunked column sums +
+// fixed-order finalize; sparse: one CSC gather pass)
+void matvec_t(scs_ctx* c, const double* v, double* out) {
+  const int np = matvec_t_part(c, v);
+  HCK(launch_gemv_t_finalize(c->tpart, np, c->mpad, c->m, out, c->st));
 }
 
 void require_dense(scs_ctx* c, const char* what) {
@@ -2228,6 +2236,95 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         if (rel_kind == 1) return ss / (double)m;
         return jmax(std::sqrt(ss) / jmax(nstar, 1.0), x_tol);
       };
+      // ProxLQNSCORE, fused epoch (lqn_tail / lqn_post, vec.hip): 7 launches per epoch around the two
+      // products instead of ~22; every quantity the history and the termination test read for the
+      // NEXT x is produced by this epoch's post pass, so the hand-off at the epoch end is the only
+      // one.  Same per-element arithmetic and partial-sum order as the unfused step (bit-identical
+      // x, obj, fval, pri_res_norm; SCS_LQN_FUSED=0 selects the unfused epoch).
+      const char* fz = std::getenv("SCS_LQN_FUSED");
+      const bool fused = c->method == SCS_PROX_LQNSCORE && c->ss_type == 1 && m >= 16384 && !sharded(c) &&
+                         c->smooth != SCS_SMOOTH_PHUBER_GL && c->smooth != SCS_SMOOTH_OSBA_GL &&
+                         !(c->use_prox && c->reg == SCS_REG_GL) && c->reg != SCS_REG_GL && !(fz && fz[0] == '0');
+      if (fused) {
+        const double Mg = get_Mg(c, c->Mh, c->nu, c->mu, m);
+        const double step = c->has_L ? jl_min_h(1 / c->L, 1.0) : 0.5;
+        // state at x0: ∇q(x0) -> gq, then smoother(x0) -> gr, Hr, hinv and η's partials, f / get_reg / norms
+        grad_q_dev(c, x, c->x, c->gq);
+        HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
+        HCK(launch_lqn_eta(c->gr, c->Hr, m, c->lam, c->hinv, c->lqR, c->st));
+        HCK(launch_reg_value(prox_args(c), c->x, m, c->scal + RX_SLOT, c->scal + 64 + 2 * 256, c->st));
+        HCK(launch_norms3(c->x, c->xstar, nullptr, m, c->scal + NRM_SLOT, c->scal + 64 + 3 * 256, c->st));
+        forward(c, x, c->x, 0, false);   // cached: the z of x0 from ∇q(x0)
+        d2h(c, hs, c->scal, LOOP_SLOTS);
+        sync(c);
+        double fcur = loss_scale_value(c, hs[ZF_SLOT]), regcur = hs[RX_SLOT];
+        double relcur = rel_from(hs[NRM_SLOT]), nxcur = std::sqrt(hs[NRM_SLOT + 1]);
+        for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
+          const double dt = now();
+          const double obj = fcur + regcur;
+          const double frel = frel_of(obj);
+          push(obj, fcur, pri, relcur, frel, dt);
+          if (epoch == max_epoch) push(obj, fcur, pri, relcur, frel, now());   // iterate.jl:219-231
+          hipEvent_t e0;
+          tbegin(c, T_STEP, &e0);
+          const int k = (int)c->ring.size();
+          const bool neg = (epoch == 1 || k == 0);   // prox-L-BFGS-SCORE.jl:102-106
+          if (!neg) {
+            std::memcpy(c->hring, c->ring.data(), sizeof(int) * k);
+            HCK(hipMemcpyAsync(c->d_order, c->hring, sizeof(int) * k, hipMemcpyHostToDevice, c->st));
+            HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->tlwork,
+                                c->st));
+          }
+          HCK(launch_lqn_tail(c->x, neg ? c->gq : c->d, neg ? 1 : 0, m, Mg, step, prox_args(c), c->hinv, c->xn,
+                              c->dxv, c->q, c->lqR, c->scal, c->st));
+          tag_slot(x_new).v = c->xtag_next++;
+          forward(c, x_new, c->xn, EPI_GRAD, false);   // z = A x_new, r, f(x_new) in flight
+          hipEvent_t e1;
+          tbegin(c, T_GEMV, &e1);
+          const int np = matvec_t_part(c, c->gN);       // Aᵀ r partials
+          tend(c, T_GEMV, e1);
+          const int slot = c->spare;
+          HCK(launch_lqn_post(c->tpart, np, c->mpad, m, c->lam, c->smooth, c->mu, c->slb, c->sub, prox_args(c), c->xstar,
+                              c->x, c->xn, c->gq, c->q, c->gqn, c->S + (int64_t)slot * c->mpad,
+                              c->Yv + (int64_t)slot * c->mpad, c->gr, c->Hr, c->hinv, c->lqR, c->scal, RX_SLOT,
+                              NRM_SLOT, c->st));
+          tend(c, T_STEP, e0);
+          d2h(c, hs, c->scal, LOOP_SLOTS);
+          sync(c);
+          c->lbfgs_pending = true;
+          c->lbfgs_slot = slot;
+          lbfgs_settle(c, true);
+          pri = hs[0];
+          const double ndx = std::sqrt(hs[NRM_SLOT + 2]);
+          const double fnext = loss_scale_value(c, hs[ZF_SLOT]), regnext = hs[RX_SLOT];
+          c->zfval = fnext;
+          c->zf_pending = false;
+          const double relnext = rel_from(hs[NRM_SLOT]), nxnext = std::sqrt(hs[NRM_SLOT + 1]);
+          const bool stop = ndx < x_tol * std::max(nxcur, 1.0) || frel <= f_tol || pri < x_tol;
+          if (stop && epoch != max_epoch)   // iterate.jl:235-247: stats of x_new
+            push(fnext + regnext, fnext, pri, relnext, frel_of(fnext + regnext), now());
+          std::swap(x_prev, x);
+          tag_slot(x).v = tag_slot(x_new).v;
+          double* t = c->xp;
+          c->xp = c->x;
+          c->x = c->xn;
+          c->xn = t;
+          std::swap(c->gq, c->gqn);          // ∇q(x) of the next epoch
+          c->gvalid[0] = c->gvalid[1] = false;
+          fcur = fnext;
+          regcur = regnext;
+          relcur = relnext;
+          nxcur = nxnext;
+          ++epochs;
+          if (stop) break;
+        }
+        d2h(c, x_out, c->x, m);
+        sync(c);
+        *n_hist = nh;
+        *epochs_out = epochs;
+        if (c->timing) tresolve(c);
+        return;
+      }
       for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
         double dt = now();
         // f(x): the z of x is cached (the previous step's ∇q(x_new) / the Newton step's forward)

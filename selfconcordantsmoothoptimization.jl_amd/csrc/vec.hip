@@ -58,18 +58,13 @@ __device__ __forceinline__ double osba_hess_d(double x, double mu) {   // ostrov
   return (sqrt(v) - mu) * mu / (x * x) * pow(v, -0.5) / 2.0;
 }
 
-__global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64_t m, double mu,
-                                   const double* __restrict__ a, const double* __restrict__ b,
-                                   double* __restrict__ gr, double* __restrict__ Hr) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const double xi = x[i];
-  double g, h;
+// hμ.grad / hμ.hess of the elementwise smoothers at one coordinate (a, b: that coordinate's bounds)
+__device__ __forceinline__ void smooth_elem(int kind, double xi, double ai, double bi, double mu, double& g,
+                                            double& h) {
   if (kind == SCS_SMOOTH_PHUBER_L1L2) {
     g = huber_grad_d(xi, mu);
     h = huber_hess_d(xi, mu);
   } else if (kind == SCS_SMOOTH_PHUBER_INDBOX) {
-    const double ai = a[i], bi = b[i];
     // huber_grad_indbox (phuber-smooth.jl:83-98): note the `-x < a` test.
     if (-xi < ai) {
       g = pow(ai * ai - 2.0 * xi * ai + mu * mu + xi * xi, -0.5) * (-xi + ai);
@@ -89,7 +84,6 @@ __global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64
       h = __builtin_nan("");  // NaN x: the reference leaves the entry undefined
     }
   } else if (kind == SCS_SMOOTH_LOGEXP_INDBOX) {   // log-exp-smooth.jl:45-61 (both ifelse arms, then +)
-    const double ai = a[i], bi = b[i];
     const double g1 = (xi <= ai + mu) ? (xi - ai - 2.0 * mu) / mu : ((xi >= bi - mu) ? (xi - bi + 2.0 * mu) / mu : 0.0);
     const double g2 = (xi < ai) ? mu / (ai - xi) : ((xi > bi) ? -mu / (bi - xi) : 0.0);
     g = g1 + g2;
@@ -100,10 +94,21 @@ __global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64
     g = osba_grad_d(xi, mu);
     h = osba_hess_d(xi, mu);
   } else {  // SCS_SMOOTH_EXP_INDBOX (exponential-smooth.jl:41-50)
-    const double e = exp((-xi + a[i]) / mu);
+    const double e = exp((-xi + ai) / mu);
     g = -e;
     h = 1.0 / mu * e;
   }
+}
+
+__global__ void smooth_elem_kernel(int kind, const double* __restrict__ x, int64_t m, double mu,
+                                   const double* __restrict__ a, const double* __restrict__ b,
+                                   double* __restrict__ gr, double* __restrict__ Hr) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const bool box = kind == SCS_SMOOTH_PHUBER_INDBOX || kind == SCS_SMOOTH_LOGEXP_INDBOX ||
+                   kind == SCS_SMOOTH_EXP_INDBOX;
+  double g, h;
+  smooth_elem(kind, x[i], box ? a[i] : 0.0, box && kind != SCS_SMOOTH_EXP_INDBOX ? b[i] : 0.0, mu, g, h);
   gr[i] = g;
   Hr[i] = h;
 }
@@ -851,6 +856,157 @@ hipError_t launch_norms3(const double* x, const double* xs, const double* xn, in
   const int G = (int)std::max<int64_t>(1, std::min<int64_t>(TAIL_G, ceil_div(m, 4 * TAIL_T)));
   hipLaunchKernelGGL(norms_part_kernel, dim3(G), dim3(TAIL_T), 0, st, x, xs, xn, m, part);
   hipLaunchKernelGGL(norms_final_kernel, dim3(1), dim3(64), 0, st, part, G, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// ProxLQNSCORE epoch, fused (scs_iterate's device loop at m >= 16384; scsopt.cpp): the step's
+// elementwise work runs as two passes around the two sparse/dense products --
+//   lqn_tail   d = -∇q (or the two-loop's d), η from the partials the previous post pass left,
+//              α, dx, the prox -> x_new, δh, pri partials            (prox-L-BFGS-SCORE.jl:102-146)
+//   lqn_post   at x_new: Aᵀr = Σ of the product's partials, hμ.grad/hess, ∇q_new = Aᵀr + λ gr,
+//              the memory pair (S, Y) with δhᵀγh, γhᵀγh partials (:148-162), and for the next
+//              epoch η's partials, get_reg's and optim_loop!'s norms (iterate.jl:189-197, 234)
+// with the same per-element arithmetic and the same TAIL_G x TAIL_T fixed-order partials as the
+// separate kernels (smooth_elem, tail_eta/apply, lbfgs_update_part, reg_part), so the results
+// are bitwise those of the unfused step.  R holds LQ_NPART rows of TAIL_G partials.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TAIL_T) void lqn_tail_kernel(const double* __restrict__ x, const double* __restrict__ d,
+                                                          int neg, int64_t m, double Mg, double step, ProxArgs P,
+                                                          const double* __restrict__ hinv, double* __restrict__ x_new,
+                                                          double* __restrict__ dx, double* __restrict__ dh,
+                                                          double* __restrict__ R, double* __restrict__ scal) {
+  __shared__ double sh[TAIL_T / 64];
+  const double eta = sqrt(fixed_sum(R + LQ_ETA * TAIL_G, TAIL_G, sh));
+  const double alpha = step / (1.0 + Mg * eta);
+  const double safe_alpha = jl_min(1.0, alpha);
+  double p = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)TAIL_G * TAIL_T) {
+    const double di = neg ? -d[i] : d[i];
+    const double dxi = safe_alpha * di;
+    dx[i] = dxi;
+    const double z = x[i] + dxi;
+    double xn = z;
+    if (P.use_prox) {
+      if (P.reg == SCS_REG_L1) xn = prox_l1_d(z, hinv[i], P.lam, step);
+      else if (P.reg == SCS_REG_L2) xn = prox_l2_d(z, hinv[i], P.lam, step);
+      else xn = prox_box_d(z, P.lb[i], P.ub[i]);
+    }
+    x_new[i] = xn;
+    const double r = P.use_prox ? (xn - x[i]) : dxi;
+    dh[i] = r;
+    p += r * r;
+  }
+  const double sp = block_sum<TAIL_T>(p, sh);
+  if (threadIdx.x == 0) {
+    R[LQ_PRI * TAIL_G + blockIdx.x] = sp;
+    if (blockIdx.x == 0) {
+      scal[1] = eta;
+      scal[2] = alpha;
+      scal[3] = step;
+    }
+  }
+}
+
+__global__ __launch_bounds__(TAIL_T) void lqn_post_kernel(
+    const double* __restrict__ tpart, int nchunk, int64_t ldp, int64_t m, double lam, int skind, double mu,
+    const double* __restrict__ sa, const double* __restrict__ sb, ProxArgs P, const double* __restrict__ xs,
+    const double* __restrict__ x, const double* __restrict__ xn, const double* __restrict__ gq,
+    const double* __restrict__ dh, double* __restrict__ gqn, double* __restrict__ Sslot, double* __restrict__ Yslot,
+    double* __restrict__ gr, double* __restrict__ Hr, double* __restrict__ hinv, double* __restrict__ R) {
+  __shared__ double sh[TAIL_T / 64];
+  const bool box = skind == SCS_SMOOTH_PHUBER_INDBOX || skind == SCS_SMOOTH_LOGEXP_INDBOX ||
+                   skind == SCS_SMOOTH_EXP_INDBOX;
+  double dg = 0.0, gg = 0.0, eta = 0.0, reg = 0.0, na = 0.0, nb = 0.0, nc = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)TAIL_G * TAIL_T) {
+    // Aᵀr: the partial rows summed as gemv_t_finalize does (4 interleaved accumulators)
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int c = 0;
+    for (; c + 4 <= nchunk; c += 4) {
+      s0 += tpart[(int64_t)c * ldp + i];
+      s1 += tpart[(int64_t)(c + 1) * ldp + i];
+      s2 += tpart[(int64_t)(c + 2) * ldp + i];
+      s3 += tpart[(int64_t)(c + 3) * ldp + i];
+    }
+    for (; c < nchunk; ++c) s0 += tpart[(int64_t)c * ldp + i];
+    const double g = (s0 + s1) + (s2 + s3);
+    const double xi = xn[i];
+    double grn, hrn;
+    smooth_elem(skind, xi, box ? sa[i] : 0.0, box && skind != SCS_SMOOTH_EXP_INDBOX ? sb[i] : 0.0, mu, grn, hrn);
+    const double gqi = g + lam * grn;   // ∇q(x_new)
+    gqn[i] = gqi;
+    const double gh = gqi - gq[i];      // the memory pair
+    Yslot[i] = gh;
+    Sslot[i] = dh[i];
+    dg += dh[i] * gh;
+    gg += gh * gh;
+    gr[i] = grn;                        // the next epoch's smoother, η, h = 1 ./ Hr
+    Hr[i] = hrn;
+    const double hi = 1.0 / hrn;
+    hinv[i] = hi;
+    const double lgr = lam * grn;
+    eta += lgr * (hi * lgr);
+    if (P.reg == SCS_REG_INDBOX) reg += (xi < P.lb[i] || xi > P.ub[i]) ? 1.0 : 0.0;
+    else reg += (P.reg == SCS_REG_L2) ? xi * xi : fabs(xi);
+    const double ta = xs[i] - xi;
+    na += ta * ta;
+    nb += xi * xi;
+    const double tc = xi - x[i];
+    nc += tc * tc;
+  }
+  const double v[7] = {dg, gg, eta, reg, na, nb, nc};
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const double t = block_sum<TAIL_T>(v[k], sh);
+    if (threadIdx.x == 0) R[k * TAIL_G + blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(64) void lqn_post_final_kernel(ProxArgs P, const double* __restrict__ R,
+                                                            double* __restrict__ scal, int rx_slot, int nrm_slot) {
+  __shared__ double sh[1];
+  const double dg = fixed_sum(R + LQ_DG * TAIL_G, TAIL_G, sh);
+  const double gg = fixed_sum(R + LQ_GG * TAIL_G, TAIL_G, sh);
+  const double rs = fixed_sum(R + LQ_REG * TAIL_G, TAIL_G, sh);
+  const double na = fixed_sum(R + LQ_NA * TAIL_G, TAIL_G, sh);
+  const double nb = fixed_sum(R + LQ_NB * TAIL_G, TAIL_G, sh);
+  const double nc = fixed_sum(R + LQ_NC * TAIL_G, TAIL_G, sh);
+  const double pr = fixed_sum(R + LQ_PRI * TAIL_G, TAIL_G, sh);
+  if (threadIdx.x == 0) {
+    scal[0] = sqrt(pr);
+    scal[16] = dg;
+    scal[17] = gg;
+    scal[rx_slot] = (P.reg == SCS_REG_INDBOX) ? (rs > 0 ? __builtin_inf() : 0.0) : P.lam * rs;
+    scal[nrm_slot] = na;
+    scal[nrm_slot + 1] = nb;
+    scal[nrm_slot + 2] = nc;
+  }
+}
+
+hipError_t launch_lqn_eta(const double* gr, const double* Hr, int64_t m, double lam, double* hinv, double* R,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(tail_eta_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, gr, Hr, m, lam, hinv, R + LQ_ETA * TAIL_G);
+  return hipGetLastError();
+}
+
+hipError_t launch_lqn_tail(const double* x, const double* d, int neg, int64_t m, double Mg, double step,
+                           const ProxArgsH& Ph, const double* hinv, double* x_new, double* dx, double* dh, double* R,
+                           double* scal, hipStream_t st) {
+  ProxArgs P{Ph.reg, Ph.use_prox, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
+  hipLaunchKernelGGL(lqn_tail_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, x, d, neg, m, Mg, step, P, hinv, x_new, dx,
+                     dh, R, scal);
+  return hipGetLastError();
+}
+
+hipError_t launch_lqn_post(const double* tpart, int nchunk, int64_t ldp, int64_t m, double lam, int skind, double mu,
+                           const double* sa, const double* sb, const ProxArgsH& Ph, const double* xs, const double* x,
+                           const double* xn, const double* gq, const double* dh, double* gqn, double* Sslot,
+                           double* Yslot, double* gr, double* Hr, double* hinv, double* R, double* scal, int rx_slot,
+                           int nrm_slot, hipStream_t st) {
+  ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
+  hipLaunchKernelGGL(lqn_post_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, tpart, nchunk, ldp, m, lam, skind, mu, sa, sb,
+                     P, xs, x, xn, gq, dh, gqn, Sslot, Yslot, gr, Hr, hinv, R);
+  hipLaunchKernelGGL(lqn_post_final_kernel, dim3(1), dim3(64), 0, st, P, R, scal, rx_slot, nrm_slot);
   return hipGetLastError();
 }
 

@@ -628,3 +628,31 @@ def test_cholesky_lookahead_bit_identical(m, monkeypatch):
     ser = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=4, verbose=0)
     assert la.obj == ser.obj and la.pri_res_norm == ser.pri_res_norm and la.epochs == ser.epochs
     assert np.array_equal(bits(la.x), bits(ser.x))
+
+
+@pytest.mark.parametrize("reg,use_prox", [("l1", True), ("indbox", True), ("l2", False)])
+def test_lqn_fused_epoch_bit_identical(reg, use_prox, monkeypatch):
+    """scs_iterate's fused ProxLQNSCORE epoch (m >= 16384: lqn_tail / lqn_post around the two products)
+    against the unfused device loop (SCS_LQN_FUSED=0): identical objective / fval / pri_res_norm
+    histories and x bits (same per-element arithmetic, same partial-sum order), rel_error to rounding
+    of the norms, through an L-BFGS memory that fills (two-loop recursion active) and a run that
+    stops on x_tol."""
+    N, m = 256, 20000
+    rng = np.random.default_rng(12)
+    A = rng.standard_normal((N, m)) / np.sqrt(m)
+    y = rng.standard_normal(N)
+    x0 = rng.standard_normal(m) * 0.1
+    C_set = [-0.05, 0.05] if reg == "indbox" else None
+    p = scsopt.Problem(A, y, x0, losses.least_squares(1.0 / N), 1e-4, C_set=C_set)
+    hm = scsopt.PHuberSmootherIndBox(-0.05, 0.05, 0.5) if reg == "indbox" else scsopt.PHuberSmootherL1L2(0.5)
+    for max_epoch, x_tol in ((14, 0.0), (400, 1e-4)):
+        monkeypatch.delenv("SCS_LQN_FUSED", raising=False)
+        a = scsopt.iterate(scsopt.ProxLQNSCORE(m=6, use_prox=use_prox), p, reg, hm, max_epoch=max_epoch,
+                           x_tol=x_tol, f_tol=0.0, verbose=0)
+        monkeypatch.setenv("SCS_LQN_FUSED", "0")
+        b = scsopt.iterate(scsopt.ProxLQNSCORE(m=6, use_prox=use_prox), p, reg, hm, max_epoch=max_epoch,
+                           x_tol=x_tol, f_tol=0.0, verbose=0)
+        assert a.epochs == b.epochs and len(a.obj) == len(b.obj)
+        assert a.obj == b.obj and a.fval == b.fval and a.pri_res_norm == b.pri_res_norm
+        assert np.array_equal(bits(a.x), bits(b.x))
+        np.testing.assert_allclose(a.rel, b.rel, rtol=1e-13)
