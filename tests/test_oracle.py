@@ -216,3 +216,17 @@ def test_batched_loop_semantics(meth):
     assert len(two.obj) == 5 and two.epochs == 4   # the max_epoch entry is taken before the last batch
     assert not np.array_equal(two.x, O.iterate(meth(), small(), "l1", O.PHuberSmootherL1L2(1),
                                                max_epoch=4, x_tol=0.0, f_tol=0.0).x)
+
+
+def test_set_name_plain_labels():
+    """set_name! without the prox: the literal names / labels of prox-N-SCORE.jl:24-33,
+    prox-GGN-SCORE.jl:24-33 and prox-L-BFGS-SCORE.jl:37-46."""
+    for M, name, label in ((O.ProxNSCORE, "newtonscore", "Newton-SCORE"), (O.ProxGGNSCORE, "ggnscore", "GGN-SCORE"),
+                           (O.ProxLQNSCORE, "lbfgsscore", "LBFGS-SCORE")):
+        algs = []
+        m = M(use_prox=False)
+        O.set_name(m, algs)
+        assert (m.name, m.label) == (name, label) and algs[-1] == name
+        p = M()
+        O.set_name(p, algs)
+        assert p.name.startswith("prox-") and p.label.startswith("Prox-")
