@@ -186,6 +186,10 @@ struct scs_ctx {
   int* cinfo = nullptr;
   CholAux caux;             // two-level factorization constants (chol.hip)
   LUAux lu;                 // blocked LU (lu.hip): the non-SPD fallback and the GGN sample-space system
+  double* luM = nullptr;    // scs_lu_eval's system / rhs / info, kept so the LU graphs replay
+  double* lub = nullptr;
+  int* luinfo = nullptr;
+  int64_t lu_np = 0;
   // GGN sample-space branch (N + 1 <= m): Aᵀ copy, sample Gram, (N+1)² system
   double *At = nullptr, *Ps = nullptr, *Ms = nullptr, *bS = nullptr, *uN = nullptr, *hvec = nullptr, *hg = nullptr;
   int64_t NpS = 0;
@@ -2538,9 +2542,21 @@ int scs_lu_eval(scs_ctx* c, int64_t n, const double* A, const double* b, double*
     if (n < 1 || !A || !b || !x) fail(c, SCS_ERR_ARG, "scs_lu_eval: bad arguments");
     HCK(hipSetDevice(c->dev));
     const int64_t np = round_up(n, 128);
-    double* M = dalloc<double>(c, (size_t)np * np);
-    double* bb = dalloc<double>(c, np);
-    int* dinfo = dalloc<int>(c, 1);
+    if (c->lu_np != np) {
+      if (c->luM) dfree_t(c, c->luM);
+      if (c->lub) dfree_t(c, c->lub);
+      if (c->luinfo) dfree_t(c, c->luinfo);
+      c->luM = dalloc<double>(c, (size_t)np * np);
+      c->lub = dalloc<double>(c, np);
+      c->luinfo = dalloc<int>(c, 1);
+      c->lu_np = np;
+    }
+    double* M = c->luM;
+    double* bb = c->lub;
+    int* dinfo = c->luinfo;
+    HCK(hipMemsetAsync(M, 0, sizeof(double) * np * np, c->st));
+    HCK(hipMemsetAsync(bb, 0, sizeof(double) * np, c->st));
+    HCK(hipMemsetAsync(dinfo, 0, sizeof(int), c->st));
     HCK(hipMemcpy2DAsync(M, sizeof(double) * np, A, sizeof(double) * n, sizeof(double) * n, n, hipMemcpyHostToDevice,
                          c->st));
     HCK(hipMemcpyAsync(bb, b, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
@@ -2557,9 +2573,6 @@ int scs_lu_eval(scs_ctx* c, int64_t n, const double* A, const double* b, double*
     if (ipiv) HCK(hipMemcpyAsync(ipiv, c->lu.ipiv, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->st));
     sync(c);
     if (info) *info = hinfo;
-    dfree_t(c, M);
-    dfree_t(c, bb);
-    dfree_t(c, dinfo);
     if (c->timing) tresolve(c);
   });
 }
