@@ -322,29 +322,46 @@ __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, i
 // that C tile traffic: 2·128 KiB per 4.2 MFLOP tile).
 static int outer_block();
 
+// The bulk stream (the lookahead's trailing updates, 2 gram_sia workgroups per CU fill every CU
+// they get) leaves SCS_CHOL_RESERVE_CUS CUs (default 8, one per XCD) to the serial
+// chain on the context stream: a chol_diag_kernel workgroup that shares its CU with MFMA-bound
+// trailing-update waves runs ~7x slower (m = 32768: 682 us against 94 us alone), and the chain
+// of 256 of them then bounds the factor.  CU masking is best effort: a failure falls back to an
+// unmasked stream.
+static hipError_t create_bulk_stream(hipStream_t* s) {
+  const char* env = getenv("SCS_CHOL_RESERVE_CUS");
+  const int reserve = env ? atoi(env) : 8;
+  int dev = 0, ncu = 0;
+  if (reserve > 0 && hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 4 * reserve) {
+    // mask bit i is CU i of the XCD-interleaved numbering (XCD i % 8; measured: clearing bits
+    // i % 16 == 15 took 16 CUs from one XCD and slowed the XCD-balanced Gram schedule 1.6x), so
+    // the top `reserve` bits take reserve / 8 CUs from every XCD
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu - reserve; ++i) mask[i / 32] |= 1u << (i % 32);
+    if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
-  const int OB = outer_block();
   a->nblk = nblk;
   std::vector<double> hw((size_t)CB + mpad, -1.0);
   for (int i = 0; i < CB; ++i) hw[i] = 1.0;
-  std::vector<int2> rl, sl;
+  std::vector<int2> rl;
   for (int R = 1; R <= 4; ++R)
     for (int j = 0; j < nblk; ++j)
       for (int i = 0; i < R; ++i) rl.push_back(make_int2(i, j));   // bj-major: first R*C = R x C rectangle
-  // pairs (i >= j) with j < OB, row-major: the first sum_{i<n} min(i+1, OB) entries cover the
-  // first OB block columns of an n x n lower triangle
-  for (int i = 0; i < nblk; ++i)
-    for (int j = 0; j <= i && j < OB; ++j) sl.push_back(make_int2(i, j));
   hipError_t e = hipMalloc(&a->w, sizeof(double) * hw.size());
   if (e == hipSuccess) e = hipMalloc(&a->rect, sizeof(int2) * rl.size());
-  if (e == hipSuccess) e = hipMalloc(&a->strip, sizeof(int2) * sl.size());
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(a->strip, sl.data(), sizeof(int2) * sl.size(), hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&a->st2, hipStreamNonBlocking);
+  if (e == hipSuccess) e = create_bulk_stream(&a->st2);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev2, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev3, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   return e;
 }
@@ -353,14 +370,13 @@ void chol_aux_free(CholAux* a) {
   if (a->st2) (void)hipStreamSynchronize(a->st2);
   if (a->w) (void)hipFree(a->w);
   if (a->rect) (void)hipFree(a->rect);
-  if (a->strip) (void)hipFree(a->strip);
   if (a->ev1) (void)hipEventDestroy(a->ev1);
   if (a->ev2) (void)hipEventDestroy(a->ev2);
+  if (a->ev3) (void)hipEventDestroy(a->ev3);
   if (a->st2) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
-  a->strip = nullptr;
-  a->ev1 = a->ev2 = nullptr;
+  a->ev1 = a->ev2 = a->ev3 = nullptr;
   a->st2 = nullptr;
 }
 
@@ -397,13 +413,20 @@ static hipError_t strip_solve(double* G, int64_t ld, const double* W, const Chol
   return strip_solve(G, ld, W, a, mid, hi, c0, nc, st);
 }
 
-// Lookahead (default; SCS_CHOL_LA=0 off): the trailing update C of outer block t is cut into
-//   C1 = the next outer block's strip (block pairs whose smaller index is in block t+1), on st;
-//   C2 = everything right of / below that strip, on st2,
-// so block t+1's serial diagonal steps (A, 128 chol_diag_kernel launches of one workgroup
-// each over the whole factor) and strip solve (B) run while C2_t fills the machine.
-// Every element still receives its updates in block order (C1_{t+1} waits for C2_t, which
-// also covers strip t+2's rows), so U is bit-identical to the serial order.
+// Lookahead (default; SCS_CHOL_LA=0 off).  Outer block t's strip solve B and trailing update C
+// are cut so that only what outer block t+1's serial diagonal steps need stays on the chain
+// stream st:
+//   Ba  (st)  strip solve of the next block's OB columns;
+//   C1a (st)  the next outer block's diagonal triangle -= X_tᵀ X_t (latency kernel);
+//   Bb  (st2) strip solve of the columns beyond the next block (starts when A_t is done);
+//   C12 (st2) everything else of the trailing update in ONE launch: the rest of the next
+//             block's strip and all pairs beyond it (the full trailing tile list minus its
+//             first OB(OB+1)/2 entries, which are C1a's).
+// st2 is the bulk stream (CU-masked: create_bulk_stream) and streams Bb_t, C12_t, Bb_{t+1}, ...
+// back to back whenever the chain (A + Ba + C1a) is shorter than C12 (large m); the chain's
+// Ba_{t+1} / C1a_{t+1} wait for C12_t (same elements).  Every element still receives its
+// updates in block order with the same per-tile arithmetic (the kernels share one MFMA order),
+// so U is bit-identical to the serial order.
 static bool chol_lookahead() {
   const char* e = getenv("SCS_CHOL_LA");
   return !(e && e[0] == '0');
@@ -414,7 +437,11 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
   const int nblk = (int)(mpad / CB);
   const int OB = outer_block();
   const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
-  bool c2_pending = false;
+  bool c12_pending = false;
+  hipError_t e = hipSuccess;
+  auto wait = [&](hipStream_t s, hipEvent_t ev) {
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+  };
   if (mpad > m) hipLaunchKernelGGL(diag_pad_kernel, dim3((unsigned)ceil_div(mpad - m, 256)), dim3(256), 0, st, G, ld,
                                    m, mpad);
   for (int i0 = 0; i0 < nblk; i0 += OB) {
@@ -425,8 +452,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
       const int nb = i1 - k - 1;
       if (nb == 0) break;
       double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..i1-1)
-      hipError_t e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb,
-                                     rowpanel, ld, 0, st);
+      e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb, rowpanel, ld,
+                          0, st);
       if (e != hipSuccess) return e;
       double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
       e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld,
@@ -435,49 +462,45 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     }
     const int nc = nblk - i1;
     if (nc == 0) break;
-    // B: strip solve, C: trailing update with K = (i1 - i0)·128
-    hipError_t e = strip_solve(G, ld, W, a, i0, i1, i1, nc, st);
-    if (e != hipSuccess) return e;
     const double* X = G + (int64_t)i1 * CB * ld;
     double* trail = G + (int64_t)i1 * CB * ld + (int64_t)i1 * CB;
-    const int nc2 = nc - OB;   // block pairs both beyond the next outer block
-    if (!la || nc2 <= 0) {
-      if (c2_pending) {
-        e = hipStreamWaitEvent(st, a->ev2, 0);
-        if (e != hipSuccess) return e;
-        c2_pending = false;
+    const int ntri = nc * (nc + 1) / 2;
+    if (!la || nc <= OB) {
+      if (c12_pending) {   // the previous block's bulk update reaches these elements first
+        wait(st, a->ev2);
+        c12_pending = false;
       }
-      e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, nc * (nc + 1) / 2,
-                          trail, ld, 2 | 4, st);
+      // B: strip solve, C: trailing update with K = (i1 - i0)·128
+      if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1, nc, st);
+      if (e == hipSuccess)
+        e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, ntri, trail, ld,
+                            2 | 4, st);
       if (e != hipSuccess) return e;
       continue;
     }
-    // C1: the next block's strip, after C2 of the previous block (same elements, block order)
-    if (c2_pending) {
-      e = hipStreamWaitEvent(st, a->ev2, 0);
-      if (e != hipSuccess) return e;
-    }
-    const int n1 = (OB * (OB + 1)) / 2 + (nc - OB) * OB;   // sum_{i<nc} min(i+1, OB)
-    e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, a->strip, n1, trail, ld, 2 | 4, st);
+    // Bb on st2 once A_t is done (stream order keeps C12_{t-1} before it)
+    if (e == hipSuccess) e = hipEventRecord(a->ev3, st);
+    wait(a->st2, a->ev3);
+    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2);
+    // Ba, C1a on the chain after C12_{t-1}
+    if (c12_pending) wait(st, a->ev2);
+    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
+    const int n1a = (OB * (OB + 1)) / 2;
+    if (e == hipSuccess)
+      e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, n1a, trail, ld,
+                            2 | 4, st);
+    // C12 on st2 after Ba (it reads X's columns of the next block)
+    if (e == hipSuccess) e = hipEventRecord(a->ev1, st);
+    wait(a->st2, a->ev1);
+    if (e == hipSuccess)
+      e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n1a, ntri - n1a, trail,
+                          ld, 2 | 4, a->st2);
+    if (e == hipSuccess) e = hipEventRecord(a->ev2, a->st2);
     if (e != hipSuccess) return e;
-    e = hipEventRecord(a->ev1, st);
-    if (e == hipSuccess) e = hipStreamWaitEvent(a->st2, a->ev1, 0);
-    if (e != hipSuccess) return e;
-    // C2 on st2, overlapping the next block's A and B on st
-    const int i2 = i1 + OB;
-    const double* X2 = G + (int64_t)i2 * CB * ld;
-    double* trail2 = G + (int64_t)i2 * CB * ld + (int64_t)i2 * CB;
-    e = gram_launch_gen(X2, ld, X2, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, nc2 * (nc2 + 1) / 2,
-                        trail2, ld, 2 | 4, a->st2);
-    if (e != hipSuccess) return e;
-    e = hipEventRecord(a->ev2, a->st2);
-    if (e != hipSuccess) return e;
-    c2_pending = true;
+    c12_pending = true;
   }
-  if (c2_pending) {
-    hipError_t e = hipStreamWaitEvent(st, a->ev2, 0);
-    if (e != hipSuccess) return e;
-  }
+  if (c12_pending) wait(st, a->ev2);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 

@@ -828,84 +828,97 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
   return hipGetLastError();
 }
 
-// Latency variant for the small launches of the Cholesky (K <= 512, few tiles): each
-// 128 x 128 list tile is computed by 4 workgroups, one per 32-column strip (4 waves of
-// 32 x 32 along the rows), so one K=16 stage costs a quarter of the MFMA time per SIMD.
-// A workgroup reads the A2 columns it writes and nothing else of the output, so the
-// in-place panel solve (G == A2) stays race-free.  Column-major operands (gen form),
-// register-staged double-buffered LDS as gram_f64_kernel, same epilogue placement.
+// Latency variant for the small launches of the Cholesky and the LU (short K or few
+// tiles): each 128 x 128 list tile is computed by 128/QC workgroups, one per QC-column
+// strip (4 waves of 32 rows x QC along the rows).  A workgroup reads the A2 columns it
+// writes and nothing else of the output, so the in-place panel solve (G == A2) stays
+// race-free.  The global loads run RING stages (RING x 16 samples) ahead of the MFMAs in a
+// register ring: one K = 128 launch pays one memory latency, not one per 16-sample stage
+// (the per-stage double buffer it replaces left each stage's L2/HBM round trip exposed,
+// ~1.5 us x 8 stages against ~0.4 us of MFMAs per stage).  Column-major operands (gen
+// form), swizzled LDS stages, and per accumulator the MFMA order of gram_f64_kernel /
+// gram_sia_kernel ((p, u) per stage, stages ascending): the tile is bitwise the same.
+template <int QC>
 __global__ __launch_bounds__(256) void gram_small_kernel(const double* __restrict__ A1, int64_t lda1,
                                                          const double* A2, int64_t lda2,
                                                          const double* __restrict__ w, int64_t k0, int64_t Nk,
                                                          const int2* __restrict__ tiles, double* G, int64_t ldg,
                                                          int flags) {
-  constexpr int QC = 32;                   // columns per workgroup
-  constexpr int SBQ = (GT + QC) * GBK;     // doubles per LDS stage (A1 128 x 16 | A2 32 x 16)
+  constexpr int RING = 8;                  // stages in flight
+  constexpr int NQ = GT / QC;              // workgroups per tile
+  constexpr int TJ = QC / 16;              // 16-column MFMA tiles per wave
+  constexpr int SBQ = (GT + QC) * GBK;     // doubles per LDS stage (A1 128 x 16 | A2 QC x 16)
   __shared__ __attribute__((aligned(16))) double lds[2 * SBQ];
   const int accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
-  const int2 tl = tiles[blockIdx.x >> 2];
-  const int64_t I0 = (int64_t)tl.x * GT, J0 = (int64_t)tl.y * GT + (blockIdx.x & 3) * QC;
+  const int2 tl = tiles[blockIdx.x / NQ];
+  const int64_t I0 = (int64_t)tl.x * GT, J0 = (int64_t)tl.y * GT + (blockIdx.x % NQ) * QC;
   const double* __restrict__ Ai = A1 + I0 * lda1;
   const double* Aj = A2 + J0 * lda2;
   const int tid = threadIdx.x, lane = tid & 63, wr = tid >> 6;
   const int sc = tid & 7, sf0 = tid >> 3;   // staging: feature sf0 + 32 i, 16-B chunk sc
-  v2d ra[4], rb, rw;
-  auto gload = [&](int64_t n0) {
+  const bool hasb = QC == 32 || sf0 < QC;   // A2 rows staged by this thread (QC = 16: half the threads)
+  const int sfb = sf0 & (QC - 1);           // loads stay unconditional (a branch drains vmcnt)
+  v2d ra[RING][4], rb[RING], rw[RING];
+  auto gload = [&](int slot, int64_t n0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = *(const v2d*)(Ai + (int64_t)(sf0 + 32 * i) * lda1 + n0 + 2 * sc);
-    rb = *(const v2d*)(Aj + (int64_t)sf0 * lda2 + n0 + 2 * sc);
-    rw = *(const v2d*)(w + n0 + 2 * sc);
+    for (int i = 0; i < 4; ++i) ra[slot][i] = *(const v2d*)(Ai + (int64_t)(sf0 + 32 * i) * lda1 + n0 + 2 * sc);
+    rb[slot] = *(const v2d*)(Aj + (int64_t)sfb * lda2 + n0 + 2 * sc);
+    rw[slot] = *(const v2d*)(w + n0 + 2 * sc);
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](int slot, int buf) {
     double* la = lds + buf * SBQ;
     double* lb = la + GT * GBK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = sf0 + 32 * i;
-      *(v2d*)(la + f * GBK + 2 * (sc ^ swz(f))) = ra[i];
+      *(v2d*)(la + f * GBK + 2 * (sc ^ swz(f))) = ra[slot][i];
     }
-    *(v2d*)(lb + sf0 * GBK + 2 * (sc ^ swz(sf0))) = rb * rw;
+    if (hasb) *(v2d*)(lb + sf0 * GBK + 2 * (sc ^ swz(sf0))) = rb[slot] * rw[slot];
   };
-  v4d acc[2][2];
+  v4d acc[2][TJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
   const int fl = lane & 15, g = lane >> 4, s = swz(fl);
+  // nk is a multiple of RING (gram_launch_small); the loads past the end re-read the last stage
+  // (branch-free: a conditional load would make the compiler drain vmcnt at every stage)
   const int nk = (int)((Nk - k0) / GBK);
-  if (nk > 0) {
-    gload(k0);
-    swrite(0);
-  }
-  __syncthreads();
-  for (int k = 0; k < nk; ++k) {
-    if (k + 1 < nk) gload(k0 + (int64_t)(k + 1) * GBK);
-    const double* la = lds + (k & 1) * SBQ;
-    const double* lb = la + GT * GBK;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int pc = ((4 * p + g) ^ s) * 2;
-      v2d a[2], b[2];
+  for (int j = 0; j < RING; ++j) gload(j, k0 + (int64_t)j * GBK);
+  for (int kk = 0; kk < nk; kk += RING) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t] = *(const v2d*)(la + (wr * 32 + 16 * t + fl) * GBK + pc);
-        b[t] = *(const v2d*)(lb + (16 * t + fl) * GBK + pc);
+    for (int j = 0; j < RING; ++j) {
+      const int k = kk + j;
+      {
+        swrite(j, k & 1);
+        gload(j, k0 + (int64_t)min(k + RING, nk - 1) * GBK);
+        __syncthreads();
+        const double* la = lds + (k & 1) * SBQ;
+        const double* lb = la + GT * GBK;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int pc = ((4 * p + g) ^ s) * 2;
+          v2d a[2], b[TJ];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) a[t] = *(const v2d*)(la + (wr * 32 + 16 * t + fl) * GBK + pc);
+#pragma unroll
+          for (int t = 0; t < TJ; ++t) b[t] = *(const v2d*)(lb + (16 * t + fl) * GBK + pc);
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+              for (int tj = 0; tj < TJ; ++tj)
+                acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
+        }
       }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-          for (int tj = 0; tj < 2; ++tj)
-            acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
     }
-    if (k + 1 < nk) swrite((k + 1) & 1);
-    __syncthreads();
   }
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-    for (int tj = 0; tj < 2; ++tj)
+    for (int tj = 0; tj < TJ; ++tj)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t I = I0 + wr * 32 + 16 * ti + g + 4 * r;
@@ -916,22 +929,34 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const double* __restric
       }
 }
 
+hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                             int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
+                             hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  if ((k1 - k0) % (8 * GBK) != 0 || k1 <= k0) return hipErrorInvalidValue;   // whole 8-stage rings
+  // 16-column strips (8 workgroups per tile) while the launch would leave most CUs idle
+  if (ntiles <= 32)
+    hipLaunchKernelGGL(gram_small_kernel<16>, dim3(8 * ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles,
+                       G, ldg, flags);
+  else
+    hipLaunchKernelGGL(gram_small_kernel<32>, dim3(4 * ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles,
+                       G, ldg, flags);
+  return hipGetLastError();
+}
+
 // General form: operand panels from two matrices, K range [k0, k1), flags GRAM_*.
 hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                            hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   // short contractions with few tiles are latency-bound (one 128 x 128 x 128 tile on one CU is
-  // 2048 MFMAs = 13.6 us): spread each tile over 4 CUs.  SCS_GRAM_SMALL=0 disables (A/B).
-  static const int small_max = [] {
-    const char* e = getenv("SCS_GRAM_SMALL");
-    return e ? atoi(e) : 1024;
-  }();
-  if (k1 - k0 <= 512 && ntiles <= small_max) {
-    hipLaunchKernelGGL(gram_small_kernel, dim3(4 * ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1, tiles, G,
-                       ldg, flags);
-    return hipGetLastError();
-  }
+  // 2048 MFMAs = 13.6 us): spread each tile over 4-8 CUs.  SCS_GRAM_SMALL=<max tiles>, 0 disables.
+  // up to 64 tiles (256-512 latency workgroups); beyond, the throughput kernels fill the chip with
+  // one 128 x 128 tile per workgroup at 2 per CU (m = 32768: the strip solves of the bulk stream
+  // took 26 ms as 397 latency launches, ~8 ms of MFMA work)
+  const char* se = getenv("SCS_GRAM_SMALL");   // read per launch (tests toggle it in-process)
+  const int small_max = se ? atoi(se) : 64;
+  if (k1 - k0 <= 512 && (k1 - k0) % (8 * GBK) == 0 && k1 > k0 && ntiles <= small_max) return gram_launch_small(A1, lda1, A2, lda2, w, k0, k1, tiles, ntiles, G, ldg, flags, st);
   if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)   // the Cholesky's trailing updates
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);

@@ -41,6 +41,11 @@ void gram_tile_list_rowmajor(int nb, int2* out);
 hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                            hipStream_t st);
+// the latency form of gram_launch_gen (128 x 16/32 strips per workgroup, loads 8 stages ahead);
+// the same bits per tile as gram_launch_gen's other kernels
+hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                             int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
+                             hipStream_t st);
 // Tail-balanced schedule of the main Gram (see gram.hip): work items (bi, bj, ks, idx),
 // combine items (bi, bj, tix, first partial slot)
 int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<int4>& work, std::vector<int4>& comb,
@@ -56,9 +61,8 @@ hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, do
 struct CholAux {             // device constants of the two-level factorization (chol_aux_init)
   double* w = nullptr;       // [128 x +1.0 | mpad x -1.0] Gram weights (panel solve | block updates)
   int2* rect = nullptr;      // R x nblk rectangle tile lists, R = 1..4 (bj-major)
-  int2* strip = nullptr;     // lookahead: the next outer block's strip of a trailing update
-  hipStream_t st2 = nullptr; // lookahead: the rest of each trailing update runs here
-  hipEvent_t ev1 = nullptr, ev2 = nullptr;
+  hipStream_t st2 = nullptr; // lookahead: the bulk stream (strip solve beyond the next block, C12)
+  hipEvent_t ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   int nblk = 0;
 };
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);

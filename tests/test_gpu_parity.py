@@ -630,6 +630,24 @@ def test_cholesky_lookahead_bit_identical(m, monkeypatch):
     assert np.array_equal(bits(la.x), bits(ser.x))
 
 
+@pytest.mark.parametrize("m", [2304])
+def test_cholesky_small_gram_bit_identical(m, monkeypatch):
+    """The latency Gram kernel (gram_small_kernel: 128 x 16/32 strips, 8-stage register ring) that
+    runs the factor's short-K launches and the lookahead's critical diagonal triangle keeps the MFMA
+    order of the throughput kernels, so forcing every launch onto the throughput kernels
+    (SCS_GRAM_SMALL=0) leaves the ProxNSCORE trajectory bit-identical."""
+    N = 4000
+    x0 = np.random.default_rng(37).standard_normal(m) * 0.3
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=29)
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    a = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    monkeypatch.setenv("SCS_GRAM_SMALL", "0")
+    monkeypatch.setenv("SCS_CHOL_LA", "0")
+    b = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    assert a.obj == b.obj and a.pri_res_norm == b.pri_res_norm and a.epochs == b.epochs
+    assert np.array_equal(bits(a.x), bits(b.x))
+
+
 @pytest.mark.parametrize("reg,use_prox", [("l1", True), ("indbox", True), ("l2", False)])
 def test_lqn_fused_epoch_bit_identical(reg, use_prox, monkeypatch):
     """scs_iterate's fused ProxLQNSCORE epoch (m >= 16384: lqn_tail / lqn_post around the two products)
