@@ -1678,17 +1678,26 @@ static void build_blocked(scs_ctx* c, int64_t nrows, int64_t ncols, int64_t* ptr
   int64_t* cnt = dalloc<int64_t>(c, nk + 1);
   int64_t* first = dalloc<int64_t>(c, nk + 1);
   B.ptr = dalloc<int64_t>(c, nk + 1);
-  B.lidx = dalloc<uint16_t>(c, nnz);
-  B.val = dalloc_vals(c, nnz, c->sp_f32);
   if (nrows > 0) {
     HCK(blk_count(ptr, idx, nrows, B.shift, cnt, first, c->st));
+    // fp64: segments in whole 4-entry slots (padding: index 0xFFFF, value 0; launch_spmv_blk)
+    if (!c->sp_f32) HCK(blk_pad(cnt, nk, c->st));
     tb = 0;
     HCK(blk_scan(nullptr, &tb, cnt, B.ptr, nk + 1, c->st));
     void* tmp = dalloc<char>(c, tb);
     HCK(blk_scan(tmp, &tb, cnt, B.ptr, nk + 1, c->st));
-    HCK(blk_scatter(ptr, idx, val, c->sp_f32, nrows, B.shift, B.ptr, first, B.lidx, B.val, c->st));
+    int64_t nnzp = 0;
+    HCK(hipMemcpyAsync(&nnzp, B.ptr + nk, sizeof(int64_t), hipMemcpyDeviceToHost, c->st));
     sync(c);
     dfree(c, tmp);
+    B.lidx = dalloc<uint16_t>(c, nnzp + 4);
+    HCK(hipMemsetAsync(B.lidx, 0xFF, sizeof(uint16_t) * (nnzp + 4), c->st));
+    B.val = dalloc_vals(c, nnzp + 4, c->sp_f32);
+    HCK(blk_scatter(ptr, idx, val, c->sp_f32, nrows, B.shift, B.ptr, first, B.lidx, B.val, c->st));
+    sync(c);
+  } else {
+    B.lidx = dalloc<uint16_t>(c, 4);
+    B.val = dalloc_vals(c, 4, c->sp_f32);
   }
   sync(c);
   dfree_t(c, cnt);

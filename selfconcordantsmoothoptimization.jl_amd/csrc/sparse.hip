@@ -41,15 +41,151 @@ constexpr int SPB_MAXSHIFT = 14;
 constexpr int SPB_THREADS = 1024;
 constexpr int SPB_ROWS = 1024;   // rows per workgroup
 
+// fp64 layout: segments are padded to multiples of 4 entries (index 0xFFFF -- never a local index, the
+// block is <= 16384 wide -- value 0; blk_pad / blk_scatter) and start 4-aligned, so a lane
+// takes 4 consecutive entries with one 8-B index load and one 16-B (fp32) or two 16-B (fp64)
+// value loads.  One wave works on RW rows at a time (of its 64 contiguous rows): all loads of a
+// round are issued before any use (clamped addresses, no branches), a segment of up to 256
+// entries -- C5: ~164 per (row, block) in both directions -- costs one round, and the RW rows'
+// lane partials are reduced together (multi_row_sum: log2(RW) exchange levels that halve the
+// live rows, then the plain butterfly; 10 shuffles for 8 rows instead of 48).  C5 shape, one
+// box, against the previous one-entry-per-lane form: fp64 1.380 -> 1.223 ms, fp32 0.943 ->
+// 0.869 ms per pass (tools/probes/probe_spmv.hip).  Per row the summation order is fixed
+// (entries ascending within a lane, lanes by the fixed exchange tree).
+template <int RW>
+__device__ __forceinline__ double multi_row_sum(double (&acc)[RW], int lane, int& row) {
+  row = 0;
+  int off = 32;
+#pragma unroll
+  for (int half = RW / 2; half >= 1; half >>= 1) {
+    const bool hi = (lane & off) != 0;
+#pragma unroll
+    for (int j = 0; j < half; ++j) {
+      const double keep = hi ? acc[j + half] : acc[j];
+      const double send = hi ? acc[j] : acc[j + half];
+      acc[j] = keep + __shfl_xor(send, off, 64);
+    }
+    if (hi) row += half;
+    off >>= 1;
+  }
+  double v = acc[0];
+  for (int o = off; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void load4(const double* p, double (&o)[4]) {
+  const v2d a = *(const v2d*)p, b = *(const v2d*)(p + 2);
+  o[0] = a[0];
+  o[1] = a[1];
+  o[2] = b[0];
+  o[3] = b[1];
+}
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load4(const float* p, double (&o)[4]) {
+  const v4f a = *(const v4f*)p;
+  o[0] = a[0];
+  o[1] = a[1];
+  o[2] = a[2];
+  o[3] = a[3];
+}
+
+template <typename VT, int RW>
+__global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
+                                                               const uint16_t* __restrict__ lidx,
+                                                               const VT* __restrict__ val,
+                                                               const double* __restrict__ x, int64_t nrows,
+                                                               int64_t ncols, int shift, double* __restrict__ out,
+                                                               int64_t ldo, int chunks) {
+  __shared__ double xs[1 << SPB_MAXSHIFT];
+  const int b = blockIdx.y;
+  const int64_t c0 = (int64_t)b << shift;
+  const int nb = (int)min((int64_t)1 << shift, ncols - c0);
+  // stage the slice: all loads of a thread in flight before the LDS stores (a plain
+  // load->store loop serializes 16 L2 round trips while every wave waits at the barrier)
+  {
+    constexpr int PER = (1 << SPB_MAXSHIFT) / SPB_THREADS;
+    double t[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * SPB_THREADS;
+      t[k] = (i < nb) ? x[c0 + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) xs[threadIdx.x + k * SPB_THREADS] = t[k];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t* pb = ptr + (int64_t)b * nrows;
+  // the workgroup walks `chunks` consecutive 1024-row chunks of block b with the slice staged
+  // once; its waves run through the chunks without a barrier (no per-chunk drain)
+  for (int ch = 0; ch < chunks; ++ch) {
+    const int64_t cb = (int64_t)blockIdx.x * chunks + ch;
+    if (cb * SPB_ROWS >= nrows) break;
+    const int64_t r1 = min(nrows, (cb + 1) * SPB_ROWS);
+    // each wave owns 64 contiguous rows: their pointer pairs are loaded once (lane k: row
+    // rw0 + k, coalesced) and broadcast per round with readlane
+    const int64_t rw0 = cb * SPB_ROWS + (int64_t)wv * 64;
+    const int64_t myr = rw0 + lane;
+    const int64_t mp0 = (myr < r1) ? pb[myr] : 0, mp1 = (myr < r1) ? pb[myr + 1] : 0;
+    const int nrw = (int)max((int64_t)0, min((int64_t)64, r1 - rw0));
+    for (int k0 = 0; k0 < nrw; k0 += RW) {
+      // per row: wave-uniform base pointers (SGPRs) + 32-bit lane offsets
+      const uint16_t* li[RW];
+      const VT* va[RW];
+      int n4[RW];
+      double acc[RW];
+      int rem = 0;   // longest segment of the group in 4-entry slots (wave-uniform)
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+        const int k = k0 + j;   // rows past nrw have mp0 = mp1 = 0 -> empty
+        const int64_t a0 = ((int64_t)__builtin_amdgcn_readlane((int)(mp0 >> 32), k) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)mp0, k);
+        const int64_t a1 = ((int64_t)__builtin_amdgcn_readlane((int)(mp1 >> 32), k) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)mp1, k);
+        n4[j] = (int)((a1 - a0) >> 2);
+        li[j] = lidx + a0;   // an empty segment reads its (valid, 4-aligned) start, masked
+        va[j] = val + a0;
+        acc[j] = 0.0;
+        rem = max(rem, n4[j]);
+      }
+      for (int o = lane; o - lane < rem; o += 64) {
+        uint64_t id[RW];
+        double v[RW][4];
+#pragma unroll
+        for (int j = 0; j < RW; ++j) {
+          const int q = max(min(o, n4[j] - 1), 0);
+          id[j] = *(const uint64_t*)(li[j] + 4 * q);
+          load4(va[j] + 4 * q, v[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+          if (o < n4[j]) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int cidx = (int)((id[j] >> (16 * e)) & 0xFFFF);
+              if (cidx != 0xFFFF) acc[j] += v[j][e] * xs[cidx];
+            }
+          }
+      }
+      int row;
+      const double sum = multi_row_sum<RW>(acc, lane, row);
+      if ((lane & (64 / RW - 1)) == 0 && k0 + row < nrw) out[(int64_t)b * ldo + rw0 + k0 + row] = sum;
+    }
+  }
+}
+
+// Unpadded layout, one entry per lane (the fp32 arm: measured faster there than 4-entry slots,
+// 0.844-0.87 against 0.89 ms -- with 6 B per entry the pass is bound by per-entry LDS/VALU
+// instructions, and 4-entry slots leave ~36% of the lanes idle on 164-entry segments).
 // One wave works on RW rows at a time (of its 64 contiguous rows): all RW*U (index,
 // value) loads of a round are issued before any use,
 // masked per lane (clamped addresses), so a row segment of up to 64*U entries --
 // the common case: ~164 per (row, block) at C5 in both directions -- costs one
 // round with RW*U*64 loads per wave in flight (the kernel runs at one workgroup per
 // CU because of the 128 KiB LDS slice).  Per row the summation order is fixed
-// (lane-ascending p, then the wave butterfly).
+// (lane-ascending p, then multi_row_sum's fixed exchange tree).
 template <typename VT, int U, int RW>
-__global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
+__global__ __launch_bounds__(SPB_THREADS) void spmv_blk1_kernel(const int64_t* __restrict__ ptr,
                                                                const uint16_t* __restrict__ lidx,
                                                                const VT* __restrict__ val,
                                                                const double* __restrict__ x, int64_t nrows,
@@ -126,12 +262,9 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
         for (int u = 0; u < U; ++u)
           if (o + 64 * u < len[j]) acc[j] += v[j][u] * xs[id[j][u]];
     }
-#pragma unroll
-    for (int j = 0; j < RW; ++j) {
-      const double a = wave_sum(acc[j]);
-      const int k = k0 + j;
-      if (lane == 0 && k < nrw) out[(int64_t)b * ldo + rw0 + k] = a;
-    }
+    int row;
+    const double sum = multi_row_sum<RW>(acc, lane, row);
+    if ((lane & (64 / RW - 1)) == 0 && k0 + row < nrw) out[(int64_t)b * ldo + rw0 + k0 + row] = sum;
   }
   }
 }
@@ -147,31 +280,29 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
                            hipStream_t st) {
   if (nrows <= 0) return hipSuccess;
   const int nblk = (int)ceil_div(ncols, (int64_t)1 << shift);
-  // row chunks per workgroup: 4 for fp32 values, 2 for fp64 (C5 spmv, one box: fp32 0.936 /
-  // 0.894 / 0.868 ms at 1 / 2 / 4, fp64 1.374 / 1.357 / 1.393 ms); SCS_SPMV_CHUNKS overrides (A/B)
+  // fp64 (padded layout, 4-entry slots): 4 rows per round (8 spill at 128 VGPRs), 2 row chunks
+  // per workgroup; C5, one box (ms): RW 2 / 4 / 8 at 2 chunks 1.341 / 1.218 / 1.486, RW 4 at
+  // 1 / 4 chunks 1.223 / 1.220.  fp32 (unpadded, one entry per lane): U = 3 slots x 8 rows for
+  // short segments (C5: ~164 per (row, block)), 8 x 2 for long ones, 4 chunks.
+  // SCS_SPMV_CHUNKS overrides the chunks (A/B).
   static const int chunks_env = [] {
     const char* e = getenv("SCS_SPMV_CHUNKS");
     return e ? std::max(1, atoi(e)) : 0;
   }();
-  const int chunks = chunks_env ? chunks_env : (f32 ? 4 : 2);
-  const dim3 grid((unsigned)ceil_div(ceil_div(nrows, SPB_ROWS), chunks), (unsigned)nblk);
-  const int64_t avg = nnz / (nrows * nblk);
-  // short segments (C5: ~164 entries per row and block): 3 x 64 slots, 8 rows per round;
-  // long ones: 8 x 64 slots, 2 rows
   if (f32) {
-    if (avg <= 64 * 3)
-      hipLaunchKernelGGL((spmv_blk_kernel<float, 3, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
-                         x, nrows, ncols, shift, out, ldo, chunks);
+    const int chunks = chunks_env ? chunks_env : 4;
+    const dim3 grid((unsigned)ceil_div(ceil_div(nrows, SPB_ROWS), chunks), (unsigned)nblk);
+    if (nnz / (nrows * nblk) <= 64 * 3)
+      hipLaunchKernelGGL((spmv_blk1_kernel<float, 3, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+                         (const float*)val, x, nrows, ncols, shift, out, ldo, chunks);
     else
-      hipLaunchKernelGGL((spmv_blk_kernel<float, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val,
-                         x, nrows, ncols, shift, out, ldo, chunks);
+      hipLaunchKernelGGL((spmv_blk1_kernel<float, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
+                         (const float*)val, x, nrows, ncols, shift, out, ldo, chunks);
   } else {
-    if (avg <= 64 * 3)
-      hipLaunchKernelGGL((spmv_blk_kernel<double, 3, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
-                         (const double*)val, x, nrows, ncols, shift, out, ldo, chunks);
-    else
-      hipLaunchKernelGGL((spmv_blk_kernel<double, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
-                         (const double*)val, x, nrows, ncols, shift, out, ldo, chunks);
+    const int chunks = chunks_env ? chunks_env : 2;
+    const dim3 grid((unsigned)ceil_div(ceil_div(nrows, SPB_ROWS), chunks), (unsigned)nblk);
+    hipLaunchKernelGGL((spmv_blk_kernel<double, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const double*)val,
+                       x, nrows, ncols, shift, out, ldo, chunks);
   }
   return hipGetLastError();
 }
@@ -220,6 +351,18 @@ hipError_t blk_count(const int64_t* ptr, const int* idx, int64_t nrows, int shif
                      hipStream_t st) {
   hipLaunchKernelGGL(blk_count_kernel, dim3((unsigned)ceil_div(nrows, 4)), dim3(256), 0, st, ptr, idx, nrows, shift,
                      cnt, first);
+  return hipGetLastError();
+}
+
+// segment counts rounded up to whole 4-entry slots (the SpMV's per-lane unit)
+__global__ void blk_pad_kernel(int64_t* __restrict__ cnt, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) cnt[i] = (cnt[i] + 3) & ~(int64_t)3;
+}
+
+hipError_t blk_pad(int64_t* cnt, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(blk_pad_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, cnt, n);
   return hipGetLastError();
 }
 

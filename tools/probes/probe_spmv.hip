@@ -1,8 +1,10 @@
 // Experiment harness (not part of libscsopt): the LDS-blocked SpMV (sparse.hip) at C5's shape
 // against candidate variants.  Segment lengths ~ 164 +- 11 per (row, block), as C5 has them.
-//   A  : the product kernel (launch_spmv_blk), unpadded segments
-//   B  : segments padded to multiples of 4 entries (pad index 0xFFFF), one lane = 4 consecutive
-//        entries (8-B index load + 16/32-B value loads), transposed multi-row wave reduction
+//   A  : the product kernel (launch_spmv_blk): fp64 on the padded layout, fp32 unpadded
+//   B  : this file's copy of the padded-segment kernel (one lane = 4 consecutive entries, 8-B
+//        index load + 16/32-B value loads, transposed multi-row wave reduction) at other RW /
+//        chunk settings.  (The unpadded one-entry-per-lane form it replaced ran fp64 1.380 ms,
+//        fp32 0.943 ms at dir 0.)
 // usage: probe_spmv [f32] [dir]   dir 0: 2^20 rows x 4 blocks (A x), 1: 2^16 rows x 64 blocks (Aᵀ v)
 #include <chrono>
 #include <cmath>
@@ -240,7 +242,10 @@ static void run(int dir) {
     printf("  %-28s %.4f ms  %.0f GB/s (nnz*(val+2) B)\n", name, ms, bytes / (ms * 1e-3) / 1e9);
   };
   const int f32 = sizeof(VT) == 4;
-  timeit("A product", [&] { CK(launch_spmv_blk(dpa, ia, va, f32, x, nrows, ncols, shift, nnz, oa, nrows, 0)); });
+  timeit("A product", [&] {
+    if (f32) CK(launch_spmv_blk(dpa, ia, va, f32, x, nrows, ncols, shift, nnz, oa, nrows, 0));
+    else CK(launch_spmv_blk(dpb, ib, vb, f32, x, nrows, ncols, shift, nnz, oa, nrows, 0));
+  });
   for (int chunks : {1, 2, 4}) {
     const dim3 grid((unsigned)((nrows / 1024 + chunks - 1) / chunks), (unsigned)nblk);
     char nm[64];
