@@ -199,14 +199,22 @@ struct scs_ctx {
   // minibatches (scs_set_batches / scs_select_batch): the collected DataLoader batch list of
   // iterate.jl:141-146 as one device row list; each distinct batch size owns a gathered view
   // (NView) that is swapped in for the steps on that batch
+  // On several ranks the list holds GLOBAL row indices: each rank keeps the batch's rows it
+  // owns (possibly none) and their positions in the batch (bpos, for the sample-space gather);
+  // the batch's global size (bglob) drives the branch choice and the exchange covers the rest.
   int64_t* brows = nullptr;
-  std::vector<int64_t> boff;   // batch b = brows[boff[b] .. boff[b + 1])
-  std::vector<NView> bpool;    // gathered views, one per distinct batch size
+  std::vector<int64_t> boff;   // batch b = brows[boff[b] .. boff[b + 1]) (local rows)
+  std::vector<int64_t> bglob;  // global size of batch b
+  std::vector<int64_t> bpos;   // position in its batch of each local row of brows (host)
+  std::vector<NView> bpool;    // gathered views, one per distinct (local, global) batch size
   std::vector<int64_t> bheld;  // the batch each pool view currently holds (-1: none)
   int bview = -1;              // the selected batch's pool view (-1: the full data)
-  // all ranks' rows (GGN sample-space branch with N_global + 1 <= m on several ranks)
+  int64_t bsel = -1;           // the selected batch (-1: the full data)
+  // all ranks' rows of the full data or of the selected batch (GGN sample-space branch with
+  // N_global + 1 <= m on several ranks)
   NView gview;
   bool gview_ok = false;
+  int64_t gview_batch = -1;    // the batch gview holds (-1: the full data)
   bool lu_fallback_used = false;
 
   // caches (CSE of identical evaluations; keyed by the host x content)
@@ -638,8 +646,11 @@ void clear_batches(scs_ctx* c) {
   c->bpool.clear();
   c->bheld.clear();
   c->boff.clear();
+  c->bglob.clear();
+  c->bpos.clear();
   dfree_t(c, c->brows);
   c->bview = -1;
+  c->bsel = -1;
 }
 
 // select batch b (-1: the full data) for the following steps: its size's pool view is
@@ -647,17 +658,21 @@ void clear_batches(scs_ctx* c) {
 // and re-gathered only when it holds another batch
 void select_batch(scs_ctx* c, int64_t b) {
   c->bview = -1;
+  c->bsel = b < 0 ? -1 : b;
   if (b < 0) return;
   // f(A, y, x) = 1/2 x'(A x) + y'x reads A as an m x m operator, not as samples
   if (c->loss == SCS_LOSS_QUADRATIC) fail(c, SCS_ERR_ARG, "the quadratic loss has no samples to batch");
-  const int64_t n = c->boff[b + 1] - c->boff[b];
+  const int64_t n = c->boff[b + 1] - c->boff[b], ng = c->bglob[b];
   int k = -1;
   for (int i = 0; i < (int)c->bpool.size(); ++i)
-    if (c->bpool[i].N == n) k = i;
+    if (c->bpool[i].N == n && c->bpool[i].Nglob == ng) k = i;
   if (k < 0) {
     NView v;
-    v.N = v.Nglob = n;
-    v.Npad = round_up(n, 16);
+    v.N = n;
+    v.Nglob = ng;
+    // a rank that owns none of the batch's rows keeps one zero 16-row stage (the kernels mask
+    // rows >= N, so it contributes nothing to the exchanged sums)
+    v.Npad = round_up(std::max<int64_t>(n, 1), 16);
     v.nstage = v.Npad / 16;
     v.A = dalloc<double>(c, (size_t)v.Npad * c->mpad);
     v.y = dalloc<double>(c, v.Npad);
@@ -670,7 +685,10 @@ void select_batch(scs_ctx* c, int64_t b) {
   }
   if (c->bheld[k] != b) {
     NView& v = c->bpool[k];
-    if (c->sparse) {   // CSR rows -> the dense batch (the reference's Matrix(As') of a sparse A)
+    if (n == 0) {
+      HCK(hipMemsetAsync(v.A, 0, sizeof(double) * (size_t)v.Npad * c->mpad, c->st));
+      HCK(hipMemsetAsync(v.y, 0, sizeof(double) * v.Npad, c->st));
+    } else if (c->sparse) {   // CSR rows -> the dense batch (the reference's Matrix(As') of a sparse A)
       HCK(hipMemsetAsync(v.A, 0, sizeof(double) * (size_t)v.Npad * c->mpad, c->st));
       HCK(launch_densify_rows(c->rowptr, c->colidx, c->val, c->sp_f32, c->brows + c->boff[b], n, v.Npad, c->y,
                               v.A, v.y, c->st));
@@ -1104,11 +1122,22 @@ void ggn_sample_direction(scs_ctx* c, const double* xh);
 void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
   if (c->sparse) fail(c, SCS_ERR_ARG, "the sharded GGN sample-space branch needs a dense A");
   ensure_red(c);
+  if (c->gview_ok && c->gview_batch != c->bsel) {   // built for another batch (or the full data)
+    free_view(c, c->gview);
+    c->gview = NView();
+    c->gview_ok = false;
+  }
   if (!c->gview_ok) {
     const int64_t Ng = c->Nglob, Npg = round_up(std::max<int64_t>(Ng, 1), 16);
     if (Npg * c->mpad + Npg > c->red_cap) fail(c, SCS_ERR_COMM, "reduce buffer too small for the row all-gather");
+    // each local row at its global position: in the data (row0 + r) or in the selected batch
     std::vector<int64_t> rows(Ng, -1);
-    for (int64_t r = 0; r < c->N; ++r) rows[c->row0 + r] = r;
+    if (c->bsel < 0) {
+      for (int64_t r = 0; r < c->N; ++r) rows[c->row0 + r] = r;
+    } else {
+      const int64_t o = c->boff[c->bsel];
+      for (int64_t r = 0; r < c->N; ++r) rows[c->bpos[o + r]] = r;
+    }
     int64_t* drows = dalloc<int64_t>(c, Ng);
     HCK(hipMemcpyAsync(drows, rows.data(), sizeof(int64_t) * Ng, hipMemcpyHostToDevice, c->st));
     HCK(launch_gather_rows(c->A, c->Npad, c->y, drows, Ng, Npg, c->mpad, c->red, c->red + Npg * c->mpad, c->st));
@@ -1127,6 +1156,7 @@ void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
     alloc_nspace(c);
     swap_view(c, v);
     c->gview_ok = true;
+    c->gview_batch = c->bsel;
   }
   struct Scope {   // the gathered rows on one logical rank, restored even when the step fails
     scs_ctx* c;
@@ -2056,17 +2086,28 @@ int scs_set_batches(scs_ctx* c, const int64_t* rows, const int64_t* offsets, int
     if (nbatch == 0) return;
     if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
     if (c->generic) fail(c, SCS_ERR_ARG, "a ProblemGeneric has no samples to batch");
-    if (c->nranks > 1) fail(c, SCS_ERR_ARG, "minibatches run on one rank");
     if (nbatch < 0 || !rows || !offsets || offsets[0] != 0) fail(c, SCS_ERR_ARG, "scs_set_batches: bad batch list");
     for (int64_t b = 0; b < nbatch; ++b)
       if (offsets[b + 1] <= offsets[b]) fail(c, SCS_ERR_ARG, "scs_set_batches: batch %lld is empty", (long long)b);
     const int64_t tot = offsets[nbatch];
+    // rows are global indices (row0 = 0, Nglob = N on one rank): keep this rank's rows of each batch
     for (int64_t i = 0; i < tot; ++i)
-      if (rows[i] < 0 || rows[i] >= c->N)
+      if (rows[i] < 0 || rows[i] >= c->Nglob)
         fail(c, SCS_ERR_ARG, "scs_set_batches: row %lld out of range", (long long)rows[i]);
-    c->brows = dalloc<int64_t>(c, tot);
-    HCK(hipMemcpyAsync(c->brows, rows, sizeof(int64_t) * tot, hipMemcpyHostToDevice, c->st));
-    c->boff.assign(offsets, offsets + nbatch + 1);
+    std::vector<int64_t> loc;
+    c->boff.assign(1, 0);
+    for (int64_t b = 0; b < nbatch; ++b) {
+      for (int64_t i = offsets[b]; i < offsets[b + 1]; ++i)
+        if (rows[i] >= c->row0 && rows[i] < c->row0 + c->N) {
+          loc.push_back(rows[i] - c->row0);
+          c->bpos.push_back(i - offsets[b]);
+        }
+      c->boff.push_back((int64_t)loc.size());
+      c->bglob.push_back(offsets[b + 1] - offsets[b]);
+    }
+    c->brows = dalloc<int64_t>(c, std::max<size_t>(loc.size(), 1));
+    if (!loc.empty())
+      HCK(hipMemcpyAsync(c->brows, loc.data(), sizeof(int64_t) * loc.size(), hipMemcpyHostToDevice, c->st));
     sync(c);
   });
 }

@@ -135,8 +135,12 @@ def iterate(method: ProximalMethod, model, reg_name, hmu, *, metrics=None, alpha
     if local_max_iter is not None:
         max_epoch = 1
     batches = None
-    if getattr(model, "N", 0) and (batch_size is not None or slice_samples):
-        batches = loader_batches(model.N, batch_size, slice_samples, shuffle_batch, local_max_iter, batch_perm, rng)
+    N = getattr(model, "N_global", getattr(model, "N", 0))
+    if N and (batch_size is not None or slice_samples):
+        batches = loader_batches(N, batch_size, slice_samples, shuffle_batch, local_max_iter, batch_perm, rng)
+        comm = getattr(model, "comm", None)
+        if comm is not None and comm.active:   # one batch list (one shuffle) for every rank
+            batches = comm.broadcast_object(batches)
     if device_loop is None:
         device_loop = not metrics and verbose <= 1
     if device_loop and (metrics or verbose > 1):

@@ -114,6 +114,9 @@ class Problem:
             N = C.c_int64()
             self.ctx.check(_lib.lib.scs_get_dims(self.ctx.h, C.byref(N), None, None, None))
             self.N = int(N.value)
+        Ng = C.c_int64()
+        self.ctx.check(_lib.lib.scs_get_dims(self.ctx.h, None, None, C.byref(Ng), None))
+        self.N_global = int(Ng.value)   # the rows of all ranks (the minibatch loader's N)
         if comm is not None and comm.active:
             comm.bind_buffer(self.ctx)
         ggn = ggn_kind(out_fn)
@@ -267,9 +270,10 @@ class Problem:
         self.ctx.check(_lib.lib.scs_set_gram_cache(self.ctx.h, int(bool(on))))
 
     def set_batches(self, batches=None):
-        """Register the collected loader batches (iterate.jl:141-146): a list of local row-index
-        arrays (0-based), gathered on the device as the As, ys of their step! calls
-        (iterate.jl:205-207).  None / [] clears the list.  f / get_reg stay on the full data."""
+        """Register the collected loader batches (iterate.jl:141-146): a list of row-index arrays
+        (0-based, GLOBAL rows: on several ranks every rank passes the same list and keeps the rows
+        it owns), gathered on the device as the As, ys of their step! calls (iterate.jl:205-207).
+        None / [] clears the list.  f / get_reg stay on the full data."""
         if not batches:
             self.ctx.check(_lib.lib.scs_set_batches(self.ctx.h, None, None, 0))
             return

@@ -77,6 +77,13 @@ class Comm:
         if self.force:
             ctx.check(_lib.lib.scs_set_comm_force(ctx.h, 1))
 
+    def broadcast_object(self, obj):
+        """rank 0's `obj` on every rank (e.g. the shuffled minibatch list: one permutation for all)."""
+        import torch.distributed as dist
+        box = [obj if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=self.group)
+        return box[0]
+
     def bind_buffer(self, ctx):
         """Allocate the all-reduce payload buffer (torch-owned device memory) once the dims are known;
         the native RCCL path lets libscsopt own it."""

@@ -18,6 +18,8 @@ pytestmark = pytest.mark.gpu
 
 N, M = 3001, 192
 NS = 151          # sample-space case: N + 1 <= M
+METHODS = ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample", "ggn_batch", "nscore_batch_ordered",
+           "ggn_sample_batch")
 
 
 def _free_port():
@@ -44,6 +46,21 @@ def _run(method, comm=None):
         p = scsopt.Problem.synthetic(NS, M, x0, f, 2e-3, kind=kind, seed=13, out_fn=out, comm=comm)
         sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=6, verbose=0)
         return {"obj": list(sol.obj), "x": sol.x.copy(), "epochs": sol.epochs}
+    elif method in ("ggn_batch", "nscore_batch_ordered", "ggn_sample_batch"):
+        # minibatches over the row shards (iterate.jl:125-146): global batch rows, each rank keeps
+        # its own; the unshuffled 1000-row batches leave some ranks with no rows of a batch, and the
+        # 48-row batches of the 151-row problem take the sample-space branch (per-batch row gather)
+        n = NS if method == "ggn_sample_batch" else N
+        if method == "nscore_batch_ordered":
+            f, out, kind, meth = losses.logistic_margin(1.0 / n), None, 2, scsopt.ProxNSCORE()
+        else:
+            f, out, kind, meth = losses.logistic_ce(1.0 / n), losses.sigmoid_ce(1.0 / n), 1, scsopt.ProxGGNSCORE()
+        p = scsopt.Problem.synthetic(n, M, x0, f, 2e-3, kind=kind, seed=19, out_fn=out, comm=comm)
+        bs = 48 if method == "ggn_sample_batch" else 1000
+        sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=4, verbose=0, batch_size=bs,
+                             shuffle_batch=method != "nscore_batch_ordered",
+                             batch_perm=np.random.default_rng(3).permutation(n))
+        return {"obj": list(sol.obj), "x": sol.x.copy(), "epochs": sol.epochs}
     elif method == "ggn_ls_cached":
         f, out, kind = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N), 3
         meth = scsopt.ProxGGNSCORE()
@@ -68,7 +85,7 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = {}
-    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample"):
+    for method in METHODS:
         comm = shard.Comm(device=torch.device("cuda", 0))
         res[method] = _run(method, comm)
     out[rank] = res
@@ -79,12 +96,14 @@ def _worker(rank, world, port, out):
 def test_two_rank_shard_matches_single_process(world, tall, monkeypatch):
     """tall = "1" forces the 256 x 128 Gram kernel (the C3 kernel) at this small m, so the packed
     multi-rank slots of its tile halves (gram_unpack) are exercised too; world = 4 splits the 3001
-    rows unevenly (751/750/750/750) and the 151-row sample-space case into 38/38/38/37."""
+    rows unevenly (751/750/750/750) and the 151-row sample-space case into 38/38/38/37.  The
+    *_batch cases run minibatches over the shards (global batch rows; ranks without rows of a
+    batch contribute zero) against the one-process run of the same batch list."""
     monkeypatch.setenv("SCS_GRAM_TALL", tall)
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    for method in ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample"):
+    for method in METHODS:
         full = _run(method)
         r0 = out[0][method]
         for r in range(1, world):

@@ -92,3 +92,55 @@ def test_gloo_world2_exchange_matches_full():
     d_shard = -np.linalg.solve(Gs, out[0][nt:nt + m] + lam * gr)
     d_full = O.ggn_score_step(A, s, r, q, lam * gr, Hr, lam)
     np.testing.assert_allclose(d_shard, d_full, rtol=1e-10, atol=1e-14)
+
+
+def _batch_worker(rank, world, port, out):
+    """Minibatches over row shards: every rank draws its own shuffle (different seeds), the batch
+    list that reaches scs_set_batches is rank 0's (Comm.broadcast_object), and the rows each rank
+    keeps (its share of every global batch) partition each batch; the per-batch Gram / Aᵀv of the
+    kept rows sum to the single-process batch quantities."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "selfconcordantsmoothoptimization.jl_amd"), os.path.join(root, "oracle")]
+    from scsopt.iterate import loader_batches
+    from scsopt.shard import Comm, allreduce_inplace, row_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    A, y, x = _problem()
+    N, m = A.shape
+    comm = Comm()
+    mine = loader_batches(N, 50, shuffle_batch=True, rng=np.random.default_rng(100 + rank))
+    batches = comm.broadcast_object(mine)
+    r0, r1 = row_range(N, world, rank)
+    res = []
+    for b in batches:
+        loc = [int(g) - r0 for g in b if r0 <= g < r1]   # the rows libscsopt keeps on this rank
+        Al = A[r0:r1][loc]
+        G = Al.T @ Al
+        e = Al.T @ y[r0:r1][loc]
+        t = torch.from_numpy(np.concatenate([G.ravel(), e, [float(len(loc))]]))
+        allreduce_inplace(t)
+        res.append(t.numpy().copy())
+    out[rank] = ([np.asarray(b) for b in batches], res)
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_minibatches():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    world = 2
+    mp.spawn(_batch_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    A, y, x = _problem()
+    N, m = A.shape
+    b0, r0 = out[0]
+    b1, r1 = out[1]
+    assert len(b0) == len(b1) == -(-N // 50)
+    for u, v in zip(b0, b1):
+        assert np.array_equal(u, v)   # one permutation on every rank
+    for b, t in zip(b0, r0):
+        Ab = A[b]
+        np.testing.assert_allclose(t[:m * m].reshape(m, m), Ab.T @ Ab, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(t[m * m:m * m + m], Ab.T @ y[b], rtol=1e-12, atol=1e-12)
+        assert t[-1] == len(b)   # the ranks' kept rows partition the batch
