@@ -323,14 +323,17 @@ __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, i
 static int outer_block();
 
 // The bulk stream (the lookahead's trailing updates, 2 gram_sia workgroups per CU fill every CU
-// they get) leaves SCS_CHOL_RESERVE_CUS CUs (default 8, one per XCD) to the serial
-// chain on the context stream: a chol_diag_kernel workgroup that shares its CU with MFMA-bound
-// trailing-update waves runs ~7x slower (m = 32768: 682 us against 94 us alone), and the chain
-// of 256 of them then bounds the factor.  CU masking is best effort: a failure falls back to an
-// unmasked stream.
+// they get) can leave SCS_CHOL_RESERVE_CUS CUs (a multiple of 8: that many / 8 per XCD) to the
+// serial chain on the context stream.  A chol_diag_kernel workgroup that shares its CU with
+// MFMA-bound trailing-update waves runs ~7x slower (m = 32768, before the chain was cut down to
+// Ba / C1a: 682 us against 94 us alone, and the 256-long chain bounded the factor).  With the
+// current split the chain has slack and the reserve no longer pays (m = 32768 factor + solves
+// 220.6 / 224.2 / 223.2 ms at 0 / 8 / 16 reserved CUs; m = 8192 13.0 / 12.8 / 12.5 ms), and
+// rocprofv3 segfaults at exit on a process that created a CU-masked stream, so the default is
+// 0 (an ordinary non-blocking stream).  Masking is best effort: a failure falls back too.
 static hipError_t create_bulk_stream(hipStream_t* s) {
   const char* env = getenv("SCS_CHOL_RESERVE_CUS");
-  const int reserve = env ? atoi(env) : 8;
+  const int reserve = env ? atoi(env) : 0;
   int dev = 0, ncu = 0;
   if (reserve > 0 && hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 4 * reserve) {
