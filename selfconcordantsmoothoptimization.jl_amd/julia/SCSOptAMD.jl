@@ -280,13 +280,24 @@ end
 # optim_loop! (iterate.jl:100-267) as ONE ccall (scs_iterate) -- no per-epoch host round trips;
 # minibatches are gathered on the device from the registered row lists (scs_set_batches).
 # Returns the reference's Solution (iterate.jl:3-32); pri_res_norm[1] is `nothing` as there.
+# The rows of all ranks (scs_get_dims): the loader's N on a row-sharded problem.
+function global_rows(model::DeviceProblem)
+    Ng = Ref{Int64}(0)
+    chk(ccall((:scs_get_dims, lib), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Ref{Int64}, Ptr{Int64}),
+              model.ctx, C_NULL, C_NULL, Ng, C_NULL), model.ctx)
+    Ng[]
+end
+
+# Row-sharded minibatches: every rank registers the same GLOBAL batch list and keeps its own rows
+# of each batch; `bcast` (e.g. `b -> MPI.bcast(b, 0, comm)`) hands rank 0's shuffled list to all.
 function iterate_device!(method::ProximalMethod, model::DeviceProblem, reg_name::String, hμ;
                          α=nothing, batch_size=nothing, slice_samples=false, shuffle_batch=true,
-                         max_epoch=1000, local_max_iter=nothing, x_tol=1e-10, f_tol=1e-10)
+                         max_epoch=1000, local_max_iter=nothing, x_tol=1e-10, f_tol=1e-10, bcast=identity)
     local_max_iter === nothing || (max_epoch = 1)      # iterate.jl:66
     α === nothing || (model.L = 1 / α)                 # iterate.jl:113-115
     batches = (batch_size !== nothing || slice_samples) ?
-              loader_batches(size(model.A, 1), batch_size, slice_samples, shuffle_batch, local_max_iter) : nothing
+              bcast(loader_batches(Int(global_rows(model)), batch_size, slice_samples, shuffle_batch,
+                                   local_max_iter)) : nothing
     set_batches!(model, batches)
     try
         return iterate_registered!(method, model, reg_name, hμ, max_epoch, x_tol, f_tol)
