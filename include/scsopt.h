@@ -37,6 +37,7 @@ extern "C" {
 #define SCS_ERR_STATE 4    /* call order (e.g. step before data)             */
 #define SCS_ERR_REF 5      /* an error the reference itself raises           */
 #define SCS_ERR_COMM 6     /* all-reduce callback failed                     */
+#define SCS_ERR_CALLBACK 7 /* a user loss callback returned non-zero         */
 
 /* f(A, y, x) kinds -- closed forms of the reference's user callbacks.       */
 enum scs_loss_kind {
@@ -44,7 +45,8 @@ enum scs_loss_kind {
   SCS_LOSS_LOGISTIC_CE = 2,     /* f(y, sigmoid(A*x)), cross-entropy  SURVEY §8a C3 */
   SCS_LOSS_LEAST_SQUARES = 3,   /* 0.5*sum((A*x-y).^2)*c           README.md:212-214 */
   SCS_LOSS_QUADRATIC = 4,       /* 1/2*(x'*(A*x)) + y'*x             test/test_algs.jl:90 */
-  SCS_LOSS_ROSENBROCK = 5       /* chained Rosenbrock, no data        README.md:49 */
+  SCS_LOSS_ROSENBROCK = 5,      /* chained Rosenbrock, no data        README.md:49 */
+  SCS_LOSS_CALLBACK = 6         /* the caller's f / grad_fx / hess_fx (scs_set_loss_callback) */
 };
 
 /* (out_fn, f(y, ŷ)) pairs used by ProxGGNSCORE (prox-GGN-SCORE.jl:44-56).    */
@@ -133,10 +135,28 @@ int scs_set_comm_force(scs_ctx* ctx, int on);
 int scs_reduce_buffer_size(scs_ctx* ctx, int64_t* ndoubles);
 int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
 
+/* ---- user callbacks (Problem(x0, f, λ; grad_fx, hess_fx), problems.jl:44-59; call sites
+ * prox-N-SCORE.jl:49-56, prox-L-BFGS-SCORE.jl:85-91, iterate.jl:168) -------------------
+ * SCS_LOSS_CALLBACK evaluates the loss on the caller's side (a data problem's closure captures
+ * its own A, y: the device holds no data, as for a ProblemGeneric -- scs_set_data(N = 0,
+ * A = NULL, m)); the smoother, the m x m solve, damping, prox and the loop stay on the device.
+ * `what`: SCS_CB_F    out[0] = f(x)
+ *         SCS_CB_GRAD out[0..m) = grad_fx(x)
+ *         SCS_CB_HESS out = hess_fx(x), m x m column-major (ProxNSCORE)
+ * x (m) and out are host arrays owned by the library, valid for the call; return 0 on
+ * success, anything else fails the calling ABI function with SCS_ERR_CALLBACK.  There is no
+ * automatic differentiation on this path: ProxNSCORE needs SCS_CB_HESS, ProxGGNSCORE needs a
+ * data loss kind with an out_fn.                                                          */
+#define SCS_CB_F 0
+#define SCS_CB_GRAD 1
+#define SCS_CB_HESS 2
+typedef int (*scs_loss_fn)(void* user, int what, const double* x, int64_t m, double* out);
+int scs_set_loss_callback(scs_ctx* ctx, scs_loss_fn fn, void* user);
+
 /* ---- data  (Problem(A, y, ...) -- problems.jl:61-81) --------------------- */
 /* Upload host A (column-major, N x m, leading dim lda) and y (N).  N is the
  * local row count; N_global/row0 describe the shard.  A may be NULL with
- * m > 0 only for SCS_LOSS_ROSENBROCK (ProblemGeneric, problems.jl:44-59).   */
+ * m > 0 for a ProblemGeneric (problems.jl:44-59): SCS_LOSS_ROSENBROCK or SCS_LOSS_CALLBACK. */
 int scs_set_data(scs_ctx* ctx, int64_t N, int64_t m, const double* A, int64_t lda,
                  const double* y, int64_t N_global, int64_t row0);
 int scs_gen_data(scs_ctx* ctx, const scs_synth* spec);

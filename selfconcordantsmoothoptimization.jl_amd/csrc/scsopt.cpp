@@ -149,6 +149,11 @@ struct scs_ctx {
   int spare = 0;
   int* d_order = nullptr;
   int* hring = nullptr;       // pinned copy of the ring order (asynchronous upload)
+  // SCS_LOSS_CALLBACK: the caller's f / grad_fx / hess_fx, with a pinned [x | out] exchange buffer
+  scs_loss_fn cb = nullptr;
+  void* cb_user = nullptr;
+  double* cbh = nullptr;
+  size_t cbh_cap = 0;
   bool lbfgs_pending = false; // scs_iterate's device loop: the memory update's dg/gg are read at the epoch end
   int lbfgs_slot = 0;
   double H0 = 1.0;
@@ -804,8 +809,36 @@ void gemv_t_global(scs_ctx* c, const double* v, double* out) {
   }
 }
 
+// SCS_LOSS_CALLBACK: call the caller's loss with x (the host copy xh, or xd downloaded) and
+// return the host output area (nout doubles) of the pinned exchange buffer.  The stream is
+// drained first: the previous upload from the buffer must have landed before it is reused.
+double* cb_eval(scs_ctx* c, int what, const double* xh, const double* xd, size_t nout) {
+  if (!c->cb) fail(c, SCS_ERR_STATE, "no loss callback: call scs_set_loss_callback");
+  const int64_t m = c->m;
+  const size_t need = (size_t)m + nout;
+  sync(c);
+  if (need > c->cbh_cap) {
+    if (c->cbh) HCK(hipHostFree(c->cbh));
+    c->cbh = nullptr;
+    c->cbh_cap = 0;
+    HCK(hipHostMalloc((void**)&c->cbh, need * sizeof(double), hipHostMallocDefault));
+    c->cbh_cap = need;
+  }
+  double* xb = c->cbh;
+  if (xh) {
+    std::memcpy(xb, xh, sizeof(double) * m);
+  } else {
+    d2h(c, xb, xd, m);
+    sync(c);
+  }
+  const int rc = c->cb(c->cb_user, what, xb, m, xb + m);
+  if (rc != 0) fail(c, SCS_ERR_CALLBACK, "loss callback (what = %d) returned %d", what, rc);
+  return xb + m;
+}
+
 // f(x) for a device vector with host copy xh
 double eval_f_dev(scs_ctx* c, const double* xh, const double* xd) {
+  if (c->loss == SCS_LOSS_CALLBACK) return cb_eval(c, SCS_CB_F, xh, xd, 1)[0];
   if (c->loss == SCS_LOSS_ROSENBROCK) {
     HCK(launch_rosen(xd, c->m, 0, c->scal + 8, nullptr, 0, c->st));
     d2h(c, c->hscal + 8, c->scal + 8, 1);
@@ -827,6 +860,11 @@ double eval_f_dev(scs_ctx* c, const double* xh, const double* xd) {
 
 // ∇f(x) -> out (device)
 void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
+  if (c->loss == SCS_LOSS_CALLBACK) {
+    const double* g = cb_eval(c, SCS_CB_GRAD, xh, xd, c->m);
+    HCK(hipMemcpyAsync(out, g, sizeof(double) * c->m, hipMemcpyHostToDevice, c->st));
+    return;
+  }
   if (c->loss == SCS_LOSS_ROSENBROCK) {
     HCK(launch_rosen(xd, c->m, 1, out, nullptr, 0, c->st));
     return;
@@ -1254,6 +1292,14 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
     if (c->loss == SCS_LOSS_ROSENBROCK) {
       HCK(launch_rosen(c->x, m, 2, nullptr, c->G, c->mpad, c->st));
       HCK(launch_rosen(c->x, m, 1, c->gtmp, nullptr, 0, c->st));
+    } else if (c->loss == SCS_LOSS_CALLBACK) {
+      // H = hess_fx(x) (m x m, column-major) into the leading block of G; the padded rows /
+      // columns keep block-diag(H, I) (zero from the allocation, the padded diagonal set by
+      // chol_factor)
+      const double* H = cb_eval(c, SCS_CB_HESS, xh, c->x, (size_t)m * m);
+      HCK(hipMemcpy2DAsync(c->G, sizeof(double) * c->mpad, H, sizeof(double) * m, sizeof(double) * m, m,
+                           hipMemcpyHostToDevice, c->st));
+      grad_f_dev(c, xh, c->x, c->gtmp);
     } else if (c->loss == SCS_LOSS_QUADRATIC) {
       require_dense(c, "the quadratic loss");
       HCK(launch_half_sym(c->A, c->nstage, m, c->G, c->mpad, c->st));
@@ -1427,6 +1473,7 @@ int scs_destroy(scs_ctx* c) {
   for (auto& a : c->allocs) (void)hipFree(a.p);
   if (c->hscal) (void)hipHostFree(c->hscal);
   if (c->hring) (void)hipHostFree(c->hring);
+  if (c->cbh) (void)hipHostFree(c->cbh);
   lu_aux_free(&c->lu);
   if (c->own_stream) (void)hipStreamDestroy(c->st);
   delete c;
@@ -1858,15 +1905,27 @@ int scs_get_sparse(scs_ctx* c, int64_t* rowptr, int32_t* colidx, double* val) {
 
 int scs_set_loss(scs_ctx* c, int loss, int ggn, double scale) {
   return guarded(c, [&] {
-    if (loss < SCS_LOSS_LOGISTIC_MARGIN || loss > SCS_LOSS_ROSENBROCK) fail(c, SCS_ERR_ARG, "unknown loss %d", loss);
+    if (loss < SCS_LOSS_LOGISTIC_MARGIN || loss > SCS_LOSS_CALLBACK) fail(c, SCS_ERR_ARG, "unknown loss %d", loss);
     if (ggn < SCS_GGN_NONE || ggn > SCS_GGN_LINEAR_LS) fail(c, SCS_ERR_ARG, "unknown ggn kind %d", ggn);
-    if ((loss == SCS_LOSS_QUADRATIC || loss == SCS_LOSS_ROSENBROCK) && c->nranks > 1)
-      fail(c, SCS_ERR_ARG, "quadratic / Rosenbrock problems are not row-sharded");
+    if ((loss == SCS_LOSS_QUADRATIC || loss == SCS_LOSS_ROSENBROCK || loss == SCS_LOSS_CALLBACK) && sharded(c))
+      fail(c, SCS_ERR_ARG, "quadratic / Rosenbrock / callback problems are not row-sharded");
+    if (loss == SCS_LOSS_CALLBACK && (!c->has_data || !c->generic))
+      fail(c, SCS_ERR_ARG, "a callback loss holds no device data: scs_set_data(N = 0, A = NULL, m) first");
+    if (loss == SCS_LOSS_CALLBACK && ggn != SCS_GGN_NONE)
+      fail(c, SCS_ERR_ARG, "a callback loss has no out_fn kind (ProxGGNSCORE needs a data loss kind)");
     c->loss = loss;
     c->ggn = ggn;
     c->scale = scale;
     c->loss_set = true;
     ++c->data_gen;
+    invalidate_caches(c);
+  });
+}
+
+int scs_set_loss_callback(scs_ctx* c, scs_loss_fn fn, void* user) {
+  return guarded(c, [&] {
+    c->cb = fn;
+    c->cb_user = user;
     invalidate_caches(c);
   });
 }

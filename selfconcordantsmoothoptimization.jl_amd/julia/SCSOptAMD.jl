@@ -18,7 +18,8 @@ export DeviceProblem, configure!, iterate_device!, set_gram_cache!, rccl_unique_
 
 const lib = joinpath(@__DIR__, "..", "scsopt", "libscsopt.so")
 
-const LOSS = Dict(:logistic_margin => 1, :logistic_ce => 2, :least_squares => 3, :quadratic => 4, :rosenbrock => 5)
+const LOSS = Dict(:logistic_margin => 1, :logistic_ce => 2, :least_squares => 3, :quadratic => 4, :rosenbrock => 5,
+                  :callback => 6)
 const GGN = Dict(nothing => 0, :sigmoid_ce => 1, :linear_ls => 2)
 const REG = Dict("l1" => 1, "l2" => 2, "indbox" => 3, "gl" => 4)
 const SCS_ERR_REF = 5
@@ -102,6 +103,62 @@ function DeviceProblem(A::SparseMatrixCSC{Float64}, y::AbstractVector, x0::Vecto
         ctx)
     return finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
 end
+
+# ---- user losses outside the menu: the reference's own keyword callbacks ------------------
+# Problem(x0, f, λ; grad_fx, hess_fx) (problems.jl:44-59) / Problem(A, y, x0, f, λ; grad_fx,
+# hess_fx) (:61-81) evaluated on the host (SCS_LOSS_CALLBACK); the smoother, the solve, damping,
+# prox and the loop stay on the device.  No ForwardDiff fallback: ProxLQNSCORE needs grad_fx,
+# ProxNSCORE grad_fx and hess_fx.
+struct LossCallbacks
+    f::Function
+    grad_fx::Union{Function,Nothing}
+    hess_fx::Union{Function,Nothing}
+    data::Union{Tuple,Nothing}       # (A, y) of a data problem: the closures take (A, y, x)
+end
+
+function loss_trampoline(user::Ptr{Cvoid}, what::Cint, xp::Ptr{Float64}, m::Int64, outp::Ptr{Float64})::Cint
+    cbs = unsafe_pointer_to_objref(user)::LossCallbacks
+    try
+        x = copy(unsafe_wrap(Array, xp, m))
+        args = cbs.data === nothing ? (x,) : (cbs.data..., x)
+        if what == 0
+            unsafe_store!(outp, Float64(cbs.f(args...)))
+        elseif what == 1
+            cbs.grad_fx === nothing && error("this method needs grad_fx (no automatic differentiation on the device path)")
+            copyto!(unsafe_wrap(Array, outp, m), cbs.grad_fx(args...))
+        else
+            cbs.hess_fx === nothing && error("ProxNSCORE needs hess_fx (no automatic differentiation on the device path)")
+            copyto!(unsafe_wrap(Array, outp, m * m), vec(Matrix{Float64}(cbs.hess_fx(args...))))   # column-major
+        end
+        return Cint(0)
+    catch err
+        @error "loss callback failed" exception = (err, catch_backtrace())
+        return Cint(1)
+    end
+end
+
+function callback_problem(cbs::LossCallbacks, x0::Vector{Float64}, λ, L, sol, C_set, P, device)
+    ctx = create_ctx(device)
+    m = length(x0)
+    chk(ccall((:scs_set_data, lib), Cint,
+              (Ptr{Cvoid}, Int64, Int64, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Int64),
+              ctx, 0, m, C_NULL, 0, C_NULL, 0, 0), ctx)
+    model = finish_problem(ctx, nothing, nothing, x0, :callback, λ, nothing, 1.0, L, sol, C_set, P)
+    model.grad_fx = cbs                         # rooted with the model: `user` points at it
+    fp = @cfunction(loss_trampoline, Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}, Int64, Ptr{Float64}))
+    chk(ccall((:scs_set_loss_callback, lib), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
+              ctx, fp, pointer_from_objref(cbs)), ctx)
+    return model
+end
+
+DeviceProblem(x0::Vector{Float64}, f::Function, λ; grad_fx=nothing, hess_fx=nothing, L=nothing,
+              sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0) =
+    callback_problem(LossCallbacks(f, grad_fx, hess_fx, nothing), x0, λ, L, sol, C_set, P, device)
+
+DeviceProblem(A::AbstractMatrix, y::AbstractVector, x0::Vector{Float64}, f::Function, λ; grad_fx=nothing,
+              hess_fx=nothing, L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing,
+              device::Integer=0) =
+    callback_problem(LossCallbacks(f, grad_fx, hess_fx, (A, y)), x0, λ, L, sol, C_set, P, device)
 
 # ---- row sharding (SURVEY.md §8e): one process per GPU, A's rows split across them ---------
 # libscsopt's own RCCL communicator: rank 0 draws the id, the caller hands the 128 bytes to

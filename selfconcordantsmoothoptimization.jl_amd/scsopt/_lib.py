@@ -15,9 +15,10 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCSOPT_LIB", os.path.join(_HERE, "libscsopt.so"))
 
-SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS_ERR_COMM = range(7)
+SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS_ERR_COMM, SCS_ERR_CALLBACK = range(8)
+SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS = range(3)
 
-LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5}
+LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5, "callback": 6}
 GGN = {None: 0, "sigmoid_ce": 1, "linear_ls": 2}
 REG = {"l1": 1, "l2": 2, "indbox": 3, "gl": 4}
 SMOOTH = {"phuber_l1l2": 1, "phuber_indbox": 2, "phuber_gl": 3, "exp_indbox": 4, "logexp_indbox": 5, "osba_l1l2": 6,
@@ -43,6 +44,7 @@ c_dp = C.POINTER(C.c_double)
 c_i64p = C.POINTER(C.c_int64)
 c_i32p = C.POINTER(C.c_int32)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
+LOSS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, c_dp, C.c_int64, c_dp)
 
 
 class Synth(C.Structure):
@@ -86,6 +88,7 @@ _SIGS = {
     "scs_get_nnz": (C.c_int, [C.c_void_p, c_i64p]),
     "scs_get_sparse": (C.c_int, [C.c_void_p, c_i64p, c_i32p, c_dp]),
     "scs_set_loss": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double]),
+    "scs_set_loss_callback": (C.c_int, [C.c_void_p, LOSS_FN, C.c_void_p]),
     "scs_set_reg": (C.c_int, [C.c_void_p, C.c_int, c_dp, C.c_int, c_dp, c_dp, C.c_int64, c_i64p, C.c_int64]),
     "scs_set_smoother": (C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_double, c_dp, c_dp,
                                    C.c_int64]),
@@ -159,9 +162,13 @@ class Context:
         self.h = h
         self.device = device
         self._keep = []  # ctypes callbacks / buffers that must outlive the context
+        self._cb_exc = None  # the exception a Python loss callback raised (re-raised by check)
 
     def check(self, rc):
         if rc != SCS_OK:
+            if rc == SCS_ERR_CALLBACK and self._cb_exc is not None:
+                exc, self._cb_exc = self._cb_exc, None
+                raise exc
             msg = lib.scs_last_error(self.h).decode(errors="replace")
             if rc == SCS_ERR_REF:
                 raise ScsReferenceError(rc, msg)

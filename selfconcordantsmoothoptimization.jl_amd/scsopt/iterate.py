@@ -135,6 +135,8 @@ def iterate(method: ProximalMethod, model, reg_name, hmu, *, metrics=None, alpha
     if local_max_iter is not None:
         max_epoch = 1
     batches = None
+    if (batch_size is not None or slice_samples) and getattr(model.f, "kind", None) == "callback":
+        raise ValueError("minibatches need a device loss kind (a callback loss keeps its data on the host)")
     N = getattr(model, "N_global", getattr(model, "N", 0))
     if N and (batch_size is not None or slice_samples):
         batches = loader_batches(N, batch_size, slice_samples, shuffle_batch, local_max_iter, batch_perm, rng)

@@ -9,8 +9,8 @@ HIP kernels; each kind states the reference expression it reproduces.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import Optional
+from dataclasses import dataclass, field
+from typing import Callable, Optional
 
 
 @dataclass(frozen=True)
@@ -53,6 +53,24 @@ def quadratic() -> Loss:
 def rosenbrock() -> Loss:
     """f(x) = Σ 100(x[i+1]-x[i]^2)^2 + (1-x[i])^2   (README.md:49; ProblemGeneric, no data)."""
     return Loss("rosenbrock", 1.0)
+
+
+@dataclass(frozen=True, eq=False)
+class CallbackLoss(Loss):
+    """The caller's own closures, evaluated on the host (SCS_LOSS_CALLBACK)."""
+    f: Optional[Callable] = field(default=None, repr=False)
+    grad_fx: Optional[Callable] = field(default=None, repr=False)
+    hess_fx: Optional[Callable] = field(default=None, repr=False)
+
+
+def callback(f, grad_fx=None, hess_fx=None) -> CallbackLoss:
+    """A user loss outside the menu: Problem(x0, f, λ; grad_fx, hess_fx) (problems.jl:44-59, f(x))
+    or Problem(A, y, x0, f, λ; grad_fx, hess_fx) (:61-81, f(A, y, x)), the reference's own
+    keyword callbacks (prox-N-SCORE.jl:49-56, prox-L-BFGS-SCORE.jl:85-91).  They run on the host
+    with NumPy arrays; the smoother, the m x m solve, damping, prox and the loop stay on the
+    device.  There is no automatic differentiation here (the reference falls back to
+    ForwardDiff): ProxLQNSCORE needs grad_fx, ProxNSCORE grad_fx and hess_fx."""
+    return CallbackLoss("callback", 1.0, f, grad_fx, hess_fx)
 
 
 def sigmoid_ce(scale: float = 1.0) -> OutFn:

@@ -90,6 +90,11 @@ class Problem:
         self.name = name
         self.comm = comm
         self.generic = A is None and _ctx is None
+        if f.kind == "callback":   # the data stays with the caller's closures; the device holds none
+            if _ctx is not None or comm is not None:
+                raise ValueError("a callback loss runs on one rank with host-side data")
+            self._cb_data = None if A is None else (A, np.asarray(y, dtype=np.float64).reshape(-1))
+            A, y, self.generic = None, None, True
         self.ctx = _ctx if _ctx is not None else _lib.Context(device)
         if comm is not None and comm.active and _ctx is None:
             comm.attach(self.ctx)
@@ -126,6 +131,43 @@ class Problem:
             raise ValueError("f and out_fn must use the same scale (one device loss scale)")
         scale = f.scale
         self.ctx.check(_lib.lib.scs_set_loss(self.ctx.h, LOSS[f.kind], GGN[ggn], scale))
+        if f.kind == "callback":
+            self._bind_callback(f)
+
+    def _bind_callback(self, f):
+        """Register f / grad_fx / hess_fx with scs_set_loss_callback; a Python exception inside a
+        call is kept and re-raised by Context.check."""
+        data = self._cb_data
+        args = (lambda x: (x,)) if data is None else (lambda x: (data[0], data[1], x))
+        ctx = self.ctx
+
+        def call(user, what, xp, m, outp):
+            try:
+                x = np.ctypeslib.as_array(xp, shape=(m,)).copy()
+                if what == _lib.SCS_CB_F:
+                    outp[0] = float(f.f(*args(x)))
+                elif what == _lib.SCS_CB_GRAD:
+                    if f.grad_fx is None:
+                        raise ValueError("this method needs grad_fx: the device path has no automatic "
+                                         "differentiation (the reference's ForwardDiff default)")
+                    g = np.asarray(f.grad_fx(*args(x)), dtype=np.float64).reshape(m)
+                    np.ctypeslib.as_array(outp, shape=(m,))[:] = g
+                elif what == _lib.SCS_CB_HESS:
+                    if f.hess_fx is None:
+                        raise ValueError("ProxNSCORE needs hess_fx: the device path has no automatic "
+                                         "differentiation (the reference's ForwardDiff default)")
+                    H = np.asarray(f.hess_fx(*args(x)), dtype=np.float64).reshape(m, m)
+                    np.ctypeslib.as_array(outp, shape=(m * m,))[:] = H.ravel(order="F")   # column-major
+                else:
+                    raise ValueError(f"unknown callback request {what}")
+                return 0
+            except BaseException as e:   # noqa: BLE001 -- handed back to the caller by Context.check
+                ctx._cb_exc = e
+                return 1
+
+        cb = _lib.LOSS_FN(call)
+        self.ctx._keep.append(cb)
+        self.ctx.check(_lib.lib.scs_set_loss_callback(self.ctx.h, cb, None))
 
     @classmethod
     def synthetic(cls, N, m, x0, f, lam, *, kind=1, seed=1234, density=0.1, out_fn=None, device=0,

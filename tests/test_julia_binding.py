@@ -76,7 +76,7 @@ C_POINTEE = {"Float64": "double", "Int64": "int64_t", "Int32": "int32_t", "Cint"
 
 def _compatible(jt, ct):
     ct_base = ct.replace("const ", "").strip()
-    if ct_base == "scs_allreduce_fn":                 # function pointer typedef (a @cfunction)
+    if ct_base in ("scs_allreduce_fn", "scs_loss_fn"):   # function pointer typedefs (a @cfunction)
         return jt == "Ptr{Cvoid}"
     is_ptr = ct_base.endswith("*")
     if jt in C_SCALARS:
