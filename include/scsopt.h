@@ -143,15 +143,22 @@ int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
  * `what`: SCS_CB_F    out[0] = f(x)
  *         SCS_CB_GRAD out[0..m) = grad_fx(x)
  *         SCS_CB_HESS out = hess_fx(x), m x m column-major (ProxNSCORE)
+ *         SCS_CB_GGN  out = [J (n x m, column-major) | r (n) | q (n)] with n = ggn_rows:
+ *                     J = jac_yx, r = grad_fy, Q = diag(q) = hess_fy (prox-GGN-SCORE.jl:44-49);
+ *                     a general symmetric Q is passed eigen-rotated (J̃ = VᵀJ, r̃ = Vᵀr,
+ *                     q = its eigenvalues), which leaves JᵀQJ, Jᵀr and the sample-space
+ *                     system of ggn_score_step unchanged (ProxGGNSCORE; multi-output targets
+ *                     ny > 1 are n = N·ny rows)
  * x (m) and out are host arrays owned by the library, valid for the call; return 0 on
  * success, anything else fails the calling ABI function with SCS_ERR_CALLBACK.  There is no
- * automatic differentiation on this path: ProxNSCORE needs SCS_CB_HESS, ProxGGNSCORE needs a
- * data loss kind with an out_fn.                                                          */
+ * automatic differentiation on this path: ProxNSCORE needs SCS_CB_HESS, ProxGGNSCORE
+ * ggn_rows > 0.                                                                            */
 #define SCS_CB_F 0
 #define SCS_CB_GRAD 1
 #define SCS_CB_HESS 2
+#define SCS_CB_GGN 3
 typedef int (*scs_loss_fn)(void* user, int what, const double* x, int64_t m, double* out);
-int scs_set_loss_callback(scs_ctx* ctx, scs_loss_fn fn, void* user);
+int scs_set_loss_callback(scs_ctx* ctx, scs_loss_fn fn, void* user, int64_t ggn_rows);
 
 /* ---- data  (Problem(A, y, ...) -- problems.jl:61-81) --------------------- */
 /* Upload host A (column-major, N x m, leading dim lda) and y (N).  N is the

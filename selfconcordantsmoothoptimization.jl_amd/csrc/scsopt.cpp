@@ -154,6 +154,9 @@ struct scs_ctx {
   void* cb_user = nullptr;
   double* cbh = nullptr;
   size_t cbh_cap = 0;
+  int64_t cb_nout = 0;        // rows of the SCS_CB_GGN Jacobian (0: no GGN callback)
+  NView cbv;                  // that Jacobian, panel-blocked, swapped in for the GGN step
+  double* cbstage = nullptr;  // column-major staging panel for its upload
   bool lbfgs_pending = false; // scs_iterate's device loop: the memory update's dg/gg are read at the epoch end
   int lbfgs_slot = 0;
   double H0 = 1.0;
@@ -1219,6 +1222,8 @@ void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
 void ggn_sample_direction(scs_ctx* c, const double* xh) {
   const int64_t N = c->N, m = c->m;
   if (sharded(c)) return ggn_sample_direction_sharded(c, xh);
+  if (c->At && c->loss == SCS_LOSS_CALLBACK)   // the caller's J changes every step
+    HCK(launch_transpose(c->A, c->Npad, N, m, c->At, c->mpad, c->NpS, c->st));
   if (!c->At) {
     const double* A = dense_A(c);
     c->NpS = round_up(N, 128);
@@ -1239,8 +1244,8 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
     HCK(hipMemcpyAsync(c->stiles, tl.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->st));
     c->nstiles = nt;
   }
-  // s, q, r (prox-GGN-SCORE.jl:44-56) -> gN, hN, wN
-  forward(c, xh, c->x, EPI_GGN | EPI_SQR, false);
+  // s, q, r (prox-GGN-SCORE.jl:44-56) -> gN, hN, wN (a callback loss filled them: ggn_cb_load)
+  if (c->loss != SCS_LOSS_CALLBACK) forward(c, xh, c->x, EPI_GGN | EPI_SQR, false);
   HCK(launch_ggn_sample_prep(c->Hr, c->gr, c->lam, m, c->mpad, c->hvec, c->hg, c->st));
   hipEvent_t e0;
   tbegin(c, T_GRAM, &e0);
@@ -1277,14 +1282,86 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
   HCK(launch_ggn_sample_direction(c->hvec, c->gtmp, c->hg, c->bS, N, m, c->d, c->st));
 }
 
+// host column-major rows (N x m, lda) -> panel-blocked dst (Npad x mpad), one 128-column panel
+// at a time through the column-major staging buffer C (Npad x 128)
+static void upload_panels(scs_ctx* c, const double* A, int64_t N, int64_t lda, int64_t Npad, double* dst, double* C) {
+  const int64_t m = c->m;
+  for (int64_t p = 0; p < c->mpad / 128; ++p) {
+    const int64_t j0 = p * 128, nc = std::min<int64_t>(128, m - j0);
+    HCK(hipMemsetAsync(C, 0, sizeof(double) * Npad * 128, c->st));
+    if (nc > 0 && N > 0)
+      HCK(hipMemcpy2DAsync(C, sizeof(double) * Npad, A + j0 * lda, sizeof(double) * lda, sizeof(double) * N, nc,
+                           hipMemcpyHostToDevice, c->st));
+    HCK(launch_retile(C, dst, Npad, p, 1, c->st));
+  }
+}
+
+// ProxGGNSCORE on a callback loss (jac_yx / grad_fy / hess_fy, prox-GGN-SCORE.jl:44-49): the
+// caller hands over J (n x m, column-major), r and the diagonal q of Q (a general symmetric Q
+// arrives eigen-rotated: J̃ = VᵀJ, r̃ = Vᵀr, q = eigenvalues -- JᵀQJ, Jᵀr and the sample-space
+// system are unchanged).  J is uploaded into the callback view, which then stands in for the
+// data with s = 1: w = q, v = r in the feature branch; (s, q, r) = (1, q, r) in the sample one.
+void ggn_cb_load(scs_ctx* c, const double* xh, bool sample) {
+  const int64_t n = c->cb_nout, m = c->m;
+  const double* out = cb_eval(c, SCS_CB_GGN, xh, c->x, (size_t)n * (m + 2));
+  NView& v = c->cbv;
+  if (!v.A) {
+    v.N = v.Nglob = n;
+    v.Npad = round_up(std::max<int64_t>(n, 1), 16);
+    v.nstage = v.Npad / 16;
+    v.A = dalloc<double>(c, (size_t)v.Npad * c->mpad);
+    v.y = dalloc<double>(c, v.Npad);
+    swap_view(c, v);
+    c->generic = false;
+    alloc_nspace(c);
+    c->generic = true;
+    swap_view(c, v);
+    c->cbstage = dalloc<double>(c, (size_t)v.Npad * 128);
+  }
+  upload_panels(c, out, n, n, v.Npad, v.A, c->cbstage);
+  const double* r = out + (size_t)n * m;
+  const double* q = r + n;
+  if (sample) {
+    HCK(launch_fill(v.gN, n, 1.0, c->st));
+    HCK(hipMemcpyAsync(v.hN, q, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    HCK(hipMemcpyAsync(v.wN, r, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+  } else {
+    HCK(hipMemcpyAsync(v.wN, q, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    HCK(hipMemcpyAsync(v.vN, r, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+  }
+}
+
+// the callback view in place of the (absent) data for one GGN step, restored even on failure
+struct CbScope {
+  scs_ctx* c;
+  explicit CbScope(scs_ctx* cc) : c(cc) {
+    swap_view(c, c->cbv);
+    c->generic = false;
+    invalidate_caches(c);
+  }
+  ~CbScope() {
+    swap_view(c, c->cbv);
+    c->generic = true;
+    invalidate_caches(c);
+  }
+};
+
 // ProxNSCORE / ProxGGNSCORE step
 void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, double* dx, double* pri) {
   const int64_t m = c->m;
   c->g_from_cache = false;
   HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
-  const bool sample_space = (c->method == SCS_PROX_GGNSCORE) && (c->Nglob + 1 <= m) && c->ggn != SCS_GGN_NONE;
+  const bool cbggn = c->method == SCS_PROX_GGNSCORE && c->loss == SCS_LOSS_CALLBACK;
+  const bool sample_space = (c->method == SCS_PROX_GGNSCORE) &&
+                            (cbggn ? c->cb_nout + 1 <= m : (c->Nglob + 1 <= m && c->ggn != SCS_GGN_NONE));
+  if (cbggn) ggn_cb_load(c, xh, sample_space);
   if (sample_space) {
-    ggn_sample_direction(c, xh);
+    if (cbggn) {
+      CbScope scope(c);
+      ggn_sample_direction(c, xh);
+    } else {
+      ggn_sample_direction(c, xh);
+    }
   } else {
   ensure_gram(c);
   if (c->method == SCS_PROX_NSCORE) {
@@ -1309,6 +1386,9 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
       // local Aᵀg (not yet reduced; fused into the Gram pass); reduced together with the Gram
       gram_and_reduce(c, c->hN, c->gN, c->gtmp);
     }
+  } else if (cbggn) {
+    CbScope scope(c);
+    gram_and_reduce(c, c->wN, c->vN, c->gtmp);   // JᵀQJ + Jᵀr of the caller's J (w = q, v = r)
   } else {
     if (c->ggn == SCS_GGN_NONE) fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs an out_fn / GGN loss kind");
     // J, residual, Q (prox-GGN-SCORE.jl:44-56) -> w = s²q, v = s·r
@@ -1594,6 +1674,8 @@ static void reset_data(scs_ctx* c) {
   c->ring_rows = 0;
   c->ring_r0[0] = c->ring_r0[1] = -1;
   dfree_t(c, c->Gk);
+  free_view(c, c->cbv);
+  dfree_t(c, c->cbstage);
   ++c->data_gen;
   c->nnz = 0;
   dfree_t(c, c->y);
@@ -1640,14 +1722,7 @@ int scs_set_data(scs_ctx* c, int64_t N, int64_t m, const double* A, int64_t lda,
       if (N > 0) {
         // panel by panel: host columns -> column-major staging buffer -> panel-blocked A
         double* C = dalloc<double>(c, (size_t)c->Npad * 128);
-        for (int64_t p = 0; p < c->mpad / 128; ++p) {
-          const int64_t j0 = p * 128, nc = std::min<int64_t>(128, m - j0);
-          HCK(hipMemsetAsync(C, 0, sizeof(double) * c->Npad * 128, c->st));
-          if (nc > 0)
-            HCK(hipMemcpy2DAsync(C, sizeof(double) * c->Npad, A + j0 * lda, sizeof(double) * lda, sizeof(double) * N,
-                                 nc, hipMemcpyHostToDevice, c->st));
-          HCK(launch_retile(C, c->A, c->Npad, p, 1, c->st));
-        }
+        upload_panels(c, A, N, lda, c->Npad, c->A, C);
         sync(c);
         dfree_t(c, C);
         if (y) h2d(c, c->y, y, N);
@@ -1912,7 +1987,7 @@ int scs_set_loss(scs_ctx* c, int loss, int ggn, double scale) {
     if (loss == SCS_LOSS_CALLBACK && (!c->has_data || !c->generic))
       fail(c, SCS_ERR_ARG, "a callback loss holds no device data: scs_set_data(N = 0, A = NULL, m) first");
     if (loss == SCS_LOSS_CALLBACK && ggn != SCS_GGN_NONE)
-      fail(c, SCS_ERR_ARG, "a callback loss has no out_fn kind (ProxGGNSCORE needs a data loss kind)");
+      fail(c, SCS_ERR_ARG, "a callback loss has no out_fn kind (its GGN pieces come from the callback)");
     c->loss = loss;
     c->ggn = ggn;
     c->scale = scale;
@@ -1922,10 +1997,16 @@ int scs_set_loss(scs_ctx* c, int loss, int ggn, double scale) {
   });
 }
 
-int scs_set_loss_callback(scs_ctx* c, scs_loss_fn fn, void* user) {
+int scs_set_loss_callback(scs_ctx* c, scs_loss_fn fn, void* user, int64_t ggn_rows) {
   return guarded(c, [&] {
+    if (ggn_rows < 0) fail(c, SCS_ERR_ARG, "ggn_rows must be >= 0");
     c->cb = fn;
     c->cb_user = user;
+    if (ggn_rows != c->cb_nout) {
+      free_view(c, c->cbv);
+      dfree_t(c, c->cbstage);
+      c->cb_nout = ggn_rows;
+    }
     invalidate_caches(c);
   });
 }
@@ -2072,7 +2153,9 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the method");
     if (method < SCS_PROX_NSCORE || method > SCS_PROX_LQNSCORE) fail(c, SCS_ERR_ARG, "unknown method %d", method);
-    if (method == SCS_PROX_GGNSCORE && (c->generic || c->loss == SCS_LOSS_QUADRATIC))
+    if (method == SCS_PROX_GGNSCORE && c->loss == SCS_LOSS_CALLBACK && c->cb_nout <= 0)
+      fail(c, SCS_ERR_ARG, "ProxGGNSCORE on a callback loss needs jac_yx / grad_fy / hess_fy (ggn_rows > 0)");
+    if (method == SCS_PROX_GGNSCORE && c->loss != SCS_LOSS_CALLBACK && (c->generic || c->loss == SCS_LOSS_QUADRATIC))
       fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs a data problem with an out_fn (GGN kind)");
     c->method = method;
     c->ss_type = ss_type;

@@ -8,6 +8,7 @@
 # package `scsopt` (same ABI, same call sequence).
 module SCSOptAMD
 
+using LinearAlgebra
 using Random
 using SparseArrays
 using SelfConcordantSmoothOptimization
@@ -113,7 +114,33 @@ struct LossCallbacks
     f::Function
     grad_fx::Union{Function,Nothing}
     hess_fx::Union{Function,Nothing}
+    out_fn::Union{Function,Nothing}  # ProxGGNSCORE pieces (prox-GGN-SCORE.jl:44-49)
+    jac_yx::Union{Function,Nothing}
+    grad_fy::Union{Function,Nothing}
+    hess_fy::Union{Function,Nothing}
     data::Union{Tuple,Nothing}       # (A, y) of a data problem: the closures take (A, y, x)
+    nout::Int64                      # length(vec(ŷ)): the Jacobian rows (0: no GGN pieces)
+end
+
+# J, r and diag(Q) of the step: a non-diagonal Q is eigen-rotated (J̃ = VᵀJ, r̃ = Vᵀr, q = λ),
+# which leaves JᵀQJ, Jᵀr and the sample-space system of ggn_score_step unchanged
+function ggn_pieces!(out::Vector{Float64}, cbs::LossCallbacks, x::Vector{Float64})
+    A, y = cbs.data
+    n, m = cbs.nout, length(x)
+    ŷ = cbs.out_fn(A, x)
+    J = Matrix{Float64}(reshape(cbs.jac_yx(A, y, ŷ, x), n, m))
+    r = Vector{Float64}(vec(cbs.grad_fy(A, y, ŷ)))
+    Q = cbs.hess_fy(A, y, ŷ)
+    if Q isa AbstractVector || isdiag(Q)
+        q = Q isa AbstractVector ? Vector{Float64}(Q) : Vector{Float64}(diag(Q))
+    else
+        E = eigen(Symmetric(Matrix{Float64}((Q + Q') / 2)))
+        J, r, q = E.vectors' * J, E.vectors' * r, E.values
+    end
+    out[1:n*m] .= vec(J)
+    out[n*m+1:n*(m+1)] .= r
+    out[n*(m+1)+1:n*(m+2)] .= q
+    return nothing
 end
 
 function loss_trampoline(user::Ptr{Cvoid}, what::Cint, xp::Ptr{Float64}, m::Int64, outp::Ptr{Float64})::Cint
@@ -126,6 +153,8 @@ function loss_trampoline(user::Ptr{Cvoid}, what::Cint, xp::Ptr{Float64}, m::Int6
         elseif what == 1
             cbs.grad_fx === nothing && error("this method needs grad_fx (no automatic differentiation on the device path)")
             copyto!(unsafe_wrap(Array, outp, m), cbs.grad_fx(args...))
+        elseif what == 3
+            ggn_pieces!(unsafe_wrap(Array, outp, cbs.nout * (m + 2)), cbs, x)
         else
             cbs.hess_fx === nothing && error("ProxNSCORE needs hess_fx (no automatic differentiation on the device path)")
             copyto!(unsafe_wrap(Array, outp, m * m), vec(Matrix{Float64}(cbs.hess_fx(args...))))   # column-major
@@ -146,19 +175,25 @@ function callback_problem(cbs::LossCallbacks, x0::Vector{Float64}, λ, L, sol, C
     model = finish_problem(ctx, nothing, nothing, x0, :callback, λ, nothing, 1.0, L, sol, C_set, P)
     model.grad_fx = cbs                         # rooted with the model: `user` points at it
     fp = @cfunction(loss_trampoline, Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}, Int64, Ptr{Float64}))
-    chk(ccall((:scs_set_loss_callback, lib), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
-              ctx, fp, pointer_from_objref(cbs)), ctx)
+    chk(ccall((:scs_set_loss_callback, lib), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64),
+              ctx, fp, pointer_from_objref(cbs), cbs.nout), ctx)
     return model
 end
 
 DeviceProblem(x0::Vector{Float64}, f::Function, λ; grad_fx=nothing, hess_fx=nothing, L=nothing,
               sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0) =
-    callback_problem(LossCallbacks(f, grad_fx, hess_fx, nothing), x0, λ, L, sol, C_set, P, device)
+    callback_problem(LossCallbacks(f, grad_fx, hess_fx, nothing, nothing, nothing, nothing, nothing, 0),
+                     x0, λ, L, sol, C_set, P, device)
 
-DeviceProblem(A::AbstractMatrix, y::AbstractVector, x0::Vector{Float64}, f::Function, λ; grad_fx=nothing,
-              hess_fx=nothing, L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing,
-              device::Integer=0) =
-    callback_problem(LossCallbacks(f, grad_fx, hess_fx, (A, y)), x0, λ, L, sol, C_set, P, device)
+# y may be a matrix (ny > 1 outputs, iterate.jl:105-107): out_fn / jac_yx / grad_fy / hess_fy see it as is
+function DeviceProblem(A::AbstractMatrix, y::AbstractVecOrMat, x0::Vector{Float64}, f::Function, λ; grad_fx=nothing,
+                       hess_fx=nothing, out_fn=nothing, jac_yx=nothing, grad_fy=nothing, hess_fy=nothing,
+                       L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0)
+    ggn = all(!isnothing, (out_fn, jac_yx, grad_fy, hess_fy))
+    nout = ggn ? Int64(length(out_fn(A, x0))) : 0
+    cbs = LossCallbacks(f, grad_fx, hess_fx, out_fn, jac_yx, grad_fy, hess_fy, (A, y), nout)
+    return callback_problem(cbs, x0, λ, L, sol, C_set, P, device)
+end
 
 # ---- row sharding (SURVEY.md §8e): one process per GPU, A's rows split across them ---------
 # libscsopt's own RCCL communicator: rank 0 draws the id, the caller hands the 128 bytes to

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCSOPT_LIB", os.path.join(_HERE, "libscsopt.so"))
 
 SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS_ERR_COMM, SCS_ERR_CALLBACK = range(8)
-SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS = range(3)
+SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS, SCS_CB_GGN = range(4)
 
 LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5, "callback": 6}
 GGN = {None: 0, "sigmoid_ce": 1, "linear_ls": 2}
@@ -88,7 +88,7 @@ _SIGS = {
     "scs_get_nnz": (C.c_int, [C.c_void_p, c_i64p]),
     "scs_get_sparse": (C.c_int, [C.c_void_p, c_i64p, c_i32p, c_dp]),
     "scs_set_loss": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double]),
-    "scs_set_loss_callback": (C.c_int, [C.c_void_p, LOSS_FN, C.c_void_p]),
+    "scs_set_loss_callback": (C.c_int, [C.c_void_p, LOSS_FN, C.c_void_p, C.c_int64]),
     "scs_set_reg": (C.c_int, [C.c_void_p, C.c_int, c_dp, C.c_int, c_dp, c_dp, C.c_int64, c_i64p, C.c_int64]),
     "scs_set_smoother": (C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_double, c_dp, c_dp,
                                    C.c_int64]),

@@ -61,16 +61,29 @@ class CallbackLoss(Loss):
     f: Optional[Callable] = field(default=None, repr=False)
     grad_fx: Optional[Callable] = field(default=None, repr=False)
     hess_fx: Optional[Callable] = field(default=None, repr=False)
+    out_fn: Optional[Callable] = field(default=None, repr=False)
+    jac_yx: Optional[Callable] = field(default=None, repr=False)
+    grad_fy: Optional[Callable] = field(default=None, repr=False)
+    hess_fy: Optional[Callable] = field(default=None, repr=False)
+
+    @property
+    def has_ggn(self):
+        return None not in (self.out_fn, self.jac_yx, self.grad_fy, self.hess_fy)
 
 
-def callback(f, grad_fx=None, hess_fx=None) -> CallbackLoss:
+def callback(f, grad_fx=None, hess_fx=None, *, out_fn=None, jac_yx=None, grad_fy=None,
+             hess_fy=None) -> CallbackLoss:
     """A user loss outside the menu: Problem(x0, f, λ; grad_fx, hess_fx) (problems.jl:44-59, f(x))
-    or Problem(A, y, x0, f, λ; grad_fx, hess_fx) (:61-81, f(A, y, x)), the reference's own
-    keyword callbacks (prox-N-SCORE.jl:49-56, prox-L-BFGS-SCORE.jl:85-91).  They run on the host
-    with NumPy arrays; the smoother, the m x m solve, damping, prox and the loop stay on the
-    device.  There is no automatic differentiation here (the reference falls back to
-    ForwardDiff): ProxLQNSCORE needs grad_fx, ProxNSCORE grad_fx and hess_fx."""
-    return CallbackLoss("callback", 1.0, f, grad_fx, hess_fx)
+    or Problem(A, y, x0, f, λ; grad_fx, hess_fx, out_fn, jac_yx, grad_fy, hess_fy) (:61-81,
+    f(A, y, x)), the reference's own keyword callbacks (prox-N-SCORE.jl:49-56,
+    prox-L-BFGS-SCORE.jl:85-91, prox-GGN-SCORE.jl:44-49).  They run on the host with NumPy
+    arrays; the smoother, the Gram / m x m solve or the sample-space system, damping, prox and the
+    loop stay on the device.  There is no automatic differentiation here (the reference falls
+    back to ForwardDiff): ProxLQNSCORE needs grad_fx, ProxNSCORE grad_fx and hess_fx,
+    ProxGGNSCORE out_fn(A, x), jac_yx(A, y, ŷ, x) (rows = vec(ŷ), column-major for a
+    multi-output ŷ), grad_fy(A, y, ŷ) and hess_fy(A, y, ŷ) (a vector = diagonal Q, or a
+    symmetric matrix) plus grad_fx for the line search."""
+    return CallbackLoss("callback", 1.0, f, grad_fx, hess_fx, out_fn, jac_yx, grad_fy, hess_fy)
 
 
 def sigmoid_ce(scale: float = 1.0) -> OutFn:

@@ -93,7 +93,8 @@ class Problem:
         if f.kind == "callback":   # the data stays with the caller's closures; the device holds none
             if _ctx is not None or comm is not None:
                 raise ValueError("a callback loss runs on one rank with host-side data")
-            self._cb_data = None if A is None else (A, np.asarray(y, dtype=np.float64).reshape(-1))
+            # y keeps its shape: an N x ny target is a multi-output problem (iterate.jl:105-107)
+            self._cb_data = None if A is None else (A, np.asarray(y, dtype=np.float64))
             A, y, self.generic = None, None, True
         self.ctx = _ctx if _ctx is not None else _lib.Context(device)
         if comm is not None and comm.active and _ctx is None:
@@ -140,6 +141,31 @@ class Problem:
         data = self._cb_data
         args = (lambda x: (x,)) if data is None else (lambda x: (data[0], data[1], x))
         ctx = self.ctx
+        nout = 0
+        if f.has_ggn:
+            if data is None:
+                raise ValueError("ProxGGNSCORE callbacks take the data: Problem(A, y, x0, callback(...), λ)")
+            nout = int(np.asarray(f.out_fn(data[0], self.x0)).size)
+
+        def ggn_pieces(x, m, outp):
+            """prox-GGN-SCORE.jl:44-49 on the host; a non-diagonal Q is eigen-rotated (J̃ = VᵀJ,
+            r̃ = Vᵀr, q = eigenvalues), which leaves JᵀQJ, Jᵀr and the sample-space system exact."""
+            A, y = data
+            yhat = f.out_fn(A, x)
+            J = np.asarray(f.jac_yx(A, y, yhat, x), dtype=np.float64).reshape(nout, m)
+            r = np.asarray(f.grad_fy(A, y, yhat), dtype=np.float64).ravel(order="F")
+            Q = np.asarray(f.hess_fy(A, y, yhat), dtype=np.float64)
+            if Q.ndim == 2 and np.count_nonzero(Q - np.diag(np.diagonal(Q))) == 0:
+                Q = np.diagonal(Q).copy()
+            if Q.ndim == 2:
+                lam, V = np.linalg.eigh(0.5 * (Q + Q.T))
+                J, r, q = V.T @ J, V.T @ r, lam
+            else:
+                q = Q.reshape(nout)
+            out = np.ctypeslib.as_array(outp, shape=(nout * (m + 2),))
+            out[:nout * m] = J.ravel(order="F")
+            out[nout * m:nout * (m + 1)] = r
+            out[nout * (m + 1):] = q
 
         def call(user, what, xp, m, outp):
             try:
@@ -158,6 +184,8 @@ class Problem:
                                          "differentiation (the reference's ForwardDiff default)")
                     H = np.asarray(f.hess_fx(*args(x)), dtype=np.float64).reshape(m, m)
                     np.ctypeslib.as_array(outp, shape=(m * m,))[:] = H.ravel(order="F")   # column-major
+                elif what == _lib.SCS_CB_GGN:
+                    ggn_pieces(x, m, outp)
                 else:
                     raise ValueError(f"unknown callback request {what}")
                 return 0
@@ -167,7 +195,7 @@ class Problem:
 
         cb = _lib.LOSS_FN(call)
         self.ctx._keep.append(cb)
-        self.ctx.check(_lib.lib.scs_set_loss_callback(self.ctx.h, cb, None))
+        self.ctx.check(_lib.lib.scs_set_loss_callback(self.ctx.h, cb, None, nout))
 
     @classmethod
     def synthetic(cls, N, m, x0, f, lam, *, kind=1, seed=1234, density=0.1, out_fn=None, device=0,

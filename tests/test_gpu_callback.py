@@ -136,7 +136,113 @@ def test_callback_errors():
     q = scsopt.Problem(A, y, x0, losses.callback(bad, g), 1e-3)
     with pytest.raises(Boom):                                   # the user's own exception comes back
         scsopt.iterate(scsopt.ProxLQNSCORE(m=3), q, "l1", hm, max_epoch=2, verbose=0)
-    with pytest.raises(scsopt.ScsError, match="ProxGGNSCORE"):
+    with pytest.raises(scsopt.ScsError, match="ProxGGNSCORE"):          # no jac_yx / grad_fy / hess_fy
         scsopt.iterate(scsopt.ProxGGNSCORE(), p, "l1", hm, max_epoch=2, verbose=0)
     with pytest.raises(ValueError, match="minibatches"):
         scsopt.iterate(scsopt.ProxLQNSCORE(m=3), p, "l1", hm, max_epoch=2, verbose=0, batch_size=5)
+
+
+def _sigmoid_ce_cbs(N):
+    """The reference's GGN test loss (test/test_algs.jl:10-11: Mfunc = sigmoid, CE on ŷ) written
+    as the keyword callbacks out_fn / jac_yx / grad_fy / hess_fy (prox-GGN-SCORE.jl:44-49)."""
+    sig = lambda z: 1.0 / (1.0 + np.exp(-z))  # noqa: E731
+
+    def f(A, y, x):
+        yh = sig(A @ x)
+        return -float(np.sum(y * np.log(yh) + (1 - y) * np.log(1 - yh))) / N
+
+    def g(A, y, x):
+        return A.T @ (sig(A @ x) - y) / N
+
+    def out_fn(A, x):
+        return sig(A @ x)
+
+    def jac_yx(A, y, yh, x):
+        return (yh * (1 - yh))[:, None] * A
+
+    def grad_fy(A, y, yh):
+        return (-(y / yh) + (1 - y) / (1 - yh)) / N
+
+    def hess_fy(A, y, yh):
+        return (y / yh ** 2 + (1 - y) / (1 - yh) ** 2) / N
+    return losses.callback(f, g, out_fn=out_fn, jac_yx=jac_yx, grad_fy=grad_fy, hess_fy=hess_fy)
+
+
+@pytest.mark.parametrize("N,m", [(300, 40), (30, 64)])
+def test_ggn_callback_matches_device_kind(N, m):
+    """ProxGGNSCORE on the callback pieces (J uploaded per step, w = q, v = r) vs the device
+    sigmoid-CE kind on the same data: feature branch (N+1 > m) and sample branch (N+1 <= m)."""
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((N, m)) / np.sqrt(m)
+    y = (rng.random(N) < 1.0 / (1.0 + np.exp(-A @ rng.standard_normal(m)))).astype(np.float64)
+    x0 = rng.standard_normal(m) * 0.2
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    pk = scsopt.Problem(A, y, x0, losses.logistic_ce(1.0 / N), 2e-3, out_fn=losses.sigmoid_ce(1.0 / N))
+    pc = scsopt.Problem(A, y, x0, _sigmoid_ce_cbs(N), 2e-3)
+    a = scsopt.iterate(scsopt.ProxGGNSCORE(), pk, "l1", hm, max_epoch=6, verbose=0)
+    b = scsopt.iterate(scsopt.ProxGGNSCORE(), pc, "l1", hm, max_epoch=6, verbose=0)
+    assert a.epochs == b.epochs
+    np.testing.assert_allclose(b.obj, a.obj, rtol=1e-10)
+    np.testing.assert_allclose(b.x, a.x, rtol=1e-8, atol=1e-11)
+
+
+def _softmax_cbs(N, d, ny):
+    """Multinomial logistic regression, ŷ = A X (logits, N x ny, X = reshape(x, d, ny)): a
+    multi-output target (iterate.jl:105-107,207) with a non-diagonal Q (per sample
+    diag(p) - p pᵀ, interleaved in vec(ŷ) order) -- the eigen-rotated callback path."""
+    def probs(Z):
+        E = np.exp(Z - Z.max(axis=1, keepdims=True))
+        return E / E.sum(axis=1, keepdims=True)
+
+    def f(A, Y, x):
+        P = probs(A @ x.reshape(d, ny, order="F"))
+        return -float(np.sum(Y * np.log(P))) / N
+
+    def g(A, Y, x):
+        P = probs(A @ x.reshape(d, ny, order="F"))
+        return (A.T @ (P - Y)).ravel(order="F") / N
+
+    def out_fn(A, x):
+        return A @ x.reshape(d, ny, order="F")
+
+    def jac_yx(A, Y, Z, x):
+        return np.kron(np.eye(ny), A)          # rows (i, k) = i + N k, columns (j, l) = j + d l
+
+    def grad_fy(A, Y, Z):
+        return (probs(Z) - Y) / N
+
+    def hess_fy(A, Y, Z):
+        P = probs(Z)
+        Q = np.zeros((N * ny, N * ny))
+        for i in range(N):
+            idx = i + N * np.arange(ny)
+            Q[np.ix_(idx, idx)] = (np.diag(P[i]) - np.outer(P[i], P[i])) / N
+        return Q
+    return f, g, out_fn, jac_yx, grad_fy, hess_fy
+
+
+@pytest.mark.parametrize("N,d", [(120, 20), (20, 30)])
+def test_ggn_callback_multioutput_softmax_vs_oracle(N, d):
+    """ny = 3 classes: n = N·ny Jacobian rows, Q block-diagonal in vec(ŷ) order.  (120, 20):
+    n + 1 = 361 > m = 60, feature branch; (20, 30): n + 1 = 61 <= m = 90, sample branch.  Device
+    (eigen-rotated rows, weighted Gram / LU) vs the oracle's literal ggn_score_step with the dense
+    Q (prox-GGN-SCORE.jl:114-135); the reference has no multi-output test: parity unpinned by the
+    reference."""
+    ny = 3
+    rng = np.random.default_rng(21)
+    A = rng.standard_normal((N, d)) / np.sqrt(d)
+    W = rng.standard_normal((d, ny))
+    lab = np.argmax(A @ W + 0.3 * rng.standard_normal((N, ny)), axis=1)
+    Y = np.eye(ny)[lab]
+    m = d * ny
+    x0 = np.zeros(m)
+    f, g, out_fn, jac, gfy, hfy = _softmax_cbs(N, d, ny)
+    cb = losses.callback(f, g, out_fn=out_fn, jac_yx=jac, grad_fy=gfy, hess_fy=hfy)
+    lam = 1e-3
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), scsopt.Problem(A, Y, x0, cb, lam), "l1",
+                         scsopt.PHuberSmootherL1L2(0.5), max_epoch=6, verbose=0)
+    ocb = O.CallbackLoss(f, g, out_fn=out_fn, jac_yx=jac, grad_fy=gfy, hess_fy=hfy)
+    osol = O.iterate(O.ProxGGNSCORE(), O.Problem(A, Y, x0, ocb, lam), "l1", O.PHuberSmootherL1L2(0.5), max_epoch=6)
+    assert sol.epochs == osol.epochs
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
