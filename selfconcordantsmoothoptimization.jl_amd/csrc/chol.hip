@@ -376,6 +376,13 @@ void chol_aux_free(CholAux* a) {
   if (a->ev1) (void)hipEventDestroy(a->ev1);
   if (a->ev2) (void)hipEventDestroy(a->ev2);
   if (a->ev3) (void)hipEventDestroy(a->ev3);
+  for (auto& q : a->ssched) {
+    if (q.work) (void)hipFree(q.work);
+    if (q.comb) (void)hipFree(q.comb);
+  }
+  a->ssched.clear();
+  if (a->spart) (void)hipFree(a->spart);
+  a->spart = nullptr;
   if (a->st2) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
@@ -384,6 +391,7 @@ void chol_aux_free(CholAux* a) {
 }
 
 static const int2* rect_list(const CholAux* a, int R) { return a->rect + (int64_t)a->nblk * (R - 1) * R / 2; }
+int chol_outer_block();
 
 static int outer_block() {
   static const int ob = [] {
@@ -504,6 +512,116 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
   }
   if (c12_pending) wait(st, a->ev2);
   if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Strip pipeline.  Where the Gram is computed strip by strip (scsopt.cpp), the factor runs
+// LEFT-looking behind it: strip s receives the updates of all earlier strips in one launch
+// (K = i0·128 rows of U) once its own Gram strip has landed, then its diagonal block (A) and
+// row strip (B) are factored exactly as in chol_factor.  There is no trailing update: the
+// later strips pull theirs.  Few tiles with a long K (the last strips) are what
+// gram_schedule's K-split tail pieces are for.
+int chol_outer_block() { return outer_block(); }
+
+hipError_t chol_pipe_init(CholAux* a, int64_t mpad, hipStream_t st) {
+  if (!a->ssched.empty()) return hipSuccess;
+  const int nblk = (int)(mpad / CB), OB = outer_block();
+  const int ns = (nblk + OB - 1) / OB;
+  std::vector<int2> lst;   // (i >= j, j < OB), row-major in i: a strip's list is a prefix
+  for (int i = 0; i < nblk; ++i)
+    for (int j = 0; j <= i && j < OB; ++j) lst.push_back(make_int2(i, j));
+  a->ssched.resize(ns);
+  int npart_max = 0;
+  hipError_t e = hipSuccess;
+  for (int s = 1; s < ns && e == hipSuccess; ++s) {
+    const int nc = nblk - s * OB;
+    int n = 0;
+    for (int i = 0; i < nc; ++i) n += std::min(i + 1, OB);
+    std::vector<int4> wk, cb;
+    int nsplit = 1, npart = 0;
+    const int seglen = gram_schedule(lst.data(), n, 64, wk, cb, &nsplit, &npart);
+    CholAux::StripSched& q = a->ssched[s];
+    q.seglen = seglen;
+    q.nsplit = nsplit;
+    q.ncomb = (int)cb.size();
+    npart_max = std::max(npart_max, npart);
+    e = hipMalloc(&q.work, sizeof(int4) * wk.size());
+    if (e == hipSuccess) e = hipMemcpyAsync(q.work, wk.data(), sizeof(int4) * wk.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && !cb.empty()) {
+      e = hipMalloc(&q.comb, sizeof(int4) * cb.size());
+      if (e == hipSuccess) e = hipMemcpyAsync(q.comb, cb.data(), sizeof(int4) * cb.size(), hipMemcpyHostToDevice, st);
+    }
+  }
+  if (e == hipSuccess && npart_max > 0) e = hipMalloc(&a->spart, sizeof(double) * (size_t)npart_max * CB * CB);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return e;
+}
+
+hipError_t chol_strip_update(double* G, int64_t ld, int s, const CholAux* a, hipStream_t st) {
+  if (s <= 0 || s >= (int)a->ssched.size()) return hipSuccess;
+  const int i0 = s * outer_block();
+  const CholAux::StripSched& q = a->ssched[s];
+  const double* X = G + (int64_t)i0 * CB * ld;
+  double* trail = G + (int64_t)i0 * CB * ld + (int64_t)i0 * CB;
+  return gram_launch_sched_cm(X, ld, a->w + CB, 0, (int64_t)i0 * CB, q.work, q.seglen, q.nsplit, q.comb, q.ncomb,
+                              a->spart, trail, ld, /*GRAM_ACCUMULATE*/ 2, st);
+}
+
+hipError_t chol_strip_factor(double* G, int64_t ld, int s, double* W, const CholAux* a, const int2* trilist, int* info,
+                             hipStream_t st) {
+  const int nblk = a->nblk, OB = outer_block();
+  const int i0 = s * OB, i1 = std::min(i0 + OB, nblk);
+  for (int k = i0; k < i1; ++k) {
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+    const int nb = i1 - k - 1;
+    if (nb == 0) break;
+    double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;
+    hipError_t e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb,
+                                   rowpanel, ld, 0, st);
+    if (e != hipSuccess) return e;
+    double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
+    e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld, 2 | 4, st);
+    if (e != hipSuccess) return e;
+  }
+  const int nc = nblk - i1;
+  if (nc > 0) {
+    hipError_t e = strip_solve(G, ld, W, a, i0, i1, i1, nc, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipGetLastError();
+}
+
+// dst(r0:r1, c) = src(r0:r1, c) for c in [c0, c1) (column-major, ld): a strip of the upper system.
+// One workgroup per column run of 8 columns, the rows contiguous (hipMemcpy2DAsync's rectangle blit
+// moved these 64 MB strips at 13 GB/s).
+__global__ void copy_rows_kernel(double* __restrict__ dst, const double* __restrict__ src, int64_t ld, int64_t r0,
+                                 int64_t r1, int64_t c0, int64_t c1) {
+  const int64_t nr = r1 - r0;
+  for (int64_t c = c0 + (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); c < c1; c += (int64_t)gridDim.x * 8) {
+    const double* s = src + c * ld + r0;
+    double* d = dst + c * ld + r0;
+    for (int64_t i = 2 * (threadIdx.x & 31); i + 1 < nr; i += 64) *(v2d*)(d + i) = *(const v2d*)(s + i);
+    if ((nr & 1) && (threadIdx.x & 31) == 0) d[nr - 1] = s[nr - 1];
+  }
+}
+
+hipError_t chol_copy_rows(double* dst, const double* src, int64_t ld, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                          hipStream_t st) {
+  if (r1 <= r0 || c1 <= c0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(c1 - c0, 8), 2048);
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(grid), dim3(256), 0, st, dst, src, ld, r0, r1, c0, c1);
+  return hipGetLastError();
+}
+
+__global__ void diag_pad_range_kernel(double* __restrict__ G, int64_t ld, int64_t lo, int64_t hi) {
+  const int64_t i = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < hi) G[i * ld + i] = 1.0;
+}
+
+hipError_t chol_diag_pad(double* G, int64_t ld, int64_t lo, int64_t hi, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(diag_pad_range_kernel, dim3((unsigned)ceil_div(hi - lo, 256)), dim3(256), 0, st, G, ld, lo, hi);
   return hipGetLastError();
 }
 

@@ -1070,6 +1070,21 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
   return hipGetLastError();
 }
 
+// Column-major scheduled form (the Cholesky's left-looking strip updates: long K, few tiles):
+// gram_sia_kernel<CM> over the work list, K rows [k0, k1) of X, then the combine.  flags: GRAM_*
+// with GRAM_UPPER placement (GRAM_ACCUMULATE adds into G).
+hipError_t gram_launch_sched_cm(const double* X, int64_t ld, const double* w, int64_t k0, int64_t k1, const int4* work,
+                                int seglen, int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg,
+                                int flags, hipStream_t st) {
+  if (seglen <= 0 || k1 <= k0) return hipSuccess;
+  hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(8 * seglen), dim3(256), 0, st, X, ld, w, k0, k1, nullptr, 0,
+                     G, ldg, flags | GRAM_UPPER, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
+  if (ncomb > 0)
+    hipLaunchKernelGGL(gram_combine_kernel<2>, dim3(16, ncomb), dim3(256), 0, st, P, comb, nsplit, G, ldg,
+                       (flags & GRAM_ACCUMULATE) ? 2 : 0);
+  return hipGetLastError();
+}
+
 // Host: build the scheduled work list from the canonical tile list.  The list is
 // cut into 8 contiguous XCD segments (XCD x = blocks orig % 8 == x, run in
 // orig order); in each segment the tiles that would form a partial last round

@@ -64,6 +64,16 @@ struct CholAux {             // device constants of the two-level factorization 
   hipStream_t st2 = nullptr; // lookahead: the bulk stream (strip solve beyond the next block, C12)
   hipEvent_t ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   int nblk = 0;
+  // strip pipeline (chol_pipe_init): the left-looking update of each outer strip s as a
+  // tail-balanced scheduled launch over the pairs (i >= j, j < OB) of its trailing columns
+  struct StripSched {
+    int4* work = nullptr;
+    int seglen = 0, nsplit = 1;
+    int4* comb = nullptr;
+    int ncomb = 0;
+  };
+  std::vector<StripSched> ssched;
+  double* spart = nullptr;   // K-split partial tiles of those launches
 };
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);
 void chol_aux_free(CholAux* a);
@@ -71,6 +81,24 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
                        const int2* trilist, int* info, hipStream_t st);
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
                       hipStream_t st);
+// Strip pipeline (scsopt.cpp gram_factor_pipelined): the factor runs left-looking behind a Gram
+// computed strip by strip.  Strip s = inner blocks [s·OB, min((s+1)·OB, nblk)).
+int chol_outer_block();
+hipError_t chol_pipe_init(CholAux* a, int64_t mpad, hipStream_t st);
+// strip s -= U[0:i0, strip]ᵀ U[0:i0, strip..] (all earlier strips at once, K = i0·128)
+hipError_t chol_strip_update(double* G, int64_t ld, int s, const CholAux* a, hipStream_t st);
+// A and B of strip s: its diagonal block by the 128-blocked loop, then its row strip solved
+hipError_t chol_strip_factor(double* G, int64_t ld, int s, double* W, const CholAux* a, const int2* trilist, int* info,
+                             hipStream_t st);
+// dst(r0:r1, c0:c1) = src(r0:r1, c0:c1), column-major with leading dimension ld (r0 even)
+hipError_t chol_copy_rows(double* dst, const double* src, int64_t ld, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                          hipStream_t st);
+// G[i, i] = 1 for i in [lo, hi) (the padding of block-diag(A, I))
+hipError_t chol_diag_pad(double* G, int64_t ld, int64_t lo, int64_t hi, hipStream_t st);
+// the Cholesky's column-major form of the scheduled Gram: A1 = A2 = X (lda = ld), K rows [k0, k1)
+hipError_t gram_launch_sched_cm(const double* X, int64_t ld, const double* w, int64_t k0, int64_t k1, const int4* work,
+                                int seglen, int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg,
+                                int flags, hipStream_t st);
 
 // ---- lu.hip (blocked LU with partial pivoting, row-major, in place; lu_solve after lu_factor)
 struct LUAux {

@@ -187,7 +187,20 @@ struct scs_ctx {
   int4* gcomb = nullptr;
   int gseglen = 0, gncomb = 0, gnsplit = 1;
   double* gpart = nullptr;
-  double* vpart = nullptr;   // fused Aᵀv partials: max(gnsplit, 1) rows of mpad
+  double* vpart = nullptr;   // fused Aᵀv partials: max(gnsplit, strip nsplits, 1) rows of mpad
+  // strip pipeline (gram_factor_pipelined): the Gram's tile list cut into the factor's outer
+  // strips (tiles with bj in strip s), one tail-balanced schedule each; the factor stream and
+  // one event per strip
+  struct GStrip {
+    int4* work = nullptr;
+    int4* comb = nullptr;
+    int seglen = 0, nsplit = 1, ncomb = 0;
+  };
+  std::vector<GStrip> gstrip;
+  int vpieces = 1;           // rows of vpart
+  hipStream_t sf = nullptr;
+  std::vector<hipEvent_t> evstrip;
+  hipEvent_t evfac = nullptr;
   double* W = nullptr;      // inverted diagonal blocks of the Cholesky factor [mpad/128][128*128]
   double* ysol = nullptr;   // triangular-solve scratch (mpad)
   int2* trilist = nullptr;  // row-major lower tiles
@@ -570,7 +583,44 @@ void ensure_gram(scs_ctx* c) {
       }
     }
   }
-  c->vpart = dalloc<double>(c, (size_t)std::max(c->gnsplit, 1) * mp);
+  {
+    // the strips of the pipeline: tiles whose column block (bj, 128-wide) lies in outer strip s
+    const int OB = chol_outer_block(), ns = (nb + OB - 1) / OB;
+    c->gstrip.assign(ns, scs_ctx::GStrip());
+    c->vpieces = std::max(c->gnsplit, 1);
+    int npart_max = 0;
+    for (int s2 = 0; s2 < ns; ++s2) {
+      std::vector<int2> st;
+      for (int t = 0; t < nt; ++t)
+        if (tl[t].y / OB == s2) st.push_back(tl[t]);
+      std::vector<int4> wk, cb;
+      int nsplit = 1, npart = 0;
+      scs_ctx::GStrip& g = c->gstrip[s2];
+      g.seglen = gram_schedule(st.data(), (int)st.size(), 32 * (c->tall ? 1 : 2), wk, cb, &nsplit, &npart);
+      g.nsplit = nsplit;
+      g.ncomb = (int)cb.size();
+      g.work = dalloc<int4>(c, wk.size());
+      HCK(hipMemcpyAsync(g.work, wk.data(), sizeof(int4) * wk.size(), hipMemcpyHostToDevice, c->st));
+      if (!cb.empty()) {
+        g.comb = dalloc<int4>(c, cb.size());
+        HCK(hipMemcpyAsync(g.comb, cb.data(), sizeof(int4) * cb.size(), hipMemcpyHostToDevice, c->st));
+      }
+      npart_max = std::max(npart_max, npart);
+      c->vpieces = std::max(c->vpieces, nsplit);
+    }
+    if (npart_max > 0) {
+      const size_t need = (size_t)npart_max * (c->tall ? 256 : 128) * 128;
+      // gpart is shared with the one-launch schedule: size it for the larger user
+      size_t have = 0;
+      for (auto& a : c->allocs)
+        if (a.p == c->gpart) have = a.bytes / sizeof(double);
+      if (need > have) {
+        if (c->gpart) dfree_t(c, c->gpart);
+        c->gpart = dalloc<double>(c, need);
+      }
+    }
+  }
+  c->vpart = dalloc<double>(c, (size_t)c->vpieces * mp);
   c->utiles = dalloc<int2>(c, ul.size());
   HCK(hipMemcpyAsync(c->utiles, ul.data(), sizeof(int2) * ul.size(), hipMemcpyHostToDevice, c->st));
   {
@@ -935,26 +985,11 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
 // partial pivoting (lu.hip; the reference's `\`, prox-N-SCORE.jl:70) from the saved copy when
 // a pivot is not positive (e.g. the indefinite Q of a CE loss on ±1 labels,
 // test/test_algs.jl:10), or always with force_lu (scs_solve_eval).
-void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
+// the LU fallback: the full symmetric system from the copy Gc (rebuilt from the cached Gram when
+// this step's Gram came from the cache), the reference's `\` (prox-N-SCORE.jl:70)
+void solve_lu_fallback(scs_ctx* c, double* rhs, hipEvent_t e0) {
   const int64_t m = c->m, ld = c->mpad;
-  hipEvent_t e0;
-  tbegin(c, T_SOLVE, &e0);
-  // the LU fallback needs the system the in-place factor destroys: copied up front, or -- when
-  // this step's Gram came from the cache -- rebuilt from it only if the factor fails
-  if (!c->g_from_cache) HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
   int info = 0;
-  if (!force_lu) {
-    HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
-    HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
-    HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
-    sync(c);
-    if (info == 0) {
-      HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, c->st));
-      c->lu_fallback_used = false;
-      tend(c, T_SOLVE, e0);
-      return;
-    }
-  }
   if (c->g_from_cache) {
     HCK(hipMemcpyAsync(c->Gc, c->Gk, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
     HCK(launch_diag_add(c->Gc, c->mpad, m, c->lam, c->Hr, c->st));
@@ -981,6 +1016,49 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
   if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
   HCK(lu_solve(c->Gc, ld, ld, &c->lu, rhs, c->st));
   tend(c, T_SOLVE, e0);
+}
+
+// solve (G + λ diag Hr) sol = rhs in place (rhs -> sol, length m_pad, zero-padded).
+// Hand-written blocked Cholesky on MFMA (chol.hip) first; the hand-written blocked LU with
+// partial pivoting (lu.hip; the reference's `\`, prox-N-SCORE.jl:70) from the saved copy when
+// a pivot is not positive (e.g. the indefinite Q of a CE loss on ±1 labels,
+// test/test_algs.jl:10), or always with force_lu (scs_solve_eval).
+void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
+  const int64_t m = c->m, ld = c->mpad;
+  hipEvent_t e0;
+  tbegin(c, T_SOLVE, &e0);
+  // the LU fallback needs the system the in-place factor destroys: copied up front, or -- when
+  // this step's Gram came from the cache -- rebuilt from it only if the factor fails
+  if (!c->g_from_cache) HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+  int info = 0;
+  if (!force_lu) {
+    HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+    HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
+    HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    if (info == 0) {
+      HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, c->st));
+      c->lu_fallback_used = false;
+      tend(c, T_SOLVE, e0);
+      return;
+    }
+  }
+  solve_lu_fallback(c, rhs, e0);
+}
+
+// the pipelined path's solve: the factor (and Gc) are already enqueued (gram_factor_pipelined,
+// which opened the T_SOLVE interval at the end of the Gram)
+void solve_factored(scs_ctx* c, double* rhs, hipEvent_t e0) {
+  int info = 0;
+  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  if (info == 0) {
+    HCK(chol_solve(c->G, c->mpad, c->mpad, c->W, rhs, c->ysol, c->st));
+    c->lu_fallback_used = false;
+    tend(c, T_SOLVE, e0);
+    return;
+  }
+  solve_lu_fallback(c, rhs, e0);
 }
 
 // the main Gram launch (scheduled when gram_schedule built a work list)
@@ -1131,6 +1209,80 @@ void gram_and_reduce(scs_ctx* c, const double* w, const double* v, double* vec_d
     HCK(hipMemcpyAsync(c->Gk, c->G, gbytes, hipMemcpyDeviceToDevice, c->st));
     c->gk_gen = c->data_gen;
   }
+}
+
+// The factor hidden under the Gram (SCS_CHOL_PIPE=1; off by default, see below): one scheduled Gram launch per
+// outer strip of the system on the context stream; on a second stream, as each strip lands:
+// λ·Hr on its diagonal (and the padding's 1s), its copy into Gc (the LU fallback's system), the
+// left-looking update from every earlier strip, its diagonal block and row strip
+// (chol_strip_update / chol_strip_factor).  Only the last strip's factor and the two triangular
+// solves remain after the Gram.  Single rank, dense A, Gram not served from the cache; m/128 >= 3
+// outer blocks.  The result is the same factor up to the summation order of the updates
+// (left- instead of right-looking).
+// Measured at C2 (m = 8192, one box, same build): step 118.5 ms piped vs 107.7 ms classic.  The
+// exposed solve drops 13.1 -> 6.2 ms, but the Gram grows 93.3 -> 110.9 ms: a strip launch is less
+// than one round of the chip (strip 0: 484 tiles on 512 slots took 24.3 ms alone against its 21.5 ms
+// share -- the interleaved kernel does not run a lone workgroup per CU twice as fast), and the
+// factor's workgroups share CUs with MFMA-bound Gram waves (the left-looking updates ran at ~11 %
+// of their alone rate).  At C3 (16 strips of 256 x 128 tiles) the partial rounds alone would cost
+// seconds.  Hiding the factor needs the one-launch Gram with per-strip completion counters.
+bool pipe_ok(const scs_ctx* c, bool cacheable) {
+  const char* e = std::getenv("SCS_CHOL_PIPE");   // read per step (tests toggle it in-process)
+  const bool on = e && e[0] == '1';
+  const int64_t nblk = c->mpad / 128;
+  return on && !cacheable && !sharded(c) && !sparse_streams(const_cast<scs_ctx*>(c)) && c->gwork &&
+         nblk >= 3 * chol_outer_block();
+}
+
+// Gram (+ fused Aᵀv into vec_dev) and the factor of G + λ diag(Hr); Gc receives the system.
+// Returns with the factor enqueued on c->st (info in c->cinfo).
+hipEvent_t gram_factor_pipelined(scs_ctx* c, const double* w, const double* v, double* vec_dev) {
+  const int64_t m = c->m, ld = c->mpad;
+  const int nb = (int)(ld / 128), OB = chol_outer_block(), ns = (int)c->gstrip.size();
+  HCK(chol_pipe_init(&c->caux, ld, c->st));
+  if (!c->sf) {
+    HCK(hipStreamCreateWithFlags(&c->sf, hipStreamNonBlocking));
+    HCK(hipEventCreateWithFlags(&c->evfac, hipEventDisableTiming));
+  }
+  while ((int)c->evstrip.size() < ns + 1) {
+    hipEvent_t e;
+    HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->evstrip.push_back(e);
+  }
+  const bool fuse = !c->sparse && gram_fuse_ok(c->tall);
+  if (!fuse) gemv_t_local(c, v, vec_dev);
+  const double* A = dense_A(c);
+  if (fuse && c->vpieces > 1) HCK(hipMemsetAsync(c->vpart, 0, sizeof(double) * c->vpieces * ld, c->st));
+  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+  hipEvent_t e0;
+  tbegin(c, T_GRAM, &e0);
+  // the factor stream starts after everything already on st (weights, smoother, info reset)
+  HCK(hipEventRecord(c->evstrip[ns], c->st));
+  HCK(hipStreamWaitEvent(c->sf, c->evstrip[ns], 0));
+  for (int s2 = 0; s2 < ns; ++s2) {
+    const scs_ctx::GStrip& g = c->gstrip[s2];
+    HCK(gram_launch_sched(A, c->nstage, w, c->Npad, g.work, g.seglen, g.nsplit, g.comb, g.ncomb, c->gpart, c->G, ld,
+                          0, c->tall, c->st, fuse ? v : nullptr, c->vpart, ld));
+    HCK(hipEventRecord(c->evstrip[s2], c->st));
+  }
+  tend(c, T_GRAM, e0);
+  hipEvent_t es;
+  tbegin(c, T_SOLVE, &es);   // the solve's share of the step: what runs after the Gram
+  if (fuse) HCK(gram_vfinal_launch(c->vpart, c->vpieces, ld, m, vec_dev, c->st));
+  for (int s2 = 0; s2 < ns; ++s2) {
+    HCK(hipStreamWaitEvent(c->sf, c->evstrip[s2], 0));
+    const int64_t r0 = (int64_t)s2 * OB * 128, r1 = std::min<int64_t>((int64_t)(s2 + 1) * OB * 128, ld);
+    if (r0 < m) HCK(launch_diag_add(c->G + r0 * ld + r0, ld, std::min(r1, m) - r0, c->lam, c->Hr + r0, c->sf));
+    HCK(chol_diag_pad(c->G, ld, std::max(r0, m), r1, c->sf));
+    // strip rows [r0, r1), columns [r0, ld) -> Gc
+    HCK(chol_copy_rows(c->Gc, c->G, ld, r0, r1, r0, ld, c->sf));
+    HCK(chol_strip_update(c->G, ld, s2, &c->caux, c->sf));
+    HCK(chol_strip_factor(c->G, ld, s2, c->W, &c->caux, c->trilist, c->cinfo, c->sf));
+  }
+  (void)nb;
+  HCK(hipEventRecord(c->evfac, c->sf));
+  HCK(hipStreamWaitEvent(c->st, c->evfac, 0));
+  return es;
 }
 
 // fixed step-size rules shared by ProxNSCORE / ProxGGNSCORE
@@ -1384,6 +1536,14 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
     } else {
       forward(c, xh, c->x, EPI_GRAD | EPI_HESS, false);
       // local Aᵀg (not yet reduced; fused into the Gram pass); reduced together with the Gram
+      if (pipe_ok(c, c->gram_cache && gram_x_independent(c))) {
+        ensure_gram(c);
+        const hipEvent_t es = gram_factor_pipelined(c, c->hN, c->gN, c->gtmp);
+        HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
+        solve_factored(c, c->gq, es);
+        HCK(launch_neg(c->gq, m, c->d, c->st));
+        goto newton_tail;
+      }
       gram_and_reduce(c, c->hN, c->gN, c->gtmp);
     }
   } else if (cbggn) {
@@ -1393,6 +1553,14 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
     if (c->ggn == SCS_GGN_NONE) fail(c, SCS_ERR_ARG, "ProxGGNSCORE needs an out_fn / GGN loss kind");
     // J, residual, Q (prox-GGN-SCORE.jl:44-56) -> w = s²q, v = s·r
     forward(c, xh, c->x, EPI_GGN, false);
+    if (pipe_ok(c, c->gram_cache && gram_x_independent(c))) {
+      ensure_gram(c);
+      const hipEvent_t es = gram_factor_pipelined(c, c->wN, c->vN, c->gtmp);
+      HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
+      solve_factored(c, c->gq, es);
+      HCK(launch_neg(c->gq, m, c->d, c->st));
+      goto newton_tail;
+    }
     gram_and_reduce(c, c->wN, c->vN, c->gtmp);   // Gram + Jᵀr in one pass over A
   }
   // rhs = ∇f + λ gr (NSCORE) | Jᵀr + λ gr (GGN: Jt*[r;1], prox-GGN-SCORE.jl:121-130)
@@ -1401,6 +1569,7 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
   solve_system(c, c->gq);
   HCK(launch_neg(c->gq, m, c->d, c->st));  // d = -sol
   }
+newton_tail:
   bool ls = false;
   double step = step_size_newton(c, iter, &ls);
   if (ls) step = line_search(c, xh, c->x, c->d);
@@ -1555,6 +1724,12 @@ int scs_destroy(scs_ctx* c) {
   if (c->hring) (void)hipHostFree(c->hring);
   if (c->cbh) (void)hipHostFree(c->cbh);
   lu_aux_free(&c->lu);
+  if (c->sf) {
+    (void)hipStreamSynchronize(c->sf);
+    (void)hipStreamDestroy(c->sf);
+  }
+  for (hipEvent_t e : c->evstrip) (void)hipEventDestroy(e);
+  if (c->evfac) (void)hipEventDestroy(c->evfac);
   if (c->own_stream) (void)hipStreamDestroy(c->st);
   delete c;
   return SCS_OK;
@@ -1692,6 +1867,12 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->gcomb);
   dfree_t(c, c->gpart);
   dfree_t(c, c->vpart);
+  for (auto& g : c->gstrip) {
+    dfree_t(c, g.work);
+    dfree_t(c, g.comb);
+  }
+  c->gstrip.clear();
+  c->vpieces = 1;
   c->gseglen = c->gncomb = 0;
   c->gnsplit = 1;
   dfree_t(c, c->W);

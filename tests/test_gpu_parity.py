@@ -630,6 +630,40 @@ def test_cholesky_lookahead_bit_identical(m, monkeypatch):
     assert np.array_equal(bits(la.x), bits(ser.x))
 
 
+@pytest.mark.parametrize("method,m", [("nscore", 3072), ("ggn", 3200), ("nscore", 4000)])
+def test_pipelined_factor_matches_serial(method, m, monkeypatch):
+    """The factor hidden under the Gram (strip-by-strip Gram, left-looking factor on a second
+    stream, SCS_CHOL_PIPE=1, opt-in) against the classic one-launch Gram + right-looking factor
+    (the default): the same system and factor up to the summation order of the updates, so the
+    trajectories agree to rounding (and both to the oracle).  m = 3072 / 3200 / 4000: 3 / 4 / 4
+    outer strips, the last two partial."""
+    N = 5000
+    x0 = np.random.default_rng(41).standard_normal(m) * 0.3
+    if method == "ggn":
+        f, out, kind, M, OM = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N), 1, scsopt.ProxGGNSCORE, \
+            O.ProxGGNSCORE
+        of = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+    else:
+        f, out, kind, M, OM = losses.least_squares(1.0 / N), None, 3, scsopt.ProxNSCORE, O.ProxNSCORE
+        of = O.Loss("least_squares", 1.0 / N)
+    p = scsopt.Problem.synthetic(N, m, x0, f, 1e-3, kind=kind, seed=43, out_fn=out)
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    monkeypatch.setenv("SCS_CHOL_PIPE", "1")
+    a = scsopt.iterate(M(), p, "l1", hm, max_epoch=4, verbose=0)
+    monkeypatch.setenv("SCS_CHOL_PIPE", "0")
+    b = scsopt.iterate(M(), p, "l1", hm, max_epoch=4, verbose=0)
+    assert a.epochs == b.epochs
+    np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12)
+    np.testing.assert_allclose(a.x, b.x, rtol=1e-9, atol=1e-12)
+    A, y = p.get_data()
+    O.FAST_LINALG = True
+    try:
+        osol = O.iterate(OM(), O.Problem(A, y, x0, of, 1e-3), "l1", O.PHuberSmootherL1L2(1.0), max_epoch=4)
+    finally:
+        O.FAST_LINALG = False
+    np.testing.assert_allclose(a.obj, osol.obj, rtol=1e-8)
+
+
 @pytest.mark.parametrize("m", [2304])
 def test_cholesky_small_gram_bit_identical(m, monkeypatch):
     """The latency Gram kernel (gram_small_kernel: 128 x 16/32 strips, 8-stage register ring) that
