@@ -44,7 +44,7 @@ constexpr int SPB_ROWS = 1024;   // rows per workgroup
 // fp64 layout: segments are padded to multiples of 4 entries (index 0xFFFF -- never a local index, the
 // block is <= 16384 wide -- value 0; blk_pad / blk_scatter) and start 4-aligned, so a lane
 // takes 4 consecutive entries with one 8-B index load and one 16-B (fp32) or two 16-B (fp64)
-// value loads.  One wave works on RW rows at a time (of its 64 contiguous rows): all loads of a
+// value loads.  One wave works on RW = 2 rows at a time (of its 64 contiguous rows): all loads of a
 // round are issued before any use (clamped addresses, no branches), a segment of up to 256
 // entries -- C5: ~164 per (row, block) in both directions -- costs one round, and the RW rows'
 // lane partials are reduced together (multi_row_sum: log2(RW) exchange levels that halve the
@@ -89,6 +89,64 @@ __device__ __forceinline__ void load4(const float* p, double (&o)[4]) {
   o[3] = a[3];
 }
 
+// One round = RW rows of the wave's 64: their segment bases (readlane of the pointer pair),
+// lengths in 4-entry slots, and the loaded (index, value) quads of the current slot.
+template <typename VT, int RW>
+struct SpmvRound {
+  const uint16_t* li[RW];
+  const VT* va[RW];
+  int n4[RW];
+  int rem;   // longest segment of the round in slots (wave-uniform)
+  uint64_t id[RW];
+  double v[RW][4];
+};
+
+template <typename VT, int RW>
+__device__ __forceinline__ void round_setup(SpmvRound<VT, RW>& R, const uint16_t* lidx, const VT* val, int64_t mp0,
+                                            int64_t mp1, int k0) {
+  R.rem = 0;
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const int k = k0 + j;   // rows past the wave's count have mp0 = mp1 = 0 -> empty
+    const int64_t a0 = ((int64_t)__builtin_amdgcn_readlane((int)(mp0 >> 32), k) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)mp0, k);
+    const int64_t a1 = ((int64_t)__builtin_amdgcn_readlane((int)(mp1 >> 32), k) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)mp1, k);
+    R.n4[j] = (int)((a1 - a0) >> 2);
+    R.li[j] = lidx + a0;   // an empty segment reads its (valid, 4-aligned) start, masked
+    R.va[j] = val + a0;
+    R.rem = max(R.rem, R.n4[j]);
+  }
+}
+
+template <typename VT, int RW>
+__device__ __forceinline__ void round_load(SpmvRound<VT, RW>& R, int o) {
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {   // clamped, branch-free: every load of the round issues at once
+    const int q = max(min(o, R.n4[j] - 1), 0);
+    R.id[j] = *(const uint64_t*)(R.li[j] + 4 * q);
+    load4(R.va[j] + 4 * q, R.v[j]);
+  }
+}
+
+template <typename VT, int RW>
+__device__ __forceinline__ void round_fma(const SpmvRound<VT, RW>& R, int o, const double* xs, double (&acc)[RW]) {
+#pragma unroll
+  for (int j = 0; j < RW; ++j)
+    if (o < R.n4[j]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cidx = (int)((R.id[j] >> (16 * e)) & 0xFFFF);
+        if (cidx != 0xFFFF) acc[j] += R.v[j][e] * xs[cidx];
+      }
+    }
+}
+
+// The next round's loads are issued before this round's LDS gathers, FMAs and reduction
+// (software pipelined over two named round buffers -- a dynamically indexed pair would live in
+// scratch), so each wave keeps loads in flight while it computes; segments longer than 256 entries
+// take extra unpipelined passes.  C5 probe, same box: fp64 1.339 -> 1.309 ms (A x), 1.233 ->
+// 1.205 ms (Aᵀv) against the unpipelined 4-row rounds; RW = 4 pipelined spills at 128 VGPRs.
 template <typename VT, int RW>
 __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
                                                                const uint16_t* __restrict__ lidx,
@@ -128,48 +186,31 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
     const int64_t myr = rw0 + lane;
     const int64_t mp0 = (myr < r1) ? pb[myr] : 0, mp1 = (myr < r1) ? pb[myr + 1] : 0;
     const int nrw = (int)max((int64_t)0, min((int64_t)64, r1 - rw0));
-    for (int k0 = 0; k0 < nrw; k0 += RW) {
-      // per row: wave-uniform base pointers (SGPRs) + 32-bit lane offsets
-      const uint16_t* li[RW];
-      const VT* va[RW];
-      int n4[RW];
-      double acc[RW];
-      int rem = 0;   // longest segment of the group in 4-entry slots (wave-uniform)
-#pragma unroll
-      for (int j = 0; j < RW; ++j) {
-        const int k = k0 + j;   // rows past nrw have mp0 = mp1 = 0 -> empty
-        const int64_t a0 = ((int64_t)__builtin_amdgcn_readlane((int)(mp0 >> 32), k) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)mp0, k);
-        const int64_t a1 = ((int64_t)__builtin_amdgcn_readlane((int)(mp1 >> 32), k) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)mp1, k);
-        n4[j] = (int)((a1 - a0) >> 2);
-        li[j] = lidx + a0;   // an empty segment reads its (valid, 4-aligned) start, masked
-        va[j] = val + a0;
-        acc[j] = 0.0;
-        rem = max(rem, n4[j]);
+    if (nrw == 0) continue;
+    SpmvRound<VT, RW> R0, R1;
+    auto step = [&](SpmvRound<VT, RW>& A, SpmvRound<VT, RW>& B, int k0) {
+      if (k0 + RW < nrw) {   // uniform: the next round's loads go out first
+        round_setup(B, lidx, val, mp0, mp1, k0 + RW);
+        round_load(B, lane);
       }
-      for (int o = lane; o - lane < rem; o += 64) {
-        uint64_t id[RW];
-        double v[RW][4];
+      double acc[RW];
 #pragma unroll
-        for (int j = 0; j < RW; ++j) {
-          const int q = max(min(o, n4[j] - 1), 0);
-          id[j] = *(const uint64_t*)(li[j] + 4 * q);
-          load4(va[j] + 4 * q, v[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < RW; ++j)
-          if (o < n4[j]) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int cidx = (int)((id[j] >> (16 * e)) & 0xFFFF);
-              if (cidx != 0xFFFF) acc[j] += v[j][e] * xs[cidx];
-            }
-          }
+      for (int j = 0; j < RW; ++j) acc[j] = 0.0;
+      round_fma(A, lane, xs, acc);
+      for (int o = lane + 64; o - lane < A.rem; o += 64) {   // segments past 256 entries
+        round_load(A, o);
+        round_fma(A, o, xs, acc);
       }
       int row;
       const double sum = multi_row_sum<RW>(acc, lane, row);
       if ((lane & (64 / RW - 1)) == 0 && k0 + row < nrw) out[(int64_t)b * ldo + rw0 + k0 + row] = sum;
+    };
+    round_setup(R0, lidx, val, mp0, mp1, 0);
+    round_load(R0, lane);
+    for (int k0 = 0; k0 < nrw; k0 += 2 * RW) {
+      step(R0, R1, k0);
+      if (k0 + RW >= nrw) break;
+      step(R1, R0, k0 + RW);
     }
   }
 }
@@ -280,9 +321,8 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
                            hipStream_t st) {
   if (nrows <= 0) return hipSuccess;
   const int nblk = (int)ceil_div(ncols, (int64_t)1 << shift);
-  // fp64 (padded layout, 4-entry slots): 4 rows per round (8 spill at 128 VGPRs), 2 row chunks
-  // per workgroup; C5, one box (ms): RW 2 / 4 / 8 at 2 chunks 1.341 / 1.218 / 1.486, RW 4 at
-  // 1 / 4 chunks 1.223 / 1.220.  fp32 (unpadded, one entry per lane): U = 3 slots x 8 rows for
+  // fp64 (padded layout, 4-entry slots, pipelined rounds of 2 rows), 1 row chunk per workgroup
+  // (probe, same box: 1.309 / 1.314 / 1.315 ms at 1 / 2 / 4 chunks).  fp32 (unpadded, one entry per lane): U = 3 slots x 8 rows for
   // short segments (C5: ~164 per (row, block)), 8 x 2 for long ones, 4 chunks.
   // SCS_SPMV_CHUNKS overrides the chunks (A/B).
   static const int chunks_env = [] {
@@ -299,9 +339,9 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
       hipLaunchKernelGGL((spmv_blk1_kernel<float, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
                          (const float*)val, x, nrows, ncols, shift, out, ldo, chunks);
   } else {
-    const int chunks = chunks_env ? chunks_env : 2;
+    const int chunks = chunks_env ? chunks_env : 1;
     const dim3 grid((unsigned)ceil_div(ceil_div(nrows, SPB_ROWS), chunks), (unsigned)nblk);
-    hipLaunchKernelGGL((spmv_blk_kernel<double, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const double*)val,
+    hipLaunchKernelGGL((spmv_blk_kernel<double, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const double*)val,
                        x, nrows, ncols, shift, out, ldo, chunks);
   }
   return hipGetLastError();

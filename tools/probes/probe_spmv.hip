@@ -185,6 +185,120 @@ __global__ __launch_bounds__(1024) void spmv_b_kernel(const int64_t* __restrict_
   }
 }
 
+// C: B with the next round's loads issued before the current round's LDS gathers, FMAs and
+// reduction (software pipelining across rounds; each wave keeps its loads in flight while it
+// computes).  Segments longer than 256 entries take extra unpipelined passes.
+template <typename VT, int RW>
+struct Round {
+  const uint16_t* li[RW];
+  const VT* va[RW];
+  int n4[RW];
+  int rem;
+  uint64_t id[RW];
+  double v[RW][4];
+};
+
+template <typename VT, int RW>
+__device__ __forceinline__ void round_setup(Round<VT, RW>& R, const uint16_t* lidx, const VT* val, int64_t mp0,
+                                            int64_t mp1, int k0) {
+  R.rem = 0;
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const int k = k0 + j;
+    const int64_t a0 = ((int64_t)__builtin_amdgcn_readlane((int)(mp0 >> 32), k) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)mp0, k);
+    const int64_t a1 = ((int64_t)__builtin_amdgcn_readlane((int)(mp1 >> 32), k) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)mp1, k);
+    R.n4[j] = (int)((a1 - a0) >> 2);
+    R.li[j] = lidx + a0;
+    R.va[j] = val + a0;
+    R.rem = max(R.rem, R.n4[j]);
+  }
+}
+
+template <typename VT, int RW>
+__device__ __forceinline__ void round_load(Round<VT, RW>& R, int o) {
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const int q = max(min(o, R.n4[j] - 1), 0);
+    R.id[j] = *(const uint64_t*)(R.li[j] + 4 * q);
+    load4(R.va[j] + 4 * q, R.v[j]);
+  }
+}
+
+template <typename VT, int RW>
+__device__ __forceinline__ void round_fma(const Round<VT, RW>& R, int o, const double* xs, double (&acc)[RW]) {
+#pragma unroll
+  for (int j = 0; j < RW; ++j)
+    if (o < R.n4[j]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = (int)((R.id[j] >> (16 * e)) & 0xFFFF);
+        if (c != 0xFFFF) acc[j] += R.v[j][e] * xs[c];
+      }
+    }
+}
+
+template <typename VT, int RW>
+__global__ __launch_bounds__(1024) void spmv_c_kernel(const int64_t* __restrict__ ptr, const uint16_t* __restrict__ lidx,
+                                                      const VT* __restrict__ val, const double* __restrict__ x,
+                                                      int64_t nrows, int64_t ncols, int shift, double* __restrict__ out,
+                                                      int64_t ldo, int chunks) {
+  __shared__ double xs[1 << 14];
+  const int b = blockIdx.y;
+  const int64_t c0 = (int64_t)b << shift;
+  const int nb = (int)min((int64_t)1 << shift, ncols - c0);
+  {
+    constexpr int PER = (1 << 14) / 1024;
+    double t[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * 1024;
+      t[k] = (i < nb) ? x[c0 + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) xs[threadIdx.x + k * 1024] = t[k];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t* pb = ptr + (int64_t)b * nrows;
+  for (int ch = 0; ch < chunks; ++ch) {
+    const int64_t cb = (int64_t)blockIdx.x * chunks + ch;
+    if (cb * 1024 >= nrows) break;
+    const int64_t r1 = min(nrows, (cb + 1) * 1024);
+    const int64_t rw0 = cb * 1024 + (int64_t)wv * 64;
+    const int64_t myr = rw0 + lane;
+    const int64_t mp0 = (myr < r1) ? pb[myr] : 0, mp1 = (myr < r1) ? pb[myr + 1] : 0;
+    const int nrw = (int)max((int64_t)0, min((int64_t)64, r1 - rw0));
+    if (nrw == 0) continue;
+    Round<VT, RW> R0, R1;   // named (a dynamically indexed pair would live in scratch)
+    auto step = [&](Round<VT, RW>& A, Round<VT, RW>& B, int k0) {
+      if (k0 + RW < nrw) {   // uniform: the next round's loads go out before this round's work
+        round_setup(B, lidx, val, mp0, mp1, k0 + RW);
+        round_load(B, lane);
+      }
+      double acc[RW];
+#pragma unroll
+      for (int j = 0; j < RW; ++j) acc[j] = 0.0;
+      round_fma(A, lane, xs, acc);
+      for (int o = lane + 64; o - lane < A.rem; o += 64) {   // segments past 256 entries
+        round_load(A, o);
+        round_fma(A, o, xs, acc);
+      }
+      int row;
+      const double sm = multi_row_sum<RW>(acc, lane, row);
+      if ((lane & (64 / RW - 1)) == 0 && k0 + row < nrw) out[(int64_t)b * ldo + rw0 + k0 + row] = sm;
+    };
+    round_setup(R0, lidx, val, mp0, mp1, 0);
+    round_load(R0, lane);
+    for (int k0 = 0; k0 < nrw; k0 += 2 * RW) {
+      step(R0, R1, k0);
+      if (k0 + RW >= nrw) break;
+      step(R1, R0, k0 + RW);
+    }
+  }
+}
+
 template <typename VT>
 static void run(int dir) {
   const int64_t nrows = dir == 0 ? (1 << 20) : (1 << 16);
@@ -252,6 +366,16 @@ static void run(int dir) {
     snprintf(nm, sizeof nm, "B RW=4 chunks=%d", chunks);
     timeit(nm, [&] {
       hipLaunchKernelGGL((spmv_b_kernel<VT, 4>), grid, dim3(1024), 0, 0, dpb, ib, vb, x, nrows, ncols, shift, ob, nrows,
+                         chunks);
+    });
+    snprintf(nm, sizeof nm, "C RW=4 chunks=%d", chunks);
+    timeit(nm, [&] {
+      hipLaunchKernelGGL((spmv_c_kernel<VT, 4>), grid, dim3(1024), 0, 0, dpb, ib, vb, x, nrows, ncols, shift, ob, nrows,
+                         chunks);
+    });
+    snprintf(nm, sizeof nm, "C RW=2 chunks=%d", chunks);
+    timeit(nm, [&] {
+      hipLaunchKernelGGL((spmv_c_kernel<VT, 2>), grid, dim3(1024), 0, 0, dpb, ib, vb, x, nrows, ncols, shift, ob, nrows,
                          chunks);
     });
     snprintf(nm, sizeof nm, "B RW=8 chunks=%d", chunks);
