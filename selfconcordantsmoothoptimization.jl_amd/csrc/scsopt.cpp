@@ -2598,7 +2598,10 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     // end of each epoch -- the GPU only idles for that hand-off.  Same kernels, same order as the
     // per-call path, so the histories equal the host loop's (the norms differ in summation order
     // only; test_device_loop_matches_host_loop).
-    const bool dev_ok = nb == 0 && !c->generic && c->loss != SCS_LOSS_QUADRATIC && c->loss != SCS_LOSS_ROSENBROCK;
+    // (a Rosenbrock ProblemGeneric runs here too: its f / ∇f / ∇²f are device kernels; the
+    // quadratic loss and the host callbacks keep the per-call path)
+    const bool dev_ok = nb == 0 && c->loss != SCS_LOSS_QUADRATIC && c->loss != SCS_LOSS_CALLBACK &&
+                        (!c->generic || c->loss == SCS_LOSS_ROSENBROCK);
     if (dev_ok) {
       struct DevLoop {
         scs_ctx* c;
@@ -2707,8 +2710,12 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         // f(x): the z of x is cached (the previous step's ∇q(x_new) / the Newton step's forward)
         // except at epoch 1; its value is copied out of the deferred slot before the step's
         // forward at x_new reuses it
-        forward(c, x, c->x, 0, false);
-        HCK(hipMemcpyAsync(c->scal + FX_SLOT, c->scal + ZF_SLOT, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+        if (c->loss == SCS_LOSS_ROSENBROCK) {
+          HCK(launch_rosen(c->x, m, 0, c->scal + FX_SLOT, nullptr, 0, c->st));
+        } else {
+          forward(c, x, c->x, 0, false);
+          HCK(hipMemcpyAsync(c->scal + FX_SLOT, c->scal + ZF_SLOT, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+        }
         HCK(launch_reg_value(prox_args(c), c->x, m, c->scal + RX_SLOT, c->scal + 64 + 2 * 256, c->st));
         hipEvent_t e0;
         tbegin(c, T_STEP, &e0);
