@@ -236,6 +236,7 @@ hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t
 
 // ---- sparse.hip (LDS-blocked gathers; out[b*ldo + r] = Σ_{p in row r, block b} val[p] x[(b<<shift) + lidx[p]])
 int spmv_blk_shift(int64_t ncols);
+int spmv_pad_index();   // padding index of the fp64 blocked layout (the SpMV's zero slot)
 // f32: unpadded layout (one entry per lane); fp64: segments padded to whole 4-entry slots (blk_pad)
 hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
                            int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,

@@ -2013,7 +2013,8 @@ static void build_blocked(scs_ctx* c, int64_t nrows, int64_t ncols, int64_t* ptr
   B.ptr = dalloc<int64_t>(c, nk + 1);
   if (nrows > 0) {
     HCK(blk_count(ptr, idx, nrows, B.shift, cnt, first, c->st));
-    // fp64: segments in whole 4-entry slots (padding: index 0xFFFF, value 0; launch_spmv_blk)
+    // fp64: segments in whole 4-entry slots (padding: index 16384 = the SpMV's zero slot, value 0;
+    // launch_spmv_blk)
     if (!c->sp_f32) HCK(blk_pad(cnt, nk, c->st));
     tb = 0;
     HCK(blk_scan(nullptr, &tb, cnt, B.ptr, nk + 1, c->st));
@@ -2024,7 +2025,7 @@ static void build_blocked(scs_ctx* c, int64_t nrows, int64_t ncols, int64_t* ptr
     sync(c);
     dfree(c, tmp);
     B.lidx = dalloc<uint16_t>(c, nnzp + 4);
-    HCK(hipMemsetAsync(B.lidx, 0xFF, sizeof(uint16_t) * (nnzp + 4), c->st));
+    HCK(hipMemsetD16Async((hipDeviceptr_t)B.lidx, (unsigned short)spmv_pad_index(), (size_t)(nnzp + 4), c->st));
     B.val = dalloc_vals(c, nnzp + 4, c->sp_f32);
     HCK(blk_scatter(ptr, idx, val, c->sp_f32, nrows, B.shift, B.ptr, first, B.lidx, B.val, c->st));
     sync(c);

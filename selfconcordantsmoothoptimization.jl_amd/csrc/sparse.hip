@@ -41,17 +41,138 @@ constexpr int SPB_MAXSHIFT = 14;
 constexpr int SPB_THREADS = 1024;
 constexpr int SPB_ROWS = 1024;   // rows per workgroup
 
-// fp64 layout: segments are padded to multiples of 4 entries (index 0xFFFF -- never a local index, the
-// block is <= 16384 wide -- value 0; blk_pad / blk_scatter) and start 4-aligned, so a lane
-// takes 4 consecutive entries with one 8-B index load and one 16-B (fp32) or two 16-B (fp64)
-// value loads.  One wave works on RW = 2 rows at a time (of its 64 contiguous rows): all loads of a
-// round are issued before any use (clamped addresses, no branches), a segment of up to 256
-// entries -- C5: ~164 per (row, block) in both directions -- costs one round, and the RW rows'
-// lane partials are reduced together (multi_row_sum: log2(RW) exchange levels that halve the
-// live rows, then the plain butterfly; 10 shuffles for 8 rows instead of 48).  C5 shape, one
-// box, against the previous one-entry-per-lane form: fp64 1.380 -> 1.223 ms, fp32 0.943 ->
-// 0.869 ms per pass (tools/probes/probe_spmv.hip).  Per row the summation order is fixed
-// (entries ascending within a lane, lanes by the fixed exchange tree).
+// fp64 layout: segments are padded to multiples of 4 entries (index SPB_PADIDX = 16384 -- the
+// zero slot past the staged x slice, so padding needs no compare -- value 0; blk_pad /
+// hipMemsetD16) and start 4-aligned, so a lane takes one 4-entry slot with one 8-B index load and
+// two 16-B value loads.
+constexpr int SPB_PADIDX = 1 << SPB_MAXSHIFT;
+
+// 64-bit DPP move (two 32-bit halves); lanes the pattern does not reach read 0 (bound_ctrl)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROWMASK, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROWMASK, 0xF, true);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Segmented inclusive prefix sum over lanes [max(rs, 0), lane] of a wave whose lanes' rows are
+// nondecreasing (rs = first lane of my row, < 0 if the row began before lane 0): row_shr 1/2/4/8
+// inside each 16-lane row, then row_bcast:15 and row_bcast:31 -- the wave prefix-scan pattern
+// with each step's add kept only when its source lane lies in my row.  Fixed order.
+__device__ __forceinline__ double seg_scan64(double p, int lane, int rs) {
+  const int l16 = lane & 15;
+  double u;
+  u = dpp_f64<0x111, 0xF>(p);
+  if (l16 >= 1 && lane - 1 >= rs) p += u;
+  u = dpp_f64<0x112, 0xF>(p);
+  if (l16 >= 2 && lane - 2 >= rs) p += u;
+  u = dpp_f64<0x114, 0xF>(p);
+  if (l16 >= 4 && lane - 4 >= rs) p += u;
+  u = dpp_f64<0x118, 0xF>(p);
+  if (l16 >= 8 && lane - 8 >= rs) p += u;
+  u = dpp_f64<0x142, 0xA>(p);   // row_bcast:15 -> rows 1, 3
+  if ((lane & 16) && (lane & ~15) - 1 >= rs) p += u;
+  u = dpp_f64<0x143, 0xC>(p);   // row_bcast:31 -> rows 2, 3
+  if ((lane & 32) && 31 >= rs) p += u;
+  return p;
+}
+
+// fp64 product ("flat" form, r02).  Each wave owns 64 contiguous rows of block b, whose padded
+// segments are one contiguous range of 4-entry slots; it streams that range in windows of 64
+// slots -- every lane busy, one window's loads in flight ahead of the compute -- instead of
+// per-row rounds (which left ~36 % of the lanes idle on C5's ~41-slot segments and re-read
+// clamped slots).  Per window: lane partial over its slot (LDS gathers of the staged x slice),
+// the lane's row from the wave's row starts (a wave-uniform walk over the few rows that begin in
+// the window), the DPP segmented scan, and each row's register accumulator (lane k = row k)
+// pulls its window sum from the row's last lane in the window.  Per row the order is fixed
+// (slot partials left to right within a lane's 4 entries, the scan tree, windows in order).
+// C5 probe, same box (tools/probes/probe_spmv_flat.hip): 1.318 -> 1.182 ms (A x), 1.326 ->
+// 1.185 ms (Aᵀ v) against the per-row pipelined kernel; a plain read of the same bytes takes
+// 1.13 ms; the C5 bench 369 -> 397 it/s.  fp32 values on the padded layout through the same
+// kernel measured slower than the unpadded one-entry-per-lane kernel below (0.907 vs 0.824 ms).
+struct SpmvWin {
+  uint64_t id;
+  double v[4];
+};
+
+__device__ __forceinline__ void win_load(SpmvWin& w, const uint16_t* __restrict__ lidx,
+                                         const double* __restrict__ val, int64_t slot) {
+  w.id = *(const uint64_t*)(lidx + 4 * slot);
+  const v2d a = *(const v2d*)(val + 4 * slot), b = *(const v2d*)(val + 4 * slot + 2);
+  w.v[0] = a[0];
+  w.v[1] = a[1];
+  w.v[2] = b[0];
+  w.v[3] = b[1];
+}
+__global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
+                                                               const uint16_t* __restrict__ lidx,
+                                                               const double* __restrict__ val,
+                                                               const double* __restrict__ x, int64_t nrows,
+                                                               int64_t ncols, int shift, double* __restrict__ out,
+                                                               int64_t ldo) {
+  __shared__ double xs[SPB_PADIDX + 1];
+  const int b = blockIdx.y;
+  const int64_t c0 = (int64_t)b << shift;
+  const int nb = (int)min((int64_t)1 << shift, ncols - c0);
+  // stage the slice: all loads of a thread in flight before the LDS stores
+  {
+    constexpr int PER = (1 << SPB_MAXSHIFT) / SPB_THREADS;
+    double t[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * SPB_THREADS;
+      t[k] = (i < nb) ? x[c0 + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) xs[threadIdx.x + k * SPB_THREADS] = t[k];
+    if (threadIdx.x == 0) xs[SPB_PADIDX] = 0.0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t* pb = ptr + (int64_t)b * nrows;
+  const int64_t rw0 = (int64_t)blockIdx.x * SPB_ROWS + (int64_t)wv * 64;
+  const int nrw = (int)max((int64_t)0, min((int64_t)64, nrows - rw0));
+  if (nrw == 0) return;
+  const int64_t sb = pb[rw0] >> 2;                     // the wave's first slot
+  const int total = (int)((pb[rw0 + nrw] >> 2) - sb);  // its slot count
+  // st: slot start of row `lane` relative to sb (lanes past nrw: total); en: its end
+  const int st = lane < nrw ? (int)((pb[rw0 + lane] >> 2) - sb) : total;
+  const int stn = __shfl(st, min(lane + 1, 63), 64);   // every lane takes part in a shuffle
+  const int en = lane + 1 < nrw ? stn : total;
+  const int nwin = (total + 63) >> 6;
+  SpmvWin nxt;
+  win_load(nxt, lidx, val, sb + max(min(lane, total - 1), 0));
+  double acc = 0.0;
+  int cur = 0;   // row of the window's first slot (wave-uniform)
+  for (int t = 0; t < nwin; ++t) {
+    const SpmvWin w = nxt;
+    if (t + 1 < nwin) win_load(nxt, lidx, val, sb + min(64 * (t + 1) + lane, total - 1));
+    const int base = 64 * t, slot = base + lane;
+    double p = 0.0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p += w.v[e] * xs[(int)((w.id >> (16 * e)) & 0xFFFF)];
+    if (slot >= total) p = 0.0;
+    // my row = cur + #{k > cur : st_k <= slot}; the walk stops at the first row starting past
+    // the window, and the last row starting at or before base + 64 is the next window's cur
+    int r = cur, k = cur + 1;
+    while (k < nrw) {
+      const int sk = __builtin_amdgcn_readlane(st, k);
+      if (sk > base + 64) break;
+      r += (slot >= sk) ? 1 : 0;
+      ++k;
+    }
+    cur = k - 1;
+    const int rs = __shfl(st, r, 64) - base;
+    p = seg_scan64(p, lane, rs);
+    const double pt = __shfl(p, max(min(en - base - 1, 63), 0), 64);
+    if (st < base + 64 && en > base && st < en) acc += pt;
+  }
+  if (lane < nrw) out[(int64_t)b * ldo + rw0 + lane] = acc;
+}
+
+// RW rows' lane partials -> the lane group of each row holds its sum (fp32 arm below):
+// log2(RW) exchange levels that halve the live rows, then the plain butterfly
 template <int RW>
 __device__ __forceinline__ double multi_row_sum(double (&acc)[RW], int lane, int& row) {
   row = 0;
@@ -71,148 +192,6 @@ __device__ __forceinline__ double multi_row_sum(double (&acc)[RW], int lane, int
   double v = acc[0];
   for (int o = off; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
-}
-
-__device__ __forceinline__ void load4(const double* p, double (&o)[4]) {
-  const v2d a = *(const v2d*)p, b = *(const v2d*)(p + 2);
-  o[0] = a[0];
-  o[1] = a[1];
-  o[2] = b[0];
-  o[3] = b[1];
-}
-typedef float v4f __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void load4(const float* p, double (&o)[4]) {
-  const v4f a = *(const v4f*)p;
-  o[0] = a[0];
-  o[1] = a[1];
-  o[2] = a[2];
-  o[3] = a[3];
-}
-
-// One round = RW rows of the wave's 64: their segment bases (readlane of the pointer pair),
-// lengths in 4-entry slots, and the loaded (index, value) quads of the current slot.
-template <typename VT, int RW>
-struct SpmvRound {
-  const uint16_t* li[RW];
-  const VT* va[RW];
-  int n4[RW];
-  int rem;   // longest segment of the round in slots (wave-uniform)
-  uint64_t id[RW];
-  double v[RW][4];
-};
-
-template <typename VT, int RW>
-__device__ __forceinline__ void round_setup(SpmvRound<VT, RW>& R, const uint16_t* lidx, const VT* val, int64_t mp0,
-                                            int64_t mp1, int k0) {
-  R.rem = 0;
-#pragma unroll
-  for (int j = 0; j < RW; ++j) {
-    const int k = k0 + j;   // rows past the wave's count have mp0 = mp1 = 0 -> empty
-    const int64_t a0 = ((int64_t)__builtin_amdgcn_readlane((int)(mp0 >> 32), k) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)mp0, k);
-    const int64_t a1 = ((int64_t)__builtin_amdgcn_readlane((int)(mp1 >> 32), k) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)mp1, k);
-    R.n4[j] = (int)((a1 - a0) >> 2);
-    R.li[j] = lidx + a0;   // an empty segment reads its (valid, 4-aligned) start, masked
-    R.va[j] = val + a0;
-    R.rem = max(R.rem, R.n4[j]);
-  }
-}
-
-template <typename VT, int RW>
-__device__ __forceinline__ void round_load(SpmvRound<VT, RW>& R, int o) {
-#pragma unroll
-  for (int j = 0; j < RW; ++j) {   // clamped, branch-free: every load of the round issues at once
-    const int q = max(min(o, R.n4[j] - 1), 0);
-    R.id[j] = *(const uint64_t*)(R.li[j] + 4 * q);
-    load4(R.va[j] + 4 * q, R.v[j]);
-  }
-}
-
-template <typename VT, int RW>
-__device__ __forceinline__ void round_fma(const SpmvRound<VT, RW>& R, int o, const double* xs, double (&acc)[RW]) {
-#pragma unroll
-  for (int j = 0; j < RW; ++j)
-    if (o < R.n4[j]) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int cidx = (int)((R.id[j] >> (16 * e)) & 0xFFFF);
-        if (cidx != 0xFFFF) acc[j] += R.v[j][e] * xs[cidx];
-      }
-    }
-}
-
-// The next round's loads are issued before this round's LDS gathers, FMAs and reduction
-// (software pipelined over two named round buffers -- a dynamically indexed pair would live in
-// scratch), so each wave keeps loads in flight while it computes; segments longer than 256 entries
-// take extra unpipelined passes.  C5 probe, same box: fp64 1.339 -> 1.309 ms (A x), 1.233 ->
-// 1.205 ms (Aᵀv) against the unpipelined 4-row rounds; RW = 4 pipelined spills at 128 VGPRs.
-template <typename VT, int RW>
-__global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
-                                                               const uint16_t* __restrict__ lidx,
-                                                               const VT* __restrict__ val,
-                                                               const double* __restrict__ x, int64_t nrows,
-                                                               int64_t ncols, int shift, double* __restrict__ out,
-                                                               int64_t ldo, int chunks) {
-  __shared__ double xs[1 << SPB_MAXSHIFT];
-  const int b = blockIdx.y;
-  const int64_t c0 = (int64_t)b << shift;
-  const int nb = (int)min((int64_t)1 << shift, ncols - c0);
-  // stage the slice: all loads of a thread in flight before the LDS stores (a plain
-  // load->store loop serializes 16 L2 round trips while every wave waits at the barrier)
-  {
-    constexpr int PER = (1 << SPB_MAXSHIFT) / SPB_THREADS;
-    double t[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = threadIdx.x + k * SPB_THREADS;
-      t[k] = (i < nb) ? x[c0 + i] : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) xs[threadIdx.x + k * SPB_THREADS] = t[k];
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t* pb = ptr + (int64_t)b * nrows;
-  // the workgroup walks `chunks` consecutive 1024-row chunks of block b with the slice staged
-  // once; its waves run through the chunks without a barrier (no per-chunk drain)
-  for (int ch = 0; ch < chunks; ++ch) {
-    const int64_t cb = (int64_t)blockIdx.x * chunks + ch;
-    if (cb * SPB_ROWS >= nrows) break;
-    const int64_t r1 = min(nrows, (cb + 1) * SPB_ROWS);
-    // each wave owns 64 contiguous rows: their pointer pairs are loaded once (lane k: row
-    // rw0 + k, coalesced) and broadcast per round with readlane
-    const int64_t rw0 = cb * SPB_ROWS + (int64_t)wv * 64;
-    const int64_t myr = rw0 + lane;
-    const int64_t mp0 = (myr < r1) ? pb[myr] : 0, mp1 = (myr < r1) ? pb[myr + 1] : 0;
-    const int nrw = (int)max((int64_t)0, min((int64_t)64, r1 - rw0));
-    if (nrw == 0) continue;
-    SpmvRound<VT, RW> R0, R1;
-    auto step = [&](SpmvRound<VT, RW>& A, SpmvRound<VT, RW>& B, int k0) {
-      if (k0 + RW < nrw) {   // uniform: the next round's loads go out first
-        round_setup(B, lidx, val, mp0, mp1, k0 + RW);
-        round_load(B, lane);
-      }
-      double acc[RW];
-#pragma unroll
-      for (int j = 0; j < RW; ++j) acc[j] = 0.0;
-      round_fma(A, lane, xs, acc);
-      for (int o = lane + 64; o - lane < A.rem; o += 64) {   // segments past 256 entries
-        round_load(A, o);
-        round_fma(A, o, xs, acc);
-      }
-      int row;
-      const double sum = multi_row_sum<RW>(acc, lane, row);
-      if ((lane & (64 / RW - 1)) == 0 && k0 + row < nrw) out[(int64_t)b * ldo + rw0 + k0 + row] = sum;
-    };
-    round_setup(R0, lidx, val, mp0, mp1, 0);
-    round_load(R0, lane);
-    for (int k0 = 0; k0 < nrw; k0 += 2 * RW) {
-      step(R0, R1, k0);
-      if (k0 + RW >= nrw) break;
-      step(R1, R0, k0 + RW);
-    }
-  }
 }
 
 // Unpadded layout, one entry per lane (the fp32 arm: measured faster there than 4-entry slots,
@@ -310,6 +289,8 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk1_kernel(const int64_t* _
   }
 }
 
+int spmv_pad_index() { return SPB_PADIDX; }
+
 int spmv_blk_shift(int64_t ncols) {
   int s = 0;
   while (s < SPB_MAXSHIFT && ((int64_t)1 << s) < ncols) ++s;
@@ -321,10 +302,9 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
                            hipStream_t st) {
   if (nrows <= 0) return hipSuccess;
   const int nblk = (int)ceil_div(ncols, (int64_t)1 << shift);
-  // fp64 (padded layout, 4-entry slots, pipelined rounds of 2 rows), 1 row chunk per workgroup
-  // (probe, same box: 1.309 / 1.314 / 1.315 ms at 1 / 2 / 4 chunks).  fp32 (unpadded, one entry per lane): U = 3 slots x 8 rows for
-  // short segments (C5: ~164 per (row, block)), 8 x 2 for long ones, 4 chunks.
-  // SCS_SPMV_CHUNKS overrides the chunks (A/B).
+  // fp64: the flat kernel, one 1024-row chunk per workgroup.  fp32 (unpadded, one entry per
+  // lane): U = 3 slots x 8 rows for short segments (C5: ~164 per (row, block)), 8 x 2 for long
+  // ones, 4 chunks; SCS_SPMV_CHUNKS overrides its chunks (A/B).
   static const int chunks_env = [] {
     const char* e = getenv("SCS_SPMV_CHUNKS");
     return e ? std::max(1, atoi(e)) : 0;
@@ -339,10 +319,9 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
       hipLaunchKernelGGL((spmv_blk1_kernel<float, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
                          (const float*)val, x, nrows, ncols, shift, out, ldo, chunks);
   } else {
-    const int chunks = chunks_env ? chunks_env : 1;
-    const dim3 grid((unsigned)ceil_div(ceil_div(nrows, SPB_ROWS), chunks), (unsigned)nblk);
-    hipLaunchKernelGGL((spmv_blk_kernel<double, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const double*)val,
-                       x, nrows, ncols, shift, out, ldo, chunks);
+    const dim3 grid((unsigned)ceil_div(nrows, SPB_ROWS), (unsigned)nblk);
+    hipLaunchKernelGGL(spmv_blk_kernel, grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const double*)val, x, nrows,
+                       ncols, shift, out, ldo);
   }
   return hipGetLastError();
 }

@@ -81,6 +81,32 @@ def test_user_csr_input_and_edges():
     assert pz.fx(x0) == pytest.approx(0.5 * np.dot(y, y) / N, rel=1e-13)
 
 
+def test_ragged_segments():
+    """Segment shapes the flat fp64 product walks specially: a row far longer than one 64-slot
+    window (dense row), runs of one-entry rows (many rows starting in one window), long runs of
+    empty rows, a dense column (a long CSC segment), and a row whose end meets a window boundary."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(41)
+    N, m = 5000, 20000
+    rows, cols = [], []
+    rows += [5] * m; cols += list(range(m))                                   # dense row: 5000 slots
+    rows += list(range(100, 1300)); cols += list(rng.integers(0, m, 1200))     # one entry per row
+    rows += list(range(N)); cols += [17000] * N                                # dense column
+    for r in range(2000, 3000, 3):                                            # 256 entries = 64 slots
+        rows += [r] * 256; cols += list(rng.choice(m, 256, replace=False))
+    # rows 3000..4000 stay empty but for the dense column; the rest random
+    C = sp.random(N, m, density=2e-3, random_state=42, format="coo")
+    keep = (C.row < 3000) | (C.row >= 4000)
+    rows += list(C.row[keep]); cols += list(C.col[keep])
+    A = sp.coo_matrix((rng.standard_normal(len(rows)), (rows, cols)), shape=(N, m)).tocsr()
+    A.sum_duplicates()
+    p = scsopt.Problem(A, rng.standard_normal(N), np.zeros(m), losses.least_squares(1.0 / N), 0.1)
+    _check_products(p, A)
+    # deterministic: the same product twice is bit-identical
+    x = rng.standard_normal(m)
+    np.testing.assert_array_equal(p.gemv_n(x), p.gemv_n(x))
+
+
 @pytest.mark.parametrize("N,m,rho", [(40000, 20000, 2e-4), (65536, 256, 0.05)])
 def test_multiblock_products(N, m, rho):
     """Index ranges above one 16384-wide LDS block in either direction (several blocked partials,
