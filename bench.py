@@ -299,12 +299,17 @@ def main():
             avg_ms = tm["gemv_ms"] / tm["gemv_calls"]
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             traffic = None
-            pmc = os.path.join(ROOT, "profiles", "r01_c5_spmv_pmc.json")   # tools/pmc_summary_spmv.py
-            if os.path.exists(pmc) and world == 1 and not args.f32 and N == 1 << 20 and m == 1 << 16:
+            kname = "spmv_blk_kernel<float, 8>" if args.f32 else "spmv_blk_kernel<double, 4>"
+            # PMC bytes (tools/pmc_summary_spmv.py) only when the file names the kernel launched here
+            pmc = os.path.join(ROOT, "profiles", "r02_c5_spmv_pmc_%s.json" % ("f32" if args.f32 else "f64"))
+            if os.path.exists(pmc) and world == 1 and N == 1 << 20 and m == 1 << 16:
                 with open(pmc) as f:
-                    traffic = json.load(f).get("hbm_bytes_per_launch")
+                    pm = json.load(f)
+                if pm.get("kernel") == kname:
+                    traffic = pm.get("hbm_bytes_per_launch")
+                    line["roofline_traffic_source"] = os.path.relpath(pmc, ROOT)
             line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "spmv_blk_kernel",
+                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                                 "avg_ms": avg_ms, "launches_per_step": tm["gemv_calls"] / steps,
                                 "bytes_per_launch": per_launch}
             line["config"]["nnz"] = nnz

@@ -236,14 +236,15 @@ hipError_t launch_gen_y(int kind, const double* z, double* y, int64_t N, int64_t
 
 // ---- sparse.hip (LDS-blocked gathers; out[b*ldo + r] = Σ_{p in row r, block b} val[p] x[(b<<shift) + lidx[p]])
 int spmv_blk_shift(int64_t ncols);
-int spmv_pad_index();   // padding index of the fp64 blocked layout (the SpMV's zero slot)
-// f32: unpadded layout (one entry per lane); fp64: segments padded to whole 4-entry slots (blk_pad)
+int spmv_pad_index();   // padding index of the blocked layouts (the SpMV's zero slot)
+int spmv_slot_width(int f32);   // segments padded to whole slots of 4 (fp64) / 8 (fp32) entries
+// segments padded to whole slots (blk_pad), padding index spmv_pad_index(), value 0
 hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
                            int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,
                            hipStream_t st);
 hipError_t blk_count(const int64_t* ptr, const int* idx, int64_t nrows, int shift, int64_t* cnt, int64_t* first,
                      hipStream_t st);
-hipError_t blk_pad(int64_t* cnt, int64_t n, hipStream_t st);
+hipError_t blk_pad(int64_t* cnt, int64_t n, int f32, hipStream_t st);
 hipError_t blk_scan(void* temp, size_t* temp_bytes, const int64_t* cnt, int64_t* bptr, int64_t n, hipStream_t st);
 hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int f32, int64_t nrows, int shift,
                        const int64_t* bptr, const int64_t* first, uint16_t* lidx, void* bval, hipStream_t st);

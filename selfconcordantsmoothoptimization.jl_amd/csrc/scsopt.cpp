@@ -2013,9 +2013,9 @@ static void build_blocked(scs_ctx* c, int64_t nrows, int64_t ncols, int64_t* ptr
   B.ptr = dalloc<int64_t>(c, nk + 1);
   if (nrows > 0) {
     HCK(blk_count(ptr, idx, nrows, B.shift, cnt, first, c->st));
-    // fp64: segments in whole 4-entry slots (padding: index 16384 = the SpMV's zero slot, value 0;
-    // launch_spmv_blk)
-    if (!c->sp_f32) HCK(blk_pad(cnt, nk, c->st));
+    // segments in whole slots of 4 (fp64) / 8 (fp32) entries (padding: index 16384 = the SpMV's
+    // zero slot, value 0; launch_spmv_blk)
+    HCK(blk_pad(cnt, nk, c->sp_f32, c->st));
     tb = 0;
     HCK(blk_scan(nullptr, &tb, cnt, B.ptr, nk + 1, c->st));
     void* tmp = dalloc<char>(c, tb);
@@ -2024,9 +2024,9 @@ static void build_blocked(scs_ctx* c, int64_t nrows, int64_t ncols, int64_t* ptr
     HCK(hipMemcpyAsync(&nnzp, B.ptr + nk, sizeof(int64_t), hipMemcpyDeviceToHost, c->st));
     sync(c);
     dfree(c, tmp);
-    B.lidx = dalloc<uint16_t>(c, nnzp + 4);
-    HCK(hipMemsetD16Async((hipDeviceptr_t)B.lidx, (unsigned short)spmv_pad_index(), (size_t)(nnzp + 4), c->st));
-    B.val = dalloc_vals(c, nnzp + 4, c->sp_f32);
+    B.lidx = dalloc<uint16_t>(c, nnzp + 8);
+    HCK(hipMemsetD16Async((hipDeviceptr_t)B.lidx, (unsigned short)spmv_pad_index(), (size_t)(nnzp + 8), c->st));
+    B.val = dalloc_vals(c, nnzp + 8, c->sp_f32);
     HCK(blk_scatter(ptr, idx, val, c->sp_f32, nrows, B.shift, B.ptr, first, B.lidx, B.val, c->st));
     sync(c);
   } else {

@@ -41,10 +41,10 @@ constexpr int SPB_MAXSHIFT = 14;
 constexpr int SPB_THREADS = 1024;
 constexpr int SPB_ROWS = 1024;   // rows per workgroup
 
-// fp64 layout: segments are padded to multiples of 4 entries (index SPB_PADIDX = 16384 -- the
-// zero slot past the staged x slice, so padding needs no compare -- value 0; blk_pad /
-// hipMemsetD16) and start 4-aligned, so a lane takes one 4-entry slot with one 8-B index load and
-// two 16-B value loads.
+// Layout: segments are padded to whole slots -- 4 entries (fp64: one 8-B index load, two 16-B
+// value loads per lane) or 8 (fp32: one 16-B index load, two 16-B value loads) -- with index
+// SPB_PADIDX = 16384 (the zero slot past the staged x slice, so padding needs no compare) and
+// value 0 (blk_pad / hipMemsetD16), and start slot-aligned.
 constexpr int SPB_PADIDX = 1 << SPB_MAXSHIFT;
 
 // 64-bit DPP move (two 32-bit halves); lanes the pattern does not reach read 0 (bound_ctrl)
@@ -91,26 +91,59 @@ __device__ __forceinline__ double seg_scan64(double p, int lane, int rs) {
 // 1.185 ms (Aᵀ v) against the per-row pipelined kernel; a plain read of the same bytes takes
 // 1.13 ms; the C5 bench 369 -> 397 it/s.  fp32 values on the padded layout through the same
 // kernel measured slower than the unpadded one-entry-per-lane kernel below (0.907 vs 0.824 ms).
+template <int SLOT>
 struct SpmvWin {
-  uint64_t id;
-  double v[4];
+  uint64_t id[SLOT / 4];   // SLOT 16-bit local indices
+  double v[SLOT];
 };
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void win_load(SpmvWin& w, const uint16_t* __restrict__ lidx,
-                                         const double* __restrict__ val, int64_t slot) {
-  w.id = *(const uint64_t*)(lidx + 4 * slot);
-  const v2d a = *(const v2d*)(val + 4 * slot), b = *(const v2d*)(val + 4 * slot + 2);
-  w.v[0] = a[0];
-  w.v[1] = a[1];
-  w.v[2] = b[0];
-  w.v[3] = b[1];
+template <int SLOT>
+__device__ __forceinline__ void win_load_idx(SpmvWin<SLOT>& w, const uint16_t* __restrict__ lidx, int64_t slot) {
+  if (SLOT == 4) {
+    w.id[0] = *(const uint64_t*)(lidx + 4 * slot);
+  } else {
+#pragma unroll
+    for (int k = 0; k < SLOT / 8; ++k) {
+      const v2u64 t = *(const v2u64*)(lidx + SLOT * slot + 8 * k);
+      w.id[2 * k] = t[0];
+      w.id[2 * k + 1] = t[1];
+    }
+  }
 }
+template <int SLOT>
+__device__ __forceinline__ void win_load(SpmvWin<SLOT>& w, const uint16_t* __restrict__ lidx,
+                                         const double* __restrict__ val, int64_t slot) {
+  win_load_idx(w, lidx, slot);
+#pragma unroll
+  for (int k = 0; k < SLOT / 2; ++k) {
+    const v2d a = *(const v2d*)(val + SLOT * slot + 2 * k);
+    w.v[2 * k] = a[0];
+    w.v[2 * k + 1] = a[1];
+  }
+}
+template <int SLOT>
+__device__ __forceinline__ void win_load(SpmvWin<SLOT>& w, const uint16_t* __restrict__ lidx,
+                                         const float* __restrict__ val, int64_t slot) {
+  win_load_idx(w, lidx, slot);
+#pragma unroll
+  for (int k = 0; k < SLOT / 4; ++k) {
+    const v4f a = *(const v4f*)(val + SLOT * slot + 4 * k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w.v[4 * k + q] = (double)a[q];
+  }
+}
+
+template <typename VT, int SLOT>
 __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __restrict__ ptr,
                                                                const uint16_t* __restrict__ lidx,
-                                                               const double* __restrict__ val,
+                                                               const VT* __restrict__ val,
                                                                const double* __restrict__ x, int64_t nrows,
                                                                int64_t ncols, int shift, double* __restrict__ out,
                                                                int64_t ldo) {
+  constexpr int SH = SLOT == 4 ? 2 : SLOT == 8 ? 3 : 4;
+  static_assert((1 << SH) == SLOT, "slot width 4, 8 or 16");
   __shared__ double xs[SPB_PADIDX + 1];
   const int b = blockIdx.y;
   const int64_t c0 = (int64_t)b << shift;
@@ -134,24 +167,24 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
   const int64_t rw0 = (int64_t)blockIdx.x * SPB_ROWS + (int64_t)wv * 64;
   const int nrw = (int)max((int64_t)0, min((int64_t)64, nrows - rw0));
   if (nrw == 0) return;
-  const int64_t sb = pb[rw0] >> 2;                     // the wave's first slot
-  const int total = (int)((pb[rw0 + nrw] >> 2) - sb);  // its slot count
+  const int64_t sb = pb[rw0] >> SH;                     // the wave's first slot
+  const int total = (int)((pb[rw0 + nrw] >> SH) - sb);  // its slot count
   // st: slot start of row `lane` relative to sb (lanes past nrw: total); en: its end
-  const int st = lane < nrw ? (int)((pb[rw0 + lane] >> 2) - sb) : total;
+  const int st = lane < nrw ? (int)((pb[rw0 + lane] >> SH) - sb) : total;
   const int stn = __shfl(st, min(lane + 1, 63), 64);   // every lane takes part in a shuffle
   const int en = lane + 1 < nrw ? stn : total;
   const int nwin = (total + 63) >> 6;
-  SpmvWin nxt;
+  SpmvWin<SLOT> nxt;
   win_load(nxt, lidx, val, sb + max(min(lane, total - 1), 0));
   double acc = 0.0;
   int cur = 0;   // row of the window's first slot (wave-uniform)
   for (int t = 0; t < nwin; ++t) {
-    const SpmvWin w = nxt;
+    const SpmvWin<SLOT> w = nxt;
     if (t + 1 < nwin) win_load(nxt, lidx, val, sb + min(64 * (t + 1) + lane, total - 1));
     const int base = 64 * t, slot = base + lane;
     double p = 0.0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) p += w.v[e] * xs[(int)((w.id >> (16 * e)) & 0xFFFF)];
+    for (int e = 0; e < SLOT; ++e) p += w.v[e] * xs[(int)((w.id[e / 4] >> (16 * (e & 3))) & 0xFFFF)];
     if (slot >= total) p = 0.0;
     // my row = cur + #{k > cur : st_k <= slot}; the walk stops at the first row starting past
     // the window, and the last row starting at or before base + 64 is the next window's cur
@@ -171,124 +204,6 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
   if (lane < nrw) out[(int64_t)b * ldo + rw0 + lane] = acc;
 }
 
-// RW rows' lane partials -> the lane group of each row holds its sum (fp32 arm below):
-// log2(RW) exchange levels that halve the live rows, then the plain butterfly
-template <int RW>
-__device__ __forceinline__ double multi_row_sum(double (&acc)[RW], int lane, int& row) {
-  row = 0;
-  int off = 32;
-#pragma unroll
-  for (int half = RW / 2; half >= 1; half >>= 1) {
-    const bool hi = (lane & off) != 0;
-#pragma unroll
-    for (int j = 0; j < half; ++j) {
-      const double keep = hi ? acc[j + half] : acc[j];
-      const double send = hi ? acc[j] : acc[j + half];
-      acc[j] = keep + __shfl_xor(send, off, 64);
-    }
-    if (hi) row += half;
-    off >>= 1;
-  }
-  double v = acc[0];
-  for (int o = off; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Unpadded layout, one entry per lane (the fp32 arm: measured faster there than 4-entry slots,
-// 0.844-0.87 against 0.89 ms -- with 6 B per entry the pass is bound by per-entry LDS/VALU
-// instructions, and 4-entry slots leave ~36% of the lanes idle on 164-entry segments).
-// One wave works on RW rows at a time (of its 64 contiguous rows): all RW*U (index,
-// value) loads of a round are issued before any use,
-// masked per lane (clamped addresses), so a row segment of up to 64*U entries --
-// the common case: ~164 per (row, block) at C5 in both directions -- costs one
-// round with RW*U*64 loads per wave in flight (the kernel runs at one workgroup per
-// CU because of the 128 KiB LDS slice).  Per row the summation order is fixed
-// (lane-ascending p, then multi_row_sum's fixed exchange tree).
-template <typename VT, int U, int RW>
-__global__ __launch_bounds__(SPB_THREADS) void spmv_blk1_kernel(const int64_t* __restrict__ ptr,
-                                                               const uint16_t* __restrict__ lidx,
-                                                               const VT* __restrict__ val,
-                                                               const double* __restrict__ x, int64_t nrows,
-                                                               int64_t ncols, int shift, double* __restrict__ out,
-                                                               int64_t ldo, int chunks) {
-  __shared__ double xs[1 << SPB_MAXSHIFT];
-  const int b = blockIdx.y;
-  const int64_t c0 = (int64_t)b << shift;
-  const int nb = (int)min((int64_t)1 << shift, ncols - c0);
-  // stage the slice: all loads of a thread in flight before the LDS stores (a plain
-  // load->store loop serializes 16 L2 round trips while every wave waits at the barrier)
-  {
-    constexpr int PER = (1 << SPB_MAXSHIFT) / SPB_THREADS;
-    double t[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = threadIdx.x + k * SPB_THREADS;
-      t[k] = (i < nb) ? x[c0 + i] : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) xs[threadIdx.x + k * SPB_THREADS] = t[k];
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t* pb = ptr + (int64_t)b * nrows;
-  // the workgroup walks `chunks` consecutive 1024-row chunks of block b with the slice staged
-  // once; its waves run through the chunks without a barrier (no per-chunk drain)
-  for (int ch = 0; ch < chunks; ++ch) {
-  const int64_t cb = (int64_t)blockIdx.x * chunks + ch;
-  if (cb * SPB_ROWS >= nrows) break;
-  const int64_t r1 = min(nrows, (cb + 1) * SPB_ROWS);
-  // each wave owns 64 contiguous rows: their pointer pairs are loaded once (lane k: row
-  // rw0 + k, coalesced) and broadcast per round with readlane, so a round waits on one
-  // memory latency (its data loads), not two
-  const int64_t rw0 = cb * SPB_ROWS + (int64_t)wv * 64;
-  const int64_t myr = rw0 + lane;
-  const int64_t mp0 = (myr < r1) ? pb[myr] : 0, mp1 = (myr < r1) ? pb[myr + 1] : 0;
-  const int nrw = (int)max((int64_t)0, min((int64_t)64, r1 - rw0));
-  for (int k0 = 0; k0 < nrw; k0 += RW) {
-    // per row: wave-uniform base pointers (SGPRs) + 32-bit lane offsets, so 24 loads in
-    // flight do not need 24 64-bit address pairs
-    const uint16_t* li[RW];
-    const VT* va[RW];
-    int len[RW];
-    double acc[RW];
-    int rem = 0;   // longest segment of the group (wave-uniform)
-#pragma unroll
-    for (int j = 0; j < RW; ++j) {
-      const int k = k0 + j;   // rows past nrw have mp0 = mp1 = 0 -> empty
-      const int64_t a0 = ((int64_t)__builtin_amdgcn_readlane((int)(mp0 >> 32), k) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)mp0, k);
-      const int64_t a1 = ((int64_t)__builtin_amdgcn_readlane((int)(mp1 >> 32), k) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)mp1, k);
-      len[j] = (int)(a1 - a0);
-      li[j] = len[j] > 0 ? lidx + a0 : lidx;   // empty rows read element 0 (masked)
-      va[j] = len[j] > 0 ? val + a0 : val;
-      acc[j] = 0.0;
-      rem = max(rem, len[j]);
-    }
-    for (int o = lane; o - lane < rem; o += 64 * U) {
-      int id[RW][U];
-      double v[RW][U];
-#pragma unroll
-      for (int j = 0; j < RW; ++j)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int q = max(min(o + 64 * u, len[j] - 1), 0);
-          id[j][u] = li[j][q];
-          v[j][u] = (double)va[j][q];
-        }
-#pragma unroll
-      for (int j = 0; j < RW; ++j)
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (o + 64 * u < len[j]) acc[j] += v[j][u] * xs[id[j][u]];
-    }
-    int row;
-    const double sum = multi_row_sum<RW>(acc, lane, row);
-    if ((lane & (64 / RW - 1)) == 0 && k0 + row < nrw) out[(int64_t)b * ldo + rw0 + k0 + row] = sum;
-  }
-  }
-}
-
 int spmv_pad_index() { return SPB_PADIDX; }
 
 int spmv_blk_shift(int64_t ncols) {
@@ -302,27 +217,14 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
                            hipStream_t st) {
   if (nrows <= 0) return hipSuccess;
   const int nblk = (int)ceil_div(ncols, (int64_t)1 << shift);
-  // fp64: the flat kernel, one 1024-row chunk per workgroup.  fp32 (unpadded, one entry per
-  // lane): U = 3 slots x 8 rows for short segments (C5: ~164 per (row, block)), 8 x 2 for long
-  // ones, 4 chunks; SCS_SPMV_CHUNKS overrides its chunks (A/B).
-  static const int chunks_env = [] {
-    const char* e = getenv("SCS_SPMV_CHUNKS");
-    return e ? std::max(1, atoi(e)) : 0;
-  }();
-  if (f32) {
-    const int chunks = chunks_env ? chunks_env : 4;
-    const dim3 grid((unsigned)ceil_div(ceil_div(nrows, SPB_ROWS), chunks), (unsigned)nblk);
-    if (nnz / (nrows * nblk) <= 64 * 3)
-      hipLaunchKernelGGL((spmv_blk1_kernel<float, 3, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
-                         (const float*)val, x, nrows, ncols, shift, out, ldo, chunks);
-    else
-      hipLaunchKernelGGL((spmv_blk1_kernel<float, 8, 2>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx,
-                         (const float*)val, x, nrows, ncols, shift, out, ldo, chunks);
-  } else {
-    const dim3 grid((unsigned)ceil_div(nrows, SPB_ROWS), (unsigned)nblk);
-    hipLaunchKernelGGL(spmv_blk_kernel, grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const double*)val, x, nrows,
-                       ncols, shift, out, ldo);
-  }
+  // one 1024-row chunk per workgroup; fp64 in 4-entry slots, fp32 in 8-entry slots
+  const dim3 grid((unsigned)ceil_div(nrows, SPB_ROWS), (unsigned)nblk);
+  if (f32)
+    hipLaunchKernelGGL((spmv_blk_kernel<float, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val, x,
+                       nrows, ncols, shift, out, ldo);
+  else
+    hipLaunchKernelGGL((spmv_blk_kernel<double, 4>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const double*)val,
+                       x, nrows, ncols, shift, out, ldo);
   return hipGetLastError();
 }
 
@@ -373,15 +275,18 @@ hipError_t blk_count(const int64_t* ptr, const int* idx, int64_t nrows, int shif
   return hipGetLastError();
 }
 
-// segment counts rounded up to whole 4-entry slots (the SpMV's per-lane unit)
-__global__ void blk_pad_kernel(int64_t* __restrict__ cnt, int64_t n) {
+// segment counts rounded up to whole slots (the SpMV's per-lane unit: 4 fp64 / 8 fp32 entries)
+__global__ void blk_pad_kernel(int64_t* __restrict__ cnt, int64_t n, int64_t w) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) cnt[i] = (cnt[i] + 3) & ~(int64_t)3;
+  if (i < n) cnt[i] = (cnt[i] + w - 1) & ~(w - 1);
 }
 
-hipError_t blk_pad(int64_t* cnt, int64_t n, hipStream_t st) {
+int spmv_slot_width(int f32) { return f32 ? 8 : 4; }
+
+hipError_t blk_pad(int64_t* cnt, int64_t n, int f32, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(blk_pad_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, cnt, n);
+  hipLaunchKernelGGL(blk_pad_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, cnt, n,
+                     (int64_t)spmv_slot_width(f32));
   return hipGetLastError();
 }
 

@@ -34,7 +34,8 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ void fill_kernel(const int64_t* pb, int64_t nseg, const int64_t* pa, uint16_t* ib, double* vb, int padi) {
+template <typename VT>
+__global__ void fill_kernel(const int64_t* pb, int64_t nseg, const int64_t* pa, uint16_t* ib, VT* vb, int padi) {
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nseg) return;
   const int lane = threadIdx.x & 63;
@@ -43,10 +44,10 @@ __global__ void fill_kernel(const int64_t* pb, int64_t nseg, const int64_t* pa, 
     if (e < L) {
       const uint64_t h = mix64((uint64_t)s * 1000003ull + e);
       ib[b0 + e] = (uint16_t)(h & 16383);
-      vb[b0 + e] = ((double)(h >> 20) * (1.0 / 17592186044416.0)) - 0.5;
+      vb[b0 + e] = (VT)(((double)(h >> 20) * (1.0 / 17592186044416.0)) - 0.5);
     } else {
       ib[b0 + e] = (uint16_t)padi;
-      vb[b0 + e] = 0.0;
+      vb[b0 + e] = (VT)0;
     }
   }
 }
@@ -199,6 +200,27 @@ struct WinS {
   uint64_t id[SLOT / 4];
   double v[SLOT];
 };
+typedef float v4f __attribute__((ext_vector_type(4)));
+template <int SLOT>
+__device__ __forceinline__ void wins_load(WinS<SLOT>& w, const uint16_t* __restrict__ lidx,
+                                          const float* __restrict__ val, int64_t slot) {
+  if (SLOT == 4) {
+    w.id[0] = *(const uint64_t*)(lidx + 4 * slot);
+  } else {
+#pragma unroll
+    for (int k = 0; k < SLOT / 8; ++k) {
+      const v2u t = *(const v2u*)(lidx + SLOT * slot + 8 * k);
+      w.id[2 * k] = t[0];
+      w.id[2 * k + 1] = t[1];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < SLOT / 4; ++k) {
+    const v4f a = *(const v4f*)(val + SLOT * slot + 4 * k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w.v[4 * k + q] = a[q];
+  }
+}
 template <int SLOT>
 __device__ __forceinline__ void wins_load(WinS<SLOT>& w, const uint16_t* __restrict__ lidx,
                                           const double* __restrict__ val, int64_t slot) {
@@ -219,12 +241,12 @@ __device__ __forceinline__ void wins_load(WinS<SLOT>& w, const uint16_t* __restr
 
 // flat2: DPP segmented scan, one window of loads ahead, SLOT entries per lane (segments padded to
 // SLOT), PADZ: padding index = 16384 with xs[16384] = 0 (no per-entry compare)
-template <int SLOT, bool PADZ>
+template <int SLOT, bool PADZ, typename VT = double>
 __global__ __launch_bounds__(1024) void flat2_kernel(const int64_t* __restrict__ ptr, const uint16_t* __restrict__ lidx,
-                                                     const double* __restrict__ val, const double* __restrict__ x,
+                                                     const VT* __restrict__ val, const double* __restrict__ x,
                                                      int64_t nrows, int64_t ncols, int shift, double* __restrict__ out,
                                                      int64_t ldo) {
-  constexpr int SH = SLOT == 4 ? 2 : 3;
+  constexpr int SH = SLOT == 4 ? 2 : SLOT == 8 ? 3 : 4;
   __shared__ double xs[(1 << 14) + 2];
   const int b = blockIdx.y;
   const int64_t c0 = (int64_t)b << shift;
@@ -293,8 +315,8 @@ static void run(int dir) {
   const int64_t nseg = nrows * nblk;
   std::mt19937_64 rng(7);
   std::normal_distribution<double> nd(164.0, 11.0);
-  std::vector<int64_t> pa(nseg + 1), pb(nseg + 1), p8(nseg + 1);
-  pa[0] = pb[0] = p8[0] = 0;
+  std::vector<int64_t> pa(nseg + 1), pb(nseg + 1), p8(nseg + 1), p16(nseg + 1);
+  pa[0] = pb[0] = p8[0] = p16[0] = 0;
   for (int64_t s = 0; s < nseg; ++s) {
     int64_t L = std::max<int64_t>(0, (int64_t)std::llround(nd(rng)));
     if (s % 97 == 5) L = 0;          // some empty segments
@@ -302,6 +324,7 @@ static void run(int dir) {
     pa[s + 1] = pa[s] + L;
     pb[s + 1] = pb[s] + ((L + 3) & ~3LL);
     p8[s + 1] = p8[s] + ((L + 7) & ~7LL);
+    p16[s + 1] = p16[s] + ((L + 15) & ~15LL);
   }
   const int64_t nnz = pa[nseg], nnzb = pb[nseg];
   printf("dir %d nrows %lld nblk %d nnz %lld padded %lld\n", dir, (long long)nrows, nblk, (long long)nnz,
@@ -321,7 +344,7 @@ static void run(int dir) {
   std::vector<double> hx(ncols);
   for (auto& t : hx) t = std::uniform_real_distribution<double>(-1, 1)(rng);
   CK(hipMemcpy(x, hx.data(), 8 * ncols, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dpb, nseg, dpa, ib, vb, 0xFFFF);
+  hipLaunchKernelGGL(fill_kernel<double>, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dpb, nseg, dpa, ib, vb, 0xFFFF);
   const int64_t nnz8 = p8[nseg];
   int64_t *dp8;
   uint16_t *ibz, *ib8;
@@ -332,8 +355,8 @@ static void run(int dir) {
   CK(hipMalloc(&ib8, 2 * nnz8 + 64));
   CK(hipMalloc(&vb8, 8 * nnz8 + 64));
   CK(hipMemcpy(dp8, p8.data(), 8 * (nseg + 1), hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dpb, nseg, dpa, ibz, vbz, 16384);
-  hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dp8, nseg, dpa, ib8, vb8, 16384);
+  hipLaunchKernelGGL(fill_kernel<double>, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dpb, nseg, dpa, ibz, vbz, 16384);
+  hipLaunchKernelGGL(fill_kernel<double>, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dp8, nseg, dpa, ib8, vb8, 16384);
   printf("8-padded nnz %lld (+%.2f%%)\n", (long long)nnz8, 100.0 * (nnz8 - nnz) / nnz);
   CK(hipDeviceSynchronize());
   // the product layout: ptr is nblk x (nrows + 1), segment (row r, block b) at pb[b * nrows + r]
@@ -445,7 +468,76 @@ static void run(int dir) {
     hipLaunchKernelGGL((flat2_kernel<8, true>), grid, dim3(1024), 0, 0, dp8, ib8, vb8, x, nrows, ncols, shift, ob, nrows);
   });
   check("flat2 S8 padz");
-  timeit("flat W=3", [&] {
+  {
+    uint16_t *fia, *fib, *fi8, *fi16;
+    float *fva, *fvb, *fv8, *fv16;
+    int64_t* dp16;
+    const int64_t nnz16 = p16[nseg];
+    CK(hipMalloc(&dp16, 8 * (nseg + 1)));
+    CK(hipMemcpy(dp16, p16.data(), 8 * (nseg + 1), hipMemcpyHostToDevice));
+    CK(hipMalloc(&fi16, 2 * nnz16 + 64));
+    CK(hipMalloc(&fv16, 4 * nnz16 + 64));
+    hipLaunchKernelGGL(fill_kernel<float>, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dp16, nseg, dpa, fi16, fv16, 16384);
+    printf("16-padded +%.2f%%\n", 100.0 * (nnz16 - nnz) / nnz);
+    CK(hipMalloc(&fia, 2 * nnz + 64));
+    CK(hipMalloc(&fva, 4 * nnz + 64));
+    CK(hipMalloc(&fib, 2 * nnzb + 64));
+    CK(hipMalloc(&fvb, 4 * nnzb + 64));
+    CK(hipMalloc(&fi8, 2 * nnz8 + 64));
+    CK(hipMalloc(&fv8, 4 * nnz8 + 64));
+    hipLaunchKernelGGL(fill_kernel<float>, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dpa, nseg, dpa, fia, fva, 0xFFFF);
+    hipLaunchKernelGGL(fill_kernel<float>, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dpb, nseg, dpa, fib, fvb, 16384);
+    hipLaunchKernelGGL(fill_kernel<float>, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, 0, dp8, nseg, dpa, fi8, fv8, 16384);
+    CK(hipDeviceSynchronize());
+    const double fbytes = (double)nnz * 6;
+    auto ftime = [&](const char* name, auto&& launch) {
+      for (int i = 0; i < 3; ++i) launch();
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < 20; ++i) launch();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 20;
+      printf("  %-26s %.4f ms  %.0f GB/s (nnz*6 B)\n", name, ms, fbytes / (ms * 1e-3) / 1e9);
+    };
+    ftime("f32 product", [&] { CK(launch_spmv_blk(dpa, fia, fva, 1, x, nrows, ncols, shift, nnz, oa, nrows, 0)); });
+    ftime("f32 flat2 S4", [&] {
+      hipLaunchKernelGGL((flat2_kernel<4, true, float>), grid, dim3(1024), 0, 0, dpb, fib, fvb, x, nrows, ncols, shift, ob, nrows);
+    });
+    {
+      std::vector<double> fa(nseg), fb(nseg);
+      CK(hipMemcpy(fa.data(), oa, 8 * nseg, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(fb.data(), ob, 8 * nseg, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (int64_t q = 0; q < nseg; ++q) md = std::max(md, std::fabs(fa[q] - fb[q]));
+      printf("  f32 S4 max |product - it| = %.3e\n", md);
+    }
+    ftime("f32 flat2 S8", [&] {
+      hipLaunchKernelGGL((flat2_kernel<8, true, float>), grid, dim3(1024), 0, 0, dp8, fi8, fv8, x, nrows, ncols, shift, ob, nrows);
+    });
+    {
+      std::vector<double> fa(nseg), fb(nseg);
+      CK(hipMemcpy(fa.data(), oa, 8 * nseg, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(fb.data(), ob, 8 * nseg, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (int64_t q = 0; q < nseg; ++q) md = std::max(md, std::fabs(fa[q] - fb[q]));
+      printf("  f32 S8 max |product - it| = %.3e\n", md);
+    }
+    ftime("f32 flat2 S16", [&] {
+      hipLaunchKernelGGL((flat2_kernel<16, true, float>), grid, dim3(1024), 0, 0, dp16, fi16, fv16, x, nrows, ncols, shift, ob, nrows);
+    });
+    {
+      std::vector<double> fa(nseg), fb(nseg);
+      CK(hipMemcpy(fa.data(), oa, 8 * nseg, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(fb.data(), ob, 8 * nseg, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (int64_t q = 0; q < nseg; ++q) md = std::max(md, std::fabs(fa[q] - fb[q]));
+      printf("  f32 S16 max |product - it| = %.3e\n", md);
+    }
+  }
+  if (getenv("PROBE_FULL")) timeit("flat W=3", [&] {
     hipLaunchKernelGGL(flat_kernel<3>, grid, dim3(1024), 0, 0, dpb, ib, vb, x, nrows, ncols, shift, ob, nrows);
   });
   check("flat W=3");
