@@ -159,6 +159,85 @@ __device__ __forceinline__ void chol_inv_double_mfma(double* su, int tid) {
   __syncthreads();
 }
 
+// Phase A: wave 0 factors the 16 x 16 diagonal sub-block at o in registers (lane c = column c;
+// lanes 16..63 mirror lanes 0..15), reciprocal pivots to srinv.
+__device__ __forceinline__ void diag_factor16(double* su, double* srinv, int o, int k, int* info, int tid) {
+  const int c = tid & 15;
+  double a[SB];
+#pragma unroll
+  for (int i = 0; i < SB; ++i) a[i] = su[(o + c) * CLD + o + i];   // S(o+i, o+c); zero below the diagonal
+#pragma unroll
+  for (int j = 0; j < SB; ++j) {
+    const double ajj = readlane_d(a[j], j);
+    if (tid == 0 && !(ajj > 0.0) && *info == 0) *info = k * CB + o + j + 1;
+    // 1/sqrt(ajj): v_rsq_f64 + two Newton steps (6 dependent FMAs instead of the
+    // sqrt + divide sequences on this serial chain); d = ajj * r
+    double r = __builtin_amdgcn_rsq(ajj);
+    const double hj = 0.5 * ajj;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) r = fma(r, fma(-hj * r, r, 0.5), r);
+    const double d = ajj * r;
+    if (tid == 0) srinv[o + j] = r;
+    a[j] = (c > j) ? a[j] * r : ((c == j) ? d : a[j]);    // row j of U: U(j, c)
+#pragma unroll
+    for (int i = j + 1; i < SB; ++i) a[i] -= readlane_d(a[j], i) * a[j];   // U(j, i) from lane i
+  }
+  if (tid < SB) {
+#pragma unroll
+    for (int i = 0; i < SB; ++i)
+      if (i <= c) su[(o + c) * CLD + o + i] = a[i];
+  }
+}
+
+// Phase B: panel, forward substitution Dᵀ p = x per column (D(u, t) reads are wave-uniform)
+__device__ __forceinline__ void diag_panel16(double* su, const double* srinv, int o, int np, int tid) {
+  if (tid < np) {
+    const int c = o + SB + tid;
+    double X[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) X[u] = su[c * CLD + o + u];
+#pragma unroll
+    for (int t = 0; t < SB; ++t) {
+      double sacc = X[t];
+#pragma unroll
+      for (int u = 0; u < t; ++u) sacc -= su[(o + t) * CLD + o + u] * X[u];
+      X[t] = sacc * srinv[o + t];
+    }
+#pragma unroll
+    for (int u = 0; u < SB; ++u) su[c * CLD + o + u] = X[u];
+  }
+}
+
+// Phase C, one 16 x 16 upper tile `id` (C-major: id = C(C+1)/2 + I, I <= C) of the trailing
+// update S(i, c) -= Σ_t U(o + t, i) U(o + t, c), o+16 <= i <= c, as 4 x v_mfma_f64_16x16x4
+// (A[i][k] = U(o+t0+k, i0+i), B[k][j] = U(o+t0+k, c0+j); lane l feeds i|j = l&15, k = l>>4;
+// D row = (l>>4) + 4r, col = l&15).  Diagonal tiles update only i <= c: phase A reads the
+// zeros below the diagonal.  Tile 0 is the next diagonal sub-block.
+__device__ __forceinline__ void diag_trail_tile(double* su, int o, int id, int lane) {
+  const int li = lane & 15, lk = lane >> 4;
+  int C = 0;
+  while ((C + 1) * (C + 2) / 2 <= id) ++C;
+  const int I = id - C * (C + 1) / 2;
+  const int i0 = o + SB + 16 * I, c0 = o + SB + 16 * C;
+  v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int t0 = 0; t0 < SB; t0 += 4) {
+    const double a = su[(i0 + li) * CLD + o + t0 + lk];
+    const double b = su[(c0 + li) * CLD + o + t0 + lk];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + lk + 4 * r, c = c0 + li;
+    if (i <= c) su[c * CLD + i] -= acc[r];
+  }
+}
+
+// PIPE (default): wave 0 takes tile 0 of C(kb) -- the next diagonal sub-block -- and goes straight
+// on to A(kb+1) while waves 1..3 run the rest of C(kb); one barrier per inner block instead of
+// three.  Every element receives the same updates in the same order, so U and W are bitwise those
+// of the phase-serial kernel (PIPE = false, SCS_CHOL_DIAG=0).
+template <bool PIPE>
 __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
                                                         double* __restrict__ W, int* __restrict__ info) {
   __shared__ double su[CB * CLD];   // S(r, c) = su[c*CLD + r]
@@ -194,85 +273,34 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   __syncthreads();
 
   PROF_MARK(0);
+  const int wv = tid >> 6, lane = tid & 63;
+  if (PIPE) {
+    if (tid < 64) diag_factor16(su, srinv, 0, k, info, tid);
+    __syncthreads();
+  }
   for (int kb = 0; kb < CB / SB; ++kb) {
     const int o = kb * SB;
     PROF_MARK(1 + 4 * kb);
-    // ---- A: factor the diagonal sub-block (wave 0; lanes 16..63 mirror lanes 0..15)
-    if (tid < 64) {
-      const int c = tid & 15;
-      double a[SB];
-#pragma unroll
-      for (int i = 0; i < SB; ++i) a[i] = su[(o + c) * CLD + o + i];   // S(o+i, o+c); zero below the diagonal
-#pragma unroll
-      for (int j = 0; j < SB; ++j) {
-        const double ajj = readlane_d(a[j], j);
-        if (tid == 0 && !(ajj > 0.0) && *info == 0) *info = k * CB + o + j + 1;
-        // 1/sqrt(ajj): v_rsq_f64 + two Newton steps (6 dependent FMAs instead of the
-        // sqrt + divide sequences on this serial chain); d = ajj * r
-        double r = __builtin_amdgcn_rsq(ajj);
-        const double hj = 0.5 * ajj;
-#pragma unroll
-        for (int it = 0; it < 2; ++it) r = fma(r, fma(-hj * r, r, 0.5), r);
-        const double d = ajj * r;
-        if (tid == 0) srinv[o + j] = r;
-        a[j] = (c > j) ? a[j] * r : ((c == j) ? d : a[j]);    // row j of U: U(j, c)
-#pragma unroll
-        for (int i = j + 1; i < SB; ++i) a[i] -= readlane_d(a[j], i) * a[j];   // U(j, i) from lane i
-      }
-      if (tid < SB) {
-#pragma unroll
-        for (int i = 0; i < SB; ++i)
-          if (i <= c) su[(o + c) * CLD + o + i] = a[i];
-      }
+    if (!PIPE) {
+      if (tid < 64) diag_factor16(su, srinv, o, k, info, tid);
+      __syncthreads();
     }
-    __syncthreads();
     PROF_MARK(2 + 4 * kb);
     const int np = CB - o - SB;  // columns right of the sub-block
     if (np == 0) break;
-    // ---- B: panel, forward substitution Dᵀ p = x per column (D(u, t) reads are wave-uniform)
-    if (tid < np) {
-      const int c = o + SB + tid;
-      double X[SB];
-#pragma unroll
-      for (int u = 0; u < SB; ++u) X[u] = su[c * CLD + o + u];
-#pragma unroll
-      for (int t = 0; t < SB; ++t) {
-        double sacc = X[t];
-#pragma unroll
-        for (int u = 0; u < t; ++u) sacc -= su[(o + t) * CLD + o + u] * X[u];
-        X[t] = sacc * srinv[o + t];
-      }
-#pragma unroll
-      for (int u = 0; u < SB; ++u) su[c * CLD + o + u] = X[u];
-    }
+    diag_panel16(su, srinv, o, np, tid);
     __syncthreads();
     PROF_MARK(3 + 4 * kb);
-    // ---- C: trailing update  S(i, c) -= Σ_t U(o + t, i) U(o + t, c),  o+16 <= i <= c, on MFMA:
-    // 16 x 16 upper tiles (I <= C) round-robin over the waves, 4 x v_mfma_f64_16x16x4 each
-    // (A[i][k] = U(o+t0+k, i0+i), B[k][j] = U(o+t0+k, c0+j); lane l feeds i|j = l&15, k = l>>4;
-    // D row = (l>>4) + 4r, col = l&15).  Diagonal tiles update only i <= c: phase A reads the
-    // zeros below the diagonal.
-    {
-      const int n16 = np >> 4, ntl = n16 * (n16 + 1) / 2;
-      const int wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
-      for (int id = wv; id < ntl; id += DNT / 64) {
-        int C = 0;
-        while ((C + 1) * (C + 2) / 2 <= id) ++C;
-        const int I = id - C * (C + 1) / 2;
-        const int i0 = o + SB + 16 * I, c0 = o + SB + 16 * C;
-        v4d acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int t0 = 0; t0 < SB; t0 += 4) {
-          const double a = su[(i0 + li) * CLD + o + t0 + lk];
-          const double b = su[(c0 + li) * CLD + o + t0 + lk];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = i0 + lk + 4 * r, c = c0 + li;
-          if (i <= c) su[c * CLD + i] -= acc[r];
-        }
+    const int n16 = np >> 4, ntl = n16 * (n16 + 1) / 2;
+    if (PIPE) {
+      if (wv == 0) {
+        diag_trail_tile(su, o, 0, lane);
+        diag_factor16(su, srinv, o + SB, k, info, tid);
+      } else {
+        for (int id = wv; id < ntl; id += DNT / 64 - 1) diag_trail_tile(su, o, id, lane);
       }
+    } else {
+      for (int id = wv; id < ntl; id += DNT / 64) diag_trail_tile(su, o, id, lane);
     }
     __syncthreads();
   }
@@ -300,6 +328,19 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
     Wk[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
   }
   PROF_MARK(35);
+}
+
+static bool chol_diag_pipe() {   // read per call (A/B within one process)
+  const char* e = getenv("SCS_CHOL_DIAG");
+  return !(e && e[0] == '0');
+}
+
+hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st) {
+  if (chol_diag_pipe())
+    hipLaunchKernelGGL(chol_diag_kernel<true>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+  else
+    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+  return hipGetLastError();
 }
 
 __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, int64_t mpad) {
@@ -459,7 +500,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     const int i1 = i0 + OB < nblk ? i0 + OB : nblk;
     // A: inner factor of the outer diagonal block
     for (int k = i0; k < i1; ++k) {
-      hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+      e = launch_chol_diag(G, ld, k, W, info, st);
+      if (e != hipSuccess) return e;
       const int nb = i1 - k - 1;
       if (nb == 0) break;
       double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..i1-1)
@@ -573,12 +615,13 @@ hipError_t chol_strip_factor(double* G, int64_t ld, int s, double* W, const Chol
   const int nblk = a->nblk, OB = outer_block();
   const int i0 = s * OB, i1 = std::min(i0 + OB, nblk);
   for (int k = i0; k < i1; ++k) {
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+    hipError_t e = launch_chol_diag(G, ld, k, W, info, st);
+    if (e != hipSuccess) return e;
     const int nb = i1 - k - 1;
     if (nb == 0) break;
     double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;
-    hipError_t e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb,
-                                   rowpanel, ld, 0, st);
+    e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb, rowpanel, ld, 0,
+                        st);
     if (e != hipSuccess) return e;
     double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
     e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld, 2 | 4, st);

@@ -77,6 +77,8 @@ struct CholAux {             // device constants of the two-level factorization 
 };
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);
 void chol_aux_free(CholAux* a);
+// the 128 x 128 diagonal block k: factor in place, W_k = U_kk⁻¹ (SCS_CHOL_DIAG=0: phase-serial kernel)
+hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st);
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* aux,
                        const int2* trilist, int* info, hipStream_t st);
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
@@ -145,11 +147,18 @@ hipError_t launch_lqn_eta(const double* gr, const double* Hr, int64_t m, double 
 hipError_t launch_lqn_tail(const double* x, const double* d, int neg, int64_t m, double Mg, double step,
                            const ProxArgsH& P, const double* hinv, double* x_new, double* dx, double* dh, double* R,
                            double* scal, hipStream_t st);
+// ring (device [order[0..mem] | k | spare]) non-null: the pair goes to slot ring[mem+2] and the
+// memory decision is taken on the device (H0 -> scal[h0_slot]); null: slot `slot`, the host decides.
+// A second kernel forms the sums (and, with valpart, the loss sum as sum_partials does -> scal[zf_slot]),
+// then copies scal[0..nmap) to hmap (device-mapped pinned host memory; nmap <= 64, 0: none).  (A last-
+// workgroup reduction inside lqn_post measured slower: each workgroup's device-scope release writes
+// back the XCD's L2.)
 hipError_t launch_lqn_post(const double* tpart, int nchunk, int64_t ldp, int64_t m, double lam, int skind, double mu,
                            const double* sa, const double* sb, const ProxArgsH& P, const double* xs, const double* x,
-                           const double* xn, const double* gq, const double* dh, double* gqn, double* Sslot,
-                           double* Yslot, double* gr, double* Hr, double* hinv, double* R, double* scal, int rx_slot,
-                           int nrm_slot, hipStream_t st);
+                           const double* xn, const double* gq, const double* dh, double* gqn, double* S, double* Y,
+                           int64_t lds, int* ring, int mem, int slot, double* gr, double* Hr, double* hinv, double* R,
+                           const double* valpart, int nval, double* scal, int zf_slot, int rx_slot, int nrm_slot,
+                           int h0_slot, double* hmap, int nmap, hipStream_t st);
 // out[0..3) = Σ(x − xs)², Σx², Σ(xn − x)² (xs / xn may be null); part: 3 x 256 doubles
 hipError_t launch_norms3(const double* x, const double* xs, const double* xn, int64_t m, double* out, double* part,
                          hipStream_t st);
@@ -161,12 +170,13 @@ hipError_t launch_trial_point(const double* x, const double* d, double alpha, in
 hipError_t launch_bb_step(const double* x, const double* xp, const double* g, const double* gp, int64_t m,
                           double* out, hipStream_t st);
 // m <= TWO_LOOP_SINGLE_MAX: one workgroup; above: TWO_LOOP_MAX_WG workgroups at most, one launch per
-// recursion step; work holds (k + 2) * TWO_LOOP_MAX_WG doubles
+// recursion step; work holds (kcap + 4) * TWO_LOOP_MAX_WG doubles (kcap >= k).  kp / H0p non-null: the
+// ring size and H0 are read on the device (scs_iterate's pipelined loop) and k is only their upper bound.
 constexpr int64_t TWO_LOOP_SINGLE_MAX = 16384;
 constexpr int TWO_LOOP_MAX_WG = 256;
 hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
-                           const double* g, int64_t m, double* q, double* d, double* ab, double* work,
-                           hipStream_t st);
+                           const double* g, int64_t m, double* q, double* d, double* ab, double* work, int kcap,
+                           const int* kp, const double* H0p, hipStream_t st);
 hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
                                double* Yslot, double* scal, double* part, hipStream_t st);
 hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st);

@@ -39,6 +39,7 @@ enum { T_GRAM = 0, T_GEMV, T_SOLVE, T_STEP, T_REDUCE, T_N };
 constexpr int ZF_SLOT = 24;   // scal / hscal slot of the deferred f(x) (forward with need_val = false)
 // scs_iterate's device-resident loop: f(x) and get_reg(x) of the epoch's x, the norms (3 slots)
 constexpr int FX_SLOT = 25, RX_SLOT = 26, NRM_SLOT = 28, LOOP_SLOTS = 32;
+constexpr int H0_SLOT = 19;   // the device ring's H0 (scs_iterate's pipelined ProxLQNSCORE loop)
 
 struct DevBuf {
   void* p = nullptr;
@@ -168,6 +169,9 @@ struct scs_ctx {
   double* hscal = nullptr;  // pinned host scalars
   double* xstar = nullptr;  // model.x on the device (scs_iterate's rel_error)
   double* lqR = nullptr;    // fused ProxLQNSCORE epoch: LQ_NPART x 256 partial sums
+  double* hloop = nullptr;  // pinned: the pipelined loop's per-epoch scalars, two epochs (parity)
+  double* hloop_dev = nullptr;   // its device-side address
+  hipEvent_t loop_ev[2] = {nullptr, nullptr};
   bool dev_loop = false;    // scs_iterate's device-resident loop: steps leave x_new / pri on the device
   // N-space workspace
   int nsplit = 1;
@@ -258,6 +262,7 @@ struct scs_ctx {
 
   // timing
   bool timing = false;
+  int timing_every = 1;     // scs_iterate's pipelined loop: kernel-timing events on every n-th epoch only
   std::vector<Pending> pending;
   double tms[T_N] = {0, 0, 0, 0, 0};
   int64_t tcalls[T_N] = {0, 0, 0, 0, 0};
@@ -514,6 +519,10 @@ void alloc_mspace(scs_ctx* c) {
   dfree_t(c, c->lqR);
   c->lqR = dalloc<double>(c, (size_t)LQ_NPART * LQ_G);
   if (!c->hscal) HCK(hipHostMalloc((void**)&c->hscal, 64 * sizeof(double), hipHostMallocDefault));
+  if (!c->hloop) {   // written by kernels (lqn_post): fine-grained, device-mapped
+    HCK(hipHostMalloc((void**)&c->hloop, 2 * LOOP_SLOTS * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
+    HCK(hipHostGetDevicePointer((void**)&c->hloop_dev, c->hloop, 0));
+  }
 }
 
 void alloc_nspace(scs_ctx* c) {
@@ -1631,8 +1640,8 @@ void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, dou
   } else {
     std::memcpy(c->hring, c->ring.data(), sizeof(int) * k);   // pinned: a truly asynchronous upload
     HCK(hipMemcpyAsync(c->d_order, c->hring, sizeof(int) * k, hipMemcpyHostToDevice, c->st));
-    HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->tlwork,
-                        c->st));
+    HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->tlwork, c->mem,
+                        nullptr, nullptr, c->st));
   }
   double step = 0.0;
   const double* step_dev = nullptr;
@@ -1722,6 +1731,9 @@ int scs_destroy(scs_ctx* c) {
   for (auto& a : c->allocs) (void)hipFree(a.p);
   if (c->hscal) (void)hipHostFree(c->hscal);
   if (c->hring) (void)hipHostFree(c->hring);
+  if (c->hloop) (void)hipHostFree(c->hloop);
+  for (hipEvent_t e : c->loop_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->cbh) (void)hipHostFree(c->cbh);
   lu_aux_free(&c->lu);
   if (c->sf) {
@@ -2350,13 +2362,13 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
       dfree_t(c, c->d_order);
       dfree_t(c, c->ab);
       dfree_t(c, c->tlwork);
-      c->tlwork = dalloc<double>(c, (size_t)(mem + 3) * TWO_LOOP_MAX_WG);
+      c->tlwork = dalloc<double>(c, (size_t)(mem + 5) * TWO_LOOP_MAX_WG);
       c->S = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
       c->Yv = dalloc<double>(c, (size_t)(mem + 1) * c->mpad);
-      c->d_order = dalloc<int>(c, mem + 1);
+      c->d_order = dalloc<int>(c, mem + 3);   // order[0..mem] | k | spare (the device ring)
       if (c->hring) (void)hipHostFree(c->hring);
       c->hring = nullptr;
-      HCK(hipHostMalloc((void**)&c->hring, sizeof(int) * (mem + 1), hipHostMallocDefault));
+      HCK(hipHostMalloc((void**)&c->hring, sizeof(int) * (mem + 3), hipHostMallocDefault));
       c->ab = dalloc<double>(c, 2 * (mem + 1));
       sync(c);
     }
@@ -2640,65 +2652,132 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         sync(c);
         double fcur = loss_scale_value(c, hs[ZF_SLOT]), regcur = hs[RX_SLOT];
         double relcur = rel_from(hs[NRM_SLOT]), nxcur = std::sqrt(hs[NRM_SLOT + 1]);
+        // Pipelined by one epoch: epoch e+1 is enqueued before the host reads epoch e's scalars, so
+        // the GPU never idles for the hand-off.  What the next epoch needs from this one stays on
+        // the device: the L-BFGS ring ([order | k | spare] in d_order, H0 in scal[H0_SLOT]) is
+        // advanced by lqn_post's last workgroup, and the two-loop launches for an upper bound of k
+        // (the ring grows by at most one per epoch in flight; surplus launches return at once).
+        // The host keeps the mirror (lbfgs_accept on the same δhᵀγh, γhᵀγh) for the history and
+        // the state after the call.  An epoch enqueued past the stopping one writes only x_prev's
+        // buffer, the spare pair slot and scratch; its buffer rotation is undone.
+        const int mem = c->mem;
+        for (int i = 0; i < mem + 3; ++i) c->hring[i] = 0;   // init!: empty ring, spare slot 0
+        HCK(hipMemcpyAsync(c->d_order, c->hring, sizeof(int) * (mem + 3), hipMemcpyHostToDevice, c->st));
+        HCK(launch_fill(c->scal + H0_SLOT, 1, 1.0, c->st));
+        for (auto& ev : c->loop_ev)
+          if (!ev) HCK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        struct Rot {
+          double *x, *xp, *xn, *gq, *gqn;
+        };
+        auto rot_get = [&] { return Rot{c->x, c->xp, c->xn, c->gq, c->gqn}; };
+        // the epoch's scalars: written by lqn_post's final kernel straight into the pinned buffer
+        // (SCS_LOOP_HOSTMAP=0: a device-to-host copy after it)
+        const char* hm_env = std::getenv("SCS_LOOP_HOSTMAP");
+        const bool hostmap = !(hm_env && hm_env[0] == '0');
+        int64_t enq = 0, done = 0;
+        Rot before_last{};   // the rotation state before the latest enqueue
+        // k = 0 is speculated while the host's ring is empty (no two-loop launches: the tail takes
+        // d = -∇q); when the epoch in flight turns out to have accepted the first pair, the epoch
+        // enqueued behind it is discarded and re-run (once per call: the ring never empties).
+        bool spec_k0 = false;   // the latest enqueue assumed k = 0
+        auto enqueue = [&](int64_t e) {
+          before_last = rot_get();
+          const bool timed = c->timing && (e % c->timing_every == 0);
+          const bool tsave = c->timing;
+          c->timing = timed;   // timing events cost a dispatch gap each: sample the epochs
+          const int kmax = c->ring.empty() ? 0 : std::min<int>(mem, (int)c->ring.size() + (int)(enq - done));
+          spec_k0 = kmax == 0;
+          hipEvent_t e0;
+          tbegin(c, T_STEP, &e0);
+          if (kmax > 0)
+            HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, kmax, 1.0, c->gq, m, c->q, c->d, c->ab, c->tlwork,
+                                mem, c->d_order + mem + 1, c->scal + H0_SLOT, c->st));
+          HCK(launch_lqn_tail(c->x, kmax > 0 ? c->d : c->gq, kmax > 0 ? 0 : 1, m, Mg, step, prox_args(c), c->hinv,
+                              c->xn, c->dxv, c->q, c->lqR, c->scal, c->st));
+          // z = A x_new, r = ∂f/∂z, f(x_new) -> scal[ZF_SLOT] (forward()'s passes, no host copies)
+          hipEvent_t e1;
+          tbegin(c, T_GEMV, &e1);
+          const int ns = matvec_n(c, c->xn, c->nsplit);
+          tend(c, T_GEMV, e1);
+          HCK(launch_epilogue(c->loss, c->ggn, EPI_GRAD | EPI_Z | EPI_VAL, c->zpart, ns, c->Npad, c->y, c->N, c->Npad,
+                              c->scale, c->z, c->gN, c->hN, c->wN, c->vN, c->valpart, c->st));   // Σ: lqn_post
+          hipEvent_t e2;
+          tbegin(c, T_GEMV, &e2);
+          const int np = matvec_t_part(c, c->gN);       // Aᵀ r partials
+          tend(c, T_GEMV, e2);
+          HCK(launch_lqn_post(c->tpart, np, c->mpad, m, c->lam, c->smooth, c->mu, c->slb, c->sub, prox_args(c),
+                              c->xstar, c->x, c->xn, c->gq, c->q, c->gqn, c->S, c->Yv, c->mpad, c->d_order, mem, 0,
+                              c->gr, c->Hr, c->hinv, c->lqR, c->valpart, c->nval, c->scal, ZF_SLOT, RX_SLOT, NRM_SLOT,
+                              H0_SLOT, c->hloop_dev + (e & 1) * LOOP_SLOTS, hostmap ? LOOP_SLOTS : 0, c->st));
+          tend(c, T_STEP, e0);
+          if (!hostmap) d2h(c, c->hloop + (e & 1) * LOOP_SLOTS, c->scal, LOOP_SLOTS);
+          HCK(hipEventRecord(c->loop_ev[e & 1], c->st));
+          double* t = c->xp;   // x_prev <- x, x <- x_new
+          c->xp = c->x;
+          c->x = c->xn;
+          c->xn = t;
+          std::swap(c->gq, c->gqn);   // ∇q(x) of the next epoch
+          ++enq;
+          c->timing = tsave;
+        };
+        auto restore_last = [&] {   // undo the rotation of the latest enqueue
+          c->x = before_last.x;
+          c->xp = before_last.xp;
+          c->xn = before_last.xn;
+          c->gq = before_last.gq;
+          c->gqn = before_last.gqn;
+        };
+        enqueue(1);
         for (int64_t epoch = 1; epoch <= max_epoch; ++epoch) {
           const double dt = now();
           const double obj = fcur + regcur;
           const double frel = frel_of(obj);
           push(obj, fcur, pri, relcur, frel, dt);
           if (epoch == max_epoch) push(obj, fcur, pri, relcur, frel, now());   // iterate.jl:219-231
-          hipEvent_t e0;
-          tbegin(c, T_STEP, &e0);
-          const int k = (int)c->ring.size();
-          const bool neg = (epoch == 1 || k == 0);   // prox-L-BFGS-SCORE.jl:102-106
-          if (!neg) {
-            std::memcpy(c->hring, c->ring.data(), sizeof(int) * k);
-            HCK(hipMemcpyAsync(c->d_order, c->hring, sizeof(int) * k, hipMemcpyHostToDevice, c->st));
-            HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->tlwork,
-                                c->st));
+          if (epoch < max_epoch) enqueue(epoch + 1);
+          HCK(hipEventSynchronize(c->loop_ev[epoch & 1]));
+          const double* he = c->hloop + (epoch & 1) * LOOP_SLOTS;
+          ++done;
+          const bool was_empty = c->ring.empty();
+          lbfgs_accept(c, c->spare, he[16], he[17]);   // the device took the same decision
+          if (was_empty && !c->ring.empty() && enq > done && spec_k0) {
+            // epoch + 1 ran with d = -∇q but the memory now holds a pair: discard it.  Restore the
+            // rotation, the ring (host mirror) and H0, and the smoother / η state at x_{epoch+1}
+            // that its post pass overwrote (the same kernels as the setup), then enqueue it again.
+            sync(c);
+            restore_last();
+            enq = done;
+            const int k = (int)c->ring.size();
+            for (int i = 0; i < mem + 3; ++i) c->hring[i] = 0;
+            for (int i = 0; i < k; ++i) c->hring[i] = c->ring[i];
+            c->hring[mem + 1] = k;
+            c->hring[mem + 2] = c->spare;
+            HCK(hipMemcpyAsync(c->d_order, c->hring, sizeof(int) * (mem + 3), hipMemcpyHostToDevice, c->st));
+            HCK(launch_fill(c->scal + H0_SLOT, 1, c->H0, c->st));
+            HCK(launch_smoother(c->smooth, c->x, m, c->mu, c->slb, c->sub, c->wel, c->gr, c->Hr, c->st));
+            HCK(launch_lqn_eta(c->gr, c->Hr, m, c->lam, c->hinv, c->lqR, c->st));
+            enqueue(epoch + 1);
           }
-          HCK(launch_lqn_tail(c->x, neg ? c->gq : c->d, neg ? 1 : 0, m, Mg, step, prox_args(c), c->hinv, c->xn,
-                              c->dxv, c->q, c->lqR, c->scal, c->st));
-          tag_slot(x_new).v = c->xtag_next++;
-          forward(c, x_new, c->xn, EPI_GRAD, false);   // z = A x_new, r, f(x_new) in flight
-          hipEvent_t e1;
-          tbegin(c, T_GEMV, &e1);
-          const int np = matvec_t_part(c, c->gN);       // Aᵀ r partials
-          tend(c, T_GEMV, e1);
-          const int slot = c->spare;
-          HCK(launch_lqn_post(c->tpart, np, c->mpad, m, c->lam, c->smooth, c->mu, c->slb, c->sub, prox_args(c), c->xstar,
-                              c->x, c->xn, c->gq, c->q, c->gqn, c->S + (int64_t)slot * c->mpad,
-                              c->Yv + (int64_t)slot * c->mpad, c->gr, c->Hr, c->hinv, c->lqR, c->scal, RX_SLOT,
-                              NRM_SLOT, c->st));
-          tend(c, T_STEP, e0);
-          d2h(c, hs, c->scal, LOOP_SLOTS);
-          sync(c);
-          c->lbfgs_pending = true;
-          c->lbfgs_slot = slot;
-          lbfgs_settle(c, true);
-          pri = hs[0];
-          const double ndx = std::sqrt(hs[NRM_SLOT + 2]);
-          const double fnext = loss_scale_value(c, hs[ZF_SLOT]), regnext = hs[RX_SLOT];
-          c->zfval = fnext;
-          c->zf_pending = false;
-          const double relnext = rel_from(hs[NRM_SLOT]), nxnext = std::sqrt(hs[NRM_SLOT + 1]);
+          pri = he[0];
+          const double ndx = std::sqrt(he[NRM_SLOT + 2]);
+          const double fnext = loss_scale_value(c, he[ZF_SLOT]), regnext = he[RX_SLOT];
+          const double relnext = rel_from(he[NRM_SLOT]), nxnext = std::sqrt(he[NRM_SLOT + 1]);
           const bool stop = ndx < x_tol * std::max(nxcur, 1.0) || frel <= f_tol || pri < x_tol;
           if (stop && epoch != max_epoch)   // iterate.jl:235-247: stats of x_new
             push(fnext + regnext, fnext, pri, relnext, frel_of(fnext + regnext), now());
-          std::swap(x_prev, x);
-          tag_slot(x).v = tag_slot(x_new).v;
-          double* t = c->xp;
-          c->xp = c->x;
-          c->x = c->xn;
-          c->xn = t;
-          std::swap(c->gq, c->gqn);          // ∇q(x) of the next epoch
-          c->gvalid[0] = c->gvalid[1] = false;
           fcur = fnext;
           regcur = regnext;
           relcur = relnext;
           nxcur = nxnext;
           ++epochs;
-          if (stop) break;
+          if (stop) {
+            if (enq > done) restore_last();   // the epoch enqueued past this one
+            break;
+          }
         }
+        sync(c);
+        c->lbfgs_pending = false;
+        invalidate_caches(c);   // z, f and ∇q of the last enqueued point, which may be past the stop
         d2h(c, x_out, c->x, m);
         sync(c);
         *n_hist = nh;
@@ -3043,7 +3122,10 @@ int scs_gemv_n_eval(scs_ctx* c, const double* x, double* out) {
 }
 
 int scs_timing_enable(scs_ctx* c, int on) {
-  return guarded(c, [&] { c->timing = on != 0; });
+  return guarded(c, [&] {
+    c->timing = on != 0;
+    c->timing_every = on > 1 ? on : 1;
+  });
 }
 
 int scs_timing_get(scs_ctx* c, scs_timing* t) {

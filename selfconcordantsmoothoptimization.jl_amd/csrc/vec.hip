@@ -443,12 +443,21 @@ __global__ __launch_bounds__(VB) void bb_step_kernel(const double* __restrict__ 
 // L-BFGS two-loop recursion (prox-L-BFGS-SCORE.jl:47-68) for one workgroup.
 // S, Y: ring buffers [mem][ld]; order[k] = ring slot of the k-th oldest pair.
 // Writes d = -r.  Dots are recomputed exactly as the reference does.
+// kp / H0p (device ring, scs_iterate's pipelined loop): k = *kp and H0 = *H0p instead of the
+// arguments; k = 0 gives d = -g (launch_neg's bits: the reference's `d = -∇q` branch).
 __global__ __launch_bounds__(VB) void two_loop_kernel(const double* __restrict__ S, const double* __restrict__ Y,
-                                                      int64_t ld, const int* __restrict__ order, int k,
+                                                      int64_t ld, const int* __restrict__ order,
+                                                      const int* __restrict__ kp, int k, const double* __restrict__ H0p,
                                                       double H0, const double* __restrict__ g, int64_t m,
                                                       double* __restrict__ q, double* __restrict__ dout,
                                                       double* __restrict__ ab /*[2*k]*/) {
   __shared__ double sh[VB / 64];
+  if (kp) k = *kp;
+  if (H0p) H0 = *H0p;
+  if (k == 0) {
+    for (int64_t i = threadIdx.x; i < m; i += VB) dout[i] = -g[i];
+    return;
+  }
   for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = g[i];
   __syncthreads();
   for (int t = k - 1; t >= 0; --t) {           // newest -> oldest
@@ -497,15 +506,22 @@ __device__ __forceinline__ double sum_parts(const double* __restrict__ p, int G)
   return s;
 }
 
-__global__ __launch_bounds__(TLB) void tl_init_kernel(const double* __restrict__ S, const double* __restrict__ Y,
-                                                      int64_t ld, const int* __restrict__ order, int k,
-                                                      const double* __restrict__ g, int64_t m, int64_t C,
-                                                      double* __restrict__ q, double* __restrict__ pys,
-                                                      double* __restrict__ psq) {
-  __shared__ double sh[TLB / 64];
-  const int G = gridDim.x, b = blockIdx.x;
+// The recursion step a launch handles is its launch index i (first loop t = k-1-i, second loop
+// t = i), so with a device ring (kp) the host launches for an upper bound of k and the surplus
+// launches return at once.  Partial dots live in parity buffers keyed by t (work: pys [k][G],
+// then first-loop P[0], P[1] and second-loop P[2], P[3], G each), not by launch order.
+// Bodies of the launches (chunk b of G).
+__device__ __forceinline__ void tl_init_body(const double* __restrict__ S, const double* __restrict__ Y, int64_t ld,
+                                             const int* __restrict__ order, int k, const double* __restrict__ g,
+                                             int64_t m, int64_t C, double* __restrict__ work, int kcap,
+                                             double* __restrict__ dout, int b, int G, double* sh) {
   const int64_t i0 = b * C, i1 = min(m, i0 + C);
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) q[i] = g[i];
+  if (k == 0) {   // d = -∇q
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) dout[i] = -g[i];
+    return;
+  }
+  double* pys = work;
+  double* psq = work + ((int64_t)kcap + ((k - 1) & 1)) * G;
   for (int t = 0; t < k; ++t) {
     const double* s = S + (int64_t)order[t] * ld;
     const double* y = Y + (int64_t)order[t] * ld;
@@ -523,23 +539,24 @@ __global__ __launch_bounds__(TLB) void tl_init_kernel(const double* __restrict__
 
 // first loop, step t (newest -> oldest): q -= α_t y_t; partial s_{t-1}·q (or, at t = 0,
 // r = H0 q and the partial y_0·r of the second loop)
-__global__ __launch_bounds__(TLB) void tl_first_kernel(const double* __restrict__ S, const double* __restrict__ Y,
-                                                       int64_t ld, const int* __restrict__ order, int t, double H0,
-                                                       int64_t m, int64_t C, double* __restrict__ q,
-                                                       const double* __restrict__ pys,
-                                                       const double* __restrict__ pin, double* __restrict__ pout,
-                                                       double* __restrict__ ab) {
-  __shared__ double sh[TLB / 64];
-  const int G = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ void tl_first_body(const double* __restrict__ S, const double* __restrict__ Y, int64_t ld,
+                                              const int* __restrict__ order, int k, int t, double H0, int64_t m,
+                                              int64_t C, const double* __restrict__ g, double* __restrict__ q,
+                                              double* __restrict__ work, int kcap, double* __restrict__ ab, int b,
+                                              int G, double* sh) {
   const int64_t i0 = b * C, i1 = min(m, i0 + C);
+  const double* pys = work;
+  const double* pin = work + ((int64_t)kcap + (t & 1)) * G;
+  double* pout = work + ((int64_t)kcap + (t > 0 ? ((t - 1) & 1) : 2)) * G;
   const double ys = sum_parts(pys + t * G, G), sq = sum_parts(pin, G);
   const double rho = 1.0 / ys;
   const double al = rho * sq;
   const double* y = Y + (int64_t)order[t] * ld;
   const double* sn = (t > 0) ? S + (int64_t)order[t - 1] * ld : Y + (int64_t)order[0] * ld;
+  const double* qin = (t == k - 1) ? g : q;   // q = ∇q before the first step
   double v = 0.0;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) {
-    double qi = q[i] - al * y[i];
+    double qi = qin[i] - al * y[i];
     if (t == 0) qi = H0 * qi;
     q[i] = qi;
     v += sn[i] * qi;
@@ -552,14 +569,14 @@ __global__ __launch_bounds__(TLB) void tl_first_kernel(const double* __restrict_
 }
 
 // second loop, step t (oldest -> newest): r += s_t (α_t − β_t); partial y_{t+1}·r, or d = −r at the end
-__global__ __launch_bounds__(TLB) void tl_second_kernel(const double* __restrict__ S, const double* __restrict__ Y,
-                                                        int64_t ld, const int* __restrict__ order, int t, int k,
-                                                        int64_t m, int64_t C, double* __restrict__ r,
-                                                        const double* __restrict__ pin, double* __restrict__ pout,
-                                                        const double* __restrict__ ab, double* __restrict__ dout) {
-  __shared__ double sh[TLB / 64];
-  const int G = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ void tl_second_body(const double* __restrict__ S, const double* __restrict__ Y, int64_t ld,
+                                               const int* __restrict__ order, int k, int t, int64_t m, int64_t C,
+                                               double* __restrict__ r, double* __restrict__ work, int kcap,
+                                               const double* __restrict__ ab, double* __restrict__ dout, int b, int G,
+                                               double* sh) {
   const int64_t i0 = b * C, i1 = min(m, i0 + C);
+  const double* pin = work + ((int64_t)kcap + 2 + (t & 1)) * G;
+  double* pout = work + ((int64_t)kcap + 2 + ((t + 1) & 1)) * G;
   const double yr = sum_parts(pin, G);
   const double al = ab[2 * t], rho = ab[2 * t + 1];
   const double beta = rho * yr;
@@ -577,6 +594,44 @@ __global__ __launch_bounds__(TLB) void tl_second_kernel(const double* __restrict
     v = block_sum<TLB>(v, sh);
     if (threadIdx.x == 0) pout[b] = v;
   }
+}
+
+__global__ __launch_bounds__(TLB) void tl_init_kernel(const double* __restrict__ S, const double* __restrict__ Y,
+                                                      int64_t ld, const int* __restrict__ order,
+                                                      const int* __restrict__ kp, int k,
+                                                      const double* __restrict__ g, int64_t m, int64_t C,
+                                                      double* __restrict__ work, int kcap,
+                                                      double* __restrict__ dout) {
+  __shared__ double sh[TLB / 64];
+  if (kp) k = *kp;
+  tl_init_body(S, Y, ld, order, k, g, m, C, work, kcap, dout, blockIdx.x, gridDim.x, sh);
+}
+
+__global__ __launch_bounds__(TLB) void tl_first_kernel(const double* __restrict__ S, const double* __restrict__ Y,
+                                                       int64_t ld, const int* __restrict__ order,
+                                                       const int* __restrict__ kp, int k, int li,
+                                                       const double* __restrict__ H0p, double H0, int64_t m,
+                                                       int64_t C, const double* __restrict__ g,
+                                                       double* __restrict__ q, double* __restrict__ work, int kcap,
+                                                       double* __restrict__ ab) {
+  __shared__ double sh[TLB / 64];
+  if (kp) k = *kp;
+  if (H0p) H0 = *H0p;
+  const int t = k - 1 - li;
+  if (t < 0) return;
+  tl_first_body(S, Y, ld, order, k, t, H0, m, C, g, q, work, kcap, ab, blockIdx.x, gridDim.x, sh);
+}
+
+__global__ __launch_bounds__(TLB) void tl_second_kernel(const double* __restrict__ S, const double* __restrict__ Y,
+                                                        int64_t ld, const int* __restrict__ order,
+                                                        const int* __restrict__ kp, int k, int t, int64_t m,
+                                                        int64_t C, double* __restrict__ r,
+                                                        double* __restrict__ work, int kcap,
+                                                        const double* __restrict__ ab, double* __restrict__ dout) {
+  __shared__ double sh[TLB / 64];
+  if (kp) k = *kp;
+  if (t >= k) return;
+  tl_second_body(S, Y, ld, order, k, t, m, C, r, work, kcap, ab, dout, blockIdx.x, gridDim.x, sh);
 }
 
 // L-BFGS memory update (prox-L-BFGS-SCORE.jl:148-162): γh = ∇q_new − ∇q,
@@ -871,12 +926,11 @@ hipError_t launch_norms3(const double* x, const double* xs, const double* xn, in
 // separate kernels (smooth_elem, tail_eta/apply, lbfgs_update_part, reg_part), so the results
 // are bitwise those of the unfused step.  R holds LQ_NPART rows of TAIL_G partials.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(TAIL_T) void lqn_tail_kernel(const double* __restrict__ x, const double* __restrict__ d,
-                                                          int neg, int64_t m, double Mg, double step, ProxArgs P,
-                                                          const double* __restrict__ hinv, double* __restrict__ x_new,
-                                                          double* __restrict__ dx, double* __restrict__ dh,
-                                                          double* __restrict__ R, double* __restrict__ scal) {
-  __shared__ double sh[TAIL_T / 64];
+__device__ __forceinline__ void lqn_tail_body(const double* __restrict__ x, const double* __restrict__ d, int neg,
+                                              int64_t m, double Mg, double step, const ProxArgs& P,
+                                              const double* __restrict__ hinv, double* __restrict__ x_new,
+                                              double* __restrict__ dx, double* __restrict__ dh,
+                                              double* __restrict__ R, double* __restrict__ scal, double* sh) {
   const double eta = sqrt(fixed_sum(R + LQ_ETA * TAIL_G, TAIL_G, sh));
   const double alpha = step / (1.0 + Mg * eta);
   const double safe_alpha = jl_min(1.0, alpha);
@@ -908,20 +962,77 @@ __global__ __launch_bounds__(TAIL_T) void lqn_tail_kernel(const double* __restri
   }
 }
 
+__global__ __launch_bounds__(TAIL_T) void lqn_tail_kernel(const double* __restrict__ x, const double* __restrict__ d,
+                                                          int neg, int64_t m, double Mg, double step, ProxArgs P,
+                                                          const double* __restrict__ hinv, double* __restrict__ x_new,
+                                                          double* __restrict__ dx, double* __restrict__ dh,
+                                                          double* __restrict__ R, double* __restrict__ scal) {
+  __shared__ double sh[TAIL_T / 64];
+  lqn_tail_body(x, d, neg, m, Mg, step, P, hinv, x_new, dx, dh, R, scal, sh);
+}
+
+// The last workgroup to finish (device-scope counter `cnt`, reset by that workgroup) forms the
+// sums of the partial rows -- the fixed_sum order: lane l adds rows[l], rows[l+64], ... from 0,
+// then the wave butterfly -- and, with a device ring, takes the L-BFGS memory decision
+// (prox-L-BFGS-SCORE.jl:154-162, as lbfgs_accept in scsopt.cpp): accept the pair written to
+// ring[mem+2] (the spare slot) when δhᵀγh > 1e-10; FIFO capped at mem; H0 = δhᵀγh / γhᵀγh.
+// ring = [order[0..mem] | k | spare] on the device.
+__device__ __forceinline__ void lqn_ring_accept(int* __restrict__ ring, int mem, double dg, double gg,
+                                                double* __restrict__ H0) {
+  if (!(dg > 1e-10)) return;
+  const int k = ring[mem + 1], slot = ring[mem + 2];
+  int spare = 0;
+  if (k == mem) {
+    spare = ring[0];
+    for (int i = 0; i + 1 < k; ++i) ring[i] = ring[i + 1];
+    ring[k - 1] = slot;
+  } else {
+    for (int j = 0; j <= mem; ++j) {   // the next unused physical slot
+      bool used = (j == slot);
+      for (int i = 0; i < k; ++i) used |= (ring[i] == j);
+      if (!used) {
+        spare = j;
+        break;
+      }
+    }
+    ring[k] = slot;
+    ring[mem + 1] = k + 1;
+  }
+  ring[mem + 2] = spare;
+  *H0 = dg / gg;
+}
+
 __global__ __launch_bounds__(TAIL_T) void lqn_post_kernel(
     const double* __restrict__ tpart, int nchunk, int64_t ldp, int64_t m, double lam, int skind, double mu,
     const double* __restrict__ sa, const double* __restrict__ sb, ProxArgs P, const double* __restrict__ xs,
     const double* __restrict__ x, const double* __restrict__ xn, const double* __restrict__ gq,
-    const double* __restrict__ dh, double* __restrict__ gqn, double* __restrict__ Sslot, double* __restrict__ Yslot,
-    double* __restrict__ gr, double* __restrict__ Hr, double* __restrict__ hinv, double* __restrict__ R) {
+    const double* __restrict__ dh, double* __restrict__ gqn, double* __restrict__ Sbase, double* __restrict__ Ybase,
+    int64_t lds, int* __restrict__ ring, int mem, int hslot, double* __restrict__ gr, double* __restrict__ Hr,
+    double* __restrict__ hinv, double* __restrict__ R) {
   __shared__ double sh[TAIL_T / 64];
   const bool box = skind == SCS_SMOOTH_PHUBER_INDBOX || skind == SCS_SMOOTH_LOGEXP_INDBOX ||
                    skind == SCS_SMOOTH_EXP_INDBOX;
+  const int64_t slot = ring ? ring[mem + 2] : hslot;
+  double* __restrict__ Sslot = Sbase + slot * lds;
+  double* __restrict__ Yslot = Ybase + slot * lds;
   double dg = 0.0, gg = 0.0, eta = 0.0, reg = 0.0, na = 0.0, nb = 0.0, nc = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)TAIL_T + threadIdx.x; i < m; i += (int64_t)TAIL_G * TAIL_T) {
     // Aᵀr: the partial rows summed as gemv_t_finalize does (4 interleaved accumulators)
+    // (16 partial loads in flight per round: one load round trip per 4 adds was the kernel's time)
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     int c = 0;
+    for (; c + 16 <= nchunk; c += 16) {
+      double t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = tpart[(int64_t)(c + u) * ldp + i];
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        s0 += t[u];
+        s1 += t[u + 1];
+        s2 += t[u + 2];
+        s3 += t[u + 3];
+      }
+    }
     for (; c + 4 <= nchunk; c += 4) {
       s0 += tpart[(int64_t)c * ldp + i];
       s1 += tpart[(int64_t)(c + 1) * ldp + i];
@@ -962,25 +1073,79 @@ __global__ __launch_bounds__(TAIL_T) void lqn_post_kernel(
   }
 }
 
-__global__ __launch_bounds__(64) void lqn_post_final_kernel(ProxArgs P, const double* __restrict__ R,
-                                                            double* __restrict__ scal, int rx_slot, int nrm_slot) {
-  __shared__ double sh[1];
-  const double dg = fixed_sum(R + LQ_DG * TAIL_G, TAIL_G, sh);
-  const double gg = fixed_sum(R + LQ_GG * TAIL_G, TAIL_G, sh);
-  const double rs = fixed_sum(R + LQ_REG * TAIL_G, TAIL_G, sh);
-  const double na = fixed_sum(R + LQ_NA * TAIL_G, TAIL_G, sh);
-  const double nb = fixed_sum(R + LQ_NB * TAIL_G, TAIL_G, sh);
-  const double nc = fixed_sum(R + LQ_NC * TAIL_G, TAIL_G, sh);
-  const double pr = fixed_sum(R + LQ_PRI * TAIL_G, TAIL_G, sh);
-  if (threadIdx.x == 0) {
-    scal[0] = sqrt(pr);
-    scal[16] = dg;
-    scal[17] = gg;
-    scal[rx_slot] = (P.reg == SCS_REG_INDBOX) ? (rs > 0 ? __builtin_inf() : 0.0) : P.lam * rs;
-    scal[nrm_slot] = na;
-    scal[nrm_slot + 1] = nb;
-    scal[nrm_slot + 2] = nc;
+// The sums of lqn_post's partial rows in fixed_sum's order (lane l adds rows[l], rows[l+64], ...
+// from 0, then the wave butterfly), the loss sum of the epilogue's block partials in
+// sum_partials_kernel's order (1024 lane-strided accumulators, their wave sums, the 16 wave sums in
+// order: thread t plays the virtual threads t + 256 j, whose waves are this thread's wave + 4 j),
+// with a device ring the L-BFGS memory decision, and the epoch's scalars into pinned host memory.
+__global__ __launch_bounds__(256) void lqn_post_final_kernel(ProxArgs P, const double* __restrict__ R,
+                                                             const double* __restrict__ valpart, int nval,
+                                                             int* __restrict__ ring, int mem,
+                                                             double* __restrict__ scal, int zf_slot, int rx_slot,
+                                                             int nrm_slot, int h0_slot, double* __restrict__ hmap,
+                                                             int nmap) {
+  __shared__ double sh[16];
+  __shared__ double sr[7];
+  __shared__ double sv[64];   // scal[0..nmap) as this kernel leaves it (nmap <= 64)
+  if (threadIdx.x < nmap) sv[threadIdx.x] = scal[threadIdx.x];
+  if (valpart) {
+    double a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] = 0.0;
+      for (int i = threadIdx.x + 256 * j; i < nval; i += 1024) a[j] += valpart[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double w = wave_sum(a[j]);
+      if ((threadIdx.x & 63) == 0) sh[(threadIdx.x >> 6) + 4 * j] = w;
+    }
   }
+  if (threadIdx.x < 64) {
+    constexpr int rows[7] = {LQ_DG, LQ_GG, LQ_REG, LQ_NA, LQ_NB, LQ_NC, LQ_PRI};
+    constexpr int PER = TAIL_G / 64;
+    double p[7][PER];
+#pragma unroll
+    for (int r = 0; r < 7; ++r)
+#pragma unroll
+      for (int j = 0; j < PER; ++j) p[r][j] = R[rows[r] * TAIL_G + threadIdx.x + 64 * j];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) a += p[r][j];
+      a = wave_sum(a);
+      if (threadIdx.x == 0) sr[r] = a;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double sdg = sr[0], sgg = sr[1], rs = sr[2];
+    auto put = [&](int j, double v) {
+      scal[j] = v;
+      if (j < nmap) sv[j] = v;
+    };
+    put(0, sqrt(sr[6]));
+    put(16, sdg);
+    put(17, sgg);
+    put(rx_slot, (P.reg == SCS_REG_INDBOX) ? (rs > 0 ? __builtin_inf() : 0.0) : P.lam * rs);
+    put(nrm_slot, sr[3]);
+    put(nrm_slot + 1, sr[4]);
+    put(nrm_slot + 2, sr[5]);
+    if (valpart) {
+      double r = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) r += sh[i];
+      put(zf_slot, r);
+    }
+    if (ring) {
+      lqn_ring_accept(ring, mem, sdg, sgg, scal + h0_slot);
+      if (h0_slot < nmap) sv[h0_slot] = scal[h0_slot];
+    }
+  }
+  __syncthreads();
+  // one store per lane into the fine-grained host buffer: visible once the kernel has ended
+  if (threadIdx.x < nmap) hmap[threadIdx.x] = sv[threadIdx.x];
 }
 
 hipError_t launch_lqn_eta(const double* gr, const double* Hr, int64_t m, double lam, double* hinv, double* R,
@@ -1000,13 +1165,15 @@ hipError_t launch_lqn_tail(const double* x, const double* d, int neg, int64_t m,
 
 hipError_t launch_lqn_post(const double* tpart, int nchunk, int64_t ldp, int64_t m, double lam, int skind, double mu,
                            const double* sa, const double* sb, const ProxArgsH& Ph, const double* xs, const double* x,
-                           const double* xn, const double* gq, const double* dh, double* gqn, double* Sslot,
-                           double* Yslot, double* gr, double* Hr, double* hinv, double* R, double* scal, int rx_slot,
-                           int nrm_slot, hipStream_t st) {
+                           const double* xn, const double* gq, const double* dh, double* gqn, double* S, double* Y,
+                           int64_t lds, int* ring, int mem, int slot, double* gr, double* Hr, double* hinv, double* R,
+                           const double* valpart, int nval, double* scal, int zf_slot, int rx_slot, int nrm_slot,
+                           int h0_slot, double* hmap, int nmap, hipStream_t st) {
   ProxArgs P{Ph.reg, 1, Ph.lam, Ph.lam2, Ph.lb, Ph.ub, Ph.gstart, Ph.gend, Ph.gw, Ph.ngroups, Ph.gmap};
   hipLaunchKernelGGL(lqn_post_kernel, dim3(TAIL_G), dim3(TAIL_T), 0, st, tpart, nchunk, ldp, m, lam, skind, mu, sa, sb,
-                     P, xs, x, xn, gq, dh, gqn, Sslot, Yslot, gr, Hr, hinv, R);
-  hipLaunchKernelGGL(lqn_post_final_kernel, dim3(1), dim3(64), 0, st, P, R, scal, rx_slot, nrm_slot);
+                     P, xs, x, xn, gq, dh, gqn, S, Y, lds, ring, mem, slot, gr, Hr, hinv, R);
+  hipLaunchKernelGGL(lqn_post_final_kernel, dim3(1), dim3(256), 0, st, P, R, valpart, nval, ring, mem, scal, zf_slot,
+                     rx_slot, nrm_slot, h0_slot, hmap, nmap);
   return hipGetLastError();
 }
 
@@ -1037,26 +1204,22 @@ hipError_t launch_bb_step(const double* x, const double* xp, const double* g, co
   return hipGetLastError();
 }
 hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
-                           const double* g, int64_t m, double* q, double* d, double* ab, double* work,
-                           hipStream_t st) {
-  if (m <= TWO_LOOP_SINGLE_MAX || k < 1) {
-    hipLaunchKernelGGL(two_loop_kernel, dim3(1), dim3(VB), 0, st, S, Y, ld, order, k, H0, g, m, q, d, ab);
+                           const double* g, int64_t m, double* q, double* d, double* ab, double* work, int kcap,
+                           const int* kp, const double* H0p, hipStream_t st) {
+  // kp: k on the device, `k` its upper bound (launches beyond the device k return at once)
+  if (m <= TWO_LOOP_SINGLE_MAX || (!kp && k < 1)) {
+    hipLaunchKernelGGL(two_loop_kernel, dim3(1), dim3(VB), 0, st, S, Y, ld, order, kp, k, H0p, H0, g, m, q, d, ab);
     return hipGetLastError();
   }
   const int G = (int)std::min<int64_t>(TWO_LOOP_MAX_WG, ceil_div(m, 1024));
   const int64_t C = ceil_div(m, G);
-  double* pys = work;               // [k][G]
-  double* pa = work + (int64_t)k * G;
-  double* pb = pa + G;
-  hipLaunchKernelGGL(tl_init_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, k, g, m, C, q, pys, pa);
-  for (int t = k - 1; t >= 0; --t) {
-    hipLaunchKernelGGL(tl_first_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, t, H0, m, C, q, pys, pa, pb, ab);
-    std::swap(pa, pb);
-  }
-  for (int t = 0; t < k; ++t) {
-    hipLaunchKernelGGL(tl_second_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, t, k, m, C, q, pa, pb, ab, d);
-    std::swap(pa, pb);
-  }
+  hipLaunchKernelGGL(tl_init_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, g, m, C, work, kcap, d);
+  for (int i = 0; i < k; ++i)
+    hipLaunchKernelGGL(tl_first_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, i, H0p, H0, m, C, g, q,
+                       work, kcap, ab);
+  for (int t = 0; t < k; ++t)
+    hipLaunchKernelGGL(tl_second_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, t, m, C, q, work, kcap,
+                       ab, d);
   return hipGetLastError();
 }
 // the same update over TAIL_G workgroups (large m): per-block partial dots, fixed-order sums

@@ -630,6 +630,22 @@ def test_cholesky_lookahead_bit_identical(m, monkeypatch):
     assert np.array_equal(bits(la.x), bits(ser.x))
 
 
+def test_cholesky_diag_pipe_bit_identical(monkeypatch):
+    """The diagonal-block kernel's default schedule (wave 0 factors the next 16 x 16 sub-block while
+    waves 1..3 finish the trailing update) gives every element the same updates in the same order
+    as the phase-serial kernel (SCS_CHOL_DIAG=0): bit-identical ProxNSCORE trajectory (m = 2304:
+    18 diagonal blocks, with the pivot of a non-SPD system reported the same way)."""
+    N, m = 4000, 2304
+    x0 = np.random.default_rng(33).standard_normal(m) * 0.3
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=27)
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    a = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    monkeypatch.setenv("SCS_CHOL_DIAG", "0")
+    b = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    assert a.obj == b.obj and a.pri_res_norm == b.pri_res_norm and a.epochs == b.epochs
+    assert np.array_equal(bits(a.x), bits(b.x))
+
+
 @pytest.mark.parametrize("method,m", [("nscore", 3072), ("ggn", 3200), ("nscore", 4000)])
 def test_pipelined_factor_matches_serial(method, m, monkeypatch):
     """The factor hidden under the Gram (strip-by-strip Gram, left-looking factor on a second
@@ -682,14 +698,17 @@ def test_cholesky_small_gram_bit_identical(m, monkeypatch):
     assert np.array_equal(bits(a.x), bits(b.x))
 
 
-@pytest.mark.parametrize("reg,use_prox", [("l1", True), ("indbox", True), ("l2", False)])
-def test_lqn_fused_epoch_bit_identical(reg, use_prox, monkeypatch):
+@pytest.mark.parametrize("reg,use_prox,m", [("l1", True, 20000), ("indbox", True, 20000), ("l2", False, 20000),
+                                            ("l1", True, 16384)])
+def test_lqn_fused_epoch_bit_identical(reg, use_prox, m, monkeypatch):
     """scs_iterate's fused ProxLQNSCORE epoch (m >= 16384: lqn_tail / lqn_post around the two products)
     against the unfused device loop (SCS_LQN_FUSED=0): identical objective / fval / pri_res_norm
     histories and x bits (same per-element arithmetic, same partial-sum order), rel_error to rounding
     of the norms, through an L-BFGS memory that fills (two-loop recursion active) and a run that
-    stops on x_tol."""
-    N, m = 256, 20000
+    stops on x_tol.  The fused loop is pipelined one epoch deep with the ring on the device (the
+    two-loop's launches for an upper bound of k, surplus ones returning at once; m = 16384 takes
+    the one-workgroup two-loop), and the x_tol run stops with an epoch enqueued past the stop."""
+    N = 256
     rng = np.random.default_rng(12)
     A = rng.standard_normal((N, m)) / np.sqrt(m)
     y = rng.standard_normal(N)

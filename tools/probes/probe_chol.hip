@@ -11,7 +11,7 @@
   printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
 namespace scs {
-__global__ void chol_diag_kernel(double* G, int64_t ld, int k, double* W, int* info);
+hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st);
 #ifdef CHOL_PROF
 extern __device__ long long chol_prof[64];
 #endif
@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
     CK(hipMemset(info, 0, 4));
     CK(hipEventRecord(e0));
-    for (int k = 0; k < 64; ++k) hipLaunchKernelGGL(scs::chol_diag_kernel, dim3(1), dim3(256), 0, 0, G, n, k, W, info);
+    for (int k = 0; k < 64; ++k) CK(scs::launch_chol_diag(G, n, k, W, info, 0));
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
     printf("n=%ld diag kernel: %.1f us/launch\n", (long)n, ms * 1000 / 64);
 #ifdef CHOL_PROF
