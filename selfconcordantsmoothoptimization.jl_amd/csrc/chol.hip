@@ -162,7 +162,10 @@ __device__ __forceinline__ void chol_inv_double_mfma(double* su, int tid) {
 // Phase A: wave 0 factors the 16 x 16 diagonal sub-block at o in registers (lane c = column c;
 // lanes 16..63 mirror lanes 0..15), reciprocal pivots to srinv.
 __device__ __forceinline__ void diag_factor16(double* su, double* srinv, int o, int k, int* info, int tid) {
-  const int c = tid & 15;
+  int c = tid & 15;
+  // opaque per call: keeps the compiler from hoisting the 32 lane masks (c > j, c == j) out of the
+  // inner-block loop into SGPR pairs it then spills to VGPR lanes (v_writelane / v_readlane)
+  asm volatile("" : "+v"(c));
   double a[SB];
 #pragma unroll
   for (int i = 0; i < SB; ++i) a[i] = su[(o + c) * CLD + o + i];   // S(o+i, o+c); zero below the diagonal
@@ -196,12 +199,14 @@ __device__ __forceinline__ void diag_panel16(double* su, const double* srinv, in
     double X[SB];
 #pragma unroll
     for (int u = 0; u < SB; ++u) X[u] = su[c * CLD + o + u];
+    // right-looking: X[t] takes D(u, t) X[u] as soon as X[u] is final -- the same fused
+    // multiply-subtracts in the same u order as the dot-product form (bit-identical), but the
+    // dependent chain is 16 x (fma + mul) instead of all 120 fmas in a row
 #pragma unroll
-    for (int t = 0; t < SB; ++t) {
-      double sacc = X[t];
+    for (int u = 0; u < SB; ++u) {
+      X[u] *= srinv[o + u];
 #pragma unroll
-      for (int u = 0; u < t; ++u) sacc -= su[(o + t) * CLD + o + u] * X[u];
-      X[t] = sacc * srinv[o + t];
+      for (int t = u + 1; t < SB; ++t) X[t] -= su[(o + t) * CLD + o + u] * X[u];
     }
 #pragma unroll
     for (int u = 0; u < SB; ++u) su[c * CLD + o + u] = X[u];
@@ -252,18 +257,18 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   }
   // inverse of the (final) 16 x 16 diagonal block kb by one wave (lane c = column c)
   auto inv16 = [&](int kb) {
-    const int o = kb * SB, c = tid & 15;
-    double a[SB], w[SB];
+    // U(o+i, o+t) as a wave-uniform LDS read (broadcast), not v_readlane of a register copy: the
+    // 120 independent readlanes were hoisted into SGPRs and spilled to VGPR lanes
+    const int o = kb * SB;
+    const int c = tid & 15;
+    double w[SB];
 #pragma unroll
-    for (int i = 0; i < SB; ++i) {
-      a[i] = su[(o + c) * CLD + o + i];
-      w[i] = (i == c) ? 1.0 : 0.0;
-    }
+    for (int i = 0; i < SB; ++i) w[i] = (i == c) ? 1.0 : 0.0;
 #pragma unroll
     for (int t = SB - 1; t >= 0; --t) {
       w[t] *= srinv[o + t];
 #pragma unroll
-      for (int i = 0; i < t; ++i) w[i] -= readlane_d(a[i], t) * w[t];
+      for (int i = 0; i < t; ++i) w[i] -= su[(o + t) * CLD + o + i] * w[t];
     }
     if ((tid & 63) < SB) {
 #pragma unroll
@@ -297,6 +302,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
         diag_trail_tile(su, o, 0, lane);
         diag_factor16(su, srinv, o + SB, k, info, tid);
       } else {
+        if (wv == 1 + kb % 3) inv16(kb);   // U_kb,kb is final: its inverse beside the update
         for (int id = wv; id < ntl; id += DNT / 64 - 1) diag_trail_tile(su, o, id, lane);
       }
     } else {
@@ -310,8 +316,13 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
     const int c = e >> 7, r = e & 127;
     if (r <= c) blk[(int64_t)c * ld + r] = su[c * CLD + r];
   }
-  // (running inv16 beside phase B on the idle last wave measured slower: B waits for it)
-  for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) inv16(kb);
+  // (running inv16 beside phase B on the idle last wave measured slower: B waits for it; PIPE runs
+  // inv16(kb) beside C(kb), so only the last block's is left)
+  if (PIPE) {
+    if (wv == DNT / 64 - 1) inv16(CB / SB - 1);
+  } else {
+    for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) inv16(kb);
+  }
   __syncthreads();   // storeU has read the diagonal blocks; swinv complete
   // ---- diagonal 16 x 16 inverses into the diagonal blocks of S (start of the doubling)
   for (int e = tid; e < CB * SB; e += DNT) {

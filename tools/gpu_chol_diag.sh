@@ -12,3 +12,5 @@ for rep in 1 2; do
     python3 -c "import json; d=json.loads(open('$O/c2_d$d.json').read().strip().splitlines()[-1]); print('diag=$d', round(d['value'],3), d['breakdown_ms_per_step'])"
   done
 done
+timeout -k 10 120 ./tools/probes/bin/probe_chol_prof > $O/prof.log 2>&1 || { echo "prof failed"; tail $O/prof.log; exit 1; }
+grep -E "diag kernel|load|factor:" $O/prof.log
