@@ -8,8 +8,8 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --ti
 tail -1 $O/pytest.log
 for rep in 1 2; do
   for d in 0 1; do
-    SCS_CHOL_DIAG=$d timeout -k 10 300 python3 bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-check > $O/c2_d$d.json 2> $O/c2_d$d.err || { echo "bench failed"; tail $O/c2_d$d.err; exit 1; }
-    python3 -c "import json; d=json.loads(open('$O/c2_d$d.json').read().strip().splitlines()[-1]); print('diag=$d', round(d['value'],3), d['breakdown_ms_per_step'])"
+    SCS_CHOL_ILA=$d timeout -k 10 300 python3 bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-check > $O/c2_d$d.json 2> $O/c2_d$d.err || { echo "bench failed"; tail $O/c2_d$d.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/c2_d$d.json').read().strip().splitlines()[-1]); print('ila=$d', round(d['value'],3), d['breakdown_ms_per_step'])"
   done
 done
 timeout -k 10 120 ./tools/probes/bin/probe_chol_prof > $O/prof.log 2>&1 || { echo "prof failed"; tail $O/prof.log; exit 1; }
