@@ -376,6 +376,9 @@ def main():
         print(json.dumps(line))
         if check is not None and not check["pass"]:
             raise SystemExit("sampled full-size Gram / Aᵀv check FAILED: " + json.dumps(check))
+    # release the library context (its streams, a CU-masked one included) before the runtime and
+    # any profiler tear down, instead of leaving it to interpreter-exit finalizers
+    ctx.close()
     if comm is not None:
         dist.destroy_process_group()
 

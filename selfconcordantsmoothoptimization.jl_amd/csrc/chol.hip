@@ -376,16 +376,18 @@ static int outer_block();
 
 // The bulk stream (the lookahead's trailing updates, 2 gram_sia workgroups per CU fill every CU
 // they get) can leave SCS_CHOL_RESERVE_CUS CUs (a multiple of 8: that many / 8 per XCD) to the
-// serial chain on the context stream.  A chol_diag_kernel workgroup that shares its CU with
-// MFMA-bound trailing-update waves runs ~7x slower (m = 32768, before the chain was cut down to
-// Ba / C1a: 682 us against 94 us alone, and the 256-long chain bounded the factor).  With the
-// current split the chain has slack and the reserve no longer pays (m = 32768 factor + solves
-// 220.6 / 224.2 / 223.2 ms at 0 / 8 / 16 reserved CUs; m = 8192 13.0 / 12.8 / 12.5 ms), and
-// rocprofv3 segfaults at exit on a process that created a CU-masked stream, so the default is
-// 0 (an ordinary non-blocking stream).  Masking is best effort: a failure falls back too.
-static hipError_t create_bulk_stream(hipStream_t* s) {
+// serial chain on the context stream.  A chain kernel that shares its CU with MFMA-bound
+// trailing-update waves runs slower: in an m = 8192 kernel trace the latency Gram launches take
+// 9.3 us alone and 28.7 us while the bulk update runs, the diagonal kernel 77.5 / 111.2 us
+// (profiles/r02/chol/).  r02 sweep with the r02 diagonal kernel (profiles/r02/chol/reserve/):
+// m = 8192 solve 12.04 / 10.97 / 11.53 / 10.98 ms at 0 / 32 / 48 / 64 reserved CUs, m = 16384
+// 42.1 / 40.2 / 43.8 / 43.1 ms, m = 32768 216.7 / 220.3 ms at 0 / 32 -- so 32 up to m = 16384,
+// none above.  (rocprofv3 segfaults at exit, after writing its output, in a process that created
+// a CU-masked stream; profile runs go last in a GPU call.)  Masking is best effort: a failure
+// falls back to an ordinary non-blocking stream.
+static hipError_t create_bulk_stream(hipStream_t* s, int nblk) {
   const char* env = getenv("SCS_CHOL_RESERVE_CUS");
-  const int reserve = env ? atoi(env) : 0;
+  const int reserve = env ? atoi(env) : (nblk <= 128 ? 32 : 0);
   int dev = 0, ncu = 0;
   if (reserve > 0 && hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 4 * reserve) {
@@ -413,7 +415,7 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipMalloc(&a->rect, sizeof(int2) * rl.size());
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = create_bulk_stream(&a->st2);
+  if (e == hipSuccess) e = create_bulk_stream(&a->st2, nblk);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev2, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev3, hipEventDisableTiming);
