@@ -408,7 +408,7 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   std::vector<double> hw((size_t)CB + mpad, -1.0);
   for (int i = 0; i < CB; ++i) hw[i] = 1.0;
   std::vector<int2> rl;
-  for (int R = 1; R <= 4; ++R)
+  for (int R = 1; R <= 8; ++R)
     for (int j = 0; j < nblk; ++j)
       for (int i = 0; i < R; ++i) rl.push_back(make_int2(i, j));   // bj-major: first R*C = R x C rectangle
   hipError_t e = hipMalloc(&a->w, sizeof(double) * hw.size());
@@ -447,12 +447,22 @@ void chol_aux_free(CholAux* a) {
 static const int2* rect_list(const CholAux* a, int R) { return a->rect + (int64_t)a->nblk * (R - 1) * R / 2; }
 int chol_outer_block();
 
+// Outer block (inner 128-blocks per outer step) of chol_factor: SCS_CHOL_OB (1..16, read per call),
+// else 8.  (16 at m = 32768, where the bulk stream's K = 1024 trailing updates bound the factor,
+// measured slower: C4-half cached solve 221.5 -> 229.8 ms, profiles/r02/chol/ob16/.)  The
+// strip-solve recursion needs rectangle lists of up to OB/2 block rows (chol_aux_init: R <= 8).
+static int outer_block_for(int nblk) {
+  (void)nblk;
+  const char* e = getenv("SCS_CHOL_OB");
+  const int v = e ? atoi(e) : 8;
+  return v < 1 ? 1 : (v > 16 ? 16 : v);
+}
+
+// the strip pipeline's outer strip (SCS_CHOL_PIPE): 8, or SCS_CHOL_OB up to 8
 static int outer_block() {
   static const int ob = [] {
     const char* e = getenv("SCS_CHOL_OB");
     const int v = e ? atoi(e) : 8;
-    // the strip-solve recursion needs rectangle lists of up to OB/2 block rows (chol_aux_init
-    // builds R <= 4), so OB is capped at 8
     return v < 1 ? 1 : (v > 8 ? 8 : v);
   }();
   return ob;
@@ -500,7 +510,7 @@ static bool chol_lookahead() {
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* a,
                        const int2* trilist, int* info, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
-  const int OB = outer_block();
+  const int OB = outer_block_for(nblk);
   const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
   bool c12_pending = false;
   hipError_t e = hipSuccess;

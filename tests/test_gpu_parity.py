@@ -613,12 +613,15 @@ def test_fused_gram_atv_matches_separate_pass(method, m, tall, monkeypatch):
     np.testing.assert_allclose(fused.x, osol.x, rtol=1e-6, atol=1e-9)
 
 
-@pytest.mark.parametrize("m", [2304, 3200])
-def test_cholesky_lookahead_bit_identical(m, monkeypatch):
+@pytest.mark.parametrize("m,ob", [(2304, None), (3200, None), (4608, "16")])
+def test_cholesky_lookahead_bit_identical(m, ob, monkeypatch):
     """The factor's lookahead (next outer block's diagonal steps overlapping the rest of the trailing
     update on a second stream) keeps every element's update order, so the ProxNSCORE trajectory is
     bit-identical to the serial order (SCS_CHOL_LA=0); m = 2304 / 3200: 18 / 25 inner blocks, i.e.
-    2-3 outer blocks with a lookahead split and a short last block."""
+    2-3 outer blocks with a lookahead split and a short last block; m = 4608 with 16-block outer
+    steps (the default from m = 32768 on: strip solves over 16 block rows, K = 2048 updates)."""
+    if ob:
+        monkeypatch.setenv("SCS_CHOL_OB", ob)
     N = 4000
     x0 = np.random.default_rng(31).standard_normal(m) * 0.3
     p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=23)
