@@ -527,7 +527,7 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     const double* __restrict__ A, int64_t S, const double* __restrict__ w, int64_t k0, int64_t Nk,
     const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int flags,
     const int4* __restrict__ work, int seglen, int nsplit, double* __restrict__ P,
-    const double* __restrict__ v, double* __restrict__ VP, int64_t vps) {
+    const double* __restrict__ v, double* __restrict__ VP, int64_t vps, unsigned* __restrict__ scnt, int sob) {
   static_assert(!(AV && CM), "the fused Aᵀv runs on the panel-blocked A only");
   constexpr int GTI = 64 * TI;        // tile rows (A1 features)
   constexpr int NT = 128 * TI;        // threads
@@ -752,6 +752,13 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
         if (accumulate) *dst += acc[ti][tj][r];
         else *dst = acc[ti][tj][r];
       }
+  // strip completion (scsopt.cpp gram_factor_pipelined, one-launch mode): this tile's rows lie in
+  // outer strip bj / sob; each thread's stores are released to device scope before one count
+  if (scnt && part < 0) {
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) atomicAdd(scnt + bj / sob, 1u);
+  }
 }
 
 // Main-Gram kernel selection (A/B switches, read once):
@@ -807,10 +814,10 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
     if (!gram_fuse_ok(tall)) return hipErrorInvalidValue;
     if (tall)
       hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0,
-                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps);
+                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
     else
       hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0,
-                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps);
+                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
     return hipGetLastError();
   }
   if (!tall && gram_sia_mode() == 0)
@@ -818,10 +825,10 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
                        (int64_t)0, Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   else if (!tall)
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   else if (gram_tall_mode() == 3)
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   else
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -959,7 +966,7 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
   if (k1 - k0 <= 512 && (k1 - k0) % (8 * GBK) == 0 && k1 > k0 && ntiles <= small_max) return gram_launch_small(A1, lda1, A2, lda2, w, k0, k1, tiles, ntiles, G, ldg, flags, st);
   if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)   // the Cholesky's trailing updates
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -972,13 +979,13 @@ hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
   if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
     hipLaunchKernelGGL((noload == 16 ? gram_sia_kernel<1, 4> : gram_sia_kernel<3, 4>), dim3(ntiles), dim3(512), 0,
-                       st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
+                       st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   else if (noload == 12)
     hipLaunchKernelGGL((gram_sia_kernel<3>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   else if (noload == 9 || noload == 10)
     hipLaunchKernelGGL((noload == 9 ? gram_sia_kernel<1> : gram_sia_kernel<0>), dim3(ntiles), dim3(256), 0, st, A,
-                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0);
+                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   else if (noload == 11)
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, A,
                        (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -1029,20 +1036,23 @@ __global__ void gram_combine_kernel(const double* __restrict__ P, const int4* __
 // Scheduled main Gram (gram_schedule's work list + tail combine).
 hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
-                             int tall, hipStream_t st, const double* v, double* VP, int64_t vps) {
+                             int tall, hipStream_t st, const double* v, double* VP, int64_t vps, unsigned* scnt,
+                             int sob) {
+  if (scnt && !(gram_fuse_ok(tall) || (tall ? gram_tall_mode() == 3 : gram_sia_mode() == 1)))
+    return hipErrorInvalidValue;   // strip counts come from the interleaved kernels only
   // packed: bit 0 = packed slots (else the upper triangle), bit 1 = accumulate into G
   const int flags = ((packed & 1) ? GRAM_PACKED : GRAM_UPPER) | ((packed & 2) ? GRAM_ACCUMULATE : 0);
   const int glds = gram_tall_mode();
   if (v && !gram_fuse_ok(tall)) return hipErrorInvalidValue;
   if (v && tall)
     hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w,
-                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps);
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
   else if (v)
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w,
-                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps);
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
   else if (tall && glds == 3)
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk,
-                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
+                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
   else if (tall && glds == 2)
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
                        Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
@@ -1054,10 +1064,10 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   else if (gram_sia_mode() == 1)
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr,
-                       0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
+                       0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
   else if (gram_sia_mode() == 2)
     hipLaunchKernelGGL((gram_sia_kernel<0>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr, 0,
-                       G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
+                       G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
@@ -1070,6 +1080,27 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
   return hipGetLastError();
 }
 
+// The factor stream's wait for strip s of a one-launch Gram: one lane polls the strip's count
+// (device-scope acquire) until it reaches `target`, sleeping between polls; a wait longer than
+// ~30 s (100 MHz s_memrealtime) sets *flag and returns, so the grid always drains (the caller
+// then fails the step instead of factoring an incomplete strip).
+__global__ void strip_wait_kernel(const unsigned* __restrict__ cnt, unsigned target, int* __restrict__ flag) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(16);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+      __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
+
+hipError_t strip_wait_launch(const unsigned* cnt, unsigned target, int* flag, hipStream_t st) {
+  hipLaunchKernelGGL(strip_wait_kernel, dim3(1), dim3(64), 0, st, cnt, target, flag);
+  return hipGetLastError();
+}
+
 // Column-major scheduled form (the Cholesky's left-looking strip updates: long K, few tiles):
 // gram_sia_kernel<CM> over the work list, K rows [k0, k1) of X, then the combine.  flags: GRAM_*
 // with GRAM_UPPER placement (GRAM_ACCUMULATE adds into G).
@@ -1078,7 +1109,7 @@ hipError_t gram_launch_sched_cm(const double* X, int64_t ld, const double* w, in
                                 int flags, hipStream_t st) {
   if (seglen <= 0 || k1 <= k0) return hipSuccess;
   hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(8 * seglen), dim3(256), 0, st, X, ld, w, k0, k1, nullptr, 0,
-                     G, ldg, flags | GRAM_UPPER, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0);
+                     G, ldg, flags | GRAM_UPPER, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, nullptr, 0);
   if (ncomb > 0)
     hipLaunchKernelGGL(gram_combine_kernel<2>, dim3(16, ncomb), dim3(256), 0, st, P, comb, nsplit, G, ldg,
                        (flags & GRAM_ACCUMULATE) ? 2 : 0);

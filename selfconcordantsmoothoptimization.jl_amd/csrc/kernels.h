@@ -53,7 +53,10 @@ int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<
 hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
                              int tall, hipStream_t st, const double* v = nullptr, double* VP = nullptr,
-                             int64_t vps = 0);
+                             int64_t vps = 0, unsigned* scnt = nullptr, int sob = 0);
+// scnt: per-strip completion counts (each finished whole tile adds 1 to scnt[bj / sob]); the
+// factor stream waits for a strip with strip_wait_launch (flag: set on a timed-out wait)
+hipError_t strip_wait_launch(const unsigned* cnt, unsigned target, int* flag, hipStream_t st);
 hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,
                               hipStream_t st);
 

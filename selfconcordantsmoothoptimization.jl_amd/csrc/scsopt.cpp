@@ -201,6 +201,13 @@ struct scs_ctx {
     int seglen = 0, nsplit = 1, ncomb = 0;
   };
   std::vector<GStrip> gstrip;
+  // the one-launch form (SCS_CHOL_PIPE=2): every strip's tiles in one scheduled launch, each XCD's
+  // segment strip-major (its share of strip 0, then of strip 1, ...), K-split pieces in the last
+  // strip only; whole tiles count into gp_cnt[strip], gp_target[s] = whole tiles of strip s
+  GStrip gpipe;
+  std::vector<unsigned> gp_target;
+  unsigned* gp_cnt = nullptr;
+  int* gp_flag = nullptr;
   int vpieces = 1;           // rows of vpart
   hipStream_t sf = nullptr;
   std::vector<hipEvent_t> evstrip;
@@ -616,6 +623,66 @@ void ensure_gram(scs_ctx* c) {
       }
       npart_max = std::max(npart_max, npart);
       c->vpieces = std::max(c->vpieces, nsplit);
+    }
+    // the one-launch schedule: strips 0 .. ns-2 cut into 8 contiguous per-XCD chunks (no split),
+    // the last strip as gram_schedule lays it out (tail pieces + combine items)
+    {
+      const int slots = 32 * (c->tall ? 1 : 2);
+      std::vector<std::vector<int4>> seg(8);
+      c->gp_target.assign(ns, 0u);
+      std::vector<int4> cbl;
+      int nsplit = 1, npart = 0;
+      for (int s2 = 0; s2 < ns; ++s2) {
+        std::vector<int2> st;
+        std::vector<int> ix;
+        for (int t = 0; t < nt; ++t)
+          if (tl[t].y / OB == s2) {
+            st.push_back(tl[t]);
+            ix.push_back(t);
+          }
+        const int n = (int)st.size();
+        if (s2 + 1 < ns) {
+          c->gp_target[s2] = (unsigned)n;
+          const int q = n / 8, r = n % 8;
+          int t0 = 0;
+          for (int x = 0; x < 8; ++x) {
+            const int nx = q + (x < r ? 1 : 0);
+            for (int i = 0; i < nx; ++i) seg[x].push_back(make_int4(st[t0 + i].x, st[t0 + i].y, -1, ix[t0 + i]));
+            t0 += nx;
+          }
+        } else {
+          std::vector<int4> wk;
+          const int sl = gram_schedule(st.data(), n, slots, wk, cbl, &nsplit, &npart);
+          for (int x = 0; x < 8; ++x)
+            for (int i = 0; i < sl; ++i) {
+              int4 it = wk[(size_t)x * sl + i];
+              if (it.x < 0) continue;
+              if (it.z < 0) it.w = ix[it.w];   // whole tile: its canonical index
+              seg[x].push_back(it);
+            }
+          for (auto& cb : cbl) cb.z = ix[cb.z];
+        }
+      }
+      size_t seglen = 0;
+      for (auto& v : seg) seglen = std::max(seglen, v.size());
+      std::vector<int4> wk(8 * seglen, make_int4(-1, -1, -1, -1));
+      for (int x = 0; x < 8; ++x)
+        for (size_t i = 0; i < seg[x].size(); ++i) wk[x * seglen + i] = seg[x][i];
+      scs_ctx::GStrip& g = c->gpipe;
+      g.seglen = (int)seglen;
+      g.nsplit = nsplit;
+      g.ncomb = (int)cbl.size();
+      g.work = dalloc<int4>(c, wk.size());
+      HCK(hipMemcpyAsync(g.work, wk.data(), sizeof(int4) * wk.size(), hipMemcpyHostToDevice, c->st));
+      if (!cbl.empty()) {
+        g.comb = dalloc<int4>(c, cbl.size());
+        HCK(hipMemcpyAsync(g.comb, cbl.data(), sizeof(int4) * cbl.size(), hipMemcpyHostToDevice, c->st));
+      }
+      npart_max = std::max(npart_max, npart);
+      c->vpieces = std::max(c->vpieces, nsplit);
+      c->gp_cnt = dalloc<unsigned>(c, ns);
+      c->gp_flag = dalloc<int>(c, 1);
+      HCK(hipMemsetAsync(c->gp_flag, 0, sizeof(int), c->st));
     }
     if (npart_max > 0) {
       const size_t need = (size_t)npart_max * (c->tall ? 256 : 128) * 128;
@@ -1058,9 +1125,14 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
 // the pipelined path's solve: the factor (and Gc) are already enqueued (gram_factor_pipelined,
 // which opened the T_SOLVE interval at the end of the Gram)
 void solve_factored(scs_ctx* c, double* rhs, hipEvent_t e0) {
-  int info = 0;
+  int info = 0, late = 0;
   HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  if (c->gp_flag) HCK(hipMemcpyAsync(&late, c->gp_flag, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
+  if (late) {
+    HCK(hipMemsetAsync(c->gp_flag, 0, sizeof(int), c->st));
+    fail(c, SCS_ERR_STATE, "pipelined factor: a strip wait timed out (the strip was factored incomplete)");
+  }
   if (info == 0) {
     HCK(chol_solve(c->G, c->mpad, c->mpad, c->W, rhs, c->ysol, c->st));
     c->lu_fallback_used = false;
@@ -1235,9 +1307,21 @@ void gram_and_reduce(scs_ctx* c, const double* w, const double* v, double* vec_d
 // factor's workgroups share CUs with MFMA-bound Gram waves (the left-looking updates ran at ~11 %
 // of their alone rate).  At C3 (16 strips of 256 x 128 tiles) the partial rounds alone would cost
 // seconds.  Hiding the factor needs the one-launch Gram with per-strip completion counters.
+// SCS_CHOL_PIPE=2: ONE scheduled Gram launch whose per-XCD segments run the strips in order and
+// count each finished tile into its strip; the factor stream waits for a strip's count
+// (strip_wait_kernel) instead of an event after a per-strip launch, so the Gram keeps whole
+// rounds.  (gram_factor_pipelined)
+int pipe_mode(const scs_ctx* c, bool cacheable) {
+  const char* e = std::getenv("SCS_CHOL_PIPE");   // read per step (tests toggle it in-process)
+  const int mode = e ? std::atoi(e) : 0;
+  const int64_t nblk = c->mpad / 128;
+  const bool ok = !cacheable && !sharded(c) && !sparse_streams(const_cast<scs_ctx*>(c)) && c->gwork &&
+                  nblk >= 3 * chol_outer_block();
+  return ok && (mode == 1 || mode == 2) ? mode : 0;
+}
 bool pipe_ok(const scs_ctx* c, bool cacheable) {
   const char* e = std::getenv("SCS_CHOL_PIPE");   // read per step (tests toggle it in-process)
-  const bool on = e && e[0] == '1';
+  const bool on = e && (e[0] == '1' || e[0] == '2');
   const int64_t nblk = c->mpad / 128;
   return on && !cacheable && !sharded(c) && !sparse_streams(const_cast<scs_ctx*>(c)) && c->gwork &&
          nblk >= 3 * chol_outer_block();
@@ -1263,23 +1347,35 @@ hipEvent_t gram_factor_pipelined(scs_ctx* c, const double* w, const double* v, d
   const double* A = dense_A(c);
   if (fuse && c->vpieces > 1) HCK(hipMemsetAsync(c->vpart, 0, sizeof(double) * c->vpieces * ld, c->st));
   HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+  const bool one = pipe_mode(c, false) == 2;
+  if (one) HCK(hipMemsetAsync(c->gp_cnt, 0, sizeof(unsigned) * ns, c->st));
   hipEvent_t e0;
   tbegin(c, T_GRAM, &e0);
   // the factor stream starts after everything already on st (weights, smoother, info reset)
   HCK(hipEventRecord(c->evstrip[ns], c->st));
   HCK(hipStreamWaitEvent(c->sf, c->evstrip[ns], 0));
-  for (int s2 = 0; s2 < ns; ++s2) {
-    const scs_ctx::GStrip& g = c->gstrip[s2];
+  if (one) {
+    const scs_ctx::GStrip& g = c->gpipe;
     HCK(gram_launch_sched(A, c->nstage, w, c->Npad, g.work, g.seglen, g.nsplit, g.comb, g.ncomb, c->gpart, c->G, ld,
-                          0, c->tall, c->st, fuse ? v : nullptr, c->vpart, ld));
-    HCK(hipEventRecord(c->evstrip[s2], c->st));
+                          0, c->tall, c->st, fuse ? v : nullptr, c->vpart, ld, c->gp_cnt, OB));
+    HCK(hipEventRecord(c->evstrip[ns - 1], c->st));   // the last strip (and its combined pieces)
+  } else {
+    for (int s2 = 0; s2 < ns; ++s2) {
+      const scs_ctx::GStrip& g = c->gstrip[s2];
+      HCK(gram_launch_sched(A, c->nstage, w, c->Npad, g.work, g.seglen, g.nsplit, g.comb, g.ncomb, c->gpart, c->G, ld,
+                            0, c->tall, c->st, fuse ? v : nullptr, c->vpart, ld));
+      HCK(hipEventRecord(c->evstrip[s2], c->st));
+    }
   }
   tend(c, T_GRAM, e0);
   hipEvent_t es;
   tbegin(c, T_SOLVE, &es);   // the solve's share of the step: what runs after the Gram
   if (fuse) HCK(gram_vfinal_launch(c->vpart, c->vpieces, ld, m, vec_dev, c->st));
   for (int s2 = 0; s2 < ns; ++s2) {
-    HCK(hipStreamWaitEvent(c->sf, c->evstrip[s2], 0));
+    if (one && s2 + 1 < ns)
+      HCK(strip_wait_launch(c->gp_cnt + s2, c->gp_target[s2], c->gp_flag, c->sf));
+    else
+      HCK(hipStreamWaitEvent(c->sf, c->evstrip[s2], 0));
     const int64_t r0 = (int64_t)s2 * OB * 128, r1 = std::min<int64_t>((int64_t)(s2 + 1) * OB * 128, ld);
     if (r0 < m) HCK(launch_diag_add(c->G + r0 * ld + r0, ld, std::min(r1, m) - r0, c->lam, c->Hr + r0, c->sf));
     HCK(chol_diag_pad(c->G, ld, std::max(r0, m), r1, c->sf));

@@ -649,10 +649,12 @@ def test_cholesky_diag_pipe_bit_identical(monkeypatch):
     assert np.array_equal(bits(a.x), bits(b.x))
 
 
-@pytest.mark.parametrize("method,m", [("nscore", 3072), ("ggn", 3200), ("nscore", 4000)])
-def test_pipelined_factor_matches_serial(method, m, monkeypatch):
+@pytest.mark.parametrize("method,m,mode", [("nscore", 3072, "1"), ("ggn", 3200, "1"), ("nscore", 4000, "1"),
+                                           ("nscore", 3072, "2"), ("ggn", 3200, "2"), ("nscore", 4000, "2")])
+def test_pipelined_factor_matches_serial(method, m, mode, monkeypatch):
     """The factor hidden under the Gram (strip-by-strip Gram, left-looking factor on a second
-    stream, SCS_CHOL_PIPE=1, opt-in) against the classic one-launch Gram + right-looking factor
+    stream; SCS_CHOL_PIPE=1: one Gram launch per strip, 2: one launch whose tiles count into their
+    strips, the factor stream polling the counts) against the classic Gram + right-looking factor
     (the default): the same system and factor up to the summation order of the updates, so the
     trajectories agree to rounding (and both to the oracle).  m = 3072 / 3200 / 4000: 3 / 4 / 4
     outer strips, the last two partial."""
@@ -667,7 +669,7 @@ def test_pipelined_factor_matches_serial(method, m, monkeypatch):
         of = O.Loss("least_squares", 1.0 / N)
     p = scsopt.Problem.synthetic(N, m, x0, f, 1e-3, kind=kind, seed=43, out_fn=out)
     hm = scsopt.PHuberSmootherL1L2(1.0)
-    monkeypatch.setenv("SCS_CHOL_PIPE", "1")
+    monkeypatch.setenv("SCS_CHOL_PIPE", mode)
     a = scsopt.iterate(M(), p, "l1", hm, max_epoch=4, verbose=0)
     monkeypatch.setenv("SCS_CHOL_PIPE", "0")
     b = scsopt.iterate(M(), p, "l1", hm, max_epoch=4, verbose=0)
