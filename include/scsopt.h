@@ -310,6 +310,9 @@ int scs_gram_atv_eval(scs_ctx* ctx, const double* w, const double* v, const int6
                       double* gvals, double* atv, int* fused);
 
 /* ---- timing ------------------------------------------------------------- */
+/* on = 0: off; 1: HIP events around every Gram / product / solve / step; n > 1: in
+ * scs_iterate's pipelined ProxLQNSCORE loop only every n-th epoch's launches are bracketed
+ * (each event record costs a dispatch gap), everything else as for 1.                      */
 int scs_timing_enable(scs_ctx* ctx, int on);
 int scs_timing_get(scs_ctx* ctx, scs_timing* out);
 int scs_timing_reset(scs_ctx* ctx);
