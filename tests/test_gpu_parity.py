@@ -703,6 +703,31 @@ def test_cholesky_small_gram_bit_identical(m, monkeypatch):
     assert np.array_equal(bits(a.x), bits(b.x))
 
 
+@pytest.mark.parametrize("mem,max_epoch,x_tol", [(1, 9, 0.0), (3, 1, 0.0), (2, 60, 1e-3)])
+def test_lqn_pipelined_loop_edges(mem, max_epoch, x_tol, monkeypatch):
+    """Edges of the pipelined ProxLQNSCORE loop against the unfused device loop, bit for bit: a
+    one-pair memory (the device ring full from its first acceptance: FIFO replace every step), a
+    single epoch (nothing enqueued past it), and an x_tol stop with a small memory."""
+    N, m = 192, 17000
+    rng = np.random.default_rng(5)
+    A = rng.standard_normal((N, m)) / np.sqrt(m)
+    y = rng.standard_normal(N)
+    x0 = rng.standard_normal(m) * 0.1
+    p = scsopt.Problem(A, y, x0, losses.least_squares(1.0 / N), 1e-4)
+    hm = scsopt.PHuberSmootherL1L2(0.5)
+    monkeypatch.delenv("SCS_LQN_FUSED", raising=False)
+    a = scsopt.iterate(scsopt.ProxLQNSCORE(m=mem), p, "l1", hm, max_epoch=max_epoch, x_tol=x_tol, f_tol=0.0,
+                       verbose=0)
+    monkeypatch.setenv("SCS_LQN_FUSED", "0")
+    b = scsopt.iterate(scsopt.ProxLQNSCORE(m=mem), p, "l1", hm, max_epoch=max_epoch, x_tol=x_tol, f_tol=0.0,
+                       verbose=0)
+    assert a.epochs == b.epochs and len(a.obj) == len(b.obj)
+    assert a.obj == b.obj and a.fval == b.fval
+    pr = lambda s: np.array([np.nan if v is None else v for v in s.pri_res_norm])   # `nothing` / NaN entries
+    assert np.array_equal(pr(a), pr(b), equal_nan=True)
+    assert np.array_equal(bits(a.x), bits(b.x))
+
+
 @pytest.mark.parametrize("reg,use_prox,m", [("l1", True, 20000), ("indbox", True, 20000), ("l2", False, 20000),
                                             ("l1", True, 16384)])
 def test_lqn_fused_epoch_bit_identical(reg, use_prox, m, monkeypatch):
