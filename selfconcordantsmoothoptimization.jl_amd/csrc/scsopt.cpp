@@ -1319,13 +1319,7 @@ int pipe_mode(const scs_ctx* c, bool cacheable) {
                   nblk >= 3 * chol_outer_block();
   return ok && (mode == 1 || mode == 2) ? mode : 0;
 }
-bool pipe_ok(const scs_ctx* c, bool cacheable) {
-  const char* e = std::getenv("SCS_CHOL_PIPE");   // read per step (tests toggle it in-process)
-  const bool on = e && (e[0] == '1' || e[0] == '2');
-  const int64_t nblk = c->mpad / 128;
-  return on && !cacheable && !sharded(c) && !sparse_streams(const_cast<scs_ctx*>(c)) && c->gwork &&
-         nblk >= 3 * chol_outer_block();
-}
+bool pipe_ok(const scs_ctx* c, bool cacheable) { return pipe_mode(c, cacheable) != 0; }
 
 // Gram (+ fused Aᵀv into vec_dev) and the factor of G + λ diag(Hr); Gc receives the system.
 // Returns with the factor enqueued on c->st (info in c->cinfo).
