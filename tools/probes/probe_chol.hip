@@ -34,6 +34,10 @@ __global__ void rowsum(const double* G, int64_t n, double* b) {   // b = G * one
 }
 
 int main(int argc, char** argv) {
+  // the library's context stream is non-blocking: the factor's (CU-masked, blocking) bulk stream
+  // would serialize with the legacy null stream
+  hipStream_t sq;
+  CK(hipStreamCreateWithFlags(&sq, hipStreamNonBlocking));
   for (int64_t n : {(int64_t)8192, (int64_t)16384}) {
     double *G, *G0, *W, *b, *y;
     int* info;
@@ -51,7 +55,7 @@ int main(int argc, char** argv) {
     std::vector<double> hw(256); for (int i = 0; i < 256; ++i) hw[i] = i < 128 ? 1.0 : -1.0;
     CK(hipMemcpy(wpm, hw.data(), 256 * 8, hipMemcpyHostToDevice));
     scs::CholAux aux;
-    CK(scs::chol_aux_init(&aux, n, 0));
+    CK(scs::chol_aux_init(&aux, n, sq));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); float ms;
     // diag kernel alone, 64 launches on distinct blocks of a fresh copy
     CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
@@ -81,15 +85,15 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep) {
       CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
       CK(hipMemset(info, 0, 4));
-      CK(hipEventRecord(e0));
-      CK(scs::chol_factor(G, n, n, n, W, &aux, dtr, info, 0));
-      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      CK(hipEventRecord(e0, sq));
+      CK(scs::chol_factor(G, n, n, n, W, &aux, dtr, info, sq));
+      CK(hipEventRecord(e1, sq)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
       int hinfo; CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost));
       printf("n=%ld factor: %.2f ms (info %d)\n", (long)n, ms, hinfo);
-      hipLaunchKernelGGL(rowsum, dim3((unsigned)(n / 256)), dim3(256), 0, 0, G0, n, b);
-      CK(hipEventRecord(e0));
-      CK(scs::chol_solve(G, n, n, W, b, y, 0));
-      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      hipLaunchKernelGGL(rowsum, dim3((unsigned)(n / 256)), dim3(256), 0, sq, G0, n, b);
+      CK(hipEventRecord(e0, sq));
+      CK(scs::chol_solve(G, n, n, W, b, y, sq));
+      CK(hipEventRecord(e1, sq)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
       std::vector<double> hx(n);
       CK(hipMemcpy(hx.data(), b, n * 8, hipMemcpyDeviceToHost));
       double err = 0.0;
