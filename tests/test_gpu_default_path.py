@@ -116,13 +116,15 @@ def test_c4_shape_solve_backward_error(mode, clean_env):
 
 
 @pytest.mark.timeout(600)
-def test_c5_shape_lqn_sparse(clean_env):
-    """C5 with N = 2^17 (m = 2^16 as configured): ProxLQNSCORE(mem 20) + indbox + PHuberSmootherIndBox(0.6)."""
+@pytest.mark.parametrize("f32", [False, True])
+def test_c5_shape_lqn_sparse(f32, clean_env):
+    """C5 with N = 2^17 (m = 2^16 as configured): ProxLQNSCORE(mem 20) + indbox + PHuberSmootherIndBox(0.6),
+    fp64 or fp32-stored values (the oracle runs on the values read back, widened to fp64)."""
     N, m, rho = 1 << 17, 1 << 16, 0.01
     x0 = np.random.default_rng(1234).standard_normal(m)
     lam, mu = 1e-4, 0.6
     p = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), lam, density=rho, seed=2026,
-                                        C_set=[-1.0, 1.0])
+                                        C_set=[-1.0, 1.0], f32=f32)
     A, y = p.get_sparse()
     om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), lam, C_set=[-1.0, 1.0])
     sol = scsopt.iterate(scsopt.ProxLQNSCORE(m=20), p, "indbox", scsopt.PHuberSmootherIndBox(-1.0, 1.0, mu),
