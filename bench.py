@@ -20,11 +20,21 @@ logistic N=100k m=8k (configs[1]), c4 ProxGGNSCORE sparse-group lasso N=4M m=32k
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+Multi-GPU: under torchrun / torch.distributed.run (WORLD_SIZE set) every process is
+one rank and WORLD_SIZE must equal --gpus.  Without WORLD_SIZE, --gpus N > 1 starts
+the N rank processes itself (launch_ranks) before anything touches a GPU and exits
+with the worst rank's status.  --comm picks the exchange and the process group:
+rccl -> libscsopt's own RCCL communicator, "nccl" group (one GPU per rank);
+torch -> torch.distributed.all_reduce over a "gloo" group, which also runs with
+--share-device (ranks round-robin over fewer GPUs, to exercise the launcher on a
+one-GPU box; the line then says so in "devices").
 """
 import argparse
 import glob
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -172,6 +182,130 @@ def cpu_threads():
     return max(1, n)
 
 
+GIB = float(1 << 30)
+
+
+def memory_plan(cfg, N, m, world, gram_cache=False):
+    """Per-rank device bytes of the row-sharded dense Gram methods: the local
+    panel-blocked A (N_pad x m_pad fp64) + y and the sample vectors, G and its LU-fallback copy Gc
+    (m_pad² each), W (m_pad x 128), the cached AᵀQA (--gram-cache) and, at world > 1, the packed
+    128 x 128 tile exchange buffer [tiles ‖ Aᵀv].  The largest rank (row_range: first N % world
+    ranks hold one more row) sets the plan."""
+    rows = -(-int(N) // int(world))
+    npad = -(-rows // 16) * 16
+    mpad = -(-int(m) // 128) * 128
+    nb = mpad // 128
+    plan = {"rows_per_rank": rows, "A": 8.0 * npad * mpad, "sample_vectors": 8.0 * npad * 12}
+    if cfg.get("method") != "lqn":
+        plan["G"] = 8.0 * mpad * mpad
+        plan["Gc"] = 8.0 * mpad * mpad
+        plan["W"] = 8.0 * mpad * 128
+        if gram_cache:
+            plan["Gk"] = 8.0 * mpad * mpad
+        if world > 1:
+            plan["exchange"] = 8.0 * (nb * (nb + 1) // 2 * 128 * 128 + mpad + 64)
+    plan["total"] = sum(v for k, v in plan.items() if k != "rows_per_rank")
+    return plan
+
+
+def plan_text(plan):
+    return ", ".join(f"{k} {v / GIB:.1f} GiB" for k, v in plan.items() if k != "rows_per_rank")
+
+
+def world_from_env(args, env):
+    """(world, rank, local_rank) of this process and whether it must launch the ranks itself.
+    Raises SystemExit with the reason when the launch does not match --gpus."""
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        rank = int(env.get("RANK", "0"))
+        local = int(env.get("LOCAL_RANK", str(rank)))
+        if world != args.gpus:
+            raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                             f"(torchrun --nproc-per-node {args.gpus}) or drop WORLD_SIZE")
+        return world, rank, local, False
+    return args.gpus, 0, 0, args.gpus > 1
+
+
+def check_devices(args, ndev):
+    """Fail fast (before any rank starts) when the node has fewer GPUs than ranks, unless
+    --share-device was asked for (only with --comm torch: RCCL refuses two ranks on one GPU)."""
+    if args.share_device:
+        if args.comm != "torch":
+            raise SystemExit("--share-device needs --comm torch (RCCL takes one GPU per rank)")
+        if ndev < 1:
+            raise SystemExit("--share-device: no HIP device visible")
+        return
+    if ndev < args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} needs {args.gpus} visible GPUs, this node shows {ndev} "
+                         f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', 'unset')}); "
+                         "use --share-device --comm torch to rehearse the launcher on fewer GPUs")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def rank_envs(n, port, base):
+    """The environment of each of the n rank processes (torch.distributed.run's variables)."""
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out.append(e)
+    return out
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (one per GPU) and wait; if one fails the others are
+    ended (their exact PIDs) and the worst status is returned.  The parent never touches a GPU."""
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=e)
+             for e in rank_envs(n, free_port(), os.environ)]
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def plumbing_check(world, rank, local, args):
+    """--plumbing-check: the rank processes' world wiring without a GPU (gloo): every rank reports
+    (rank, local, world) and rank 0 prints the gathered list as one JSON line."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world and dist.get_rank() == rank
+    t = torch.tensor([float(rank), float(local), float(world)])
+    got = [torch.zeros(3) for _ in range(world)]
+    dist.all_gather(got, t)
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"plumbing": [[int(v) for v in g.tolist()] for g in got], "gpus": args.gpus,
+                          "comm": args.comm, "backend": "gloo"}))
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -192,8 +326,30 @@ def main():
                     help="run the exchange path (packed Gram -> all-reduce -> unpack) at one rank too")
     ap.add_argument("--cpu-Ns", type=int, default=2048)
     ap.add_argument("--cpu-ms", type=int, default=4096)
+    ap.add_argument("--share-device", action="store_true",
+                    help="let ranks share GPUs round-robin (launcher rehearsal on a small box; --comm torch)")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="launch the ranks and check their world wiring over gloo, no GPU work")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+
+    world, rank, local, spawn = world_from_env(args, os.environ)
+    if spawn:
+        # --gpus N without a launcher: the N rank processes are started here, before any GPU call
+        # (counting devices does not initialise the GPU)
+        if not args.plumbing_check:
+            import torch
+            check_devices(args, torch.cuda.device_count())
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.plumbing_check:
+        plumbing_check(world, rank, local, args)
+        return
+    N = args.N or cfg["N"]
+    m = args.m or cfg["m"]
+    if cfg.get("sparse") and world > 1:
+        raise SystemExit("c5 runs on one GPU (BASELINE configs[4]); the sparse generator is single-context")
+    if cfg["loss"] == "rosenbrock" and world > 1:
+        raise SystemExit("c1 (Rosenbrock, no data) has nothing to shard")
 
     import numpy as np
     import torch
@@ -202,25 +358,37 @@ def main():
     from scsopt import shard
     from scsopt.iterate import device_optim_loop, init_method
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     comm = None
+    ndev = torch.cuda.device_count()
+    if world > 1:
+        check_devices(args, ndev)
+    dev = local % max(1, ndev) if args.share_device else local
+    gloo = args.comm == "torch"
     if world > 1 or args.force_comm:
         # one process per GPU; the row-sharded exchange runs on libscsopt's own RCCL communicator
-        # (--comm rccl) or through torch.distributed.all_reduce (--comm torch); torch.distributed
-        # itself only carries the communicator's unique id and the timing barrier / max
-        torch.cuda.set_device(local)
-        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+        # (--comm rccl, "nccl" group) or through torch.distributed.all_reduce (--comm torch, "gloo"
+        # group); torch.distributed otherwise carries only the communicator's unique id and the
+        # timing barrier / max
+        torch.cuda.set_device(dev)
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(free_port())), ("RANK", "0"),
+                     ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        comm = shard.Comm(device=torch.device("cuda", local), native=(args.comm == "rccl"),
-                          force=args.force_comm)
-    N = args.N or cfg["N"]
-    m = args.m or cfg["m"]
-    if cfg.get("sparse") and world > 1:
-        raise SystemExit("c5 runs on one GPU (BASELINE configs[4]); the sparse generator is single-context")
-    model, hmu, method = build_problem(cfg, N, m, comm, local, f32=args.f32)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        comm = shard.Comm(device=torch.device("cuda", dev), native=not gloo, force=args.force_comm)
+    if not cfg.get("sparse") and cfg["loss"] != "rosenbrock":
+        # fail fast, before generating anything, when the local shard does not fit this GPU
+        plan = memory_plan(cfg, N, m, world, gram_cache=args.gram_cache)
+        sharing = -(-world // max(1, ndev)) if args.share_device else 1
+        free, _total = torch.cuda.mem_get_info(dev)
+        if plan["total"] * sharing > 0.97 * free:
+            raise SystemExit(f"rank {rank}: {cfg['workload']} N={N} m={m} on {world} rank(s) needs "
+                             f"{plan['total'] * sharing / GIB:.1f} GiB on GPU {dev} ({plan_text(plan)}; "
+                             f"{plan['rows_per_rank']} rows per rank), {free / GIB:.1f} GiB free: "
+                             f"use more GPUs (--gpus) or a smaller --N")
+    model, hmu, method = build_problem(cfg, N, m, comm, dev, f32=args.f32)
     reg = cfg["reg"]
     if args.gram_cache:
         if cfg["loss"] != "least_squares" or cfg["method"] == "lqn":
@@ -263,8 +431,9 @@ def main():
     dt = time.perf_counter() - t0
     objs = sol.obj
     tm = ctx.timing()
+    gram_kname, prod_kname = ctx.kernel_names()
     if comm is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", local))
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if gloo else torch.device("cuda", dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -286,19 +455,21 @@ def main():
             "config": {"workload": cfg["workload"], "N": N, "m": m, "lambda": model.λ, "mu": hmu.mu,
                        "method": type(method).__name__, "ss_type": method.ss_type,
                        "parallelism": f"row-shard x{world}",
-                       "exchange": (("rccl (libscsopt)" if args.comm == "rccl" else "torch.distributed callback")
+                       "devices": min(world, ndev) if args.share_device else world,
+                       "exchange": (("rccl (libscsopt)" if args.comm == "rccl"
+                                     else "torch.distributed callback (gloo)")
                                     + (" forced at one rank" if world == 1 else "")) if comm is not None else None},
         }
+        if args.share_device and world > ndev:
+            line["config"]["shared_device"] = (f"{world} ranks on {ndev} GPU(s): a launcher rehearsal, "
+                                               "not a scaling number")
         if tm["gram_calls"]:
             main_calls = steps                      # one Gram per GGN/NSCORE step; the solver's own
             gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])   # launches are timed under "solve"
             gram_flops = float(N_local) * m * (m + 1)   # algorithmic symmetric Gram per launch
             achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
-            tall = m >= 12288 and (m // 128) % 2 == 0   # 256 x 128 tiles, Aᵀv fused (gram.hip gram_fuse_ok)
-            fuse = tall and os.environ.get("SCS_GRAM_FUSE", "1") != "0" and not args.gram_cache
             traffic = None
-            kname = ("gram_sia_kernel<1, 4, false, true>" if fuse else "gram_sia_kernel<1, 4>") if tall \
-                else "gram_sia_kernel<1, 2>"
+            kname = gram_kname or "unknown"   # the library reports the kernel it launched
             # PMC summaries (tools/gpu_prof_c3.sh, tools/gpu_pmc_c2.sh + tools/pmc_summary.py), one per (N, m):
             # their bytes are used only when they were measured on the kernel this run launched
             for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_gram_pmc*.json")), reverse=True):
@@ -328,7 +499,7 @@ def main():
             avg_ms = tm["gemv_ms"] / tm["gemv_calls"]
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             traffic = None
-            kname = "spmv_blk_kernel<float, 8>" if args.f32 else "spmv_blk_kernel<double, 4>"
+            kname = prod_kname or "unknown"
             # PMC bytes (tools/pmc_summary_spmv.py) only when the file names the kernel launched here
             pmc = os.path.join(ROOT, "profiles", "r02_c5_spmv_pmc_%s.json" % ("f32" if args.f32 else "f64"))
             if os.path.exists(pmc) and world == 1 and N == 1 << 20 and m == 1 << 16:

@@ -251,6 +251,12 @@ int scs_select_batch(scs_ctx* ctx, int64_t b);
  * prox-L-BFGS-SCORE.jl:69).  dx may be NULL.                               */
 int scs_step(scs_ctx* ctx, const double* x, const double* x_prev, int64_t iter,
              double* x_new, double* dx, double* pri_res_norm);
+/* step!(...; ∇fx) (iterate.jl:52-54): the caller's gradient replaces grad_f at every point the
+ * step evaluates it (`grad_f = x -> ∇fx`, prox-N-SCORE.jl:66-68 and prox-L-BFGS-SCORE.jl:98-100:
+ * ∇q, the BB step's ∇q_prev, the line search and the L-BFGS pair's γh); ProxGGNSCORE takes no ∇fx
+ * (prox-GGN-SCORE.jl:34-135 never reads it).  grad_fx (m, host) NULL = scs_step.              */
+int scs_step_grad(scs_ctx* ctx, const double* x, const double* x_prev, int64_t iter, const double* grad_fx,
+                  double* x_new, double* dx, double* pri_res_norm);
 
 /* ---- loop level  (iterate!(method, model, reg_name, hμ; max_epoch, x_tol,
  * f_tol) -> Solution, iterate.jl:56-76 / optim_loop! :100-267) ------------ */
@@ -316,6 +322,9 @@ int scs_gram_atv_eval(scs_ctx* ctx, const double* w, const double* v, const int6
 int scs_timing_enable(scs_ctx* ctx, int on);
 int scs_timing_get(scs_ctx* ctx, scs_timing* out);
 int scs_timing_reset(scs_ctx* ctx);
+/* The kernels of the latest main Gram launch and sparse product launch, as rocprofv3 names them
+ * ("" when none ran), NUL-terminated, truncated to the capacities.                          */
+int scs_kernel_names(scs_ctx* ctx, char* gram, int64_t gram_cap, char* product, int64_t product_cap);
 /* Wait for all work on the context stream.                                 */
 int scs_sync(scs_ctx* ctx);
 

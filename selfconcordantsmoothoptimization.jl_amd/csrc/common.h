@@ -3,6 +3,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Several kernels size static LDS for gfx950's 160 KiB per CU (lu_swap_cols_kernel 128 KiB,
+// lu_diag_inv_kernel ~134 KiB, spmv_blk_kernel 131 KiB): the library is built for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libscsopt targets gfx950 (MI355X) only: kernels here use more than 64 KiB of static LDS"
+#endif
+
 namespace scs {
 
 constexpr int WAVE = 64;

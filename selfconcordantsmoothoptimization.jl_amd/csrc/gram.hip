@@ -804,6 +804,10 @@ hipError_t gram_vfinal_launch(const double* VP, int npiece, int64_t vps, int64_t
   return hipGetLastError();
 }
 
+// the kernel of the latest main Gram launch (gram_launch / gram_launch_sched), as rocprofv3 names it
+static const char* g_main_name = "";
+const char* gram_main_kernel_name() { return g_main_name; }
+
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,
                        int ntiles, double* G, int64_t ldg, int packed, int tall, hipStream_t st, const double* v,
                        double* VP, int64_t vps) {
@@ -812,26 +816,34 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
   const int flags = ((packed & 1) ? GRAM_PACKED : GRAM_UPPER) | ((packed & 2) ? GRAM_ACCUMULATE : 0);
   if (v) {
     if (!gram_fuse_ok(tall)) return hipErrorInvalidValue;
-    if (tall)
+    if (tall) {
+      g_main_name = "gram_sia_kernel<1, 4, false, true>";
       hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0,
                          Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
-    else
+    } else {
+      g_main_name = "gram_sia_kernel<1, 2, false, true>";
       hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0,
                          Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
+    }
     return hipGetLastError();
   }
-  if (!tall && gram_sia_mode() == 0)
+  if (!tall && gram_sia_mode() == 0) {
+    g_main_name = "gram_f64_kernel<false, 2, true>";
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
-  else if (!tall)
+  } else if (!tall) {
+    g_main_name = "gram_sia_kernel<1, 2>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
-  else if (gram_tall_mode() == 3)
+  } else if (gram_tall_mode() == 3) {
+    g_main_name = "gram_sia_kernel<1, 4>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
-  else
+  } else {
+    g_main_name = "gram_glds_kernel<true, 1>";
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  }
   return hipGetLastError();
 }
 
@@ -1044,33 +1056,43 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
   const int flags = ((packed & 1) ? GRAM_PACKED : GRAM_UPPER) | ((packed & 2) ? GRAM_ACCUMULATE : 0);
   const int glds = gram_tall_mode();
   if (v && !gram_fuse_ok(tall)) return hipErrorInvalidValue;
-  if (v && tall)
+  if (v && tall) {
+    g_main_name = "gram_sia_kernel<1, 4, false, true>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
-  else if (v)
+  } else if (v) {
+    g_main_name = "gram_sia_kernel<1, 2, false, true>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
-  else if (tall && glds == 3)
+  } else if (tall && glds == 3) {
+    g_main_name = "gram_sia_kernel<1, 4>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk,
                        nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
-  else if (tall && glds == 2)
+  } else if (tall && glds == 2) {
+    g_main_name = "gram_glds_kernel<true, 1>";
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
                        Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
-  else if (tall && glds == 1)
+  } else if (tall && glds == 1) {
+    g_main_name = "gram_glds_kernel<true>";
     hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
-  else if (tall)
+  } else if (tall) {
+    g_main_name = "gram_f64_kernel<false, 4, true>";
     hipLaunchKernelGGL((gram_f64_kernel<false, 4, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
-  else if (gram_sia_mode() == 1)
+  } else if (gram_sia_mode() == 1) {
+    g_main_name = "gram_sia_kernel<1, 2>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr,
                        0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
-  else if (gram_sia_mode() == 2)
+  } else if (gram_sia_mode() == 2) {
+    g_main_name = "gram_sia_kernel<0>";
     hipLaunchKernelGGL((gram_sia_kernel<0>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr, 0,
                        G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
-  else
+  } else {
+    g_main_name = "gram_f64_kernel<false, 2, true>";
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
+  }
   if (ncomb > 0) {
     if (tall)
       hipLaunchKernelGGL(gram_combine_kernel<4>, dim3(16, ncomb), dim3(256), 0, st, P, comb, nsplit, G, ldg, packed);

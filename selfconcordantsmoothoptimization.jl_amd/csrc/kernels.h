@@ -32,6 +32,8 @@ void gram_tile_list_tall(int nb, int2* out, int* ntiles);
 // v != nullptr: the same launch also forms Aᵀv (fused, gram_fuse_ok kernels only) into VP: one row
 // (stride vps >= mpad) per K piece (nsplit rows for the scheduled launch, zeroed beforehand when
 // nsplit > 1), reduced by gram_vfinal_launch.
+// rocprofv3's name of the kernel the latest gram_launch / gram_launch_sched ran
+const char* gram_main_kernel_name();
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles, int ntiles,
                        double* G, int64_t ldg, int packed, int tall, hipStream_t st, const double* v = nullptr,
                        double* VP = nullptr, int64_t vps = 0);
@@ -252,6 +254,7 @@ int spmv_blk_shift(int64_t ncols);
 int spmv_pad_index();   // padding index of the blocked layouts (the SpMV's zero slot)
 int spmv_slot_width(int f32);   // segments padded to whole slots of 4 (fp64) / 8 (fp32) entries
 // segments padded to whole slots (blk_pad), padding index spmv_pad_index(), value 0
+const char* spmv_kernel_name(int f32);
 hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
                            int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,
                            hipStream_t st);

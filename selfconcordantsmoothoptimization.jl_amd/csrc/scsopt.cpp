@@ -85,6 +85,7 @@ struct scs_ctx {
 
   // data
   int64_t N = 0, Npad = 0, m = 0, mpad = 0, Nglob = 0, row0 = 0;
+  int64_t Nglob_data = 0;   // N_global of the full data (Nglob follows the swapped-in view)
   int64_t nstage = 0;  // Npad / 16: stages of the panel-blocked A (common.h tiled_off)
   bool has_data = false;
   bool generic = false;  // ProblemGeneric (no A)
@@ -158,6 +159,7 @@ struct scs_ctx {
   int64_t cb_nout = 0;        // rows of the SCS_CB_GGN Jacobian (0: no GGN callback)
   NView cbv;                  // that Jacobian, panel-blocked, swapped in for the GGN step
   double* cbstage = nullptr;  // column-major staging panel for its upload
+  const double* gfix = nullptr; // scs_step_grad: the caller's ∇fx (device copy) for the step's duration
   bool lbfgs_pending = false; // scs_iterate's device loop: the memory update's dg/gg are read at the epoch end
   int lbfgs_slot = 0;
   double H0 = 1.0;
@@ -246,7 +248,9 @@ struct scs_ctx {
   // N_global + 1 <= m on several ranks)
   NView gview;
   bool gview_ok = false;
-  int64_t gview_batch = -1;    // the batch gview holds (-1: the full data)
+  int64_t gview_batch = -1;    // the batch gview holds (-1: the full data) ...
+  uint64_t gview_gen = 0;      // ... of batch list generation gview_gen
+  uint64_t batch_gen = 1;      // bumped whenever the batch list changes (scs_set_batches)
   bool lu_fallback_used = false;
 
   // caches (CSE of identical evaluations; keyed by the host x content)
@@ -267,6 +271,8 @@ struct scs_ctx {
   uint64_t ztag = 0, gtag[2] = {0, 0};
   int gnext = 0;
 
+  // the kernels the dominant launches used (scs_kernel_names; rocprofv3's names)
+  std::string gram_kname, prod_kname;
   // timing
   bool timing = false;
   int timing_every = 1;     // scs_iterate's pipelined loop: kernel-timing events on every n-th epoch only
@@ -469,8 +475,12 @@ int64_t reduce_buffer_doubles(const scs_ctx* c) {
   const int64_t nb = c->mpad / 128;
   const int64_t tsz = (nb * (nb + 1) / 2 + nb) * 128 * 128;   // 128 x 128 slots (tall lists add <= nb)
   int64_t need = std::max<int64_t>(tsz + c->mpad, c->mpad);
-  if (c->Nglob + 1 <= c->m) {   // GGN sample-space branch across ranks: all-gather of A and y
-    const int64_t Ng = round_up(std::max<int64_t>(c->Nglob, 1), 16);
+  // GGN sample-space branch across ranks: all-gather of A and y.  Sized from the full data's
+  // N_global (a batch view swapped in at the first exchange is never larger): the buffer is
+  // allocated once, whichever view is active then
+  const int64_t Nfull = std::max(c->Nglob_data, c->Nglob);
+  if (Nfull + 1 <= c->m || c->Nglob + 1 <= c->m) {
+    const int64_t Ng = round_up(std::max<int64_t>(std::min(Nfull, c->m), 1), 16);
     need = std::max<int64_t>(need, Ng * c->mpad + Ng);
   }
   return need + 64;
@@ -776,6 +786,14 @@ struct BatchScope {
 };
 
 void clear_batches(scs_ctx* c) {
+  // the gathered rows of a batch index belong to the list they came from: a new list (a
+  // reshuffle, another slice) must not reuse them
+  ++c->batch_gen;
+  if (c->gview_ok && c->gview_batch >= 0) {
+    free_view(c, c->gview);
+    c->gview = NView();
+    c->gview_ok = false;
+  }
   for (NView& v : c->bpool) free_view(c, v);
   c->bpool.clear();
   c->bheld.clear();
@@ -851,6 +869,7 @@ int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
   if (c->sparse) {
     const auto& B = c->bcsr;
     HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, c->sp_f32, xd, c->N, c->m, B.shift, c->nnz, c->zpart, c->Npad, c->st));
+    c->prod_kname = spmv_kernel_name(c->sp_f32);
     return B.nblk;
   }
   HCK(launch_gemv_n(c->A, c->nstage, c->Npad, c->mpad, xd, nsplit, c->zpart, c->Npad, c->st));
@@ -989,6 +1008,10 @@ double eval_f_dev(scs_ctx* c, const double* xh, const double* xd) {
 
 // ∇f(x) -> out (device)
 void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
+  if (c->gfix) {   // step!(...; ∇fx): grad_f = x -> ∇fx at every point (prox-L-BFGS-SCORE.jl:98-100)
+    if (out != c->gfix) HCK(hipMemcpyAsync(out, c->gfix, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
+    return;
+  }
   if (c->loss == SCS_LOSS_CALLBACK) {
     const double* g = cb_eval(c, SCS_CB_GRAD, xh, xd, c->m);
     HCK(hipMemcpyAsync(out, g, sizeof(double) * c->m, hipMemcpyHostToDevice, c->st));
@@ -1216,6 +1239,7 @@ void gram_main_stream(scs_ctx* c, const double* w, double* out, int packed) {
                             out, c->mpad, mode, c->tall, c->st));
     else
       HCK(gram_launch(slot, R / 16, w + r0, nk, c->tiles, c->ntiles, out, c->mpad, mode, c->tall, c->st));
+    c->gram_kname = gram_main_kernel_name();
   }
 }
 
@@ -1236,6 +1260,7 @@ void gram_main(scs_ctx* c, const double* w, double* out, int packed, const doubl
   else
     HCK(gram_launch(A, c->nstage, w, c->Npad, c->tiles, c->ntiles, out, c->mpad, packed, c->tall, c->st, v, c->vpart,
                     c->mpad));
+  c->gram_kname = gram_main_kernel_name();
   if (v) HCK(gram_vfinal_launch(c->vpart, npiece, c->mpad, c->m, vout, c->st));
 }
 
@@ -1414,13 +1439,15 @@ void ggn_sample_direction(scs_ctx* c, const double* xh);
 void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
   if (c->sparse) fail(c, SCS_ERR_ARG, "the sharded GGN sample-space branch needs a dense A");
   ensure_red(c);
-  if (c->gview_ok && c->gview_batch != c->bsel) {   // built for another batch (or the full data)
+  const int64_t Ng = c->Nglob, Npg = round_up(std::max<int64_t>(Ng, 1), 16);
+  const uint64_t gen = c->bsel < 0 ? 0 : c->batch_gen;
+  const bool held = c->gview_ok && c->gview_batch == c->bsel && c->gview_gen == gen;
+  if (c->gview_ok && !held && c->gview.N != Ng) {   // another size: new buffers
     free_view(c, c->gview);
     c->gview = NView();
     c->gview_ok = false;
   }
-  if (!c->gview_ok) {
-    const int64_t Ng = c->Nglob, Npg = round_up(std::max<int64_t>(Ng, 1), 16);
+  if (!held) {
     if (Npg * c->mpad + Npg > c->red_cap) fail(c, SCS_ERR_COMM, "reduce buffer too small for the row all-gather");
     // each local row at its global position: in the data (row0 + r) or in the selected batch
     std::vector<int64_t> rows(Ng, -1);
@@ -1435,20 +1462,28 @@ void ggn_sample_direction_sharded(scs_ctx* c, const double* xh) {
     HCK(launch_gather_rows(c->A, c->Npad, c->y, drows, Ng, Npg, c->mpad, c->red, c->red + Npg * c->mpad, c->st));
     allreduce(c, c->red, Npg * c->mpad + Npg);
     NView& v = c->gview;
-    v.N = v.Nglob = Ng;
-    v.Npad = Npg;
-    v.nstage = Npg / 16;
-    v.A = dalloc<double>(c, (size_t)Npg * c->mpad);
-    v.y = dalloc<double>(c, Npg);
+    const bool fresh = !c->gview_ok;   // same size as the view held: refill its buffers in place
+    if (fresh) {
+      v.N = v.Nglob = Ng;
+      v.Npad = Npg;
+      v.nstage = Npg / 16;
+      v.A = dalloc<double>(c, (size_t)Npg * c->mpad);
+      v.y = dalloc<double>(c, Npg);
+    }
     HCK(hipMemcpyAsync(v.A, c->red, sizeof(double) * Npg * c->mpad, hipMemcpyDeviceToDevice, c->st));
     HCK(hipMemcpyAsync(v.y, c->red + Npg * c->mpad, sizeof(double) * Npg, hipMemcpyDeviceToDevice, c->st));
+    // a refilled view's Aᵀ copy (built once per A by ggn_sample_direction) follows its rows
+    if (!fresh && v.At) HCK(launch_transpose(v.A, v.Npad, Ng, c->m, v.At, c->mpad, v.NpS, c->st));
     sync(c);
     dfree_t(c, drows);
-    swap_view(c, v);
-    alloc_nspace(c);
-    swap_view(c, v);
+    if (fresh) {
+      swap_view(c, v);
+      alloc_nspace(c);
+      swap_view(c, v);
+    }
     c->gview_ok = true;
     c->gview_batch = c->bsel;
+    c->gview_gen = gen;
   }
   struct Scope {   // the gathered rows on one logical rank, restored even when the step fails
     scs_ctx* c;
@@ -1638,6 +1673,7 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
       if (pipe_ok(c, c->gram_cache && gram_x_independent(c))) {
         ensure_gram(c);
         const hipEvent_t es = gram_factor_pipelined(c, c->hN, c->gN, c->gtmp);
+        if (c->gfix) grad_f_dev(c, xh, c->x, c->gtmp);   // ∇fx replaces the fused Aᵀg
         HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
         solve_factored(c, c->gq, es);
         HCK(launch_neg(c->gq, m, c->d, c->st));
@@ -1662,7 +1698,9 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
     }
     gram_and_reduce(c, c->wN, c->vN, c->gtmp);   // Gram + Jᵀr in one pass over A
   }
-  // rhs = ∇f + λ gr (NSCORE) | Jᵀr + λ gr (GGN: Jt*[r;1], prox-GGN-SCORE.jl:121-130)
+  // rhs = ∇f + λ gr (NSCORE) | Jᵀr + λ gr (GGN: Jt*[r;1], prox-GGN-SCORE.jl:121-130); a caller's
+  // ∇fx replaces ∇f in ProxNSCORE (prox-N-SCORE.jl:66-69; ProxGGNSCORE takes no ∇fx)
+  if (c->gfix && c->method == SCS_PROX_NSCORE) grad_f_dev(c, xh, c->x, c->gtmp);
   HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
   HCK(launch_diag_add(c->G, c->mpad, m, c->lam, c->Hr, c->st));
   solve_system(c, c->gq);
@@ -1922,6 +1960,7 @@ static void set_dims(scs_ctx* c, int64_t N, int64_t m, int64_t Nglob, int64_t ro
   c->mpad = round_up(m, 128);
   c->nstage = c->Npad / 16;
   c->Nglob = Nglob > 0 ? Nglob : N;
+  c->Nglob_data = c->Nglob;
   c->row0 = row0;
 }
 
@@ -2548,25 +2587,54 @@ int scs_select_batch(scs_ctx* c, int64_t b) {
   });
 }
 
-int scs_step(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, double* x_new, double* dx,
-             double* pri) {
-  return guarded(c, [&] {
-    require_ready(c, true);
-    HCK(hipSetDevice(c->dev));
-    hipEvent_t e0;
-    tbegin(c, T_STEP, &e0);
-    BatchScope bs(c);
-    h2d(c, c->x, x, c->m);
-    h2d(c, c->xp, x_prev ? x_prev : x, c->m);
-    std::vector<double> xnew_h(c->m);
+static void step_call(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, const double* grad_fx,
+                      double* x_new, double* dx, double* pri) {
+  require_ready(c, true);
+  HCK(hipSetDevice(c->dev));
+  hipEvent_t e0;
+  tbegin(c, T_STEP, &e0);
+  BatchScope bs(c);
+  h2d(c, c->x, x, c->m);
+  h2d(c, c->xp, x_prev ? x_prev : x, c->m);
+  std::vector<double> xnew_h(c->m);
+  {
+    // ∇fx lives in its own buffer for the call (gtmp2 is line-search scratch)
+    double* gbuf = nullptr;
+    if (grad_fx) {
+      gbuf = dalloc<double>(c, c->mpad);
+      h2d(c, gbuf, grad_fx, c->m);
+      invalidate_caches(c);
+      c->gfix = gbuf;
+    }
+    struct Release {
+      scs_ctx* c;
+      double* g;
+      ~Release() {
+        if (!g) return;
+        c->gfix = nullptr;
+        invalidate_caches(c);
+        (void)hipStreamSynchronize(c->st);
+        dfree_t(c, g);
+      }
+    } rel{c, gbuf};
     if (c->method == SCS_PROX_LQNSCORE)
       step_lqn(c, x, x_prev ? x_prev : x, iter, xnew_h.data(), dx, pri);
     else
       step_newton(c, x, iter, xnew_h.data(), dx, pri);
-    std::memcpy(x_new, xnew_h.data(), sizeof(double) * c->m);
-    tend(c, T_STEP, e0);
-    if (c->timing) tresolve(c);
-  });
+  }
+  std::memcpy(x_new, xnew_h.data(), sizeof(double) * c->m);
+  tend(c, T_STEP, e0);
+  if (c->timing) tresolve(c);
+}
+
+int scs_step(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, double* x_new, double* dx,
+             double* pri) {
+  return guarded(c, [&] { step_call(c, x, x_prev, iter, nullptr, x_new, dx, pri); });
+}
+
+int scs_step_grad(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, const double* grad_fx,
+                  double* x_new, double* dx, double* pri) {
+  return guarded(c, [&] { step_call(c, x, x_prev, iter, grad_fx, x_new, dx, pri); });
 }
 
 // optim_loop! (iterate.jl:100-267), full-batch, in C++ around the same device calls the
@@ -3231,6 +3299,19 @@ int scs_timing_get(scs_ctx* c, scs_timing* t) {
     t->step_calls = c->tcalls[T_STEP];
     t->reduce_ms = c->tms[T_REDUCE];
     t->reduce_calls = c->tcalls[T_REDUCE];
+  });
+}
+
+int scs_kernel_names(scs_ctx* c, char* gram, int64_t gram_cap, char* product, int64_t product_cap) {
+  return guarded(c, [&] {
+    auto put = [](char* dst, int64_t cap, const std::string& v) {
+      if (!dst || cap <= 0) return;
+      const size_t n = std::min<size_t>(v.size(), (size_t)cap - 1);
+      std::memcpy(dst, v.data(), n);
+      dst[n] = 0;
+    };
+    put(gram, gram_cap, c->gram_kname);
+    put(product, product_cap, c->prod_kname);
   });
 }
 

@@ -212,6 +212,8 @@ int spmv_blk_shift(int64_t ncols) {
   return s;
 }
 
+const char* spmv_kernel_name(int f32) { return f32 ? "spmv_blk_kernel<float, 8>" : "spmv_blk_kernel<double, 4>"; }
+
 hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
                            int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,
                            hipStream_t st) {

@@ -110,7 +110,7 @@ end
 # hess_fx) (:61-81) evaluated on the host (SCS_LOSS_CALLBACK); the smoother, the solve, damping,
 # prox and the loop stay on the device.  No ForwardDiff fallback: ProxLQNSCORE needs grad_fx,
 # ProxNSCORE grad_fx and hess_fx.
-struct LossCallbacks
+mutable struct LossCallbacks   # mutable: `user` is pointer_from_objref(cbs), rooted by the model
     f::Function
     grad_fx::Union{Function,Nothing}
     hess_fx::Union{Function,Nothing}
@@ -335,9 +335,12 @@ function step!(method::ProximalMethod, model::DeviceProblem, reg_name, hμ, As, 
     As === nothing || size(As, 1) == size(model.A, 1) ||
         error("minibatch As on a DeviceProblem: use iterate_device!(...; batch_size, shuffle_batch)")
     x_new = similar(x); dx = similar(x); pri = Ref{Float64}(0.0)
-    chk(ccall((:scs_step, lib), Cint,
-              (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Ref{Float64}),
-              model.ctx, x, x_prev, iter, x_new, dx, pri), model.ctx)
+    # ∇fx (iterate.jl:52-54): grad_f = x -> ∇fx inside the step (prox-L-BFGS-SCORE.jl:98-100)
+    g = ∇fx === nothing ? C_NULL : Vector{Float64}(vec(∇fx))
+    g === C_NULL || length(g) == length(x) || error("∇fx must have length(x) entries")
+    chk(ccall((:scs_step_grad, lib), Cint,
+              (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{Float64}),
+              model.ctx, x, x_prev, iter, g, x_new, dx, pri), model.ctx)
     return return_dx ? (x_new, dx, pri[]) : (x_new, pri[])
 end
 

@@ -102,6 +102,7 @@ _SIGS = {
     "scs_set_batches": (C.c_int, [C.c_void_p, c_i64p, c_i64p, C.c_int64]),
     "scs_select_batch": (C.c_int, [C.c_void_p, C.c_int64]),
     "scs_step": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, c_dp, c_dp, c_dp]),
+    "scs_step_grad": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, c_dp, c_dp, c_dp, c_dp]),
     "scs_iterate": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, C.c_double, C.c_double, C.c_int, c_dp,
                               C.POINTER(History), c_i64p, c_i64p]),
     "scs_smoother_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, c_dp]),
@@ -116,6 +117,7 @@ _SIGS = {
     "scs_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_timing_get": (C.c_int, [C.c_void_p, C.POINTER(Timing)]),
     "scs_timing_reset": (C.c_int, [C.c_void_p]),
+    "scs_kernel_names": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]),
     "scs_sync": (C.c_int, [C.c_void_p]),
 }
 
@@ -189,6 +191,12 @@ class Context:
         s = C.c_void_p()
         self.check(lib.scs_get_stream(self.h, C.byref(s)))
         return s.value
+
+    def kernel_names(self):
+        """(main Gram kernel, sparse product kernel) of the latest launches, rocprofv3's names."""
+        g, p = C.create_string_buffer(128), C.create_string_buffer(128)
+        self.check(lib.scs_kernel_names(self.h, g, 128, p, 128))
+        return g.value.decode(), p.value.decode()
 
     def timing(self):
         t = Timing()

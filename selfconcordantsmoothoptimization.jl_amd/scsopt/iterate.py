@@ -57,20 +57,26 @@ def _norm(v):
     return float(np.linalg.norm(v))
 
 
-def step(method, model, reg_name, hmu, x, x_prev, iter_, return_dx=False, batch=None):
-    """step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter; return_dx).
+def step(method, model, reg_name, hmu, x, x_prev, iter_, return_dx=False, batch=None, grad_fx=None):
+    """step!(method, model, reg_name, hμ, As, x, x_prev, ys, Cmat, iter; ∇fx, return_dx).
 
-    As, ys: the full data, or registered batch `batch` (Problem.set_batches)."""
+    As, ys: the full data, or registered batch `batch` (Problem.set_batches).  grad_fx: the
+    reference's ∇fx keyword -- the step uses it as grad_f at every point (scs_step_grad)."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     x_prev = np.ascontiguousarray(x_prev, dtype=np.float64)
     x_new = np.empty_like(x)
     dx = np.empty_like(x) if return_dx else None
+    g = None
+    if grad_fx is not None:
+        g = np.ascontiguousarray(np.asarray(grad_fx, dtype=np.float64).reshape(-1))
+        if g.shape != x.shape:
+            raise ValueError(f"∇fx must have length m = {x.shape[0]}")
     pri = C.c_double()
     if batch is not None:
         model.select_batch(batch)
     try:
-        model.ctx.check(_lib.lib.scs_step(model.ctx.h, dptr(x), dptr(x_prev), int(iter_), dptr(x_new), dptr(dx),
-                                          C.byref(pri)))
+        model.ctx.check(_lib.lib.scs_step_grad(model.ctx.h, dptr(x), dptr(x_prev), int(iter_), dptr(g), dptr(x_new),
+                                               dptr(dx), C.byref(pri)))
     finally:
         if batch is not None:
             model.select_batch(-1)

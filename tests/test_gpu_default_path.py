@@ -135,3 +135,40 @@ def test_c5_shape_lqn_sparse(f32, clean_env):
     np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
     np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
     assert np.all(sol.x >= -1.0) and np.all(sol.x <= 1.0)
+
+
+@pytest.mark.timeout(900)
+def test_c4_shape_ggn_group_lasso(clean_env):
+    """C4 shape (BASELINE configs[3]) on one GPU: ProxGGNSCORE least squares + sparse-group lasso,
+    m = 32768 in 1024 groups of 32, N = 36864 (N + 1 > m: the feature branch), μ = 1e-2,
+    λ = [1e-8, 0.1·max_g ‖∇_g f(0)‖] -- the 256 x 128 Gram with the fused Jᵀr, the m = 32768
+    two-level Cholesky (no CU reserve above m = 16384), the multi-workgroup PHuberSmootherGL with its
+    global dot(Dg, Dg) (phuber-smooth.jl:137-164) and the group prox over 1024 groups
+    (prox-operators.jl:48-66, prox-reg-utils.jl:84-119).  2 epochs vs the oracle at rtol 1e-8 on
+    obj / fval and on rel (the mean_square_error of reg "gl", iterate.jl:171-175)."""
+    N, m, gs, mu = 36864, 32768, 32, 1e-2
+    ng = m // gs
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    f, out = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N)
+    p = scsopt.Problem.synthetic(N, m, x0, f, 1.0, kind=3, seed=2026, out_fn=out)
+    g0 = p.gradx(np.zeros(m))
+    lam = [1e-8, 0.1 * float(np.max(np.linalg.norm(g0.reshape(ng, gs), axis=1)))]
+    p.λ = lam
+    ind = np.array([[1 + gs * g for g in range(ng)], [gs * (g + 1) for g in range(ng)], [1] * ng])
+    p.P = scsopt.get_P(m, np.arange(1, m + 1), ind)
+    A, y = p.get_data()
+    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N, ggn="linear_ls"), lam,
+                   P=O.GroupP(m, ind, np.arange(1, m + 1)))
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "gl", scsopt.PHuberSmootherGL(mu, p), max_epoch=2, x_tol=0.0,
+                         f_tol=0.0, verbose=0)
+    del A
+    osol = O.iterate(O.ProxGGNSCORE(), om, "gl", O.PHuberSmootherGL(mu, om), max_epoch=2, x_tol=0.0, f_tol=0.0)
+    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.fval, osol.fval, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.rel, osol.rel, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+    # the group prox zeroes whole groups: the support pattern is group-aligned on both sides
+    zd = (sol.x.reshape(ng, gs) == 0).all(axis=1)
+    zo = (osol.x.reshape(ng, gs) == 0).all(axis=1)
+    assert np.array_equal(zd, zo)

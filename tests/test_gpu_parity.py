@@ -757,3 +757,38 @@ def test_lqn_fused_epoch_bit_identical(reg, use_prox, m, monkeypatch):
         assert a.obj == b.obj and a.fval == b.fval and a.pri_res_norm == b.pri_res_norm
         assert np.array_equal(bits(a.x), bits(b.x))
         np.testing.assert_allclose(a.rel, b.rel, rtol=1e-13)
+
+
+@pytest.mark.parametrize("method,ss", [("nscore", 1), ("nscore", 3), ("lqn", 1), ("lqn", 2), ("lqn", 3), ("ggn", 1)])
+def test_step_grad_fx_keyword(method, ss):
+    """step!(...; ∇fx) (iterate.jl:52-54): grad_f = x -> ∇fx everywhere inside the step
+    (prox-N-SCORE.jl:66-68, prox-L-BFGS-SCORE.jl:98-100: ∇q, BB's ∇q_prev, the line search and
+    the L-BFGS pair); ProxGGNSCORE never reads it.  Lock-step vs the oracle over 4 steps with a
+    caller gradient that is NOT the model's; then a plain step must not see a stale ∇fx."""
+    N, m, lam = 2048, 96, 3e-3
+    p, om, _, _ = _synthetic_pair(method, N=N, m=m, lam=lam, max_epoch=1)
+    hm, ohm = scsopt.PHuberSmootherL1L2(1.0), O.PHuberSmootherL1L2(1.0)
+    meth = {"ggn": (scsopt.ProxGGNSCORE, O.ProxGGNSCORE), "nscore": (scsopt.ProxNSCORE, O.ProxNSCORE),
+            "lqn": (scsopt.ProxLQNSCORE, O.ProxLQNSCORE)}[method]
+    kw = {"m": 3} if method == "lqn" else {}
+    dm, omth = meth[0](ss_type=ss, **kw), meth[1](ss_type=ss, **kw)
+    if ss == 3:
+        p.L = om.L = 2.0
+    p.configure("l1", hm)
+    from scsopt.iterate import init_method, step
+    init_method(dm, p)
+    omth.init(om.x0)
+    rng = np.random.default_rng(17)
+    x = om.x0.copy()
+    xp = x.copy()
+    for it in range(1, 5):
+        g = 0.7 * om.gradx(x) + 1e-3 * rng.standard_normal(m)
+        xn_d, pri_d = step(dm, p, "l1", hm, x, xp, it, grad_fx=g)
+        xn_o, pri_o = O.step(omth, om, "l1", ohm, x, xp, None, it, grad_fx=g)
+        np.testing.assert_allclose(xn_d, xn_o, rtol=1e-9, atol=1e-12)
+        assert pri_d == pytest.approx(pri_o, rel=1e-9)
+        xp, x = x, xn_o
+    # the keyword is per call: the next plain step uses the model's gradient again
+    xn_d, pri_d = step(dm, p, "l1", hm, x, xp, 5)
+    xn_o, pri_o = O.step(omth, om, "l1", ohm, x, xp, None, 5)
+    np.testing.assert_allclose(xn_d, xn_o, rtol=1e-9, atol=1e-12)

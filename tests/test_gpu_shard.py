@@ -19,7 +19,8 @@ pytestmark = pytest.mark.gpu
 N, M = 3001, 192
 NS = 151          # sample-space case: N + 1 <= M
 METHODS = ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample", "ggn_batch", "nscore_batch_ordered",
-           "ggn_sample_batch")
+           "ggn_sample_batch", "ggn_ls_gl", "ggn_sample_rebatch")
+GS = 32           # ggn_ls_gl: C4's sparse-group lasso (groups of 32) on the row shards
 
 
 def _free_port():
@@ -60,6 +61,32 @@ def _run(method, comm=None):
         sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=4, verbose=0, batch_size=bs,
                              shuffle_batch=method != "nscore_batch_ordered",
                              batch_perm=np.random.default_rng(3).permutation(n))
+        return {"obj": list(sol.obj), "x": sol.x.copy(), "epochs": sol.epochs}
+    elif method == "ggn_sample_rebatch":
+        # two iterate! calls, each registering ONE batch (local_max_iter = 1) of another shuffle:
+        # batch index 0 names different rows in the second list, so the all-gathered rows of the
+        # first (the sharded sample-space view) must not be reused
+        f, out = losses.logistic_ce(1.0 / NS), losses.sigmoid_ce(1.0 / NS)
+        p = scsopt.Problem.synthetic(NS, M, x0, f, 2e-3, kind=1, seed=29, out_fn=out, comm=comm)
+        objs, xs = [], []
+        for seed in (3, 4):
+            sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), verbose=0,
+                                 batch_size=48, local_max_iter=1,
+                                 batch_perm=np.random.default_rng(seed).permutation(NS))
+            objs += list(sol.obj)
+            xs.append(sol.x.copy())
+        return {"obj": objs, "x": np.concatenate(xs), "epochs": sol.epochs}
+    elif method == "ggn_ls_gl":
+        # C4 (BASELINE configs[3]) in miniature: least squares + l1/group lasso, PHuberSmootherGL(1e-2)
+        # -- the GL smoother's global dot(Dg, Dg) and the group prox run redundantly on every rank
+        f, out = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N)
+        ng = M // GS
+        p = scsopt.Problem.synthetic(N, M, x0, f, 1.0, kind=3, seed=23, out_fn=out, comm=comm)
+        ind = np.array([[1 + GS * g for g in range(ng)], [GS * (g + 1) for g in range(ng)], [1] * ng])
+        p.P = scsopt.get_P(M, np.arange(1, M + 1), ind)
+        p.λ = [1e-8, 0.02]
+        sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "gl", scsopt.PHuberSmootherGL(1e-2, p), max_epoch=6,
+                             verbose=0)
         return {"obj": list(sol.obj), "x": sol.x.copy(), "epochs": sol.epochs}
     elif method == "ggn_ls_cached":
         f, out, kind = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N), 3

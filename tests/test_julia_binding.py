@@ -112,7 +112,7 @@ def test_every_ccall_matches_the_header():
         seen.add(name)
     # the binding covers the step / loop / comm / sparse entry points a maintainer needs
     for need in ("scs_create", "scs_set_data", "scs_set_sparse", "scs_set_loss", "scs_set_reg", "scs_set_smoother",
-                 "scs_method_init", "scs_step", "scs_iterate", "scs_set_comm", "scs_set_reduce_buffer",
+                 "scs_method_init", "scs_step_grad", "scs_iterate", "scs_set_comm", "scs_set_reduce_buffer",
                  "scs_reduce_buffer_size", "scs_eval_f"):
         assert need in seen, need
 
@@ -122,3 +122,19 @@ def test_indbox_bounds_come_from_the_closures():
     assert "hμ.lb" not in src and "hμ.ub" not in src        # no such fields (phuber-smooth.jl:38-58)
     assert "getfield(g, :lb)" in src and "getfield(g, :ub)" in src
     assert "is_interval_set" in src                         # C_set forms of prox-operators.jl:34-46
+
+
+def test_callback_user_pointer_is_a_mutable_object():
+    """pointer_from_objref throws on immutable objects: the struct whose address libscsopt hands
+    back to the loss trampoline must be mutable (and rooted by the model)."""
+    src = open(JL).read()
+    assert re.search(r"^mutable struct LossCallbacks", src, flags=re.M)
+    assert "pointer_from_objref(cbs)" in src and "model.grad_fx = cbs" in src
+
+
+def test_step_passes_grad_fx():
+    """step!(...; ∇fx) reaches the library (scs_step_grad), it is not dropped."""
+    src = open(JL).read()
+    body = src[src.index("function step!("):]
+    body = body[:body.index("\nend")]
+    assert "∇fx" in body and "scs_step_grad" in body and ":scs_step," not in body

@@ -144,3 +144,73 @@ def test_gloo_world2_sharded_minibatches():
         np.testing.assert_allclose(t[:m * m].reshape(m, m), Ab.T @ Ab, rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(t[m * m:m * m + m], Ab.T @ y[b], rtol=1e-12, atol=1e-12)
         assert t[-1] == len(b)   # the ranks' kept rows partition the batch
+
+
+def _gl_worker(rank, world, port, out):
+    """C4 (sparse-group lasso, ProxGGNSCORE least squares) over row shards: the exchanged
+    [Gram ‖ Jᵀr] of the ranks' rows, then the GL smoother / solve / group prox run on the sums."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "selfconcordantsmoothoptimization.jl_amd"), os.path.join(root, "oracle")]
+    from scsopt.shard import allreduce_inplace, row_range
+    import scsopt_oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    A, y, x = _gl_problem()
+    N, m = A.shape
+    r0, r1 = row_range(N, world, rank)
+    loss = O.Loss("least_squares", 1.0 / N, ggn="linear_ls")
+    s, r, q = loss.ggn_parts(A[r0:r1], y[r0:r1], x)
+    Al = A[r0:r1]
+    G = Al.T @ ((s * s * q)[:, None] * Al)
+    e = Al.T @ (s * r)
+    payload = torch.from_numpy(np.concatenate([G[np.tril_indices(m)], e]))
+    allreduce_inplace(payload)
+    out[rank] = payload.numpy().copy()
+    dist.destroy_process_group()
+
+
+def _gl_problem():
+    rng = np.random.default_rng(31)
+    N, m = 157, 64
+    A = rng.standard_normal((N, m))
+    y = A @ (rng.standard_normal(m) * (rng.random(m) < 0.3)) + 0.1 * rng.standard_normal(N)
+    x = rng.standard_normal(m)
+    return A, y, x
+
+
+def test_gloo_world2_group_lasso_step():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gl_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    import scsopt_oracle as O
+    A, y, x = _gl_problem()
+    N, m = A.shape
+    gs = 16
+    ng = m // gs
+    ind = np.array([[1 + gs * g for g in range(ng)], [gs * (g + 1) for g in range(ng)], [1] * ng])
+    lam = [1e-8, 0.05]
+    om = O.Problem(A, y, x, O.Loss("least_squares", 1.0 / N, ggn="linear_ls"), lam,
+                   P=O.GroupP(m, ind, np.arange(1, m + 1)))
+    hm = O.PHuberSmootherGL(1e-2, om)
+    nt = m * (m + 1) // 2
+    assert np.array_equal(out[0], out[1])
+    gr, Hr = hm.grad(om.P, x), hm.hess(om.P, x)
+    Gs = np.zeros((m, m))
+    Gs[np.tril_indices(m)] = out[0][:nt]
+    Gs = Gs + np.tril(Gs, -1).T + np.diag(lam[0] * Hr)
+    d_shard = -np.linalg.solve(Gs, out[0][nt:] + lam[0] * gr)
+    s, r, q = om.f.ggn_parts(A, y, x)
+    d_full = O.ggn_score_step(A, s, r, q, lam[0] * gr, Hr, lam[0])
+    np.testing.assert_allclose(d_shard, d_full, rtol=1e-9, atol=1e-12)
+    # the step from the sharded direction equals the unsharded step!, group prox included
+    meth = O.ProxGGNSCORE()
+    meth.init(x)
+    x_full, _ = O.step(meth, om, "gl", hm, x, x, om.P, 1)
+    x_shard, _, _ = O._score_finish(meth, om, "gl", hm, x, d_shard, lam[0], lam[0] * gr, Hr, 0.5)
+    np.testing.assert_allclose(x_shard, x_full, rtol=1e-9, atol=1e-12)
+    zs = (x_shard.reshape(ng, gs) == 0).all(axis=1)
+    assert np.array_equal(zs, (x_full.reshape(ng, gs) == 0).all(axis=1))
