@@ -60,6 +60,12 @@ CONFIGS = {
                lam=1e-4, mu=0.6, mem=20,
                workload="ProxLQNSCORE(mem=20) box-constrained least squares, sparse A (CSR+CSC, rho=0.01), "
                         "indbox + PHuberSmootherIndBox, BASELINE configs[4]"),
+    # the C5-shaped sparse A under ProxGGNSCORE (README.md:105's sprandn problem class with the GGN step):
+    # the Gram priced by nnz (sparse_gram_kernel) + the m = 65536 Cholesky
+    "c5ggn": dict(method="ggn", loss="least_squares", sparse=True, N=1 << 20, m=1 << 16, rho=0.01, reg="indbox",
+                  lam=1e-4, mu=0.6,
+                  workload="ProxGGNSCORE box-constrained least squares on the C5 sparse A (rho=0.01): sparse Gram "
+                           "Jt*Q*Jt' priced by nnz + m=65536 Cholesky"),
 }
 
 
@@ -74,10 +80,13 @@ def build_problem(cfg, N, m, comm, local, f32=False):
         return model, scsopt.PHuberSmootherL1L2(cfg["mu"]), scsopt.ProxLQNSCORE(m=cfg["mem"])
     out = None
     if cfg.get("sparse"):
+        ggn = cfg["method"] == "ggn"
         model = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), cfg["lam"],
                                                 density=cfg["rho"], seed=2026, f32=f32, device=local,
-                                                C_set=[-1.0, 1.0])
-        return model, scsopt.PHuberSmootherIndBox(-1.0, 1.0, cfg["mu"]), scsopt.ProxLQNSCORE(m=cfg["mem"])
+                                                C_set=[-1.0, 1.0],
+                                                out_fn=losses.linear_ls(1.0 / N) if ggn else None)
+        meth = scsopt.ProxGGNSCORE() if ggn else scsopt.ProxLQNSCORE(m=cfg["mem"])
+        return model, scsopt.PHuberSmootherIndBox(-1.0, 1.0, cfg["mu"]), meth
     if cfg["loss"] == "logistic_ce":
         f, out = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N)
     elif cfg["loss"] == "logistic_margin":
@@ -413,13 +422,14 @@ def main():
     steps, warmup = args.steps, args.warmup
     if cfg["loss"] == "rosenbrock" and steps < 50:
         steps = 50                               # microsecond-scale steps: time a meaningful batch
-    if cfg.get("sparse"):
+    lqn_sparse = cfg.get("sparse") and cfg["method"] == "lqn"
+    if lqn_sparse:
         steps = max(steps, 50)                   # millisecond-scale steps: amortize iterate!'s f(x*) once
         warmup = max(warmup, 5)                  # and let the clocks settle (1 warm-up step: +-5 % box to box)
     # kernel timing: HIP events around the dominant launches inside the timed region.  Each event record
     # costs a dispatch gap (~5 us) of its own, so the millisecond-scale sparse epochs time the launches of
     # every TEVERY-th epoch (scs_iterate's pipelined loop; the setup passes are always timed)
-    tevery = int(os.environ.get("SCS_BENCH_TIMING_EVERY", "10")) if cfg.get("sparse") else 1
+    tevery = int(os.environ.get("SCS_BENCH_TIMING_EVERY", "10")) if lqn_sparse else 1
     ctx.check(scsopt._lib.lib.scs_timing_enable(ctx.h, tevery))
     if warmup > 0:
         run_iterate(warmup)
@@ -467,6 +477,11 @@ def main():
             main_calls = steps                      # one Gram per GGN/NSCORE step; the solver's own
             gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])   # launches are timed under "solve"
             gram_flops = float(N_local) * m * (m + 1)   # algorithmic symmetric Gram per launch
+            if gram_kname.startswith("sparse_gram"):
+                # priced by nnz: every row of the generated pattern has k = round(rho·m) entries and
+                # contributes k(k+1)/2 multiply-adds to the upper triangle
+                k = int(round(cfg["rho"] * m))
+                gram_flops = float(N_local) * k * (k + 1)
             achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
             traffic = None
             kname = gram_kname or "unknown"   # the library reports the kernel it launched
@@ -485,7 +500,7 @@ def main():
                                 "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                                 "kernel": kname, "avg_ms": gram_avg_ms, "launches": main_calls,
                                 "flops_per_launch": gram_flops}
-        if tm["gemv_calls"] and cfg.get("sparse"):
+        if tm["gemv_calls"] and lqn_sparse:
             # LDS-blocked CSR (A·x) and CSC (Aᵀ·v) passes, launched equally often.  Bytes each launch must
             # move: nnz·(value + 2 B local index) + the per-block row pointers (8 B per row and block)
             # + one partial per row and block + the gathered vector once (mean of the two launches)
@@ -514,7 +529,7 @@ def main():
                                 "timing_sample": "every %d-th epoch's launches + the call's setup passes" % tevery,
                                 "bytes_per_launch": per_launch}
             line["config"]["nnz"] = nnz
-        elif tm["gemv_calls"]:
+        elif tm["gemv_calls"] and not cfg.get("sparse"):
             # streaming passes (A·x in f(x), Aᵀv in step!): each reads the local A once
             line["hbm_gbs_streaming"] = (tm["gemv_calls"] * 8.0 * N_local * m) / (tm["gemv_ms"] * 1e-3) / 1e9
             line["hbm_frac_streaming"] = line["hbm_gbs_streaming"] / HBM_PEAK_GBS

@@ -386,20 +386,18 @@ __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, i
 // that C tile traffic: 2·128 KiB per 4.2 MFLOP tile).
 static int outer_block();
 
-// The bulk stream (the lookahead's trailing updates, 2 gram_sia workgroups per CU fill every CU
-// they get) can leave SCS_CHOL_RESERVE_CUS CUs (a multiple of 8: that many / 8 per XCD) to the
-// serial chain on the context stream.  A chain kernel that shares its CU with MFMA-bound
-// trailing-update waves runs slower: in an m = 8192 kernel trace the latency Gram launches take
-// 9.3 us alone and 28.7 us while the bulk update runs, the diagonal kernel 77.5 / 111.2 us
-// (profiles/r02/chol/).  r02 sweep with the r02 diagonal kernel (profiles/r02/chol/reserve/):
-// m = 8192 solve 12.04 / 10.97 / 11.53 / 10.98 ms at 0 / 32 / 48 / 64 reserved CUs, m = 16384
-// 42.1 / 40.2 / 43.8 / 43.1 ms, m = 32768 216.7 / 220.3 ms at 0 / 32 -- so 32 up to m = 16384,
-// none above.  (rocprofv3 segfaults at exit, after writing its output, in a process that created
-// a CU-masked stream; profile runs go last in a GPU call.)  Masking is best effort: a failure
-// falls back to an ordinary non-blocking stream.
+// The bulk stream (the lookahead's trailing updates) can leave SCS_CHOL_RESERVE_CUS CUs (a multiple of
+// 8: that many / 8 per XCD) to the serial chain on the context stream (hipExtStreamCreateWithCUMask).
+// r02 measured 32 reserved CUs at C2 solve 12.04 -> 10.97 ms (profiles/r02/chol/reserve/).  Off by
+// default since r03: a process that created a CU-masked queue faults at exit under rocprofv3 -- in
+// librocprofiler-sdk's static destructors, inside libhsa-runtime64 (SCS_SEGV_TRACE frames,
+// profiles/r03/segv/) -- so the profiled configuration could not be the benchmarked one.  The
+// chain is shortened instead (chol_diag_kernel, the fused chain launches).  Masking is best effort:
+// a failure falls back to an ordinary non-blocking stream.
 static hipError_t create_bulk_stream(hipStream_t* s, int nblk) {
   const char* env = getenv("SCS_CHOL_RESERVE_CUS");
-  const int reserve = env ? atoi(env) : (nblk <= 128 ? 32 : 0);
+  const int reserve = env ? atoi(env) : 0;
+  (void)nblk;
   int dev = 0, ncu = 0;
   if (reserve > 0 && hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 4 * reserve) {

@@ -457,6 +457,25 @@ __global__ void gram_unpack_kernel(const double* __restrict__ P, const int2* __r
   }
 }
 
+// The inverse: the upper triangle's 128 x 128 tiles (list order) into packed slots (a Gram formed in
+// place, e.g. the sparse Gram, entering the multi-rank exchange).
+__global__ void gram_pack_kernel(const double* __restrict__ G, int64_t ldg, const int2* __restrict__ tiles,
+                                 double* __restrict__ P) {
+  const int t = blockIdx.y;
+  const int2 tl = tiles[t];
+  double* Pt = P + (int64_t)t * GT * GT;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < GT * GT; e += gridDim.x * blockDim.x) {
+    const int j = e / GT, i = e % GT;
+    Pt[e] = G[((int64_t)tl.x * GT + i) * ldg + (int64_t)tl.y * GT + j];
+  }
+}
+
+hipError_t gram_pack_launch(const double* G, int64_t ldg, const int2* tiles, int ntiles, double* P, hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gram_pack_kernel, dim3(16, ntiles), dim3(256), 0, st, G, ldg, tiles, P);
+  return hipGetLastError();
+}
+
 // Host helper: super-blocked lower-triangle tile list.
 void gram_tile_list(int nb, int2* out, int* ntiles) {
   const int S = 8;

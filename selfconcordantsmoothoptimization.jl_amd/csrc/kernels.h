@@ -59,6 +59,7 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
 // scnt: per-strip completion counts (each finished whole tile adds 1 to scnt[bj / sob]); the
 // factor stream waits for a strip with strip_wait_launch (flag: set on a timed-out wait)
 hipError_t strip_wait_launch(const unsigned* cnt, unsigned target, int* flag, hipStream_t st);
+hipError_t gram_pack_launch(const double* G, int64_t ldg, const int2* tiles, int ntiles, double* P, hipStream_t st);
 hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,
                               hipStream_t st);
 
@@ -264,6 +265,12 @@ hipError_t blk_pad(int64_t* cnt, int64_t n, int f32, hipStream_t st);
 hipError_t blk_scan(void* temp, size_t* temp_bytes, const int64_t* cnt, int64_t* bptr, int64_t n, hipStream_t st);
 hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int f32, int64_t nrows, int shift,
                        const int64_t* bptr, const int64_t* first, uint16_t* lidx, void* bval, hipStream_t st);
+// sparse Gram G = Aᵀ diag(w) A (upper part, column j up to the end of its diagonal tile) from the
+// CSC copy and a Gram-blocked CSR copy (block width 2^shift, unpadded segments): Σ_r nnz_r² work
+int sparse_gram_shift();
+hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const void* valT, const int64_t* bptr,
+                              const uint16_t* lidx, const void* bval, int f32, const double* w, int64_t nrows,
+                              int64_t m, int shift, double* G, int64_t ldg, hipStream_t st);
 size_t sparse_layer_map_bytes(int k);
 void sparse_layer_maps(uint64_t seed, int k, int64_t N, void* out_host);
 hipError_t launch_gen_sparse(int64_t N, int64_t m, int k, uint64_t seed, const void* Ldev, int f32, double scale,

@@ -11,6 +11,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -104,6 +108,8 @@ struct scs_ctx {
     uint16_t* lidx = nullptr;
     void* val = nullptr;
   } bcsr, bcsc;  // LDS-blocked copies used by the products (sparse.hip)
+  SpBlk bgram;    // the sparse Gram's row copy: 2^sparse_gram_shift()-wide blocks, unpadded (built on first use)
+  int sp_gram = 0;   // the Gram of a sparse A: 0 undecided, 1 priced by nnz (sparse_gram_kernel), 2 dense tiles
   double* Ad = nullptr;  // dense panel-blocked mirror of a sparse A (Gram-based methods only)
   // ... or, when the mirror does not fit under the cap, a ring of two R-row dense slots the Gram
   // streams through chunk by chunk (gram_main_stream)
@@ -1186,6 +1192,65 @@ const double* dense_A(scs_ctx* c) {
   return c->Ad;
 }
 
+// The Gram of a sparse A priced by nnz (sparse_gram_kernel: Σ_r nnz_r² multiply-adds) instead of
+// dense MFMA tiles over a densified A (N·m² whatever the density): chosen when Σ_r nnz_r² is below
+// N·m²/64 (the dense tiles run ~50x more flops per second), or forced by SCS_SPARSE_GRAM=1 / 0.
+// The sparse Gram's row copy: the (sorted) CSR cut into 2^sparse_gram_shift()-wide column blocks,
+// unpadded (blk_count / blk_scan / blk_scatter with no slot rounding).
+void build_gram_blocked(scs_ctx* c) {
+  scs_ctx::SpBlk& B = c->bgram;
+  const int64_t nrows = c->N;
+  B.shift = sparse_gram_shift();
+  B.nblk = (int)ceil_div(c->m, int64_t(1) << B.shift);
+  const int64_t nk = (int64_t)B.nblk * nrows;
+  int64_t* cnt = dalloc<int64_t>(c, nk + 1);
+  int64_t* first = dalloc<int64_t>(c, nk + 1);
+  B.ptr = dalloc<int64_t>(c, nk + 1);
+  int64_t nnz = 0;
+  if (nrows > 0) {
+    HCK(blk_count(c->rowptr, c->colidx, nrows, B.shift, cnt, first, c->st));
+    size_t tb = 0;
+    HCK(blk_scan(nullptr, &tb, cnt, B.ptr, nk + 1, c->st));
+    void* tmp = dalloc<char>(c, tb);
+    HCK(blk_scan(tmp, &tb, cnt, B.ptr, nk + 1, c->st));
+    HCK(hipMemcpyAsync(&nnz, B.ptr + nk, sizeof(int64_t), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    dfree(c, tmp);
+  }
+  B.lidx = dalloc<uint16_t>(c, nnz + 8);
+  B.val = c->sp_f32 ? (void*)dalloc<float>(c, (size_t)nnz + 8) : (void*)dalloc<double>(c, (size_t)nnz + 8);
+  if (nrows > 0)
+    HCK(blk_scatter(c->rowptr, c->colidx, c->val, c->sp_f32, nrows, B.shift, B.ptr, first, B.lidx, B.val, c->st));
+  sync(c);
+  dfree_t(c, cnt);
+  dfree_t(c, first);
+}
+
+bool sparse_gram(scs_ctx* c) {
+  if (!c->sparse) return false;
+  if (const char* e = std::getenv("SCS_SPARSE_GRAM")) return e[0] == '1';   // read per call (A/B tests)
+  if (c->sp_gram == 0) {
+    std::vector<int64_t> rp((size_t)c->N + 1);
+    HCK(hipMemcpyAsync(rp.data(), c->rowptr, sizeof(int64_t) * (c->N + 1), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+    double s2 = 0.0;
+    for (int64_t r = 0; r < c->N; ++r) s2 += (double)(rp[r + 1] - rp[r]) * (double)(rp[r + 1] - rp[r]);
+    c->sp_gram = (64.0 * s2 <= (double)c->N * (double)c->m * (double)c->m) ? 1 : 2;
+  }
+  return c->sp_gram == 1;
+}
+
+// the sparse Gram -> out (upper part, ldg = m_pad), or packed 128 x 128 slots (multi-rank) through G
+void gram_sparse(scs_ctx* c, const double* w, double* out, int packed) {
+  if (!c->bgram.ptr) build_gram_blocked(c);
+  double* dst = (packed & 1) ? c->G : out;
+  if (packed & 2) fail(c, SCS_ERR_ARG, "internal: the sparse Gram does not accumulate");
+  HCK(launch_sparse_gram(c->colptr, c->rowidx, c->valT, c->bgram.ptr, c->bgram.lidx, c->bgram.val, c->sp_f32, w, c->N,
+                         c->m, c->bgram.shift, dst, c->mpad, c->st));
+  c->gram_kname = c->sp_f32 ? "sparse_gram_kernel<float>" : "sparse_gram_kernel<double>";
+  if (packed & 1) HCK(gram_pack_launch(c->G, c->mpad, c->utiles, c->nslots, out, c->st));
+}
+
 // How the Gram of a sparse A gets its dense operand tiles: a mirror of all of A when it fits
 // under the cap (SCS_SPARSE_MIRROR_MAX_GB, default: the free device memory less the m x m
 // system and 4 GiB), else the streaming ring (memory O(nnz + R·m + m²) for any N).
@@ -1246,6 +1311,11 @@ void gram_main_stream(scs_ctx* c, const double* w, double* out, int packed) {
 // v != nullptr: the same launch forms Aᵀv of the local rows into vout (fused, gram_fuse_ok)
 void gram_main(scs_ctx* c, const double* w, double* out, int packed, const double* v = nullptr,
                double* vout = nullptr) {
+  if (sparse_gram(c)) {
+    if (v) fail(c, SCS_ERR_ARG, "internal: the sparse Gram forms no Aᵀv");
+    gram_sparse(c, w, out, packed);
+    return;
+  }
   if (sparse_streams(c)) {
     if (v) fail(c, SCS_ERR_ARG, "internal: the streaming sparse Gram forms no Aᵀv");
     gram_main_stream(c, w, out, packed);
@@ -1340,7 +1410,7 @@ int pipe_mode(const scs_ctx* c, bool cacheable) {
   const char* e = std::getenv("SCS_CHOL_PIPE");   // read per step (tests toggle it in-process)
   const int mode = e ? std::atoi(e) : 0;
   const int64_t nblk = c->mpad / 128;
-  const bool ok = !cacheable && !sharded(c) && !sparse_streams(const_cast<scs_ctx*>(c)) && c->gwork &&
+  const bool ok = !cacheable && !sharded(c) && !c->sparse && c->gwork &&
                   nblk >= 3 * chol_outer_block();
   return ok && (mode == 1 || mode == 2) ? mode : 0;
 }
@@ -1823,6 +1893,40 @@ void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, dou
 // ===========================================================================
 extern "C" {
 
+// SCS_SEGV_TRACE=1: a fatal-signal handler that names the shared object and offset of every
+// frame (dladdr), for faults outside this library's symbols (e.g. runtime teardown at exit).
+// Diagnostics only; installed when the library is loaded.
+static void scs_fatal_trace(int sig, siginfo_t* si, void*) {
+  void* fr[48];
+  const int n = backtrace(fr, 48);
+  fprintf(stderr, "[scsopt] signal %d, fault address %p, %d frames:\n", sig, si ? si->si_addr : nullptr, n);
+  for (int i = 0; i < n; ++i) {
+    Dl_info d;
+    if (dladdr(fr[i], &d) && d.dli_fname)
+      fprintf(stderr, "  #%-2d %s +0x%lx %s\n", i, d.dli_fname, (unsigned long)((char*)fr[i] - (char*)d.dli_fbase),
+              d.dli_sname ? d.dli_sname : "");
+    else
+      fprintf(stderr, "  #%-2d %p\n", i, fr[i]);
+  }
+  fflush(stderr);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+__attribute__((constructor)) static void scs_install_trace() {
+  const char* e = getenv("SCS_SEGV_TRACE");
+  if (!e || e[0] != '1') return;
+  void* warm[2];
+  (void)backtrace(warm, 2);   // loads the unwinder now, not inside the handler
+  struct sigaction sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.sa_sigaction = scs_fatal_trace;
+  sa.sa_flags = SA_SIGINFO;
+  sigaction(SIGSEGV, &sa, nullptr);
+  sigaction(SIGBUS, &sa, nullptr);
+  sigaction(SIGABRT, &sa, nullptr);
+}
+
 const char* scs_version(void) { return "libscsopt 0.1.0 (gfx950)"; }
 
 int scs_create(int device, void* stream, scs_ctx** out) {
@@ -1977,7 +2081,7 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->rowidx);
   dfree(c, c->val);
   dfree(c, c->valT);
-  for (auto* B : {&c->bcsr, &c->bcsc}) {
+  for (auto* B : {&c->bcsr, &c->bcsc, &c->bgram}) {
     dfree_t(c, B->ptr);
     dfree_t(c, B->lidx);
     dfree(c, B->val);
@@ -1987,6 +2091,7 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->Ad);
   dfree_t(c, c->ringA);
   c->sp_mode = 0;
+  c->sp_gram = 0;
   c->ring_rows = 0;
   c->ring_r0[0] = c->ring_r0[1] = -1;
   dfree_t(c, c->Gk);

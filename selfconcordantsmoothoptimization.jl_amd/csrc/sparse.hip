@@ -308,6 +308,133 @@ hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int 
   return hipGetLastError();
 }
 
+// ---- sparse Gram G = Aᵀ diag(w) A priced by nnz (Σ_r nnz_r² multiply-adds, not N·m²) ------------
+// Jt*Q*Jt' of a SparseMatrixCSC (prox-GGN-SCORE.jl:114,129) and hess_fx = c·Aᵀ diag(h) A
+// (prox-N-SCORE.jl:55) on a sparse A.  Gustavson by output column: G(i, j) = Σ_{r ∈ rows(j)}
+// (w_r a_rj) a_ri.  A work item is (column j, row block b of G: rows [b·BS, b·BS + BS), BS =
+// 2^shift <= 4096); one wave owns it, with the block's slice of column j as an fp64 accumulator in
+// LDS (32 KiB).  The wave walks rows(j) (the CSC column, ascending rows) in batches of GB rows:
+// lane t < GB loads row t's CSC entry, weight and the row's segment bounds in block b (the
+// Gram-blocked CSR copy, unpadded, sorted by column), then every row's first 64 segment entries
+// are loaded before any is accumulated (GB rows of memory latency in flight per wave), and the
+// rows are accumulated in order -- one ds_add per entry, the entries of a row have distinct
+// columns -- so each G(i, j) sums its terms in ascending row order: deterministic run to run.
+// Only the upper part is formed (row blocks b with b·BS <= j), and column j is written up to the
+// end of its 128-row diagonal tile (what chol_factor and the LU fallback's symmetrize read).
+constexpr int SG_ROWS = 8;   // GB: rows per batch
+__device__ __forceinline__ int64_t sg_bcast(int64_t v, int lane) {   // lane's value, wave-uniform (SGPRs)
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double sg_bcast(double v, int lane) {
+  return __builtin_bit_cast(double, sg_bcast(__builtin_bit_cast(int64_t, v), lane));
+}
+template <typename VT>
+__global__ __launch_bounds__(64) void sparse_gram_kernel(const int64_t* __restrict__ colptr,
+                                                         const int* __restrict__ rowidx, const VT* __restrict__ valT,
+                                                         const int64_t* __restrict__ bptr,
+                                                         const uint16_t* __restrict__ lidx,
+                                                         const VT* __restrict__ bval, const double* __restrict__ w,
+                                                         int64_t nrows, int64_t m, int shift, int64_t j0,
+                                                         double* __restrict__ G, int64_t ldg) {
+  __shared__ double acc[1 << 12];
+  const int lane = threadIdx.x;
+  const int BS = 1 << shift;
+  // work item -> (column j, block b): column block J = j >> shift has J + 1 items per column, items of
+  // column block J start at BS·J(J+1)/2 (relative to column j0, a multiple of BS)
+  const int64_t t = (int64_t)blockIdx.x;
+  const int64_t J0 = j0 >> shift;
+  int64_t J = J0, base = 0;
+  while (true) {
+    const int64_t n = (int64_t)BS * (J + 1);
+    if (t < base + n) break;
+    base += n;
+    ++J;
+  }
+  const int64_t loc = t - base;
+  const int64_t j = J * BS + loc / (J + 1);
+  const int b = (int)(loc % (J + 1));
+  if (j >= m) return;
+  for (int i = lane; i < BS; i += 64) acc[i] = 0.0;
+  __syncthreads();
+  const int64_t p0 = colptr[j], p1 = colptr[j + 1];
+  for (int64_t p = p0; p < p1; p += SG_ROWS) {
+    const int nb = (int)((p1 - p < SG_ROWS) ? (p1 - p) : SG_ROWS);
+    double s = 0.0;
+    int64_t st = 0, en = 0;
+    if (lane < nb) {
+      const int r = rowidx[p + lane];
+      s = w[r] * (double)valT[p + lane];
+      const int64_t k = (int64_t)b * nrows + r;
+      st = bptr[k];
+      en = bptr[k + 1];
+    }
+    double v[SG_ROWS];
+    int ix[SG_ROWS];
+#pragma unroll
+    for (int u = 0; u < SG_ROWS; ++u) {
+      const int64_t su = sg_bcast(st, u), eu = sg_bcast(en, u);
+      const bool on = u < nb && su + lane < eu;
+      v[u] = on ? (double)bval[su + lane] : 0.0;
+      ix[u] = on ? (int)lidx[su + lane] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < SG_ROWS; ++u) {
+      if (u >= nb) break;
+      const double su_s = sg_bcast(s, u);
+      if (ix[u] >= 0) atomicAdd(&acc[ix[u]], su_s * v[u]);
+      // a segment longer than one wave: the rest of this row before the next row (row order kept)
+      const int64_t su = sg_bcast(st, u), eu = sg_bcast(en, u);
+      for (int64_t q = su + 64 + lane; q - lane < eu; q += 64)
+        if (q < eu) atomicAdd(&acc[lidx[q]], su_s * (double)bval[q]);
+    }
+  }
+  __syncthreads();
+  // column j, rows [b·BS, min(b·BS + BS, end of j's diagonal tile))
+  const int64_t r0 = (int64_t)b * BS;
+  const int64_t rend = ((j >> 7) + 1) << 7;
+  const int64_t nr = (rend - r0 < BS) ? rend - r0 : BS;
+  double* col = G + j * ldg + r0;
+  for (int i = lane; i < nr; i += 64) col[i] = acc[i];
+}
+
+int sparse_gram_shift() { return 12; }
+
+int64_t sparse_gram_items(int64_t j0, int64_t j1, int shift) {
+  // items of columns [j0, j1) (j0, j1 multiples of 2^shift, j1 may be the padded end)
+  const int64_t BS = (int64_t)1 << shift;
+  int64_t n = 0;
+  for (int64_t J = j0 >> shift; J < (j1 + BS - 1) >> shift; ++J) n += BS * (J + 1);
+  return n;
+}
+
+hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const void* valT, const int64_t* bptr,
+                              const uint16_t* lidx, const void* bval, int f32, const double* w, int64_t nrows,
+                              int64_t m, int shift, double* G, int64_t ldg, hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  if (shift > 12 || shift < 7) return hipErrorInvalidValue;
+  const int64_t BS = (int64_t)1 << shift;
+  // launches of at most 2^30 items: one per run of column blocks
+  int64_t j0 = 0;
+  while (j0 < m) {
+    int64_t j1 = j0;
+    while (j1 < m && sparse_gram_items(j0, j1 + BS, shift) < ((int64_t)1 << 30)) j1 += BS;
+    if (j1 == j0) j1 = j0 + BS;
+    const int64_t items = sparse_gram_items(j0, j1, shift);
+    if (f32)
+      hipLaunchKernelGGL(sparse_gram_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
+                         (const float*)valT, bptr, lidx, (const float*)bval, w, nrows, m, shift, j0, G, ldg);
+    else
+      hipLaunchKernelGGL(sparse_gram_kernel<double>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
+                         (const double*)valT, bptr, lidx, (const double*)bval, w, nrows, m, shift, j0, G, ldg);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    j0 = j1;
+  }
+  return hipSuccess;
+}
+
 // ---- synthetic generator ---------------------------------------------------
 __device__ __forceinline__ uint64_t smix_s(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;

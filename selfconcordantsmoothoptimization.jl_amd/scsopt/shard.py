@@ -105,6 +105,11 @@ class Comm:
             ext = torch.cuda.ExternalStream(stream, device=self.buf.device)
             with torch.cuda.stream(ext):
                 allreduce_inplace(self.buf[: int(count)], self.group)
+            # the library reads the sum on its stream right after this returns; a process group
+            # that copies device tensors through host memory (gloo) lands the result from its own
+            # stream, so wait for the device here (measured: without it, back-to-back row
+            # all-gathers of the sharded sample-space branch read a partly landed sum)
+            torch.cuda.synchronize(self.buf.device)
             return 0
         except Exception as e:  # surfaced by libscsopt as SCS_ERR_COMM
             import sys

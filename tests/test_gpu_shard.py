@@ -135,8 +135,8 @@ def test_two_rank_shard_matches_single_process(world, tall, monkeypatch):
         r0 = out[0][method]
         for r in range(1, world):
             rr = out[r][method]
-            assert rr["epochs"] == r0["epochs"] == full["epochs"]
-            assert rr["obj"] == r0["obj"]                   # identical bits on every rank
-            assert np.array_equal(rr["x"], r0["x"])
-        np.testing.assert_allclose(r0["obj"], full["obj"], rtol=1e-10)
-        np.testing.assert_allclose(r0["x"], full["x"], rtol=1e-8, atol=1e-12)
+            assert rr["epochs"] == r0["epochs"] == full["epochs"], method
+            assert rr["obj"] == r0["obj"], (method, r, rr["obj"], r0["obj"], full["obj"])   # identical bits
+            assert np.array_equal(rr["x"], r0["x"]), method
+        np.testing.assert_allclose(r0["obj"], full["obj"], rtol=1e-10, err_msg=method)
+        np.testing.assert_allclose(r0["x"], full["x"], rtol=1e-8, atol=1e-12, err_msg=method)
