@@ -69,7 +69,7 @@ CONFIGS = {
 }
 
 
-def build_problem(cfg, N, m, comm, local, f32=False):
+def build_problem(cfg, N, m, comm, local, f32=False, devices=None):
     import numpy as np
     import scsopt
     from scsopt import losses
@@ -94,7 +94,7 @@ def build_problem(cfg, N, m, comm, local, f32=False):
     else:
         f, out = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N)
     model = scsopt.Problem.synthetic(N, m, x0, f, 1.0, kind=cfg["kind"], seed=2026, density=0.1, out_fn=out,
-                                     device=local, comm=comm)
+                                     device=local, comm=comm, devices=devices)
     g0 = model.gradx(np.zeros(m))
     if cfg["reg"] == "gl":
         gs = cfg["group"]
@@ -337,12 +337,20 @@ def main():
     ap.add_argument("--cpu-ms", type=int, default=4096)
     ap.add_argument("--share-device", action="store_true",
                     help="let ranks share GPUs round-robin (launcher rehearsal on a small box; --comm torch)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="--gpus N from ONE process: a multi-device context (scs_create_multi) splits the rows "
+                         "across GPUs 0..N-1 and runs one host thread per device (the Julia drop-in's mode)")
     ap.add_argument("--plumbing-check", action="store_true",
                     help="launch the ranks and check their world wiring over gloo, no GPU work")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
     world, rank, local, spawn = world_from_env(args, os.environ)
+    single = args.single_process and args.gpus > 1
+    if single:
+        if "WORLD_SIZE" in os.environ:
+            raise SystemExit("--single-process runs without a launcher (one process drives the GPUs)")
+        world, spawn = 1, False
     if spawn:
         # --gpus N without a launcher: the N rank processes are started here, before any GPU call
         # (counting devices does not initialise the GPU)
@@ -369,8 +377,11 @@ def main():
 
     comm = None
     ndev = torch.cuda.device_count()
-    if world > 1:
+    if world > 1 or single:
         check_devices(args, ndev)
+    devices = list(range(args.gpus)) if single else None
+    if single and (cfg.get("sparse") or cfg["loss"] == "rosenbrock"):
+        raise SystemExit("--single-process shards a dense A (c2, c3, c4)")
     dev = local % max(1, ndev) if args.share_device else local
     gloo = args.comm == "torch"
     if world > 1 or args.force_comm:
@@ -389,7 +400,7 @@ def main():
         comm = shard.Comm(device=torch.device("cuda", dev), native=not gloo, force=args.force_comm)
     if not cfg.get("sparse") and cfg["loss"] != "rosenbrock":
         # fail fast, before generating anything, when the local shard does not fit this GPU
-        plan = memory_plan(cfg, N, m, world, gram_cache=args.gram_cache)
+        plan = memory_plan(cfg, N, m, args.gpus if single else world, gram_cache=args.gram_cache)
         sharing = -(-world // max(1, ndev)) if args.share_device else 1
         free, _total = torch.cuda.mem_get_info(dev)
         if plan["total"] * sharing > 0.97 * free:
@@ -397,7 +408,7 @@ def main():
                              f"{plan['total'] * sharing / GIB:.1f} GiB on GPU {dev} ({plan_text(plan)}; "
                              f"{plan['rows_per_rank']} rows per rank), {free / GIB:.1f} GiB free: "
                              f"use more GPUs (--gpus) or a smaller --N")
-    model, hmu, method = build_problem(cfg, N, m, comm, dev, f32=args.f32)
+    model, hmu, method = build_problem(cfg, N, m, comm, dev, f32=args.f32, devices=devices)
     reg = cfg["reg"]
     if args.gram_cache:
         if cfg["loss"] != "least_squares" or cfg["method"] == "lqn":
@@ -448,23 +459,25 @@ def main():
         dt = float(t.item())
 
     check = None
-    if rank == 0 and not cfg.get("sparse") and cfg["loss"] != "rosenbrock" and not args.no_check:
-        check = sampled_gram_check(model, m)
+    if rank == 0 and not cfg.get("sparse") and cfg["loss"] != "rosenbrock" and not args.no_check and not single:
+        check = sampled_gram_check(model, m)   # kernel-level entry points: single-device contexts
     if rank == 0 and cfg.get("sparse") and not args.no_check:
         check = sparse_check(model, np.asarray(sol.x, dtype=np.float64))
 
     if rank == 0:
         ms_step = 1e3 * dt / steps
         value = steps / dt
-        N_local = model.N
+        N_local = -(-model.N // args.gpus) if single else model.N   # device 0's rows (row_range)
         line = {
             "metric": METRIC if args.config == "c3" else f"iterate!() iterations/sec, {cfg['workload']}",
-            "value": value, "unit": "iterations/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "value": value, "unit": "iterations/s", "n_gpus": args.gpus if single else world, "steps": steps,
+            "warmup": warmup,
             "ms_per_step": ms_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": ("f64 (fp32-stored A values)" if args.f32 else "f64"), "data": "synthetic (on-device counter RNG: A ~ N(0,1)/sqrt(m), y from a sparse x_true)",
             "config": {"workload": cfg["workload"], "N": N, "m": m, "lambda": model.λ, "mu": hmu.mu,
                        "method": type(method).__name__, "ss_type": method.ss_type,
-                       "parallelism": f"row-shard x{world}",
+                       "parallelism": (f"row-shard x{args.gpus} (one process, scs_create_multi)" if single
+                                       else f"row-shard x{world}"),
                        "devices": min(world, ndev) if args.share_device else world,
                        "exchange": (("rccl (libscsopt)" if args.comm == "rccl"
                                      else "torch.distributed callback (gloo)")
@@ -529,6 +542,16 @@ def main():
                                 "timing_sample": "every %d-th epoch's launches + the call's setup passes" % tevery,
                                 "bytes_per_launch": per_launch}
             line["config"]["nnz"] = nnz
+            if args.f32:
+                # the full-size fp32-vs-fp64 study of this configuration (tools/c5_tolerance.py): the fp32
+                # arm stores A's values in fp32 and computes in fp64 -- a storage study
+                tol = os.path.join(ROOT, "profiles", "r03", "c5", "tolerance.json")
+                if os.path.exists(tol) and N == 1 << 20 and m == 1 << 16:
+                    with open(tol) as f:
+                        ts = json.load(f)
+                    line["tolerance_study"] = {k: ts[k] for k in ("max_rel_dobj", "max_dx_inf", "max_active_diff")}
+                    line["tolerance_study"].update(epochs=ts["config"]["epochs"], source=os.path.relpath(tol, ROOT),
+                                                   arms=ts["arms"])
         elif tm["gemv_calls"] and not cfg.get("sparse"):
             # streaming passes (A·x in f(x), Aᵀv in step!): each reads the local A once
             line["hbm_gbs_streaming"] = (tm["gemv_calls"] * 8.0 * N_local * m) / (tm["gemv_ms"] * 1e-3) / 1e9
@@ -548,7 +571,7 @@ def main():
         line["objective_last"] = objs[-1]
         if check is not None:
             line["parity_check"] = check
-        do_cpu = not args.no_cpu_baseline and world == 1   # the CPU baseline: rank 0 at N = 1 only
+        do_cpu = not args.no_cpu_baseline and world == 1 and not single   # the CPU baseline: rank 0 at N = 1 only
         if do_cpu and args.config == "c1":
             try:
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline_c1.py")],

@@ -113,6 +113,20 @@ const char* scs_version(void);
  * NULL to create one.                                                       */
 int scs_create(int device, void* stream, scs_ctx** out);
 int scs_destroy(scs_ctx* ctx);
+/* One process, several GPUs (the reference's iterate! is one process, iterate.jl:56-76): a context
+ * over devs[0..ndev) that splits the problem's rows across them (contiguous balanced blocks, the
+ * first N % ndev devices one more row -- the blocks of one process per GPU), with an RCCL
+ * communicator over the devices (ncclCommInitAll; one GPU each).  scs_set_data / scs_gen_data
+ * take the WHOLE problem (N_global = N, row0 = 0); the problem / method / step / loop entry
+ * points (scs_set_loss ... scs_iterate, scs_eval_*, scs_step*, scs_set_batches, timing) run on
+ * every device at once, one host thread each, and return device 0's results (every device
+ * holds the same replicated x and m-vectors).  scs_get_data gathers rows across devices;
+ * kernel-level entry points and sparse data take a single-device context (SCS_ERR_ARG).
+ * ndev = 1 is a plain one-device run.  A device that fails inside a collective aborts the
+ * communicators (then every call returns SCS_ERR_COMM: destroy the context).                 */
+int scs_create_multi(const int* devs, int ndev, scs_ctx** out);
+/* Devices of a context (1 for scs_create).                                                   */
+int scs_group_size(scs_ctx* ctx, int* ndev);
 const char* scs_last_error(const scs_ctx* ctx);
 int scs_get_stream(scs_ctx* ctx, void** stream);
 

@@ -23,13 +23,16 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
 #include "../../include/scsopt.h"
 #include "common.h"
 #include "kernels.h"
+#include "shard_plan.h"
 
 using namespace scs;
 
@@ -287,6 +290,14 @@ struct scs_ctx {
   int64_t tcalls[T_N] = {0, 0, 0, 0, 0};
 
   std::vector<DevBuf> allocs;
+
+  // a multi-device context (scs_create_multi): one sub-context per device holding its row block
+  // (row_plan), one RCCL communicator over the devices (ncclCommInitAll); the entry points a group
+  // supports run on every sub-context at once, one host thread each (group_run)
+  std::vector<scs_ctx*> subs;
+  std::vector<RowBlock> plan;
+  int64_t grpN = 0, grpm = 0;   // the whole problem's rows and columns
+  bool group_broken = false;
 };
 
 // ---------------------------------------------------------------------------
@@ -329,6 +340,10 @@ void set_err(scs_ctx* c, const char* fmt, ...) {
 template <class F>
 int guarded(scs_ctx* c, F&& f) {
   if (!c) return SCS_ERR_ARG;
+  if (!c->subs.empty()) {   // the group-aware entry points branch to group_* before this
+    c->err = "this entry point takes a single-device context (scs_create), not a multi-device one";
+    return SCS_ERR_ARG;
+  }
   try {
     c->err.clear();
     f();
@@ -1888,6 +1903,22 @@ void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, dou
 
 }  // namespace
 
+namespace {
+bool is_group(const scs_ctx* c);
+template <class F>
+int group_run(scs_ctx* g, F&& f);
+int group_destroy(scs_ctx* g);
+int group_set_data(scs_ctx* g, int64_t N, int64_t m, const double* A, int64_t lda, const double* y, int64_t Nglob,
+                   int64_t row0);
+int group_gen_data(scs_ctx* g, const scs_synth* sp);
+int group_get_data(scs_ctx* g, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y);
+int group_eval(scs_ctx* g, const double* x, double* out, int64_t nout, int (*fn)(scs_ctx*, const double*, double*));
+int group_step(scs_ctx* g, const double* x, const double* x_prev, int64_t iter, const double* grad_fx, double* x_new,
+               double* dx, double* pri);
+int group_iterate(scs_ctx* g, const double* x0, const double* x_star, int64_t max_epoch, double x_tol, double f_tol,
+                  int rel_kind, double* x_out, const scs_history* h, int64_t* n_hist, int64_t* epochs);
+}  // namespace
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -1952,6 +1983,7 @@ int scs_create(int device, void* stream, scs_ctx** out) {
 }
 
 int scs_destroy(scs_ctx* c) {
+  if (is_group(c)) return group_destroy(c);
   if (!c) return SCS_OK;
   (void)hipSetDevice(c->dev);
   (void)hipStreamSynchronize(c->st);
@@ -1982,6 +2014,7 @@ int scs_destroy(scs_ctx* c) {
 const char* scs_last_error(const scs_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int scs_get_stream(scs_ctx* c, void** stream) {
+  if (is_group(c)) return (*stream = (void*)c->st), SCS_OK;
   return guarded(c, [&] { *stream = (void*)c->st; });
 }
 
@@ -2032,6 +2065,7 @@ int scs_set_comm_rccl(scs_ctx* c, int rank, int nranks, const void* id) {
 }
 
 int scs_set_comm_force(scs_ctx* c, int on) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_comm_force(s_, on); });
   return guarded(c, [&] {
     if (on && !c->rccl && !c->ar) fail(c, SCS_ERR_STATE, "scs_set_comm_force needs a communicator");
     c->comm_force = on != 0;
@@ -2137,6 +2171,7 @@ static void reset_data(scs_ctx* c) {
 
 int scs_set_data(scs_ctx* c, int64_t N, int64_t m, const double* A, int64_t lda, const double* y, int64_t Nglob,
                  int64_t row0) {
+  if (is_group(c)) return group_set_data(c, N, m, A, lda, y, Nglob, row0);
   return guarded(c, [&] {
     HCK(hipSetDevice(c->dev));
     reset_data(c);
@@ -2163,6 +2198,7 @@ int scs_set_data(scs_ctx* c, int64_t N, int64_t m, const double* A, int64_t lda,
 }
 
 int scs_gen_data(scs_ctx* c, const scs_synth* s) {
+  if (is_group(c)) return group_gen_data(c, s);
   return guarded(c, [&] {
     if (!s) fail(c, SCS_ERR_ARG, "null synth spec");
     HCK(hipSetDevice(c->dev));
@@ -2184,6 +2220,7 @@ int scs_gen_data(scs_ctx* c, const scs_synth* s) {
 }
 
 int scs_get_data(scs_ctx* c, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y) {
+  if (is_group(c)) return group_get_data(c, r0, nr, A, lda_out, y);
   return guarded(c, [&] {
     if (!c->has_data || c->generic) fail(c, SCS_ERR_STATE, "no data");
     if (c->sparse && A) fail(c, SCS_ERR_ARG, "sparse A: use scs_get_sparse");
@@ -2206,6 +2243,13 @@ int scs_get_data(scs_ctx* c, int64_t r0, int64_t nr, double* A, int64_t lda_out,
 }
 
 int scs_get_dims(scs_ctx* c, int64_t* N, int64_t* m, int64_t* Ng, int64_t* r0) {
+  if (is_group(c)) {   // the group holds the whole problem
+    if (N) *N = c->grpN;
+    if (m) *m = c->grpm;
+    if (Ng) *Ng = c->grpN;
+    if (r0) *r0 = 0;
+    return SCS_OK;
+  }
   return guarded(c, [&] {
     if (N) *N = c->N;
     if (m) *m = c->m;
@@ -2407,6 +2451,7 @@ int scs_get_sparse(scs_ctx* c, int64_t* rowptr, int32_t* colidx, double* val) {
 }
 
 int scs_set_loss(scs_ctx* c, int loss, int ggn, double scale) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_loss(s_, loss, ggn, scale); });
   return guarded(c, [&] {
     if (loss < SCS_LOSS_LOGISTIC_MARGIN || loss > SCS_LOSS_CALLBACK) fail(c, SCS_ERR_ARG, "unknown loss %d", loss);
     if (ggn < SCS_GGN_NONE || ggn > SCS_GGN_LINEAR_LS) fail(c, SCS_ERR_ARG, "unknown ggn kind %d", ggn);
@@ -2458,6 +2503,7 @@ static double* upload_bounds(scs_ctx* c, double* old, const double* v, int64_t n
 
 int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* lb, const double* ub, int64_t nbound,
                 const int64_t* ind, int64_t ngroups) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_reg(s_, reg, lam, nlam, lb, ub, nbound, ind, ngroups); });
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the regularizer");
     if (reg < SCS_REG_L1 || reg > SCS_REG_GL) fail(c, SCS_ERR_REF, "reg_name not valid.");
@@ -2517,6 +2563,7 @@ int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* 
 }
 
 int scs_set_gram_cache(scs_ctx* c, int on) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_gram_cache(s_, on); });
   return guarded(c, [&] {
     c->gram_cache = on ? 1 : 0;
     ++c->data_gen;
@@ -2525,6 +2572,7 @@ int scs_set_gram_cache(scs_ctx* c, int on) {
 }
 
 int scs_set_group_map(scs_ctx* c, const int64_t* G, int64_t ntotal) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_group_map(s_, G, ntotal); });
   return guarded(c, [&] {
     if (!c->reg_set || c->reg != SCS_REG_GL) fail(c, SCS_ERR_STATE, "scs_set_group_map needs reg gl set first");
     if (!G || ntotal != c->m)
@@ -2549,6 +2597,7 @@ int scs_set_group_map(scs_ctx* c, const int64_t* G, int64_t ntotal) {
 
 int scs_set_smoother(scs_ctx* c, int kind, double mu, double Mh, double nu, const double* lb, const double* ub,
                      int64_t nbound) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_smoother(s_, kind, mu, Mh, nu, lb, ub, nbound); });
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the smoother");
     if (kind < SCS_SMOOTH_PHUBER_L1L2 || kind > SCS_SMOOTH_OSBA_GL) fail(c, SCS_ERR_ARG, "unknown smoother %d", kind);
@@ -2571,6 +2620,7 @@ int scs_set_smoother(scs_ctx* c, int kind, double mu, double Mh, double nu, cons
 }
 
 int scs_set_L(scs_ctx* c, int has_L, double L) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_L(s_, has_L, L); });
   return guarded(c, [&] {
     c->has_L = has_L != 0;
     c->L = L;
@@ -2578,6 +2628,7 @@ int scs_set_L(scs_ctx* c, int has_L, double L) {
 }
 
 int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_method_init(s_, method, ss_type, use_prox, mem); });
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "set the data before the method");
     if (method < SCS_PROX_NSCORE || method > SCS_PROX_LQNSCORE) fail(c, SCS_ERR_ARG, "unknown method %d", method);
@@ -2617,6 +2668,7 @@ int scs_method_init(scs_ctx* c, int method, int ss_type, int use_prox, int mem) 
 }
 
 int scs_eval_f(scs_ctx* c, const double* x, double* fval) {
+  if (is_group(c)) return group_eval(c, x, fval, 1, scs_eval_f);
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
     if (!c->loss_set) fail(c, SCS_ERR_STATE, "no loss: call scs_set_loss first");
@@ -2627,6 +2679,7 @@ int scs_eval_f(scs_ctx* c, const double* x, double* fval) {
 }
 
 int scs_eval_grad(scs_ctx* c, const double* x, double* g) {
+  if (is_group(c)) return group_eval(c, x, g, c->grpm, scs_eval_grad);
   return guarded(c, [&] {
     if (!c->has_data) fail(c, SCS_ERR_STATE, "no data: call scs_set_data / scs_gen_data first");
     if (!c->loss_set) fail(c, SCS_ERR_STATE, "no loss: call scs_set_loss first");
@@ -2639,6 +2692,7 @@ int scs_eval_grad(scs_ctx* c, const double* x, double* g) {
 }
 
 int scs_eval_reg(scs_ctx* c, const double* x, double* gval) {
+  if (is_group(c)) return group_eval(c, x, gval, 1, scs_eval_reg);
   return guarded(c, [&] {
     require_ready(c, false);
     HCK(hipSetDevice(c->dev));
@@ -2648,6 +2702,7 @@ int scs_eval_reg(scs_ctx* c, const double* x, double* gval) {
 }
 
 int scs_set_batches(scs_ctx* c, const int64_t* rows, const int64_t* offsets, int64_t nbatch) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_batches(s_, rows, offsets, nbatch); });
   return guarded(c, [&] {
     HCK(hipSetDevice(c->dev));
     sync(c);
@@ -2683,6 +2738,7 @@ int scs_set_batches(scs_ctx* c, const int64_t* rows, const int64_t* offsets, int
 }
 
 int scs_select_batch(scs_ctx* c, int64_t b) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_select_batch(s_, b); });
   return guarded(c, [&] {
     const int64_t nb = c->boff.empty() ? 0 : (int64_t)c->boff.size() - 1;
     if (b < -1 || b >= nb) fail(c, SCS_ERR_ARG, "scs_select_batch: batch %lld of %lld", (long long)b, (long long)nb);
@@ -2734,11 +2790,13 @@ static void step_call(scs_ctx* c, const double* x, const double* x_prev, int64_t
 
 int scs_step(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, double* x_new, double* dx,
              double* pri) {
+  if (is_group(c)) return group_step(c, x, x_prev, iter, nullptr, x_new, dx, pri);
   return guarded(c, [&] { step_call(c, x, x_prev, iter, nullptr, x_new, dx, pri); });
 }
 
 int scs_step_grad(scs_ctx* c, const double* x, const double* x_prev, int64_t iter, const double* grad_fx,
                   double* x_new, double* dx, double* pri) {
+  if (is_group(c)) return group_step(c, x, x_prev, iter, grad_fx, x_new, dx, pri);
   return guarded(c, [&] { step_call(c, x, x_prev, iter, grad_fx, x_new, dx, pri); });
 }
 
@@ -2750,6 +2808,7 @@ int scs_step_grad(scs_ctx* c, const double* x, const double* x_prev, int64_t ite
 // `nothing` (NaN here).  Termination uses the pre-step f_rel_error (:234, :257).
 int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_epoch, double x_tol, double f_tol,
                 int rel_kind, double* x_out, const scs_history* h, int64_t* n_hist, int64_t* epochs_out) {
+  if (is_group(c)) return group_iterate(c, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, x_out, h, n_hist, epochs_out);
   return guarded(c, [&] {
     require_ready(c, true);
     if (!x0 || !x_star || !x_out || !h || !n_hist || !epochs_out) fail(c, SCS_ERR_ARG, "scs_iterate: null argument");
@@ -3181,6 +3240,7 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
 }
 
 int scs_smoother_eval(scs_ctx* c, const double* x, double* gr, double* Hr) {
+  if (is_group(c)) return scs_smoother_eval(c->subs[0], x, gr, Hr);   // m-space, no exchange
   return guarded(c, [&] {
     if (!c->smooth_set) fail(c, SCS_ERR_STATE, "no smoother");
     h2d(c, c->xn, x, c->m);
@@ -3192,6 +3252,7 @@ int scs_smoother_eval(scs_ctx* c, const double* x, double* gr, double* Hr) {
 }
 
 int scs_prox_eval(scs_ctx* c, const double* z, const double* Hr, double lam, double alpha, double* out) {
+  if (is_group(c)) return scs_prox_eval(c->subs[0], z, Hr, lam, alpha, out);
   return guarded(c, [&] {
     if (!c->reg_set) fail(c, SCS_ERR_STATE, "no regularizer");
     h2d(c, c->zb, z, c->m);
@@ -3385,6 +3446,7 @@ int scs_gemv_n_eval(scs_ctx* c, const double* x, double* out) {
 }
 
 int scs_timing_enable(scs_ctx* c, int on) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_timing_enable(s_, on); });
   return guarded(c, [&] {
     c->timing = on != 0;
     c->timing_every = on > 1 ? on : 1;
@@ -3392,6 +3454,7 @@ int scs_timing_enable(scs_ctx* c, int on) {
 }
 
 int scs_timing_get(scs_ctx* c, scs_timing* t) {
+  if (is_group(c)) return scs_timing_get(c->subs[0], t);   // device 0's accumulators
   return guarded(c, [&] {
     tresolve(c);
     t->gram_ms = c->tms[T_GRAM];
@@ -3408,6 +3471,7 @@ int scs_timing_get(scs_ctx* c, scs_timing* t) {
 }
 
 int scs_kernel_names(scs_ctx* c, char* gram, int64_t gram_cap, char* product, int64_t product_cap) {
+  if (is_group(c)) return scs_kernel_names(c->subs[0], gram, gram_cap, product, product_cap);
   return guarded(c, [&] {
     auto put = [](char* dst, int64_t cap, const std::string& v) {
       if (!dst || cap <= 0) return;
@@ -3421,6 +3485,7 @@ int scs_kernel_names(scs_ctx* c, char* gram, int64_t gram_cap, char* product, in
 }
 
 int scs_timing_reset(scs_ctx* c) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_timing_reset(s_); });
   return guarded(c, [&] {
     tresolve(c);
     for (int i = 0; i < T_N; ++i) {
@@ -3431,7 +3496,232 @@ int scs_timing_reset(scs_ctx* c) {
 }
 
 int scs_sync(scs_ctx* c) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_sync(s_); });
   return guarded(c, [&] { sync(c); });
 }
 
 }  // extern "C"
+
+// ===========================================================================
+// Multi-device contexts (scs_create_multi): one process drives several GPUs
+// ===========================================================================
+// The reference's iterate! is one process (iterate.jl:56-76; no MPI / Distributed), so a Julia
+// caller gets the node's GPUs from one DeviceProblem(...; devices): the library splits the rows
+// (row_plan, the same blocks as one process per GPU), gives every device a sub-context with its
+// rows and an RCCL communicator from ncclCommInitAll, and runs each supported call on all
+// sub-contexts at once -- one host thread per device, since the step's exchange is a collective
+// every device must enter.  Every sub-context computes the same replicated m-vectors with the same
+// bits, so outputs are device 0's.
+namespace {
+
+// run f(sub, i) on every sub-context, one host thread each; the first failing device's code and
+// message become the group's.  A device that fails while the others may be waiting inside a
+// collective aborts the communicators after a grace period, so the call returns instead of
+// hanging; the group is then unusable (SCS_ERR_COMM) and must be destroyed.
+template <class F>
+int group_run(scs_ctx* g, F&& f) {
+  if (g->group_broken) {
+    g->err = "multi-device context: an earlier call aborted its communicators; destroy it";
+    return SCS_ERR_COMM;
+  }
+  const int n = (int)g->subs.size();
+  std::vector<int> rc(n, SCS_OK);
+  std::atomic<int> done{0};
+  std::atomic<bool> aborted{false};
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (int i = 0; i < n; ++i)
+    th.emplace_back([&, i] {
+      scs_ctx* s = g->subs[i];
+      (void)hipSetDevice(s->dev);
+      rc[i] = f(s, i);
+      done.fetch_add(1);
+      if (rc[i] == SCS_OK || n == 1) return;
+      for (int t = 0; t < 500 && done.load() < n; ++t) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      if (done.load() < n && !aborted.exchange(true))
+        for (scs_ctx* o : g->subs)
+          if (o->rccl) (void)ncclCommAbort(o->rccl), o->rccl = nullptr;
+    });
+  for (auto& t : th) t.join();
+  if (aborted.load()) g->group_broken = true;
+  for (int i = 0; i < n; ++i)
+    if (rc[i] != SCS_OK) {
+      g->err = "device " + std::to_string(g->subs[i]->dev) + ": " + g->subs[i]->err;
+      return rc[i];
+    }
+  g->err.clear();
+  return SCS_OK;
+}
+
+bool is_group(const scs_ctx* c) { return c && !c->subs.empty(); }
+
+}  // namespace
+
+extern "C" {
+
+int scs_create_multi(const int* devs, int ndev, scs_ctx** out) {
+  if (!out || !devs || ndev < 1) return SCS_ERR_ARG;
+  *out = nullptr;
+  scs_ctx* g = new scs_ctx();
+  for (int i = 0; i < ndev; ++i)
+    for (int j = 0; j < i; ++j)
+      if (devs[i] == devs[j]) {
+        delete g;
+        return SCS_ERR_ARG;   // RCCL takes one rank per GPU
+      }
+  for (int i = 0; i < ndev; ++i) {
+    scs_ctx* s = nullptr;
+    const int rc = scs_create(devs[i], nullptr, &s);
+    if (rc != SCS_OK) {
+      for (scs_ctx* o : g->subs) scs_destroy(o);
+      delete g;
+      return rc;
+    }
+    g->subs.push_back(s);
+  }
+  std::vector<ncclComm_t> comms((size_t)ndev, nullptr);
+  const ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devs);
+  if (r != ncclSuccess) {
+    for (scs_ctx* o : g->subs) scs_destroy(o);
+    delete g;
+    return SCS_ERR_COMM;
+  }
+  for (int i = 0; i < ndev; ++i) {
+    g->subs[i]->rccl = comms[(size_t)i];
+    g->subs[i]->rank = i;
+    g->subs[i]->nranks = ndev;
+  }
+  g->dev = devs[0];
+  g->st = g->subs[0]->st;
+  *out = g;
+  return SCS_OK;
+}
+
+int scs_group_size(scs_ctx* c, int* ndev) {
+  if (!c || !ndev) return SCS_ERR_ARG;
+  *ndev = is_group(c) ? (int)c->subs.size() : 1;
+  return SCS_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int group_destroy(scs_ctx* g) {
+  for (scs_ctx* s : g->subs) scs_destroy(s);
+  g->subs.clear();
+  delete g;
+  return SCS_OK;
+}
+
+int group_set_data(scs_ctx* g, int64_t N, int64_t m, const double* A, int64_t lda, const double* y, int64_t Nglob,
+                   int64_t row0) {
+  const int n = (int)g->subs.size();
+  if ((Nglob > 0 && Nglob != N) || row0 != 0) {
+    g->err = "a multi-device context holds the whole problem: N_global = N, row0 = 0 (it splits the rows itself)";
+    return SCS_ERR_ARG;
+  }
+  if (A && N < n) {
+    g->err = "a multi-device context needs at least one row per device";
+    return SCS_ERR_ARG;
+  }
+  g->plan = A ? row_plan(N, n) : std::vector<RowBlock>((size_t)n);
+  const int rc = group_run(g, [&](scs_ctx* s, int i) {
+    const RowBlock b = g->plan[(size_t)i];
+    return scs_set_data(s, A ? b.rows() : 0, m, A ? A + b.r0 : nullptr, lda, y ? y + b.r0 : nullptr, A ? N : 0,
+                        b.r0);
+  });
+  if (rc == SCS_OK) {
+    g->grpN = A ? N : 0;
+    g->grpm = m;
+  }
+  return rc;
+}
+
+int group_gen_data(scs_ctx* g, const scs_synth* sp) {
+  const int n = (int)g->subs.size();
+  if (!sp || sp->row0 != 0 || sp->N != sp->N_global || sp->N < n) {
+    g->err = "a multi-device context generates the whole problem: spec N = N_global >= devices, row0 = 0";
+    return SCS_ERR_ARG;
+  }
+  g->plan = row_plan(sp->N, n);
+  const int rc = group_run(g, [&](scs_ctx* s, int i) {
+    scs_synth q = *sp;
+    q.row0 = g->plan[(size_t)i].r0;
+    q.N = g->plan[(size_t)i].rows();
+    return scs_gen_data(s, &q);
+  });
+  if (rc == SCS_OK) {
+    g->grpN = sp->N;
+    g->grpm = sp->m;
+  }
+  return rc;
+}
+
+int group_get_data(scs_ctx* g, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y) {
+  if (r0 < 0 || nr < 0 || r0 + nr > g->grpN) {
+    g->err = "scs_get_data: rows out of range";
+    return SCS_ERR_ARG;
+  }
+  for (const RowPiece& p : window_pieces(g->plan, r0, nr)) {
+    scs_ctx* s = g->subs[(size_t)p.dev];
+    const int rc = scs_get_data(s, p.local0, p.n, A ? A + p.off : nullptr, lda_out, y ? y + p.off : nullptr);
+    if (rc != SCS_OK) {
+      g->err = s->err;
+      return rc;
+    }
+  }
+  return SCS_OK;
+}
+
+// one scalar / one m-vector out of a collective evaluation: every device runs it, device 0's result
+int group_eval(scs_ctx* g, const double* x, double* out, int64_t nout,
+               int (*fn)(scs_ctx*, const double*, double*)) {
+  std::vector<std::vector<double>> o(g->subs.size(), std::vector<double>((size_t)std::max<int64_t>(nout, 1)));
+  const int rc = group_run(g, [&](scs_ctx* s, int i) { return fn(s, x, o[(size_t)i].data()); });
+  if (rc == SCS_OK && out) std::memcpy(out, o[0].data(), sizeof(double) * nout);
+  return rc;
+}
+
+int group_step(scs_ctx* g, const double* x, const double* x_prev, int64_t iter, const double* grad_fx, double* x_new,
+               double* dx, double* pri) {
+  const size_t n = g->subs.size(), m = (size_t)g->grpm;
+  std::vector<std::vector<double>> xn(n, std::vector<double>(m)), d(n, std::vector<double>(dx ? m : 1));
+  std::vector<double> pr(n, 0.0);
+  const int rc = group_run(g, [&](scs_ctx* s, int i) {
+    return scs_step_grad(s, x, x_prev, iter, grad_fx, xn[(size_t)i].data(), dx ? d[(size_t)i].data() : nullptr,
+                         &pr[(size_t)i]);
+  });
+  if (rc != SCS_OK) return rc;
+  std::memcpy(x_new, xn[0].data(), sizeof(double) * m);
+  if (dx) std::memcpy(dx, d[0].data(), sizeof(double) * m);
+  if (pri) *pri = pr[0];
+  return SCS_OK;
+}
+
+int group_iterate(scs_ctx* g, const double* x0, const double* x_star, int64_t max_epoch, double x_tol, double f_tol,
+                  int rel_kind, double* x_out, const scs_history* h, int64_t* n_hist, int64_t* epochs) {
+  const size_t n = g->subs.size(), m = (size_t)g->grpm;
+  const size_t cap = (size_t)std::max<int64_t>(2 * max_epoch + 1, 1);
+  std::vector<std::vector<double>> buf(n, std::vector<double>(6 * cap + m));
+  std::vector<int64_t> nh(n, 0), ep(n, 0);
+  const int rc = group_run(g, [&](scs_ctx* s, int i) {
+    double* b = buf[(size_t)i].data();
+    scs_history hi{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap, b + 5 * cap};
+    return scs_iterate(s, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, b + 6 * cap, &hi, &nh[(size_t)i],
+                       &ep[(size_t)i]);
+  });
+  if (rc != SCS_OK) return rc;
+  const double* b = buf[0].data();
+  const size_t k = (size_t)nh[0];
+  double* dst[6] = {h ? h->obj : nullptr, h ? h->fval : nullptr, h ? h->pri_res_norm : nullptr, h ? h->rel : nullptr,
+                    h ? h->objrel : nullptr, h ? h->times : nullptr};
+  for (int a = 0; a < 6; ++a)
+    if (dst[a]) std::memcpy(dst[a], b + a * cap, sizeof(double) * k);
+  if (x_out) std::memcpy(x_out, b + 6 * cap, sizeof(double) * m);
+  if (n_hist) *n_hist = nh[0];
+  if (epochs) *epochs = ep[0];
+  return SCS_OK;
+}
+
+}  // namespace

@@ -53,10 +53,19 @@ mutable struct DeviceProblem <: ProxModel
     name
 end
 
-function create_ctx(device::Integer)
+# devices = [d0, d1, ...]: one process drives those GPUs (scs_create_multi) -- the library splits
+# the rows across them, so a plain iterate! call uses the node's GPUs with no MPI (the reference's
+# iterate! is one process, iterate.jl:56-76)
+function create_ctx(device::Integer, devices=nothing)
     ctx = Ref{Ptr{Cvoid}}(C_NULL)
-    rc = ccall((:scs_create, lib), Cint, (Cint, Ptr{Cvoid}, Ref{Ptr{Cvoid}}), device, C_NULL, ctx)
-    rc == 0 || error("scs_create failed ($rc)")
+    if devices === nothing
+        rc = ccall((:scs_create, lib), Cint, (Cint, Ptr{Cvoid}, Ref{Ptr{Cvoid}}), device, C_NULL, ctx)
+        rc == 0 || error("scs_create failed ($rc)")
+    else
+        devs = Cint.(collect(devices))
+        rc = ccall((:scs_create_multi, lib), Cint, (Ptr{Cint}, Cint, Ref{Ptr{Cvoid}}), devs, length(devs), ctx)
+        rc == 0 || error("scs_create_multi($(devs)) failed ($rc)")
+    end
     return ctx[]
 end
 
@@ -75,8 +84,8 @@ end
 function DeviceProblem(A::Matrix{Float64}, y::AbstractVector, x0::Vector{Float64}, loss::Symbol, λ;
                        out_fn::Union{Symbol,Nothing}=nothing, scale::Float64=1.0 / size(A, 1),
                        L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0,
-                       N_global::Integer=size(A, 1), row0::Integer=0)
-    ctx = create_ctx(device)
+                       N_global::Integer=size(A, 1), row0::Integer=0, devices=nothing)
+    ctx = create_ctx(device, devices)
     N, m = size(A)
     yv = Vector{Float64}(y)
     chk(ccall((:scs_set_data, lib), Cint,

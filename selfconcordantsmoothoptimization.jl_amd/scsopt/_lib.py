@@ -70,6 +70,8 @@ _SIGS = {
     "scs_version": (C.c_char_p, []),
     "scs_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
     "scs_destroy": (C.c_int, [C.c_void_p]),
+    "scs_create_multi": (C.c_int, [c_i32p, C.c_int, C.POINTER(C.c_void_p)]),
+    "scs_group_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "scs_last_error": (C.c_char_p, [C.c_void_p]),
     "scs_get_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "scs_set_comm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, C.c_void_p]),
@@ -154,15 +156,24 @@ def dptr(a):
 
 
 class Context:
-    """Owns one scs_ctx (one device, one stream)."""
+    """Owns one scs_ctx: one device and stream (scs_create), or -- devices=[d0, d1, ...] -- one
+    process driving several GPUs (scs_create_multi: the library splits the rows across them)."""
 
-    def __init__(self, device=0, stream=None):
+    def __init__(self, device=0, stream=None, devices=None):
         h = C.c_void_p()
-        rc = lib.scs_create(int(device), stream, C.byref(h))
-        if rc != SCS_OK:
-            raise ScsError(rc, f"scs_create(device={device}) failed")
+        if devices is not None:
+            devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            rc = lib.scs_create_multi(devs, len(devices), C.byref(h))
+            if rc != SCS_OK:
+                raise ScsError(rc, f"scs_create_multi(devices={list(devices)}) failed")
+            device = int(devices[0])
+        else:
+            rc = lib.scs_create(int(device), stream, C.byref(h))
+            if rc != SCS_OK:
+                raise ScsError(rc, f"scs_create(device={device}) failed")
         self.h = h
         self.device = device
+        self.devices = list(devices) if devices is not None else [device]
         self._keep = []  # ctypes callbacks / buffers that must outlive the context
         self._cb_exc = None  # the exception a Python loss callback raised (re-raised by check)
 

@@ -68,7 +68,7 @@ class Problem:
     """problems.jl:21-40 (data) / :5-19 (generic)."""
 
     def __init__(self, *args, L=None, sol=None, C_set=None, P=None, out_fn: Optional[OutFn] = None,
-                 name=None, device=0, comm=None, N_global=None, row0=0, sparse_f32=False, _ctx=None):
+                 name=None, device=0, comm=None, N_global=None, row0=0, sparse_f32=False, devices=None, _ctx=None):
         if len(args) == 5:
             A, y, x0, f, lam = args
         elif len(args) == 3:
@@ -96,7 +96,9 @@ class Problem:
             # y keeps its shape: an N x ny target is a multi-output problem (iterate.jl:105-107)
             self._cb_data = None if A is None else (A, np.asarray(y, dtype=np.float64))
             A, y, self.generic = None, None, True
-        self.ctx = _ctx if _ctx is not None else _lib.Context(device)
+        if devices is not None and (comm is not None or _is_sparse(A)):
+            raise ValueError("devices=[...] (one process, several GPUs) takes a dense A and no comm")
+        self.ctx = _ctx if _ctx is not None else _lib.Context(device, devices=devices)
         if comm is not None and comm.active and _ctx is None:
             comm.attach(self.ctx)
         if _ctx is None:
@@ -199,14 +201,18 @@ class Problem:
 
     @classmethod
     def synthetic(cls, N, m, x0, f, lam, *, kind=1, seed=1234, density=0.1, out_fn=None, device=0,
-                  comm=None, **kw):
+                  comm=None, devices=None, **kw):
         """A ~ N(0,1)/sqrt(m) (kind 1, 2) or N(0,1) (kind 3) generated on the device, y from a
         sparse x_true (kind 1: Bernoulli(σ(A x_true)) ∈ {0,1}; kind 2: ±1; kind 3: A x_true + 0.1ε).
-        With comm, this rank generates its contiguous row shard in place."""
+        With comm, this rank generates its contiguous row shard in place; with devices=[...] one
+        process drives those GPUs and the library generates each one's row block."""
         from .shard import row_range
+        if devices is not None and comm is not None:
+            raise ValueError("devices=[...] (one process, several GPUs) and comm (one process per GPU) exclude "
+                             "each other")
         rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
         r0, r1 = row_range(N, world, rank)
-        ctx = _lib.Context(device)
+        ctx = _lib.Context(device, devices=devices)
         if comm is not None and comm.active:
             comm.attach(ctx)
         spec = _lib.Synth(N_global=N, row0=r0, N=r1 - r0, m=m, seed=seed, kind=kind, density=density)
