@@ -429,6 +429,11 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev2, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev3, hipEventDisableTiming);
+  // the one-launch triangular solves' block flags (generation-stamped: never reset) and error flag
+  if (e == hipSuccess) e = hipMalloc(&a->sflags, sizeof(unsigned) * 2 * (size_t)nblk + sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(a->sflags, 0, sizeof(unsigned) * 2 * (size_t)nblk + sizeof(int), st);
+  if (e == hipSuccess) a->serr = (int*)(a->sflags + 2 * nblk);
+  a->sgen = 0;
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   return e;
 }
@@ -447,6 +452,9 @@ void chol_aux_free(CholAux* a) {
   a->ssched.clear();
   if (a->spart) (void)hipFree(a->spart);
   a->spart = nullptr;
+  if (a->sflags) (void)hipFree(a->sflags);
+  a->sflags = nullptr;
+  a->serr = nullptr;
   if (a->st2) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
@@ -838,11 +846,228 @@ __global__ __launch_bounds__(256) void chol_bwd_update_kernel(const double* __re
   if (wv == 0 && r < nr) y[r] -= ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
+// ---------------------------------------------------------------------------
+// Triangular solves as ONE launch per direction (default; SCS_SOLVE_PERSIST=0: the two-launch-per-
+// block form above).  The per-block form is launch-bound: m = 8192 has 64 blocks x 2 launches x 2
+// directions = 256 launches, ~7 us each (1.9 ms).  Here workgroup j owns block j of the
+// right-hand side for the whole solve: it applies the earlier blocks' contributions as their
+// results appear -- each published by its owner with a release store of the solve's generation
+// number into flags[block] -- and then publishes its own.  A workgroup waits only on blocks
+// dispatched before it (forward: lower ids; backward: blockIdx b owns block nblk-1-b), so the grid
+// always progresses whatever is resident; a wait longer than ~30 s sets *err and drains.
+//   forward  Uᵀ y = b:  acc = b_j - Σ_{k<j} U_kjᵀ y_k (k ascending), y_j = W_jᵀ acc
+//   backward U x = y:   acc = y_k - Σ_{j>k} U_kj x_j (j descending), x_k = W_k acc
+// Fixed summation orders: bitwise run to run.
+constexpr int PS_NT = 256;
+
+__device__ __forceinline__ bool ps_wait(const unsigned* flag, unsigned gen, int* err) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {   // 30 s at 100 MHz
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  return true;
+}
+
+__device__ __forceinline__ void ps_publish(unsigned* flag, unsigned gen) {
+  __threadfence();   // every thread's stores of the block's result, then the flag
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A 128 x 128 column-major tile held in registers for the two GEMV forms below, loaded before the
+// vector it multiplies is published (the load latency leaves the serial chain).
+//   column form  out[c] += sign · Σ_r T(r, c) v[r] (ps_load_col / ps_apply_col below);
+//   row form     out[r] += sign · Σ_t T(r, t) v[t]: wave w holds columns [32w, 32w + 32), lane l
+//                rows l and l + 64 (coalesced, no lane reduction); the four wave partials are
+//                summed in wave order through LDS.
+// Fixed summation orders: bitwise run to run.
+struct PsTile {
+  double a[32][2];
+};
+
+// column form: wave w holds columns [32w, 32w + 32) as 8 groups of 4; in group g the 16 lanes of
+// row ρ = l >> 4 hold column 32w + 4g + ρ, lane l its rows [8(l & 15), 8(l & 15) + 8) (four 16-B
+// loads: each column's 1 KiB read by 16 lanes).  After the 8-row partial sums, a transposing
+// butterfly inside each 16-lane row needs only DPP: row_mirror (lane bit 3), row_half_mirror (bit
+// 2), quad_perm xor 2, xor 1 -- 8 value moves for 8 columns -- and lane l (bit 0 clear) ends with
+// the column of group ((l>>3)&1)·4 + ((l>>2)&1)·2 + ((l>>1)&1).
+template <int CTRL>
+__device__ __forceinline__ double ps_dpp(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_XOR2 = 0x4E, DPP_XOR1 = 0xB1;
+
+__device__ __forceinline__ void ps_load_col(const double* __restrict__ T, int64_t ld, PsTile& R) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r0 = 8 * (lane & 15), cq = lane >> 4;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const double* col = T + (int64_t)(32 * wv + 4 * g + cq) * ld + r0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const v2d t = *(const v2d*)(col + 2 * h);
+      R.a[4 * g + h][0] = t[0];
+      R.a[4 * g + h][1] = t[1];
+    }
+  }
+}
+
+__device__ __forceinline__ void ps_apply_col(const PsTile& R, const double* v, double* out, double sign) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r0 = 8 * (lane & 15);
+  double vv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) vv[i] = v[r0 + i];
+  double p[8];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    double t = 0.0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) t += R.a[4 * g + h][0] * vv[2 * h] + R.a[4 * g + h][1] * vv[2 * h + 1];
+    p[g] = t;
+  }
+  {  // row_mirror: bit 3, 8 -> 4 values
+    const bool hi = (lane & 8) != 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double send = hi ? p[i] : p[i + 4], keep = hi ? p[i + 4] : p[i];
+      p[i] = keep + ps_dpp<DPP_ROW_MIRROR>(send);
+    }
+  }
+  {  // row_half_mirror: bit 2, 4 -> 2
+    const bool hi = (lane & 4) != 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const double send = hi ? p[i] : p[i + 2], keep = hi ? p[i + 2] : p[i];
+      p[i] = keep + ps_dpp<DPP_ROW_HALF_MIRROR>(send);
+    }
+  }
+  {  // xor 2: bit 1, 2 -> 1
+    const bool hi = (lane & 2) != 0;
+    const double send = hi ? p[0] : p[1], keep = hi ? p[1] : p[0];
+    p[0] = keep + ps_dpp<DPP_XOR2>(send);
+  }
+  const double t = p[0] + ps_dpp<DPP_XOR1>(p[0]);   // xor 1: the whole 16-lane sum
+  if ((lane & 1) == 0) {
+    const int g = ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
+    out[32 * wv + 4 * g + (lane >> 4)] += sign * t;
+  }
+}
+
+__device__ __forceinline__ void ps_load_row(const double* __restrict__ T, int64_t ld, PsTile& R) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const double* col = T + (int64_t)(32 * wv + q) * ld;
+    R.a[q][0] = col[lane];
+    R.a[q][1] = col[lane + 64];
+  }
+}
+
+__device__ __forceinline__ void ps_apply_row(const PsTile& R, const double* v, double* part, double* out,
+                                             double sign) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const double vt = v[32 * wv + q];
+    s0 += R.a[q][0] * vt;
+    s1 += R.a[q][1] * vt;
+  }
+  part[wv * CB + lane] = s0;
+  part[wv * CB + lane + 64] = s1;
+  __syncthreads();
+  if (threadIdx.x < CB) {
+    const int r = threadIdx.x;
+    out[r] += sign * (((part[r] + part[CB + r]) + part[2 * CB + r]) + part[3 * CB + r]);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(PS_NT) void chol_fwd_persist_kernel(const double* __restrict__ G, int64_t ld,
+                                                                 const double* __restrict__ W,
+                                                                 const double* __restrict__ b, double* __restrict__ y,
+                                                                 unsigned* __restrict__ flags, unsigned gen,
+                                                                 int* __restrict__ err) {
+  __shared__ double acc[CB], yk[CB], yj[CB];
+  const int j = blockIdx.x, tid = threadIdx.x;
+  PsTile Wr, Tr;
+  ps_load_col(W + (int64_t)j * CB * CB, CB, Wr);
+  if (tid < CB) {
+    acc[tid] = b[(int64_t)j * CB + tid];
+    yj[tid] = 0.0;
+  }
+  for (int k = 0; k < j; ++k) {
+    ps_load_col(G + (int64_t)j * CB * ld + (int64_t)k * CB, ld, Tr);   // U_kj, before y_k is out
+    ps_wait(flags + k, gen, err);
+    if (tid < CB) yk[tid] = __hip_atomic_load(y + (int64_t)k * CB + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    ps_apply_col(Tr, yk, acc, -1.0);
+    __syncthreads();
+  }
+  __syncthreads();
+  ps_apply_col(Wr, acc, yj, 1.0);   // y_j[t] = Σ_u W(u, t) acc[u]
+  __syncthreads();
+  if (tid < CB) __hip_atomic_store(y + (int64_t)j * CB + tid, yj[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ps_publish(flags + j, gen);
+}
+
+__global__ __launch_bounds__(PS_NT) void chol_bwd_persist_kernel(const double* __restrict__ G, int64_t ld,
+                                                                 const double* __restrict__ W,
+                                                                 const double* __restrict__ y, double* __restrict__ x,
+                                                                 unsigned* __restrict__ flags, unsigned gen,
+                                                                 int* __restrict__ err, int nblk) {
+  __shared__ double acc[CB], xj[CB], xk[CB], part[4 * CB];
+  const int k = nblk - 1 - (int)blockIdx.x, tid = threadIdx.x;
+  PsTile Wr, Tr;
+  ps_load_row(W + (int64_t)k * CB * CB, CB, Wr);
+  if (tid < CB) {
+    acc[tid] = y[(int64_t)k * CB + tid];
+    xk[tid] = 0.0;
+  }
+  __syncthreads();
+  for (int j = nblk - 1; j > k; --j) {
+    ps_load_row(G + (int64_t)j * CB * ld + (int64_t)k * CB, ld, Tr);   // U_kj, before x_j is out
+    ps_wait(flags + j, gen, err);
+    if (tid < CB) xj[tid] = __hip_atomic_load(x + (int64_t)j * CB + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    ps_apply_row(Tr, xj, part, acc, -1.0);
+  }
+  ps_apply_row(Wr, acc, part, xk, 1.0);   // x_k[t] = Σ_u W(t, u) acc[u]
+  if (tid < CB) __hip_atomic_store(x + (int64_t)k * CB + tid, xk[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ps_publish(flags + k, gen);
+}
+
+static bool solve_persist() {
+  const char* e = getenv("SCS_SOLVE_PERSIST");
+  return !(e && e[0] == '0');
+}
+
 // Solve G x = b given the factor; b (length mpad, zero-padded) is overwritten by x; y is
 // scratch (mpad).
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
-                      hipStream_t st) {
+                      CholAux* a, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
+  if (a && a->sflags && solve_persist()) {
+    // y (forward) then b := x (backward); flags [0, nblk) forward, [nblk, 2 nblk) backward
+    const unsigned gen = ++a->sgen == 0 ? ++a->sgen : a->sgen;
+    hipLaunchKernelGGL(chol_fwd_persist_kernel, dim3((unsigned)nblk), dim3(PS_NT), 0, st, G, ld, W, b, y, a->sflags,
+                       gen, a->serr);
+    hipLaunchKernelGGL(chol_bwd_persist_kernel, dim3((unsigned)nblk), dim3(PS_NT), 0, st, G, ld, W, y, b,
+                       a->sflags + nblk, gen, a->serr, nblk);
+    return hipGetLastError();
+  }
   // one 128-block per outer step measured fastest for the solves (m = 16384: 4.2 ms vs 6.6 ms
   // with 8); SCS_SOLVE_OB overrides (A/B)
   static const int sob = [] {

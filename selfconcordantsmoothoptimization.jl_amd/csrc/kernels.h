@@ -80,6 +80,11 @@ struct CholAux {             // device constants of the two-level factorization 
   };
   std::vector<StripSched> ssched;
   double* spart = nullptr;   // K-split partial tiles of those launches
+  // one-launch triangular solves (chol_solve): per-block flags (2 nblk), their error flag, and
+  // the generation number the next solve stamps
+  unsigned* sflags = nullptr;
+  int* serr = nullptr;
+  unsigned sgen = 0;
 };
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);
 void chol_aux_free(CholAux* a);
@@ -87,7 +92,7 @@ void chol_aux_free(CholAux* a);
 hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st);
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* aux,
                        const int2* trilist, int* info, hipStream_t st);
-hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
+hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y, CholAux* a,
                       hipStream_t st);
 // Strip pipeline (scsopt.cpp gram_factor_pipelined): the factor runs left-looking behind a Gram
 // computed strip by strip.  Strip s = inner blocks [s·OB, min((s+1)·OB, nblk)).

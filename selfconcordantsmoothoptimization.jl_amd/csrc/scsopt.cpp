@@ -1157,7 +1157,7 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
     HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
     sync(c);
     if (info == 0) {
-      HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, c->st));
+      HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, &c->caux, c->st));
       c->lu_fallback_used = false;
       tend(c, T_SOLVE, e0);
       return;
@@ -1178,7 +1178,7 @@ void solve_factored(scs_ctx* c, double* rhs, hipEvent_t e0) {
     fail(c, SCS_ERR_STATE, "pipelined factor: a strip wait timed out (the strip was factored incomplete)");
   }
   if (info == 0) {
-    HCK(chol_solve(c->G, c->mpad, c->mpad, c->W, rhs, c->ysol, c->st));
+    HCK(chol_solve(c->G, c->mpad, c->mpad, c->W, rhs, c->ysol, &c->caux, c->st));
     c->lu_fallback_used = false;
     tend(c, T_SOLVE, e0);
     return;

@@ -792,3 +792,25 @@ def test_step_grad_fx_keyword(method, ss):
     xn_d, pri_d = step(dm, p, "l1", hm, x, xp, 5)
     xn_o, pri_o = O.step(omth, om, "l1", ohm, x, xp, None, 5)
     np.testing.assert_allclose(xn_d, xn_o, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("m", [300, 2304, 8192])
+def test_one_launch_triangular_solves(m, monkeypatch):
+    """The one-launch-per-direction triangular solves (chol_fwd/bwd_persist_kernel: a workgroup per
+    128-block, flags stamped with the solve's generation) against the per-block launches
+    (SCS_SOLVE_PERSIST=0) on the same factor: equal to rounding, bitwise run to run, and the
+    system's backward error at the fp64 level (the residual through the independent GEMV kernels)."""
+    N = m + 512
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=5)
+    rng = np.random.default_rng(6)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-2
+    rhs = rng.standard_normal(m)
+    x1, _ = p.solve_eval(w, d, rhs)
+    x2, _ = p.solve_eval(w, d, rhs)
+    assert np.array_equal(x1, x2)
+    monkeypatch.setenv("SCS_SOLVE_PERSIST", "0")
+    x0, _ = p.solve_eval(w, d, rhs)
+    np.testing.assert_allclose(x1, x0, rtol=1e-9, atol=1e-12 * float(np.max(np.abs(x0))))
+    r = p.gemv_t(w * p.gemv_n(x1)) + d * x1 - rhs
+    assert np.linalg.norm(r) <= 1e-11 * np.linalg.norm(rhs) * max(1.0, float(np.max(np.abs(x1))))

@@ -92,7 +92,7 @@ int main(int argc, char** argv) {
       printf("n=%ld factor: %.2f ms (info %d)\n", (long)n, ms, hinfo);
       hipLaunchKernelGGL(rowsum, dim3((unsigned)(n / 256)), dim3(256), 0, sq, G0, n, b);
       CK(hipEventRecord(e0, sq));
-      CK(scs::chol_solve(G, n, n, W, b, y, sq));
+      CK(scs::chol_solve(G, n, n, W, b, y, &aux, sq));
       CK(hipEventRecord(e1, sq)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
       std::vector<double> hx(n);
       CK(hipMemcpy(hx.data(), b, n * 8, hipMemcpyDeviceToHost));
