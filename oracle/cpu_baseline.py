@@ -130,6 +130,9 @@ def main():
                   f"sample part on {Ns} of {N} rows x m={m} scaled x{N / Ns:.0f}, "
                   f"{'dgetrf/dgetrs' if a.method == 'nscore' else 'dgeqrf/dormqr/dtrtrs'} solve at "
                   f"m={msz}" + (f" scaled x{(m / msz) ** 3:.0f}" if msz != m else ""),
+        "threads_note": (f"{threads} BLAS threads = this job's CPU share on the GPU box (OMP_NUM_THREADS is set to 16 "
+                         "per GPU there; os.cpu_count() and the affinity mask report the whole multi-GPU host, "
+                         "whose other cores belong to the other GPUs' jobs)"),
     }))
 
 

@@ -138,3 +138,33 @@ def test_step_passes_grad_fx():
     body = src[src.index("function step!("):]
     body = body[:body.index("\nend")]
     assert "∇fx" in body and "scs_step_grad" in body and ":scs_step," not in body
+
+
+def _struct_fields(src, name):
+    m = re.search(r"mutable struct " + name + r"\b[^\n]*\n(.*?)\nend", src, flags=re.S)
+    assert m, name
+    body = re.sub(r"#[^\n]*", "", m.group(1))
+    return [f.split("::")[0].strip() for f in re.split(r"[;\n]", body) for f in [f] if f.strip()
+            for f in f.split(";") if f.strip()]
+
+
+def test_integration_doc_matches_module():
+    """INTEGRATION.md's inline binding is the module's, not an older sketch: the same DeviceProblem
+    fields in the same order, and every ccall tuple in the document matches the header too."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    mod = open(JL).read()
+    fd = [x for f in _struct_fields(doc, "DeviceProblem") for x in f.split() if x]
+    fm = [x for f in _struct_fields(mod, "DeviceProblem") for x in f.split() if x]
+    assert fd == fm and len(fm) == 19, (fd, fm)
+    protos = _header_protos()
+    n = 0
+    for m in re.finditer(r"ccall\(\(:(\w+),\s*lib\),\s*(\w+),\s*\(([^()]*(?:\{[^{}]*\}[^()]*)*)\)", doc):
+        name, ret = m.group(1), m.group(2)
+        args = _split_top(m.group(3))
+        assert name in protos, name
+        cret, ctypes = protos[name]
+        assert len(args) == len(ctypes), (name, args, ctypes)
+        for a, ct in zip(args, ctypes):
+            assert _compatible(a, ct), (name, a, ct)
+        n += 1
+    assert n >= 5
