@@ -17,10 +17,13 @@
 //
 // Layout: G is m_pad x m_pad, ld = m_pad, m_pad % 128 == 0; the padded tail of
 // the diagonal is set to 1 by the caller (block-diag(A, I)).
+#include <algorithm>
 #include <cstdlib>
+#include <functional>
 #include <vector>
 
 #include "common.h"
+#include "gram_strip.h"
 #include "kernels.h"
 
 namespace scs {
@@ -455,6 +458,14 @@ void chol_aux_free(CholAux* a) {
   if (a->sflags) (void)hipFree(a->sflags);
   a->sflags = nullptr;
   a->serr = nullptr;
+  for (void* p : {(void*)a->dtasks, (void*)a->ddeps, (void*)a->dcnt, (void*)a->dper})
+    if (p) (void)hipFree(p);
+  a->dtasks = nullptr;
+  a->ddeps = nullptr;
+  a->dcnt = a->dper = nullptr;
+  a->dag_ob = 0;
+  a->dstep.clear();
+  a->dnext.clear();
   if (a->st2) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
@@ -525,11 +536,273 @@ static bool chol_lookahead() {
   return !(e && e[0] == '0');
 }
 
+// ---------------------------------------------------------------------------
+// Dependency-driven chain launches (opt-in SCS_CHOL_DAG=1; default: one launch per operation).
+// The serial chain of the factor was ~300 small launches at m = 8192 (per inner block a row
+// panel and a trailing-update launch; per outer block the next block's recursive strip solve, 15
+// launches, and its diagonal triangle), each paying a launch and a ramp (~17 us) for 2-3 us of
+// MFMA work.  Here each of those groups is ONE launch of independent 256-thread workgroups, each
+// a strip task (a 16-column strip of one 128 x 128 tile of the operation, gram_small_strip<16>:
+// the per-tile MFMA order of every Gram kernel, so U is bitwise that of the launch-per-operation
+// schedule).  A task first waits for the counters of the tasks it reads (a completed task
+// releases its stores, then advances its counters), so the recursion of the strip solve and the
+// panel -> trailing dependency run inside one launch.  Tasks are listed in a topological order
+// and a task waits only on tasks listed before it -- dispatched before it -- so the grid always
+// progresses whatever is resident; a wait over ~30 s sets the error flag and drains.  Counters
+// only grow: run g of a list waits for (g - 1)·period + target.
+// Measured at C2 (profiles/r03/chol/dag/): bitwise identical, but SLOWER -- a step list (row panel +
+// trailing, 280 strip tasks) takes 79 us against 2 x 17 us for the two launches it replaces (61 us
+// even with the agent-scope fences removed, which is not coherent across XCDs and was a timing
+// probe only: SCS_CHOL_DAG_FENCE=0); C2 solve 10.35 -> 11.3 ms.  Kept opt-in for the record.
+template <int FENCE>
+__global__ __launch_bounds__(256) void chol_dag_kernel(const DagTask* __restrict__ tasks, const DagDep* __restrict__ deps,
+                                                       double* G, int64_t ld, const double* __restrict__ W,
+                                                       const double* __restrict__ wv, unsigned* cnt,
+                                                       const unsigned* __restrict__ period, unsigned gen,
+                                                       int* __restrict__ err, int nap) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * (GT + 16) * GBK];
+  const DagTask t = tasks[blockIdx.x];
+  if (threadIdx.x == 0 && t.ndep > 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int d = 0; d < t.ndep; ++d) {
+      const DagDep q = deps[t.dep0 + d];
+      const unsigned target = (gen - 1u) * period[q.c] + (unsigned)q.target;
+      while ((int)(__hip_atomic_load(cnt + q.c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+        for (int z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {   // 30 s at 100 MHz
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    if (FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  gram_small_strip<16>((t.a1w ? W : G) + t.a1, t.lda1, G + t.a2, ld, wv + (t.wneg ? CB : 0), t.k0, t.k0 + t.nk,
+                       G + t.out, ld, t.flags, lds);
+  if (t.sig0 < 0 && t.sig1 < 0) return;
+  if (FENCE) __threadfence();   // every thread's stores of the strip, then the counters
+  else __builtin_amdgcn_s_waitcnt(0);   // A/B timing only (SCS_CHOL_DAG_FENCE=0): NOT coherent across XCDs
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (t.sig0 >= 0) __hip_atomic_fetch_add(cnt + t.sig0, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (t.sig1 >= 0) __hip_atomic_fetch_add(cnt + t.sig1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+static bool chol_dag_on() {
+  const char* e = getenv("SCS_CHOL_DAG");
+  return e && e[0] == '1';
+}
+
+namespace {
+struct DagBuilder {
+  std::vector<DagTask> t;
+  std::vector<DagDep> d;
+  std::vector<unsigned> per;
+  int counter() {
+    per.push_back(0);
+    return (int)per.size() - 1;
+  }
+  void add(DagTask x, const std::vector<DagDep>& dep) {
+    x.dep0 = (int)d.size();
+    x.ndep = (int)dep.size();
+    for (const DagDep& q : dep) d.push_back(q);
+    if (x.sig0 >= 0) ++per[(size_t)x.sig0];
+    if (x.sig1 >= 0) ++per[(size_t)x.sig1];
+    t.push_back(x);
+  }
+};
+
+DagTask strip_task(int64_t a1, int lda1, bool a1w, int64_t a2, int64_t out, int k0, int nk, bool neg, int flags) {
+  DagTask x;
+  x.a1 = a1;
+  x.a2 = a2;
+  x.out = out;
+  x.lda1 = lda1;
+  x.a1w = a1w ? 1 : 0;
+  x.k0 = k0;
+  x.nk = nk;
+  x.wneg = neg ? 1 : 0;
+  x.flags = flags;
+  x.dep0 = x.ndep = 0;
+  x.sig0 = x.sig1 = -1;
+  return x;
+}
+}  // namespace
+
+// The task lists of one factorization shape (nblk inner blocks, outer block OB, ld):
+//   step k (k not the last of its outer block [i0, i1)), nb = i1 - k - 1 blocks right of it:
+//     row panel  U_kj = W_kᵀ A_kj, j = k+1 .. i1-1 (8 strips each, counter rp_j);
+//     trailing   A_xy -= U_kxᵀ U_ky over the outer block (upper), after rp_x and rp_y;
+//   next t (outer block t, columns c0 = i1 .. i1 + OB - 1 of the next block):
+//     the strip solve X = U_Dᵀ⁻¹ R of strip_solve(i0, i1, c0, OB) -- its recursion replayed
+//     per strip: every update / leaf of output strip (row r, column j, strip s) waits for the
+//     previous operation on that strip and for the leaves of the X rows it reads;
+//     C1a  the next diagonal triangle -= Xᵀ X (K = the block's rows, upper), after every leaf of
+//     its two column blocks.
+static hipError_t chol_dag_build(const CholAux* a, int nblk, int OB, int64_t ld, hipStream_t st) {
+  if (a->dag_ob == OB && a->dag_ld == ld && a->dtasks) return hipSuccess;
+  DagBuilder B;
+  a->dstep.assign((size_t)nblk, DagList());
+  a->dnext.assign((size_t)((nblk + OB - 1) / OB), DagList());
+  const int up = GRAM_ACCUMULATE | GRAM_UPPER;
+  for (int i0 = 0; i0 < nblk; i0 += OB) {
+    const int i1 = std::min(i0 + OB, nblk);
+    for (int k = i0; k + 1 < i1; ++k) {
+      const int nb = i1 - k - 1;
+      DagList L;
+      L.t0 = (int)B.t.size();
+      std::vector<int> rp((size_t)nb);
+      for (int j = 0; j < nb; ++j) {
+        rp[(size_t)j] = B.counter();
+        for (int sq = 0; sq < 8; ++sq) {
+          const int64_t a2 = ((int64_t)(k + 1 + j) * CB + 16 * sq) * ld + (int64_t)k * CB;
+          DagTask x = strip_task((int64_t)k * CB * CB, CB, true, a2, a2, 0, CB, false, 0);
+          x.sig0 = rp[(size_t)j];
+          B.add(x, {});
+        }
+      }
+      for (int x = 0; x < nb; ++x)
+        for (int y = 0; y <= x; ++y)
+          for (int sq = 0; sq < 8; ++sq) {
+            const int64_t a1 = (int64_t)(k + 1 + x) * CB * ld + (int64_t)k * CB;
+            const int64_t a2 = ((int64_t)(k + 1 + y) * CB + 16 * sq) * ld + (int64_t)k * CB;
+            const int64_t out = (int64_t)(k + 1 + x) * CB * ld + (int64_t)(k + 1 + y) * CB + 16 * sq;
+            std::vector<DagDep> dep{{rp[(size_t)x], 8}};
+            if (y != x) dep.push_back({rp[(size_t)y], 8});
+            B.add(strip_task(a1, (int)ld, false, a2, out, 0, CB, true, up), dep);
+          }
+      L.nt = (int)B.t.size() - L.t0;
+      a->dstep[(size_t)k] = L;
+    }
+    const int nc = nblk - i1;
+    if (nc <= OB) continue;   // the serial tail (chol_factor's !la branch) has no next-block list
+    const int c0 = i1, R = i1 - i0;
+    DagList L;
+    L.t0 = (int)B.t.size();
+    // per output strip (row r in [0, R), column j in [0, OB), strip s): its operation counter and
+    // how many operations it has seen so far; per column the count of finished leaves
+    std::vector<int> sc((size_t)R * OB * 8), nops((size_t)R * OB * 8, 0), col((size_t)OB);
+    for (auto& c : sc) c = B.counter();
+    for (auto& c : col) c = B.counter();
+    auto sid = [&](int r, int j, int sq) { return ((size_t)r * OB + j) * 8 + sq; };
+    std::vector<int> nleaf_ops((size_t)R * OB * 8, 0);   // operations of a strip including its leaf
+    // first pass: count the operations each output strip receives (updates + its leaf)
+    std::function<void(int, int, bool)> walk = [&](int lo, int hi, bool emit) {
+      if (hi - lo == 1) {
+        for (int j = 0; j < OB; ++j)
+          for (int sq = 0; sq < 8; ++sq) {
+            const size_t id = sid(lo - i0, j, sq);
+            if (!emit) {
+              ++nleaf_ops[id];
+              continue;
+            }
+            const int64_t a2 = ((int64_t)c0 * CB + (int64_t)j * CB + 16 * sq) * ld + (int64_t)lo * CB;
+            DagTask x = strip_task((int64_t)lo * CB * CB, CB, true, a2, a2, 0, CB, false, 0);
+            x.sig0 = sc[id];
+            x.sig1 = col[(size_t)j];
+            std::vector<DagDep> dep;
+            if (nops[id] > 0) dep.push_back({sc[id], nops[id]});
+            B.add(x, dep);
+            ++nops[id];
+          }
+        return;
+      }
+      const int mid = (lo + hi) / 2;
+      walk(lo, mid, emit);
+      for (int i = 0; i < hi - mid; ++i)
+        for (int j = 0; j < OB; ++j)
+          for (int sq = 0; sq < 8; ++sq) {
+            const size_t id = sid(mid + i - i0, j, sq);
+            if (!emit) {
+              ++nleaf_ops[id];
+              continue;
+            }
+            const int64_t a1 = ((int64_t)mid * CB + (int64_t)i * CB) * ld + (int64_t)lo * CB;
+            const int64_t a2 = ((int64_t)c0 * CB + (int64_t)j * CB + 16 * sq) * ld + (int64_t)lo * CB;
+            const int64_t out = ((int64_t)c0 * CB + (int64_t)j * CB + 16 * sq) * ld + (int64_t)(mid + i) * CB;
+            DagTask x = strip_task(a1, (int)ld, false, a2, out, 0, (mid - lo) * CB, true, GRAM_ACCUMULATE);
+            x.sig0 = sc[id];
+            std::vector<DagDep> dep;
+            if (nops[id] > 0) dep.push_back({sc[id], nops[id]});
+            for (int r = lo; r < mid; ++r) {   // the X1 rows it reads: their leaves, strip s of column j
+              const size_t rid = sid(r - i0, j, sq);
+              dep.push_back({sc[rid], nleaf_ops[rid]});
+            }
+            B.add(x, dep);
+            ++nops[id];
+          }
+      walk(mid, hi, emit);
+    };
+    walk(i0, i1, false);
+    walk(i0, i1, true);
+    // C1a: the next block's diagonal triangle (tiles x >= y < OB, row-major), K = rows [i0, i1)
+    for (int x = 0; x < OB; ++x)
+      for (int y = 0; y <= x; ++y)
+        for (int sq = 0; sq < 8; ++sq) {
+          const int64_t a1 = ((int64_t)c0 * CB + (int64_t)x * CB) * ld;
+          const int64_t a2 = ((int64_t)c0 * CB + (int64_t)y * CB + 16 * sq) * ld;
+          const int64_t out = ((int64_t)c0 * CB + (int64_t)x * CB) * ld + (int64_t)c0 * CB + (int64_t)y * CB + 16 * sq;
+          std::vector<DagDep> dep{{col[(size_t)x], 8 * R}};
+          if (y != x) dep.push_back({col[(size_t)y], 8 * R});
+          B.add(strip_task(a1, (int)ld, false, a2, out, i0 * CB, R * CB, true, up), dep);
+        }
+    L.nt = (int)B.t.size() - L.t0;
+    a->dnext[(size_t)(i0 / OB)] = L;
+  }
+  if (a->dtasks) (void)hipFree(a->dtasks);
+  if (a->ddeps) (void)hipFree(a->ddeps);
+  if (a->dcnt) (void)hipFree(a->dcnt);
+  if (a->dper) (void)hipFree(a->dper);
+  a->dtasks = nullptr;
+  a->ddeps = nullptr;
+  a->dcnt = a->dper = nullptr;
+  hipError_t e = hipMalloc(&a->dtasks, sizeof(DagTask) * std::max<size_t>(B.t.size(), 1));
+  if (e == hipSuccess) e = hipMalloc(&a->ddeps, sizeof(DagDep) * std::max<size_t>(B.d.size(), 1));
+  if (e == hipSuccess) e = hipMalloc(&a->dcnt, sizeof(unsigned) * std::max<size_t>(B.per.size(), 1));
+  if (e == hipSuccess) e = hipMalloc(&a->dper, sizeof(unsigned) * std::max<size_t>(B.per.size(), 1));
+  if (e == hipSuccess && !B.t.empty())
+    e = hipMemcpyAsync(a->dtasks, B.t.data(), sizeof(DagTask) * B.t.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !B.d.empty())
+    e = hipMemcpyAsync(a->ddeps, B.d.data(), sizeof(DagDep) * B.d.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !B.per.empty()) {
+    e = hipMemsetAsync(a->dcnt, 0, sizeof(unsigned) * B.per.size(), st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(a->dper, B.per.data(), sizeof(unsigned) * B.per.size(), hipMemcpyHostToDevice, st);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) {
+    a->dag_ob = OB;
+    a->dag_ld = ld;
+  }
+  return e;
+}
+
+static hipError_t chol_dag_launch(const CholAux* a, DagList& L, double* G, int64_t ld, const double* W, hipStream_t st) {
+  if (L.nt <= 0) return hipSuccess;
+  ++L.gen;
+  static const int nap = [] { const char* e = getenv("SCS_CHOL_DAG_SLEEP"); return e ? atoi(e) : 1; }();
+  const char* fe = getenv("SCS_CHOL_DAG_FENCE");
+  if (fe && fe[0] == '0')
+    hipLaunchKernelGGL(chol_dag_kernel<0>, dim3((unsigned)L.nt), dim3(256), 0, st, a->dtasks + L.t0, a->ddeps, G, ld, W,
+                       a->w, a->dcnt, a->dper, L.gen, a->serr, nap);
+  else
+    hipLaunchKernelGGL(chol_dag_kernel<1>, dim3((unsigned)L.nt), dim3(256), 0, st, a->dtasks + L.t0, a->ddeps, G, ld, W,
+                       a->w, a->dcnt, a->dper, L.gen, a->serr, nap);
+  return hipGetLastError();
+}
+
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* a,
                        const int2* trilist, int* info, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
   const int OB = outer_block_for(nblk);
   const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
+  const bool dag = chol_dag_on() && a->serr;
+  if (dag) {
+    const hipError_t eb = chol_dag_build(a, nblk, OB, ld, st);
+    if (eb != hipSuccess) return eb;
+  }
   bool c12_pending = false;
   hipError_t e = hipSuccess;
   auto wait = [&](hipStream_t s, hipEvent_t ev) {
@@ -545,6 +818,11 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
       if (e != hipSuccess) return e;
       const int nb = i1 - k - 1;
       if (nb == 0) break;
+      if (dag) {   // the row panel and the trailing update of step k as one launch
+        e = chol_dag_launch(a, a->dstep[(size_t)k], G, ld, W, st);
+        if (e != hipSuccess) return e;
+        continue;
+      }
       double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..i1-1)
       e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb, rowpanel, ld,
                           0, st);
@@ -578,11 +856,15 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2);
     // Ba, C1a on the chain after C12_{t-1}
     if (c12_pending) wait(st, a->ev2);
-    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
     const int n1a = (OB * (OB + 1)) / 2;
-    if (e == hipSuccess)
-      e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, n1a, trail, ld,
-                            2 | 4, st);
+    if (dag) {   // the recursive strip solve and the next diagonal triangle as one launch
+      if (e == hipSuccess) e = chol_dag_launch(a, a->dnext[(size_t)(i0 / OB)], G, ld, W, st);
+    } else {
+      if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
+      if (e == hipSuccess)
+        e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, n1a, trail, ld,
+                              2 | 4, st);
+    }
     // C12 on st2 after Ba (it reads X's columns of the next block)
     if (e == hipSuccess) e = hipEventRecord(a->ev1, st);
     wait(a->st2, a->ev1);

@@ -39,11 +39,9 @@
 
 namespace scs {
 
-constexpr int GT = 128;   // output tile edge
-enum { GRAM_PACKED = 1, GRAM_ACCUMULATE = 2, GRAM_UPPER = 4 };
-constexpr int GBK = 16;   // samples per stage
-
-__device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
+}  // namespace scs
+#include "gram_strip.h"   // GT, GBK, swz, the GRAM_* flags and the latency strip body
+namespace scs {
 
 // Workgroup barrier that orders LDS only: the staged global loads (two stages
 // ahead) stay in flight across it (a __syncthreads() here makes hipcc drain
@@ -876,95 +874,19 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
 // ~1.5 us x 8 stages against ~0.4 us of MFMAs per stage).  Column-major operands (gen
 // form), swizzled LDS stages, and per accumulator the MFMA order of gram_f64_kernel /
 // gram_sia_kernel ((p, u) per stage, stages ascending): the tile is bitwise the same.
+// the strip's output base: element (I0, J0) of the tile in the chosen placement
 template <int QC>
 __global__ __launch_bounds__(256) void gram_small_kernel(const double* __restrict__ A1, int64_t lda1,
                                                          const double* A2, int64_t lda2,
                                                          const double* __restrict__ w, int64_t k0, int64_t Nk,
                                                          const int2* __restrict__ tiles, double* G, int64_t ldg,
                                                          int flags) {
-  constexpr int RING = 8;                  // stages in flight
-  constexpr int NQ = GT / QC;              // workgroups per tile
-  constexpr int TJ = QC / 16;              // 16-column MFMA tiles per wave
-  constexpr int SBQ = (GT + QC) * GBK;     // doubles per LDS stage (A1 128 x 16 | A2 QC x 16)
-  __shared__ __attribute__((aligned(16))) double lds[2 * SBQ];
-  const int accumulate = flags & GRAM_ACCUMULATE, upper = flags & GRAM_UPPER;
+  constexpr int NQ = GT / QC;
+  __shared__ __attribute__((aligned(16))) double lds[2 * (GT + QC) * GBK];
   const int2 tl = tiles[blockIdx.x / NQ];
   const int64_t I0 = (int64_t)tl.x * GT, J0 = (int64_t)tl.y * GT + (blockIdx.x % NQ) * QC;
-  const double* __restrict__ Ai = A1 + I0 * lda1;
-  const double* Aj = A2 + J0 * lda2;
-  const int tid = threadIdx.x, lane = tid & 63, wr = tid >> 6;
-  const int sc = tid & 7, sf0 = tid >> 3;   // staging: feature sf0 + 32 i, 16-B chunk sc
-  const bool hasb = QC == 32 || sf0 < QC;   // A2 rows staged by this thread (QC = 16: half the threads)
-  const int sfb = sf0 & (QC - 1);           // loads stay unconditional (a branch drains vmcnt)
-  v2d ra[RING][4], rb[RING], rw[RING];
-  auto gload = [&](int slot, int64_t n0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ra[slot][i] = *(const v2d*)(Ai + (int64_t)(sf0 + 32 * i) * lda1 + n0 + 2 * sc);
-    rb[slot] = *(const v2d*)(Aj + (int64_t)sfb * lda2 + n0 + 2 * sc);
-    rw[slot] = *(const v2d*)(w + n0 + 2 * sc);
-  };
-  auto swrite = [&](int slot, int buf) {
-    double* la = lds + buf * SBQ;
-    double* lb = la + GT * GBK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = sf0 + 32 * i;
-      *(v2d*)(la + f * GBK + 2 * (sc ^ swz(f))) = ra[slot][i];
-    }
-    if (hasb) *(v2d*)(lb + sf0 * GBK + 2 * (sc ^ swz(sf0))) = rb[slot] * rw[slot];
-  };
-  v4d acc[2][TJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
-  const int fl = lane & 15, g = lane >> 4, s = swz(fl);
-  // nk is a multiple of RING (gram_launch_small); the loads past the end re-read the last stage
-  // (branch-free: a conditional load would make the compiler drain vmcnt at every stage)
-  const int nk = (int)((Nk - k0) / GBK);
-#pragma unroll
-  for (int j = 0; j < RING; ++j) gload(j, k0 + (int64_t)j * GBK);
-  for (int kk = 0; kk < nk; kk += RING) {
-#pragma unroll
-    for (int j = 0; j < RING; ++j) {
-      const int k = kk + j;
-      {
-        swrite(j, k & 1);
-        gload(j, k0 + (int64_t)min(k + RING, nk - 1) * GBK);
-        __syncthreads();
-        const double* la = lds + (k & 1) * SBQ;
-        const double* lb = la + GT * GBK;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int pc = ((4 * p + g) ^ s) * 2;
-          v2d a[2], b[TJ];
-#pragma unroll
-          for (int t = 0; t < 2; ++t) a[t] = *(const v2d*)(la + (wr * 32 + 16 * t + fl) * GBK + pc);
-#pragma unroll
-          for (int t = 0; t < TJ; ++t) b[t] = *(const v2d*)(lb + (16 * t + fl) * GBK + pc);
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-              for (int tj = 0; tj < TJ; ++tj)
-                acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti][u], b[tj][u], acc[ti][tj], 0, 0, 0);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < TJ; ++tj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t I = I0 + wr * 32 + 16 * ti + g + 4 * r;
-        const int64_t J = J0 + 16 * tj + fl;
-        double* dst = upper ? G + I * ldg + J : G + J * ldg + I;
-        if (accumulate) *dst += acc[ti][tj][r];
-        else *dst = acc[ti][tj][r];
-      }
+  double* Gt = (flags & GRAM_UPPER) ? G + I0 * ldg + J0 : G + J0 * ldg + I0;
+  gram_small_strip<QC>(A1 + I0 * lda1, lda1, A2 + J0 * lda2, lda2, w, k0, Nk, Gt, ldg, flags, lds);
 }
 
 hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,

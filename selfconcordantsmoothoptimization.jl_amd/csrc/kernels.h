@@ -64,6 +64,25 @@ hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, do
                               hipStream_t st);
 
 // ---- chol.hip (upper Cholesky on MFMA; W holds the inverted diagonal blocks)
+// One strip task of the Cholesky's dependency-driven chain launches (chol_dag_kernel): a latency
+// Gram strip (gram_small_strip<16>) with its operands as offsets, the counters it waits for and
+// the ones it advances when done.
+struct DagTask {
+  int64_t a1, a2, out;   // element offsets: A1 in W (a1w) or G; A2 and the output strip origin in G
+  int32_t lda1, a1w;     // A1 leading dimension (128 for W, ld for G), A1 in W?
+  int32_t k0, nk;        // contraction [k0, k0 + nk), whole 8-stage rings
+  int32_t wneg, flags;   // weights +1 (0) or -1 (1); GRAM_ACCUMULATE | GRAM_UPPER
+  int32_t dep0, ndep;    // its dependencies: deps[dep0 .. dep0 + ndep)
+  int32_t sig0, sig1;    // counters advanced on completion (-1: none)
+};
+struct DagDep {
+  int32_t c, target;     // counter c has reached target (in this run)
+};
+struct DagList {
+  int t0 = 0, nt = 0;    // task range
+  unsigned gen = 0;      // runs so far (the counters only grow: run g waits for (g-1)·period + target)
+};
+
 struct CholAux {             // device constants of the two-level factorization (chol_aux_init)
   double* w = nullptr;       // [128 x +1.0 | mpad x -1.0] Gram weights (panel solve | block updates)
   int2* rect = nullptr;      // R x nblk rectangle tile lists, R = 1..4 (bj-major)
@@ -85,6 +104,16 @@ struct CholAux {             // device constants of the two-level factorization 
   unsigned* sflags = nullptr;
   int* serr = nullptr;
   unsigned sgen = 0;
+  // dependency-driven chain launches (chol_dag_build, built for one outer block size dag_ob): per
+  // inner block k the A-phase step (row panel + trailing strips inside the outer block), per outer
+  // block t the next block's strip solve + diagonal triangle (Ba + C1a)
+  mutable int dag_ob = 0;
+  mutable int64_t dag_ld = 0;
+  mutable DagTask* dtasks = nullptr;
+  mutable DagDep* ddeps = nullptr;
+  mutable unsigned* dcnt = nullptr;
+  mutable unsigned* dper = nullptr;
+  mutable std::vector<DagList> dstep, dnext;
 };
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);
 void chol_aux_free(CholAux* a);

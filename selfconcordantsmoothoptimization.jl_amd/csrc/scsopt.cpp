@@ -1155,7 +1155,13 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
     HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
     HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
     HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    int late = 0;   // a dependency wait of the chain launches or the solves gave up (~30 s): never expected
+    HCK(hipMemcpyAsync(&late, c->caux.serr, sizeof(int), hipMemcpyDeviceToHost, c->st));
     sync(c);
+    if (late) {
+      HCK(hipMemsetAsync(c->caux.serr, 0, sizeof(int), c->st));
+      fail(c, SCS_ERR_HIP, "Cholesky: a dependency wait of the chain launches timed out");
+    }
     if (info == 0) {
       HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, &c->caux, c->st));
       c->lu_fallback_used = false;

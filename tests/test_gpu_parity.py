@@ -814,3 +814,29 @@ def test_one_launch_triangular_solves(m, monkeypatch):
     np.testing.assert_allclose(x1, x0, rtol=1e-9, atol=1e-12 * float(np.max(np.abs(x0))))
     r = p.gemv_t(w * p.gemv_n(x1)) + d * x1 - rhs
     assert np.linalg.norm(r) <= 1e-11 * np.linalg.norm(rhs) * max(1.0, float(np.max(np.abs(x1))))
+
+
+@pytest.mark.parametrize("m,ob,la", [(2304, None, "1"), (3200, None, "1"), (4608, "16", "1"), (3200, None, "0"),
+                                     (8192, None, "1")])
+def test_cholesky_dag_launches_bit_identical(m, ob, la, monkeypatch):
+    """The factor's dependency-driven chain launches (chol_dag_kernel: per inner block the row panel +
+    trailing update, per outer block the next block's recursive strip solve + diagonal triangle, as
+    one launch of strip tasks waiting on counters) compute every tile with the latency kernel's MFMA
+    order in the original operation order: the ProxNSCORE trajectory is bitwise that of one launch
+    per operation (SCS_CHOL_DAG=0) -- with the lookahead (la = 1) or the serial order (la = 0), 8- or
+    16-block outer steps, and at the C2 shape (m = 8192: 64 inner blocks)."""
+    if ob:
+        monkeypatch.setenv("SCS_CHOL_OB", ob)
+    monkeypatch.setenv("SCS_CHOL_LA", la)
+    monkeypatch.setenv("SCS_CHOL_DAG", "1")   # opt-in (measured slower than one launch per operation)
+    N = 4000 if m < 8192 else 9000
+    x0 = np.random.default_rng(37).standard_normal(m) * 0.3
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=29)
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    a = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    b = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)   # the counters' 2nd run
+    monkeypatch.setenv("SCS_CHOL_DAG", "0")
+    c = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    for r in (b, c):
+        assert a.obj == r.obj and a.pri_res_norm == r.pri_res_norm and a.epochs == r.epochs
+        assert np.array_equal(bits(a.x), bits(r.x))
