@@ -225,6 +225,16 @@ int scs_set_reg(scs_ctx* ctx, int reg_kind, const double* lam, int nlam,
  * only the gradient is all-reduced.  Bit-identical results.  Costs one more
  * m_pad² fp64 buffer.                                                        */
 int scs_set_gram_cache(scs_ctx* ctx, int on);
+/* The m x m (and the GGN sample-space (N+1)²) systems' solver.  SCS_SOLVER_DEFAULT: blocked
+ * Cholesky on MFMA with the LU fallback (sample space: LU) -- equal to the reference's solves to
+ * O(cond·eps).  SCS_SOLVER_REFERENCE: the reference's own factorizations -- Householder QR
+ * (LAPACK dgeqrf / dlarfg / dlarft conventions, 128-column compact-WY panels) for ProxGGNSCORE's
+ * `qr(JQJ) \ Je` and `qr(I + A) \ residual` (prox-GGN-SCORE.jl:126,131) and the LU for
+ * ProxNSCORE's `(H + λ·Diagonal(Hr)) \ ∇q` (prox-N-SCORE.jl:70) -- for parity work on
+ * ill-conditioned systems; slower (the QR panel is a column-by-column chain).                  */
+#define SCS_SOLVER_DEFAULT 0
+#define SCS_SOLVER_REFERENCE 1
+int scs_set_solver(scs_ctx* ctx, int kind);
 /* G of get_P(n, G, ind) (1-based, a permutation of 1..m): get_reg's group
  * term reads P.matrix*x = x[G] (prox-reg-utils.jl:31, regularizers.jl:24-27);
  * the prox (ProxL2) and the GL smoothers (Cmat) index x directly, as in the
@@ -313,8 +323,9 @@ int scs_gemv_n_eval(scs_ctx* ctx, const double* x, double* out);
 
 /* The m x m system of ProxNSCORE / ProxGGNSCORE, (Aᵀ diag(w) A + diag(dvec)) x = rhs
  * ((H + λ·Diagonal(Hr)) \ ∇q, prox-N-SCORE.jl:69-70; qr(JQJ) \ Je, prox-GGN-SCORE.jl:129-131),
- * through the step's own path: MFMA Gram, then the hand-written Cholesky with the LU
- * fallback (mode 0) or the hand-written LU alone (mode 1).  *used_lu = 1 when the LU ran.  */
+ * through the step's own path: MFMA Gram, then the solver scs_set_solver selects (mode 0: by
+ * default the hand-written Cholesky with the LU fallback), the hand-written LU alone (mode 1) or
+ * the Householder QR (mode 2).  *used_lu = 1 when the LU ran.                                */
 int scs_solve_eval(scs_ctx* ctx, const double* w, const double* dvec, const double* rhs, int mode,
                    double* x, int* used_lu);
 /* Julia's `A \ b` for a dense square Matrix (LAPACK getrf + getrs) by the hand-written

@@ -356,6 +356,61 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   PROF_MARK(35);
 }
 
+// W_k = R_kk⁻¹ for the upper 128 x 128 diagonal blocks of a triangular R (the QR solve): the
+// inverse part of chol_diag_kernel (the 16 x 16 inverses, then recursive doubling on MFMA) on a
+// block whose factor is given; the strictly lower part of the block is ignored.
+__global__ __launch_bounds__(DNT) void tri_inv_kernel(const double* __restrict__ R, int64_t ld,
+                                                      double* __restrict__ W) {
+  __shared__ double su[CB * CLD];
+  __shared__ double srinv[CB];
+  __shared__ double swinv[CB / SB][SB * SB];
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const double* blk = R + (int64_t)k * CB * ld + (int64_t)k * CB;
+  for (int e = tid; e < CB * CB; e += DNT) {
+    const int c = e >> 7, r = e & 127;
+    su[c * CLD + r] = (r <= c) ? blk[(int64_t)c * ld + r] : 0.0;
+  }
+  __syncthreads();
+  if (tid < CB) srinv[tid] = 1.0 / su[tid * CLD + tid];
+  __syncthreads();
+  for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) {
+    const int o = kb * SB, c = tid & 15;
+    double w[SB];
+#pragma unroll
+    for (int i = 0; i < SB; ++i) w[i] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int t = SB - 1; t >= 0; --t) {
+      w[t] *= srinv[o + t];
+#pragma unroll
+      for (int i = 0; i < t; ++i) w[i] -= su[(o + t) * CLD + o + i] * w[t];
+    }
+    if ((tid & 63) < SB) {
+#pragma unroll
+      for (int i = 0; i < SB; ++i) swinv[kb][c * SB + i] = (i <= c) ? w[i] : 0.0;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < CB * SB; e += DNT) {
+    const int kb = e >> 8, c = (e >> 4) & 15, i = e & 15;
+    if (i <= c) su[(kb * SB + c) * CLD + kb * SB + i] = swinv[kb][c * SB + i];
+  }
+  __syncthreads();
+  chol_inv_double_mfma<16>(su, tid);
+  chol_inv_double_mfma<32>(su, tid);
+  chol_inv_double_mfma<64>(su, tid);
+  double* Wk = W + (int64_t)k * CB * CB;
+  for (int e = tid; e < CB * CB; e += DNT) {
+    const int c = e >> 7, r = e & 127;
+    Wk[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
+  }
+}
+
+hipError_t chol_tri_inverse(const double* R, int64_t ld, int nblk, double* W, hipStream_t st) {
+  if (nblk <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tri_inv_kernel, dim3((unsigned)nblk), dim3(DNT), 0, st, R, ld, W);
+  return hipGetLastError();
+}
+
 static bool chol_diag_pipe() {   // read per call (A/B within one process)
   const char* e = getenv("SCS_CHOL_DIAG");
   return !(e && e[0] == '0');
@@ -1334,6 +1389,16 @@ __global__ __launch_bounds__(PS_NT) void chol_bwd_persist_kernel(const double* _
 static bool solve_persist() {
   const char* e = getenv("SCS_SOLVE_PERSIST");
   return !(e && e[0] == '0');
+}
+
+hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, const double* y, double* x,
+                           CholAux* a, hipStream_t st) {
+  const int nblk = (int)(mpad / CB);
+  if (!a || !a->sflags || (int64_t)a->nblk < nblk) return hipErrorInvalidValue;
+  const unsigned gen = ++a->sgen == 0 ? ++a->sgen : a->sgen;
+  hipLaunchKernelGGL(chol_bwd_persist_kernel, dim3((unsigned)nblk), dim3(PS_NT), 0, st, U, ld, W, y, x,
+                     a->sflags + a->nblk, gen, a->serr, nblk);
+  return hipGetLastError();
 }
 
 // Solve G x = b given the factor; b (length mpad, zero-padded) is overwritten by x; y is

@@ -168,6 +168,28 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
 // b (npad, zero-padded) <- A⁻¹ b
 hipError_t lu_solve(const double* A, int64_t ld, int64_t npad, const LUAux* a, double* b, hipStream_t st);
 
+// ---- qr.hip: Householder QR solve (LAPACK dgeqrf / dlarfg / dlarft conventions), the reference
+// solver mode (scs_set_solver).  A: column-major npad x npad, rows/cols [n, npad) the identity;
+// A is overwritten, b (npad) receives x.
+struct QRAux {
+  int64_t npad = 0;
+  double *part = nullptr, *tw = nullptr, *tau = nullptr, *scal = nullptr, *V = nullptr, *Vt = nullptr,
+         *Wm = nullptr, *Ym = nullptr, *Gv = nullptr, *T = nullptr, *ones = nullptr, *W = nullptr;
+  int2* tiles = nullptr;
+};
+// set the identity padding of a column-major system in place / build it from a row-major one
+hipError_t qr_prepare(double* A, int64_t ld, int64_t n, int64_t npad, hipStream_t st);
+hipError_t qr_from_rowmajor(const double* S, int64_t lds, double* D, int64_t ldd, int64_t n, int64_t npad,
+                            hipStream_t st);
+hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st);
+void qr_aux_free(QRAux* a);
+hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, CholAux* ca, hipStream_t st);
+// chol.hip pieces the QR solve reuses: the inverses of the 128 x 128 upper diagonal blocks of R
+// (W, as the Cholesky's), and the one-launch backward solve U x = y
+hipError_t chol_tri_inverse(const double* R, int64_t ld, int nblk, double* W, hipStream_t st);
+hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, const double* y, double* x,
+                           CholAux* a, hipStream_t st);
+
 // ---- vec.hip
 hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,
                            const double* wel, double* gr, double* Hr, hipStream_t st);

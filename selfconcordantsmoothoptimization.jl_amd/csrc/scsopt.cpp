@@ -229,6 +229,12 @@ struct scs_ctx {
   int* cinfo = nullptr;
   CholAux caux;             // two-level factorization constants (chol.hip)
   LUAux lu;                 // blocked LU (lu.hip): the non-SPD fallback and the GGN sample-space system
+  // scs_set_solver: SCS_SOLVER_REFERENCE solves the way the reference does -- Householder QR for
+  // ProxGGNSCORE's systems (prox-GGN-SCORE.jl:126,131), LU (Julia's `\`) for ProxNSCORE's
+  int solver = 0;
+  QRAux qr;                 // qr.hip workspace
+  double* qrM = nullptr;    // the sample-space system transposed to column-major for the QR
+  int64_t qrM_n = 0;
   double* luM = nullptr;    // scs_lu_eval's system / rhs / info, kept so the LU graphs replay
   double* lub = nullptr;
   int* luinfo = nullptr;
@@ -1143,13 +1149,46 @@ void solve_lu_fallback(scs_ctx* c, double* rhs, hipEvent_t e0) {
 // partial pivoting (lu.hip; the reference's `\`, prox-N-SCORE.jl:70) from the saved copy when
 // a pivot is not positive (e.g. the indefinite Q of a CE loss on ±1 labels,
 // test/test_algs.jl:10), or always with force_lu (scs_solve_eval).
-void solve_system(scs_ctx* c, double* rhs, bool force_lu = false) {
+// the reference's own solver (scs_set_solver(SCS_SOLVER_REFERENCE)): qr(JQJ) \ Je by Householder QR
+// (prox-GGN-SCORE.jl:131) on the symmetrized copy Gc; a NaN / Inf system gives a NaN direction
+void solve_qr(scs_ctx* c, double* rhs, hipEvent_t e0) {
+  const int64_t m = c->m, ld = c->mpad;
+  if (c->g_from_cache) {
+    HCK(hipMemcpyAsync(c->Gc, c->Gk, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+    HCK(launch_diag_add(c->Gc, c->mpad, m, c->lam, c->Hr, c->st));
+  }
+  HCK(launch_symmetrize(c->Gc, ld, m, c->st));
+  int info = 0;
+  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+  HCK(launch_nonfinite(c->Gc, ld, m, rhs, c->cinfo, c->st));
+  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  c->lu_fallback_used = false;
+  if (info != 0) {
+    HCK(launch_fill(rhs, m, std::numeric_limits<double>::quiet_NaN(), c->st));
+    tend(c, T_SOLVE, e0);
+    return;
+  }
+  HCK(qr_prepare(c->Gc, ld, m, ld, c->st));
+  HCK(qr_solve(c->Gc, ld, ld, &c->qr, rhs, &c->caux, c->st));
+  tend(c, T_SOLVE, e0);
+}
+
+void solve_system(scs_ctx* c, double* rhs, bool force_lu = false, bool force_qr = false) {
   const int64_t m = c->m, ld = c->mpad;
   hipEvent_t e0;
   tbegin(c, T_SOLVE, &e0);
   // the LU fallback needs the system the in-place factor destroys: copied up front, or -- when
   // this step's Gram came from the cache -- rebuilt from it only if the factor fails
   if (!c->g_from_cache) HCK(hipMemcpyAsync(c->Gc, c->G, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+  if (c->solver == SCS_SOLVER_REFERENCE && !force_lu && !force_qr) {
+    if (c->method == SCS_PROX_GGNSCORE) force_qr = true;   // qr(JQJ) \ Je
+    else force_lu = true;                                  // (H + λHr) \ ∇q: Julia's `\` = LU
+  }
+  if (force_qr) {
+    solve_qr(c, rhs, e0);
+    return;
+  }
   int info = 0;
   if (!force_lu) {
     HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
@@ -1431,7 +1470,7 @@ int pipe_mode(const scs_ctx* c, bool cacheable) {
   const char* e = std::getenv("SCS_CHOL_PIPE");   // read per step (tests toggle it in-process)
   const int mode = e ? std::atoi(e) : 0;
   const int64_t nblk = c->mpad / 128;
-  const bool ok = !cacheable && !sharded(c) && !c->sparse && c->gwork &&
+  const bool ok = !cacheable && !sharded(c) && !c->sparse && c->gwork && c->solver == 0 &&
                   nblk >= 3 * chol_outer_block();
   return ok && (mode == 1 || mode == 2) ? mode : 0;
 }
@@ -1645,6 +1684,16 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
   sync(c);
   if (info != 0) {
     HCK(launch_fill(c->bS, n1, std::numeric_limits<double>::quiet_NaN(), c->st));
+  } else if (c->solver == SCS_SOLVER_REFERENCE) {
+    // qr(I + A) \ residual (prox-GGN-SCORE.jl:126): the row-major system transposed into a
+    // column-major copy with identity padding, Householder QR
+    if (c->qrM_n != np1) {
+      dfree_t(c, c->qrM);
+      c->qrM = dalloc<double>(c, (size_t)np1 * np1);
+      c->qrM_n = np1;
+    }
+    HCK(qr_from_rowmajor(c->Ms, np1, c->qrM, np1, n1, np1, c->st));
+    HCK(qr_solve(c->qrM, np1, np1, &c->qr, c->bS, &c->caux, c->st));
   } else {
     HCK(lu_aux_init(&c->lu, np1, c->st));
     HCK(lu_factor(c->Ms, np1, n1, np1, &c->lu, c->cinfo, c->st));
@@ -2006,6 +2055,7 @@ int scs_destroy(scs_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->cbh) (void)hipHostFree(c->cbh);
   lu_aux_free(&c->lu);
+  qr_aux_free(&c->qr);
   if (c->sf) {
     (void)hipStreamSynchronize(c->sf);
     (void)hipStreamDestroy(c->sf);
@@ -2565,6 +2615,14 @@ int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* 
       sync(c);
     }
     c->reg_set = true;
+  });
+}
+
+int scs_set_solver(scs_ctx* c, int kind) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_solver(s_, kind); });
+  return guarded(c, [&] {
+    if (kind != SCS_SOLVER_DEFAULT && kind != SCS_SOLVER_REFERENCE) fail(c, SCS_ERR_ARG, "scs_set_solver: kind %d", kind);
+    c->solver = kind;
   });
 }
 
@@ -3315,7 +3373,8 @@ int scs_solve_eval(scs_ctx* c, const double* w, const double* dvec, const double
     h2d(c, c->gq, v.data(), c->mpad);
     sync(c);
     c->g_from_cache = false;
-    solve_system(c, c->gq, mode == 1);
+    if (mode < 0 || mode > 2) fail(c, SCS_ERR_ARG, "scs_solve_eval: mode %d (0 step path, 1 LU, 2 QR)", mode);
+    solve_system(c, c->gq, mode == 1, mode == 2);
     d2h(c, x, c->gq, c->m);
     sync(c);
     if (used_lu) *used_lu = c->lu_fallback_used ? 1 : 0;

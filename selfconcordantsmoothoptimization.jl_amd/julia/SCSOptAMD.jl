@@ -14,7 +14,7 @@ using SparseArrays
 using SelfConcordantSmoothOptimization
 import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel, is_interval_set
 
-export DeviceProblem, configure!, iterate_device!, set_gram_cache!, rccl_unique_id, set_comm_rccl!,
+export DeviceProblem, configure!, iterate_device!, set_gram_cache!, set_solver!, rccl_unique_id, set_comm_rccl!,
        set_comm_callback!
 
 const lib = joinpath(@__DIR__, "..", "scsopt", "libscsopt.so")
@@ -326,6 +326,11 @@ end
 # the reference recomputes it every step (prox-GGN-SCORE.jl:129) and that stays the default.
 set_gram_cache!(model::DeviceProblem, on::Bool=true) =
     chk(ccall((:scs_set_gram_cache, lib), Cint, (Ptr{Cvoid}, Cint), model.ctx, on ? 1 : 0), model.ctx)
+
+# The reference's own factorizations (scs_set_solver): Householder QR for ProxGGNSCORE's systems
+# (prox-GGN-SCORE.jl:126,131), LU for ProxNSCORE's -- the default is Cholesky with the LU fallback.
+set_solver!(model::DeviceProblem, reference::Bool=true) =
+    chk(ccall((:scs_set_solver, lib), Cint, (Ptr{Cvoid}, Cint), model.ctx, reference ? 1 : 0), model.ctx)
 
 method_code(m) = m isa ProxNSCORE ? 1 : m isa ProxGGNSCORE ? 2 : m isa ProxLQNSCORE ? 3 : error("unknown method")
 

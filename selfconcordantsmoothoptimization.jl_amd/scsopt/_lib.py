@@ -24,6 +24,7 @@ REG = {"l1": 1, "l2": 2, "indbox": 3, "gl": 4}
 SMOOTH = {"phuber_l1l2": 1, "phuber_indbox": 2, "phuber_gl": 3, "exp_indbox": 4, "logexp_indbox": 5, "osba_l1l2": 6,
           "osba_gl": 7}
 METHOD = {"nscore": 1, "ggnscore": 2, "lqnscore": 3}
+SOLVER = {"default": 0, "reference": 1}
 
 # One HIP runtime per process: torch's wheel bundles ROCm libraries whose NEEDED
 # names ("libamdhip64.so") differ from the SONAMEs ("libamdhip64.so.7"), so if
@@ -100,6 +101,7 @@ _SIGS = {
     "scs_eval_grad": (C.c_int, [C.c_void_p, c_dp, c_dp]),
     "scs_eval_reg": (C.c_int, [C.c_void_p, c_dp, c_dp]),
     "scs_set_gram_cache": (C.c_int, [C.c_void_p, C.c_int]),
+    "scs_set_solver": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_set_group_map": (C.c_int, [C.c_void_p, c_i64p, C.c_int64]),
     "scs_set_batches": (C.c_int, [C.c_void_p, c_i64p, c_i64p, C.c_int64]),
     "scs_select_batch": (C.c_int, [C.c_void_p, C.c_int64]),

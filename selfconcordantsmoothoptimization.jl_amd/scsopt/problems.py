@@ -345,6 +345,12 @@ class Problem:
         step (prox-GGN-SCORE.jl:129), which stays the default.  Results are bit-identical."""
         self.ctx.check(_lib.lib.scs_set_gram_cache(self.ctx.h, int(bool(on))))
 
+    def set_solver(self, kind="default"):
+        """"default": Cholesky (LU fallback) / LU; "reference": the reference's factorizations --
+        Householder QR for ProxGGNSCORE's systems (prox-GGN-SCORE.jl:126,131), LU for ProxNSCORE's
+        (prox-N-SCORE.jl:70).  scs_set_solver."""
+        self.ctx.check(_lib.lib.scs_set_solver(self.ctx.h, _lib.SOLVER[kind]))
+
     def set_batches(self, batches=None):
         """Register the collected loader batches (iterate.jl:141-146): a list of row-index arrays
         (0-based, GLOBAL rows: on several ranks every rank passes the same list and keeps the rows

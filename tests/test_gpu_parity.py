@@ -840,3 +840,78 @@ def test_cholesky_dag_launches_bit_identical(m, ob, la, monkeypatch):
     for r in (b, c):
         assert a.obj == r.obj and a.pri_res_norm == r.pri_res_norm and a.epochs == r.epochs
         assert np.array_equal(bits(a.x), bits(r.x))
+
+
+@pytest.mark.parametrize("m", [300, 1000, 2304])
+def test_householder_qr_solve(m):
+    """The reference solver's Householder QR (qr.hip, scs_solve_eval mode 2: LAPACK dgeqrf / dlarfg
+    conventions, 128-column compact-WY panels, identity padding for m not a multiple of 128) on
+    (Aᵀ diag(w) A + diag d) x = rhs: against LAPACK's own QR solve (numpy), and its backward error."""
+    N = m + 77
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=41)
+    rng = np.random.default_rng(42)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-3
+    rhs = rng.standard_normal(m)
+    x, used_lu = p.solve_eval(w, d, rhs, mode=2)
+    assert not used_lu
+    A, _ = p.get_data()
+    M = A.T @ (w[:, None] * A) + np.diag(d)
+    Q, R = np.linalg.qr(M)
+    xr = np.linalg.solve(R, Q.T @ rhs)
+    cond = np.linalg.cond(M)
+    np.testing.assert_allclose(x, xr, rtol=0, atol=1e-13 * cond * float(np.max(np.abs(xr))))
+    assert np.linalg.norm(M @ x - rhs) <= 1e-12 * np.linalg.norm(M, 2) * np.linalg.norm(x)
+
+
+@pytest.mark.parametrize("case", ["ggn_feature", "ggn_sample", "nscore"])
+def test_reference_solver_trajectory(case, monkeypatch):
+    """scs_set_solver(SCS_SOLVER_REFERENCE): ProxGGNSCORE's qr(JQJ) \\ Je (feature branch) and
+    qr(I + A) \\ residual (sample branch, N + 1 <= m) by Householder QR, ProxNSCORE's `\\` by LU --
+    trajectories vs the oracle's literal restatement (np.linalg.qr, not FAST_LINALG) at rtol 1e-8."""
+    monkeypatch.setattr(O, "FAST_LINALG", False)
+    N, m = {"ggn_feature": (2048, 700), "ggn_sample": (200, 640), "nscore": (1500, 600)}[case]
+    x0 = np.random.default_rng(5).standard_normal(m)
+    if case == "nscore":
+        f, out, kind, of = losses.logistic_margin(1.0 / N), None, 2, O.Loss("logistic_margin", 1.0 / N)
+        meth, ometh = scsopt.ProxNSCORE(), O.ProxNSCORE()
+    else:
+        f, out, kind = losses.logistic_ce(1.0 / N), losses.sigmoid_ce(1.0 / N), 1
+        of = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+        meth, ometh = scsopt.ProxGGNSCORE(), O.ProxGGNSCORE()
+    p = scsopt.Problem.synthetic(N, m, x0, f, 2e-3, kind=kind, seed=43, out_fn=out)
+    p.set_solver("reference")
+    A, y = p.get_data()
+    om = O.Problem(A, y, x0, of, 2e-3)
+    sol = scsopt.iterate(meth, p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=6, verbose=0)
+    osol = O.iterate(ometh, om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=6)
+    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+
+
+def test_reference_solver_ill_conditioned():
+    """C4's tiny first λ (1e-8) with N barely above m: JQJ + 1e-8·diag(Hr) is ill-conditioned
+    (cond ~1e5 .. 1e6).  The reference-mode QR direction agrees with LAPACK's QR solve of the same system
+    at the O(cond·eps) level, as does the default Cholesky; both are reported."""
+    N, m = 1030, 1024
+    x0 = np.random.default_rng(9).standard_normal(m)
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-8, kind=3, seed=47,
+                                 out_fn=losses.linear_ls(1.0 / N))
+    A, y = p.get_data()
+    rng = np.random.default_rng(10)
+    w = np.full(N, 1.0 / N)
+    d = 1e-8 * (rng.random(m) + 0.5)
+    rhs = rng.standard_normal(m)
+    M = A.T @ (w[:, None] * A) + np.diag(d)
+    Q, R = np.linalg.qr(M)
+    xr = np.linalg.solve(R, Q.T @ rhs)
+    cond = np.linalg.cond(M)
+    assert cond > 1e4
+    xq, _ = p.solve_eval(w, d, rhs, mode=2)
+    xc, _ = p.solve_eval(w, d, rhs, mode=0)
+    scale = float(np.max(np.abs(xr)))
+    eq = float(np.max(np.abs(xq - xr))) / scale
+    ec = float(np.max(np.abs(xc - xr))) / scale
+    print(f"[qr] cond {cond:.2e}: max rel |x_QR - x_LAPACK-QR| = {eq:.2e}, Cholesky {ec:.2e}")
+    assert eq <= 1e-13 * cond and ec <= 1e-13 * cond
