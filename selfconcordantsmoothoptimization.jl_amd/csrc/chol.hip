@@ -1392,12 +1392,11 @@ static bool solve_persist() {
 }
 
 hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, const double* y, double* x,
-                           CholAux* a, hipStream_t st) {
+                           unsigned* flags, unsigned gen, int* err, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
-  if (!a || !a->sflags || (int64_t)a->nblk < nblk) return hipErrorInvalidValue;
-  const unsigned gen = ++a->sgen == 0 ? ++a->sgen : a->sgen;
-  hipLaunchKernelGGL(chol_bwd_persist_kernel, dim3((unsigned)nblk), dim3(PS_NT), 0, st, U, ld, W, y, x,
-                     a->sflags + a->nblk, gen, a->serr, nblk);
+  if (!flags || !err || gen == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(chol_bwd_persist_kernel, dim3((unsigned)nblk), dim3(PS_NT), 0, st, U, ld, W, y, x, flags, gen,
+                     err, nblk);
   return hipGetLastError();
 }
 

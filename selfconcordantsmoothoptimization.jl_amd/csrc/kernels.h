@@ -176,6 +176,11 @@ struct QRAux {
   double *part = nullptr, *tw = nullptr, *tau = nullptr, *scal = nullptr, *V = nullptr, *Vt = nullptr,
          *Wm = nullptr, *Ym = nullptr, *Gv = nullptr, *T = nullptr, *ones = nullptr, *W = nullptr;
   int2* tiles = nullptr;
+  // the one-launch backward solve's block flags (generation-stamped, never reset) and its
+  // dependency-wait error flag (set when a wait gives up after ~30 s: never expected)
+  unsigned* flags = nullptr;
+  int* err = nullptr;
+  unsigned gen = 0;
 };
 // set the identity padding of a column-major system in place / build it from a row-major one
 hipError_t qr_prepare(double* A, int64_t ld, int64_t n, int64_t npad, hipStream_t st);
@@ -183,12 +188,12 @@ hipError_t qr_from_rowmajor(const double* S, int64_t lds, double* D, int64_t ldd
                             hipStream_t st);
 hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st);
 void qr_aux_free(QRAux* a);
-hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, CholAux* ca, hipStream_t st);
+hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hipStream_t st);
 // chol.hip pieces the QR solve reuses: the inverses of the 128 x 128 upper diagonal blocks of R
 // (W, as the Cholesky's), and the one-launch backward solve U x = y
 hipError_t chol_tri_inverse(const double* R, int64_t ld, int nblk, double* W, hipStream_t st);
 hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, const double* y, double* x,
-                           CholAux* a, hipStream_t st);
+                           unsigned* flags, unsigned gen, int* err, hipStream_t st);
 
 // ---- vec.hip
 hipError_t launch_smoother(int kind, const double* x, int64_t m, double mu, const double* a, const double* b,

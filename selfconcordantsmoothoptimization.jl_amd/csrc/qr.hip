@@ -179,6 +179,10 @@ static void qr_free_bufs(QRAux* a) {
     }
   if (a->tiles) (void)hipFree(a->tiles);
   a->tiles = nullptr;
+  if (a->flags) (void)hipFree(a->flags);
+  a->flags = nullptr;
+  a->err = nullptr;
+  a->gen = 0;
   a->npad = 0;
 }
 
@@ -210,6 +214,9 @@ hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st) {
   if (e == hipSuccess) e = hipMalloc(&a->tiles, sizeof(int2) * std::max<size_t>(tl.size(), 1));
   if (e == hipSuccess && !tl.empty())
     e = hipMemcpyAsync(a->tiles, tl.data(), sizeof(int2) * tl.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMalloc(&a->flags, sizeof(unsigned) * (size_t)nbk + sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(a->flags, 0, sizeof(unsigned) * (size_t)nbk + sizeof(int), st);
+  if (e == hipSuccess) a->err = (int*)(a->flags + nbk);
   if (e == hipSuccess) {
     // ones[0, npad) = +1, ones[npad, npad + QB) = -1 (the Gram kernels' weights)
     hipLaunchKernelGGL(qr_fill_kernel, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, st, a->ones, npad, 1.0);
@@ -238,7 +245,7 @@ static hipError_t qr_gram(const double* A1, int64_t lda1, const double* A2, int6
   return hipSuccess;
 }
 
-hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, CholAux* ca, hipStream_t st) {
+hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hipStream_t st) {
   hipError_t e = qr_aux_init(a, npad, st);
   if (e != hipSuccess) return e;
   const int nbk = (int)(npad / QB);
@@ -277,7 +284,8 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, Ch
   if (e != hipSuccess) return e;
   e = hipMemcpyAsync(a->Ym, b, sizeof(double) * npad, hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return e;
-  return chol_back_solve(A, ld, npad, a->W, a->Ym, b, ca, st);
+  a->gen = ++a->gen == 0 ? ++a->gen : a->gen;
+  return chol_back_solve(A, ld, npad, a->W, a->Ym, b, a->flags, a->gen, a->err, st);
 }
 
 }  // namespace scs

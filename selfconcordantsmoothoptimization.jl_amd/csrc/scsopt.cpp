@@ -1151,6 +1151,19 @@ void solve_lu_fallback(scs_ctx* c, double* rhs, hipEvent_t e0) {
 // test/test_algs.jl:10), or always with force_lu (scs_solve_eval).
 // the reference's own solver (scs_set_solver(SCS_SOLVER_REFERENCE)): qr(JQJ) \ Je by Householder QR
 // (prox-GGN-SCORE.jl:131) on the symmetrized copy Gc; a NaN / Inf system gives a NaN direction
+// Householder QR solve of the column-major npad x npad system A (identity-padded) with b := A \ b;
+// a backward-solve dependency wait that gave up (~30 s, never expected) fails the call
+static void qr_run(scs_ctx* c, double* A, int64_t npad, double* b) {
+  HCK(qr_solve(A, npad, npad, &c->qr, b, c->st));
+  int late = 0;
+  HCK(hipMemcpyAsync(&late, c->qr.err, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  if (late) {
+    HCK(hipMemsetAsync(c->qr.err, 0, sizeof(int), c->st));
+    fail(c, SCS_ERR_HIP, "QR: a dependency wait of the backward solve timed out");
+  }
+}
+
 void solve_qr(scs_ctx* c, double* rhs, hipEvent_t e0) {
   const int64_t m = c->m, ld = c->mpad;
   if (c->g_from_cache) {
@@ -1170,7 +1183,7 @@ void solve_qr(scs_ctx* c, double* rhs, hipEvent_t e0) {
     return;
   }
   HCK(qr_prepare(c->Gc, ld, m, ld, c->st));
-  HCK(qr_solve(c->Gc, ld, ld, &c->qr, rhs, &c->caux, c->st));
+  qr_run(c, c->Gc, ld, rhs);
   tend(c, T_SOLVE, e0);
 }
 
@@ -1693,7 +1706,7 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
       c->qrM_n = np1;
     }
     HCK(qr_from_rowmajor(c->Ms, np1, c->qrM, np1, n1, np1, c->st));
-    HCK(qr_solve(c->qrM, np1, np1, &c->qr, c->bS, &c->caux, c->st));
+    qr_run(c, c->qrM, np1, c->bS);
   } else {
     HCK(lu_aux_init(&c->lu, np1, c->st));
     HCK(lu_factor(c->Ms, np1, n1, np1, &c->lu, c->cinfo, c->st));
