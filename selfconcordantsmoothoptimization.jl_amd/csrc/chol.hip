@@ -452,6 +452,20 @@ static int outer_block();
 // profiles/r03/segv/) -- so the profiled configuration could not be the benchmarked one.  The
 // chain is shortened instead (chol_diag_kernel, the fused chain launches).  Masking is best effort:
 // a failure falls back to an ordinary non-blocking stream.
+// SCS_CHOL_BULK_SKIP: the CU ids (within a shader engine, HW_REG_HW_ID bits 11:8; a bit mask,
+// hex accepted) whose workgroup slots the bulk stream's launches leave to the chain
+// (gram_launch_bounded); 0 = plain launches.  Default: CU id 5 (present in every shader engine
+// of the measured boxes: 4 CUs per XCD, 32 in all -- the r02 CU reserve) up to m = 8192, where
+// the chain's launches waited for slots the trailing update held (C2 solve 10.20 -> 9.55 ms);
+// none above: m = 16384 38.6 vs 39.3 ms, m = 32768 212.6 vs 228.8 ms with it (the bulk stream
+// bounds those factors; profiles/r03/chol/bounded/).  Which CUs a harvested part lacks only
+// changes how many are left free.
+static unsigned bulk_skip_mask(int nblk) {
+  const char* e = getenv("SCS_CHOL_BULK_SKIP");
+  if (e) return (unsigned)strtoul(e, nullptr, 0);
+  return nblk <= 64 ? 0x20u : 0u;
+}
+
 static hipError_t create_bulk_stream(hipStream_t* s, int nblk) {
   const char* env = getenv("SCS_CHOL_RESERVE_CUS");
   const int reserve = env ? atoi(env) : 0;
@@ -465,6 +479,16 @@ static hipError_t create_bulk_stream(hipStream_t* s, int nblk) {
     std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
     for (int i = 0; i < ncu - reserve; ++i) mask[i / 32] |= 1u << (i % 32);
     if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+  }
+  // SCS_CHOL_BULK_PRIO=1: the bulk stream at the lowest stream priority, so a workgroup slot a
+  // finished bulk workgroup frees goes to the chain's pending launch first (A/B)
+  const char* pe = getenv("SCS_CHOL_BULK_PRIO");
+  if (pe && atoi(pe) > 0) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+        hipStreamCreateWithPriority(s, hipStreamNonBlocking, least) == hipSuccess)
+      return hipSuccess;
     (void)hipGetLastError();
   }
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
@@ -484,6 +508,15 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = create_bulk_stream(&a->st2, nblk);
+  if (e == hipSuccess) e = hipMalloc(&a->bctr, 16 * sizeof(unsigned));
+  if (e == hipSuccess) {
+    a->bskip = bulk_skip_mask(nblk);
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      a->bslots = 2 * ncu;   // the 128 x 128 throughput kernels: 2 workgroups per CU
+    else
+      a->bslots = 0;
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev2, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev3, hipEventDisableTiming);
@@ -512,6 +545,8 @@ void chol_aux_free(CholAux* a) {
   a->spart = nullptr;
   if (a->sflags) (void)hipFree(a->sflags);
   a->sflags = nullptr;
+  if (a->bctr) (void)hipFree(a->bctr);
+  a->bctr = nullptr;
   a->serr = nullptr;
   for (void* p : {(void*)a->dtasks, (void*)a->ddeps, (void*)a->dcnt, (void*)a->dper})
     if (p) (void)hipFree(p);
@@ -521,7 +556,10 @@ void chol_aux_free(CholAux* a) {
   a->dag_ob = 0;
   a->dstep.clear();
   a->dnext.clear();
-  if (a->st2) (void)hipStreamDestroy(a->st2);
+  // SCS_CHOL_KEEP_BULK=1 (diagnosis of the profiler's exit fault with a CU-masked stream): the
+  // bulk stream is left to the runtime's teardown instead of destroyed here
+  static const bool keep = getenv("SCS_CHOL_KEEP_BULK") && atoi(getenv("SCS_CHOL_KEEP_BULK")) > 0;
+  if (a->st2 && !keep) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
   a->ev1 = a->ev2 = a->ev3 = nullptr;
@@ -553,23 +591,31 @@ static int outer_block() {
 }
 
 // forward solve of the strip rows [lo, hi) (inner blocks) x nc columns starting at block c0
+// (bulk: the bulk stream's CU-bounded launches, gram_launch_bounded)
 static hipError_t strip_solve(double* G, int64_t ld, const double* W, const CholAux* a, int lo, int hi, int c0, int nc,
-                              hipStream_t st) {
+                              hipStream_t st, bool bulk = false) {
+  auto launch = [&](const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w, int64_t k1,
+                    const int2* tiles, int ntiles, double* R, int flags) {
+    if (bulk)
+      return gram_launch_bounded(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, a->bctr, a->bskip, a->bslots,
+                                 st);
+    return gram_launch_gen(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, st);
+  };
   if (hi - lo == 1) {
     double* R = G + (int64_t)c0 * CB * ld + (int64_t)lo * CB;
-    return gram_launch_gen(W + (int64_t)lo * CB * CB, CB, R, ld, a->w, 0, CB, rect_list(a, 1), nc, R, ld, 0, st);
+    return launch(W + (int64_t)lo * CB * CB, CB, R, ld, a->w, CB, rect_list(a, 1), nc, R, 0);
   }
   const int mid = (lo + hi) / 2;
-  hipError_t e = strip_solve(G, ld, W, a, lo, mid, c0, nc, st);
+  hipError_t e = strip_solve(G, ld, W, a, lo, mid, c0, nc, st, bulk);
   if (e != hipSuccess) return e;
   // R2 -= U12ᵀ X1: A1 = U[lo:mid, mid:hi] (panels mid.., rows from lo), A2 = X1 (panels c0.., rows from lo)
   const double* U12 = G + (int64_t)mid * CB * ld + (int64_t)lo * CB;
   const double* X1 = G + (int64_t)c0 * CB * ld + (int64_t)lo * CB;
   double* R2 = G + (int64_t)c0 * CB * ld + (int64_t)mid * CB;
-  e = gram_launch_gen(U12, ld, X1, ld, a->w + CB, 0, (int64_t)(mid - lo) * CB, rect_list(a, hi - mid), (hi - mid) * nc,
-                      R2, ld, /*GRAM_ACCUMULATE*/ 2, st);
+  e = launch(U12, ld, X1, ld, a->w + CB, (int64_t)(mid - lo) * CB, rect_list(a, hi - mid), (hi - mid) * nc, R2,
+             /*GRAM_ACCUMULATE*/ 2);
   if (e != hipSuccess) return e;
-  return strip_solve(G, ld, W, a, mid, hi, c0, nc, st);
+  return strip_solve(G, ld, W, a, mid, hi, c0, nc, st, bulk);
 }
 
 // Lookahead (default; SCS_CHOL_LA=0 off).  Outer block t's strip solve B and trailing update C
@@ -908,7 +954,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     // Bb on st2 once A_t is done (stream order keeps C12_{t-1} before it)
     if (e == hipSuccess) e = hipEventRecord(a->ev3, st);
     wait(a->st2, a->ev3);
-    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2);
+    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2, true);
     // Ba, C1a on the chain after C12_{t-1}
     if (c12_pending) wait(st, a->ev2);
     const int n1a = (OB * (OB + 1)) / 2;
@@ -924,8 +970,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (e == hipSuccess) e = hipEventRecord(a->ev1, st);
     wait(a->st2, a->ev1);
     if (e == hipSuccess)
-      e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n1a, ntri - n1a, trail,
-                          ld, 2 | 4, a->st2);
+      e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n1a, ntri - n1a,
+                              trail, ld, 2 | 4, a->bctr, a->bskip, a->bslots, a->st2);
     if (e == hipSuccess) e = hipEventRecord(a->ev2, a->st2);
     if (e != hipSuccess) return e;
     c12_pending = true;

@@ -57,7 +57,42 @@ namespace scs {
 // TI = 64-row wave groups along i: TI = 2 -> 128 x 128 tiles, 4 waves, 2 WG/CU;
 // TI = 4 -> 256 x 128 tiles, 8 waves, 1 WG/CU (25 % less operand traffic per flop).
 // TILED: operands are the panel-blocked A (common.h tiled_off), lda1/lda2 = S stages.
-template <bool NOLOAD, int TI, bool TILED = false>
+// CU-bounded persistent launches (BND instances; the Cholesky's bulk stream, chol.hip): a
+// workgroup on a CU whose id within its shader engine (HW_REG_HW_ID bits 11:8) is set in `skip`
+// leaves at once -- unless it is the launch's last arrival, so the tiles never depend on where
+// the dispatcher puts the workgroups -- and every other workgroup claims tiles until none is left.
+// The skipped CUs stay free for the serial chain's launches on the other stream (the effect of a
+// CU-masked queue without one).  Claims keep the plain launch's XCD-aware split: the tile list is
+// cut into 8 contiguous segments, a workgroup claims from its XCD's segment (HW_REG_XCC_ID) first
+// and then from the others in turn.  ctr = {claims per segment [8], arrivals}, zero at launch.
+__device__ __forceinline__ int bnd_claim(unsigned* ctr, int ntiles) {
+  const int q8 = ntiles / 8, r8 = ntiles % 8;
+  const int x0 = (int)((unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u);   // HW_REG_XCC_ID
+  for (int d = 0; d < 8; ++d) {
+    const int x = (x0 + d) & 7, len = q8 + (x < r8 ? 1 : 0);
+    if (len == 0) continue;
+    const unsigned t = atomicAdd(ctr + x, 1u);
+    if ((int)t < len) return x * q8 + (x < r8 ? x : r8) + (int)t;
+  }
+  return ntiles;
+}
+__device__ __forceinline__ int bnd_first(unsigned* ctr, unsigned skip, int ntiles, int* s) {
+  if (threadIdx.x == 0) {
+    const unsigned cu = ((unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 15u;   // HW_REG_HW_ID
+    const unsigned arr = atomicAdd(ctr + 8, 1u);
+    *s = (((skip >> cu) & 1u) && arr + 1 < gridDim.x) ? -1 : bnd_claim(ctr, ntiles);
+  }
+  __syncthreads();
+  return *s;
+}
+__device__ __forceinline__ int bnd_next(unsigned* ctr, int ntiles, int* s) {
+  __syncthreads();   // every wave is done with the previous tile's LDS and with *s
+  if (threadIdx.x == 0) *s = bnd_claim(ctr, ntiles);
+  __syncthreads();
+  return *s;
+}
+
+template <bool NOLOAD, int TI, bool TILED = false, bool BND = false>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
     const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
     const double* __restrict__ w, int64_t k0, int64_t Nk, const int2* __restrict__ tiles, int ntiles,
@@ -74,7 +109,13 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
   const int orig = blockIdx.x;
   const int xcd = orig % 8;
   int bi, bj, tix, part = -1;
-  if (work) {
+  __shared__ int s_claim;
+  if constexpr (BND) {   // counters in P, skip mask in seglen (bnd_first)
+    tix = bnd_first(reinterpret_cast<unsigned*>(P), (unsigned)seglen, ntiles, &s_claim);
+    if (tix < 0 || tix >= ntiles) return;
+    bi = tiles[tix].x;
+    bj = tiles[tix].y;
+  } else if (work) {
     // scheduled work list (gram_schedule): XCD x runs items [x*seglen, (x+1)*seglen) in order;
     // item = (bi, bj, ks, idx): ks < 0 -> whole K, canonical tile idx; ks >= 0 -> K piece ks of
     // nsplit, partial slot idx; bi < 0 -> padding
@@ -97,8 +138,10 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
     bi = tl.x;
     bj = tl.y;
   }
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+bnd_tile:
+  int tid_ = threadIdx.x;
+  if constexpr (BND) asm volatile("" : "+v"(tid_));   // per tile: nothing derived from it is hoisted out of the loop
+  const int tid = tid_, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const double* __restrict__ Ai = A1 + (int64_t)bi * GTI * lda1;
   const double* __restrict__ Aj = A2 + (int64_t)bj * GT * lda2;
@@ -208,6 +251,13 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
         if (accumulate) *dst += acc[ti][tj][r];
         else *dst = acc[ti][tj][r];
       }
+  if constexpr (BND) {
+    tix = bnd_next(reinterpret_cast<unsigned*>(P), ntiles, &s_claim);
+    if (tix >= ntiles) return;
+    bi = tiles[tix].x;
+    bj = tiles[tix].y;
+    goto bnd_tile;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -539,7 +589,7 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 // order, then a fixed 8-lane butterfly; piece p of a K-split tile writes row p of VP (row
 // stride vps, features of panel bj), summed in piece order by gram_vfinal_kernel.  G is
 // unchanged bit for bit (the MFMA stream is the same).
-template <int PIPE, int TI = 2, bool CM = false, bool AV = false>
+template <int PIPE, int TI = 2, bool CM = false, bool AV = false, bool BND = false>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     const double* __restrict__ A, int64_t S, const double* __restrict__ w, int64_t k0, int64_t Nk,
     const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int flags,
@@ -560,7 +610,13 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
   const int orig = blockIdx.x;
   const int xcd = orig % 8;
   int bi, bj, tix, part = -1, piece = 0;
-  if (work) {
+  __shared__ int s_claim;
+  if constexpr (BND) {   // counters in scnt, skip mask in sob (bnd_first)
+    tix = bnd_first(scnt, (unsigned)sob, ntiles, &s_claim);
+    if (tix < 0 || tix >= ntiles) return;
+    bi = tiles[tix].x;
+    bj = tiles[tix].y;
+  } else if (work) {
     const int4 it = work[xcd * seglen + orig / 8];
     if (it.x < 0) return;
     bi = it.x;
@@ -581,7 +637,10 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     bi = tl.x;
     bj = tl.y;
   }
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+bnd_tile:
+  int tid_ = threadIdx.x;
+  if constexpr (BND) asm volatile("" : "+v"(tid_));   // per tile: nothing derived from it is hoisted out of the loop
+  const int tid = tid_, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int sc = tid & 7, sf0 = tid >> 3;
   const int64_t st0 = k0 / GBK;
@@ -771,10 +830,17 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
       }
   // strip completion (scsopt.cpp gram_factor_pipelined, one-launch mode): this tile's rows lie in
   // outer strip bj / sob; each thread's stores are released to device scope before one count
-  if (scnt && part < 0) {
+  if (!BND && scnt && part < 0) {
     __threadfence();
     __syncthreads();
     if (tid == 0) atomicAdd(scnt + bj / sob, 1u);
+  }
+  if constexpr (BND) {
+    tix = bnd_next(scnt, ntiles, &s_claim);
+    if (tix >= ntiles) return;
+    bi = tiles[tix].x;
+    bj = tiles[tix].y;
+    goto bnd_tile;
   }
 }
 
@@ -923,6 +989,34 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
+  return hipGetLastError();
+}
+
+// gram_launch_gen's throughput launches as CU-bounded persistent launches (bnd_first): at most
+// `slots` workgroups, the CUs of `skip` left free.  Latency-sized launches and skip == 0 take
+// gram_launch_gen's path.  Per tile the same kernel body and MFMA order: bitwise the same G.
+hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                               int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
+                               unsigned* ctr, unsigned skip, int slots, hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  const char* se = getenv("SCS_GRAM_SMALL");
+  const int small_max = se ? atoi(se) : 64;
+  const bool small = k1 - k0 <= 512 && (k1 - k0) % (8 * GBK) == 0 && k1 > k0 && ntiles <= small_max;
+  if (!ctr || skip == 0 || slots <= 0 || small)
+    return gram_launch_gen(A1, lda1, A2, lda2, w, k0, k1, tiles, ntiles, G, ldg, flags, st);
+  hipError_t e = hipMemsetAsync(ctr, 0, 9 * sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  // enough workgroups that the ones left after the skipped CUs' leave take every tile in one round
+  // (a launch smaller than the chip), else one per workgroup slot of the device
+  const int want = ntiles + (ntiles + 6) / 7 + 8;
+  const unsigned grid = (unsigned)(want < slots ? want : slots);
+  if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2, true, false, true>), dim3(grid), dim3(256), 0, st, A1, lda1, w, k0, k1,
+                       tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, ctr,
+                       (int)skip);
+  else
+    hipLaunchKernelGGL((gram_f64_kernel<false, 2, false, true>), dim3(grid), dim3(256), 0, st, A1, lda1, A2, lda2, w,
+                       k0, k1, tiles, ntiles, G, ldg, flags, nullptr, (int)skip, 0, reinterpret_cast<double*>(ctr));
   return hipGetLastError();
 }
 

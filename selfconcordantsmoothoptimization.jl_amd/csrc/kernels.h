@@ -43,6 +43,11 @@ void gram_tile_list_rowmajor(int nb, int2* out);
 hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                            hipStream_t st);
+// the same as CU-bounded persistent launches leaving the CUs of `skip` (ids within a shader engine)
+// free; ctr: 9 device counters, zeroed in stream order by the call
+hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                               int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
+                               unsigned* ctr, unsigned skip, int slots, hipStream_t st);
 // the latency form of gram_launch_gen (128 x 16/32 strips per workgroup, loads 8 stages ahead);
 // the same bits per tile as gram_launch_gen's other kernels
 hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
@@ -89,6 +94,11 @@ struct CholAux {             // device constants of the two-level factorization 
   hipStream_t st2 = nullptr; // lookahead: the bulk stream (strip solve beyond the next block, C12)
   hipEvent_t ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   int nblk = 0;
+  // the bulk stream's launches as CU-bounded persistent launches (gram_launch_bounded): claim /
+  // arrival counters, the skipped CU ids (SCS_CHOL_BULK_SKIP), workgroup slots of the device
+  unsigned* bctr = nullptr;
+  unsigned bskip = 0;
+  int bslots = 0;
   // strip pipeline (chol_pipe_init): the left-looking update of each outer strip s as a
   // tail-balanced scheduled launch over the pairs (i >= j, j < OB) of its trailing columns
   struct StripSched {

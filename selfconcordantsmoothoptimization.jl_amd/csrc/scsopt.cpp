@@ -2038,7 +2038,13 @@ int scs_create(int device, void* stream, scs_ctx** out) {
     if (stream) {
       c->st = (hipStream_t)stream;
     } else {
-      HCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+      // SCS_CHOL_BULK_PRIO=2: the context stream (the factor's chain) at the highest priority (A/B)
+      const char* pe = getenv("SCS_CHOL_BULK_PRIO");
+      int least = 0, greatest = 0;
+      if (pe && atoi(pe) >= 2 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        HCK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, greatest));
+      else
+        HCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
       c->own_stream = true;
     }
   });

@@ -633,6 +633,30 @@ def test_cholesky_lookahead_bit_identical(m, ob, monkeypatch):
     assert np.array_equal(bits(la.x), bits(ser.x))
 
 
+@pytest.mark.parametrize("skip", ["0x20", "0x30", "0xffff"])
+def test_cholesky_bounded_bulk_bit_identical(skip, monkeypatch):
+    """The bulk stream's strip solves and trailing updates as CU-bounded persistent launches
+    (SCS_CHOL_BULK_SKIP: workgroups on those CU ids leave at once, the rest claim tiles) compute
+    every tile with the same kernel body: a bit-identical ProxNSCORE trajectory.  0xffff skips every
+    CU, so all tiles fall to the launch's last-arriving workgroup (the placement-independent
+    fallback).  m = 4608: 36 inner blocks, lookahead over 4 outer blocks."""
+    N, m = 4000, 4608
+    x0 = np.random.default_rng(35).standard_normal(m) * 0.3
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+
+    def run():
+        p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=29)
+        sol = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+        p.ctx.close()
+        return sol
+
+    ref = run()
+    monkeypatch.setenv("SCS_CHOL_BULK_SKIP", skip)
+    got = run()
+    assert got.obj == ref.obj and got.epochs == ref.epochs
+    assert np.array_equal(bits(got.x), bits(ref.x))
+
+
 def test_cholesky_diag_pipe_bit_identical(monkeypatch):
     """The diagonal-block kernel's default schedule (wave 0 factors the next 16 x 16 sub-block while
     waves 1..3 finish the trailing update) gives every element the same updates in the same order
