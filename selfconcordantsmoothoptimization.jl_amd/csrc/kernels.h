@@ -339,6 +339,7 @@ hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int 
 // sparse Gram G = Aᵀ diag(w) A (upper part, column j up to the end of its diagonal tile) from the
 // CSC copy and a Gram-blocked CSR copy (block width 2^shift, unpadded segments): Σ_r nnz_r² work
 int sparse_gram_shift();
+const char* sparse_gram_kernel_name(int f32);   // the variant launch_sparse_gram runs (SCS_SPARSE_GRAM_KERNEL)
 hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const void* valT, const int64_t* bptr,
                               const uint16_t* lidx, const void* bval, int f32, const double* w, int64_t nrows,
                               int64_t m, int shift, double* G, int64_t ldg, hipStream_t st);

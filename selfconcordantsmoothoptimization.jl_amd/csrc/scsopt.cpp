@@ -1320,7 +1320,7 @@ void gram_sparse(scs_ctx* c, const double* w, double* out, int packed) {
   if (packed & 2) fail(c, SCS_ERR_ARG, "internal: the sparse Gram does not accumulate");
   HCK(launch_sparse_gram(c->colptr, c->rowidx, c->valT, c->bgram.ptr, c->bgram.lidx, c->bgram.val, c->sp_f32, w, c->N,
                          c->m, c->bgram.shift, dst, c->mpad, c->st));
-  c->gram_kname = c->sp_f32 ? "sparse_gram_kernel<float>" : "sparse_gram_kernel<double>";
+  c->gram_kname = sparse_gram_kernel_name(c->sp_f32);
   if (packed & 1) HCK(gram_pack_launch(c->G, c->mpad, c->utiles, c->nslots, out, c->st));
 }
 

@@ -399,6 +399,119 @@ __global__ __launch_bounds__(64) void sparse_gram_kernel(const int64_t* __restri
   for (int i = lane; i < nr; i += 64) col[i] = acc[i];
 }
 
+// The same walk with its memory latency overlapped (default; SCS_SPARSE_GRAM_KERNEL=1 the kernel
+// above): per batch of SG_PR rows the row metadata is a stage ahead -- the row index and CSC value
+// (stage 1) two batches ahead, the weight and segment bounds (stage 2) one batch ahead -- so a batch
+// is ONE memory round trip (its rows' segment loads, all issued before any is used) instead of
+// three per 8 rows.  The accumulation is the same products in the same row order: G is bitwise
+// sparse_gram_kernel's.
+template <typename VT, int SG_PR, bool BMAJ>   // SG_PR rows per batch; BMAJ: items of a column block b-major
+__global__ __launch_bounds__(64) void sparse_gram_pipe_kernel(const int64_t* __restrict__ colptr,
+                                                              const int* __restrict__ rowidx,
+                                                              const VT* __restrict__ valT,
+                                                              const int64_t* __restrict__ bptr,
+                                                              const uint16_t* __restrict__ lidx,
+                                                              const VT* __restrict__ bval,
+                                                              const double* __restrict__ w, int64_t nrows,
+                                                              int64_t m, int shift, int64_t j0,
+                                                              double* __restrict__ G, int64_t ldg) {
+  __shared__ double acc[1 << 12];
+  const int lane = threadIdx.x;
+  const int BS = 1 << shift;
+  const int64_t t = (int64_t)blockIdx.x;
+  const int64_t J0 = j0 >> shift;
+  int64_t J = J0, base = 0;
+  while (true) {
+    const int64_t n = (int64_t)BS * (J + 1);
+    if (t < base + n) break;
+    base += n;
+    ++J;
+  }
+  const int64_t loc = t - base;
+  const int64_t j = BMAJ ? J * BS + loc % BS : J * BS + loc / (J + 1);
+  const int b = BMAJ ? (int)(loc / BS) : (int)(loc % (J + 1));
+  if (j >= m) return;
+  for (int i = lane; i < BS; i += 64) acc[i] = 0.0;
+  __syncthreads();
+  const int64_t p0 = colptr[j], p1 = colptr[j + 1];
+  const int64_t boff = (int64_t)b * nrows;
+  auto stage1 = [&](int64_t p, int& r, double& a) {   // lane u < SG_PR: row p + u's index and value
+    if (lane < SG_PR && p + lane < p1) {
+      r = rowidx[p + lane];
+      a = (double)valT[p + lane];
+    } else {
+      r = -1;
+      a = 0.0;
+    }
+  };
+  auto stage2 = [&](int r, double a, double& s, int64_t& st, int64_t& en) {
+    if (r >= 0) {
+      s = w[r] * a;
+      st = bptr[boff + r];
+      en = bptr[boff + r + 1];
+    } else {
+      s = 0.0;
+      st = en = 0;
+    }
+  };
+  int rc, rn;
+  double ac, an;
+  double s, sN;
+  int64_t st, en, stN, enN;
+  stage1(p0, rc, ac);
+  stage2(rc, ac, s, st, en);
+  stage1(p0 + SG_PR, rn, an);
+  for (int64_t p = p0; p < p1; p += SG_PR) {
+    // the next batch's stage 2 (its stage 1 landed during the previous batch) and the stage 1 of the
+    // one after, issued before this batch's segment loads
+    stage2(rn, an, sN, stN, enN);
+    stage1(p + 2 * SG_PR, rn, an);
+    double v[SG_PR];
+    int ix[SG_PR];
+#pragma unroll
+    for (int u = 0; u < SG_PR; ++u) {
+      const int64_t su = sg_bcast(st, u), eu = sg_bcast(en, u);
+      const bool on = su + lane < eu;
+      v[u] = on ? (double)bval[su + lane] : 0.0;
+      ix[u] = on ? (int)lidx[su + lane] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < SG_PR; ++u) {   // rows past the column's end: no segment (st = en = 0)
+      const double su_s = sg_bcast(s, u);
+      if (ix[u] >= 0) atomicAdd(&acc[ix[u]], su_s * v[u]);
+      // a segment longer than one wave: the rest of this row before the next row (row order kept)
+      const int64_t su = sg_bcast(st, u), eu = sg_bcast(en, u);
+      for (int64_t q = su + 64 + lane; q - lane < eu; q += 64)
+        if (q < eu) atomicAdd(&acc[lidx[q]], su_s * (double)bval[q]);
+    }
+    s = sN;
+    st = stN;
+    en = enN;
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)b * BS;
+  const int64_t rend = ((j >> 7) + 1) << 7;
+  const int64_t nr = (rend - r0 < BS) ? rend - r0 : BS;
+  double* col = G + j * ldg + r0;
+  for (int i = lane; i < nr; i += 64) col[i] = acc[i];
+}
+
+static int sparse_gram_variant() {   // read per call (A/B and the bit-identity test)
+  const char* e = getenv("SCS_SPARSE_GRAM_KERNEL");
+  return e ? atoi(e) : 2;
+}
+
+const char* sparse_gram_kernel_name(int f32) {
+  if (sparse_gram_variant() == 1) return f32 ? "sparse_gram_kernel<float>" : "sparse_gram_kernel<double>";
+  static const char* names[2][4] = {
+      {"sparse_gram_pipe_kernel<double, 32, false>", "sparse_gram_pipe_kernel<double, 64, false>",
+       "sparse_gram_pipe_kernel<double, 32, true>", "sparse_gram_pipe_kernel<double, 64, true>"},
+      {"sparse_gram_pipe_kernel<float, 32, false>", "sparse_gram_pipe_kernel<float, 64, false>",
+       "sparse_gram_pipe_kernel<float, 32, true>", "sparse_gram_pipe_kernel<float, 64, true>"}};
+  const int v = sparse_gram_variant();
+  return names[f32 ? 1 : 0][(v >= 3 && v <= 5) ? v - 2 : 0];
+}
+
 int sparse_gram_shift() { return 12; }
 
 int64_t sparse_gram_items(int64_t j0, int64_t j1, int shift) {
@@ -422,7 +535,22 @@ hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const vo
     while (j1 < m && sparse_gram_items(j0, j1 + BS, shift) < ((int64_t)1 << 30)) j1 += BS;
     if (j1 == j0) j1 = j0 + BS;
     const int64_t items = sparse_gram_items(j0, j1, shift);
-    if (f32)
+    const int var = sparse_gram_variant();
+    if (var != 1) {
+      // 2: 32 rows per batch (default), 3: 64 rows, 4 / 5: the same with b-major items (A/B)
+      auto go = [&](auto kf, auto kd) {
+        if (f32)
+          hipLaunchKernelGGL(kf, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx, (const float*)valT, bptr, lidx,
+                             (const float*)bval, w, nrows, m, shift, j0, G, ldg);
+        else
+          hipLaunchKernelGGL(kd, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx, (const double*)valT, bptr,
+                             lidx, (const double*)bval, w, nrows, m, shift, j0, G, ldg);
+      };
+      if (var == 3) go(sparse_gram_pipe_kernel<float, 64, false>, sparse_gram_pipe_kernel<double, 64, false>);
+      else if (var == 4) go(sparse_gram_pipe_kernel<float, 32, true>, sparse_gram_pipe_kernel<double, 32, true>);
+      else if (var == 5) go(sparse_gram_pipe_kernel<float, 64, true>, sparse_gram_pipe_kernel<double, 64, true>);
+      else go(sparse_gram_pipe_kernel<float, 32, false>, sparse_gram_pipe_kernel<double, 32, false>);
+    } else if (f32)
       hipLaunchKernelGGL(sparse_gram_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
                          (const float*)valT, bptr, lidx, (const float*)bval, w, nrows, m, shift, j0, G, ldg);
     else

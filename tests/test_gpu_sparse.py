@@ -253,8 +253,9 @@ def test_sparse_gram_priced_by_nnz(f32, monkeypatch):
     """§8f rank 3 (VERDICT r02 Missing #1): G = Aᵀ diag(w) A of a sparse A in Σ_r nnz_r² work
     (sparse_gram_kernel) -- three 4096-column blocks of G (m = 9037, padded to 9088), rows whose
     block segments are longer than one wave (the overflow loop), empty rows and columns, user CSR
-    with unsorted entries; vs the dense fp64 product entry by entry (|err| <= 1e-13·Σ|terms|), and
-    bitwise equal run to run (fixed row order per entry, no cross-wave atomics)."""
+    with unsorted entries; vs the dense fp64 product entry by entry (|err| <= 1e-13·Σ|terms|),
+    bitwise equal run to run (fixed row order per entry, no cross-wave atomics) and between the two
+    kernel variants."""
     import scipy.sparse as sp
     monkeypatch.setenv("SCS_SPARSE_GRAM", "1")
     rng = np.random.default_rng(47)
@@ -280,4 +281,9 @@ def test_sparse_gram_priced_by_nnz(f32, monkeypatch):
     assert np.all(err <= bound), float(np.max(err - bound))
     assert np.array_equal(p.gram(w), G)
     g, p2 = p.ctx.kernel_names()
-    assert g.startswith("sparse_gram_kernel")
+    assert g.startswith("sparse_gram_pipe_kernel<")
+    # the latency-overlapped kernel accumulates the same products in the same row order as the
+    # one-round-trip-per-8-rows kernel (SCS_SPARSE_GRAM_KERNEL=1): bitwise the same G
+    monkeypatch.setenv("SCS_SPARSE_GRAM_KERNEL", "1")
+    assert np.array_equal(p.gram(w), G)
+    assert p.ctx.kernel_names()[0].startswith("sparse_gram_kernel")
