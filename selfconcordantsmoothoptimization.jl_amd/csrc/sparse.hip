@@ -496,9 +496,13 @@ __global__ __launch_bounds__(64) void sparse_gram_pipe_kernel(const int64_t* __r
   for (int i = lane; i < nr; i += 64) col[i] = acc[i];
 }
 
-static int sparse_gram_variant() {   // read per call (A/B and the bit-identity test)
+// SCS_SPARSE_GRAM_KERNEL (read per call: A/B and the bit-identity test): 1 the one-round-trip-per-8-
+// rows kernel; 2 / 3: the pipelined kernel, 32 / 64 rows per batch, items j-major; 4 / 5: the same,
+// items b-major (concurrent waves share a 4096-row block of the Gram-blocked CSR copy).  Default 5:
+// C5-shaped Gram 1733 (1) -> 934 (2) / 794 (3) / 901 (4) / 766 ms (5), profiles/r03/sparse_gram/.
+static int sparse_gram_variant() {
   const char* e = getenv("SCS_SPARSE_GRAM_KERNEL");
-  return e ? atoi(e) : 2;
+  return e ? atoi(e) : 5;
 }
 
 const char* sparse_gram_kernel_name(int f32) {
@@ -537,7 +541,7 @@ hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const vo
     const int64_t items = sparse_gram_items(j0, j1, shift);
     const int var = sparse_gram_variant();
     if (var != 1) {
-      // 2: 32 rows per batch (default), 3: 64 rows, 4 / 5: the same with b-major items (A/B)
+      // 2: 32 rows per batch, 3: 64 rows, 4 / 5: the same with b-major items (5: default)
       auto go = [&](auto kf, auto kd) {
         if (f32)
           hipLaunchKernelGGL(kf, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx, (const float*)valT, bptr, lidx,

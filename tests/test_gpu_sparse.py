@@ -282,8 +282,9 @@ def test_sparse_gram_priced_by_nnz(f32, monkeypatch):
     assert np.array_equal(p.gram(w), G)
     g, p2 = p.ctx.kernel_names()
     assert g.startswith("sparse_gram_pipe_kernel<")
-    # the latency-overlapped kernel accumulates the same products in the same row order as the
-    # one-round-trip-per-8-rows kernel (SCS_SPARSE_GRAM_KERNEL=1): bitwise the same G
-    monkeypatch.setenv("SCS_SPARSE_GRAM_KERNEL", "1")
-    assert np.array_equal(p.gram(w), G)
-    assert p.ctx.kernel_names()[0].startswith("sparse_gram_kernel")
+    # every variant (the one-round-trip-per-8-rows kernel, the pipelined one at 32 / 64 rows per
+    # batch, j- or b-major items) accumulates the same products in the same row order: bitwise G
+    for var in ("2", "3", "4", "1"):
+        monkeypatch.setenv("SCS_SPARSE_GRAM_KERNEL", var)
+        assert np.array_equal(p.gram(w), G), var
+    assert p.ctx.kernel_names()[0].startswith("sparse_gram_kernel<")
