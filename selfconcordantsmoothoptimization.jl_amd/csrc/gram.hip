@@ -900,26 +900,26 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
   if (v) {
     if (!gram_fuse_ok(tall)) return hipErrorInvalidValue;
     if (tall) {
-      g_main_name = "gram_sia_kernel<1, 4, false, true>";
+      g_main_name = "gram_sia_kernel<1, 4, false, true, false>";
       hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0,
                          Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
     } else {
-      g_main_name = "gram_sia_kernel<1, 2, false, true>";
+      g_main_name = "gram_sia_kernel<1, 2, false, true, false>";
       hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0,
                          Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
     }
     return hipGetLastError();
   }
   if (!tall && gram_sia_mode() == 0) {
-    g_main_name = "gram_f64_kernel<false, 2, true>";
+    g_main_name = "gram_f64_kernel<false, 2, true, false>";
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
   } else if (!tall) {
-    g_main_name = "gram_sia_kernel<1, 2>";
+    g_main_name = "gram_sia_kernel<1, 2, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   } else if (gram_tall_mode() == 3) {
-    g_main_name = "gram_sia_kernel<1, 4>";
+    g_main_name = "gram_sia_kernel<1, 4, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
   } else {
@@ -1092,15 +1092,15 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
   const int glds = gram_tall_mode();
   if (v && !gram_fuse_ok(tall)) return hipErrorInvalidValue;
   if (v && tall) {
-    g_main_name = "gram_sia_kernel<1, 4, false, true>";
+    g_main_name = "gram_sia_kernel<1, 4, false, true, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
   } else if (v) {
-    g_main_name = "gram_sia_kernel<1, 2, false, true>";
+    g_main_name = "gram_sia_kernel<1, 2, false, true, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
   } else if (tall && glds == 3) {
-    g_main_name = "gram_sia_kernel<1, 4>";
+    g_main_name = "gram_sia_kernel<1, 4, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk,
                        nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
   } else if (tall && glds == 2) {
@@ -1108,23 +1108,23 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
                        Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   } else if (tall && glds == 1) {
-    g_main_name = "gram_glds_kernel<true>";
+    g_main_name = "gram_glds_kernel<true, 0>";
     hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
                        nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   } else if (tall) {
-    g_main_name = "gram_f64_kernel<false, 4, true>";
+    g_main_name = "gram_f64_kernel<false, 4, true, false>";
     hipLaunchKernelGGL((gram_f64_kernel<false, 4, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   } else if (gram_sia_mode() == 1) {
-    g_main_name = "gram_sia_kernel<1, 2>";
+    g_main_name = "gram_sia_kernel<1, 2, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr,
                        0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
   } else if (gram_sia_mode() == 2) {
-    g_main_name = "gram_sia_kernel<0>";
+    g_main_name = "gram_sia_kernel<0, 2, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<0>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr, 0,
                        G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
   } else {
-    g_main_name = "gram_f64_kernel<false, 2, true>";
+    g_main_name = "gram_f64_kernel<false, 2, true, false>";
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w,
                        (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P);
   }

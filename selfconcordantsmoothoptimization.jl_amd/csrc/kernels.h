@@ -186,6 +186,7 @@ struct QRAux {
   double *part = nullptr, *tw = nullptr, *tau = nullptr, *scal = nullptr, *V = nullptr, *Vt = nullptr,
          *Wm = nullptr, *Ym = nullptr, *Gv = nullptr, *T = nullptr, *ones = nullptr, *W = nullptr;
   int2* tiles = nullptr;
+  std::vector<int64_t> rect_off;   // per panel: offset of its update rectangle in tiles
   // the one-launch backward solve's block flags (generation-stamped, never reset) and its
   // dependency-wait error flag (set when a wait gives up after ~30 s: never expected)
   unsigned* flags = nullptr;

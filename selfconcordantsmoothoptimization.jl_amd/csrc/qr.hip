@@ -179,6 +179,7 @@ static void qr_free_bufs(QRAux* a) {
     }
   if (a->tiles) (void)hipFree(a->tiles);
   a->tiles = nullptr;
+  a->rect_off.clear();
   if (a->flags) (void)hipFree(a->flags);
   a->flags = nullptr;
   a->err = nullptr;
@@ -207,10 +208,17 @@ hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st) {
   al(&a->T, (size_t)QB * QB);
   al(&a->ones, (size_t)npad + QB);
   al(&a->W, (size_t)npad * QB);
-  // tile lists: (i, j) for i < nbk, j < nbk (row-major in i): prefixes give any rectangle
+  // tile lists, one launch per product of a panel: [row 0: (0, j), j < nbk] then, per panel p, the
+  // rectangle (i, j), i < nbk - p (rows of the panel's reflectors), j < nbk - p - 1 (trailing column
+  // blocks), j-major -- the update A_trail -= V Y as ONE launch (was one launch per column block)
   std::vector<int2> tl;
-  for (int j = 0; j < nbk; ++j)
-    for (int i = 0; i < nbk; ++i) tl.push_back(make_int2(i, j));
+  for (int j = 0; j < nbk; ++j) tl.push_back(make_int2(0, j));
+  a->rect_off.assign((size_t)nbk, 0);
+  for (int p = 0; p < nbk; ++p) {
+    a->rect_off[(size_t)p] = (int64_t)tl.size();
+    for (int j = 0; j < nbk - p - 1; ++j)
+      for (int i = 0; i < nbk - p; ++i) tl.push_back(make_int2(i, j));
+  }
   if (e == hipSuccess) e = hipMalloc(&a->tiles, sizeof(int2) * std::max<size_t>(tl.size(), 1));
   if (e == hipSuccess && !tl.empty())
     e = hipMemcpyAsync(a->tiles, tl.data(), sizeof(int2) * tl.size(), hipMemcpyHostToDevice, st);
@@ -229,21 +237,6 @@ hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st) {
 }
 
 void qr_aux_free(QRAux* a) { qr_free_bufs(a); }
-
-// the rectangle list (i, j), i < ni, j < nj, of a QR operation: (i, j) pairs bj-major -- built on
-// the host once per shape would need one list per (ni, nj); a column-block run of the full list
-// (all i < nbk for each j) is used instead and the tiles with i >= ni are masked by launching
-// per column block.  Rows of the trailing update: ni row blocks; each launch covers one j.
-static hipError_t qr_gram(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w, int64_t K,
-                          const QRAux* a, int ni, int nj, double* out, int64_t ldo, int flags, hipStream_t st) {
-  const int nbk = (int)(a->npad / QB);
-  for (int j = 0; j < nj; ++j) {
-    // tiles (i, j) for i < ni are a->tiles[j * nbk .. j * nbk + ni)
-    const hipError_t e = gram_launch_gen(A1, lda1, A2, lda2, w, 0, K, a->tiles + (int64_t)j * nbk, ni, out, ldo, flags, st);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
 
 hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hipStream_t st) {
   hipError_t e = qr_aux_init(a, npad, st);
@@ -267,16 +260,18 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
     e = gram_launch_gen(a->V, npad, a->V, npad, a->ones, 0, rows, a->tiles, 1, a->Gv, QB, 0, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(qr_build_t, dim3(1), dim3(QB), 0, st, a->Gv, a->tau, QB, a->T);
-    // Wm (QB x trailing) = Vᵀ A_trail: features = reflectors (A1 = V) x trailing columns (A2)
+    // Wm (QB x trailing) = Vᵀ A_trail: features = reflectors (A1 = V) x trailing columns (A2), the
+    // tiles (0, j < ntr) in one launch
     double* At = A + c1 * ld + c0;
-    e = qr_gram(a->V, npad, At, ld, a->ones, rows, a, 1, ntr, a->Wm, QB, 0, st);
+    e = gram_launch_gen(a->V, npad, At, ld, a->ones, 0, rows, a->tiles, ntr, a->Wm, QB, 0, st);
     if (e != hipSuccess) return e;
     // Ym = Tᵀ Wm: Ym(i, j) = Σ_q T(q, i) Wm(q, j)
-    e = qr_gram(a->T, QB, a->Wm, QB, a->ones, QB, a, 1, ntr, a->Ym, QB, 0, st);
+    e = gram_launch_gen(a->T, QB, a->Wm, QB, a->ones, 0, QB, a->tiles, ntr, a->Ym, QB, 0, st);
     if (e != hipSuccess) return e;
-    // A_trail -= V Ym: A(r, j) -= Σ_i Vt(i, r) Ym(i, j) (features r of Vt, K = i)
+    // A_trail -= V Ym: A(r, j) -= Σ_i Vt(i, r) Ym(i, j) (features r of Vt, K = i), panel p's rectangle
     hipLaunchKernelGGL(qr_transpose_v, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, a->V, npad, rows, a->Vt);
-    e = qr_gram(a->Vt, QB, a->Ym, QB, a->ones + npad, QB, a, (int)(rows / QB), ntr, At, ld, /*ACCUMULATE*/ 2, st);
+    e = gram_launch_gen(a->Vt, QB, a->Ym, QB, a->ones + npad, 0, QB, a->tiles + a->rect_off[(size_t)p],
+                        (int)(rows / QB) * ntr, At, ld, /*ACCUMULATE*/ 2, st);
     if (e != hipSuccess) return e;
   }
   // R x = Qᵀ b: the diagonal blocks' inverses, then the one-launch backward solve (b holds Qᵀ b)

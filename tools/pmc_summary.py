@@ -11,8 +11,12 @@ import csv
 import json
 import os
 
-KERNELS = ("gram_sia_kernel<1, 4, false, true>", "gram_sia_kernel<1, 4>", "gram_sia_kernel<1, 2>",
-           "gram_sia_kernel<1, 2, false, false>", "gram_sia_kernel<1, 4, false, false>", "gram_glds_kernel", "gram_f64_kernel<false, 4, true>", "gram_f64_kernel<false, 2, true>")
+# the main-Gram kernels (their rocprofv3 names: every template argument, defaults included)
+KERNELS = ("gram_sia_kernel<1, 4, false, true, false>", "gram_sia_kernel<1, 2, false, true, false>",
+           "gram_sia_kernel<1, 4, false, false, false>", "gram_sia_kernel<1, 2, false, false, false>",
+           "gram_sia_kernel<1, 4, false, true>", "gram_sia_kernel<1, 4>", "gram_sia_kernel<1, 2>",
+           "gram_sia_kernel<1, 2, false, false>", "gram_sia_kernel<1, 4, false, false>", "gram_glds_kernel",
+           "gram_f64_kernel<false, 4, true", "gram_f64_kernel<false, 2, true")
 
 
 def load(d, name):
