@@ -405,6 +405,57 @@ __global__ __launch_bounds__(DNT) void tri_inv_kernel(const double* __restrict__
   }
 }
 
+// T of a 128-column compact WY block (dlarft forward, columnwise; qr.hip) from Gv = VᵀV and tau,
+// by the same doubling as W = U⁻¹: T = [T11, -T11 G12 T22; 0, T22] with G12 = V1ᵀV2 in the place
+// of U12.  The 16 x 16 diagonal blocks come from dlarft's recurrence T(0:i, i) = -tau_i T(0:i, 0:i)
+// Gv(0:i, i) (one wave per block, lane t = row t); the doubling levels 16 -> 32 -> 64 on MFMA.
+__global__ __launch_bounds__(DNT) void wy_t_kernel(const double* __restrict__ Gv, const double* __restrict__ tau,
+                                                   double* __restrict__ T) {
+  __shared__ double su[CB * CLD];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < CB * CB; e += DNT) {   // G12 entries (different 16-blocks) in the upper part
+    const int c = e >> 7, r = e & 127;
+    su[c * CLD + r] = (r < c && (r >> 4) != (c >> 4)) ? Gv[(int64_t)c * CB + r] : 0.0;
+  }
+  __syncthreads();
+  const int wv = tid >> 6, lane = tid & 63, t = lane & 15;
+  for (int kb = wv; kb < CB / SB; kb += DNT / 64) {
+    const int o = kb * SB;
+    double tc[SB];
+#pragma unroll
+    for (int q = 0; q < SB; ++q) tc[q] = 0.0;
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      const double ti = tau[o + i];
+      const double z = (t < i) ? -ti * Gv[(int64_t)(o + i) * CB + o + t] : 0.0;   // lane q: z_q
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < SB; ++q) {
+        const double zq = __shfl(z, q, 64);
+        if (q < i && q >= t) s += tc[q] * zq;   // T(t, q), q >= t (upper)
+      }
+      tc[i] = (t < i) ? s : ((t == i) ? ti : 0.0);
+    }
+    if (lane < SB) {
+#pragma unroll
+      for (int q = 0; q < SB; ++q) su[(o + q) * CLD + o + t] = (t <= q) ? tc[q] : 0.0;
+    }
+  }
+  __syncthreads();
+  chol_inv_double_mfma<16>(su, tid);
+  chol_inv_double_mfma<32>(su, tid);
+  chol_inv_double_mfma<64>(su, tid);
+  for (int e = tid; e < CB * CB; e += DNT) {
+    const int c = e >> 7, r = e & 127;
+    T[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
+  }
+}
+
+hipError_t wy_t_build(const double* Gv, const double* tau, double* T, hipStream_t st) {
+  hipLaunchKernelGGL(wy_t_kernel, dim3(1), dim3(DNT), 0, st, Gv, tau, T);
+  return hipGetLastError();
+}
+
 hipError_t chol_tri_inverse(const double* R, int64_t ld, int nblk, double* W, hipStream_t st) {
   if (nblk <= 0) return hipSuccess;
   hipLaunchKernelGGL(tri_inv_kernel, dim3((unsigned)nblk), dim3(DNT), 0, st, R, ld, W);

@@ -992,6 +992,15 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
   return hipGetLastError();
 }
 
+// A K-split work list (bi, bj, piece, partial slot) of two column-major operands over [0, K) (the
+// QR's Vᵀ products, qr.hip): every item's partial tile to P, slot-major; the caller combines.
+hipError_t gram_launch_work_cm(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                               int64_t K, const int4* work, int seglen, int nsplit, double* P, hipStream_t st) {
+  hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3((unsigned)(8 * seglen)), dim3(256), 0, st, A1, lda1, A2, lda2, w,
+                     (int64_t)0, K, nullptr, 0, nullptr, (int64_t)0, 0, work, seglen, nsplit, P);
+  return hipGetLastError();
+}
+
 // gram_launch_gen's throughput launches as CU-bounded persistent launches (bnd_first): at most
 // `slots` workgroups, the CUs of `skip` left free.  Latency-sized launches and skip == 0 take
 // gram_launch_gen's path.  Per tile the same kernel body and MFMA order: bitwise the same G.

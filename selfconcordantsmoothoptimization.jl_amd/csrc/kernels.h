@@ -45,6 +45,9 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
                            hipStream_t st);
 // the same as CU-bounded persistent launches leaving the CUs of `skip` (ids within a shader engine)
 // free; ctr: 9 device counters, zeroed in stream order by the call
+// K-split work list over two column-major operands: partial tiles to P (gram.hip; the QR's Vᵀ products)
+hipError_t gram_launch_work_cm(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
+                               int64_t K, const int4* work, int seglen, int nsplit, double* P, hipStream_t st);
 hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                                int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                                unsigned* ctr, unsigned skip, int slots, hipStream_t st);
@@ -184,9 +187,16 @@ hipError_t lu_solve(const double* A, int64_t ld, int64_t npad, const LUAux* a, d
 struct QRAux {
   int64_t npad = 0;
   double *part = nullptr, *tw = nullptr, *tau = nullptr, *scal = nullptr, *V = nullptr, *Vt = nullptr,
-         *Wm = nullptr, *Ym = nullptr, *Gv = nullptr, *T = nullptr, *ones = nullptr, *W = nullptr;
+         *Wm = nullptr, *Ym = nullptr, *Gv = nullptr, *T = nullptr, *ones = nullptr, *W = nullptr, *rowc = nullptr, *xs = nullptr;
   int2* tiles = nullptr;
   std::vector<int64_t> rect_off;   // per panel: offset of its update rectangle in tiles
+  struct KList {                   // a K-split work list (qr_ksplit)
+    int64_t off = 0;
+    int seglen = 0, nsplit = 1, nj = 1;
+  };
+  std::vector<KList> klists;       // per panel: [Gv, Wm]
+  int4* kwork = nullptr;
+  double* kpart = nullptr;         // the pieces' partial tiles
   // the one-launch backward solve's block flags (generation-stamped, never reset) and its
   // dependency-wait error flag (set when a wait gives up after ~30 s: never expected)
   unsigned* flags = nullptr;
@@ -202,6 +212,8 @@ void qr_aux_free(QRAux* a);
 hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hipStream_t st);
 // chol.hip pieces the QR solve reuses: the inverses of the 128 x 128 upper diagonal blocks of R
 // (W, as the Cholesky's), and the one-launch backward solve U x = y
+// T (128 x 128, upper) of a compact WY block from Gv = VᵀV and tau (chol.hip; the QR's panels)
+hipError_t wy_t_build(const double* Gv, const double* tau, double* T, hipStream_t st);
 hipError_t chol_tri_inverse(const double* R, int64_t ld, int nblk, double* W, hipStream_t st);
 hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, const double* y, double* x,
                            unsigned* flags, unsigned gen, int* err, hipStream_t st);
