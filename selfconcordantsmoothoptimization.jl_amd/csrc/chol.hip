@@ -42,9 +42,9 @@ constexpr int CLD = CB + 1;      // LDS row pitch (doubles) -> conflict-light co
 //   C  trailing update of the upper triangle with 4 x 4 register tiles.
 // Then W = U⁻¹: the eight 16 x 16 diagonal inverses (two per wave, in
 // registers), and recursive doubling W12 = -W11 · (U12 · W22) at block sizes
-// 16 -> 32 -> 64 -> 128, as register-blocked LDS products (4 x S/16 outputs per
-// thread); the intermediate T = U12·W22 lives in the (unused) strictly-lower
-// triangle of S.  Only the factorization steps are a serial chain.
+// 16 -> 32 -> 64 -> 128 on MFMA (chol_inv_double_mfma); the intermediate T = U12·W22
+// lives in the (unused) strictly-lower triangle of S.  Only the factorization steps
+// are a serial chain.
 constexpr int SB = 16;
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -55,75 +55,27 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 
 #ifdef CHOL_PROF
 // probe_chol -DCHOL_PROF: thread 0 records s_memrealtime (100 MHz) at phase boundaries
-__device__ long long chol_prof[64];
+__device__ long long chol_prof[128];
 #define PROF_MARK(i) \
   if (threadIdx.x == 0 && k == 0) chol_prof[i] = (long long)__builtin_amdgcn_s_memrealtime()
+#define PROF_MARK_T(i, t) \
+  if (threadIdx.x == (t) && k == 0) chol_prof[i] = (long long)__builtin_amdgcn_s_memrealtime()
 #else
 #define PROF_MARK(i)
+#define PROF_MARK_T(i, t)
 #endif
 
-// one doubling level: for every pair (i0 = 2pS, j0 = i0 + S):
+constexpr int DNT = 256;          // threads of chol_diag_kernel (4 waves; 512 spills: measured slower)
+
+// One doubling level of W = U⁻¹ for every pair (i0 = 2pS, j0 = i0 + S):
 //   step 1  T(r, c) = Σ_{t <= c} U(i0+r, j0+t) W(j0+t, j0+c)   -> S[j0 + r][i0 + c] (strictly lower)
 //   step 2  W(i0+r, j0+c) = -Σ_{t >= r} W(i0+r, i0+t) T(t, c)  -> S[i0 + r][j0 + c]
-constexpr int DNT = 256;          // threads of chol_diag_kernel (4 waves; 512 spills: measured slower)
-constexpr int RQ = 1024 / DNT;    // rows per thread in the doubling products
-
-template <int S>
-__device__ __forceinline__ void chol_inv_double(double* su, int tid) {
-  constexpr int MC = S / 16;                  // columns per thread (RQ rows x MC)
-  constexpr int TPP = DNT / (CB / (2 * S));   // threads per pair
-  const int pair = tid / TPP, loc = tid % TPP;
-  const int rg = loc / 16, cg = loc % 16;
-  const int i0 = 2 * S * pair, j0 = i0 + S;
-  const int r0 = RQ * rg, c0 = cg * MC;
-  double acc[RQ][MC];
-#pragma unroll
-  for (int q = 0; q < RQ; ++q)
-#pragma unroll
-    for (int m = 0; m < MC; ++m) acc[q][m] = 0.0;
-#pragma unroll 4
-  for (int t = 0; t < S; ++t) {
-    double u[RQ], wv[MC];
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) u[q] = su[(j0 + t) * CLD + i0 + r0 + q];
-#pragma unroll
-    for (int m = 0; m < MC; ++m) wv[m] = (t <= c0 + m) ? su[(j0 + c0 + m) * CLD + j0 + t] : 0.0;
-#pragma unroll
-    for (int q = 0; q < RQ; ++q)
-#pragma unroll
-      for (int m = 0; m < MC; ++m) acc[q][m] += u[q] * wv[m];
-  }
-#pragma unroll
-  for (int q = 0; q < RQ; ++q)
-#pragma unroll
-    for (int m = 0; m < MC; ++m) su[(i0 + c0 + m) * CLD + j0 + r0 + q] = acc[q][m];
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < RQ; ++q)
-#pragma unroll
-    for (int m = 0; m < MC; ++m) acc[q][m] = 0.0;
-#pragma unroll 4
-  for (int t = 0; t < S; ++t) {
-    double wv[RQ], tv[MC];
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) wv[q] = (t >= r0 + q) ? su[(i0 + t) * CLD + i0 + r0 + q] : 0.0;
-#pragma unroll
-    for (int m = 0; m < MC; ++m) tv[m] = su[(i0 + c0 + m) * CLD + j0 + t];
-#pragma unroll
-    for (int q = 0; q < RQ; ++q)
-#pragma unroll
-      for (int m = 0; m < MC; ++m) acc[q][m] += wv[q] * tv[m];
-  }
-#pragma unroll
-  for (int q = 0; q < RQ; ++q)
-#pragma unroll
-    for (int m = 0; m < MC; ++m) su[(j0 + c0 + m) * CLD + i0 + r0 + q] = -acc[q][m];
-  __syncthreads();
-}
-
-// The same doubling level on MFMA: S x S products as 16 x 16 output tiles (S/4 MFMAs
-// each), (pair, tile) items round-robin over the waves.  Fragment maps as in phase C;
-// the triangular operands are masked per lane (W22: k <= j; W11: k >= i).
+// on MFMA: S x S products as 16 x 16 output tiles (S/4 MFMAs each), (pair, tile) items round-robin
+// over the waves.  Fragment maps as in phase C; the triangular operands are masked per lane (W22:
+// k <= j; W11: k >= i) AFTER unconditional LDS reads: a masked read compiles to a branch the
+// compiler cannot hoist, one LDS wait per MFMA (doubling + W store 17.4 -> 11.5 us).  (Skipping the
+// k blocks that lie wholly in the zero part of the triangle -- 5/8 of the MFMAs at S = 64 -- with a
+// run-time trip count measured slower, 13.0 us: the reads of a block then wait in front of its MFMAs.)
 template <int S>
 __device__ __forceinline__ void chol_inv_double_mfma(double* su, int tid) {
   constexpr int NP = CB / (2 * S), NT16 = (S / 16) * (S / 16);
@@ -137,7 +89,8 @@ __device__ __forceinline__ void chol_inv_double_mfma(double* su, int tid) {
     for (int t0 = 0; t0 < S; t0 += 4) {
       const int k = t0 + lk;
       const double a = su[(j0 + k) * CLD + i0 + ti + li];
-      const double b = (k <= tj + li) ? su[(j0 + tj + li) * CLD + j0 + k] : 0.0;
+      const double bl = su[(j0 + tj + li) * CLD + j0 + k];
+      const double b = (k <= tj + li) ? bl : 0.0;
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
 #pragma unroll
@@ -152,7 +105,8 @@ __device__ __forceinline__ void chol_inv_double_mfma(double* su, int tid) {
 #pragma unroll
     for (int t0 = 0; t0 < S; t0 += 4) {
       const int k = t0 + lk;
-      const double a = (k >= ti + li) ? su[(i0 + k) * CLD + i0 + ti + li] : 0.0;
+      const double al = su[(i0 + k) * CLD + i0 + ti + li];
+      const double a = (k >= ti + li) ? al : 0.0;
       const double b = su[(i0 + tj + li) * CLD + j0 + k];
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
@@ -162,20 +116,40 @@ __device__ __forceinline__ void chol_inv_double_mfma(double* su, int tid) {
   __syncthreads();
 }
 
-// Phase A: wave 0 factors the 16 x 16 diagonal sub-block at o in registers (lane c = column c;
-// lanes 16..63 mirror lanes 0..15), reciprocal pivots to srinv.
-__device__ __forceinline__ void diag_factor16(double* su, double* srinv, int o, int k, int* info, int tid) {
-  int c = tid & 15;
-  // opaque per call: keeps the compiler from hoisting the 32 lane masks (c > j, c == j) out of the
-  // inner-block loop into SGPR pairs it then spills to VGPR lanes (v_writelane / v_readlane)
-  asm volatile("" : "+v"(c));
-  double a[SB];
+// 64-bit DPP lane move within each quad: lane 4c + t takes lane 4c + Q (quad_perm Q,Q,Q,Q)
+template <int Q>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, Q * 0x55, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), Q * 0x55, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Phase A: wave 0 factors the 16 x 16 diagonal sub-block at o in registers, reciprocal pivots to
+// srinv.  Lane 4c + q holds rows 4q .. 4q+3 of column c (a[s] = S(o+4q+s, o+c)), so all 64 lanes
+// work and a column step is ~35 instructions instead of ~80 (the one-column-per-lane form
+// broadcast each of the 15 row-j values with a v_readlane pair and spilled SGPRs).  Per column j:
+// the pivot by v_readlane; row j scaled in the lanes of quarter j/4; U(j, c) to the other lanes of
+// the column's quad by DPP; U(j, i) of the lane's own rows from a 16-double LDS row copy (urow).
+// The serial chain is pivot -> rsq -> row scale -> DPP -> the next pivot's update (pnext), computed
+// ahead of the LDS-fed updates.  Every element takes the same fused multiply-subtracts in the same
+// j order as the one-column-per-lane form: bitwise the same U and pivots.
+__device__ __forceinline__ void diag_factor16(double* su, double* srinv, double* urow, int o, int k, int* info,
+                                              int tid) {
+  int c = (tid & 63) >> 2, q = tid & 3;
+  // opaque per call: keeps the compiler from hoisting the lane masks out of the inner-block loop
+  asm volatile("" : "+v"(c), "+v"(q));
+  double a[4];
 #pragma unroll
-  for (int i = 0; i < SB; ++i) a[i] = su[(o + c) * CLD + o + i];   // S(o+i, o+c); zero below the diagonal
+  for (int s = 0; s < 4; ++s) a[s] = su[(o + c) * CLD + o + 4 * q + s];   // zero below the diagonal
+  double pnext = a[0];   // S(j, j) of the next pivot, in lane 4j + j/4
+  double rr[SB];         // the reciprocal pivots (wave-uniform), to srinv after the loop
+  int bad = -1;
 #pragma unroll
   for (int j = 0; j < SB; ++j) {
-    const double ajj = readlane_d(a[j], j);
-    if (tid == 0 && !(ajj > 0.0) && *info == 0) *info = k * CB + o + j + 1;
+    const int jq = j >> 2, js = j & 3;
+    const double ajj = readlane_d(pnext, 4 * j + jq);
+    bad = (bad < 0 && !(ajj > 0.0)) ? j : bad;   // the first non-positive pivot, off the chain
     // 1/sqrt(ajj): v_rsq_f64 + two Newton steps (6 dependent FMAs instead of the
     // sqrt + divide sequences on this serial chain); d = ajj * r
     double r = __builtin_amdgcn_rsq(ajj);
@@ -183,15 +157,42 @@ __device__ __forceinline__ void diag_factor16(double* su, double* srinv, int o, 
 #pragma unroll
     for (int it = 0; it < 2; ++it) r = fma(r, fma(-hj * r, r, 0.5), r);
     const double d = ajj * r;
-    if (tid == 0) srinv[o + j] = r;
-    a[j] = (c > j) ? a[j] * r : ((c == j) ? d : a[j]);    // row j of U: U(j, c)
+    rr[j] = r;
+    // row j of U, U(j, c), in the lanes of quarter jq (slot js)
+    const double ar = a[js] * r;
+    const double sc = (c > j) ? ar : ((c == j) ? d : a[js]);
+    a[js] = (q == jq) ? sc : a[js];
+    if (j == SB - 1) break;
+    // U(j, c) in every lane of column c's quad, straight from the product (the selects above are off
+    // the chain: in columns c <= j it feeds only rows i > c, which are never stored)
+    double ujc;
+    switch (jq) {
+      case 0: ujc = quad_bcast<0>(ar); break;
+      case 1: ujc = quad_bcast<1>(ar); break;
+      case 2: ujc = quad_bcast<2>(ar); break;
+      default: ujc = quad_bcast<3>(ar); break;
+    }
+    // the next pivot first: S(j+1, j+1) -= U(j, j+1)² (its lane holds U(j, j+1) as ujc)
+    const int s1 = (j + 1) & 3;
+    pnext = fma(-ujc, ujc, a[s1]);
+    if (q == jq) urow[c] = ar;   // = U(j, c) wherever it is read (columns c > j)
+    // the other lanes' row-j values: without a (wavefront-scope, instruction-free) fence the compiler
+    // may reuse a lane's previous-iteration loads where that lane did not store itself
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const v2d u01 = *(const v2d*)(urow + 4 * q), u23 = *(const v2d*)(urow + 4 * q + 2);
+    const double uji[4] = {u01[0], u01[1], u23[0], u23[1]};
 #pragma unroll
-    for (int i = j + 1; i < SB; ++i) a[i] -= readlane_d(a[j], i) * a[j];   // U(j, i) from lane i
+    for (int s = 0; s < 4; ++s)
+      if (4 * q + s > j) a[s] = fma(-uji[s], ujc, a[s]);   // rows i > j: S(i, c) -= U(j, i) U(j, c)
   }
-  if (tid < SB) {
 #pragma unroll
-    for (int i = 0; i < SB; ++i)
-      if (i <= c) su[(o + c) * CLD + o + i] = a[i];
+  for (int s = 0; s < 4; ++s)
+    if (4 * q + s <= c) su[(o + c) * CLD + o + 4 * q + s] = a[s];
+  if (tid == 0) {
+#pragma unroll
+    for (int j = 0; j < SB; ++j) srinv[o + j] = rr[j];
+    if (bad >= 0 && *info == 0) *info = k * CB + o + bad + 1;
   }
 }
 
@@ -251,23 +252,26 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   __shared__ double su[CB * CLD];   // S(r, c) = su[c*CLD + r]
   __shared__ double srinv[CB];      // 1 / U(j, j)
   __shared__ double swinv[CB / SB][SB * SB];   // inverses of the 16 x 16 diagonal blocks (col-major)
+  __shared__ __attribute__((aligned(16))) double urow[SB];   // phase A's row-j copy
+  __shared__ int tctr;                                        // phase C's tile counter
   double* blk = G + (int64_t)k * CB * ld + (int64_t)k * CB;
   double* Wk = W + (int64_t)k * CB * CB;
   const int tid = threadIdx.x;
-  // the block into LDS: 32 loads per thread in flight before their LDS stores (a latency-bound
-  // one-at-a-time loop was ~5 us of the launch)
-#pragma unroll
-  for (int hb = 0; hb < CB * CB / DNT; hb += 32) {
-    double t[32];
+  // the block into LDS: all 32 16-B loads per thread in flight before their LDS stores, and
+  // unconditional (the block is whole in memory; the lower triangle is masked after the load -- a
+  // masked load compiled to a branch with a kernel-argument reload and an lgkmcnt wait per element)
+  {
+    v2d t[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
-      const int e = tid + DNT * (hb + i), c = e >> 7, r = e & 127;
-      t[i] = (r <= c) ? blk[(int64_t)c * ld + r] : 0.0;
+      const int e = tid + DNT * i, c = e >> 6, r = 2 * (e & 63);
+      t[i] = *(const v2d*)(blk + (int64_t)c * ld + r);
     }
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
-      const int e = tid + DNT * (hb + i), c = e >> 7, r = e & 127;
-      su[c * CLD + r] = t[i];
+      const int e = tid + DNT * i, c = e >> 6, r = 2 * (e & 63);
+      su[c * CLD + r] = (r <= c) ? t[i][0] : 0.0;
+      su[c * CLD + r + 1] = (r + 1 <= c) ? t[i][1] : 0.0;
     }
   }
   // inverse of the (final) 16 x 16 diagonal block kb by one wave (lane c = column c)
@@ -290,35 +294,78 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
       for (int i = 0; i < SB; ++i) swinv[kb][c * SB + i] = (i <= c) ? w[i] : 0.0;
     }
   };
+  // row block rb of U (rows 16 rb .. 16 rb + 15, columns from 16 rb) from S to G by threads t0, t0 + nt,
+  // ...: 16-B stores of row pairs, the diagonal element of an even pair alone
+  auto store_urows = [&](int rb, int t0, int nt) {
+    const int o = rb * SB, n = (CB - o) * (SB / 2);
+    for (int e = t0; e < n; e += nt) {
+      const int c = o + (e >> 3), r = o + 2 * (e & 7);
+      if (r + 1 <= c) {
+        v2d v;
+        v[0] = su[c * CLD + r];
+        v[1] = su[c * CLD + r + 1];
+        *(v2d*)(blk + (int64_t)c * ld + r) = v;
+      } else if (r == c) {
+        blk[(int64_t)c * ld + r] = su[c * CLD + r];
+      }
+    }
+  };
   __syncthreads();
 
   PROF_MARK(0);
   const int wv = tid >> 6, lane = tid & 63;
   if (PIPE) {
-    if (tid < 64) diag_factor16(su, srinv, 0, k, info, tid);
+    if (tid < 64) diag_factor16(su, srinv, urow, 0, k, info, tid);
     __syncthreads();
   }
   for (int kb = 0; kb < CB / SB; ++kb) {
     const int o = kb * SB;
     PROF_MARK(1 + 4 * kb);
     if (!PIPE) {
-      if (tid < 64) diag_factor16(su, srinv, o, k, info, tid);
+      if (tid < 64) diag_factor16(su, srinv, urow, o, k, info, tid);
       __syncthreads();
     }
     PROF_MARK(2 + 4 * kb);
     const int np = CB - o - SB;  // columns right of the sub-block
     if (np == 0) break;
     diag_panel16(su, srinv, o, np, tid);
+    if (tid == 0) tctr = 1;   // C(kb)'s tile counter (tile 0 is wave 0's)
     __syncthreads();
     PROF_MARK(3 + 4 * kb);
     const int n16 = np >> 4, ntl = n16 * (n16 + 1) / 2;
     if (PIPE) {
+      // tiles 1.. of C(kb) are claimed from an LDS counter: waves 1..3 at once (the one that inverts
+      // block kb after its inverse), wave 0 once it has factored sub-block kb+1
+      auto claim_tiles = [&]() {
+        for (;;) {
+          int id = 0;
+          if (lane == 0) id = __hip_atomic_fetch_add(&tctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          id = __builtin_amdgcn_readfirstlane(id);
+          if (id >= ntl) break;
+          diag_trail_tile(su, o, id, lane);
+        }
+      };
       if (wv == 0) {
         diag_trail_tile(su, o, 0, lane);
-        diag_factor16(su, srinv, o + SB, k, info, tid);
+        PROF_MARK_T(36 + kb, 0);
+        diag_factor16(su, srinv, urow, o + SB, k, info, tid);
+        PROF_MARK_T(43 + kb, 0);
+#ifndef CHOL_NO_W0CLAIM
+        claim_tiles();
+#endif
       } else {
-        if (wv == 1 + kb % 3) inv16(kb);   // U_kb,kb is final: its inverse beside the update
-        for (int id = wv; id < ntl; id += DNT / 64 - 1) diag_trail_tile(su, o, id, lane);
+        if (wv == 1 + kb % 3) {
+          inv16(kb);   // U_kb,kb is final: its inverse beside the update
+          PROF_MARK_T(50 + kb, 64 * wv);
+        }
+        claim_tiles();
+        // row blocks of U are final after their panel step: waves 1..3 store them while wave 0 is
+        // on the chain (kb = 3: blocks 0, 1; 4: 2, 3; 5: 4, 5; 6: 6 -- where these waves have slack)
+        if (kb >= 3) {
+          store_urows(2 * (kb - 3), tid - 64, DNT - 64);
+          if (kb < 6) store_urows(2 * (kb - 3) + 1, tid - 64, DNT - 64);
+        }
+        PROF_MARK_T(57 + 3 * kb + wv - 1, 64 * wv);
       }
     } else {
       for (int id = wv; id < ntl; id += DNT / 64) diag_trail_tile(su, o, id, lane);
@@ -326,16 +373,14 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
     __syncthreads();
   }
   PROF_MARK(33);
-  // ---- store U
-  for (int e = tid; e < CB * CB; e += DNT) {
-    const int c = e >> 7, r = e & 127;
-    if (r <= c) blk[(int64_t)c * ld + r] = su[c * CLD + r];
-  }
-  // (running inv16 beside phase B on the idle last wave measured slower: B waits for it; PIPE runs
-  // inv16(kb) beside C(kb), so only the last block's is left)
+  // ---- store U (PIPE: the last row block; the others went out during the loop).  (Running inv16
+  // beside phase B on the idle last wave measured slower: B waits for it; PIPE runs inv16(kb) beside
+  // C(kb), so only the last block's is left.)
   if (PIPE) {
     if (wv == DNT / 64 - 1) inv16(CB / SB - 1);
+    else store_urows(CB / SB - 1, tid, DNT - 64);
   } else {
+    for (int rb = 0; rb < CB / SB; ++rb) store_urows(rb, tid, DNT);
     for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) inv16(kb);
   }
   __syncthreads();   // storeU has read the diagonal blocks; swinv complete
@@ -349,9 +394,14 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   chol_inv_double_mfma<16>(su, tid);
   chol_inv_double_mfma<32>(su, tid);
   chol_inv_double_mfma<64>(su, tid);
-  for (int e = tid; e < CB * CB; e += DNT) {
-    const int c = e >> 7, r = e & 127;
-    Wk[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    const int e = tid + DNT * i, c = e >> 6, r = 2 * (e & 63);
+    const double w0 = su[c * CLD + r], w1 = su[c * CLD + r + 1];   // unconditional reads, then the mask
+    v2d v;
+    v[0] = (r <= c) ? w0 : 0.0;
+    v[1] = (r + 1 <= c) ? w1 : 0.0;
+    *(v2d*)(Wk + (int64_t)c * CB + r) = v;
   }
   PROF_MARK(35);
 }

@@ -13,7 +13,7 @@
 namespace scs {
 hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st);
 #ifdef CHOL_PROF
-extern __device__ long long chol_prof[64];
+extern __device__ long long chol_prof[128];
 #endif
 }
 
@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
     printf("n=%ld diag kernel: %.1f us/launch\n", (long)n, ms * 1000 / 64);
 #ifdef CHOL_PROF
     {
-      long long hp[64];
+      long long hp[128];
       CK(hipMemcpyFromSymbol(hp, HIP_SYMBOL(scs::chol_prof), sizeof(hp)));
       // s_memtime runs at the 100 MHz constant clock on gfx950
       printf("phase times (k=0 launch, us): ");
@@ -75,6 +75,13 @@ int main(int argc, char** argv) {
         const long long a3 = (kb < 7) ? hp[1 + 4 * (kb + 1)] : hp[33];
         printf("[kb%d A %.2f B %.2f C %.2f] ", kb, (a1 - a0) / 100.0, kb < 7 ? (a2 - a1) / 100.0 : 0.0,
                kb < 7 ? (a3 - a2) / 100.0 : 0.0);
+      }
+      printf("\n  C detail (us from C start): ");
+      for (int kb = 0; kb < 7; ++kb) {
+        const long long c0 = hp[3 + 4 * kb];
+        printf("[kb%d w0 tile %.2f fac %.2f | inv %.2f | w1 %.2f w2 %.2f w3 %.2f] ", kb, (hp[36 + kb] - c0) / 100.0,
+               (hp[43 + kb] - c0) / 100.0, (hp[50 + kb] - c0) / 100.0, (hp[57 + 3 * kb] - c0) / 100.0,
+               (hp[58 + 3 * kb] - c0) / 100.0, (hp[59 + 3 * kb] - c0) / 100.0);
       }
       printf("\n  load %.2f  factor %.2f  storeU+diaginv %.2f  doubling+storeW %.2f  total %.2f\n", (hp[1] - hp[0]) / 100.0,
              (hp[33] - hp[1]) / 100.0, (hp[34] - hp[33]) / 100.0, (hp[35] - hp[34]) / 100.0,
@@ -85,6 +92,9 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep) {
       CK(hipMemcpy(G, G0, n * n * 8, hipMemcpyDeviceToDevice));
       CK(hipMemset(info, 0, 4));
+      // a device-to-device hipMemcpy may return before it completes, and sq is non-blocking: without
+      // this the factor's launches overtook the copy's tail at n = 16384 (stale trailing columns)
+      CK(hipDeviceSynchronize());
       CK(hipEventRecord(e0, sq));
       CK(scs::chol_factor(G, n, n, n, W, &aux, dtr, info, sq));
       CK(hipEventRecord(e1, sq)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
