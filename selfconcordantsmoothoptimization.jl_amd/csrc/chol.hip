@@ -610,6 +610,7 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = create_bulk_stream(&a->st2, nblk);
   if (e == hipSuccess) e = hipMalloc(&a->bctr, 16 * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc(&a->sscr, sizeof(double) * 2 * (size_t)CB * 16 * CB);
   if (e == hipSuccess) {
     a->bskip = bulk_skip_mask(nblk);
     int dev = 0, ncu = 0;
@@ -648,6 +649,8 @@ void chol_aux_free(CholAux* a) {
   a->sflags = nullptr;
   if (a->bctr) (void)hipFree(a->bctr);
   a->bctr = nullptr;
+  if (a->sscr) (void)hipFree(a->sscr);
+  a->sscr = nullptr;
   a->serr = nullptr;
   for (void* p : {(void*)a->dtasks, (void*)a->ddeps, (void*)a->dcnt, (void*)a->dper})
     if (p) (void)hipFree(p);
@@ -717,6 +720,66 @@ static hipError_t strip_solve(double* G, int64_t ld, const double* W, const Chol
              /*GRAM_ACCUMULATE*/ 2);
   if (e != hipSuccess) return e;
   return strip_solve(G, ld, W, a, mid, hi, c0, nc, st, bulk);
+}
+
+// The chain's strip solve (Ba, and the same columns of the serial order) as right-looking steps:
+// step r is ONE launch in which every workgroup takes a 16-column strip s of column tile j and forms
+// Y = W_rᵀ R_rj[:, s] (row r's leaf, 128 x 16, in LDS); for row q = r that is X_rj's strip (to a
+// scratch row, in place at the last step), for q > r it updates R_qj[:, s] -= U_rqᵀ Y.  The leaf is
+// recomputed per strip (bitwise the leaf's own value: the same latency-kernel body) instead of being a
+// launch of its own; extra workgroups copy the previous step's scratch row into G (row r - 1 is read
+// by no one in this launch).  OB steps instead of the recursion's 2 OB - 1 launches; every R_qj takes
+// its updates in row order with K = 128 each (the recursion groups them by K = 128 .. OB/2·128).
+__global__ __launch_bounds__(256) void strip_step_kernel(double* G, int64_t ld, const double* __restrict__ W,
+                                                         const double* __restrict__ wv, int r, int hi, int c0,
+                                                         int nc, double* __restrict__ scur,
+                                                         const double* __restrict__ sprev) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * (GT + 16) * GBK];
+  __shared__ __attribute__((aligned(16))) double Y[GT * 16];
+  const int nitem = (hi - r) * nc * 8, it = blockIdx.x;
+  if (it >= nitem) {   // copy-back of the previous step's row r - 1: one 128 x 16 strip
+    const int ci = it - nitem, j = ci >> 3, s = ci & 7;
+    for (int e = threadIdx.x; e < GT * 8; e += 256) {
+      const int col = j * GT + 16 * s + (e >> 6), rr = 2 * (e & 63);
+      *(v2d*)(G + ((int64_t)c0 * GT + col) * ld + (int64_t)(r - 1) * GT + rr) = *(const v2d*)(sprev + (int64_t)col * GT + rr);
+    }
+    return;
+  }
+  const int q = r + it / (nc * 8), j = (it >> 3) % nc, s = it & 7;
+  const int64_t col0 = (int64_t)(c0 + j) * GT + 16 * s;   // the strip's first column of G
+  const double* Wr = W + (int64_t)r * GT * GT;
+  const double* Rr = G + col0 * ld + (int64_t)r * GT;
+  if (q == r) {   // the leaf: X_rj[:, s] (in place at the last step)
+    double* out = scur ? scur + ((int64_t)j * GT + 16 * s) * GT : G + col0 * ld + (int64_t)r * GT;
+    gram_small_strip<16>(Wr, GT, Rr, ld, wv, 0, GT, out, scur ? GT : ld, 0, lds);
+    return;
+  }
+  gram_small_strip<16>(Wr, GT, Rr, ld, wv, 0, GT, Y, GT, 0, lds);
+  __syncthreads();   // Y complete; the staging buffer free again
+  gram_small_strip<16>(G + (int64_t)q * GT * ld + (int64_t)r * GT, ld, Y, GT, wv + GT, 0, GT,
+                       G + col0 * ld + (int64_t)q * GT, ld, GRAM_ACCUMULATE, lds);
+}
+
+static hipError_t strip_solve_steps(double* G, int64_t ld, const double* W, const CholAux* a, int lo, int hi, int c0,
+                                    int nc, hipStream_t st) {
+  if (nc <= 0) return hipSuccess;
+  if (nc > 16 || !a->sscr) return hipErrorInvalidValue;
+  const size_t row = (size_t)CB * 16 * CB;
+  for (int r = lo; r < hi; ++r) {
+    const bool last = r == hi - 1;
+    double* scur = last ? nullptr : a->sscr + row * ((r - lo) & 1);
+    const double* sprev = a->sscr + row * ((r - lo + 1) & 1);
+    const unsigned grid = (unsigned)((hi - r) * nc * 8 + (r > lo ? nc * 8 : 0));
+    hipLaunchKernelGGL(strip_step_kernel, dim3(grid), dim3(256), 0, st, G, ld, W, a->w, r, hi, c0, nc, scur, sprev);
+  }
+  return hipGetLastError();
+}
+
+// SCS_CHOL_BA_STEPS (default 1): the chain's strip solve by strip_solve_steps; 0 = the recursion
+// (also whenever the dependency-driven launches replay it, SCS_CHOL_DAG=1)
+static bool ba_steps() {
+  const char* e = getenv("SCS_CHOL_BA_STEPS");
+  return !(e && e[0] == '0');
 }
 
 // Lookahead (default; SCS_CHOL_LA=0 off).  Outer block t's strip solve B and trailing update C
@@ -1001,6 +1064,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
   const int OB = outer_block_for(nblk);
   const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
   const bool dag = chol_dag_on() && a->serr;
+  const bool steps = !dag && ba_steps() && a->sscr && OB <= 16;
   if (dag) {
     const hipError_t eb = chol_dag_build(a, nblk, OB, ld, st);
     if (eb != hipSuccess) return eb;
@@ -1044,8 +1108,18 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
         wait(st, a->ev2);
         c12_pending = false;
       }
-      // B: strip solve, C: trailing update with K = (i1 - i0)·128
-      if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1, nc, st);
+      // B: strip solve, C: trailing update with K = (i1 - i0)·128.  With the step launches for the
+      // chain's columns, the first OB columns take them here too (the lookahead's Ba) and the rest
+      // the recursion (its Bb): the same operations per element in both orders
+      if (e == hipSuccess) {
+        if (steps) {
+          const int nb = nc < OB ? nc : OB;
+          e = strip_solve_steps(G, ld, W, a, i0, i1, i1, nb, st);
+          if (e == hipSuccess && nc > nb) e = strip_solve(G, ld, W, a, i0, i1, i1 + nb, nc - nb, st);
+        } else {
+          e = strip_solve(G, ld, W, a, i0, i1, i1, nc, st);
+        }
+      }
       if (e == hipSuccess)
         e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, ntri, trail, ld,
                             2 | 4, st);
@@ -1062,7 +1136,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (dag) {   // the recursive strip solve and the next diagonal triangle as one launch
       if (e == hipSuccess) e = chol_dag_launch(a, a->dnext[(size_t)(i0 / OB)], G, ld, W, st);
     } else {
-      if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
+      if (e == hipSuccess)
+        e = steps ? strip_solve_steps(G, ld, W, a, i0, i1, i1, OB, st) : strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
       if (e == hipSuccess)
         e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, n1a, trail, ld,
                               2 | 4, st);

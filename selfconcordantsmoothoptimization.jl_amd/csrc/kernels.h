@@ -102,6 +102,9 @@ struct CholAux {             // device constants of the two-level factorization 
   unsigned* bctr = nullptr;
   unsigned bskip = 0;
   int bslots = 0;
+  // the chain's strip solve as right-looking step launches (strip_solve_steps): two rows of
+  // 128 x (16 x 128) doubles for a step's leaf (its copy-back is the next step's)
+  double* sscr = nullptr;
   // strip pipeline (chol_pipe_init): the left-looking update of each outer strip s as a
   // tail-balanced scheduled launch over the pairs (i >= j, j < OB) of its trailing columns
   struct StripSched {
