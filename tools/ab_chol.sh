@@ -1,4 +1,6 @@
 #!/bin/bash
+# (old = a build of the comparison commit in _ab_old/, new = this tree; probes copied to tools/probes/bin/
+# as probe_chol_{old,new}[_prof] beforehand -- build/ does not travel to the GPU box)
 # A/B of the Cholesky factor: the library built from HEAD in _ab_old/ against the working tree,
 # probe_chol (diag kernel alone, factor, solve) and bench --config c2, alternated; then the
 # factor's bit-identity tests on the new build.  Usage: ab_chol.sh [outdir]

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the probes are built here with `make -C selfconcordantsmoothoptimization.jl_amd/csrc probe` and copied to
+# tools/probes/bin/probe_chol_new -- build/ does not travel to the GPU box; tools/probes/bin/ does)
 # kernel trace of the Cholesky probe (factor/solve timelines at m = 8192 / 16384), summarised by
 # tools/trace_chol_factor.py; then rocprofv3 --stats of the C2 bench (default configuration)
 set -o pipefail
