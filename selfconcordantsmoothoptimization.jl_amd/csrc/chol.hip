@@ -677,10 +677,13 @@ int chol_outer_block();
 // else 8.  (16 at m = 32768, where the bulk stream's K = 1024 trailing updates bound the factor,
 // measured slower: C4-half cached solve 221.5 -> 229.8 ms, profiles/r02/chol/ob16/.)  The
 // strip-solve recursion needs rectangle lists of up to OB/2 block rows (chol_aux_init: R <= 8).
+// Default since the r03 chain (faster diagonal kernel, strip-solve steps): 4 up to m = 8192, where
+// the chain bounds the factor and shorter outer blocks put less of it on the critical path (C2
+// factor 8.45 -> 8.08 ms), else 8 (m = 16384: 34.8 with 8, 36.3 with 4, 38.3 with 16;
+// profiles/r03/chol/ob/).
 static int outer_block_for(int nblk) {
-  (void)nblk;
   const char* e = getenv("SCS_CHOL_OB");
-  const int v = e ? atoi(e) : 8;
+  const int v = e ? atoi(e) : (nblk <= 64 ? 4 : 8);
   return v < 1 ? 1 : (v > 16 ? 16 : v);
 }
 
