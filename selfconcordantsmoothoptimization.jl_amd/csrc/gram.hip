@@ -980,8 +980,11 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
   // up to 64 tiles (256-512 latency workgroups); beyond, the throughput kernels fill the chip with
   // one 128 x 128 tile per workgroup at 2 per CU (m = 32768: the strip solves of the bulk stream
   // took 26 ms as 397 latency launches, ~8 ms of MFMA work)
+  // default 128 since r03 (with the 4-block outer steps): m = 8192 factor 8.07 -> 7.8 ms, m = 16384
+  // 34.3 -> 33.6 ms; the m = 32768 cached solve, the LU and the QR at n = 8192 unchanged
+  // (profiles/r03/chol/gram_small/)
   const char* se = getenv("SCS_GRAM_SMALL");   // read per launch (tests toggle it in-process)
-  const int small_max = se ? atoi(se) : 64;
+  const int small_max = se ? atoi(se) : 128;
   if (k1 - k0 <= 512 && (k1 - k0) % (8 * GBK) == 0 && k1 > k0 && ntiles <= small_max) return gram_launch_small(A1, lda1, A2, lda2, w, k0, k1, tiles, ntiles, G, ldg, flags, st);
   if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)   // the Cholesky's trailing updates
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
@@ -1009,7 +1012,7 @@ hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2,
                                unsigned* ctr, unsigned skip, int slots, hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   const char* se = getenv("SCS_GRAM_SMALL");
-  const int small_max = se ? atoi(se) : 64;
+  const int small_max = se ? atoi(se) : 128;
   const bool small = k1 - k0 <= 512 && (k1 - k0) % (8 * GBK) == 0 && k1 > k0 && ntiles <= small_max;
   if (!ctr || skip == 0 || slots <= 0 || small)
     return gram_launch_gen(A1, lda1, A2, lda2, w, k0, k1, tiles, ntiles, G, ldg, flags, st);
