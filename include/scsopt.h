@@ -157,6 +157,8 @@ int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
  * `what`: SCS_CB_F    out[0] = f(x)
  *         SCS_CB_GRAD out[0..m) = grad_fx(x)
  *         SCS_CB_HESS out = hess_fx(x), m x m column-major (ProxNSCORE)
+ *         SCS_CB_FTEST out[0] = f(Atest, ytest, x), the held-out loss (iterate.jl:173), asked
+ *                     only after scs_set_test_callback(ctx, 1)
  *         SCS_CB_GGN  out = [J (n x m, column-major) | r (n) | q (n)] with n = ggn_rows:
  *                     J = jac_yx, r = grad_fy, Q = diag(q) = hess_fy (prox-GGN-SCORE.jl:44-49);
  *                     a general symmetric Q is passed eigen-rotated (J̃ = VᵀJ, r̃ = Vᵀr,
@@ -171,6 +173,7 @@ int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
 #define SCS_CB_GRAD 1
 #define SCS_CB_HESS 2
 #define SCS_CB_GGN 3
+#define SCS_CB_FTEST 4
 typedef int (*scs_loss_fn)(void* user, int what, const double* x, int64_t m, double* out);
 int scs_set_loss_callback(scs_ctx* ctx, scs_loss_fn fn, void* user, int64_t ggn_rows);
 
@@ -181,6 +184,30 @@ int scs_set_loss_callback(scs_ctx* ctx, scs_loss_fn fn, void* user, int64_t ggn_
 int scs_set_data(scs_ctx* ctx, int64_t N, int64_t m, const double* A, int64_t lda,
                  const double* y, int64_t N_global, int64_t row0);
 int scs_gen_data(scs_ctx* ctx, const scs_synth* spec);
+/* ---- held-out data  (Problem(A, y, x0, f, λ; Atest, ytest), problems.jl:27-28,67-68) -------
+ * optim_loop! evaluates ftest(x) = f(Atest, ytest, x) with the problem's own f (same loss kind,
+ * same scale literal) at every stats push when BOTH Atest and ytest are given (iterate.jl:169-175,
+ * utils.jl:55-57); the values become Solution.fvaltest (scs_history.fvaltest).  Call after the
+ * data (a new scs_set_data / scs_gen_data / scs_set_sparse drops the test set).  Row-sharded
+ * contexts pass their shard of the held-out rows (N local rows of N_global, every rank calls,
+ * a rank may hold none); a multi-device context takes the whole set (N_global = N, row0 = 0)
+ * and splits it like the data.  A = y = NULL clears the test set.                             */
+int scs_set_test_data(scs_ctx* ctx, int64_t N, const double* A, int64_t lda, const double* y,
+                      int64_t N_global, int64_t row0);
+/* CSR held-out rows (0-based, m columns; values stored fp64, or fp32 with val_f32 = 1).       */
+int scs_set_test_sparse(scs_ctx* ctx, int64_t N, int64_t nnz, const int64_t* rowptr, const int32_t* colidx,
+                        const double* val, int val_f32, const double* y, int64_t N_global, int64_t row0);
+/* Rows [row0, row0 + N) of the scs_gen_data generator (dense kinds 1-3, spec->m = the data's m):
+ * with row0 >= the data's N_global they are held-out samples of the same distribution.  A
+ * multi-device context splits spec->N rows across its devices.                                */
+int scs_gen_test_data(scs_ctx* ctx, const scs_synth* spec);
+/* A callback loss (SCS_LOSS_CALLBACK) keeps its held-out data on the caller's side: on = 1 makes
+ * the loop ask SCS_CB_FTEST at every push.                                                     */
+int scs_set_test_callback(scs_ctx* ctx, int on);
+/* ftest(x) now; *on = 1 when the context holds test data.                                      */
+int scs_eval_ftest(scs_ctx* ctx, const double* x, double* fval);
+int scs_has_test(scs_ctx* ctx, int* on);
+
 /* Copy device A rows [r0, r0+nr) (column-major, lda_out) and y back.       */
 int scs_get_data(scs_ctx* ctx, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y);
 int scs_get_dims(scs_ctx* ctx, int64_t* N, int64_t* m, int64_t* N_global, int64_t* row0);
@@ -297,13 +324,17 @@ typedef struct scs_history {
                        mean_square_error for reg "gl" (rel_kind = 1)       */
   double* objrel;   /* f_rel_error: max(|obj − obj*| / |obj*|, f_tol)       */
   double* times;    /* seconds since the start, millisecond resolution       */
+  double* fvaltest; /* ftest(x) = f(Atest, ytest, x) of every pushed point when the context
+                       holds test data (scs_set_test_*; iterate.jl:169-175, utils.jl:55-57:
+                       one entry per obj entry); may be NULL                   */
 } scs_history;
 /* optim_loop! on the device: init! + per epoch f(x) + get_reg(x) + one step!
  * per batch (the full batch, or the scs_set_batches list in order), the
  * reference's termination tests and history pushes.  x_star is
  * model.x (the comparison solution).  Outputs: final x, *n_hist entries,
- * *epochs (Solution.epochs).  Metrics / test data / verbose printing stay in
- * the host loop (scsopt.iterate).  Requires scs_method_init.                */
+ * *epochs (Solution.epochs).  With test data, hist->fvaltest gets ftest(x) at
+ * every push.  Metrics / verbose printing stay in the host loop
+ * (scsopt.iterate).  Requires scs_method_init.                              */
 int scs_iterate(scs_ctx* ctx, const double* x0, const double* x_star, int64_t max_epoch, double x_tol,
                 double f_tol, int rel_kind, double* x_out, const scs_history* hist, int64_t* n_hist,
                 int64_t* epochs);

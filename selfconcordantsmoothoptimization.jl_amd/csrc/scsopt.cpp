@@ -46,6 +46,7 @@ enum { T_GRAM = 0, T_GEMV, T_SOLVE, T_STEP, T_REDUCE, T_N };
 constexpr int ZF_SLOT = 24;   // scal / hscal slot of the deferred f(x) (forward with need_val = false)
 // scs_iterate's device-resident loop: f(x) and get_reg(x) of the epoch's x, the norms (3 slots)
 constexpr int FX_SLOT = 25, RX_SLOT = 26, NRM_SLOT = 28, LOOP_SLOTS = 32;
+constexpr int TF_SLOT = 31;   // ftest(x) of the held-out data (inside LOOP_SLOTS: it rides the loop's hand-off)
 constexpr int H0_SLOT = 19;   // the device ring's H0 (scs_iterate's pipelined ProxLQNSCORE loop)
 
 struct DevBuf {
@@ -262,6 +263,20 @@ struct scs_ctx {
   // all ranks' rows of the full data or of the selected batch (GGN sample-space branch with
   // N_global + 1 <= m on several ranks)
   NView gview;
+  // held-out data (Problem(...; Atest, ytest), problems.jl:27-28,67-68): a view of its own (rows, y,
+  // the f workspace; a sparse set also its CSR + LDS-blocked copy) swapped in only to evaluate
+  // ftest(x) = f(Atest, ytest, x) at the loop's stats pushes (iterate.jl:169-175, utils.jl:55-57).
+  // `host`: a callback loss evaluates it on the caller's side (SCS_CB_FTEST)
+  struct TestSet {
+    NView v;
+    bool on = false, host = false;
+    int sp_f32 = 0;
+    int64_t nnz = 0;
+    SpBlk bcsr;
+    int64_t* rowptr = nullptr;
+    int* colidx = nullptr;
+    void* val = nullptr;
+  } tset;
   bool gview_ok = false;
   int64_t gview_batch = -1;    // the batch gview holds (-1: the full data) ...
   uint64_t gview_gen = 0;      // ... of batch list generation gview_gen
@@ -793,6 +808,47 @@ void free_view(scs_ctx* c, NView& v) {
   v = NView();
 }
 
+// the held-out view <-> the context's data fields (f's fields only: rows, y, the products'
+// workspace and, for a sparse set, the CSR arrays and the SpMV's blocked copy).  Not a data
+// change: the data generation (the Gram cache's key) and the product kernel name are kept.
+void swap_test(scs_ctx* c) {
+  auto& t = c->tset;
+  const uint64_t gen = c->data_gen;
+  swap_view(c, t.v);
+  c->data_gen = gen;
+  std::swap(c->sp_f32, t.sp_f32);
+  std::swap(c->nnz, t.nnz);
+  std::swap(c->bcsr, t.bcsr);
+  std::swap(c->rowptr, t.rowptr);
+  std::swap(c->colidx, t.colidx);
+  std::swap(c->val, t.val);
+}
+
+struct TestScope {
+  scs_ctx* c;
+  std::string pk;
+  explicit TestScope(scs_ctx* cc) : c(cc), pk(cc->prod_kname) { swap_test(c); }
+  ~TestScope() {
+    swap_test(c);
+    c->prod_kname = pk;
+  }
+};
+
+void free_test(scs_ctx* c) {
+  auto& t = c->tset;
+  free_view(c, t.v);
+  dfree_t(c, t.bcsr.ptr);
+  dfree_t(c, t.bcsr.lidx);
+  dfree(c, t.bcsr.val);
+  t.bcsr = scs_ctx::SpBlk();
+  dfree_t(c, t.rowptr);
+  dfree_t(c, t.colidx);
+  dfree(c, t.val);
+  t.nnz = 0;
+  t.sp_f32 = 0;
+  t.on = t.host = false;
+}
+
 // scs_step on the selected minibatch view: swapped in (and the data-keyed caches dropped) for
 // the call, swapped back even when the step fails
 struct BatchScope {
@@ -1031,6 +1087,36 @@ double eval_f_dev(scs_ctx* c, const double* xh, const double* xd) {
     return 0.5 * c->hscal[8] + c->hscal[9];
   }
   return forward(c, xh, xd, 0);
+}
+
+// ftest(x) = f(Atest, ytest, x) (iterate.jl:173) at the device vector xd, enqueued: the loss sum of
+// the held-out rows lands in scal[TF_SLOT] (all-reduced across ranks for a row-sharded test set);
+// loss_scale_value(hscal / hloop[TF_SLOT]) is the value.  The same products and epilogue as f(x),
+// on the held-out view; the z / f caches of the data are not touched.
+void ftest_enqueue(scs_ctx* c, const double* xd) {
+  ensure_red(c);   // sized by the data's view, before the held-out one is swapped in
+  TestScope ts(c);
+  const int ns = matvec_n(c, xd, c->nsplit);
+  HCK(launch_epilogue(c->loss, c->ggn, EPI_VAL, c->zpart, ns, c->Npad, c->y, c->N, c->Npad, c->scale, c->z, c->gN,
+                      c->hN, c->wN, c->vN, c->valpart, c->st));
+  double* dst = sharded(c) ? c->red : c->scal + TF_SLOT;
+  HCK(launch_sum_partials(c->valpart, c->nval, dst, c->st));
+  allreduce(c, c->red, 1);
+  if (sharded(c)) HCK(hipMemcpyAsync(c->scal + TF_SLOT, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+}
+
+// ftest(x) now (host copy xh, may be null, and device copy xd)
+double eval_ftest_dev(scs_ctx* c, const double* xh, const double* xd) {
+  if (!c->tset.on) fail(c, SCS_ERR_STATE, "no test data: call scs_set_test_data first");
+  if (c->tset.host) return cb_eval(c, SCS_CB_FTEST, xh, xd, 1)[0];
+  if (c->loss == SCS_LOSS_QUADRATIC) {   // 1/2*(x'*(Atest*x)) + ytest'*x
+    TestScope ts(c);
+    return eval_f_dev(c, xh, xd);
+  }
+  ftest_enqueue(c, xd);
+  d2h(c, c->hscal + TF_SLOT, c->scal + TF_SLOT, 1);
+  sync(c);
+  return loss_scale_value(c, c->hscal[TF_SLOT]);
 }
 
 // ∇f(x) -> out (device)
@@ -1980,6 +2066,9 @@ int group_set_data(scs_ctx* g, int64_t N, int64_t m, const double* A, int64_t ld
                    int64_t row0);
 int group_gen_data(scs_ctx* g, const scs_synth* sp);
 int group_get_data(scs_ctx* g, int64_t r0, int64_t nr, double* A, int64_t lda_out, double* y);
+int group_set_test_data(scs_ctx* g, int64_t N, const double* A, int64_t lda, const double* y, int64_t Nglob,
+                        int64_t row0);
+int group_gen_test_data(scs_ctx* g, const scs_synth* sp);
 int group_eval(scs_ctx* g, const double* x, double* out, int64_t nout, int (*fn)(scs_ctx*, const double*, double*));
 int group_step(scs_ctx* g, const double* x, const double* x_prev, int64_t iter, const double* grad_fx, double* x_new,
                double* dx, double* pri);
@@ -2237,6 +2326,7 @@ static void reset_data(scs_ctx* c) {
   chol_aux_free(&c->caux);
   clear_batches(c);
   free_view(c, c->gview);
+  free_test(c);
   c->gview_ok = false;
   c->ntiles = c->nslots = 0;
   invalidate_caches(c);
@@ -2523,6 +2613,143 @@ int scs_get_sparse(scs_ctx* c, int64_t* rowptr, int32_t* colidx, double* val) {
     }
     sync(c);
   });
+}
+
+// ---- held-out data (Problem(...; Atest, ytest), problems.jl:27-28,67-68) -----------------------
+// the rows of a new held-out view (after free_test): Npad, nstage and the buffers of its dense form
+static void test_view_dims(scs_ctx* c, int64_t N, int64_t Nglob, bool sparse) {
+  if (!c->has_data || c->generic)
+    fail(c, SCS_ERR_STATE, "test data needs a data problem: call scs_set_data / scs_gen_data / scs_set_sparse first");
+  if (N < 0) fail(c, SCS_ERR_ARG, "test data: N = %lld", (long long)N);
+  NView& v = c->tset.v;
+  v.N = N;
+  v.Nglob = Nglob > 0 ? Nglob : N;
+  v.Npad = std::max<int64_t>(round_up(std::max<int64_t>(N, 1), 16), 16);
+  v.nstage = v.Npad / 16;
+  v.sparse = sparse;
+  v.y = dalloc<double>(c, v.Npad);
+  if (!sparse) v.A = dalloc<double>(c, (size_t)v.Npad * c->mpad);
+}
+
+int scs_set_test_data(scs_ctx* c, int64_t N, const double* A, int64_t lda, const double* y, int64_t Nglob,
+                      int64_t row0) {
+  if (is_group(c)) return group_set_test_data(c, N, A, lda, y, Nglob, row0);
+  return guarded(c, [&] {
+    HCK(hipSetDevice(c->dev));
+    free_test(c);
+    if (!A && !y) return;   // clears the held-out set
+    if (!A || !y) fail(c, SCS_ERR_ARG, "test data: Atest and ytest are both required (iterate.jl:169-171)");
+    if (lda < N) fail(c, SCS_ERR_ARG, "test data: lda (%lld) < N (%lld)", (long long)lda, (long long)N);
+    (void)row0;
+    test_view_dims(c, N, Nglob, false);
+    TestScope ts(c);
+    if (N > 0) {
+      double* C = dalloc<double>(c, (size_t)c->Npad * 128);
+      upload_panels(c, A, N, lda, c->Npad, c->A, C);
+      h2d(c, c->y, y, N);
+      sync(c);
+      dfree_t(c, C);
+    }
+    alloc_nspace(c);
+    sync(c);
+    c->tset.on = true;
+  });
+}
+
+int scs_set_test_sparse(scs_ctx* c, int64_t N, int64_t nnz, const int64_t* rowptr, const int32_t* colidx,
+                        const double* val, int f32, const double* y, int64_t Nglob, int64_t row0) {
+  if (is_group(c)) {
+    c->err = "sparse test data takes a single-device context";
+    return SCS_ERR_ARG;
+  }
+  return guarded(c, [&] {
+    HCK(hipSetDevice(c->dev));
+    free_test(c);
+    if (!rowptr || !y || nnz < 0 || (nnz > 0 && (!colidx || !val)))
+      fail(c, SCS_ERR_ARG, "sparse test data: null arrays (Atest and ytest are both required)");
+    if (N < 0 || rowptr[0] != 0 || rowptr[N] != nnz)
+      fail(c, SCS_ERR_ARG, "sparse test data: rowptr must start at 0 and end at nnz");
+    for (int64_t i = 0; i < N; ++i)
+      if (rowptr[i + 1] < rowptr[i]) fail(c, SCS_ERR_ARG, "sparse test data: rowptr not monotone at %lld", (long long)i);
+    for (int64_t p = 0; p < nnz; ++p)
+      if (colidx[p] < 0 || colidx[p] >= c->m)
+        fail(c, SCS_ERR_ARG, "sparse test data: column index out of range at %lld", (long long)p);
+    if (nnz > INT32_MAX * 64LL) fail(c, SCS_ERR_ARG, "sparse test data: nnz too large");
+    (void)row0;
+    test_view_dims(c, N, Nglob, true);
+    TestScope ts(c);
+    c->sp_f32 = f32 ? 1 : 0;
+    c->nnz = nnz;
+    c->rowptr = dalloc<int64_t>(c, N + 1);
+    c->colidx = dalloc<int>(c, nnz);
+    c->val = dalloc_vals(c, nnz, c->sp_f32);
+    HCK(hipMemcpyAsync(c->rowptr, rowptr, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice, c->st));
+    if (nnz > 0) {
+      HCK(hipMemcpyAsync(c->colidx, colidx, sizeof(int) * nnz, hipMemcpyHostToDevice, c->st));
+      upload_vals(c, c->val, val, nnz, c->sp_f32);
+    }
+    if (N > 0) h2d(c, c->y, y, N);
+    build_blocked(c, N, c->m, c->rowptr, c->colidx, c->val, c->bcsr);
+    alloc_nspace(c);
+    sync(c);
+    c->tset.on = true;
+  });
+}
+
+int scs_gen_test_data(scs_ctx* c, const scs_synth* s) {
+  if (is_group(c)) return group_gen_test_data(c, s);
+  return guarded(c, [&] {
+    if (!s) fail(c, SCS_ERR_ARG, "null synth spec");
+    if (s->kind < 1 || s->kind > 3) fail(c, SCS_ERR_ARG, "scs_gen_test_data: dense kinds 1-3");
+    if (s->m != c->m) fail(c, SCS_ERR_ARG, "scs_gen_test_data: m = %lld, the data has %lld", (long long)s->m,
+                           (long long)c->m);
+    HCK(hipSetDevice(c->dev));
+    free_test(c);
+    test_view_dims(c, s->N, s->N_global, false);
+    TestScope ts(c);
+    alloc_nspace(c);
+    const double scale = (s->kind == 3) ? 1.0 : 1.0 / std::sqrt((double)s->m);
+    // rows [row0, row0 + N) of the same generator as scs_gen_data: with row0 >= the data's N_global
+    // they are held-out samples of the same distribution (the same x_true)
+    HCK(launch_gen_A(c->A, c->Npad, c->N, c->m, c->mpad, s->row0, s->seed, scale, c->st));
+    HCK(launch_gen_xtrue(c->xn, c->m, s->seed, s->density, c->st));
+    HCK(launch_gemv_n(c->A, c->nstage, c->Npad, c->mpad, c->xn, 1, c->zpart, c->Npad, c->st));
+    HCK(launch_gen_y(s->kind, c->zpart, c->y, c->N, s->row0, s->seed, c->st));
+    sync(c);
+    c->tset.on = true;
+  });
+}
+
+int scs_set_test_callback(scs_ctx* c, int on) {
+  if (is_group(c)) {
+    c->err = "a callback loss takes a single-device context";
+    return SCS_ERR_ARG;
+  }
+  return guarded(c, [&] {
+    free_test(c);
+    if (!on) return;
+    if (c->loss != SCS_LOSS_CALLBACK || !c->cb)
+      fail(c, SCS_ERR_STATE, "scs_set_test_callback: the loss is not a callback (scs_set_loss_callback first)");
+    c->tset.on = c->tset.host = true;
+  });
+}
+
+int scs_eval_ftest(scs_ctx* c, const double* x, double* fval) {
+  if (is_group(c)) return group_eval(c, x, fval, 1, scs_eval_ftest);
+  return guarded(c, [&] {
+    if (!x || !fval) fail(c, SCS_ERR_ARG, "scs_eval_ftest: null argument");
+    require_ready(c, false);
+    HCK(hipSetDevice(c->dev));
+    h2d(c, c->xn, x, c->m);
+    *fval = eval_ftest_dev(c, x, c->xn);
+  });
+}
+
+int scs_has_test(scs_ctx* c, int* on) {
+  if (!on) return SCS_ERR_ARG;
+  if (is_group(c)) return scs_has_test(c->subs[0], on);
+  *on = c->tset.on ? 1 : 0;
+  return SCS_OK;
 }
 
 int scs_set_loss(scs_ctx* c, int loss, int ggn, double scale) {
@@ -2844,7 +3071,9 @@ static void step_call(scs_ctx* c, const double* x, const double* x_prev, int64_t
   {
     // ∇fx lives in its own buffer for the call (gtmp2 is line-search scratch)
     double* gbuf = nullptr;
-    if (grad_fx) {
+    // ProxGGNSCORE takes ∇fx and never reads it (prox-GGN-SCORE.jl:34-135: its grad_f -- the line
+    // search's ∇q, :58-63,83-84 -- is the model's gradient): only NSCORE / LQN install it
+    if (grad_fx && c->method != SCS_PROX_GGNSCORE) {
       gbuf = dalloc<double>(c, c->mpad);
       h2d(c, gbuf, grad_fx, c->m);
       invalidate_caches(c);
@@ -2941,6 +3170,16 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
       *fv = eval_f_dev(c, xx, c->xn);
       return *fv + eval_reg_dev(c, c->xn);
     };
+    // ftest(x) of a host vector (uploaded to c->xn unless it is already there, as fobj_of)
+    auto ftest_of = [&](const double* xx) -> double {
+      if (!c->tset.on) return std::numeric_limits<double>::quiet_NaN();
+      const uint64_t t = xtag_of(c, xx);
+      if (!(t && t == dev_xn)) {
+        h2d(c, c->xn, xx, m);
+        dev_xn = t;
+      }
+      return eval_ftest_dev(c, xx, c->xn);
+    };
     const double nstar = nrm(x_star, nullptr);
     auto rel_of = [&](const double* xx) {
       if (rel_kind == 1) return sumsq(x_star, xx) / (double)m;   // mean_square_error (utils.jl:3-5), the "gl" rel_error
@@ -2955,13 +3194,19 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     const double obj_star = fobj_of(x_star, &fstar);
     auto frel_of = [&](double ob) { return jmax(std::fabs(ob - obj_star) / std::fabs(obj_star), f_tol); };
     int64_t nh = 0;
-    auto push = [&](double ob, double fv, double pr, double rl, double fr, double dt) {
+    // show_stat! + update_stat! (utils.jl:50-57,106-113): with held-out data every push carries
+    // ftest of the pushed point too (the `fvaltests` vector, iterate.jl:169-175), so the test
+    // history has one entry per obj entry
+    const bool tst = c->tset.on;
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    auto push = [&](double ob, double fv, double pr, double rl, double fr, double dt, double ft) {
       h->obj[nh] = ob;
       h->fval[nh] = fv;
       h->pri_res_norm[nh] = pr;
       h->rel[nh] = rl;
       h->objrel[nh] = fr;
       if (h->times) h->times[nh] = dt;
+      if (h->fvaltest) h->fvaltest[nh] = ft;
       ++nh;
     };
     // init!(method, x): reset the method state (prox-L-BFGS-SCORE.jl:31-36)
@@ -3053,9 +3298,11 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         HCK(launch_reg_value(prox_args(c), c->x, m, c->scal + RX_SLOT, c->scal + 64 + 2 * 256, c->st));
         HCK(launch_norms3(c->x, c->xstar, nullptr, m, c->scal + NRM_SLOT, c->scal + 64 + 3 * 256, c->st));
         forward(c, x, c->x, 0, false);   // cached: the z of x0 from ∇q(x0)
+        if (tst) ftest_enqueue(c, c->x);
         d2h(c, hs, c->scal, LOOP_SLOTS);
         sync(c);
         double fcur = loss_scale_value(c, hs[ZF_SLOT]), regcur = hs[RX_SLOT];
+        double ftcur = tst ? loss_scale_value(c, hs[TF_SLOT]) : nan;
         double relcur = rel_from(hs[NRM_SLOT]), nxcur = std::sqrt(hs[NRM_SLOT + 1]);
         // Pipelined by one epoch: epoch e+1 is enqueued before the host reads epoch e's scalars, so
         // the GPU never idles for the hand-off.  What the next epoch needs from this one stays on
@@ -3099,6 +3346,7 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
                                 mem, c->d_order + mem + 1, c->scal + H0_SLOT, c->st));
           HCK(launch_lqn_tail(c->x, kmax > 0 ? c->d : c->gq, kmax > 0 ? 0 : 1, m, Mg, step, prox_args(c), c->hinv,
                               c->xn, c->dxv, c->q, c->lqR, c->scal, c->st));
+          if (tst) ftest_enqueue(c, c->xn);   // -> scal[TF_SLOT], carried to the host by lqn_post_final
           // z = A x_new, r = ∂f/∂z, f(x_new) -> scal[ZF_SLOT] (forward()'s passes, no host copies)
           hipEvent_t e1;
           tbegin(c, T_GEMV, &e1);
@@ -3137,8 +3385,8 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
           const double dt = now();
           const double obj = fcur + regcur;
           const double frel = frel_of(obj);
-          push(obj, fcur, pri, relcur, frel, dt);
-          if (epoch == max_epoch) push(obj, fcur, pri, relcur, frel, now());   // iterate.jl:219-231
+          push(obj, fcur, pri, relcur, frel, dt, ftcur);
+          if (epoch == max_epoch) push(obj, fcur, pri, relcur, frel, now(), ftcur);   // iterate.jl:219-231
           if (epoch < max_epoch) enqueue(epoch + 1);
           HCK(hipEventSynchronize(c->loop_ev[epoch & 1]));
           const double* he = c->hloop + (epoch & 1) * LOOP_SLOTS;
@@ -3167,10 +3415,12 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
           const double ndx = std::sqrt(he[NRM_SLOT + 2]);
           const double fnext = loss_scale_value(c, he[ZF_SLOT]), regnext = he[RX_SLOT];
           const double relnext = rel_from(he[NRM_SLOT]), nxnext = std::sqrt(he[NRM_SLOT + 1]);
+          const double ftnext = tst ? loss_scale_value(c, he[TF_SLOT]) : nan;
           const bool stop = ndx < x_tol * std::max(nxcur, 1.0) || frel <= f_tol || pri < x_tol;
           if (stop && epoch != max_epoch)   // iterate.jl:235-247: stats of x_new
-            push(fnext + regnext, fnext, pri, relnext, frel_of(fnext + regnext), now());
+            push(fnext + regnext, fnext, pri, relnext, frel_of(fnext + regnext), now(), ftnext);
           fcur = fnext;
+          ftcur = ftnext;
           regcur = regnext;
           relcur = relnext;
           nxcur = nxnext;
@@ -3202,6 +3452,7 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
           HCK(hipMemcpyAsync(c->scal + FX_SLOT, c->scal + ZF_SLOT, sizeof(double), hipMemcpyDeviceToDevice, c->st));
         }
         HCK(launch_reg_value(prox_args(c), c->x, m, c->scal + RX_SLOT, c->scal + 64 + 2 * 256, c->st));
+        if (tst) ftest_enqueue(c, c->x);   // -> scal[TF_SLOT], read back with the epoch's scalars
         hipEvent_t e0;
         tbegin(c, T_STEP, &e0);
         tag_slot(x_new).v = c->xtag_next++;   // the step writes x_new (c->xn)
@@ -3218,8 +3469,9 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         const double obj = fval + hs[RX_SLOT];
         const double rel = rel_from(hs[NRM_SLOT]);
         const double frel = frel_of(obj);
-        push(obj, fval, pri, rel, frel, dt);
-        if (epoch == max_epoch) push(obj, fval, pri, rel, frel, now());   // iterate.jl:219-231
+        const double ft = tst ? loss_scale_value(c, hs[TF_SLOT]) : nan;
+        push(obj, fval, pri, rel, frel, dt, ft);
+        if (epoch == max_epoch) push(obj, fval, pri, rel, frel, now(), ft);   // iterate.jl:219-231
         pri = hs[0];
         const double nx = std::sqrt(hs[NRM_SLOT + 1]), ndx = std::sqrt(hs[NRM_SLOT + 2]);
         const bool stop = ndx < x_tol * std::max(nx, 1.0) || frel <= f_tol || pri < x_tol;
@@ -3227,10 +3479,11 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
           dt = now();
           double fv = eval_f_dev(c, x_new, c->xn);
           const double ob = fv + eval_reg_dev(c, c->xn);
+          const double ft = tst ? eval_ftest_dev(c, x_new, c->xn) : nan;
           HCK(launch_norms3(c->xn, c->xstar, nullptr, m, c->scal + NRM_SLOT, c->scal + 64 + 3 * 256, c->st));
           d2h(c, hs + NRM_SLOT, c->scal + NRM_SLOT, 1);
           sync(c);
-          push(ob, fv, pri, rel_from(hs[NRM_SLOT]), frel_of(ob), dt);
+          push(ob, fv, pri, rel_from(hs[NRM_SLOT]), frel_of(ob), dt, ft);
         }
         // x_prev <- x, x <- x_new: rotate the device buffers and the host identities' tags
         std::swap(x_prev, x);
@@ -3253,16 +3506,18 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
       double dt = now();
       double fval = 0.0;
       double obj = fobj_of(x, &fval);
+      double ft = ftest_of(x);
       double rel = rel_of(x);
       double frel = frel_of(obj);
-      push(obj, fval, pri, rel, frel, dt);
+      push(obj, fval, pri, rel, frel, dt, ft);
       for (int64_t i = 1; i <= iend; ++i) {   // for (i, sample) in enumerate(data) (iterate.jl:204-255)
         if (epoch == max_epoch && i == iend) {   // iterate.jl:219-231 (x as of this batch)
           dt = now();
           obj = fobj_of(x, &fval);
+          ft = ftest_of(x);
           rel = rel_of(x);
           frel = frel_of(obj);
-          push(obj, fval, pri, rel, frel, dt);
+          push(obj, fval, pri, rel, frel, dt, ft);
         }
         hipEvent_t e0;
         tbegin(c, T_STEP, &e0);
@@ -3297,9 +3552,10 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
         if (stop && epoch != max_epoch) {   // iterate.jl:235-247 (f_rel_error is refreshed for the test at :257)
           dt = now();
           obj = fobj_of(x_new, &fval);
+          ft = ftest_of(x_new);
           rel = rel_of(x_new);
           frel = frel_of(obj);
-          push(obj, fval, pri, rel, frel, dt);
+          push(obj, fval, pri, rel, frel, dt, ft);
         }
         std::swap(x_prev, x);
         std::memcpy(x, x_new, sizeof(double) * m);
@@ -3758,6 +4014,35 @@ int group_get_data(scs_ctx* g, int64_t r0, int64_t nr, double* A, int64_t lda_ou
   return SCS_OK;
 }
 
+// the held-out rows split like the data's (row_plan; a device may hold none of them)
+int group_set_test_data(scs_ctx* g, int64_t N, const double* A, int64_t lda, const double* y, int64_t Nglob,
+                        int64_t row0) {
+  if ((Nglob > 0 && Nglob != N) || row0 != 0) {
+    g->err = "a multi-device context holds the whole test set: N_global = N, row0 = 0";
+    return SCS_ERR_ARG;
+  }
+  const std::vector<RowBlock> plan = row_plan(std::max<int64_t>(N, 0), (int)g->subs.size());
+  return group_run(g, [&](scs_ctx* s, int i) {
+    const RowBlock b = plan[(size_t)i];
+    return scs_set_test_data(s, b.rows(), A ? A + b.r0 : nullptr, lda, y ? y + b.r0 : nullptr, N, b.r0);
+  });
+}
+
+int group_gen_test_data(scs_ctx* g, const scs_synth* sp) {
+  if (!sp) {
+    g->err = "null synth spec";
+    return SCS_ERR_ARG;
+  }
+  const std::vector<RowBlock> plan = row_plan(sp->N, (int)g->subs.size());
+  return group_run(g, [&](scs_ctx* s, int i) {
+    scs_synth q = *sp;
+    q.row0 = sp->row0 + plan[(size_t)i].r0;
+    q.N = plan[(size_t)i].rows();
+    q.N_global = sp->N;
+    return scs_gen_test_data(s, &q);
+  });
+}
+
 // one scalar / one m-vector out of a collective evaluation: every device runs it, device 0's result
 int group_eval(scs_ctx* g, const double* x, double* out, int64_t nout,
                int (*fn)(scs_ctx*, const double*, double*)) {
@@ -3787,22 +4072,22 @@ int group_iterate(scs_ctx* g, const double* x0, const double* x_star, int64_t ma
                   int rel_kind, double* x_out, const scs_history* h, int64_t* n_hist, int64_t* epochs) {
   const size_t n = g->subs.size(), m = (size_t)g->grpm;
   const size_t cap = (size_t)std::max<int64_t>(2 * max_epoch + 1, 1);
-  std::vector<std::vector<double>> buf(n, std::vector<double>(6 * cap + m));
+  std::vector<std::vector<double>> buf(n, std::vector<double>(7 * cap + m));
   std::vector<int64_t> nh(n, 0), ep(n, 0);
   const int rc = group_run(g, [&](scs_ctx* s, int i) {
     double* b = buf[(size_t)i].data();
-    scs_history hi{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap, b + 5 * cap};
-    return scs_iterate(s, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, b + 6 * cap, &hi, &nh[(size_t)i],
+    scs_history hi{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap, b + 5 * cap, b + 6 * cap};
+    return scs_iterate(s, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, b + 7 * cap, &hi, &nh[(size_t)i],
                        &ep[(size_t)i]);
   });
   if (rc != SCS_OK) return rc;
   const double* b = buf[0].data();
   const size_t k = (size_t)nh[0];
-  double* dst[6] = {h ? h->obj : nullptr, h ? h->fval : nullptr, h ? h->pri_res_norm : nullptr, h ? h->rel : nullptr,
-                    h ? h->objrel : nullptr, h ? h->times : nullptr};
-  for (int a = 0; a < 6; ++a)
+  double* dst[7] = {h ? h->obj : nullptr, h ? h->fval : nullptr, h ? h->pri_res_norm : nullptr, h ? h->rel : nullptr,
+                    h ? h->objrel : nullptr, h ? h->times : nullptr, h ? h->fvaltest : nullptr};
+  for (int a = 0; a < 7; ++a)
     if (dst[a]) std::memcpy(dst[a], b + a * cap, sizeof(double) * k);
-  if (x_out) std::memcpy(x_out, b + 6 * cap, sizeof(double) * m);
+  if (x_out) std::memcpy(x_out, b + 7 * cap, sizeof(double) * m);
   if (n_hist) *n_hist = nh[0];
   if (epochs) *epochs = ep[0];
   return SCS_OK;

@@ -15,7 +15,7 @@ using SelfConcordantSmoothOptimization
 import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel, is_interval_set
 
 export DeviceProblem, configure!, iterate_device!, set_gram_cache!, set_solver!, rccl_unique_id, set_comm_rccl!,
-       set_comm_callback!
+       set_comm_callback!, set_test!
 
 const lib = joinpath(@__DIR__, "..", "scsopt", "libscsopt.so")
 
@@ -73,8 +73,46 @@ function finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, 
     chk(ccall((:scs_set_loss, lib), Cint, (Ptr{Cvoid}, Cint, Cint, Float64), ctx, LOSS[loss], GGN[out_fn], scale), ctx)
     model = DeviceProblem(ctx, A, yv, x0, nothing, λ, nothing, nothing, L, sol, C_set, P, out_fn,
                           nothing, nothing, nothing, nothing, nothing, nothing)
-    model.f = (A_, y_, x) -> devf(model, x)        # optim_loop! calls model.f(model.A, model.y, x)
+    # optim_loop! calls model.f(model.A, model.y, x) and, with held-out data, ftest(x) =
+    # model.f(model.Atest, model.ytest, x) (iterate.jl:168,173): both evaluate on the device
+    model.f = (A_, y_, x) -> (A_ !== nothing && A_ === model.Atest) ? devftest(model, x) : devf(model, x)
     finalizer(m_ -> ccall((:scs_destroy, lib), Cint, (Ptr{Cvoid},), m_.ctx), model)
+    return model
+end
+
+# Problem(...; Atest, ytest) (problems.jl:27-28,67-68): the held-out rows go to the device; both
+# are required, one alone is the reference's "Will skip testing..." case (iterate.jl:169-171).
+# Sharded: this rank's rows of Ntest_global held-out rows starting at global row test_row0.
+function set_test!(model::DeviceProblem, Atest, ytest; Ntest_global::Integer=0, test_row0::Integer=0,
+                   val_f32::Bool=false)
+    ctx = model.ctx
+    chk(ccall((:scs_set_test_data, lib), Cint,
+              (Ptr{Cvoid}, Int64, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Int64),
+              ctx, 0, C_NULL, 0, C_NULL, 0, 0), ctx)           # clear
+    model.Atest, model.ytest = nothing, nothing
+    (Atest === nothing && ytest === nothing) && return model
+    if xor(Atest === nothing, ytest === nothing)
+        @info "Both input (Atest) and target (ytest) data are required for testing the model, but only one of these has been provided.\nWill skip testing..."
+        return model
+    end
+    yt = Vector{Float64}(vec(ytest))
+    if model.grad_fx isa LossCallbacks                        # a callback loss: evaluated on the host
+        model.grad_fx.test = (Atest, ytest)
+        chk(ccall((:scs_set_test_callback, lib), Cint, (Ptr{Cvoid}, Cint), ctx, 1), ctx)
+    elseif Atest isa SparseMatrixCSC
+        At = SparseMatrixCSC(transpose(Atest))
+        rowptr = Int64.(At.colptr .- 1); colidx = Int32.(At.rowval .- 1); val = Vector{Float64}(At.nzval)
+        chk(ccall((:scs_set_test_sparse, lib), Cint,
+                  (Ptr{Cvoid}, Int64, Int64, Ptr{Int64}, Ptr{Int32}, Ptr{Float64}, Cint, Ptr{Float64}, Int64, Int64),
+                  ctx, size(Atest, 1), nnz(Atest), rowptr, colidx, val, val_f32 ? 1 : 0, yt, Ntest_global,
+                  test_row0), ctx)
+    else
+        Am = Matrix{Float64}(Atest)
+        chk(ccall((:scs_set_test_data, lib), Cint,
+                  (Ptr{Cvoid}, Int64, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Int64),
+                  ctx, size(Am, 1), Am, size(Am, 1), yt, Ntest_global, test_row0), ctx)
+    end
+    model.Atest, model.ytest = Atest, ytest
     return model
 end
 
@@ -84,14 +122,16 @@ end
 function DeviceProblem(A::Matrix{Float64}, y::AbstractVector, x0::Vector{Float64}, loss::Symbol, λ;
                        out_fn::Union{Symbol,Nothing}=nothing, scale::Float64=1.0 / size(A, 1),
                        L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0,
-                       N_global::Integer=size(A, 1), row0::Integer=0, devices=nothing)
+                       N_global::Integer=size(A, 1), row0::Integer=0, devices=nothing, Atest=nothing,
+                       ytest=nothing, Ntest_global::Integer=0, test_row0::Integer=0)
     ctx = create_ctx(device, devices)
     N, m = size(A)
     yv = Vector{Float64}(y)
     chk(ccall((:scs_set_data, lib), Cint,
               (Ptr{Cvoid}, Int64, Int64, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Int64),
               ctx, N, m, A, N, yv, N_global, row0), ctx)
-    return finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
+    model = finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
+    return set_test!(model, Atest, ytest; Ntest_global, test_row0)
 end
 
 # A::SparseMatrixCSC (README.md:105 builds it with sprandn): its CSC arrays are the column copy;
@@ -99,7 +139,8 @@ end
 function DeviceProblem(A::SparseMatrixCSC{Float64}, y::AbstractVector, x0::Vector{Float64}, loss::Symbol, λ;
                        out_fn::Union{Symbol,Nothing}=nothing, scale::Float64=1.0 / size(A, 1),
                        L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0,
-                       val_f32::Bool=false, N_global::Integer=size(A, 1), row0::Integer=0)
+                       val_f32::Bool=false, N_global::Integer=size(A, 1), row0::Integer=0, Atest=nothing,
+                       ytest=nothing, Ntest_global::Integer=0, test_row0::Integer=0)
     ctx = create_ctx(device)
     N, m = size(A)
     yv = Vector{Float64}(y)
@@ -111,7 +152,8 @@ function DeviceProblem(A::SparseMatrixCSC{Float64}, y::AbstractVector, x0::Vecto
                Ptr{Float64}, Cint, Ptr{Float64}, Int64, Int64),
               ctx, N, m, nnz(A), rowptr, colidx, val, colptr, rowidx, valT, val_f32 ? 1 : 0, yv, N_global, row0),
         ctx)
-    return finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
+    model = finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, P)
+    return set_test!(model, Atest, ytest; Ntest_global, test_row0, val_f32)
 end
 
 # ---- user losses outside the menu: the reference's own keyword callbacks ------------------
@@ -129,6 +171,7 @@ mutable struct LossCallbacks   # mutable: `user` is pointer_from_objref(cbs), ro
     hess_fy::Union{Function,Nothing}
     data::Union{Tuple,Nothing}       # (A, y) of a data problem: the closures take (A, y, x)
     nout::Int64                      # length(vec(ŷ)): the Jacobian rows (0: no GGN pieces)
+    test::Union{Tuple,Nothing}       # (Atest, ytest): f(Atest, ytest, x) for SCS_CB_FTEST
 end
 
 # J, r and diag(Q) of the step: a non-diagonal Q is eigen-rotated (J̃ = VᵀJ, r̃ = Vᵀr, q = λ),
@@ -164,6 +207,8 @@ function loss_trampoline(user::Ptr{Cvoid}, what::Cint, xp::Ptr{Float64}, m::Int6
             copyto!(unsafe_wrap(Array, outp, m), cbs.grad_fx(args...))
         elseif what == 3
             ggn_pieces!(unsafe_wrap(Array, outp, cbs.nout * (m + 2)), cbs, x)
+        elseif what == 4                                   # SCS_CB_FTEST (iterate.jl:173)
+            unsafe_store!(outp, Float64(cbs.f(cbs.test..., x)))
         else
             cbs.hess_fx === nothing && error("ProxNSCORE needs hess_fx (no automatic differentiation on the device path)")
             copyto!(unsafe_wrap(Array, outp, m * m), vec(Matrix{Float64}(cbs.hess_fx(args...))))   # column-major
@@ -191,17 +236,19 @@ end
 
 DeviceProblem(x0::Vector{Float64}, f::Function, λ; grad_fx=nothing, hess_fx=nothing, L=nothing,
               sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0) =
-    callback_problem(LossCallbacks(f, grad_fx, hess_fx, nothing, nothing, nothing, nothing, nothing, 0),
+    callback_problem(LossCallbacks(f, grad_fx, hess_fx, nothing, nothing, nothing, nothing, nothing, 0, nothing),
                      x0, λ, L, sol, C_set, P, device)
 
 # y may be a matrix (ny > 1 outputs, iterate.jl:105-107): out_fn / jac_yx / grad_fy / hess_fy see it as is
 function DeviceProblem(A::AbstractMatrix, y::AbstractVecOrMat, x0::Vector{Float64}, f::Function, λ; grad_fx=nothing,
                        hess_fx=nothing, out_fn=nothing, jac_yx=nothing, grad_fy=nothing, hess_fy=nothing,
-                       L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0)
+                       L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0,
+                       Atest=nothing, ytest=nothing)
     ggn = all(!isnothing, (out_fn, jac_yx, grad_fy, hess_fy))
     nout = ggn ? Int64(length(out_fn(A, x0))) : 0
-    cbs = LossCallbacks(f, grad_fx, hess_fx, out_fn, jac_yx, grad_fy, hess_fy, (A, y), nout)
-    return callback_problem(cbs, x0, λ, L, sol, C_set, P, device)
+    cbs = LossCallbacks(f, grad_fx, hess_fx, out_fn, jac_yx, grad_fy, hess_fy, (A, y), nout, nothing)
+    model = callback_problem(cbs, x0, λ, L, sol, C_set, P, device)
+    return set_test!(model, Atest, ytest)
 end
 
 # ---- row sharding (SURVEY.md §8e): one process per GPU, A's rows split across them ---------
@@ -253,6 +300,12 @@ end
 function devf(model::DeviceProblem, x::Vector{Float64})
     out = Ref{Float64}(0.0)
     chk(ccall((:scs_eval_f, lib), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Float64}), model.ctx, x, out), model.ctx)
+    return out[]
+end
+
+function devftest(model::DeviceProblem, x::Vector{Float64})
+    out = Ref{Float64}(0.0)
+    chk(ccall((:scs_eval_ftest, lib), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Float64}), model.ctx, x, out), model.ctx)
     return out[]
 end
 
@@ -419,19 +472,22 @@ function iterate_registered!(method, model, reg_name, hμ, max_epoch, x_tol, f_t
     configure!(model, reg_name, hμ)
     init_device!(method, model)
     cap = 2 * max_epoch + 1                           # scsopt.h: up to two pushes per epoch
-    obj, fval, pri, rel, objrel, tms = (Vector{Float64}(undef, cap) for _ in 1:6)
-    hist = (pointer(obj), pointer(fval), pointer(pri), pointer(rel), pointer(objrel), pointer(tms))
+    obj, fval, pri, rel, objrel, tms, ftst = (Vector{Float64}(undef, cap) for _ in 1:7)
+    has_test = model.Atest !== nothing                # iterate.jl:169-175: Solution.fvaltest
+    hist = (pointer(obj), pointer(fval), pointer(pri), pointer(rel), pointer(objrel), pointer(tms),
+            has_test ? pointer(ftst) : Ptr{Float64}(C_NULL))
     x_out = similar(model.x0); nh = Ref{Int64}(0); ep = Ref{Int64}(0)
-    GC.@preserve obj fval pri rel objrel tms begin
+    GC.@preserve obj fval pri rel objrel tms ftst begin
         chk(ccall((:scs_iterate, lib), Cint,
                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Cint, Ptr{Float64},
-                   Ref{NTuple{6,Ptr{Float64}}}, Ref{Int64}, Ref{Int64}),
+                   Ref{NTuple{7,Ptr{Float64}}}, Ref{Int64}, Ref{Int64}),
                   model.ctx, model.x0, model.x, max_epoch, x_tol, f_tol, reg_name == "gl" ? 1 : 0, x_out,
                   hist, nh, ep), model.ctx)
     end
     n = nh[]
     pris = Any[isnan(pri[i]) && i == 1 ? nothing : pri[i] for i in 1:n]
-    return Solution(x_out, obj[1:n], fval[1:n], pris, [], rel[1:n], objrel[1:n], Dict(), tms[1:n], ep[], model)
+    return Solution(x_out, obj[1:n], fval[1:n], pris, has_test ? ftst[1:n] : [], rel[1:n], objrel[1:n], Dict(),
+                    tms[1:n], ep[], model)
 end
 
 end # module

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -16,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCSOPT_LIB", os.path.join(_HERE, "libscsopt.so"))
 
 SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS_ERR_COMM, SCS_ERR_CALLBACK = range(8)
-SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS, SCS_CB_GGN = range(4)
+SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS, SCS_CB_GGN, SCS_CB_FTEST = range(5)
 
 LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5, "callback": 6}
 GGN = {None: 0, "sigmoid_ce": 1, "linear_ls": 2}
@@ -26,13 +27,28 @@ SMOOTH = {"phuber_l1l2": 1, "phuber_indbox": 2, "phuber_gl": 3, "exp_indbox": 4,
 METHOD = {"nscore": 1, "ggnscore": 2, "lqnscore": 3}
 SOLVER = {"default": 0, "reference": 1}
 
-# One HIP runtime per process: torch's wheel bundles ROCm libraries whose NEEDED
-# names ("libamdhip64.so") differ from the SONAMEs ("libamdhip64.so.7"), so if
-# libscsopt pulled /opt/rocm's copies in first, importing torch afterwards would
-# load a second runtime and crash.  Importing torch first makes libscsopt's
-# NEEDED entries resolve to the already-loaded (torch-bundled) HIP runtime and RCCL
-# (same SONAMEs).  torch is plumbing only (streams, torch.distributed).
-import torch  # noqa: E402,F401  (must precede the CDLL below)
+# One HIP runtime per process.  The product needs no torch: without it, libscsopt binds
+# /opt/rocm's HIP runtime and RCCL (preloaded RTLD_GLOBAL below).  torch's wheel bundles its own
+# copies, whose NEEDED names ("libamdhip64.so") differ from their SONAMEs ("libamdhip64.so.7"):
+# a torch imported AFTER /opt/rocm's runtime is bound would load a second runtime.  So when torch
+# is already imported (the tests, torch.distributed users), libscsopt's NEEDED entries resolve to
+# torch's loaded copies (same SONAMEs) instead, and scsopt.shard refuses to import torch late.
+if "torch" in sys.modules:
+    RUNTIME = "torch"
+else:
+    _ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+    for _so in ("libamdhip64.so.7", "librccl.so.1"):
+        _p = os.path.join(_ROCM, "lib", _so)
+        if os.path.exists(_p):
+            C.CDLL(_p, mode=C.RTLD_GLOBAL)
+    RUNTIME = "rocm"
+
+
+def require_torch_runtime(what):
+    """torch may join the process only when libscsopt is bound to torch's runtime."""
+    if RUNTIME == "rocm" and "torch" not in sys.modules:
+        raise ImportError(f"{what} needs torch, but scsopt was imported first and bound /opt/rocm's HIP runtime; "
+                          "import torch before scsopt in a process that uses torch")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -64,7 +80,8 @@ class Timing(C.Structure):
 class History(C.Structure):
     _fields_ = [("obj", C.POINTER(C.c_double)), ("fval", C.POINTER(C.c_double)),
                 ("pri_res_norm", C.POINTER(C.c_double)), ("rel", C.POINTER(C.c_double)),
-                ("objrel", C.POINTER(C.c_double)), ("times", C.POINTER(C.c_double))]
+                ("objrel", C.POINTER(C.c_double)), ("times", C.POINTER(C.c_double)),
+                ("fvaltest", C.POINTER(C.c_double))]
 
 
 _SIGS = {
@@ -85,6 +102,13 @@ _SIGS = {
     "scs_gen_data": (C.c_int, [C.c_void_p, C.POINTER(Synth)]),
     "scs_get_data": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_dp, C.c_int64, c_dp]),
     "scs_get_dims": (C.c_int, [C.c_void_p, c_i64p, c_i64p, c_i64p, c_i64p]),
+    "scs_set_test_data": (C.c_int, [C.c_void_p, C.c_int64, c_dp, C.c_int64, c_dp, C.c_int64, C.c_int64]),
+    "scs_set_test_sparse": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_i64p, c_i32p, c_dp, C.c_int, c_dp,
+                                      C.c_int64, C.c_int64]),
+    "scs_gen_test_data": (C.c_int, [C.c_void_p, C.POINTER(Synth)]),
+    "scs_set_test_callback": (C.c_int, [C.c_void_p, C.c_int]),
+    "scs_eval_ftest": (C.c_int, [C.c_void_p, c_dp, c_dp]),
+    "scs_has_test": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "scs_set_sparse": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, c_i64p, c_i32p, c_dp, c_i64p, c_i32p,
                                  c_dp, C.c_int, c_dp, C.c_int64, C.c_int64]),
     "scs_gen_sparse": (C.c_int, [C.c_void_p, C.POINTER(Synth), C.c_int]),

@@ -178,8 +178,10 @@ def device_optim_loop(method, model, reg_name, hmu, *, alpha=None, max_epoch=100
     init_method(method, model)
     m = model.m
     cap = 2 * int(max_epoch) + 1                       # scsopt.h: up to two pushes per epoch
-    hist = {k: np.empty(cap) for k in ("obj", "fval", "pri_res_norm", "rel", "objrel", "times")}
-    h = _lib.History(*(dptr(hist[k]) for k in ("obj", "fval", "pri_res_norm", "rel", "objrel", "times")))
+    keys = ("obj", "fval", "pri_res_norm", "rel", "objrel", "times", "fvaltest")
+    hist = {k: np.empty(cap) for k in keys}
+    test_model = bool(getattr(model, "test_model", False))
+    h = _lib.History(*(dptr(hist[k]) if (k != "fvaltest" or test_model) else None for k in keys))
     x0 = np.ascontiguousarray(model.x0, dtype=np.float64)
     xs = np.ascontiguousarray(model.x, dtype=np.float64)
     x_out = np.empty(m)
@@ -190,15 +192,18 @@ def device_optim_loop(method, model, reg_name, hmu, *, alpha=None, max_epoch=100
     n = int(nh.value)
     pris = [None if (i == 0 and math.isnan(v)) else float(v) for i, v in enumerate(hist["pri_res_norm"][:n])]
     as_list = lambda k: [float(v) for v in hist[k][:n]]   # noqa: E731
-    return Solution(x_out, as_list("obj"), as_list("fval"), pris, [], as_list("rel"), as_list("objrel"), {},
+    fvaltest = as_list("fvaltest") if test_model else []
+    return Solution(x_out, as_list("obj"), as_list("fval"), pris, fvaltest, as_list("rel"), as_list("objrel"), {},
                     as_list("times"), int(ep.value), model)
 
 
-def _show(opt_verbose, label, tag, epoch, obj, fval, pri, rel, dt):
+def _show(opt_verbose, label, tag, epoch, obj, fval, pri, rel, dt, ftest=None):
     if opt_verbose > 1:
         print("\n" + "=" * 30)
         print(f"Optimizer:\t{label}")
-        print(f"{tag} = {epoch}\nobj = {obj}\nfval = {fval}\npri_res_norm = {pri}\nrel_error = {rel}\nΔtime = {dt}")
+        ft = "" if ftest is None else f"fvaltest = {ftest}\n"
+        print(f"{tag} = {epoch}\nobj = {obj}\nfval = {fval}\npri_res_norm = {pri}\n{ft}rel_error = {rel}\n"
+              f"Δtime = {dt}")
 
 
 def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_epoch=1000, x_tol=1e-10,
@@ -215,6 +220,8 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
     f = model.fx
     greg = model.get_reg
     fvals, pris, objs, rels, frels, times = [], [], [], [], [], []
+    fvaltests = []
+    test_model = bool(getattr(model, "test_model", False))   # iterate.jl:169-175
     metric_vals = {k: [] for k in (metrics or {})}
     epochs = 0
     x_star = model.x
@@ -239,10 +246,16 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
             q = np.float64(abs(ob - obj_star)) / np.float64(abs(obj_star))
         return _jl_max(q, f_tol)
 
-    def push(ob, fv, pr, rl, fr, dt, xx):
+    def push(ob, fv, pr, rl, fr, dt, xx, ft):
+        # show_stat! (utils.jl:50-57: ftest, metrics) + update_stat! (utils.jl:106-113)
+        if test_model:
+            fvaltests.append(ft)
         objs.append(ob); fvals.append(fv); pris.append(pr); rels.append(rl); frels.append(fr); times.append(dt)
         for k in metric_vals:
             metric_vals[k].append(metrics[k](model, xx))
+
+    def ftest(xx):
+        return model.ftest(xx) if test_model else None
 
     iend = max(nbatch, 1)
     for epoch_t in range(1, max_epoch + 1):
@@ -251,17 +264,19 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
         obj = fval + greg(x)
         rel_error = rel_of(x)
         f_rel_error = frel_of(obj)
-        _show(verbose, method.label, "epoch", epoch_t - 1, obj, fval, pri, rel_error, dt)
-        push(obj, fval, pri, rel_error, f_rel_error, dt, x)
+        ft = ftest(x)
+        _show(verbose, method.label, "epoch", epoch_t - 1, obj, fval, pri, rel_error, dt, ft)
+        push(obj, fval, pri, rel_error, f_rel_error, dt, x, ft)
         for i in range(1, iend + 1):                          # iterate.jl:204-255
             if epoch_t == max_epoch and i == iend:            # iterate.jl:219-231
                 dt = now()
                 fval = f(x)
                 obj = fval + greg(x)
                 rel_error = rel_of(x)
-                _show(verbose, method.label, "max_epoch", epoch_t, obj, fval, pri, rel_error, dt)
+                ft = ftest(x)
+                _show(verbose, method.label, "max_epoch", epoch_t, obj, fval, pri, rel_error, dt, ft)
                 f_rel_error = frel_of(obj)
-                push(obj, fval, pri, rel_error, f_rel_error, dt, x)
+                push(obj, fval, pri, rel_error, f_rel_error, dt, x, ft)
             x_new, pri = step(method, model, reg_name, hmu, x, x_prev, epoch_t, batch=(i - 1) if nbatch else None)
             if _norm(x_new - x) < x_tol * max(_norm(x), 1.0) or f_rel_error <= f_tol or pri < x_tol:
                 if epoch_t != max_epoch:                      # iterate.jl:235-247
@@ -269,9 +284,10 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
                     fval = f(x_new)
                     obj = fval + greg(x_new)
                     rel_error = rel_of(x_new)
-                    _show(verbose, method.label, "terminate_epoch", epoch_t, obj, fval, pri, rel_error, dt)
+                    ft = ftest(x_new)
+                    _show(verbose, method.label, "terminate_epoch", epoch_t, obj, fval, pri, rel_error, dt, ft)
                     f_rel_error = frel_of(obj)
-                    push(obj, fval, pri, rel_error, f_rel_error, dt, x_new)
+                    push(obj, fval, pri, rel_error, f_rel_error, dt, x_new, ft)
                 x_prev = x
                 x = x_new
                 epochs += 1
@@ -281,4 +297,4 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
         if _norm(x - x_prev) < x_tol * max(_norm(x_prev), 1.0) or f_rel_error <= f_tol or pri < x_tol:
             break                                             # iterate.jl:257-259
         epochs += 1
-    return Solution(x, objs, fvals, pris, [], rels, frels, metric_vals, times, epochs, model)
+    return Solution(x, objs, fvals, pris, fvaltests, rels, frels, metric_vals, times, epochs, model)

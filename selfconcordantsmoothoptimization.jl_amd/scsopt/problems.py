@@ -10,6 +10,7 @@ host.  Row sharding: pass ``comm=shard.Comm(...)`` and the local rows.
 from __future__ import annotations
 
 import ctypes as C
+import logging
 from dataclasses import dataclass
 from typing import Any, Optional
 
@@ -19,6 +20,8 @@ from . import _lib
 from ._lib import LOSS, GGN, REG, SMOOTH, dptr
 from .losses import Loss, OutFn, ggn_kind
 from .smoothers import Smoother, bounds_array
+
+log = logging.getLogger("scsopt")
 
 
 @dataclass
@@ -67,8 +70,9 @@ def _is_sparse(A):
 class Problem:
     """problems.jl:21-40 (data) / :5-19 (generic)."""
 
-    def __init__(self, *args, L=None, sol=None, C_set=None, P=None, out_fn: Optional[OutFn] = None,
-                 name=None, device=0, comm=None, N_global=None, row0=0, sparse_f32=False, devices=None, _ctx=None):
+    def __init__(self, *args, Atest=None, ytest=None, L=None, sol=None, C_set=None, P=None,
+                 out_fn: Optional[OutFn] = None, name=None, device=0, comm=None, N_global=None, row0=0,
+                 sparse_f32=False, devices=None, Ntest_global=None, test_row0=0, _ctx=None):
         if len(args) == 5:
             A, y, x0, f, lam = args
         elif len(args) == 3:
@@ -134,8 +138,77 @@ class Problem:
             raise ValueError("f and out_fn must use the same scale (one device loss scale)")
         scale = f.scale
         self.ctx.check(_lib.lib.scs_set_loss(self.ctx.h, LOSS[f.kind], GGN[ggn], scale))
+        self._cb_test = None
         if f.kind == "callback":
             self._bind_callback(f)
+        self.set_test(Atest, ytest, Ntest_global=Ntest_global, row0=test_row0)
+
+    # held-out data (problems.jl:27-28,67-68; iterate.jl:169-175) --------------------------
+    def set_test(self, Atest=None, ytest=None, *, Ntest_global=None, row0=0, sparse_f32=False):
+        """Atest / ytest: ftest(x) = f(Atest, ytest, x) -- the problem's own f, scale literal
+        included -- is pushed into Solution.fvaltest at every stats push.  Both are required; one
+        alone is the reference's "Will skip testing..." case.  Sharded: this rank's rows of the
+        held-out set (Ntest_global rows in all); a devices=[...] problem takes the whole set."""
+        self.ctx.check(_lib.lib.scs_set_test_data(self.ctx.h, 0, None, 0, None, 0, 0))   # clear
+        self._cb_test = None
+        self.test_model = False
+        if Atest is None and ytest is None:
+            return
+        if Atest is None or ytest is None:    # iterate.jl:170-171
+            log.info("Both input (Atest) and target (ytest) data are required for testing the model, but only one "
+                     "of these has been provided.\nWill skip testing...")
+            return
+        if self.generic and getattr(self.f, "kind", None) != "callback":
+            raise ValueError("a ProblemGeneric has no test data (problems.jl:5-19)")
+        if self.f.kind == "callback":
+            if self._cb_data is None:
+                raise ValueError("Atest / ytest need a data problem: Problem(A, y, x0, f, λ; Atest, ytest)")
+            self._cb_test = (Atest, np.asarray(ytest, dtype=np.float64))
+            self.ctx.check(_lib.lib.scs_set_test_callback(self.ctx.h, 1))
+            self.test_model = True
+            return
+        yv = np.ascontiguousarray(np.asarray(ytest, dtype=np.float64).reshape(-1))
+        Ng = int(Ntest_global) if Ntest_global is not None else 0
+        if _is_sparse(Atest):
+            csr = Atest.tocsr()
+            if csr.shape[1] != self.m or csr.shape[0] != yv.shape[0]:
+                raise ValueError(f"Atest must be Ntest x m (m = {self.m}) with len(ytest) = Ntest")
+            rowptr = np.ascontiguousarray(csr.indptr, dtype=np.int64)
+            colidx = np.ascontiguousarray(csr.indices, dtype=np.int32)
+            val = np.ascontiguousarray(csr.data, dtype=np.float64)
+            self.ctx.check(_lib.lib.scs_set_test_sparse(
+                self.ctx.h, int(csr.shape[0]), int(val.shape[0]), rowptr.ctypes.data_as(_lib.c_i64p),
+                colidx.ctypes.data_as(_lib.c_i32p), dptr(val), 1 if sparse_f32 else 0, dptr(yv), Ng, int(row0)))
+        else:
+            At = np.asarray(Atest, dtype=np.float64)
+            if At.ndim != 2 or At.shape[1] != self.m or At.shape[0] != yv.shape[0]:
+                raise ValueError(f"Atest must be Ntest x m (m = {self.m}) with len(ytest) = Ntest")
+            Af = np.asfortranarray(At)
+            self.ctx.check(_lib.lib.scs_set_test_data(self.ctx.h, int(At.shape[0]), Af.ctypes.data_as(_lib.c_dp),
+                                                      int(At.shape[0]), dptr(yv), Ng, int(row0)))
+        self.test_model = True
+
+    def gen_test(self, Ntest, *, row0=None, seed=1234, kind=1, density=0.1):
+        """Held-out rows of the synthetic generator: rows [row0, row0 + Ntest) with row0 = N_global
+        by default (samples the training rows never saw, same x_true).  Sharded: this rank
+        generates its contiguous block of the Ntest rows."""
+        from .shard import row_range
+        r0 = self.N_global if row0 is None else int(row0)
+        comm = self.comm
+        # one process per GPU: this rank's block; one process (one or several devices): all rows
+        # (a devices=[...] context splits them itself)
+        a, b = row_range(Ntest, comm.world, comm.rank) if comm is not None else (0, int(Ntest))
+        spec = _lib.Synth(N_global=int(Ntest), row0=r0 + a, N=b - a, m=self.m, seed=seed, kind=kind, density=density)
+        self.ctx.check(_lib.lib.scs_gen_test_data(self.ctx.h, C.byref(spec)))
+        self._cb_test = None
+        self.test_model = True
+
+    def ftest(self, x):
+        """f(Atest, ytest, x) (iterate.jl:173) on the device (a callback loss: on the host)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = C.c_double()
+        self.ctx.check(_lib.lib.scs_eval_ftest(self.ctx.h, dptr(x), C.byref(out)))
+        return out.value
 
     def _bind_callback(self, f):
         """Register f / grad_fx / hess_fx with scs_set_loss_callback; a Python exception inside a
@@ -188,6 +261,9 @@ class Problem:
                     np.ctypeslib.as_array(outp, shape=(m * m,))[:] = H.ravel(order="F")   # column-major
                 elif what == _lib.SCS_CB_GGN:
                     ggn_pieces(x, m, outp)
+                elif what == _lib.SCS_CB_FTEST:   # iterate.jl:173: the same closure on the held-out data
+                    At, yt = self._cb_test
+                    outp[0] = float(f.f(At, yt, x))
                 else:
                     raise ValueError(f"unknown callback request {what}")
                 return 0
@@ -201,7 +277,7 @@ class Problem:
 
     @classmethod
     def synthetic(cls, N, m, x0, f, lam, *, kind=1, seed=1234, density=0.1, out_fn=None, device=0,
-                  comm=None, devices=None, **kw):
+                  comm=None, devices=None, test_N=None, **kw):
         """A ~ N(0,1)/sqrt(m) (kind 1, 2) or N(0,1) (kind 3) generated on the device, y from a
         sparse x_true (kind 1: Bernoulli(σ(A x_true)) ∈ {0,1}; kind 2: ±1; kind 3: A x_true + 0.1ε).
         With comm, this rank generates its contiguous row shard in place; with devices=[...] one
@@ -217,7 +293,10 @@ class Problem:
             comm.attach(ctx)
         spec = _lib.Synth(N_global=N, row0=r0, N=r1 - r0, m=m, seed=seed, kind=kind, density=density)
         ctx.check(_lib.lib.scs_gen_data(ctx.h, C.byref(spec)))
-        return cls(x0, f, lam, out_fn=out_fn, device=device, comm=comm, _ctx=ctx, **kw)
+        p = cls(x0, f, lam, out_fn=out_fn, device=device, comm=comm, _ctx=ctx, **kw)
+        if test_N:   # held-out rows [N, N + test_N) of the same generator (same x_true)
+            p.gen_test(int(test_N), row0=N, seed=seed, kind=kind, density=density)
+        return p
 
     @classmethod
     def synthetic_sparse(cls, N, m, x0, f, lam, *, density=0.01, seed=1234, f32=False, device=0, **kw):

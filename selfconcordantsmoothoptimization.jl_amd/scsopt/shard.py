@@ -38,6 +38,8 @@ class Comm:
     """Binds a libscsopt context to a torch.distributed process group."""
 
     def __init__(self, rank=None, world=None, group=None, device=None, native=None, force=False):
+        from . import _lib
+        _lib.require_torch_runtime("scsopt.shard.Comm")
         import torch.distributed as dist
         self.rank = dist.get_rank(group) if rank is None else int(rank)
         self.world = dist.get_world_size(group) if world is None else int(world)
@@ -46,6 +48,9 @@ class Comm:
         if native is None:
             native = dist.get_backend(group) == "nccl"
         self.native = bool(native)
+        # a backend that stages device tensors through host memory (gloo) lands the sum from its own
+        # stream: the callback then waits for the device before handing back to libscsopt
+        self.host_staged = dist.get_backend(group) != "nccl"
         self.force = bool(force)
         self.buf = None
         self._cb = None
@@ -108,8 +113,10 @@ class Comm:
             # the library reads the sum on its stream right after this returns; a process group
             # that copies device tensors through host memory (gloo) lands the result from its own
             # stream, so wait for the device here (measured: without it, back-to-back row
-            # all-gathers of the sharded sample-space branch read a partly landed sum)
-            torch.cuda.synchronize(self.buf.device)
+            # all-gathers of the sharded sample-space branch read a partly landed sum).  NCCL
+            # (RCCL) enqueues on the external stream itself: no wait.
+            if self.host_staged:
+                torch.cuda.synchronize(self.buf.device)
             return 0
         except Exception as e:  # surfaced by libscsopt as SCS_ERR_COMM
             import sys

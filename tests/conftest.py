@@ -11,6 +11,9 @@ import subprocess
 import sys
 
 import pytest
+# the tests use torch (streams, torch.distributed): import it before scsopt so libscsopt binds
+# torch's HIP runtime (scsopt/_lib.py); the torch-free import is covered by test_abi.py
+import torch  # noqa: F401,E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd")

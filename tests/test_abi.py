@@ -84,3 +84,23 @@ def test_get_P_validates_partition():
         scsopt.get_P(6, np.array([1, 2, 3, 3, 4, 5]), np.array([[1, 4], [3, 6], [1, 1]]))
     with pytest.raises(ValueError):   # ntotal != n: the reference's Cmat / smoothers raise DimensionMismatch
         scsopt.get_P(6, np.arange(1, 7), np.array([[1, 3], [4, 6], [1, 1]]))
+
+
+def test_product_loads_without_torch():
+    """scsopt needs no torch: in a fresh interpreter it binds /opt/rocm's HIP runtime and RCCL
+    (preloaded RTLD_GLOBAL), never imports torch, and refuses a late torch.distributed binding
+    (which would load a second HIP runtime)."""
+    import subprocess
+    import sys
+    code = ("import sys; import scsopt; assert 'torch' not in sys.modules, 'torch imported'; "
+            "print(scsopt._lib.RUNTIME)\n"
+            "try:\n    scsopt.shard.Comm(rank=0, world=1)\n    print('no-error')\n"
+            "except ImportError as e:\n    print('refused')\n")
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["rocm", "refused"], out.stdout
+    maps = subprocess.run([sys.executable, "-c", "import scsopt, os; print(open('/proc/self/maps').read())"],
+                          capture_output=True, text=True, env=env, timeout=120).stdout
+    hip = {ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln}
+    assert hip and all(p.startswith(os.environ.get("ROCM_PATH", "/opt/rocm")) or "/rocm" in p for p in hip), hip

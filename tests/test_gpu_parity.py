@@ -783,7 +783,8 @@ def test_lqn_fused_epoch_bit_identical(reg, use_prox, m, monkeypatch):
         np.testing.assert_allclose(a.rel, b.rel, rtol=1e-13)
 
 
-@pytest.mark.parametrize("method,ss", [("nscore", 1), ("nscore", 3), ("lqn", 1), ("lqn", 2), ("lqn", 3), ("ggn", 1)])
+@pytest.mark.parametrize("method,ss", [("nscore", 1), ("nscore", 3), ("lqn", 1), ("lqn", 2), ("lqn", 3), ("ggn", 1),
+                                       ("ggn", 3)])
 def test_step_grad_fx_keyword(method, ss):
     """step!(...; ∇fx) (iterate.jl:52-54): grad_f = x -> ∇fx everywhere inside the step
     (prox-N-SCORE.jl:66-68, prox-L-BFGS-SCORE.jl:98-100: ∇q, BB's ∇q_prev, the line search and

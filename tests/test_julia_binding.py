@@ -4,7 +4,7 @@ Julia is absent here and on the GPU box, so the binding is never executed; this 
 can be checked without it: every `ccall((:scs_*, lib), Ret, (Args...), ...)` names a function the
 header declares, with the same number of arguments and Julia types that match the C prototype
 (Ptr{Float64} <-> double*, Int64 <-> int64_t, Cint <-> int, Ref{T} <-> T*, Ptr{Cvoid} <-> any
-pointer, the 6-pointer scs_history struct as Ref{NTuple{6,Ptr{Float64}}}), and that the binding
+pointer, the 7-pointer scs_history struct as Ref{NTuple{7,Ptr{Float64}}}), and that the binding
 reads the IndBox smoothers' bounds the way the reference builds them (closure captures,
 phuber-smooth.jl:59-65), not from fields the reference structs do not have.
 """
@@ -92,7 +92,7 @@ def _compatible(jt, ct):
         return True                                   # void* / scs_ctx* / struct pointers
     if inner == "Ptr{Cvoid}":
         return pointee.endswith("*")                  # scs_ctx** / void**
-    if inner.startswith("NTuple{6,Ptr{Float64}}"):
+    if inner.startswith("NTuple{7,Ptr{Float64}}"):
         return pointee == "scs_history"
     return C_POINTEE.get(inner) == pointee
 

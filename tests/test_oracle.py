@@ -230,3 +230,29 @@ def test_set_name_plain_labels():
         p = M()
         O.set_name(p, algs)
         assert p.name.startswith("prox-") and p.label.startswith("Prox-")
+
+
+def test_oracle_fvaltest_history():
+    """iterate.jl:169-175 / utils.jl:55-57: with Atest AND ytest every stats push appends
+    ftest(x) = f(Atest, ytest, x) of the pushed point (same f, same scale), so len(fvaltest) ==
+    len(obj), including the duplicated max-epoch push; one of the two alone (the xor case) and a
+    ProblemGeneric record nothing."""
+    A = np.array([[-0.560501, 0.0], [0.0, 1.85278], [-0.0192918, -0.827763], [0.128064, 0.110096],
+                  [0.0, -0.251176]])
+    y = np.array([-1.0, -1.0, -1.0, 1.0, -1.0])
+    At = np.array([[0.3, -0.2], [-1.1, 0.4], [0.7, 0.9]])
+    yt = np.array([1.0, -1.0, 1.0])
+    x0 = np.array([0.5908446386657102, 0.7667970365022592])
+    loss = O.Loss("logistic_margin", 1 / 5)
+    for max_epoch in (2, 1000):
+        om = O.Problem(A, y, x0, loss, 1.0, Atest=At, ytest=yt)
+        sol = O.iterate(O.ProxNSCORE(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=max_epoch)
+        assert len(sol.fvaltest) == len(sol.obj)
+        assert sol.fvaltest[0] == loss.f(At, yt, x0)
+        if max_epoch == 1000:   # the termination push is of x_new = the returned x (iterate.jl:235-247)
+            assert sol.fvaltest[-1] == pytest.approx(loss.f(At, yt, sol.x), rel=1e-12)
+        else:   # 2 epoch pushes + the duplicated max-epoch push (iterate.jl:219-231)
+            assert len(sol.obj) == 3 and sol.fvaltest[-1] == sol.fvaltest[-2] and sol.obj[-1] == sol.obj[-2]
+    om = O.Problem(A, y, x0, loss, 1.0, Atest=At)
+    assert not om.test_model
+    assert O.iterate(O.ProxNSCORE(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=3).fvaltest == []
