@@ -145,7 +145,9 @@ int scs_set_comm_rccl(scs_ctx* ctx, int rank, int nranks, const void* id /* 128 
  * communicator is exercised on a one-GPU host (results are unchanged).                        */
 int scs_set_comm_force(scs_ctx* ctx, int on);
 /* Device buffer (>= scs_reduce_buffer_size() doubles) owned by the caller,
- * used as the in-place all-reduce payload.                                  */
+ * used as the in-place all-reduce payload.  The size depends on the data and
+ * on the registered batch list (the sample-space all-gather of batches with
+ * N_global + 1 <= m): query it again after scs_set_batches.                 */
 int scs_reduce_buffer_size(scs_ctx* ctx, int64_t* ndoubles);
 int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
 

@@ -545,14 +545,11 @@ __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, i
 // that C tile traffic: 2·128 KiB per 4.2 MFLOP tile).
 static int outer_block();
 
-// The bulk stream (the lookahead's trailing updates) can leave SCS_CHOL_RESERVE_CUS CUs (a multiple of
-// 8: that many / 8 per XCD) to the serial chain on the context stream (hipExtStreamCreateWithCUMask).
-// r02 measured 32 reserved CUs at C2 solve 12.04 -> 10.97 ms (profiles/r02/chol/reserve/).  Off by
-// default since r03: a process that created a CU-masked queue faults at exit under rocprofv3 -- in
-// librocprofiler-sdk's static destructors, inside libhsa-runtime64 (SCS_SEGV_TRACE frames,
-// profiles/r03/segv/) -- so the profiled configuration could not be the benchmarked one.  The
-// chain is shortened instead (chol_diag_kernel, the fused chain launches).  Masking is best effort:
-// a failure falls back to an ordinary non-blocking stream.
+// The bulk stream (the lookahead's trailing updates) is a plain non-blocking stream.  (r02 kept 32
+// CUs from it with a CU-masked queue, hipExtStreamCreateWithCUMask; a process that created one
+// faulted at exit under rocprofv3 -- in librocprofiler-sdk's static destructors, profiles/r03/segv/
+// -- so the profiled configuration could not be the benchmarked one.  Removed in r04: the CU-bounded
+// persistent bulk launches below keep the same CUs free.)
 // SCS_CHOL_BULK_SKIP: the CU ids (within a shader engine, HW_REG_HW_ID bits 11:8; a bit mask,
 // hex accepted) whose workgroup slots the bulk stream's launches leave to the chain
 // (gram_launch_bounded); 0 = plain launches.  Default: CU id 5 (present in every shader engine
@@ -567,33 +564,7 @@ static unsigned bulk_skip_mask(int nblk) {
   return nblk <= 64 ? 0x20u : 0u;
 }
 
-static hipError_t create_bulk_stream(hipStream_t* s, int nblk) {
-  const char* env = getenv("SCS_CHOL_RESERVE_CUS");
-  const int reserve = env ? atoi(env) : 0;
-  (void)nblk;
-  int dev = 0, ncu = 0;
-  if (reserve > 0 && hipGetDevice(&dev) == hipSuccess &&
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 4 * reserve) {
-    // mask bit i is CU i of the XCD-interleaved numbering (XCD i % 8; measured: clearing bits
-    // i % 16 == 15 took 16 CUs from one XCD and slowed the XCD-balanced Gram schedule 1.6x), so
-    // the top `reserve` bits take reserve / 8 CUs from every XCD
-    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu - reserve; ++i) mask[i / 32] |= 1u << (i % 32);
-    if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
-    (void)hipGetLastError();
-  }
-  // SCS_CHOL_BULK_PRIO=1: the bulk stream at the lowest stream priority, so a workgroup slot a
-  // finished bulk workgroup frees goes to the chain's pending launch first (A/B)
-  const char* pe = getenv("SCS_CHOL_BULK_PRIO");
-  if (pe && atoi(pe) > 0) {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
-        hipStreamCreateWithPriority(s, hipStreamNonBlocking, least) == hipSuccess)
-      return hipSuccess;
-    (void)hipGetLastError();
-  }
-  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-}
+static hipError_t create_bulk_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
 
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
@@ -608,7 +579,7 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipMalloc(&a->rect, sizeof(int2) * rl.size());
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = create_bulk_stream(&a->st2, nblk);
+  if (e == hipSuccess) e = create_bulk_stream(&a->st2);
   if (e == hipSuccess) e = hipMalloc(&a->bctr, 16 * sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&a->sscr, sizeof(double) * 2 * (size_t)CB * 16 * CB);
   if (e == hipSuccess) {
@@ -660,10 +631,7 @@ void chol_aux_free(CholAux* a) {
   a->dag_ob = 0;
   a->dstep.clear();
   a->dnext.clear();
-  // SCS_CHOL_KEEP_BULK=1 (diagnosis of the profiler's exit fault with a CU-masked stream): the
-  // bulk stream is left to the runtime's teardown instead of destroyed here
-  static const bool keep = getenv("SCS_CHOL_KEEP_BULK") && atoi(getenv("SCS_CHOL_KEEP_BULK")) > 0;
-  if (a->st2 && !keep) (void)hipStreamDestroy(a->st2);
+  if (a->st2) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
   a->ev1 = a->ev2 = a->ev3 = nullptr;
@@ -794,7 +762,7 @@ static bool ba_steps() {
 //   C12 (st2) everything else of the trailing update in ONE launch: the rest of the next
 //             block's strip and all pairs beyond it (the full trailing tile list minus its
 //             first OB(OB+1)/2 entries, which are C1a's).
-// st2 is the bulk stream (CU-masked: create_bulk_stream) and streams Bb_t, C12_t, Bb_{t+1}, ...
+// st2 is the bulk stream (create_bulk_stream; CU-bounded launches) and streams Bb_t, C12_t, Bb_{t+1}, ...
 // back to back whenever the chain (A + Ba + C1a) is shorter than C12 (large m); the chain's
 // Ba_{t+1} / C1a_{t+1} wait for C12_t (same elements).  Every element still receives its
 // updates in block order with the same per-tile arithmetic (the kernels share one MFMA order),

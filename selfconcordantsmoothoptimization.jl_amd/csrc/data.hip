@@ -257,6 +257,21 @@ hipError_t launch_retile(double* C, double* A, int64_t Npad, int64_t p, int to_t
   return hipGetLastError();
 }
 
+__global__ void ls_pair_kernel(const double* __restrict__ z0, const double* __restrict__ zd, double alpha,
+                               int64_t Npad, double* __restrict__ out) {
+  for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < Npad; n += (int64_t)gridDim.x * blockDim.x) {
+    out[n] = z0[n];
+    out[Npad + n] = alpha * zd[n];
+  }
+}
+
+hipError_t launch_ls_pair(const double* z0, const double* zd, double alpha, int64_t Npad, double* out,
+                          hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(Npad, 256), 4096);
+  hipLaunchKernelGGL(ls_pair_kernel, dim3(grid), dim3(256), 0, st, z0, zd, alpha, Npad, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_sum_partials(const double* part, int n, double* out, hipStream_t st) {
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, st, part, n, out);
   return hipGetLastError();

@@ -888,7 +888,7 @@ hipError_t gram_vfinal_launch(const double* VP, int npiece, int64_t vps, int64_t
 }
 
 // the kernel of the latest main Gram launch (gram_launch / gram_launch_sched), as rocprofv3 names it
-static const char* g_main_name = "";
+static thread_local const char* g_main_name = "";   // per host thread: a multi-device context drives its devices from one thread each
 const char* gram_main_kernel_name() { return g_main_name; }
 
 hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk, const int2* tiles,

@@ -24,6 +24,10 @@
 #include <cstring>
 #include <limits>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -179,6 +183,7 @@ struct scs_ctx {
          *zb = nullptr, *d = nullptr, *gq = nullptr, *gqn = nullptr, *gtmp = nullptr, *gtmp2 = nullptr, *q = nullptr,
          *ab = nullptr, *tlwork = nullptr, *scal = nullptr, *gcache[2] = {nullptr, nullptr};
   double* hscal = nullptr;  // pinned host scalars
+  int* hserr = nullptr;     // pinned: the one-launch triangular solves' timeout flag, copied after each solve
   double* xstar = nullptr;  // model.x on the device (scs_iterate's rel_error)
   double* lqR = nullptr;    // fused ProxLQNSCORE epoch: LQ_NPART x 256 partial sums
   double* hloop = nullptr;  // pinned: the pipelined loop's per-epoch scalars, two epochs (parity)
@@ -282,6 +287,9 @@ struct scs_ctx {
   uint64_t gview_gen = 0;      // ... of batch list generation gview_gen
   uint64_t batch_gen = 1;      // bumped whenever the batch list changes (scs_set_batches)
   bool lu_fallback_used = false;
+  // the incremental line search's N-space scratch: [z0 | α·A d] trial pair (2 Npad) + A d (Npad)
+  double* lsbuf = nullptr;
+  int64_t lscap = 0;
 
   // caches (CSE of identical evaluations; keyed by the host x content)
   std::vector<double> zkey;
@@ -319,6 +327,13 @@ struct scs_ctx {
   std::vector<RowBlock> plan;
   int64_t grpN = 0, grpm = 0;   // the whole problem's rows and columns
   bool group_broken = false;
+  // one persistent host thread per device (group_run hands each call's per-device work to them:
+  // no thread spawn per ABI call); `aborting` is shared with the sub-contexts (comm_abort), which
+  // check it before every RCCL call once a failing device has aborted the communicators
+  struct Workers;
+  std::unique_ptr<Workers> workers;
+  std::shared_ptr<std::atomic<bool>> comm_abort;
+  ~scs_ctx();
 };
 
 // ---------------------------------------------------------------------------
@@ -411,7 +426,23 @@ void h2d(scs_ctx* c, double* dst, const double* src, int64_t n) {
 void d2h(scs_ctx* c, double* dst, const double* src, int64_t n) {
   HCK(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
 }
-void sync(scs_ctx* c) { HCK(hipStreamSynchronize(c->st)); }
+// Drain the stream.  A triangular solve whose block wait gave up (~30 s, never expected) flagged
+// caux.serr; its copy lands in hserr behind the solve, so the first drain after that solve reports
+// it (the step's direction is invalid) instead of the next factor's chain check.
+void sync(scs_ctx* c) {
+  HCK(hipStreamSynchronize(c->st));
+  if (c->hserr && *c->hserr) {
+    *c->hserr = 0;
+    if (c->caux.serr) HCK(hipMemsetAsync(c->caux.serr, 0, sizeof(int), c->st));
+    HCK(hipStreamSynchronize(c->st));
+    fail(c, SCS_ERR_HIP, "Cholesky triangular solve: a block wait timed out; this step's direction is invalid");
+  }
+}
+
+// after a chol_solve on the context stream: its timeout flag -> hserr (checked by sync)
+void solve_flag_copy(scs_ctx* c) {
+  if (c->hserr && c->caux.serr) HCK(hipMemcpyAsync(c->hserr, c->caux.serr, sizeof(int), hipMemcpyDeviceToHost, c->st));
+}
 
 void tbegin(scs_ctx* c, int cat, hipEvent_t* e0) {
   if (!c->timing) return;
@@ -517,12 +548,17 @@ int64_t reduce_buffer_doubles(const scs_ctx* c) {
   const int64_t nb = c->mpad / 128;
   const int64_t tsz = (nb * (nb + 1) / 2 + nb) * 128 * 128;   // 128 x 128 slots (tall lists add <= nb)
   int64_t need = std::max<int64_t>(tsz + c->mpad, c->mpad);
-  // GGN sample-space branch across ranks: all-gather of A and y.  Sized from the full data's
-  // N_global (a batch view swapped in at the first exchange is never larger): the buffer is
-  // allocated once, whichever view is active then
-  const int64_t Nfull = std::max(c->Nglob_data, c->Nglob);
-  if (Nfull + 1 <= c->m || c->Nglob + 1 <= c->m) {
-    const int64_t Ng = round_up(std::max<int64_t>(std::min(Nfull, c->m), 1), 16);
+  // GGN sample-space branch across ranks: the all-gather of the rows (Ng x m_pad) and y of the
+  // full data when N_global + 1 <= m, and of every registered batch whose global size b has
+  // b + 1 <= m -- sized from those sizes, not from m (the buffer outlives view swaps; a new batch
+  // list that needs more reallocates a library-owned buffer, scs_set_batches)
+  int64_t ng = 0;
+  if (c->Nglob_data + 1 <= c->m) ng = c->Nglob_data;
+  for (int64_t b : c->bglob)
+    if (b + 1 <= c->m) ng = std::max(ng, b);
+  if (c->bsel < 0 && c->Nglob + 1 <= c->m) ng = std::max(ng, c->Nglob);
+  if (ng > 0) {
+    const int64_t Ng = round_up(ng, 16);
     need = std::max<int64_t>(need, Ng * c->mpad + Ng);
   }
   return need + 64;
@@ -545,6 +581,8 @@ void allreduce(scs_ctx* c, double* buf, int64_t count) {
                                (long long)c->red_cap, (long long)count);
   hipEvent_t e0;
   tbegin(c, T_REDUCE, &e0);
+  if (c->comm_abort && c->comm_abort->load(std::memory_order_acquire))
+    fail(c, SCS_ERR_COMM, "the multi-device context's communicators were aborted by a failing device");
   if (c->rccl) {   // in place, on the context stream (one fp64 sum per exchange)
     const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->rccl, c->st);
     if (r != ncclSuccess) fail(c, SCS_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
@@ -578,6 +616,10 @@ void alloc_mspace(scs_ctx* c) {
   dfree_t(c, c->lqR);
   c->lqR = dalloc<double>(c, (size_t)LQ_NPART * LQ_G);
   if (!c->hscal) HCK(hipHostMalloc((void**)&c->hscal, 64 * sizeof(double), hipHostMallocDefault));
+  if (!c->hserr) {
+    HCK(hipHostMalloc((void**)&c->hserr, sizeof(int), hipHostMallocDefault));
+    *c->hserr = 0;
+  }
   if (!c->hloop) {   // written by kernels (lqn_post): fine-grained, device-mapped
     HCK(hipHostMalloc((void**)&c->hloop, 2 * LOOP_SLOTS * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
     HCK(hipHostGetDevicePointer((void**)&c->hloop_dev, c->hloop, 0));
@@ -1173,7 +1215,18 @@ double eval_reg_dev(scs_ctx* c, const double* xd) {
 
 // linesearch (utils.jl:27-35): Armijo with ρ = 0.5, c = 1e-4 and no cap.
 // obj(x) and grad_q(x) are evaluated once (the reference re-evaluates the
-// same deterministic values on every trial).
+// same deterministic values on every trial).  For the data losses the trial's
+// f(x + αd) is formed incrementally: A(x + αd) = Ax + α·Ad with
+// Ax from f(x)'s forward pass and ONE extra pass for Ad, then O(N) per trial (the
+// epilogue over z0 + α·zd) instead of a full pass over A per trial.  The values
+// equal the direct form to rounding (SCS_LS_INCR=0 keeps the direct form).
+bool ls_incremental(const scs_ctx* c) {
+  const char* e = std::getenv("SCS_LS_INCR");   // read per call (A/B within one process)
+  const bool off = e && e[0] == '0';
+  return !off && !c->generic && (c->loss == SCS_LOSS_LOGISTIC_MARGIN || c->loss == SCS_LOSS_LOGISTIC_CE ||
+                                 c->loss == SCS_LOSS_LEAST_SQUARES);
+}
+
 double line_search(scs_ctx* c, const double* xh, const double* xd, const double* dd) {
   const double f0 = eval_f_dev(c, xh, xd) + eval_reg_dev(c, xd);
   grad_q_dev(c, xh, xd, c->gqn);
@@ -1181,11 +1234,46 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
   d2h(c, c->hscal + 11, c->scal + 11, 1);
   sync(c);
   const double gd = c->hscal[11];
+  const bool incr = ls_incremental(c);
+  double* zd = nullptr;
+  double* pair = nullptr;
+  if (incr) {
+    // z0 = A x: f(x) above left it in c->z (forward with EPI_Z); A d once into zd
+    forward(c, xh, xd, 0);
+    if (c->lscap < 3 * c->Npad) {
+      dfree_t(c, c->lsbuf);
+      c->lsbuf = dalloc<double>(c, 3 * c->Npad);
+      c->lscap = 3 * c->Npad;
+    }
+    pair = c->lsbuf;
+    zd = c->lsbuf + 2 * c->Npad;
+    hipEvent_t e0;
+    tbegin(c, T_GEMV, &e0);
+    const int ns = matvec_n(c, dd, c->nsplit);
+    tend(c, T_GEMV, e0);
+    HCK(launch_epilogue(c->loss, c->ggn, EPI_Z, c->zpart, ns, c->Npad, c->y, c->N, c->Npad, c->scale, zd, nullptr,
+                        nullptr, nullptr, nullptr, c->valpart, c->st));
+    ensure_red(c);
+  }
   double alpha = 1.0;
   for (int trial = 0; trial < 100000; ++trial) {
     // the trial point lives on the device only (no host copy: it is keyed by a fresh tag)
     HCK(launch_trial_point(xd, dd, alpha, c->m, c->gtmp2, c->st));
-    const double ft = eval_f_dev(c, nullptr, c->gtmp2) + eval_reg_dev(c, c->gtmp2);
+    double ft;
+    if (incr) {
+      HCK(launch_ls_pair(c->z, zd, alpha, c->Npad, pair, c->st));
+      HCK(launch_epilogue(c->loss, c->ggn, EPI_VAL, pair, 2, c->Npad, c->y, c->N, c->Npad, c->scale, nullptr, nullptr,
+                          nullptr, nullptr, nullptr, c->valpart, c->st));
+      double* dst = sharded(c) ? c->red : c->scal + 14;
+      HCK(launch_sum_partials(c->valpart, c->nval, dst, c->st));
+      allreduce(c, c->red, 1);
+      if (sharded(c)) HCK(hipMemcpyAsync(c->scal + 14, c->red, sizeof(double), hipMemcpyDeviceToDevice, c->st));
+      d2h(c, c->hscal + 14, c->scal + 14, 1);
+      const double rg = eval_reg_dev(c, c->gtmp2);   // syncs: hscal[14] has landed too
+      ft = loss_scale_value(c, c->hscal[14]) + rg;
+    } else {
+      ft = eval_f_dev(c, nullptr, c->gtmp2) + eval_reg_dev(c, c->gtmp2);
+    }
     if (!(ft > f0 + 1e-4 * alpha * gd)) return alpha;
     alpha = 0.5 * alpha;
   }
@@ -1302,6 +1390,7 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false, bool force_qr 
     }
     if (info == 0) {
       HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, &c->caux, c->st));
+      solve_flag_copy(c);
       c->lu_fallback_used = false;
       tend(c, T_SOLVE, e0);
       return;
@@ -1323,6 +1412,7 @@ void solve_factored(scs_ctx* c, double* rhs, hipEvent_t e0) {
   }
   if (info == 0) {
     HCK(chol_solve(c->G, c->mpad, c->mpad, c->W, rhs, c->ysol, &c->caux, c->st));
+    solve_flag_copy(c);
     c->lu_fallback_used = false;
     tend(c, T_SOLVE, e0);
     return;
@@ -2127,13 +2217,7 @@ int scs_create(int device, void* stream, scs_ctx** out) {
     if (stream) {
       c->st = (hipStream_t)stream;
     } else {
-      // SCS_CHOL_BULK_PRIO=2: the context stream (the factor's chain) at the highest priority (A/B)
-      const char* pe = getenv("SCS_CHOL_BULK_PRIO");
-      int least = 0, greatest = 0;
-      if (pe && atoi(pe) >= 2 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-        HCK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, greatest));
-      else
-        HCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+      HCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
       c->own_stream = true;
     }
   });
@@ -2157,6 +2241,7 @@ int scs_destroy(scs_ctx* c) {
   if (c->rccl) (void)ncclCommDestroy(c->rccl);
   for (auto& a : c->allocs) (void)hipFree(a.p);
   if (c->hscal) (void)hipHostFree(c->hscal);
+  if (c->hserr) (void)hipHostFree(c->hserr);
   if (c->hring) (void)hipHostFree(c->hring);
   if (c->hloop) (void)hipHostFree(c->hloop);
   for (hipEvent_t e : c->loop_ev)
@@ -2323,6 +2408,8 @@ static void reset_data(scs_ctx* c) {
   dfree_t(c, c->ysol);
   dfree_t(c, c->trilist);
   dfree_t(c, c->cinfo);
+  dfree_t(c, c->lsbuf);
+  c->lscap = 0;
   chol_aux_free(&c->caux);
   clear_batches(c);
   free_view(c, c->gview);
@@ -3044,6 +3131,13 @@ int scs_set_batches(scs_ctx* c, const int64_t* rows, const int64_t* offsets, int
     if (!loc.empty())
       HCK(hipMemcpyAsync(c->brows, loc.data(), sizeof(int64_t) * loc.size(), hipMemcpyHostToDevice, c->st));
     sync(c);
+    // the exchange payload of the new list's sample-space batches (reduce_buffer_doubles)
+    if (c->own_red && c->red && reduce_buffer_doubles(c) > c->red_cap) {
+      dfree_t(c, c->red);
+      c->red_cap = 0;
+      c->own_red = false;
+      ensure_red(c);
+    }
   });
 }
 
@@ -3852,12 +3946,80 @@ int scs_sync(scs_ctx* c) {
 // sub-contexts at once -- one host thread per device, since the step's exchange is a collective
 // every device must enter.  Every sub-context computes the same replicated m-vectors with the same
 // bits, so outputs are device 0's.
+
+// One persistent host thread per device of a group (started by scs_create_multi, joined by
+// group_destroy).  A call posts one job per device and waits for all of them.
+struct scs_ctx::Workers {
+  struct Slot {
+    std::thread th;
+    std::function<void()> job;
+    bool has_job = false;
+  };
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  std::vector<Slot> slots;
+  int pending = 0;
+  bool quit = false;
+
+  explicit Workers(const std::vector<int>& devs) : slots(devs.size()) {
+    for (size_t i = 0; i < devs.size(); ++i)
+      slots[i].th = std::thread([this, i, d = devs[i]] {
+        (void)hipSetDevice(d);   // once: the thread drives this device for the group's lifetime
+        for (;;) {
+          std::function<void()> job;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_job.wait(lk, [&] { return quit || slots[i].has_job; });
+            if (!slots[i].has_job) return;   // quit
+            job = std::move(slots[i].job);
+            slots[i].has_job = false;
+          }
+          job();
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            --pending;
+          }
+          cv_done.notify_all();
+        }
+      });
+  }
+  // run jobs[i] on worker i, all at once; returns when every job has returned
+  void run(std::vector<std::function<void()>>& jobs) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = 0; i < slots.size(); ++i) {
+        slots[i].job = std::move(jobs[i]);
+        slots[i].has_job = true;
+      }
+      pending = (int)slots.size();
+    }
+    cv_job.notify_all();
+    std::unique_lock<std::mutex> lk(mu);
+    cv_done.wait(lk, [&] { return pending == 0; });
+  }
+  ~Workers() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit = true;
+    }
+    cv_job.notify_all();
+    for (auto& sl : slots)
+      if (sl.th.joinable()) sl.th.join();
+  }
+};
+
+scs_ctx::~scs_ctx() = default;
+
 namespace {
 
-// run f(sub, i) on every sub-context, one host thread each; the first failing device's code and
-// message become the group's.  A device that fails while the others may be waiting inside a
-// collective aborts the communicators after a grace period, so the call returns instead of
-// hanging; the group is then unusable (SCS_ERR_COMM) and must be destroyed.
+// run f(sub, i) on every sub-context, each on its device's worker thread; the first failing
+// device's code and message become the group's.  A device that fails while the others may be
+// waiting inside a collective aborts the communicators after a grace period (ncclCommAbort unblocks
+// them), so the call returns instead of hanging.  The abort only sets the shared flag and calls
+// ncclCommAbort: the sub-contexts' rccl handles are cleared after every worker has returned (no
+// other thread reads them then), and the flag stops any further RCCL call in the meantime.  The
+// group is then unusable (SCS_ERR_COMM) and must be destroyed.  Unverified on hardware beyond one
+// device (no multi-GPU box here): DESIGN.md §6.
 template <class F>
 int group_run(scs_ctx* g, F&& f) {
   if (g->group_broken) {
@@ -3868,22 +4030,25 @@ int group_run(scs_ctx* g, F&& f) {
   std::vector<int> rc(n, SCS_OK);
   std::atomic<int> done{0};
   std::atomic<bool> aborted{false};
-  std::vector<std::thread> th;
-  th.reserve(n);
+  std::vector<std::function<void()>> jobs((size_t)n);
   for (int i = 0; i < n; ++i)
-    th.emplace_back([&, i] {
+    jobs[(size_t)i] = [&, i] {
       scs_ctx* s = g->subs[i];
-      (void)hipSetDevice(s->dev);
       rc[i] = f(s, i);
       done.fetch_add(1);
       if (rc[i] == SCS_OK || n == 1) return;
       for (int t = 0; t < 500 && done.load() < n; ++t) std::this_thread::sleep_for(std::chrono::milliseconds(10));
-      if (done.load() < n && !aborted.exchange(true))
+      if (done.load() < n && !aborted.exchange(true)) {
+        g->comm_abort->store(true, std::memory_order_release);
         for (scs_ctx* o : g->subs)
-          if (o->rccl) (void)ncclCommAbort(o->rccl), o->rccl = nullptr;
-    });
-  for (auto& t : th) t.join();
-  if (aborted.load()) g->group_broken = true;
+          if (o->rccl) (void)ncclCommAbort(o->rccl);
+      }
+    };
+  g->workers->run(jobs);
+  if (aborted.load()) {
+    g->group_broken = true;
+    for (scs_ctx* o : g->subs) o->rccl = nullptr;   // aborted (freed) by ncclCommAbort
+  }
   for (int i = 0; i < n; ++i)
     if (rc[i] != SCS_OK) {
       g->err = "device " + std::to_string(g->subs[i]->dev) + ": " + g->subs[i]->err;
@@ -3926,11 +4091,14 @@ int scs_create_multi(const int* devs, int ndev, scs_ctx** out) {
     delete g;
     return SCS_ERR_COMM;
   }
+  g->comm_abort = std::make_shared<std::atomic<bool>>(false);
   for (int i = 0; i < ndev; ++i) {
     g->subs[i]->rccl = comms[(size_t)i];
     g->subs[i]->rank = i;
     g->subs[i]->nranks = ndev;
+    g->subs[i]->comm_abort = g->comm_abort;
   }
+  g->workers.reset(new scs_ctx::Workers(std::vector<int>(devs, devs + ndev)));
   g->dev = devs[0];
   g->st = g->subs[0]->st;
   *out = g;
@@ -3948,6 +4116,7 @@ int scs_group_size(scs_ctx* c, int* ndev) {
 namespace {
 
 int group_destroy(scs_ctx* g) {
+  g->workers.reset();   // joins the device threads
   for (scs_ctx* s : g->subs) scs_destroy(s);
   g->subs.clear();
   delete g;

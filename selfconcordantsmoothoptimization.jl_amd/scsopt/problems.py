@@ -444,6 +444,8 @@ class Problem:
         off[1:] = np.cumsum([r.size for r in rs])
         self.ctx.check(_lib.lib.scs_set_batches(self.ctx.h, rows.ctypes.data_as(_lib.c_i64p),
                                                 off.ctypes.data_as(_lib.c_i64p), len(rs)))
+        if self.comm is not None and self.comm.active:   # the exchange payload may have grown
+            self.comm.bind_buffer(self.ctx)
 
     def select_batch(self, b=-1):
         """The registered batch the following step! calls see as As, ys (-1: the full data)."""

@@ -98,6 +98,8 @@ class Comm:
         from . import _lib
         n = C.c_int64()
         ctx.check(_lib.lib.scs_reduce_buffer_size(ctx.h, C.byref(n)))
+        if self.buf is not None and self.buf.numel() >= int(n.value):
+            return   # still large enough (a new batch list may need more: Problem.set_batches re-binds)
         dev = torch.device("cuda", ctx.device) if self.device is None else self.device
         self.buf = torch.zeros(int(n.value), dtype=torch.float64, device=dev)
         ctx._keep.append(self.buf)

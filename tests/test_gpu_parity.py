@@ -283,6 +283,30 @@ def test_nscore_linesearch():
     np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
 
 
+@pytest.mark.parametrize("method,loss,kind", [("nscore", "logistic_margin", 2), ("ggn", "logistic_ce", 1),
+                                              ("lqn", "least_squares", 3)])
+def test_incremental_linesearch_same_decisions(method, loss, kind, monkeypatch):
+    """The line search's trial f(x + αd) from Ax + α·Ad (one extra pass, O(N) per trial) takes the
+    same accept / reject decisions as the direct form (a pass over A per trial, SCS_LS_INCR=0):
+    the same step sizes, so bitwise the same iterates and histories (utils.jl:27-35)."""
+    N, m = 1536, 64
+    x0 = np.random.default_rng(6).standard_normal(m) * 1.5
+    f = getattr(losses, loss)(1.0 / N)
+    out = losses.sigmoid_ce(1.0 / N) if method == "ggn" else None
+    meth = {"nscore": scsopt.ProxNSCORE, "ggn": scsopt.ProxGGNSCORE, "lqn": scsopt.ProxLQNSCORE}[method]
+    p = scsopt.Problem.synthetic(N, m, x0, f, 1e-3, kind=kind, seed=16, out_fn=out)
+    if method == "lqn":
+        p.L = 4.0   # ss_type 3 with L set: the line search (prox-L-BFGS-SCORE.jl:112)
+    runs = []
+    for incr in ("1", "0"):
+        monkeypatch.setenv("SCS_LS_INCR", incr)
+        runs.append(scsopt.iterate(meth(ss_type=3), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=10,
+                                   verbose=0))
+    a, b = runs
+    assert a.obj == b.obj and a.pri_res_norm == b.pri_res_norm and a.epochs == b.epochs
+    assert np.array_equal(bits(a.x), bits(b.x))
+
+
 def test_group_lasso_ggn():
     """C4 in miniature: least squares + sparse-group lasso, ProxGGNSCORE + PHuberSmootherGL."""
     N, m, gs = 2048, 128, 16
