@@ -348,6 +348,11 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
       if (wv == 0) {
         diag_trail_tile(su, o, 0, lane);
         PROF_MARK_T(36 + kb, 0);
+        // tile 0's elements go from the lanes that updated them to the lanes that factor them (lane
+        // 4c + q reads rows 4q.. of column c): an intra-wave LDS hand-off with no barrier, so order it
+        // for the compiler (instruction-free wavefront fence + wave barrier, as in diag_factor16)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         diag_factor16(su, srinv, urow, o + SB, k, info, tid);
         PROF_MARK_T(43 + kb, 0);
 #ifndef CHOL_NO_W0CLAIM

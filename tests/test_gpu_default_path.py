@@ -116,6 +116,27 @@ def test_c4_shape_solve_backward_error(mode, clean_env):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("m", [16384, 8192])
+def test_c3_c2_shape_cholesky_backward_error(m, clean_env):
+    """The m = 16384 (C3) and m = 8192 (C2) default factor + one-launch solves (mode 0) -- the sizes
+    where round 3 saw a wrong-result race (the diagonal kernel's intra-wave LDS exchange, fenced
+    since; DESIGN §3 lists every intra-wave hand-off) -- by the backward error through the
+    independent GEMV kernels: ||r|| <= 1e-12 ||G|| ||x||, on two right-hand sides."""
+    N = m + 2048
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=m + 1)
+    rng = np.random.default_rng(m)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-2
+    gn = _norm2_est(p, w, d, m)
+    for _ in range(2):
+        rhs = rng.standard_normal(m)
+        x, used_lu = p.solve_eval(w, d, rhs, mode=0)
+        assert not used_lu
+        r = _gemv_residual(p, w, d, x, rhs)
+        assert np.linalg.norm(r) <= 1e-12 * gn * np.linalg.norm(x), (np.linalg.norm(r), gn, np.linalg.norm(x))
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("f32", [False, True])
 def test_c5_shape_lqn_sparse(f32, clean_env):
     """C5 with N = 2^17 (m = 2^16 as configured): ProxLQNSCORE(mem 20) + indbox + PHuberSmootherIndBox(0.6),
