@@ -324,6 +324,9 @@ def main():
     ap.add_argument("--N", type=int, default=0, help="override the config's N")
     ap.add_argument("--m", type=int, default=0, help="override the config's m")
     ap.add_argument("--f32", action="store_true", help="c5: fp32-stored sparse values (fp64 accumulation)")
+    ap.add_argument("--f32-compute", action="store_true",
+                    help="c5: fp32-stored values AND fp32 arithmetic in the sparse products and the L-BFGS two-loop "
+                         "(scs_set_compute_f32; the compute arm of the BASELINE configs[4] study)")
     ap.add_argument("--gram-cache", action="store_true",
                     help="c4: reuse the x-independent AᵀQA of least squares across steps (scs_set_gram_cache; "
                          "reported separately -- the reference recomputes it every step)")
@@ -408,7 +411,13 @@ def main():
                              f"{plan['total'] * sharing / GIB:.1f} GiB on GPU {dev} ({plan_text(plan)}; "
                              f"{plan['rows_per_rank']} rows per rank), {free / GIB:.1f} GiB free: "
                              f"use more GPUs (--gpus) or a smaller --N")
+    if args.f32_compute:
+        if not cfg.get("sparse") or cfg["method"] != "lqn":
+            raise SystemExit("--f32-compute applies to the sparse ProxLQNSCORE config (c5)")
+        args.f32 = True
     model, hmu, method = build_problem(cfg, N, m, comm, dev, f32=args.f32, devices=devices)
+    if args.f32_compute:
+        model.set_compute_f32(True)
     reg = cfg["reg"]
     if args.gram_cache:
         if cfg["loss"] != "least_squares" or cfg["method"] == "lqn":
@@ -473,7 +482,9 @@ def main():
             "value": value, "unit": "iterations/s", "n_gpus": args.gpus if single else world, "steps": steps,
             "warmup": warmup,
             "ms_per_step": ms_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": ("f64 (fp32-stored A values)" if args.f32 else "f64"), "data": "synthetic (on-device counter RNG: A ~ N(0,1)/sqrt(m), y from a sparse x_true)",
+            "dtype": ("f32 (fp32-stored A values; fp32 arithmetic in the sparse products and the two-loop, "
+                      "f / eta / step / prox in f64)" if args.f32_compute else
+                      "f64 (fp32-stored A values)" if args.f32 else "f64"), "data": "synthetic (on-device counter RNG: A ~ N(0,1)/sqrt(m), y from a sparse x_true)",
             "config": {"workload": cfg["workload"], "N": N, "m": m, "lambda": model.λ, "mu": hmu.mu,
                        "method": type(method).__name__, "ss_type": method.ss_type,
                        "parallelism": (f"row-shard x{args.gpus} (one process, scs_create_multi)" if single
@@ -543,9 +554,11 @@ def main():
                                 "bytes_per_launch": per_launch}
             line["config"]["nnz"] = nnz
             if args.f32:
-                # the full-size fp32-vs-fp64 study of this configuration (tools/c5_tolerance.py): the fp32
-                # arm stores A's values in fp32 and computes in fp64 -- a storage study
-                tol = os.path.join(ROOT, "profiles", "r03", "c5", "tolerance.json")
+                # the full-size fp32-vs-fp64 studies of this configuration (tools/c5_tolerance.py): the storage
+                # arm (r03) stores A's values in fp32 and computes in fp64; the compute arm (r04) also runs
+                # the sparse products and the two-loop in fp32 arithmetic
+                tol = os.path.join(ROOT, "profiles", *(("r04", "c5", "tolerance_f32compute.json")
+                                                       if args.f32_compute else ("r03", "c5", "tolerance.json")))
                 if os.path.exists(tol) and N == 1 << 20 and m == 1 << 16:
                     with open(tol) as f:
                         ts = json.load(f)

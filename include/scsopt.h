@@ -254,6 +254,11 @@ int scs_set_reg(scs_ctx* ctx, int reg_kind, const double* lam, int nlam,
  * only the gradient is all-reduced.  Bit-identical results.  Costs one more
  * m_pad² fp64 buffer.                                                        */
 int scs_set_gram_cache(scs_ctx* ctx, int on);
+/* The compute arm of the fp32-vs-fp64 tolerance study (BASELINE configs[4]): on = 1 runs the
+ * sparse products of fp32-stored values (scs_set_sparse val_f32 = 1) and the L-BFGS two-loop
+ * recursion in fp32 ARITHMETIC (fp32 products, fp32 accumulation and dots, results widened to fp64);
+ * everything else (f / η / step / prox / the m x m solves) stays fp64.  0 (default): fp64.      */
+int scs_set_compute_f32(scs_ctx* ctx, int on);
 /* The m x m (and the GGN sample-space (N+1)²) systems' solver.  SCS_SOLVER_DEFAULT: blocked
  * Cholesky on MFMA with the LU fallback (sample space: LU) -- equal to the reference's solves to
  * O(cond·eps).  SCS_SOLVER_REFERENCE: the reference's own factorizations -- Householder QR

@@ -38,7 +38,8 @@ __device__ __forceinline__ double jl_sign(double x) {
 
 // ---- deterministic reductions ---------------------------------------------
 // Butterfly over the 64 lanes; every lane ends with the same fixed-order sum.
-__device__ __forceinline__ double wave_sum(double v) {
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -46,21 +47,23 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // Block-wide sum in a fixed order (wave partials summed by thread 0 in wave
 // order).  `sh` must hold NT/64 doubles.  Result broadcast to all threads.
-template <int NT>
-__device__ __forceinline__ double block_sum(double v, double* sh) {
-  v = wave_sum(v);
+// T = float: the same fixed order in fp32 arithmetic (the partials kept in the double scratch,
+// exactly representable).
+template <int NT, typename T = double>
+__device__ __forceinline__ T block_sum(T v, double* sh) {
+  v = wave_sum<T>(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   __syncthreads();
-  if (l == 0) sh[w] = v;
+  if (l == 0) sh[w] = (double)v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    double r = 0.0;
+    T r = 0;
 #pragma unroll
-    for (int i = 0; i < NT / 64; ++i) r += sh[i];
-    sh[0] = r;
+    for (int i = 0; i < NT / 64; ++i) r += (T)sh[i];
+    sh[0] = (double)r;
   }
   __syncthreads();
-  const double r = sh[0];
+  const T r = (T)sh[0];
   __syncthreads();
   return r;
 }

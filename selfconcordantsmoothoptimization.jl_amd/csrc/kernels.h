@@ -267,9 +267,10 @@ hipError_t launch_bb_step(const double* x, const double* xp, const double* g, co
 // ring size and H0 are read on the device (scs_iterate's pipelined loop) and k is only their upper bound.
 constexpr int64_t TWO_LOOP_SINGLE_MAX = 16384;
 constexpr int TWO_LOOP_MAX_WG = 256;
+// f32 = 1: fp32 arithmetic (the compute arm of the C5 tolerance study, scs_set_compute_f32)
 hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
                            const double* g, int64_t m, double* q, double* d, double* ab, double* work, int kcap,
-                           const int* kp, const double* H0p, hipStream_t st);
+                           const int* kp, const double* H0p, hipStream_t st, int f32 = 0);
 hipError_t launch_lbfgs_update(const double* dh, const double* gq_new, const double* gq, int64_t m, double* Sslot,
                                double* Yslot, double* scal, double* part, hipStream_t st);
 hipError_t launch_diag_add(double* G, int64_t ldg, int64_t m, double lam, const double* Hr, hipStream_t st);
@@ -346,6 +347,7 @@ int spmv_blk_shift(int64_t ncols);
 int spmv_pad_index();   // padding index of the blocked layouts (the SpMV's zero slot)
 int spmv_slot_width(int f32);   // segments padded to whole slots of 4 (fp64) / 8 (fp32) entries
 // segments padded to whole slots (blk_pad), padding index spmv_pad_index(), value 0
+// f32: 0 fp64 values, 1 fp32-stored values (fp64 arithmetic), 2 fp32-stored values with fp32 arithmetic
 const char* spmv_kernel_name(int f32);
 hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
                            int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,

@@ -106,6 +106,9 @@ struct scs_ctx {
   // sparse A: CSR (rows) + CSC copy (columns), values fp64 or fp32
   bool sparse = false;
   int sp_f32 = 0;
+  // scs_set_compute_f32: fp32 ARITHMETIC in the sparse products (fp32-stored values) and the L-BFGS
+  // two-loop -- the compute arm of BASELINE configs[4]'s fp32-vs-fp64 study; 0 (fp64) by default
+  int f32c = 0;
   int64_t nnz = 0;
   int64_t *rowptr = nullptr, *colptr = nullptr;
   int *colidx = nullptr, *rowidx = nullptr;
@@ -993,8 +996,9 @@ double loss_scale_value(scs_ctx* c, double s) {
 int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
   if (c->sparse) {
     const auto& B = c->bcsr;
-    HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, c->sp_f32, xd, c->N, c->m, B.shift, c->nnz, c->zpart, c->Npad, c->st));
-    c->prod_kname = spmv_kernel_name(c->sp_f32);
+    const int vk = c->sp_f32 ? (c->f32c ? 2 : 1) : 0;
+    HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, vk, xd, c->N, c->m, B.shift, c->nnz, c->zpart, c->Npad, c->st));
+    c->prod_kname = spmv_kernel_name(vk);
     return B.nblk;
   }
   HCK(launch_gemv_n(c->A, c->nstage, c->Npad, c->mpad, xd, nsplit, c->zpart, c->Npad, c->st));
@@ -1005,7 +1009,8 @@ int matvec_n(scs_ctx* c, const double* xd, int nsplit) {
 int matvec_t_part(scs_ctx* c, const double* v) {
   if (c->sparse) {
     const auto& B = c->bcsc;
-    HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, c->sp_f32, v, c->m, c->N, B.shift, c->nnz, c->tpart, c->mpad, c->st));
+    const int vk = c->sp_f32 ? (c->f32c ? 2 : 1) : 0;
+    HCK(launch_spmv_blk(B.ptr, B.lidx, B.val, vk, v, c->m, c->N, B.shift, c->nnz, c->tpart, c->mpad, c->st));
     return B.nblk;
   }
   HCK(launch_gemv_t(c->A, c->nstage, c->Npad, c->m, c->mpad, v, c->tpart, c->st));
@@ -2098,7 +2103,7 @@ void step_lqn(scs_ctx* c, const double* xh, const double* xph, int64_t iter, dou
     std::memcpy(c->hring, c->ring.data(), sizeof(int) * k);   // pinned: a truly asynchronous upload
     HCK(hipMemcpyAsync(c->d_order, c->hring, sizeof(int) * k, hipMemcpyHostToDevice, c->st));
     HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, k, c->H0, c->gq, m, c->q, c->d, c->ab, c->tlwork, c->mem,
-                        nullptr, nullptr, c->st));
+                        nullptr, nullptr, c->st, c->f32c));
   }
   double step = 0.0;
   const double* step_dev = nullptr;
@@ -2951,6 +2956,15 @@ int scs_set_reg(scs_ctx* c, int reg, const double* lam, int nlam, const double* 
   });
 }
 
+int scs_set_compute_f32(scs_ctx* c, int on) {
+  if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_compute_f32(s_, on); });
+  return guarded(c, [&] {
+    sync(c);
+    c->f32c = on ? 1 : 0;
+    invalidate_caches(c);
+  });
+}
+
 int scs_set_solver(scs_ctx* c, int kind) {
   if (is_group(c)) return group_run(c, [&](scs_ctx* s_, int) { return scs_set_solver(s_, kind); });
   return guarded(c, [&] {
@@ -3437,7 +3451,7 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
           tbegin(c, T_STEP, &e0);
           if (kmax > 0)
             HCK(launch_two_loop(c->S, c->Yv, c->mpad, c->d_order, kmax, 1.0, c->gq, m, c->q, c->d, c->ab, c->tlwork,
-                                mem, c->d_order + mem + 1, c->scal + H0_SLOT, c->st));
+                                mem, c->d_order + mem + 1, c->scal + H0_SLOT, c->st, c->f32c));
           HCK(launch_lqn_tail(c->x, kmax > 0 ? c->d : c->gq, kmax > 0 ? 0 : 1, m, Mg, step, prox_args(c), c->hinv,
                               c->xn, c->dxv, c->q, c->lqR, c->scal, c->st));
           if (tst) ftest_enqueue(c, c->xn);   // -> scal[TF_SLOT], carried to the host by lqn_post_final

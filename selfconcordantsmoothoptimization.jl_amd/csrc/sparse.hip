@@ -204,6 +204,113 @@ __global__ __launch_bounds__(SPB_THREADS) void spmv_blk_kernel(const int64_t* __
   if (lane < nrw) out[(int64_t)b * ldo + rw0 + lane] = acc;
 }
 
+// fp32-ARITHMETIC product (the compute arm of the C5 tolerance study, BASELINE configs[4];
+// scs_set_compute_f32): fp32-stored values, the x slice staged in LDS as fp32, every product, lane
+// partial, scan step and row accumulation in fp32 (v_fma_f32 / 32-bit DPP), the row sum widened to
+// fp64 on the store.  The window / row bookkeeping is spmv_blk_kernel's, so only the arithmetic type
+// differs.  Fixed order per row: bitwise run to run.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF, true));
+}
+__device__ __forceinline__ float seg_scan64_f32(float p, int lane, int rs) {
+  const int l16 = lane & 15;
+  float u;
+  u = dpp_f32<0x111, 0xF>(p);
+  if (l16 >= 1 && lane - 1 >= rs) p += u;
+  u = dpp_f32<0x112, 0xF>(p);
+  if (l16 >= 2 && lane - 2 >= rs) p += u;
+  u = dpp_f32<0x114, 0xF>(p);
+  if (l16 >= 4 && lane - 4 >= rs) p += u;
+  u = dpp_f32<0x118, 0xF>(p);
+  if (l16 >= 8 && lane - 8 >= rs) p += u;
+  u = dpp_f32<0x142, 0xA>(p);   // row_bcast:15 -> rows 1, 3
+  if ((lane & 16) && (lane & ~15) - 1 >= rs) p += u;
+  u = dpp_f32<0x143, 0xC>(p);   // row_bcast:31 -> rows 2, 3
+  if ((lane & 32) && 31 >= rs) p += u;
+  return p;
+}
+
+struct SpmvWin32 {
+  uint64_t id[2];   // 8 16-bit local indices
+  float v[8];
+};
+__device__ __forceinline__ void win_load32(SpmvWin32& w, const uint16_t* __restrict__ lidx,
+                                           const float* __restrict__ val, int64_t slot) {
+  const v2u64 t = *(const v2u64*)(lidx + 8 * slot);
+  w.id[0] = t[0];
+  w.id[1] = t[1];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const v4f a = *(const v4f*)(val + 8 * slot + 4 * k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w.v[4 * k + q] = a[q];
+  }
+}
+
+__global__ __launch_bounds__(SPB_THREADS) void spmv_blk32_kernel(const int64_t* __restrict__ ptr,
+                                                                 const uint16_t* __restrict__ lidx,
+                                                                 const float* __restrict__ val,
+                                                                 const double* __restrict__ x, int64_t nrows,
+                                                                 int64_t ncols, int shift, double* __restrict__ out,
+                                                                 int64_t ldo) {
+  constexpr int SH = 3;   // 8-entry slots (the fp32 layout)
+  __shared__ float xs[SPB_PADIDX + 1];
+  const int b = blockIdx.y;
+  const int64_t c0 = (int64_t)b << shift;
+  const int nb = (int)min((int64_t)1 << shift, ncols - c0);
+  {
+    constexpr int PER = (1 << SPB_MAXSHIFT) / SPB_THREADS;
+    float t[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * SPB_THREADS;
+      t[k] = (i < nb) ? (float)x[c0 + i] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) xs[threadIdx.x + k * SPB_THREADS] = t[k];
+    if (threadIdx.x == 0) xs[SPB_PADIDX] = 0.0f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t* pb = ptr + (int64_t)b * nrows;
+  const int64_t rw0 = (int64_t)blockIdx.x * SPB_ROWS + (int64_t)wv * 64;
+  const int nrw = (int)max((int64_t)0, min((int64_t)64, nrows - rw0));
+  if (nrw == 0) return;
+  const int64_t sb = pb[rw0] >> SH;
+  const int total = (int)((pb[rw0 + nrw] >> SH) - sb);
+  const int st = lane < nrw ? (int)((pb[rw0 + lane] >> SH) - sb) : total;
+  const int stn = __shfl(st, min(lane + 1, 63), 64);
+  const int en = lane + 1 < nrw ? stn : total;
+  const int nwin = (total + 63) >> 6;
+  SpmvWin32 nxt;
+  win_load32(nxt, lidx, val, sb + max(min(lane, total - 1), 0));
+  float acc = 0.0f;
+  int cur = 0;
+  for (int t = 0; t < nwin; ++t) {
+    const SpmvWin32 w = nxt;
+    if (t + 1 < nwin) win_load32(nxt, lidx, val, sb + min(64 * (t + 1) + lane, total - 1));
+    const int base = 64 * t, slot = base + lane;
+    float p = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) p = fmaf(w.v[e], xs[(int)((w.id[e / 4] >> (16 * (e & 3))) & 0xFFFF)], p);
+    if (slot >= total) p = 0.0f;
+    int r = cur, k = cur + 1;
+    while (k < nrw) {
+      const int sk = __builtin_amdgcn_readlane(st, k);
+      if (sk > base + 64) break;
+      r += (slot >= sk) ? 1 : 0;
+      ++k;
+    }
+    cur = k - 1;
+    const int rs = __shfl(st, r, 64) - base;
+    p = seg_scan64_f32(p, lane, rs);
+    const float pt = __shfl(p, max(min(en - base - 1, 63), 0), 64);
+    if (st < base + 64 && en > base && st < en) acc += pt;
+  }
+  if (lane < nrw) out[(int64_t)b * ldo + rw0 + lane] = (double)acc;
+}
+
 int spmv_pad_index() { return SPB_PADIDX; }
 
 int spmv_blk_shift(int64_t ncols) {
@@ -212,7 +319,9 @@ int spmv_blk_shift(int64_t ncols) {
   return s;
 }
 
-const char* spmv_kernel_name(int f32) { return f32 ? "spmv_blk_kernel<float, 8>" : "spmv_blk_kernel<double, 4>"; }
+const char* spmv_kernel_name(int f32) {
+  return f32 == 2 ? "spmv_blk32_kernel" : f32 ? "spmv_blk_kernel<float, 8>" : "spmv_blk_kernel<double, 4>";
+}
 
 hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void* val, int f32, const double* x,
                            int64_t nrows, int64_t ncols, int shift, int64_t nnz, double* out, int64_t ldo,
@@ -221,7 +330,10 @@ hipError_t launch_spmv_blk(const int64_t* ptr, const uint16_t* lidx, const void*
   const int nblk = (int)ceil_div(ncols, (int64_t)1 << shift);
   // one 1024-row chunk per workgroup; fp64 in 4-entry slots, fp32 in 8-entry slots
   const dim3 grid((unsigned)ceil_div(nrows, SPB_ROWS), (unsigned)nblk);
-  if (f32)
+  if (f32 == 2)   // fp32-stored values, fp32 arithmetic (the compute arm)
+    hipLaunchKernelGGL(spmv_blk32_kernel, grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val, x, nrows,
+                       ncols, shift, out, ldo);
+  else if (f32)
     hipLaunchKernelGGL((spmv_blk_kernel<float, 8>), grid, dim3(SPB_THREADS), 0, st, ptr, lidx, (const float*)val, x,
                        nrows, ncols, shift, out, ldo);
   else

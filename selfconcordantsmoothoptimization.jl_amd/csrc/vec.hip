@@ -445,48 +445,52 @@ __global__ __launch_bounds__(VB) void bb_step_kernel(const double* __restrict__ 
 // Writes d = -r.  Dots are recomputed exactly as the reference does.
 // kp / H0p (device ring, scs_iterate's pipelined loop): k = *kp and H0 = *H0p instead of the
 // arguments; k = 0 gives d = -g (launch_neg's bits: the reference's `d = -∇q` branch).
+// T = float: the fp32-arithmetic arm (scs_set_compute_f32; BASELINE configs[4]): every operand
+// rounded to fp32 on load, dots / axpys / α, ρ, β in fp32, results stored widened (exact) in the
+// fp64 buffers.  T = double is the default path, unchanged.
+template <typename T>
 __global__ __launch_bounds__(VB) void two_loop_kernel(const double* __restrict__ S, const double* __restrict__ Y,
                                                       int64_t ld, const int* __restrict__ order,
                                                       const int* __restrict__ kp, int k, const double* __restrict__ H0p,
-                                                      double H0, const double* __restrict__ g, int64_t m,
+                                                      double H0d, const double* __restrict__ g, int64_t m,
                                                       double* __restrict__ q, double* __restrict__ dout,
                                                       double* __restrict__ ab /*[2*k]*/) {
   __shared__ double sh[VB / 64];
   if (kp) k = *kp;
-  if (H0p) H0 = *H0p;
+  const T H0 = (T)(H0p ? *H0p : H0d);
   if (k == 0) {
-    for (int64_t i = threadIdx.x; i < m; i += VB) dout[i] = -g[i];
+    for (int64_t i = threadIdx.x; i < m; i += VB) dout[i] = -(double)(T)g[i];
     return;
   }
-  for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = g[i];
+  for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = (double)(T)g[i];
   __syncthreads();
   for (int t = k - 1; t >= 0; --t) {           // newest -> oldest
     const double* s = S + (int64_t)order[t] * ld;
     const double* y = Y + (int64_t)order[t] * ld;
-    double ys = 0.0, sq = 0.0;
+    T ys = 0, sq = 0;
     for (int64_t i = threadIdx.x; i < m; i += VB) {
-      ys += y[i] * s[i];
-      sq += s[i] * q[i];
+      ys += (T)y[i] * (T)s[i];
+      sq += (T)s[i] * (T)q[i];
     }
-    ys = block_sum<VB>(ys, sh);
-    sq = block_sum<VB>(sq, sh);
-    const double rho = 1.0 / ys;
-    const double al = rho * sq;
-    for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = q[i] - al * y[i];
-    if (threadIdx.x == 0) { ab[2 * t] = al; ab[2 * t + 1] = rho; }
+    ys = block_sum<VB, T>(ys, sh);
+    sq = block_sum<VB, T>(sq, sh);
+    const T rho = (T)1 / ys;
+    const T al = rho * sq;
+    for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = (double)((T)q[i] - al * (T)y[i]);
+    if (threadIdx.x == 0) { ab[2 * t] = (double)al; ab[2 * t + 1] = (double)rho; }
     __syncthreads();
   }
-  for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = H0 * q[i];   // r = H0*q (in place)
+  for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = (double)(H0 * (T)q[i]);   // r = H0*q (in place)
   __syncthreads();
   for (int t = 0; t < k; ++t) {                // oldest -> newest
     const double* s = S + (int64_t)order[t] * ld;
     const double* y = Y + (int64_t)order[t] * ld;
-    double yr = 0.0;
-    for (int64_t i = threadIdx.x; i < m; i += VB) yr += y[i] * q[i];
-    yr = block_sum<VB>(yr, sh);
-    const double al = ab[2 * t], rho = ab[2 * t + 1];
-    const double beta = rho * yr;
-    for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = q[i] + s[i] * (al - beta);
+    T yr = 0;
+    for (int64_t i = threadIdx.x; i < m; i += VB) yr += (T)y[i] * (T)q[i];
+    yr = block_sum<VB, T>(yr, sh);
+    const T al = (T)ab[2 * t], rho = (T)ab[2 * t + 1];
+    const T beta = rho * yr;
+    for (int64_t i = threadIdx.x; i < m; i += VB) q[i] = (double)((T)q[i] + (T)s[i] * (al - beta));
     __syncthreads();
   }
   for (int64_t i = threadIdx.x; i < m; i += VB) dout[i] = -q[i];
@@ -498,11 +502,12 @@ __global__ __launch_bounds__(VB) void two_loop_kernel(const double* __restrict__
 // exactly).  One launch per recursion step; each launch applies its axpy to
 // its chunk and immediately forms the next step's partial dot on the updated
 // chunk, so q / r are read once per step.  The chunk partition (not the
-// single-workgroup stride) sets the summation order of the dots.
+// single-workgroup stride) sets the summation order of the dots.  T as above.
 constexpr int TLB = 256;
-__device__ __forceinline__ double sum_parts(const double* __restrict__ p, int G) {
-  double s = 0.0;
-  for (int b = 0; b < G; ++b) s += p[b];
+template <typename T>
+__device__ __forceinline__ T sum_parts(const double* __restrict__ p, int G) {
+  T s = 0;
+  for (int b = 0; b < G; ++b) s += (T)p[b];
   return s;
 }
 
@@ -511,13 +516,14 @@ __device__ __forceinline__ double sum_parts(const double* __restrict__ p, int G)
 // launches return at once.  Partial dots live in parity buffers keyed by t (work: pys [k][G],
 // then first-loop P[0], P[1] and second-loop P[2], P[3], G each), not by launch order.
 // Bodies of the launches (chunk b of G).
+template <typename T>
 __device__ __forceinline__ void tl_init_body(const double* __restrict__ S, const double* __restrict__ Y, int64_t ld,
                                              const int* __restrict__ order, int k, const double* __restrict__ g,
                                              int64_t m, int64_t C, double* __restrict__ work, int kcap,
                                              double* __restrict__ dout, int b, int G, double* sh) {
   const int64_t i0 = b * C, i1 = min(m, i0 + C);
   if (k == 0) {   // d = -∇q
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) dout[i] = -g[i];
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) dout[i] = -(double)(T)g[i];
     return;
   }
   double* pys = work;
@@ -525,22 +531,23 @@ __device__ __forceinline__ void tl_init_body(const double* __restrict__ S, const
   for (int t = 0; t < k; ++t) {
     const double* s = S + (int64_t)order[t] * ld;
     const double* y = Y + (int64_t)order[t] * ld;
-    double v = 0.0;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) v += y[i] * s[i];
-    v = block_sum<TLB>(v, sh);
-    if (threadIdx.x == 0) pys[t * G + b] = v;
+    T v = 0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) v += (T)y[i] * (T)s[i];
+    v = block_sum<TLB, T>(v, sh);
+    if (threadIdx.x == 0) pys[t * G + b] = (double)v;
   }
   const double* s = S + (int64_t)order[k - 1] * ld;
-  double v = 0.0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) v += s[i] * g[i];
-  v = block_sum<TLB>(v, sh);
-  if (threadIdx.x == 0) psq[b] = v;
+  T v = 0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) v += (T)s[i] * (T)g[i];
+  v = block_sum<TLB, T>(v, sh);
+  if (threadIdx.x == 0) psq[b] = (double)v;
 }
 
 // first loop, step t (newest -> oldest): q -= α_t y_t; partial s_{t-1}·q (or, at t = 0,
 // r = H0 q and the partial y_0·r of the second loop)
+template <typename T>
 __device__ __forceinline__ void tl_first_body(const double* __restrict__ S, const double* __restrict__ Y, int64_t ld,
-                                              const int* __restrict__ order, int k, int t, double H0, int64_t m,
+                                              const int* __restrict__ order, int k, int t, T H0, int64_t m,
                                               int64_t C, const double* __restrict__ g, double* __restrict__ q,
                                               double* __restrict__ work, int kcap, double* __restrict__ ab, int b,
                                               int G, double* sh) {
@@ -548,27 +555,28 @@ __device__ __forceinline__ void tl_first_body(const double* __restrict__ S, cons
   const double* pys = work;
   const double* pin = work + ((int64_t)kcap + (t & 1)) * G;
   double* pout = work + ((int64_t)kcap + (t > 0 ? ((t - 1) & 1) : 2)) * G;
-  const double ys = sum_parts(pys + t * G, G), sq = sum_parts(pin, G);
-  const double rho = 1.0 / ys;
-  const double al = rho * sq;
+  const T ys = sum_parts<T>(pys + t * G, G), sq = sum_parts<T>(pin, G);
+  const T rho = (T)1 / ys;
+  const T al = rho * sq;
   const double* y = Y + (int64_t)order[t] * ld;
   const double* sn = (t > 0) ? S + (int64_t)order[t - 1] * ld : Y + (int64_t)order[0] * ld;
   const double* qin = (t == k - 1) ? g : q;   // q = ∇q before the first step
-  double v = 0.0;
+  T v = 0;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) {
-    double qi = qin[i] - al * y[i];
+    T qi = (T)qin[i] - al * (T)y[i];
     if (t == 0) qi = H0 * qi;
-    q[i] = qi;
-    v += sn[i] * qi;
+    q[i] = (double)qi;
+    v += (T)sn[i] * qi;
   }
-  v = block_sum<TLB>(v, sh);
+  v = block_sum<TLB, T>(v, sh);
   if (threadIdx.x == 0) {
-    pout[b] = v;
-    if (b == 0) { ab[2 * t] = al; ab[2 * t + 1] = rho; }
+    pout[b] = (double)v;
+    if (b == 0) { ab[2 * t] = (double)al; ab[2 * t + 1] = (double)rho; }
   }
 }
 
 // second loop, step t (oldest -> newest): r += s_t (α_t − β_t); partial y_{t+1}·r, or d = −r at the end
+template <typename T>
 __device__ __forceinline__ void tl_second_body(const double* __restrict__ S, const double* __restrict__ Y, int64_t ld,
                                                const int* __restrict__ order, int k, int t, int64_t m, int64_t C,
                                                double* __restrict__ r, double* __restrict__ work, int kcap,
@@ -577,25 +585,26 @@ __device__ __forceinline__ void tl_second_body(const double* __restrict__ S, con
   const int64_t i0 = b * C, i1 = min(m, i0 + C);
   const double* pin = work + ((int64_t)kcap + 2 + (t & 1)) * G;
   double* pout = work + ((int64_t)kcap + 2 + ((t + 1) & 1)) * G;
-  const double yr = sum_parts(pin, G);
-  const double al = ab[2 * t], rho = ab[2 * t + 1];
-  const double beta = rho * yr;
+  const T yr = sum_parts<T>(pin, G);
+  const T al = (T)ab[2 * t], rho = (T)ab[2 * t + 1];
+  const T beta = rho * yr;
   const double* s = S + (int64_t)order[t] * ld;
   const bool last = (t == k - 1);
   const double* yn = last ? s : Y + (int64_t)order[t + 1] * ld;
-  double v = 0.0;
+  T v = 0;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += TLB) {
-    const double ri = r[i] + s[i] * (al - beta);
-    if (last) dout[i] = -ri;
-    else r[i] = ri;
-    v += yn[i] * ri;
+    const T ri = (T)r[i] + (T)s[i] * (al - beta);
+    if (last) dout[i] = -(double)ri;
+    else r[i] = (double)ri;
+    v += (T)yn[i] * ri;
   }
   if (!last) {
-    v = block_sum<TLB>(v, sh);
-    if (threadIdx.x == 0) pout[b] = v;
+    v = block_sum<TLB, T>(v, sh);
+    if (threadIdx.x == 0) pout[b] = (double)v;
   }
 }
 
+template <typename T>
 __global__ __launch_bounds__(TLB) void tl_init_kernel(const double* __restrict__ S, const double* __restrict__ Y,
                                                       int64_t ld, const int* __restrict__ order,
                                                       const int* __restrict__ kp, int k,
@@ -604,9 +613,10 @@ __global__ __launch_bounds__(TLB) void tl_init_kernel(const double* __restrict__
                                                       double* __restrict__ dout) {
   __shared__ double sh[TLB / 64];
   if (kp) k = *kp;
-  tl_init_body(S, Y, ld, order, k, g, m, C, work, kcap, dout, blockIdx.x, gridDim.x, sh);
+  tl_init_body<T>(S, Y, ld, order, k, g, m, C, work, kcap, dout, blockIdx.x, gridDim.x, sh);
 }
 
+template <typename T>
 __global__ __launch_bounds__(TLB) void tl_first_kernel(const double* __restrict__ S, const double* __restrict__ Y,
                                                        int64_t ld, const int* __restrict__ order,
                                                        const int* __restrict__ kp, int k, int li,
@@ -619,9 +629,10 @@ __global__ __launch_bounds__(TLB) void tl_first_kernel(const double* __restrict_
   if (H0p) H0 = *H0p;
   const int t = k - 1 - li;
   if (t < 0) return;
-  tl_first_body(S, Y, ld, order, k, t, H0, m, C, g, q, work, kcap, ab, blockIdx.x, gridDim.x, sh);
+  tl_first_body<T>(S, Y, ld, order, k, t, (T)H0, m, C, g, q, work, kcap, ab, blockIdx.x, gridDim.x, sh);
 }
 
+template <typename T>
 __global__ __launch_bounds__(TLB) void tl_second_kernel(const double* __restrict__ S, const double* __restrict__ Y,
                                                         int64_t ld, const int* __restrict__ order,
                                                         const int* __restrict__ kp, int k, int t, int64_t m,
@@ -631,7 +642,7 @@ __global__ __launch_bounds__(TLB) void tl_second_kernel(const double* __restrict
   __shared__ double sh[TLB / 64];
   if (kp) k = *kp;
   if (t >= k) return;
-  tl_second_body(S, Y, ld, order, k, t, m, C, r, work, kcap, ab, dout, blockIdx.x, gridDim.x, sh);
+  tl_second_body<T>(S, Y, ld, order, k, t, m, C, r, work, kcap, ab, dout, blockIdx.x, gridDim.x, sh);
 }
 
 // L-BFGS memory update (prox-L-BFGS-SCORE.jl:148-162): γh = ∇q_new − ∇q,
@@ -1203,24 +1214,32 @@ hipError_t launch_bb_step(const double* x, const double* xp, const double* g, co
   hipLaunchKernelGGL(bb_step_kernel, dim3(1), dim3(VB), 0, st, x, xp, g, gp, m, out);
   return hipGetLastError();
 }
-hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
-                           const double* g, int64_t m, double* q, double* d, double* ab, double* work, int kcap,
-                           const int* kp, const double* H0p, hipStream_t st) {
+template <typename T>
+static hipError_t two_loop_t(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
+                             const double* g, int64_t m, double* q, double* d, double* ab, double* work, int kcap,
+                             const int* kp, const double* H0p, hipStream_t st) {
   // kp: k on the device, `k` its upper bound (launches beyond the device k return at once)
   if (m <= TWO_LOOP_SINGLE_MAX || (!kp && k < 1)) {
-    hipLaunchKernelGGL(two_loop_kernel, dim3(1), dim3(VB), 0, st, S, Y, ld, order, kp, k, H0p, H0, g, m, q, d, ab);
+    hipLaunchKernelGGL(two_loop_kernel<T>, dim3(1), dim3(VB), 0, st, S, Y, ld, order, kp, k, H0p, H0, g, m, q, d, ab);
     return hipGetLastError();
   }
   const int G = (int)std::min<int64_t>(TWO_LOOP_MAX_WG, ceil_div(m, 1024));
   const int64_t C = ceil_div(m, G);
-  hipLaunchKernelGGL(tl_init_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, g, m, C, work, kcap, d);
+  hipLaunchKernelGGL(tl_init_kernel<T>, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, g, m, C, work, kcap, d);
   for (int i = 0; i < k; ++i)
-    hipLaunchKernelGGL(tl_first_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, i, H0p, H0, m, C, g, q,
+    hipLaunchKernelGGL(tl_first_kernel<T>, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, i, H0p, H0, m, C, g, q,
                        work, kcap, ab);
   for (int t = 0; t < k; ++t)
-    hipLaunchKernelGGL(tl_second_kernel, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, t, m, C, q, work, kcap,
+    hipLaunchKernelGGL(tl_second_kernel<T>, dim3(G), dim3(TLB), 0, st, S, Y, ld, order, kp, k, t, m, C, q, work, kcap,
                        ab, d);
   return hipGetLastError();
+}
+
+hipError_t launch_two_loop(const double* S, const double* Y, int64_t ld, const int* order, int k, double H0,
+                           const double* g, int64_t m, double* q, double* d, double* ab, double* work, int kcap,
+                           const int* kp, const double* H0p, hipStream_t st, int f32) {
+  return f32 ? two_loop_t<float>(S, Y, ld, order, k, H0, g, m, q, d, ab, work, kcap, kp, H0p, st)
+             : two_loop_t<double>(S, Y, ld, order, k, H0, g, m, q, d, ab, work, kcap, kp, H0p, st);
 }
 // the same update over TAIL_G workgroups (large m): per-block partial dots, fixed-order sums
 __global__ __launch_bounds__(TAIL_T) void lbfgs_update_part_kernel(const double* __restrict__ dh,

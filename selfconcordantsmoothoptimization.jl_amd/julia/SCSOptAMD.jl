@@ -15,7 +15,7 @@ using SelfConcordantSmoothOptimization
 import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel, is_interval_set
 
 export DeviceProblem, configure!, iterate_device!, set_gram_cache!, set_solver!, rccl_unique_id, set_comm_rccl!,
-       set_comm_callback!, set_test!
+       set_comm_callback!, set_test!, set_compute_f32!
 
 const lib = joinpath(@__DIR__, "..", "scsopt", "libscsopt.so")
 
@@ -384,6 +384,11 @@ set_gram_cache!(model::DeviceProblem, on::Bool=true) =
 # (prox-GGN-SCORE.jl:126,131), LU for ProxNSCORE's -- the default is Cholesky with the LU fallback.
 set_solver!(model::DeviceProblem, reference::Bool=true) =
     chk(ccall((:scs_set_solver, lib), Cint, (Ptr{Cvoid}, Cint), model.ctx, reference ? 1 : 0), model.ctx)
+
+# The compute arm of the fp32-vs-fp64 study (BASELINE configs[4]): fp32 arithmetic in the sparse
+# products of fp32-stored values (val_f32 = true) and the L-BFGS two-loop (scs_set_compute_f32).
+set_compute_f32!(model::DeviceProblem, on::Bool=true) =
+    chk(ccall((:scs_set_compute_f32, lib), Cint, (Ptr{Cvoid}, Cint), model.ctx, on ? 1 : 0), model.ctx)
 
 method_code(m) = m isa ProxNSCORE ? 1 : m isa ProxGGNSCORE ? 2 : m isa ProxLQNSCORE ? 3 : error("unknown method")
 

@@ -126,6 +126,7 @@ _SIGS = {
     "scs_eval_reg": (C.c_int, [C.c_void_p, c_dp, c_dp]),
     "scs_set_gram_cache": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_set_solver": (C.c_int, [C.c_void_p, C.c_int]),
+    "scs_set_compute_f32": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_set_group_map": (C.c_int, [C.c_void_p, c_i64p, C.c_int64]),
     "scs_set_batches": (C.c_int, [C.c_void_p, c_i64p, c_i64p, C.c_int64]),
     "scs_select_batch": (C.c_int, [C.c_void_p, C.c_int64]),

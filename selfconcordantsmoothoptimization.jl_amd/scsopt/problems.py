@@ -424,6 +424,12 @@ class Problem:
         step (prox-GGN-SCORE.jl:129), which stays the default.  Results are bit-identical."""
         self.ctx.check(_lib.lib.scs_set_gram_cache(self.ctx.h, int(bool(on))))
 
+    def set_compute_f32(self, on=True):
+        """The compute arm of the fp32-vs-fp64 study (BASELINE configs[4]): the sparse products of
+        fp32-stored values (sparse_f32 / f32=True) and the L-BFGS two-loop in fp32 arithmetic;
+        f, η, the step, the prox and the solves stay fp64.  Off (fp64) by default."""
+        self.ctx.check(_lib.lib.scs_set_compute_f32(self.ctx.h, int(bool(on))))
+
     def set_solver(self, kind="default"):
         """"default": Cholesky (LU fallback) / LU; "reference": the reference's factorizations --
         Householder QR for ProxGGNSCORE's systems (prox-GGN-SCORE.jl:126,131), LU for ProxNSCORE's

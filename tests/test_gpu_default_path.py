@@ -158,6 +158,35 @@ def test_c5_shape_lqn_sparse(f32, clean_env):
     assert np.all(sol.x >= -1.0) and np.all(sol.x <= 1.0)
 
 
+@pytest.mark.timeout(600)
+def test_c5_shape_lqn_sparse_fp32_compute(clean_env):
+    """The fp32-COMPUTE arm (scs_set_compute_f32: fp32 arithmetic in A x, Aᵀ r and the two-loop) on the
+    C5 shape above against the fp64 oracle on the same fp32-stored values.  Stated tolerance: every
+    history entry within rtol 1e-4 of the oracle's objective (an fp32 dot of the ~655 entries of a row
+    is good to ~1e-6 relative; the L-BFGS direction inherits that), x within 1e-3 absolute, the box-
+    active sets identical except for coordinates within 1e-3 of a bound, and the fp32 SpMV kernel is
+    the one that ran."""
+    N, m, rho = 1 << 17, 1 << 16, 0.01
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    lam, mu = 1e-4, 0.6
+    p = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), lam, density=rho, seed=2026,
+                                        C_set=[-1.0, 1.0], f32=True)
+    p.set_compute_f32(True)
+    A, y = p.get_sparse()
+    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N), lam, C_set=[-1.0, 1.0])
+    sol = scsopt.iterate(scsopt.ProxLQNSCORE(m=20), p, "indbox", scsopt.PHuberSmootherIndBox(-1.0, 1.0, mu),
+                         max_epoch=10, x_tol=0.0, f_tol=0.0, verbose=0)
+    assert p.ctx.kernel_names()[1] == "spmv_blk32_kernel"
+    osol = O.iterate(O.ProxLQNSCORE(m=20), om, "indbox", O.PHuberSmootherIndBox(-1.0, 1.0, mu), max_epoch=10,
+                     x_tol=0.0, f_tol=0.0)
+    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
+    fin = [i for i, v in enumerate(osol.obj) if np.isfinite(v)]   # entry 0: x0 outside the box, Inf
+    np.testing.assert_allclose(np.array(sol.obj)[fin], np.array(osol.obj)[fin], rtol=1e-4, atol=0)
+    assert np.max(np.abs(sol.x - osol.x)) <= 1e-3
+    ad = (np.abs(sol.x) == 1.0) != (np.abs(osol.x) == 1.0)
+    assert np.all(np.minimum(np.abs(np.abs(sol.x) - 1), np.abs(np.abs(osol.x) - 1))[ad] <= 1e-3)
+
+
 @pytest.mark.timeout(900)
 def test_c4_shape_ggn_group_lasso(clean_env):
     """C4 shape (BASELINE configs[3]) on one GPU: ProxGGNSCORE least squares + sparse-group lasso,
