@@ -139,26 +139,30 @@ def sampled_gram_check(model, m, seed=7, ncols=8):
             "pass": bool(worst <= 1.0 and worst_v <= 1.0)}
 
 
-def sparse_check(model, x, seed=7):
+def sparse_check(model, x, seed=7, f32_compute=False):
     """Full-size C5 check: f(x) and ∇f(x) of the run's final x on the device (the same CSR / CSC
     SpMV kernels the timed epochs use) against a host SciPy evaluation of the downloaded CSR copy
     of A -- least squares, f = 0.5·scale·Σ(Ax − y)², ∇f = scale·Aᵀ(Ax − y) (problems.py / losses.py).
-    Bounds: 1e-11·Σ|terms| per gradient entry, 1e-11 relative on f (different summation orders)."""
+    Bounds: 1e-11·Σ|terms| per gradient entry, 1e-11 relative on f (different summation orders); the
+    fp32-arithmetic arm: 1e-4·Σ|terms| and 1e-4 relative (fp32 sums of ~655-term rows / ~640-term
+    columns: n·2⁻²⁴ ≈ 4e-5 worst case)."""
     import numpy as np
+    tol = 1e-4 if f32_compute else 1e-11
     A, y = model.get_sparse()
     scale = 1.0 / model.N
     z = A @ x
     r = z - y
     f_ref = 0.5 * scale * float(r @ r)
     g_ref = scale * (A.T @ r)
-    g_bound = 1e-11 * scale * (abs(A).T @ np.abs(r)) + 1e-300
+    g_bound = tol * scale * (abs(A).T @ np.abs(r)) + 1e-300
     f_dev = model.fx(x)
     g_dev = model.gradx(x)
     err_g = float(np.max(np.abs(g_dev - g_ref) / g_bound))
-    err_f = abs(f_dev - f_ref) / (1e-11 * abs(f_ref) + 1e-300)
+    err_f = abs(f_dev - f_ref) / (tol * abs(f_ref) + 1e-300)
     del A
     return {"f_rel_err_over_bound": err_f, "grad_max_err_over_bound": err_g, "nnz_checked": int(model.nnz),
-            "bound": "1e-11 * sum|terms| per entry (host SciPy CSR, fp64)",
+            "bound": "%g * sum|terms| per entry (host SciPy CSR, fp64)%s" % (
+                tol, "; fp32-arithmetic arm" if f32_compute else ""),
             "pass": bool(err_f <= 1.0 and err_g <= 1.0)}
 
 
@@ -471,7 +475,7 @@ def main():
     if rank == 0 and not cfg.get("sparse") and cfg["loss"] != "rosenbrock" and not args.no_check and not single:
         check = sampled_gram_check(model, m)   # kernel-level entry points: single-device contexts
     if rank == 0 and cfg.get("sparse") and not args.no_check:
-        check = sparse_check(model, np.asarray(sol.x, dtype=np.float64))
+        check = sparse_check(model, np.asarray(sol.x, dtype=np.float64), f32_compute=args.f32_compute)
 
     if rank == 0:
         ms_step = 1e3 * dt / steps

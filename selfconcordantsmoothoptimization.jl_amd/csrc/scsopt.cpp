@@ -2830,7 +2830,7 @@ int scs_eval_ftest(scs_ctx* c, const double* x, double* fval) {
   if (is_group(c)) return group_eval(c, x, fval, 1, scs_eval_ftest);
   return guarded(c, [&] {
     if (!x || !fval) fail(c, SCS_ERR_ARG, "scs_eval_ftest: null argument");
-    require_ready(c, false);
+    if (!c->has_data || !c->loss_set) fail(c, SCS_ERR_STATE, "scs_eval_ftest: needs the data and the loss");
     HCK(hipSetDevice(c->dev));
     h2d(c, c->xn, x, c->m);
     *fval = eval_ftest_dev(c, x, c->xn);

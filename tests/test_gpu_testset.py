@@ -67,7 +67,7 @@ def test_fvaltest_matches_oracle(method, device_loop):
     p = scsopt.Problem(A, y, x0, f, lam, out_fn=out, Atest=At, ytest=yt)
     om = O.Problem(A, y, x0, of, lam, Atest=At, ytest=yt)
     assert p.test_model and om.test_model
-    for max_epoch, x_tol in ((7, 1e-10), (300, 1e-6)):
+    for max_epoch, x_tol in ((7, 1e-10), (300, 1e-4)):   # the second run terminates at 15-22 epochs
         sol = scsopt.iterate(meth(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=max_epoch, x_tol=x_tol,
                              verbose=0, device_loop=device_loop)
         osol = O.iterate(ometh(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=max_epoch, x_tol=x_tol)
