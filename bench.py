@@ -528,6 +528,27 @@ def main():
                                 "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                                 "kernel": kname, "avg_ms": gram_avg_ms, "launches": main_calls,
                                 "flops_per_launch": gram_flops}
+            if gram_kname.startswith("sparse_gram"):
+                # the Gram of a sparse A is a gather, not an MFMA contraction: its roofline is HBM on the
+                # ALGORITHMIC bytes -- the CSR and CSC copies once (value + 4-B index per entry, the row /
+                # column pointers) plus the upper-triangle G write -- with the MFMA fraction kept beside it;
+                # walk_bytes_est is what Gustavson-by-column moves (every (column, 4096-row block) item
+                # reads the block segment of each row of the column, ~k/16 entries, plus ~36 B of row
+                # metadata): the traffic the kernel's design implies, ~100x the algorithmic bytes
+                nnz_a = model.nnz
+                vbytes = 4 if args.f32 else 8
+                alg = 2.0 * nnz_a * (vbytes + 4) + 8.0 * (N_local + 1) + 8.0 * (m + 1) + 8.0 * m * (m + 1) / 2
+                nblk_g = -(-m // 4096)
+                items = 4096.0 * nblk_g * (nblk_g + 1) / 2
+                walk = items * (nnz_a / m) * ((nnz_a / N_local) / nblk_g * (vbytes + 2) + 36.0)
+                gbs = alg / (gram_avg_ms * 1e-3) / 1e9
+                line["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+                                    "avg_ms": gram_avg_ms, "launches": main_calls, "bytes_per_launch": alg,
+                                    "walk_bytes_est": walk, "walk_over_algorithmic": walk / alg,
+                                    "walk_gbs": walk / (gram_avg_ms * 1e-3) / 1e9,
+                                    "mfma_tflops": achieved, "mfma_frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+                                    "flops_per_launch": gram_flops}
         if tm["gemv_calls"] and lqn_sparse:
             # LDS-blocked CSR (A·x) and CSC (Aᵀ·v) passes, launched equally often.  Bytes each launch must
             # move: nnz·(value + 2 B local index) + the per-block row pointers (8 B per row and block)

@@ -65,7 +65,14 @@ __device__ long long chol_prof[128];
 #define PROF_MARK_T(i, t)
 #endif
 
-constexpr int DNT = 256;          // threads of chol_diag_kernel (4 waves; 512 spills: measured slower)
+constexpr int DNT = 256;
+// W = U⁻¹ by block columns beside the factor (w_column_t) instead of the recursive doubling after it
+// (chol_inv_double_mfma, kept for tri_inv_kernel / wy_t_kernel); compile-time A/B switch
+#ifndef CHOL_W_DOUBLING
+constexpr bool W_BY_COLUMNS = true;
+#else
+constexpr bool W_BY_COLUMNS = false;
+#endif          // threads of chol_diag_kernel (4 waves; 512 spills: measured slower)
 
 // One doubling level of W = U⁻¹ for every pair (i0 = 2pS, j0 = i0 + S):
 //   step 1  T(r, c) = Σ_{t <= c} U(i0+r, j0+t) W(j0+t, j0+c)   -> S[j0 + r][i0 + c] (strictly lower)
@@ -242,6 +249,59 @@ __device__ __forceinline__ void diag_trail_tile(double* su, int o, int id, int l
   }
 }
 
+// W = U⁻¹ by block columns (r04; replaces the recursive doubling on the chain): block column J of W
+// (16 columns, rows of blocks 0..J) by ONE wave, in registers: W_JJ = inv(U_JJ) (swinv), then
+// W_iJ = -inv(U_ii) · Σ_{l=i+1..J} U_il W_lJ for i = J-1 .. 0, right-looking -- as soon as W_lJ is
+// final every pending sum S_i (i < l) takes U_il W_lJ (l descending), so the dependent chain is
+// W_l -> S_{l-1} -> W_{l-1}, 8 MFMAs per block.  The accumulator of an MFMA (acc[r] = D[(lane>>4) +
+// 4r][lane & 15]) is directly the B operand of the next one's k-chunk r, so W never goes through
+// LDS; U_il are A operands read from su (final: written before the barrier of step i), swinv[i] too.
+// Column J needs U rows 0..J and swinv[0..J]: it can run in the step after inv16(J), beside the
+// factor (the doubling needed all of U first: 11.5 us after the loop).  The column goes straight to
+// global W (zeros below its diagonal block).  Fixed order per element: bitwise run to run, and the
+// same bits in both kernel schedules (PIPE or not).
+template <int J>
+__device__ __forceinline__ void w_column_t(const double* su, const double* swv /*[CB/SB][SB*SB]*/, double* Wk,
+                                           int lane) {
+  const int li = lane & 15, lk = lane >> 4;
+  v4d W[J + 1], S[J + 1];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) W[J][r] = swv[J * SB * SB + li * SB + lk + 4 * r];
+#pragma unroll
+  for (int i = 0; i < J; ++i) S[i] = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int l = J; l >= 1; --l) {
+#pragma unroll
+    for (int i = l - 1; i >= 0; --i)   // S_i += U_il W_lJ (i = l - 1 first: the chain)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        S[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(su[(16 * l + 4 * q + lk) * CLD + 16 * i + li], W[l][q], S[i], 0, 0, 0);
+    v4d acc = {0.0, 0.0, 0.0, 0.0};   // W_{l-1,J} = -inv(U_{l-1,l-1}) S_{l-1}
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(swv[(l - 1) * SB * SB + (4 * q + lk) * SB + li], S[l - 1][q], acc, 0, 0, 0);
+    W[l - 1] = -acc;
+  }
+  double* col = Wk + (int64_t)(16 * J + li) * CB + lk;
+#pragma unroll
+  for (int i = 0; i < CB / SB; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) col[16 * i + 4 * r] = (i <= J) ? W[i <= J ? i : 0][r] : 0.0;
+}
+
+__device__ __forceinline__ void w_column(const double* su, const double* swv, double* Wk, int J, int lane) {
+  switch (J) {
+    case 0: w_column_t<0>(su, swv, Wk, lane); break;
+    case 1: w_column_t<1>(su, swv, Wk, lane); break;
+    case 2: w_column_t<2>(su, swv, Wk, lane); break;
+    case 3: w_column_t<3>(su, swv, Wk, lane); break;
+    case 4: w_column_t<4>(su, swv, Wk, lane); break;
+    case 5: w_column_t<5>(su, swv, Wk, lane); break;
+    case 6: w_column_t<6>(su, swv, Wk, lane); break;
+    default: w_column_t<7>(su, swv, Wk, lane); break;
+  }
+}
+
 // PIPE (default): wave 0 takes tile 0 of C(kb) -- the next diagonal sub-block -- and goes straight
 // on to A(kb+1) while waves 1..3 run the rest of C(kb); one barrier per inner block instead of
 // three.  Every element receives the same updates in the same order, so U and W are bitwise those
@@ -363,6 +423,8 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
           inv16(kb);   // U_kb,kb is final: its inverse beside the update
           PROF_MARK_T(50 + kb, 64 * wv);
         }
+        // W's block column kb - 1 (its last input, swinv[kb - 1], came before this step's barrier)
+        if (W_BY_COLUMNS && kb >= 1 && wv == 1 + (kb + 1) % 3) w_column(su, &swinv[0][0], Wk, kb - 1, lane);
         claim_tiles();
         // row blocks of U are final after their panel step: waves 1..3 store them while wave 0 is
         // on the chain (kb = 3: blocks 0, 1; 4: 2, 3; 5: 4, 5; 6: 6 -- where these waves have slack)
@@ -384,11 +446,22 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   if (PIPE) {
     if (wv == DNT / 64 - 1) inv16(CB / SB - 1);
     else store_urows(CB / SB - 1, tid, DNT - 64);
+    if (W_BY_COLUMNS && wv == 1) w_column(su, &swinv[0][0], Wk, CB / SB - 2, lane);   // swinv[6]: step 6
   } else {
     for (int rb = 0; rb < CB / SB; ++rb) store_urows(rb, tid, DNT);
     for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) inv16(kb);
   }
   __syncthreads();   // storeU has read the diagonal blocks; swinv complete
+  if (W_BY_COLUMNS) {
+    if (PIPE) {
+      if (wv == 0) w_column(su, &swinv[0][0], Wk, CB / SB - 1, lane);
+    } else {   // every column here: wave w takes columns w and 7 - w
+      w_column(su, &swinv[0][0], Wk, wv, lane);
+      w_column(su, &swinv[0][0], Wk, CB / SB - 1 - wv, lane);
+    }
+    PROF_MARK(35);
+    return;
+  }
   // ---- diagonal 16 x 16 inverses into the diagonal blocks of S (start of the doubling)
   for (int e = tid; e < CB * SB; e += DNT) {
     const int kb = e >> 8, c = (e >> 4) & 15, i = e & 15;

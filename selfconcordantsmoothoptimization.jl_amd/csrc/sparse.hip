@@ -628,7 +628,14 @@ const char* sparse_gram_kernel_name(int f32) {
   return names[f32 ? 1 : 0][(v >= 3 && v <= 5) ? v - 2 : 0];
 }
 
-int sparse_gram_shift() { return 12; }
+// the row-block width of G items / of the Gram-blocked CSR copy: 2^12 (default); SCS_SPARSE_GRAM_SHIFT
+// (7..12) for A/B -- a narrower block makes each block's slice of the copy smaller (C5: 430 MB at 12,
+// 215 MB at 11, i.e. within the 256 MB MALL) at twice the items and half the segment per row
+int sparse_gram_shift() {
+  const char* e = getenv("SCS_SPARSE_GRAM_SHIFT");
+  const int v = e ? atoi(e) : 12;
+  return v < 7 ? 7 : (v > 12 ? 12 : v);
+}
 
 int64_t sparse_gram_items(int64_t j0, int64_t j1, int shift) {
   // items of columns [j0, j1) (j0, j1 multiples of 2^shift, j1 may be the padded end)
