@@ -453,6 +453,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   }
   __syncthreads();   // storeU has read the diagonal blocks; swinv complete
   if (W_BY_COLUMNS) {
+    PROF_MARK(34);
     if (PIPE) {
       if (wv == 0) w_column(su, &swinv[0][0], Wk, CB / SB - 1, lane);
     } else {   // every column here: wave w takes columns w and 7 - w
