@@ -645,6 +645,21 @@ static unsigned bulk_skip_mask(int nblk) {
 
 static hipError_t create_bulk_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
 
+// The bulk stream's bounded launches take counter sets from a->bctr in turn, each zero when taken
+// (r04: a 9-counter memset in front of every bounded launch was 38 fill kernels, 0.21 ms of the
+// bulk stream, per m = 8192 factor -- profiles/r03/chol/trace_end/).  All bounded launches run on
+// st2, so re-zeroing the array there when the sets run out is ordered after every launch that used
+// them.
+constexpr int BCTR_SLOTS = 1024;
+static unsigned* bulk_ctr(const CholAux* a, hipStream_t st2, hipError_t* e) {
+  if (a->bslot >= BCTR_SLOTS) {
+    const hipError_t z = hipMemsetAsync(a->bctr, 0, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned), st2);
+    if (z != hipSuccess) *e = z;
+    a->bslot = 0;
+  }
+  return a->bctr + 16 * (a->bslot++);
+}
+
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
   a->nblk = nblk;
@@ -659,7 +674,9 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = create_bulk_stream(&a->st2);
-  if (e == hipSuccess) e = hipMalloc(&a->bctr, 16 * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc(&a->bctr, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemsetAsync(a->bctr, 0, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned), st);
+  a->bslot = 0;
   if (e == hipSuccess) e = hipMalloc(&a->sscr, sizeof(double) * 2 * (size_t)CB * 16 * CB);
   if (e == hipSuccess) {
     a->bskip = bulk_skip_mask(nblk);
@@ -672,6 +689,7 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev2, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev3, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev4, hipEventDisableTiming);
   // the one-launch triangular solves' block flags (generation-stamped: never reset) and error flag
   if (e == hipSuccess) e = hipMalloc(&a->sflags, sizeof(unsigned) * 2 * (size_t)nblk + sizeof(int));
   if (e == hipSuccess) e = hipMemsetAsync(a->sflags, 0, sizeof(unsigned) * 2 * (size_t)nblk + sizeof(int), st);
@@ -688,6 +706,7 @@ void chol_aux_free(CholAux* a) {
   if (a->ev1) (void)hipEventDestroy(a->ev1);
   if (a->ev2) (void)hipEventDestroy(a->ev2);
   if (a->ev3) (void)hipEventDestroy(a->ev3);
+  if (a->ev4) (void)hipEventDestroy(a->ev4);
   for (auto& q : a->ssched) {
     if (q.work) (void)hipFree(q.work);
     if (q.comb) (void)hipFree(q.comb);
@@ -713,7 +732,7 @@ void chol_aux_free(CholAux* a) {
   if (a->st2) (void)hipStreamDestroy(a->st2);
   a->w = nullptr;
   a->rect = nullptr;
-  a->ev1 = a->ev2 = a->ev3 = nullptr;
+  a->ev1 = a->ev2 = a->ev3 = a->ev4 = nullptr;
   a->st2 = nullptr;
 }
 
@@ -750,9 +769,13 @@ static hipError_t strip_solve(double* G, int64_t ld, const double* W, const Chol
                               hipStream_t st, bool bulk = false) {
   auto launch = [&](const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w, int64_t k1,
                     const int2* tiles, int ntiles, double* R, int flags) {
-    if (bulk)
-      return gram_launch_bounded(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, a->bctr, a->bskip, a->bslots,
-                                 st);
+    if (bulk) {
+      hipError_t ez = hipSuccess;
+      unsigned* ctr = bulk_ctr(a, st, &ez);
+      if (ez != hipSuccess) return ez;
+      return gram_launch_bounded(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, ctr, a->bskip, a->bslots,
+                                 st, true);
+    }
     return gram_launch_gen(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, st);
   };
   if (hi - lo == 1) {
@@ -1108,6 +1131,20 @@ static hipError_t chol_dag_launch(const CholAux* a, DagList& L, double* G, int64
   return hipGetLastError();
 }
 
+// SCS_CHOL_C12_SPLIT (default 1): the lookahead's trailing update C12_t as two bulk launches,
+// C12a_t -- the upper triangle of the next two blocks' square less C1a_t: rows of block t+1 x
+// columns of block t+2 (what Ba_{t+1} solves) and block t+2's diagonal triangle (what C1a_{t+1}
+// updates next) -- then C12b_t, the rest.  The chain waits for C12a_t only, i.e. for C12b_{t-1}
+// one outer block later than before (stream order on st2), so in the bulk-bound outer blocks the
+// bulk stream no longer idles while the chain's Ba waits for a whole C12 (r03 trace at m = 8192:
+// 6.19 ms of chain and 6.18 ms of bulk work in an 8.23 ms span).  Every element still takes its
+// updates in block order with the per-tile-identical kernels: U bitwise the serial order's.  0 = one
+// C12 launch.
+static bool c12_split() {
+  const char* e = getenv("SCS_CHOL_C12_SPLIT");
+  return !(e && e[0] == '0');
+}
+
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* a,
                        const int2* trilist, int* info, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
@@ -1115,6 +1152,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
   const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
   const bool dag = chol_dag_on() && a->serr;
   const bool steps = !dag && ba_steps() && a->sscr && OB <= 16;
+  const bool split = la && c12_split() && a->ev4;
   if (dag) {
     const hipError_t eb = chol_dag_build(a, nblk, OB, ld, st);
     if (eb != hipSuccess) return eb;
@@ -1180,8 +1218,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (e == hipSuccess) e = hipEventRecord(a->ev3, st);
     wait(a->st2, a->ev3);
     if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2, true);
-    // Ba, C1a on the chain after C12_{t-1}
-    if (c12_pending) wait(st, a->ev2);
+    // Ba, C1a on the chain after C12a_{t-1} (and so after everything before it on st2)
+    if (c12_pending) wait(st, split ? a->ev4 : a->ev2);
     const int n1a = (OB * (OB + 1)) / 2;
     if (dag) {   // the recursive strip solve and the next diagonal triangle as one launch
       if (e == hipSuccess) e = chol_dag_launch(a, a->dnext[(size_t)(i0 / OB)], G, ld, W, st);
@@ -1192,12 +1230,23 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
         e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, n1a, trail, ld,
                               2 | 4, st);
     }
-    // C12 on st2 after Ba (it reads X's columns of the next block)
+    // C12 on st2 after Ba (it reads X's columns of the next block); split: C12a (the tiles the
+    // chain's next Ba and C1a read) as a latency launch, its event, then C12b
     if (e == hipSuccess) e = hipEventRecord(a->ev1, st);
     wait(a->st2, a->ev1);
-    if (e == hipSuccess)
-      e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n1a, ntri - n1a,
-                              trail, ld, 2 | 4, a->bctr, a->bskip, a->bslots, a->st2);
+    const int n2a = split ? std::min(ntri, OB * (2 * OB + 1)) : n1a;   // 2OB(2OB+1)/2 tiles
+    if (split) {
+      if (e == hipSuccess && n2a > n1a)
+        e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n1a, n2a - n1a,
+                              trail, ld, 2 | 4, a->st2);
+      if (e == hipSuccess) e = hipEventRecord(a->ev4, a->st2);
+    }
+    if (e == hipSuccess && ntri > n2a) {
+      unsigned* ctr = bulk_ctr(a, a->st2, &e);
+      if (e == hipSuccess)
+        e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n2a,
+                                ntri - n2a, trail, ld, 2 | 4, ctr, a->bskip, a->bslots, a->st2, true);
+    }
     if (e == hipSuccess) e = hipEventRecord(a->ev2, a->st2);
     if (e != hipSuccess) return e;
     c12_pending = true;

@@ -1009,15 +1009,17 @@ hipError_t gram_launch_work_cm(const double* A1, int64_t lda1, const double* A2,
 // gram_launch_gen's path.  Per tile the same kernel body and MFMA order: bitwise the same G.
 hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                                int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
-                               unsigned* ctr, unsigned skip, int slots, hipStream_t st) {
+                               unsigned* ctr, unsigned skip, int slots, hipStream_t st, bool zeroed) {
   if (ntiles <= 0) return hipSuccess;
   const char* se = getenv("SCS_GRAM_SMALL");
   const int small_max = se ? atoi(se) : 128;
   const bool small = k1 - k0 <= 512 && (k1 - k0) % (8 * GBK) == 0 && k1 > k0 && ntiles <= small_max;
   if (!ctr || skip == 0 || slots <= 0 || small)
     return gram_launch_gen(A1, lda1, A2, lda2, w, k0, k1, tiles, ntiles, G, ldg, flags, st);
-  hipError_t e = hipMemsetAsync(ctr, 0, 9 * sizeof(unsigned), st);
-  if (e != hipSuccess) return e;
+  if (!zeroed) {   // (the Cholesky's bulk stream hands over counter sets zeroed in advance)
+    const hipError_t e = hipMemsetAsync(ctr, 0, 9 * sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+  }
   // enough workgroups that the ones left after the skipped CUs' leave take every tile in one round
   // (a launch smaller than the chip), else one per workgroup slot of the device
   const int want = ntiles + (ntiles + 6) / 7 + 8;

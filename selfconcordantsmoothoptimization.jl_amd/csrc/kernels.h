@@ -44,13 +44,13 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
                            hipStream_t st);
 // the same as CU-bounded persistent launches leaving the CUs of `skip` (ids within a shader engine)
-// free; ctr: 9 device counters, zeroed in stream order by the call
+// free; ctr: 9 device counters, zeroed in stream order by the call (zeroed: already zero)
 // K-split work list over two column-major operands: partial tiles to P (gram.hip; the QR's Vᵀ products)
 hipError_t gram_launch_work_cm(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                                int64_t K, const int4* work, int seglen, int nsplit, double* P, hipStream_t st);
 hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                                int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
-                               unsigned* ctr, unsigned skip, int slots, hipStream_t st);
+                               unsigned* ctr, unsigned skip, int slots, hipStream_t st, bool zeroed = false);
 // the latency form of gram_launch_gen (128 x 16/32 strips per workgroup, loads 8 stages ahead);
 // the same bits per tile as gram_launch_gen's other kernels
 hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
@@ -95,13 +95,15 @@ struct CholAux {             // device constants of the two-level factorization 
   double* w = nullptr;       // [128 x +1.0 | mpad x -1.0] Gram weights (panel solve | block updates)
   int2* rect = nullptr;      // R x nblk rectangle tile lists, R = 1..4 (bj-major)
   hipStream_t st2 = nullptr; // lookahead: the bulk stream (strip solve beyond the next block, C12)
-  hipEvent_t ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  hipEvent_t ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
   int nblk = 0;
   // the bulk stream's launches as CU-bounded persistent launches (gram_launch_bounded): claim /
   // arrival counters, the skipped CU ids (SCS_CHOL_BULK_SKIP), workgroup slots of the device
+  // (BCTR_SLOTS sets of 16, zeroed together; each launch takes the next set -- no memset per launch)
   unsigned* bctr = nullptr;
   unsigned bskip = 0;
   int bslots = 0;
+  mutable int bslot = 0;   // the next unused counter set
   // the chain's strip solve as right-looking step launches (strip_solve_steps): two rows of
   // 128 x (16 x 128) doubles for a step's leaf (its copy-back is the next step's)
   double* sscr = nullptr;
@@ -361,10 +363,11 @@ hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int 
 // sparse Gram G = Aᵀ diag(w) A (upper part, column j up to the end of its diagonal tile) from the
 // CSC copy and a Gram-blocked CSR copy (block width 2^shift, unpadded segments): Σ_r nnz_r² work
 int sparse_gram_shift();
-const char* sparse_gram_kernel_name(int f32);   // the variant launch_sparse_gram runs (SCS_SPARSE_GRAM_KERNEL)
+// the variant launch_sparse_gram runs (SCS_SPARSE_GRAM_KERNEL) for a copy of `entries` entries
+const char* sparse_gram_kernel_name(int f32, int64_t entries);
 hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const void* valT, const int64_t* bptr,
-                              const uint16_t* lidx, const void* bval, int f32, const double* w, int64_t nrows,
-                              int64_t m, int shift, double* G, int64_t ldg, hipStream_t st);
+                              const uint16_t* lidx, const void* bval, int64_t entries, int f32, const double* w,
+                              int64_t nrows, int64_t m, int shift, double* G, int64_t ldg, hipStream_t st);
 size_t sparse_layer_map_bytes(int k);
 void sparse_layer_maps(uint64_t seed, int k, int64_t N, void* out_host);
 hipError_t launch_gen_sparse(int64_t N, int64_t m, int k, uint64_t seed, const void* Ldev, int f32, double scale,
