@@ -115,6 +115,7 @@ struct scs_ctx {
   void *val = nullptr, *valT = nullptr;
   struct SpBlk {
     int shift = 0, nblk = 0;
+    int64_t nnz = 0;   // entries of the copy
     int64_t* ptr = nullptr;
     uint16_t* lidx = nullptr;
     void* val = nullptr;
@@ -1471,6 +1472,7 @@ void build_gram_blocked(scs_ctx* c) {
     sync(c);
     dfree(c, tmp);
   }
+  B.nnz = nnz;
   B.lidx = dalloc<uint16_t>(c, nnz + 8);
   B.val = c->sp_f32 ? (void*)dalloc<float>(c, (size_t)nnz + 8) : (void*)dalloc<double>(c, (size_t)nnz + 8);
   if (nrows > 0)
@@ -1499,9 +1501,9 @@ void gram_sparse(scs_ctx* c, const double* w, double* out, int packed) {
   if (!c->bgram.ptr) build_gram_blocked(c);
   double* dst = (packed & 1) ? c->G : out;
   if (packed & 2) fail(c, SCS_ERR_ARG, "internal: the sparse Gram does not accumulate");
-  HCK(launch_sparse_gram(c->colptr, c->rowidx, c->valT, c->bgram.ptr, c->bgram.lidx, c->bgram.val, c->sp_f32, w, c->N,
-                         c->m, c->bgram.shift, dst, c->mpad, c->st));
-  c->gram_kname = sparse_gram_kernel_name(c->sp_f32);
+  HCK(launch_sparse_gram(c->colptr, c->rowidx, c->valT, c->bgram.ptr, c->bgram.lidx, c->bgram.val, c->bgram.nnz,
+                         c->sp_f32, w, c->N, c->m, c->bgram.shift, dst, c->mpad, c->st));
+  c->gram_kname = sparse_gram_kernel_name(c->sp_f32, c->bgram.nnz);
   if (packed & 1) HCK(gram_pack_launch(c->G, c->mpad, c->utiles, c->nslots, out, c->st));
 }
 
@@ -2374,6 +2376,7 @@ static void reset_data(scs_ctx* c) {
     dfree_t(c, B->lidx);
     dfree(c, B->val);
     B->nblk = B->shift = 0;
+    B->nnz = 0;
   }
   c->sparse = false;
   dfree_t(c, c->Ad);

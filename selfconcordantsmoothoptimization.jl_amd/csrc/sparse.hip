@@ -608,24 +608,144 @@ __global__ __launch_bounds__(64) void sparse_gram_pipe_kernel(const int64_t* __r
   for (int i = lane; i < nr; i += 64) col[i] = acc[i];
 }
 
-// SCS_SPARSE_GRAM_KERNEL (read per call: A/B and the bit-identity test): 1 the one-round-trip-per-8-
-// rows kernel; 2 / 3: the pipelined kernel, 32 / 64 rows per batch, items j-major; 4 / 5: the same,
-// items b-major (concurrent waves share a 4096-row block of the Gram-blocked CSR copy).  Default 5:
-// C5-shaped Gram 1733 (1) -> 934 (2) / 794 (3) / 901 (4) / 766 ms (5), profiles/r03/sparse_gram/.
-static int sparse_gram_variant() {
-  const char* e = getenv("SCS_SPARSE_GRAM_KERNEL");
-  return e ? atoi(e) : 5;
+// r04 (variant 6, default when the Gram-blocked copy has < 2^31 entries): the pipelined walk with
+// the per-row instruction count cut.  The r03 kernel was issue-bound, not byte-bound: ~30
+// instructions per (column, row, block) triple -- 64-bit segment bounds broadcast by four
+// v_readlane, an exec-masked load branch per row, and the long-segment check (four more readlanes)
+// per row -- at ~0.13 ns per triple chip-wide whatever the block width (shift 12: 5.8e9 triples in
+// 773 ms; shift 11: twice the triples, 1463 ms).  Here the bounds are 32-bit (start, length) pairs
+// (one readlane each), every lane loads unconditionally (lanes past the segment read entry 0 and add
+// -0.0: no exec branches), and the long-segment pass runs only in batches
+// that hold a segment longer than one wave (a ballot per batch).  The same products accumulate in
+// the same row order into every G entry: bitwise variant 5's G.
+template <typename VT>
+__global__ __launch_bounds__(64) void sparse_gram_flat_kernel(const int64_t* __restrict__ colptr,
+                                                              const int* __restrict__ rowidx,
+                                                              const VT* __restrict__ valT,
+                                                              const int64_t* __restrict__ bptr,
+                                                              const uint16_t* __restrict__ lidx,
+                                                              const VT* __restrict__ bval,
+                                                              const double* __restrict__ w, int64_t nrows,
+                                                              int64_t m, int shift, int64_t j0,
+                                                              double* __restrict__ G, int64_t ldg) {
+  constexpr int PR = 64;                  // rows per batch
+  __shared__ double acc[1 << 12];   // 32 KiB: five waves per CU, as variant 5
+  const int lane = threadIdx.x;
+  const int BS = 1 << shift;
+  const int64_t t = (int64_t)blockIdx.x;
+  const int64_t J0 = j0 >> shift;
+  int64_t J = J0, base = 0;
+  while (true) {
+    const int64_t n = (int64_t)BS * (J + 1);
+    if (t < base + n) break;
+    base += n;
+    ++J;
+  }
+  const int64_t loc = t - base;
+  const int64_t j = J * BS + loc % BS;   // items b-major within a column block
+  const int b = (int)(loc / BS);
+  if (j >= m) return;
+  for (int i = lane; i < BS; i += 64) acc[i] = 0.0;
+  __syncthreads();
+  const int64_t p0 = colptr[j], p1 = colptr[j + 1];
+  const int64_t boff = (int64_t)b * nrows;
+  auto stage1 = [&](int64_t p, int& r, double& a) {   // lane u: row p + u's index and CSC value
+    if (p + lane < p1) {
+      r = rowidx[p + lane];
+      a = (double)valT[p + lane];
+    } else {
+      r = -1;
+      a = 0.0;
+    }
+  };
+  auto stage2 = [&](int r, double a, double& s, int& st, int& ln) {   // its weight x value, segment
+    if (r >= 0) {
+      s = w[r] * a;
+      const int64_t s0 = bptr[boff + r], s1 = bptr[boff + r + 1];
+      st = (int)s0;
+      ln = (int)(s1 - s0);
+    } else {
+      s = 0.0;
+      st = ln = 0;
+    }
+  };
+  int rc, rn;
+  double ac, an, s, sN;
+  int st, ln, stN, lnN;
+  stage1(p0, rc, ac);
+  stage2(rc, ac, s, st, ln);
+  stage1(p0 + PR, rn, an);
+  for (int64_t p = p0; p < p1; p += PR) {
+    stage2(rn, an, sN, stN, lnN);
+    stage1(p + 2 * PR, rn, an);
+    const bool longseg = __builtin_amdgcn_ballot_w64(ln > 64) != 0;   // wave-uniform
+    double v[PR];
+    int ix[PR];
+#pragma unroll
+    for (int u = 0; u < PR; ++u) {   // every row's first 64 entries in flight before any is used
+      const int su = __builtin_amdgcn_readlane(st, u), lu = __builtin_amdgcn_readlane(ln, u);
+      const int q = lane < lu ? su + lane : 0;
+      v[u] = (double)bval[q];
+      ix[u] = lidx[q];
+    }
+    // rows in order (rows past the column's end: length 0).  A lane past the segment adds -0.0 into
+    // slot `lane`: x + (-0.0) == x for every x (signed zeros included), so no exec branch and no
+    // extra LDS (a dummy slot would cost the fifth wave per CU)
+    auto row = [&](int u) {
+      const double su_s = sg_bcast(s, u);
+      const int lu = __builtin_amdgcn_readlane(ln, u);
+      const bool on = lane < lu;
+      atomicAdd(&acc[on ? ix[u] : lane], on ? su_s * v[u] : -0.0);
+    };
+    if (!longseg) {
+#pragma unroll
+      for (int u = 0; u < PR; ++u) row(u);
+    } else {
+#pragma unroll
+      for (int u = 0; u < PR; ++u) {
+        row(u);
+        const int lu = __builtin_amdgcn_readlane(ln, u);
+        if (lu > 64) {   // the rest of this row before the next row (row order kept)
+          const double su_s = sg_bcast(s, u);
+          const int su = __builtin_amdgcn_readlane(st, u);
+          for (int q = 64 + lane; q - lane < lu; q += 64)
+            if (q < lu) atomicAdd(&acc[lidx[su + q]], su_s * (double)bval[su + q]);
+        }
+      }
+    }
+    s = sN;
+    st = stN;
+    ln = lnN;
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)b * BS;
+  const int64_t rend = ((j >> 7) + 1) << 7;
+  const int64_t nr = (rend - r0 < BS) ? rend - r0 : BS;
+  double* col = G + j * ldg + r0;
+  for (int i = lane; i < nr; i += 64) col[i] = acc[i];
 }
 
-const char* sparse_gram_kernel_name(int f32) {
-  if (sparse_gram_variant() == 1) return f32 ? "sparse_gram_kernel<float>" : "sparse_gram_kernel<double>";
+// SCS_SPARSE_GRAM_KERNEL (read per call: A/B and the bit-identity test): 1 the one-round-trip-per-8-
+// rows kernel; 2 / 3: the pipelined kernel, 32 / 64 rows per batch, items j-major; 4 / 5: the same,
+// items b-major (concurrent waves share a 4096-row block of the Gram-blocked CSR copy); 6: the
+// flat-issue walk above (r04 default; 5 where the copy has 2^31 entries or more).  C5-shaped Gram
+// 1733 (1) -> 934 (2) / 794 (3) / 901 (4) / 766 ms (5), profiles/r03/sparse_gram/.
+static int sparse_gram_variant(int64_t entries) {
+  const char* e = getenv("SCS_SPARSE_GRAM_KERNEL");
+  const int v = e ? atoi(e) : 6;
+  return (v == 6 && entries >= ((int64_t)1 << 31)) ? 5 : v;   // variant 6: 32-bit segment positions
+}
+
+const char* sparse_gram_kernel_name(int f32, int64_t entries) {
+  const int var = sparse_gram_variant(entries);
+  if (var == 1) return f32 ? "sparse_gram_kernel<float>" : "sparse_gram_kernel<double>";
+  if (var == 6) return f32 ? "sparse_gram_flat_kernel<float>" : "sparse_gram_flat_kernel<double>";
   static const char* names[2][4] = {
       {"sparse_gram_pipe_kernel<double, 32, false>", "sparse_gram_pipe_kernel<double, 64, false>",
        "sparse_gram_pipe_kernel<double, 32, true>", "sparse_gram_pipe_kernel<double, 64, true>"},
       {"sparse_gram_pipe_kernel<float, 32, false>", "sparse_gram_pipe_kernel<float, 64, false>",
        "sparse_gram_pipe_kernel<float, 32, true>", "sparse_gram_pipe_kernel<float, 64, true>"}};
-  const int v = sparse_gram_variant();
-  return names[f32 ? 1 : 0][(v >= 3 && v <= 5) ? v - 2 : 0];
+  return names[f32 ? 1 : 0][(var >= 3 && var <= 5) ? var - 2 : 0];
 }
 
 // the row-block width of G items / of the Gram-blocked CSR copy: 2^12 (default); SCS_SPARSE_GRAM_SHIFT
@@ -646,8 +766,8 @@ int64_t sparse_gram_items(int64_t j0, int64_t j1, int shift) {
 }
 
 hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const void* valT, const int64_t* bptr,
-                              const uint16_t* lidx, const void* bval, int f32, const double* w, int64_t nrows,
-                              int64_t m, int shift, double* G, int64_t ldg, hipStream_t st) {
+                              const uint16_t* lidx, const void* bval, int64_t entries, int f32, const double* w,
+                              int64_t nrows, int64_t m, int shift, double* G, int64_t ldg, hipStream_t st) {
   if (m <= 0) return hipSuccess;
   if (shift > 12 || shift < 7) return hipErrorInvalidValue;
   const int64_t BS = (int64_t)1 << shift;
@@ -658,8 +778,15 @@ hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const vo
     while (j1 < m && sparse_gram_items(j0, j1 + BS, shift) < ((int64_t)1 << 30)) j1 += BS;
     if (j1 == j0) j1 = j0 + BS;
     const int64_t items = sparse_gram_items(j0, j1, shift);
-    const int var = sparse_gram_variant();
-    if (var != 1) {
+    const int var = sparse_gram_variant(entries);
+    if (var == 6) {
+      if (f32)
+        hipLaunchKernelGGL(sparse_gram_flat_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
+                           (const float*)valT, bptr, lidx, (const float*)bval, w, nrows, m, shift, j0, G, ldg);
+      else
+        hipLaunchKernelGGL(sparse_gram_flat_kernel<double>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
+                           (const double*)valT, bptr, lidx, (const double*)bval, w, nrows, m, shift, j0, G, ldg);
+    } else if (var != 1) {
       // 2: 32 rows per batch, 3: 64 rows, 4 / 5: the same with b-major items (5: default)
       auto go = [&](auto kf, auto kd) {
         if (f32)

@@ -281,10 +281,11 @@ def test_sparse_gram_priced_by_nnz(f32, monkeypatch):
     assert np.all(err <= bound), float(np.max(err - bound))
     assert np.array_equal(p.gram(w), G)
     g, p2 = p.ctx.kernel_names()
-    assert g.startswith("sparse_gram_pipe_kernel<")
+    assert g.startswith("sparse_gram_flat_kernel<")
     # every variant (the one-round-trip-per-8-rows kernel, the pipelined one at 32 / 64 rows per
-    # batch, j- or b-major items) accumulates the same products in the same row order: bitwise G
-    for var in ("2", "3", "4", "1"):
+    # batch, j- or b-major items, r03's default 5) accumulates the same products in the same row
+    # order as the flat-issue kernel (6, r04 default): bitwise G
+    for var in ("5", "2", "3", "4", "1"):
         monkeypatch.setenv("SCS_SPARSE_GRAM_KERNEL", var)
         assert np.array_equal(p.gram(w), G), var
     assert p.ctx.kernel_names()[0].startswith("sparse_gram_kernel<")
