@@ -23,6 +23,8 @@ import scsopt_oracle as O  # noqa: E402
 LOGI_A = [[-0.560501, 0.0], [0.0, 1.85278], [-0.0192918, -0.827763], [0.128064, 0.110096], [0.0, -0.251176]]
 LOGI_Y = [-1, -1, -1, 1, -1]
 X0 = [0.5908446386657102, 0.7667970365022592]
+HELDOUT_A = [[0.3, -1.1], [-0.7, 0.45], [1.2, 0.05]]   # held-out rows (not from the reference)
+HELDOUT_Y = [1, -1, 1]
 QP_A = [[1.53976, 0.201833, 0.433995, 0.156497, 0.180124],
         [0.201833, 2.37257, -0.0594941, -0.671533, 0.0739676],
         [0.433995, -0.0594941, 3.15025, 0.808797, 0.954656],
@@ -34,7 +36,7 @@ QP_XS = [-0.7139006111210786, 0.642716661564418, 0.3684773651494535, 0.589048779
 
 
 def sol_dict(sol):
-    return {"x": [float(v) for v in sol.x], "obj": sol.obj, "fval": sol.fval,
+    return {"x": [float(v) for v in sol.x], "obj": sol.obj, "fval": sol.fval, "fvaltest": sol.fvaltest,
             "pri_res_norm": sol.pri_res_norm, "rel": sol.rel, "objrel": sol.objrel, "epochs": sol.epochs}
 
 
@@ -47,6 +49,13 @@ def cases():
             model = O.Problem(A, y, X0, O.Loss("logistic_margin", 1 / 5, ggn="sigmoid_ce"), 1)
             sol = O.iterate(mk(), model, reg, O.PHuberSmootherL1L2(1))
             out[f"logistic_{mname}_{reg}"] = sol_dict(sol)
+        # the held-out set (problems.jl:27-28,67-68; ftest iterate.jl:169-175, pushed by show_stat!
+        # utils.jl:55-57): the reference's tests never pass Atest / ytest, so the held-out rows here are
+        # HELDOUT_A / HELDOUT_Y below -- a restatement case, not a reference literal
+        model = O.Problem(A, y, X0, O.Loss("logistic_margin", 1 / 5, ggn="sigmoid_ce"), 1,
+                          Atest=np.array(HELDOUT_A), ytest=np.array(HELDOUT_Y, dtype=float))
+        sol = O.iterate(mk(), model, "l1", O.PHuberSmootherL1L2(1))
+        out[f"logistic_{mname}_l1_heldout"] = sol_dict(sol)
     Aq = np.array(QP_A)
     for sname, sm, alpha in (("phuber", O.PHuberSmootherIndBox(-1.0, 1.0, 0.6), 0.8),
                              ("exp", O.ExponentialSmootherIndBox(-1.0, 1.0, 0.6), 1.0)):

@@ -14,7 +14,7 @@ import pytest
 import scsopt
 import scsopt_oracle as O
 from scsopt import losses
-from make_golden import LOGI_A, LOGI_Y, X0, QP_A, QP_Y, QP_X0, QP_XS
+from make_golden import LOGI_A, LOGI_Y, X0, QP_A, QP_Y, QP_X0, QP_XS, HELDOUT_A, HELDOUT_Y
 
 pytestmark = pytest.mark.gpu
 
@@ -163,6 +163,22 @@ def test_reference_logistic(golden, mname, meth, reg):
     assert sol.objrel[-1] <= 1e-6
     _compare_solution(sol, golden["cases"][f"logistic_{mname}_{reg}"])
     assert np.array_equal(np.signbit(sol.x), np.signbit(np.array(golden["cases"][f"logistic_{mname}_{reg}"]["x"])))
+
+
+@pytest.mark.parametrize("mname,meth", [("nscore", scsopt.ProxNSCORE), ("ggnscore", scsopt.ProxGGNSCORE),
+                                        ("lqnscore", scsopt.ProxLQNSCORE)])
+def test_reference_logistic_heldout(golden, mname, meth):
+    """The same test problem with a held-out set (Problem(...; Atest, ytest), problems.jl:27-28): the
+    fvaltest history against the regenerated golden fixture (restatement case: the reference's tests
+    never pass Atest / ytest), one entry per obj entry."""
+    ref = golden["cases"][f"logistic_{mname}_l1_heldout"]
+    model = scsopt.Problem(np.array(LOGI_A), np.array(LOGI_Y, float), X0, losses.logistic_margin(1 / 5), 1,
+                           out_fn=losses.sigmoid_ce(1 / 5), Atest=np.array(HELDOUT_A),
+                           ytest=np.array(HELDOUT_Y, float))
+    sol = scsopt.iterate(meth(), model, "l1", scsopt.PHuberSmootherL1L2(1), verbose=0)
+    _compare_solution(sol, ref)
+    assert len(sol.fvaltest) == len(sol.obj) == len(ref["fvaltest"])
+    np.testing.assert_allclose(sol.fvaltest, ref["fvaltest"], rtol=1e-8, atol=0)
 
 
 @pytest.mark.parametrize("sname,alpha", [("phuber", 0.8), ("exp", 1.0)])

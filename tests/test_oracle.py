@@ -120,6 +120,12 @@ def test_golden_fixtures_reproduce(golden):
         assert len(got["obj"]) == len(ref["obj"]), name
         np.testing.assert_allclose(got["obj"], ref["obj"], rtol=1e-13, atol=0, err_msg=name)
         np.testing.assert_allclose(got["x"], ref["x"], rtol=1e-12, atol=1e-300, err_msg=name)
+        assert len(got["fvaltest"]) == len(ref["fvaltest"]), name
+        np.testing.assert_allclose(got["fvaltest"], ref["fvaltest"], rtol=1e-13, atol=0, err_msg=name)
+        if name.endswith("_heldout"):
+            assert len(got["fvaltest"]) == len(got["obj"]) > 0, name
+        else:
+            assert got["fvaltest"] == [], name
 
 
 def test_golden_kernel_vectors(golden):
