@@ -125,6 +125,12 @@ int scs_destroy(scs_ctx* ctx);
  * ndev = 1 is a plain one-device run.  A device that fails inside a collective aborts the
  * communicators (then every call returns SCS_ERR_COMM: destroy the context).                 */
 int scs_create_multi(const int* devs, int ndev, scs_ctx** out);
+/* The same with flags.  SCS_MULTI_HOST_EXCHANGE: the group's exchange through host memory instead of
+ * RCCL (every device's payload to a host slot, a barrier, the slots summed in device order on every
+ * device, written back) -- no RCCL, and devs may repeat a GPU (several sub-contexts on one device:
+ * the group's fan-out, row split and exchange on a one-GPU machine).  Two host copies per exchange.  */
+#define SCS_MULTI_HOST_EXCHANGE 1
+int scs_create_multi_ex(const int* devs, int ndev, int flags, scs_ctx** out);
 /* Devices of a context (1 for scs_create).                                                   */
 int scs_group_size(scs_ctx* ctx, int* ndev);
 const char* scs_last_error(const scs_ctx* ctx);

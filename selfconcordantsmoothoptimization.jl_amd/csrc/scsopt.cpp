@@ -337,6 +337,9 @@ struct scs_ctx {
   struct Workers;
   std::unique_ptr<Workers> workers;
   std::shared_ptr<std::atomic<bool>> comm_abort;
+  // SCS_MULTI_HOST_EXCHANGE groups: the exchange through host memory instead of RCCL
+  struct HostExchange;
+  std::unique_ptr<HostExchange> hx;
   ~scs_ctx();
 };
 
@@ -4025,6 +4028,69 @@ struct scs_ctx::Workers {
   }
 };
 
+// The exchange of a SCS_MULTI_HOST_EXCHANGE group (scs_create_multi_ex): every device's payload goes to
+// a host slot, a barrier, every device sums the slots in device order (the same bits on every device),
+// writes the sum back, a second barrier (no slot is rewritten before every device has read it).  It
+// needs no RCCL and no distinct devices -- several sub-contexts may share one GPU -- so the group's
+// fan-out, row split and exchange run on a one-GPU box; the cost is two host copies per exchange.
+// abort() releases every waiter (group_run, after a device failed).
+struct scs_ctx::HostExchange {
+  struct Rank {
+    HostExchange* ex = nullptr;
+    int rank = 0;
+    std::vector<double> sum;
+  };
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::vector<std::vector<double>> slot;
+  std::vector<Rank> ranks;
+  explicit HostExchange(int n_) : n(n_), slot((size_t)n_), ranks((size_t)n_) {
+    for (int i = 0; i < n_; ++i) ranks[(size_t)i] = Rank{this, i, {}};
+  }
+  bool wait() {   // false once aborted
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return false;
+    const uint64_t g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    cv.wait(lk, [&] { return gen != g || aborted; });
+    return gen != g;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+  static int allreduce(void* dev_buf, int64_t count, void* stream, void* user) {
+    Rank* rk = static_cast<Rank*>(user);
+    HostExchange* ex = rk->ex;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    std::vector<double>& mine = ex->slot[(size_t)rk->rank];
+    mine.resize((size_t)count);
+    if (hipMemcpyAsync(mine.data(), dev_buf, sizeof(double) * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return 2;
+    if (!ex->wait()) return 1;
+    rk->sum.assign(ex->slot[0].begin(), ex->slot[0].begin() + count);
+    for (int r = 1; r < ex->n; ++r) {
+      const double* o = ex->slot[(size_t)r].data();
+      for (int64_t e = 0; e < count; ++e) rk->sum[(size_t)e] += o[e];
+    }
+    if (hipMemcpyAsync(dev_buf, rk->sum.data(), sizeof(double) * count, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return 2;
+    return ex->wait() ? 0 : 1;
+  }
+};
+
 scs_ctx::~scs_ctx() = default;
 
 namespace {
@@ -4057,6 +4123,7 @@ int group_run(scs_ctx* g, F&& f) {
       for (int t = 0; t < 500 && done.load() < n; ++t) std::this_thread::sleep_for(std::chrono::milliseconds(10));
       if (done.load() < n && !aborted.exchange(true)) {
         g->comm_abort->store(true, std::memory_order_release);
+        if (g->hx) g->hx->abort();
         for (scs_ctx* o : g->subs)
           if (o->rccl) (void)ncclCommAbort(o->rccl);
       }
@@ -4081,11 +4148,14 @@ bool is_group(const scs_ctx* c) { return c && !c->subs.empty(); }
 
 extern "C" {
 
-int scs_create_multi(const int* devs, int ndev, scs_ctx** out) {
-  if (!out || !devs || ndev < 1) return SCS_ERR_ARG;
+int scs_create_multi(const int* devs, int ndev, scs_ctx** out) { return scs_create_multi_ex(devs, ndev, 0, out); }
+
+int scs_create_multi_ex(const int* devs, int ndev, int flags, scs_ctx** out) {
+  if (!out || !devs || ndev < 1 || (flags & ~SCS_MULTI_HOST_EXCHANGE)) return SCS_ERR_ARG;
   *out = nullptr;
+  const bool host = (flags & SCS_MULTI_HOST_EXCHANGE) != 0;
   scs_ctx* g = new scs_ctx();
-  for (int i = 0; i < ndev; ++i)
+  for (int i = 0; i < ndev && !host; ++i)
     for (int j = 0; j < i; ++j)
       if (devs[i] == devs[j]) {
         delete g;
@@ -4101,19 +4171,31 @@ int scs_create_multi(const int* devs, int ndev, scs_ctx** out) {
     }
     g->subs.push_back(s);
   }
-  std::vector<ncclComm_t> comms((size_t)ndev, nullptr);
-  const ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devs);
-  if (r != ncclSuccess) {
-    for (scs_ctx* o : g->subs) scs_destroy(o);
-    delete g;
-    return SCS_ERR_COMM;
-  }
   g->comm_abort = std::make_shared<std::atomic<bool>>(false);
-  for (int i = 0; i < ndev; ++i) {
-    g->subs[i]->rccl = comms[(size_t)i];
-    g->subs[i]->rank = i;
-    g->subs[i]->nranks = ndev;
-    g->subs[i]->comm_abort = g->comm_abort;
+  if (host) {
+    g->hx.reset(new scs_ctx::HostExchange(ndev));
+    for (int i = 0; i < ndev; ++i) {
+      scs_ctx* s = g->subs[i];
+      s->rank = i;
+      s->nranks = ndev;
+      s->ar = &scs_ctx::HostExchange::allreduce;
+      s->ar_user = &g->hx->ranks[(size_t)i];
+      s->comm_abort = g->comm_abort;
+    }
+  } else {
+    std::vector<ncclComm_t> comms((size_t)ndev, nullptr);
+    const ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devs);
+    if (r != ncclSuccess) {
+      for (scs_ctx* o : g->subs) scs_destroy(o);
+      delete g;
+      return SCS_ERR_COMM;
+    }
+    for (int i = 0; i < ndev; ++i) {
+      g->subs[i]->rccl = comms[(size_t)i];
+      g->subs[i]->rank = i;
+      g->subs[i]->nranks = ndev;
+      g->subs[i]->comm_abort = g->comm_abort;
+    }
   }
   g->workers.reset(new scs_ctx::Workers(std::vector<int>(devs, devs + ndev)));
   g->dev = devs[0];

@@ -56,15 +56,20 @@ end
 # devices = [d0, d1, ...]: one process drives those GPUs (scs_create_multi) -- the library splits
 # the rows across them, so a plain iterate! call uses the node's GPUs with no MPI (the reference's
 # iterate! is one process, iterate.jl:56-76)
-function create_ctx(device::Integer, devices=nothing)
+# device_exchange = :host: the group's exchange through host memory instead of RCCL
+# (SCS_MULTI_HOST_EXCHANGE; devices may repeat a GPU)
+const SCS_MULTI_HOST_EXCHANGE = Cint(1)
+function create_ctx(device::Integer, devices=nothing, device_exchange::Symbol=:rccl)
     ctx = Ref{Ptr{Cvoid}}(C_NULL)
     if devices === nothing
         rc = ccall((:scs_create, lib), Cint, (Cint, Ptr{Cvoid}, Ref{Ptr{Cvoid}}), device, C_NULL, ctx)
         rc == 0 || error("scs_create failed ($rc)")
     else
         devs = Cint.(collect(devices))
-        rc = ccall((:scs_create_multi, lib), Cint, (Ptr{Cint}, Cint, Ref{Ptr{Cvoid}}), devs, length(devs), ctx)
-        rc == 0 || error("scs_create_multi($(devs)) failed ($rc)")
+        flags = device_exchange === :host ? SCS_MULTI_HOST_EXCHANGE : Cint(0)
+        rc = ccall((:scs_create_multi_ex, lib), Cint, (Ptr{Cint}, Cint, Cint, Ref{Ptr{Cvoid}}), devs, length(devs),
+                   flags, ctx)
+        rc == 0 || error("scs_create_multi_ex($(devs), $(device_exchange)) failed ($rc)")
     end
     return ctx[]
 end
@@ -122,9 +127,10 @@ end
 function DeviceProblem(A::Matrix{Float64}, y::AbstractVector, x0::Vector{Float64}, loss::Symbol, λ;
                        out_fn::Union{Symbol,Nothing}=nothing, scale::Float64=1.0 / size(A, 1),
                        L=nothing, sol::Vector{Float64}=zero(x0), C_set=nothing, P=nothing, device::Integer=0,
-                       N_global::Integer=size(A, 1), row0::Integer=0, devices=nothing, Atest=nothing,
+                       N_global::Integer=size(A, 1), row0::Integer=0, devices=nothing,
+                       device_exchange::Symbol=:rccl, Atest=nothing,
                        ytest=nothing, Ntest_global::Integer=0, test_row0::Integer=0)
-    ctx = create_ctx(device, devices)
+    ctx = create_ctx(device, devices, device_exchange)
     N, m = size(A)
     yv = Vector{Float64}(y)
     chk(ccall((:scs_set_data, lib), Cint,

@@ -17,6 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCSOPT_LIB", os.path.join(_HERE, "libscsopt.so"))
 
 SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS_ERR_COMM, SCS_ERR_CALLBACK = range(8)
+SCS_MULTI_HOST_EXCHANGE = 1   # scs_create_multi_ex flag
 SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS, SCS_CB_GGN, SCS_CB_FTEST = range(5)
 
 LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5, "callback": 6}
@@ -89,6 +90,7 @@ _SIGS = {
     "scs_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
     "scs_destroy": (C.c_int, [C.c_void_p]),
     "scs_create_multi": (C.c_int, [c_i32p, C.c_int, C.POINTER(C.c_void_p)]),
+    "scs_create_multi_ex": (C.c_int, [c_i32p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "scs_group_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "scs_last_error": (C.c_char_p, [C.c_void_p]),
     "scs_get_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
@@ -184,15 +186,20 @@ def dptr(a):
 
 class Context:
     """Owns one scs_ctx: one device and stream (scs_create), or -- devices=[d0, d1, ...] -- one
-    process driving several GPUs (scs_create_multi: the library splits the rows across them)."""
+    process driving several GPUs (scs_create_multi: the library splits the rows across them).
+    device_exchange="host": the group's exchange through host memory instead of RCCL
+    (SCS_MULTI_HOST_EXCHANGE; devices may repeat a GPU)."""
 
-    def __init__(self, device=0, stream=None, devices=None):
+    def __init__(self, device=0, stream=None, devices=None, device_exchange="rccl"):
         h = C.c_void_p()
+        if device_exchange not in ("rccl", "host"):
+            raise ValueError("device_exchange is 'rccl' or 'host'")
         if devices is not None:
             devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
-            rc = lib.scs_create_multi(devs, len(devices), C.byref(h))
+            flags = SCS_MULTI_HOST_EXCHANGE if device_exchange == "host" else 0
+            rc = lib.scs_create_multi_ex(devs, len(devices), flags, C.byref(h))
             if rc != SCS_OK:
-                raise ScsError(rc, f"scs_create_multi(devices={list(devices)}) failed")
+                raise ScsError(rc, f"scs_create_multi_ex(devices={list(devices)}, {device_exchange}) failed")
             device = int(devices[0])
         else:
             rc = lib.scs_create(int(device), stream, C.byref(h))

@@ -72,7 +72,8 @@ class Problem:
 
     def __init__(self, *args, Atest=None, ytest=None, L=None, sol=None, C_set=None, P=None,
                  out_fn: Optional[OutFn] = None, name=None, device=0, comm=None, N_global=None, row0=0,
-                 sparse_f32=False, devices=None, Ntest_global=None, test_row0=0, _ctx=None):
+                 sparse_f32=False, devices=None, device_exchange="rccl", Ntest_global=None, test_row0=0,
+                 _ctx=None):
         if len(args) == 5:
             A, y, x0, f, lam = args
         elif len(args) == 3:
@@ -102,7 +103,7 @@ class Problem:
             A, y, self.generic = None, None, True
         if devices is not None and (comm is not None or _is_sparse(A)):
             raise ValueError("devices=[...] (one process, several GPUs) takes a dense A and no comm")
-        self.ctx = _ctx if _ctx is not None else _lib.Context(device, devices=devices)
+        self.ctx = _ctx if _ctx is not None else _lib.Context(device, devices=devices, device_exchange=device_exchange)
         if comm is not None and comm.active and _ctx is None:
             comm.attach(self.ctx)
         if _ctx is None:
@@ -277,7 +278,7 @@ class Problem:
 
     @classmethod
     def synthetic(cls, N, m, x0, f, lam, *, kind=1, seed=1234, density=0.1, out_fn=None, device=0,
-                  comm=None, devices=None, test_N=None, **kw):
+                  comm=None, devices=None, device_exchange="rccl", test_N=None, **kw):
         """A ~ N(0,1)/sqrt(m) (kind 1, 2) or N(0,1) (kind 3) generated on the device, y from a
         sparse x_true (kind 1: Bernoulli(σ(A x_true)) ∈ {0,1}; kind 2: ±1; kind 3: A x_true + 0.1ε).
         With comm, this rank generates its contiguous row shard in place; with devices=[...] one
@@ -288,7 +289,7 @@ class Problem:
                              "each other")
         rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
         r0, r1 = row_range(N, world, rank)
-        ctx = _lib.Context(device, devices=devices)
+        ctx = _lib.Context(device, devices=devices, device_exchange=device_exchange)
         if comm is not None and comm.active:
             comm.attach(ctx)
         spec = _lib.Synth(N_global=N, row0=r0, N=r1 - r0, m=m, seed=seed, kind=kind, density=density)
