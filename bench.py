@@ -542,6 +542,17 @@ def main():
                 items = 4096.0 * nblk_g * (nblk_g + 1) / 2
                 walk = items * (nnz_a / m) * ((nnz_a / N_local) / nblk_g * (vbytes + 2) + 36.0)
                 gbs = alg / (gram_avg_ms * 1e-3) / 1e9
+                # PMC bytes of the sparse Gram (tools/gpu_pmc_sgram.sh + tools/pmc_summary_sgram.py) when the
+                # summary names the kernel launched here at this shape
+                for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_sgram", "summary_*.json")),
+                                  reverse=True):
+                    with open(pmc) as f:
+                        pm = json.load(f)
+                    if (world == 1 and pm.get("N") == N and pm.get("m") == m and not args.f32
+                            and pm.get("kernel", "").split("::")[-1] == kname):
+                        traffic = pm.get("hbm_bytes_per_launch")
+                        line["roofline_traffic_source"] = os.path.relpath(pmc, ROOT)
+                        break
                 line["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                                     "avg_ms": gram_avg_ms, "launches": main_calls, "bytes_per_launch": alg,

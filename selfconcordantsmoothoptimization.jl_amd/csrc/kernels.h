@@ -363,6 +363,21 @@ hipError_t blk_scatter(const int64_t* ptr, const int* idx, const void* val, int 
 // sparse Gram G = Aᵀ diag(w) A (upper part, column j up to the end of its diagonal tile) from the
 // CSC copy and a Gram-blocked CSR copy (block width 2^shift, unpadded segments): Σ_r nnz_r² work
 int sparse_gram_shift();
+int64_t sparse_gram_items(int64_t j0, int64_t j1, int shift);   // work items of columns [j0, j1)
+// variant 8 (sparse.hip): the segment copy (value + index records, 8-B units), the per-triple table
+// T[tptr[j] + b·n_j + k] = n << 40 | unit, and sw[p] = w[rowidx[p]]·valT[p] formed per Gram
+int64_t seg_units_host(int64_t n, int f32);
+int sparse_gram_requested();   // SCS_SPARSE_GRAM_KERNEL (default 8)
+hipError_t seg_units(const int64_t* cnt, int64_t n, int f32, int64_t* ucnt, hipStream_t st);
+hipError_t seg_scatter(const int64_t* ptr, const int* idx, const void* val, int f32, int64_t nrows, int shift,
+                       const int64_t* cnt, const int64_t* first, const int64_t* uptr, uint64_t* seg, hipStream_t st);
+hipError_t seg_table(const int64_t* colptr, const int* rowidx, const int64_t* cnt, const int64_t* uptr, int64_t nrows,
+                     int64_t m, int shift, const int64_t* tptr, uint64_t* T, hipStream_t st);
+hipError_t csc_weight(const int* rowidx, const void* valT, int f32, const double* w, int64_t nnz, double* sw,
+                      hipStream_t st);
+hipError_t launch_sparse_gram_seg(const int64_t* colptr, const double* sw, const int64_t* tptr, const uint64_t* T,
+                                  const uint64_t* seg, int f32, int64_t m, int shift, double* G, int64_t ldg,
+                                  hipStream_t st);
 // the variant launch_sparse_gram runs (SCS_SPARSE_GRAM_KERNEL) for a copy of `entries` entries
 const char* sparse_gram_kernel_name(int f32, int64_t entries);
 hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const void* valT, const int64_t* bptr,

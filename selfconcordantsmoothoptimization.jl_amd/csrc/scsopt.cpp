@@ -121,6 +121,14 @@ struct scs_ctx {
     void* val = nullptr;
   } bcsr, bcsc;  // LDS-blocked copies used by the products (sparse.hip)
   SpBlk bgram;    // the sparse Gram's row copy: 2^sparse_gram_shift()-wide blocks, unpadded (built on first use)
+  struct SegGram {   // the sparse Gram's variant-8 structure (build_gram_seg, on first use)
+    int state = 0;   // 0 not tried, 1 built, -1 not built (memory / size): the Gram-blocked walk instead
+    int shift = 0;
+    uint64_t* seg = nullptr;   // per (block, row) segment records, 8-B units
+    uint64_t* T = nullptr;     // per (column, upper block, row of the column): n << 40 | unit
+    int64_t* tptr = nullptr;   // T's column offsets
+    double* sw = nullptr;      // w[rowidx[p]]·valT[p], per Gram
+  } sgseg;
   int sp_gram = 0;   // the Gram of a sparse A: 0 undecided, 1 priced by nnz (sparse_gram_kernel), 2 dense tiles
   double* Ad = nullptr;  // dense panel-blocked mirror of a sparse A (Gram-based methods only)
   // ... or, when the mirror does not fit under the cap, a ring of two R-row dense slots the Gram
@@ -1485,6 +1493,60 @@ void build_gram_blocked(scs_ctx* c) {
   dfree_t(c, first);
 }
 
+// The variant-8 structure (sparse.hip, r04): the segment records, the per-triple table and the sw
+// buffer.  Built only when it fits (free memory less 4 GiB) and its units fit 32 bits; else state -1
+// and gram_sparse takes the Gram-blocked walk (variant 6).  C5 shape: T 47 GB, seg 6.9 GB, sw 5.5 GB.
+bool build_gram_seg(scs_ctx* c) {
+  scs_ctx::SegGram& S = c->sgseg;
+  if (S.state) return S.state > 0;
+  S.state = -1;
+  const int64_t nrows = c->N, m = c->m;
+  const int shift = sparse_gram_shift();
+  const int64_t nblk = ceil_div(m, int64_t(1) << shift);
+  const int64_t nk = nblk * nrows;
+  std::vector<int64_t> cp((size_t)m + 1), tp((size_t)m + 1, 0);
+  HCK(hipMemcpyAsync(cp.data(), c->colptr, sizeof(int64_t) * (m + 1), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  for (int64_t j = 0; j < m; ++j) tp[(size_t)j + 1] = tp[(size_t)j] + ((j >> shift) + 1) * (cp[(size_t)j + 1] - cp[(size_t)j]);
+  const int64_t nT = tp[(size_t)m], nnz = cp[(size_t)m];
+  const double units_max = (double)seg_units_host(1, c->sp_f32) * (double)nnz + 2.0 * (double)nk;
+  const double need = 8.0 * ((double)nT + (double)nnz + units_max + 4.0 * (double)(nk + 1)) + 4.0 * 1073741824.0;
+  size_t fr = 0, tot = 0;
+  HCK(hipMemGetInfo(&fr, &tot));
+  if (nrows <= 0 || need > (double)fr) return false;
+  int64_t* cnt = dalloc<int64_t>(c, nk + 1);
+  int64_t* first = dalloc<int64_t>(c, nk + 1);
+  int64_t* ucnt = dalloc<int64_t>(c, nk + 1);
+  int64_t* uptr = dalloc<int64_t>(c, nk + 1);
+  HCK(blk_count(c->rowptr, c->colidx, nrows, shift, cnt, first, c->st));
+  HCK(seg_units(cnt, nk, c->sp_f32, ucnt, c->st));
+  size_t tb = 0;
+  HCK(blk_scan(nullptr, &tb, ucnt, uptr, nk + 1, c->st));
+  void* tmp = dalloc<char>(c, tb);
+  HCK(blk_scan(tmp, &tb, ucnt, uptr, nk + 1, c->st));
+  int64_t units = 0;
+  HCK(hipMemcpyAsync(&units, uptr + nk, sizeof(int64_t), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  dfree(c, tmp);
+  dfree_t(c, ucnt);
+  if (units < ((int64_t)1 << 31)) {   // the kernel keeps record positions in 32 bits
+    S.seg = dalloc<uint64_t>(c, units + 1);
+    HCK(seg_scatter(c->rowptr, c->colidx, c->val, c->sp_f32, nrows, shift, cnt, first, uptr, S.seg, c->st));
+    S.tptr = dalloc<int64_t>(c, m + 1);
+    HCK(hipMemcpyAsync(S.tptr, tp.data(), sizeof(int64_t) * (m + 1), hipMemcpyHostToDevice, c->st));
+    S.T = dalloc<uint64_t>(c, nT);
+    HCK(seg_table(c->colptr, c->rowidx, cnt, uptr, nrows, m, shift, S.tptr, S.T, c->st));
+    S.sw = dalloc<double>(c, nnz);
+    S.shift = shift;
+    S.state = 1;
+  }
+  sync(c);   // the temporaries' last readers
+  dfree_t(c, cnt);
+  dfree_t(c, first);
+  dfree_t(c, uptr);
+  return S.state > 0;
+}
+
 bool sparse_gram(scs_ctx* c) {
   if (!c->sparse) return false;
   if (const char* e = std::getenv("SCS_SPARSE_GRAM")) return e[0] == '1';   // read per call (A/B tests)
@@ -1501,9 +1563,17 @@ bool sparse_gram(scs_ctx* c) {
 
 // the sparse Gram -> out (upper part, ldg = m_pad), or packed 128 x 128 slots (multi-rank) through G
 void gram_sparse(scs_ctx* c, const double* w, double* out, int packed) {
-  if (!c->bgram.ptr) build_gram_blocked(c);
   double* dst = (packed & 1) ? c->G : out;
   if (packed & 2) fail(c, SCS_ERR_ARG, "internal: the sparse Gram does not accumulate");
+  if (sparse_gram_requested() == 8 && build_gram_seg(c)) {   // variant 8 (default)
+    const scs_ctx::SegGram& S = c->sgseg;
+    HCK(csc_weight(c->rowidx, c->valT, c->sp_f32, w, c->nnz, S.sw, c->st));
+    HCK(launch_sparse_gram_seg(c->colptr, S.sw, S.tptr, S.T, S.seg, c->sp_f32, c->m, S.shift, dst, c->mpad, c->st));
+    c->gram_kname = c->sp_f32 ? "sparse_gram_seg_kernel<float>" : "sparse_gram_seg_kernel<double>";
+    if (packed & 1) HCK(gram_pack_launch(c->G, c->mpad, c->utiles, c->nslots, out, c->st));
+    return;
+  }
+  if (!c->bgram.ptr) build_gram_blocked(c);
   HCK(launch_sparse_gram(c->colptr, c->rowidx, c->valT, c->bgram.ptr, c->bgram.lidx, c->bgram.val, c->bgram.nnz,
                          c->sp_f32, w, c->N, c->m, c->bgram.shift, dst, c->mpad, c->st));
   c->gram_kname = sparse_gram_kernel_name(c->sp_f32, c->bgram.nnz);
@@ -2381,6 +2451,11 @@ static void reset_data(scs_ctx* c) {
     B->nblk = B->shift = 0;
     B->nnz = 0;
   }
+  dfree_t(c, c->sgseg.seg);
+  dfree_t(c, c->sgseg.T);
+  dfree_t(c, c->sgseg.tptr);
+  dfree_t(c, c->sgseg.sw);
+  c->sgseg.state = 0;
   c->sparse = false;
   dfree_t(c, c->Ad);
   dfree_t(c, c->ringA);

@@ -725,21 +725,369 @@ __global__ __launch_bounds__(64) void sparse_gram_flat_kernel(const int64_t* __r
   for (int i = lane; i < nr; i += 64) col[i] = acc[i];
 }
 
+// Variant 7 (r04): variant 6 software-pipelined by half-batches.  In variant 6 a wave issues a
+// batch's segment loads, then waits out one memory latency before its adds can start, then issues
+// the next batch's loads only after the adds: latency and issue alternate.  Here each metadata
+// batch of 62 rows is cut into two halves of 31 rows with their own registers, and the loads of the
+// next half are issued before the adds of the current one (the register budget of variant 6's
+// 64-row batch), so a half's memory latency runs under the previous half's adds.  31 rows = 62
+// loads in flight: the most vmcnt (6 bits) can wait past, so the current half's adds never wait for
+// the next half's loads.  Same products in the same row order: G bitwise variant 5's.
+template <typename VT>
+__global__ __launch_bounds__(64) void sparse_gram_db_kernel(const int64_t* __restrict__ colptr,
+                                                            const int* __restrict__ rowidx,
+                                                            const VT* __restrict__ valT,
+                                                            const int64_t* __restrict__ bptr,
+                                                            const uint16_t* __restrict__ lidx,
+                                                            const VT* __restrict__ bval,
+                                                            const double* __restrict__ w, int64_t nrows,
+                                                            int64_t m, int shift, int64_t j0,
+                                                            double* __restrict__ G, int64_t ldg) {
+  constexpr int PR = 62, H = 31;   // rows per metadata batch, per half
+  __shared__ double acc[1 << 12];
+  const int lane = threadIdx.x;
+  const int BS = 1 << shift;
+  const int64_t t = (int64_t)blockIdx.x;
+  const int64_t J0 = j0 >> shift;
+  int64_t J = J0, base = 0;
+  while (true) {
+    const int64_t n = (int64_t)BS * (J + 1);
+    if (t < base + n) break;
+    base += n;
+    ++J;
+  }
+  const int64_t loc = t - base;
+  const int64_t j = J * BS + loc % BS;   // items b-major within a column block
+  const int b = (int)(loc / BS);
+  if (j >= m) return;
+  for (int i = lane; i < BS; i += 64) acc[i] = 0.0;
+  __syncthreads();
+  const int64_t p0 = colptr[j], p1 = colptr[j + 1];
+  const int64_t boff = (int64_t)b * nrows;
+  auto stage1 = [&](int64_t p, int& r, double& a) {   // lane u < PR: row p + u
+    if (lane < PR && p + lane < p1) {
+      r = rowidx[p + lane];
+      a = (double)valT[p + lane];
+    } else {
+      r = -1;
+      a = 0.0;
+    }
+  };
+  auto stage2 = [&](int r, double a, double& s, int& st, int& ln) {
+    if (r >= 0) {
+      s = w[r] * a;
+      const int64_t s0 = bptr[boff + r], s1 = bptr[boff + r + 1];
+      st = (int)s0;
+      ln = (int)(s1 - s0);
+    } else {
+      s = 0.0;
+      st = ln = 0;
+    }
+  };
+  // the first 64 entries of rows h·H .. h·H + H - 1 of a metadata batch (st, ln per lane = row)
+  auto load_half = [&](int stv, int lnv, int h, double* v, int* ix) {
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+      const int su = __builtin_amdgcn_readlane(stv, h * H + u), lu = __builtin_amdgcn_readlane(lnv, h * H + u);
+      const int q = lane < lu ? su + lane : 0;
+      v[u] = (double)bval[q];
+      ix[u] = lidx[q];
+    }
+  };
+  // rows in order; a lane past its segment adds -0.0 into slot `lane` (x + (-0.0) == x)
+  auto add_half = [&](double sv, int stv, int lnv, int h, const double* v, const int* ix, auto lng) {
+    constexpr bool LONG = decltype(lng)::value;   // a row of this batch has more than 64 entries
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+      const double su_s = sg_bcast(sv, h * H + u);
+      const int lu = __builtin_amdgcn_readlane(lnv, h * H + u);
+      const bool on = lane < lu;
+      atomicAdd(&acc[on ? ix[u] : lane], on ? su_s * v[u] : -0.0);
+      if (LONG && lu > 64) {   // the rest of this row before the next row
+        const int su = __builtin_amdgcn_readlane(stv, h * H + u);
+        for (int q = 64 + lane; q - lane < lu; q += 64)
+          if (q < lu) atomicAdd(&acc[lidx[su + q]], su_s * (double)bval[su + q]);
+      }
+    }
+  };
+  int rc, rn;
+  double ac, an, s, sN;
+  int st, ln, stN, lnN;
+  stage1(p0, rc, ac);
+  stage2(rc, ac, s, st, ln);
+  stage1(p0 + PR, rn, an);
+  double va[H], vb[H];
+  int ia[H], ib[H];
+  load_half(st, ln, 0, va, ia);
+  for (int64_t p = p0; p < p1; p += PR) {
+    stage2(rn, an, sN, stN, lnN);
+    stage1(p + 2 * PR, rn, an);
+    const bool longseg = __builtin_amdgcn_ballot_w64(ln > 64) != 0;   // lanes >= PR: ln = 0
+    load_half(st, ln, 1, vb, ib);         // second half of this batch in flight ...
+    if (longseg) add_half(s, st, ln, 0, va, ia, std::true_type{});   // ... under the first half's adds
+    else add_half(s, st, ln, 0, va, ia, std::false_type{});
+    if (p + PR < p1) load_half(stN, lnN, 0, va, ia);   // the next batch's first half
+    if (longseg) add_half(s, st, ln, 1, vb, ib, std::true_type{});
+    else add_half(s, st, ln, 1, vb, ib, std::false_type{});
+    s = sN;
+    st = stN;
+    ln = lnN;
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)b * BS;
+  const int64_t rend = ((j >> 7) + 1) << 7;
+  const int64_t nr = (rend - r0 < BS) ? rend - r0 : BS;
+  double* col = G + j * ldg + r0;
+  for (int i = lane; i < nr; i += 64) col[i] = acc[i];
+}
+
+// ---- variant 8 (r04): the walk on a per-triple table and interleaved segments ----------------------
+// The PMC passes of variant 6 (profiles/r04/pmc_sgram/) put its fabric reads at 5.1e12 B per Gram
+// (2 x FETCH_SIZE, the gfx950 rule) in 695 ms -- ~7.4 TB/s, i.e. the walk is bandwidth-bound -- about
+// 930 B per (column, row, block) triple against ~410 B of segment payload: a 128-B line for the
+// weight w[r], one for the segment bounds bptr[b][r], and partial lines at both ends of the two
+// separate value / index ranges.  Here
+//   * the segment of (block b, row r) is ONE record: its n values, then its n 16-bit local indices,
+//     each part rounded up to 8 B, at 8-B unit uptr[b][r] of `seg` (seg_units: vunits(n) + ceil(n/4));
+//   * a table T lists, per column j, per upper block b <= j >> shift and per row k of column j (CSC
+//     order), the packed (n << 40 | unit) of that row's segment in b, so an item reads its rows'
+//     segment positions as one coalesced 8-B stream instead of gathering bptr;
+//   * sw[p] = w[rowidx[p]] * valT[p] is formed per Gram as one streaming pass over the CSC, so the
+//     walk reads the scaled column entry instead of gathering w.
+// The structure (seg, T) is built once per sparsity pattern.  Same products (w[r]·a_rj computed the
+// same way) added in the same row order: G bitwise variant 5's.
+__host__ __device__ inline int64_t seg_vunits(int64_t n, int vb) { return (n * vb + 7) >> 3; }
+__host__ __device__ inline int64_t seg_units(int64_t n, int vb) { return seg_vunits(n, vb) + ((n + 3) >> 2); }
+int64_t seg_units_host(int64_t n, int f32) { return seg_units(n, f32 ? 4 : 8); }
+
+__global__ void seg_units_kernel(const int64_t* __restrict__ cnt, int64_t n, int vb, int64_t* __restrict__ ucnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ucnt[i] = seg_units(cnt[i], vb);
+}
+
+template <typename VT>
+__global__ void seg_scatter_kernel(const int64_t* __restrict__ ptr, const int* __restrict__ idx,
+                                   const VT* __restrict__ val, int64_t nrows, int shift,
+                                   const int64_t* __restrict__ cnt, const int64_t* __restrict__ first,
+                                   const int64_t* __restrict__ uptr, uint64_t* __restrict__ seg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const int64_t p0 = ptr[r], p1 = ptr[r + 1];
+  const int mask = (1 << shift) - 1;
+  for (int64_t p = p0 + lane; p < p1; p += 64) {
+    const int c = idx[p];
+    const int64_t k = (int64_t)(c >> shift) * nrows + r;
+    const int64_t n = cnt[k], off = p - first[k];
+    char* base = reinterpret_cast<char*>(seg + uptr[k]);
+    reinterpret_cast<VT*>(base)[off] = val[p];
+    reinterpret_cast<uint16_t*>(base + 8 * seg_vunits(n, (int)sizeof(VT)))[off] = (uint16_t)(c & mask);
+  }
+}
+
+// T[tptr[j] + b·n_j + k] = cnt[b][r] << 40 | uptr[b][r] for r = rowidx[colptr[j] + k], b <= j >> shift
+__global__ void seg_table_kernel(const int64_t* __restrict__ colptr, const int* __restrict__ rowidx,
+                                 const int64_t* __restrict__ cnt, const int64_t* __restrict__ uptr, int64_t nrows,
+                                 int shift, int64_t j0, const int64_t* __restrict__ tptr, uint64_t* __restrict__ T) {
+  const int64_t j = j0 + blockIdx.x;
+  const int64_t p0 = colptr[j], n = colptr[j + 1] - p0;
+  uint64_t* Tj = T + tptr[j];
+  const int J = (int)(j >> shift);
+  for (int b = 0; b <= J; ++b)
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+      const int64_t q = (int64_t)b * nrows + rowidx[p0 + k];
+      Tj[(int64_t)b * n + k] = ((uint64_t)cnt[q] << 40) | (uint64_t)uptr[q];
+    }
+}
+
+template <typename VT>
+__global__ void csc_weight_kernel(const int* __restrict__ rowidx, const VT* __restrict__ valT,
+                                  const double* __restrict__ w, int64_t nnz, double* __restrict__ sw) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * blockDim.x)
+    sw[p] = w[rowidx[p]] * (double)valT[p];
+}
+
+template <typename VT>
+__global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __restrict__ colptr,
+                                                             const double* __restrict__ sw,
+                                                             const int64_t* __restrict__ tptr,
+                                                             const uint64_t* __restrict__ T,
+                                                             const uint64_t* __restrict__ seg, int64_t m,
+                                                             int shift, int64_t j0, double* __restrict__ G,
+                                                             int64_t ldg) {
+  constexpr int PR = 64;
+  constexpr int VB = (int)sizeof(VT);
+  __shared__ double acc[1 << 12];
+  const int lane = threadIdx.x;
+  const int BS = 1 << shift;
+  const int64_t t = (int64_t)blockIdx.x;
+  const int64_t J0 = j0 >> shift;
+  int64_t J = J0, base = 0;
+  while (true) {
+    const int64_t n = (int64_t)BS * (J + 1);
+    if (t < base + n) break;
+    base += n;
+    ++J;
+  }
+  const int64_t loc = t - base;
+  const int64_t j = J * BS + loc % BS;   // items b-major within a column block
+  const int b = (int)(loc / BS);
+  if (j >= m) return;
+  for (int i = lane; i < BS; i += 64) acc[i] = 0.0;
+  __syncthreads();
+  const int64_t p0 = colptr[j], nj = colptr[j + 1] - p0;
+  const uint64_t* Tb = T + tptr[j] + (int64_t)b * nj;
+  const double* swj = sw + p0;
+  auto stage = [&](int64_t k, double& sv, int& st, int& ln) {   // lane u: row k + u of the column
+    if (k + lane < nj) {
+      sv = swj[k + lane];
+      const uint64_t tv = Tb[k + lane];
+      st = (int)(uint32_t)tv;
+      ln = (int)(tv >> 40);
+    } else {
+      sv = 0.0;
+      st = ln = 0;
+    }
+  };
+  double s, sN;
+  int st, ln, stN, lnN;
+  stage(0, s, st, ln);
+  for (int64_t k = 0; k < nj; k += PR) {
+    stage(k + PR, sN, stN, lnN);   // the next batch's scaled entries and segment positions
+    const bool longseg = __builtin_amdgcn_ballot_w64(ln > 64) != 0;
+    double v[PR];
+    int ix[PR];
+#pragma unroll
+    for (int u = 0; u < PR; ++u) {   // every row's first 64 entries in flight before any is used
+      const int su = __builtin_amdgcn_readlane(st, u), lu = __builtin_amdgcn_readlane(ln, u);
+      const char* rec = reinterpret_cast<const char*>(seg + su);   // wave-uniform record address
+      const int q = lane < lu ? lane : 0;
+      v[u] = (double)reinterpret_cast<const VT*>(rec)[q];
+      ix[u] = reinterpret_cast<const uint16_t*>(rec + 8 * seg_vunits(lu, VB))[q];
+    }
+    auto row = [&](int u) {   // a lane past its segment adds -0.0 into slot `lane` (x + (-0.0) == x)
+      const double su_s = sg_bcast(s, u);
+      const int lu = __builtin_amdgcn_readlane(ln, u);
+      const bool on = lane < lu;
+      atomicAdd(&acc[on ? ix[u] : lane], on ? su_s * v[u] : -0.0);
+    };
+    if (!longseg) {
+#pragma unroll
+      for (int u = 0; u < PR; ++u) row(u);
+    } else {
+#pragma unroll
+      for (int u = 0; u < PR; ++u) {
+        row(u);
+        const int lu = __builtin_amdgcn_readlane(ln, u);
+        if (lu > 64) {   // the rest of this row before the next row (row order kept)
+          const double su_s = sg_bcast(s, u);
+          const char* rec = reinterpret_cast<const char*>(seg + __builtin_amdgcn_readlane(st, u));
+          const VT* rv = reinterpret_cast<const VT*>(rec);
+          const uint16_t* ri = reinterpret_cast<const uint16_t*>(rec + 8 * seg_vunits(lu, VB));
+          for (int q = 64 + lane; q - lane < lu; q += 64)
+            if (q < lu) atomicAdd(&acc[ri[q]], su_s * (double)rv[q]);
+        }
+      }
+    }
+    s = sN;
+    st = stN;
+    ln = lnN;
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)b * BS;
+  const int64_t rend = ((j >> 7) + 1) << 7;
+  const int64_t nr = (rend - r0 < BS) ? rend - r0 : BS;
+  double* col = G + j * ldg + r0;
+  for (int i = lane; i < nr; i += 64) col[i] = acc[i];
+}
+
+hipError_t seg_units(const int64_t* cnt, int64_t n, int f32, int64_t* ucnt, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(seg_units_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, cnt, n, f32 ? 4 : 8, ucnt);
+  return hipGetLastError();
+}
+
+hipError_t seg_scatter(const int64_t* ptr, const int* idx, const void* val, int f32, int64_t nrows, int shift,
+                       const int64_t* cnt, const int64_t* first, const int64_t* uptr, uint64_t* seg, hipStream_t st) {
+  if (nrows <= 0) return hipSuccess;
+  const dim3 grid((unsigned)ceil_div(nrows, 4));
+  if (f32)
+    hipLaunchKernelGGL(seg_scatter_kernel<float>, grid, dim3(256), 0, st, ptr, idx, (const float*)val, nrows, shift,
+                       cnt, first, uptr, seg);
+  else
+    hipLaunchKernelGGL(seg_scatter_kernel<double>, grid, dim3(256), 0, st, ptr, idx, (const double*)val, nrows,
+                       shift, cnt, first, uptr, seg);
+  return hipGetLastError();
+}
+
+hipError_t seg_table(const int64_t* colptr, const int* rowidx, const int64_t* cnt, const int64_t* uptr, int64_t nrows,
+                     int64_t m, int shift, const int64_t* tptr, uint64_t* T, hipStream_t st) {
+  for (int64_t j0 = 0; j0 < m; j0 += 1 << 20) {   // launches of at most 2^20 columns
+    const int64_t nj = std::min<int64_t>(m - j0, 1 << 20);
+    hipLaunchKernelGGL(seg_table_kernel, dim3((unsigned)nj), dim3(256), 0, st, colptr, rowidx, cnt, uptr, nrows, shift,
+                       j0, tptr, T);
+  }
+  return hipGetLastError();
+}
+
+hipError_t csc_weight(const int* rowidx, const void* valT, int f32, const double* w, int64_t nnz, double* sw,
+                      hipStream_t st) {
+  if (nnz <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(nnz, 256), 65536);
+  if (f32)
+    hipLaunchKernelGGL(csc_weight_kernel<float>, dim3(grid), dim3(256), 0, st, rowidx, (const float*)valT, w, nnz, sw);
+  else
+    hipLaunchKernelGGL(csc_weight_kernel<double>, dim3(grid), dim3(256), 0, st, rowidx, (const double*)valT, w, nnz,
+                       sw);
+  return hipGetLastError();
+}
+
+hipError_t launch_sparse_gram_seg(const int64_t* colptr, const double* sw, const int64_t* tptr, const uint64_t* T,
+                                  const uint64_t* seg, int f32, int64_t m, int shift, double* G, int64_t ldg,
+                                  hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  if (shift > 12 || shift < 7) return hipErrorInvalidValue;
+  const int64_t BS = (int64_t)1 << shift;
+  int64_t j0 = 0;
+  while (j0 < m) {
+    int64_t j1 = j0;
+    while (j1 < m && sparse_gram_items(j0, j1 + BS, shift) < ((int64_t)1 << 30)) j1 += BS;
+    if (j1 == j0) j1 = j0 + BS;
+    const int64_t items = sparse_gram_items(j0, j1, shift);
+    if (f32)
+      hipLaunchKernelGGL(sparse_gram_seg_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr, T,
+                         seg, m, shift, j0, G, ldg);
+    else
+      hipLaunchKernelGGL(sparse_gram_seg_kernel<double>, dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr, T,
+                         seg, m, shift, j0, G, ldg);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    j0 = j1;
+  }
+  return hipSuccess;
+}
+
 // SCS_SPARSE_GRAM_KERNEL (read per call: A/B and the bit-identity test): 1 the one-round-trip-per-8-
 // rows kernel; 2 / 3: the pipelined kernel, 32 / 64 rows per batch, items j-major; 4 / 5: the same,
 // items b-major (concurrent waves share a 4096-row block of the Gram-blocked CSR copy); 6: the
 // flat-issue walk above (r04 default; 5 where the copy has 2^31 entries or more).  C5-shaped Gram
 // 1733 (1) -> 934 (2) / 794 (3) / 901 (4) / 766 ms (5), profiles/r03/sparse_gram/.
-static int sparse_gram_variant(int64_t entries) {
+int sparse_gram_requested() {   // SCS_SPARSE_GRAM_KERNEL, default 8 (the host builds its structure)
   const char* e = getenv("SCS_SPARSE_GRAM_KERNEL");
-  const int v = e ? atoi(e) : 6;
-  return (v == 6 && entries >= ((int64_t)1 << 31)) ? 5 : v;   // variant 6: 32-bit segment positions
+  return e ? atoi(e) : 8;
+}
+// the variant launch_sparse_gram (the Gram-blocked copy's walks) runs: 8 falls back to 6 there
+static int sparse_gram_variant(int64_t entries) {
+  int v = sparse_gram_requested();
+  if (v == 8) v = 6;
+  return (v >= 6 && entries >= ((int64_t)1 << 31)) ? 5 : v;   // variants 6, 7: 32-bit segment positions
 }
 
 const char* sparse_gram_kernel_name(int f32, int64_t entries) {
   const int var = sparse_gram_variant(entries);
   if (var == 1) return f32 ? "sparse_gram_kernel<float>" : "sparse_gram_kernel<double>";
   if (var == 6) return f32 ? "sparse_gram_flat_kernel<float>" : "sparse_gram_flat_kernel<double>";
+  if (var == 7) return f32 ? "sparse_gram_db_kernel<float>" : "sparse_gram_db_kernel<double>";
   static const char* names[2][4] = {
       {"sparse_gram_pipe_kernel<double, 32, false>", "sparse_gram_pipe_kernel<double, 64, false>",
        "sparse_gram_pipe_kernel<double, 32, true>", "sparse_gram_pipe_kernel<double, 64, true>"},
@@ -779,7 +1127,14 @@ hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const vo
     if (j1 == j0) j1 = j0 + BS;
     const int64_t items = sparse_gram_items(j0, j1, shift);
     const int var = sparse_gram_variant(entries);
-    if (var == 6) {
+    if (var == 7) {
+      if (f32)
+        hipLaunchKernelGGL(sparse_gram_db_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
+                           (const float*)valT, bptr, lidx, (const float*)bval, w, nrows, m, shift, j0, G, ldg);
+      else
+        hipLaunchKernelGGL(sparse_gram_db_kernel<double>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
+                           (const double*)valT, bptr, lidx, (const double*)bval, w, nrows, m, shift, j0, G, ldg);
+    } else if (var == 6) {
       if (f32)
         hipLaunchKernelGGL(sparse_gram_flat_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
                            (const float*)valT, bptr, lidx, (const float*)bval, w, nrows, m, shift, j0, G, ldg);
