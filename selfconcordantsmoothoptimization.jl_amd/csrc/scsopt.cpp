@@ -598,6 +598,9 @@ void allreduce(scs_ctx* c, double* buf, int64_t count) {
   tbegin(c, T_REDUCE, &e0);
   if (c->comm_abort && c->comm_abort->load(std::memory_order_acquire))
     fail(c, SCS_ERR_COMM, "the multi-device context's communicators were aborted by a failing device");
+  // fault injection for the abort path's tests: this rank's exchanges fail (read per call)
+  if (const char* fe = std::getenv("SCS_FAULT_EXCHANGE_RANK"))
+    if (c->nranks > 1 && std::atoi(fe) == c->rank) fail(c, SCS_ERR_COMM, "injected exchange failure at rank %d", c->rank);
   if (c->rccl) {   // in place, on the context stream (one fp64 sum per exchange)
     const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->rccl, c->st);
     if (r != ncclSuccess) fail(c, SCS_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));

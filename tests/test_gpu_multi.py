@@ -82,6 +82,26 @@ def test_multi_host_exchange_several_subcontexts(method, ndev, batches):
     assert np.array_equal(np.asarray(again[0].obj), np.asarray(got[0].obj)) and np.array_equal(again[0].x, got[0].x)
 
 
+def test_multi_host_exchange_fault_aborts(monkeypatch):
+    """The abort path of a group (group_run): one sub-context's exchange fails (SCS_FAULT_EXCHANGE_RANK)
+    while the other waits in it; after the grace period the failing worker releases the waiter, the
+    call returns an error instead of hanging, and the group refuses further calls (SCS_ERR_COMM)."""
+    import time
+    x0 = np.random.default_rng(1234).standard_normal(M)
+    p = scsopt.Problem.synthetic(N, M, x0, losses.least_squares(1.0 / N), 2e-3, kind=3, seed=11, devices=[0, 0],
+                                 device_exchange="host")
+    monkeypatch.setenv("SCS_FAULT_EXCHANGE_RANK", "1")
+    t0 = time.time()
+    with pytest.raises(_lib.ScsError):
+        scsopt.iterate(scsopt.ProxLQNSCORE(m=5), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=3, verbose=0)
+    assert time.time() - t0 < 60
+    monkeypatch.delenv("SCS_FAULT_EXCHANGE_RANK")
+    with pytest.raises(_lib.ScsError) as ei:   # the group is broken: destroy it
+        p.fx(x0)
+    assert ei.value.code == _lib.SCS_ERR_COMM
+    p.ctx.close()
+
+
 def test_multi_context_contract():
     ctx = _lib.Context(devices=[0])
     n = C.c_int()
