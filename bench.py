@@ -69,7 +69,7 @@ CONFIGS = {
 }
 
 
-def build_problem(cfg, N, m, comm, local, f32=False, devices=None):
+def build_problem(cfg, N, m, comm, local, f32=False, devices=None, device_exchange="rccl"):
     import numpy as np
     import scsopt
     from scsopt import losses
@@ -94,7 +94,7 @@ def build_problem(cfg, N, m, comm, local, f32=False, devices=None):
     else:
         f, out = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N)
     model = scsopt.Problem.synthetic(N, m, x0, f, 1.0, kind=cfg["kind"], seed=2026, density=0.1, out_fn=out,
-                                     device=local, comm=comm, devices=devices)
+                                     device=local, comm=comm, devices=devices, device_exchange=device_exchange)
     g0 = model.gradx(np.zeros(m))
     if cfg["reg"] == "gl":
         gs = cfg["group"]
@@ -244,6 +244,10 @@ def world_from_env(args, env):
 def check_devices(args, ndev):
     """Fail fast (before any rank starts) when the node has fewer GPUs than ranks, unless
     --share-device was asked for (only with --comm torch: RCCL refuses two ranks on one GPU)."""
+    if getattr(args, "single_process", False) and getattr(args, "device_exchange", "rccl") == "host":
+        if ndev < 1:
+            raise SystemExit("--device-exchange host: no HIP device visible")
+        return   # the host-staged group exchange takes repeated GPUs
     if args.share_device:
         if args.comm != "torch":
             raise SystemExit("--share-device needs --comm torch (RCCL takes one GPU per rank)")
@@ -347,6 +351,10 @@ def main():
     ap.add_argument("--single-process", action="store_true",
                     help="--gpus N from ONE process: a multi-device context (scs_create_multi) splits the rows "
                          "across GPUs 0..N-1 and runs one host thread per device (the Julia drop-in's mode)")
+    ap.add_argument("--device-exchange", choices=("rccl", "host"), default="rccl",
+                    help="--single-process: the group's exchange over RCCL (one GPU per device) or host-staged "
+                         "(SCS_MULTI_HOST_EXCHANGE: --gpus N sub-contexts round-robin over the visible GPUs -- a "
+                         "rehearsal of the group on fewer GPUs, not a scaling number)")
     ap.add_argument("--plumbing-check", action="store_true",
                     help="launch the ranks and check their world wiring over gloo, no GPU work")
     args = ap.parse_args()
@@ -386,7 +394,8 @@ def main():
     ndev = torch.cuda.device_count()
     if world > 1 or single:
         check_devices(args, ndev)
-    devices = list(range(args.gpus)) if single else None
+    host_x = single and args.device_exchange == "host"
+    devices = ([i % max(1, ndev) for i in range(args.gpus)] if host_x else list(range(args.gpus))) if single else None
     if single and (cfg.get("sparse") or cfg["loss"] == "rosenbrock"):
         raise SystemExit("--single-process shards a dense A (c2, c3, c4)")
     dev = local % max(1, ndev) if args.share_device else local
@@ -408,7 +417,8 @@ def main():
     if not cfg.get("sparse") and cfg["loss"] != "rosenbrock":
         # fail fast, before generating anything, when the local shard does not fit this GPU
         plan = memory_plan(cfg, N, m, args.gpus if single else world, gram_cache=args.gram_cache)
-        sharing = -(-world // max(1, ndev)) if args.share_device else 1
+        sharing = (-(-world // max(1, ndev)) if args.share_device
+                   else -(-args.gpus // max(1, ndev)) if host_x else 1)
         free, _total = torch.cuda.mem_get_info(dev)
         if plan["total"] * sharing > 0.97 * free:
             raise SystemExit(f"rank {rank}: {cfg['workload']} N={N} m={m} on {world} rank(s) needs "
@@ -419,7 +429,8 @@ def main():
         if not cfg.get("sparse") or cfg["method"] != "lqn":
             raise SystemExit("--f32-compute applies to the sparse ProxLQNSCORE config (c5)")
         args.f32 = True
-    model, hmu, method = build_problem(cfg, N, m, comm, dev, f32=args.f32, devices=devices)
+    model, hmu, method = build_problem(cfg, N, m, comm, dev, f32=args.f32, devices=devices,
+                                       device_exchange=args.device_exchange)
     if args.f32_compute:
         model.set_compute_f32(True)
     reg = cfg["reg"]
@@ -491,9 +502,11 @@ def main():
                       "f64 (fp32-stored A values)" if args.f32 else "f64"), "data": "synthetic (on-device counter RNG: A ~ N(0,1)/sqrt(m), y from a sparse x_true)",
             "config": {"workload": cfg["workload"], "N": N, "m": m, "lambda": model.λ, "mu": hmu.mu,
                        "method": type(method).__name__, "ss_type": method.ss_type,
-                       "parallelism": (f"row-shard x{args.gpus} (one process, scs_create_multi)" if single
+                       "parallelism": (f"row-shard x{args.gpus} (one process, scs_create_multi"
+                                       + (", host-staged exchange)" if host_x else ")") if single
                                        else f"row-shard x{world}"),
-                       "devices": min(world, ndev) if args.share_device else world,
+                       "devices": (len(set(devices)) if single else min(world, ndev) if args.share_device
+                                   else world),
                        "exchange": (("rccl (libscsopt)" if args.comm == "rccl"
                                      else "torch.distributed callback (gloo)")
                                     + (" forced at one rank" if world == 1 else "")) if comm is not None else None},
@@ -501,6 +514,9 @@ def main():
         if args.share_device and world > ndev:
             line["config"]["shared_device"] = (f"{world} ranks on {ndev} GPU(s): a launcher rehearsal, "
                                                "not a scaling number")
+        if host_x and args.gpus > ndev:
+            line["config"]["shared_device"] = (f"{args.gpus} sub-contexts on {ndev} GPU(s) with the host-staged "
+                                               "exchange: a rehearsal of the multi-device group, not a scaling number")
         if tm["gram_calls"]:
             main_calls = steps                      # one Gram per GGN/NSCORE step; the solver's own
             gram_avg_ms = tm["gram_ms"] / max(1, tm["gram_calls"])   # launches are timed under "solve"
