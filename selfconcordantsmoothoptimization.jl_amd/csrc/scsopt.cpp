@@ -4129,7 +4129,7 @@ struct scs_ctx::HostExchange {
   explicit HostExchange(int n_) : n(n_), slot((size_t)n_), ranks((size_t)n_) {
     for (int i = 0; i < n_; ++i) ranks[(size_t)i] = Rank{this, i, {}};
   }
-  bool wait() {   // false once aborted
+  bool wait() {   // false once aborted, or when the others have not all arrived within 600 s
     std::unique_lock<std::mutex> lk(mu);
     if (aborted) return false;
     const uint64_t g = gen;
@@ -4139,7 +4139,11 @@ struct scs_ctx::HostExchange {
       cv.notify_all();
       return true;
     }
-    cv.wait(lk, [&] { return gen != g || aborted; });
+    if (!cv.wait_for(lk, std::chrono::seconds(600), [&] { return gen != g || aborted; })) {
+      aborted = true;   // a device that never arrives (diverged control flow): release everyone
+      cv.notify_all();
+      return false;
+    }
     return gen != g;
   }
   void abort() {

@@ -1,0 +1,99 @@
+"""GPU: parity at the FULL BASELINE sizes, default code path (no env overrides).
+
+The other default-path tests (tests/test_gpu_default_path.py) run the BASELINE m at reduced N.  Here:
+  * C2 (BASELINE configs[1]: ProxNSCORE logistic (margin) + l1, N = 100000, m = 8192), the whole
+    problem: 2 epochs of the device loop against the oracle's restatement on the downloaded A at rtol
+    1e-8 (obj, fval) -- a full-size trajectory;
+  * C3 (configs[2]: N = 2^20, m = 2^14, A = 128 GiB on the device): the production Gram launch (fused
+    Aᵀv) on 36 column pairs and 8 Aᵀv entries against host fp64 dots of downloaded columns (bound
+    1e-11·Σ|terms|: the summation order differs, a wrong tile / weight / panel is an O(1) error), then
+    two epochs of the default loop (the objective decreases, the iterate is finite);
+  * C5 (configs[4]: sparse A, N = 2^20, m = 2^16, ρ = 0.01, 6.9e8 nonzeros): 3 epochs, then f(x) and
+    ∇f(x) at the final x through the production SpMV kernels against a host SciPy evaluation of the
+    whole downloaded CSR (1e-11 relative on f, 1e-11·Σ|terms| per gradient entry).
+The oracle runs with FAST_LINALG (dsyrk Gram, LU for the QR: the same systems, equal to O(cond·eps)).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import scsopt
+import scsopt_oracle as O
+from scsopt import losses
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def clean_env(monkeypatch):
+    for k in list(os.environ):
+        if k.startswith("SCS_"):
+            monkeypatch.delenv(k)
+    monkeypatch.setattr(O, "FAST_LINALG", True)
+
+
+@pytest.mark.timeout(900)
+def test_c2_full_size_trajectory(clean_env):
+    N, m = 100_000, 8192
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    p = scsopt.Problem.synthetic(N, m, x0, losses.logistic_margin(1.0 / N), 1.0, kind=2, seed=2026)
+    lam = 0.1 * float(np.max(np.abs(p.gradx(np.zeros(m)))))   # bench.py's λ rule
+    p.λ = lam
+    A, y = p.get_data()
+    sol = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=2, x_tol=0.0,
+                         f_tol=0.0, verbose=0)
+    p.ctx.close()
+    om = O.Problem(A, y, x0, O.Loss("logistic_margin", 1.0 / N), lam)
+    osol = O.iterate(O.ProxNSCORE(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=2, x_tol=0.0, f_tol=0.0)
+    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.fval, osol.fval, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+    assert sol.obj[-1] < sol.obj[0]
+
+
+@pytest.mark.timeout(600)
+def test_c3_full_size_gram_and_step(clean_env):
+    N, m = 1 << 20, 1 << 14
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    p = scsopt.Problem.synthetic(N, m, x0, losses.logistic_ce(1.0 / N), 1.0, kind=1, seed=2026,
+                                 out_fn=losses.sigmoid_ce(1.0 / N))
+    p.λ = 0.1 * float(np.max(np.abs(p.gradx(np.zeros(m)))))
+    rng = np.random.default_rng(7)
+    cols = np.sort(rng.choice(m, 8, replace=False))
+    w, v = rng.random(N) + 0.5, rng.standard_normal(N)
+    pairs = [(int(i), int(j)) for a, i in enumerate(cols) for j in cols[a:]]
+    g, atv, fused = p.gram_atv_sample(w, v, pairs)
+    assert fused   # the production configuration at this shape: 256 x 128 tiles with the fused Aᵀv
+    Ac = p.get_columns(cols)
+    k = {int(c): n for n, c in enumerate(cols)}
+    for (i, j), gv in zip(pairs, g):
+        a, b = Ac[:, k[i]], Ac[:, k[j]]
+        assert abs(gv - float((a * w) @ b)) <= 1e-11 * float(np.abs(a * w * b).sum())
+    assert np.all(np.abs(atv[cols] - Ac.T @ v) <= 1e-11 * (np.abs(Ac).T @ np.abs(v)))
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=2, x_tol=0.0,
+                         f_tol=0.0, verbose=0)
+    # obj holds the pre-step objective of each epoch (+ the duplicated last push): obj[1] is f + λg at x1
+    assert sol.epochs == 2 and np.all(np.isfinite(sol.x)) and sol.obj[1] < sol.obj[0]
+    p.ctx.close()
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_size_f_and_gradient(clean_env):
+    N, m = 1 << 20, 1 << 16
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    p = scsopt.Problem.synthetic_sparse(N, m, x0, losses.least_squares(1.0 / N), 1e-4, density=0.01, seed=2026,
+                                        C_set=[-1.0, 1.0])
+    sol = scsopt.iterate(scsopt.ProxLQNSCORE(m=20), p, "indbox", scsopt.PHuberSmootherIndBox(-1.0, 1.0, 0.6),
+                         max_epoch=3, x_tol=0.0, f_tol=0.0, verbose=0)
+    x = sol.x
+    f_dev, g_dev = p.fx(x), p.gradx(x)
+    A, y = p.get_sparse()
+    p.ctx.close()
+    scale = 1.0 / N
+    r = A @ x - y
+    f_ref = 0.5 * scale * float(r @ r)
+    g_ref = scale * (A.T @ r)
+    assert abs(f_dev - f_ref) <= 1e-11 * abs(f_ref)
+    assert np.all(np.abs(g_dev - g_ref) <= 1e-11 * scale * (abs(A).T @ np.abs(r)) + 1e-300)
