@@ -8,6 +8,9 @@ The other default-path tests (tests/test_gpu_default_path.py) run the BASELINE m
     Aᵀv) on 36 column pairs and 8 Aᵀv entries against host fp64 dots of downloaded columns (bound
     1e-11·Σ|terms|: the summation order differs, a wrong tile / weight / panel is an O(1) error), then
     two epochs of the default loop (the objective decreases, the iterate is finite);
+  * C4's per-rank shape at 8 GPUs (configs[3]: N = 2^22 / 8 = 2^19 rows, m = 2^15, least squares +
+    sparse-group lasso, 1024 groups of 32; A = 128 GiB): the production Gram sampled like C3, then two
+    epochs of the default loop (objective decreases, group-aligned support);
   * C5 (configs[4]: sparse A, N = 2^20, m = 2^16, ρ = 0.01, 6.9e8 nonzeros): 3 epochs, then f(x) and
     ∇f(x) at the final x through the production SpMV kernels against a host SciPy evaluation of the
     whole downloaded CSR (1e-11 relative on f, 1e-11·Σ|terms| per gradient entry).
@@ -76,6 +79,37 @@ def test_c3_full_size_gram_and_step(clean_env):
                          f_tol=0.0, verbose=0)
     # obj holds the pre-step objective of each epoch (+ the duplicated last push): obj[1] is f + λg at x1
     assert sol.epochs == 2 and np.all(np.isfinite(sol.x)) and sol.obj[1] < sol.obj[0]
+    p.ctx.close()
+
+
+@pytest.mark.timeout(600)
+def test_c4_rank_shape_gram_and_steps(clean_env):
+    N, m, gs, mu = 1 << 19, 1 << 15, 32, 1e-2
+    ng = m // gs
+    x0 = np.random.default_rng(1234).standard_normal(m)
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1.0, kind=3, seed=2026,
+                                 out_fn=losses.linear_ls(1.0 / N))
+    g0 = p.gradx(np.zeros(m))
+    p.λ = [1e-8, 0.1 * float(np.max(np.linalg.norm(g0.reshape(ng, gs), axis=1)))]
+    ind = np.array([[1 + gs * g for g in range(ng)], [gs * (g + 1) for g in range(ng)], [1] * ng])
+    p.P = scsopt.get_P(m, np.arange(1, m + 1), ind)
+    rng = np.random.default_rng(11)
+    cols = np.sort(rng.choice(m, 8, replace=False))
+    w, v = rng.random(N) + 0.5, rng.standard_normal(N)
+    pairs = [(int(i), int(j)) for a, i in enumerate(cols) for j in cols[a:]]
+    g, atv, fused = p.gram_atv_sample(w, v, pairs)
+    assert fused
+    Ac = p.get_columns(cols)
+    k = {int(c): n for n, c in enumerate(cols)}
+    for (i, j), gv in zip(pairs, g):
+        a, b = Ac[:, k[i]], Ac[:, k[j]]
+        assert abs(gv - float((a * w) @ b)) <= 1e-11 * float(np.abs(a * w * b).sum())
+    assert np.all(np.abs(atv[cols] - Ac.T @ v) <= 1e-11 * (np.abs(Ac).T @ np.abs(v)))
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "gl", scsopt.PHuberSmootherGL(mu, p), max_epoch=2, x_tol=0.0,
+                         f_tol=0.0, verbose=0)
+    assert sol.epochs == 2 and np.all(np.isfinite(sol.x)) and sol.obj[1] < sol.obj[0]
+    z = (sol.x.reshape(ng, gs) == 0)
+    assert np.array_equal(z.all(axis=1), z.any(axis=1))   # the group prox zeroes whole groups only
     p.ctx.close()
 
 
