@@ -13,6 +13,6 @@ line c2 --config c2 --steps 10 --warmup 2 && line c5 --config c5 && line c5_f32 
   && line c5_f32compute --config c5 --f32-compute && line c5ggn --config c5ggn --steps 2 --warmup 1 --no-cpu-baseline \
   && line c4half_cache --config c4 --N 524288 --gram-cache --steps 5 --warmup 1 --no-cpu-baseline || exit 1
 T=$O/chol_trace; mkdir -p $T
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $T/rp -o run -- ./tools/probes/bin/probe_chol_new > $T/probe.log 2>&1 || { tail $T/probe.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $T/rp -o run -- ./tools/probes/bin/probe_chol_c12 > $T/probe.log 2>&1 || { tail $T/probe.log; exit 1; }
 python3 tools/trace_chol_factor.py $T/rp/run_kernel_trace.csv > $T/trace_summary.txt && cat $T/trace_summary.txt
 rm -rf $T/rp
