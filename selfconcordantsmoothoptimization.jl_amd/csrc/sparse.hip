@@ -725,122 +725,6 @@ __global__ __launch_bounds__(64) void sparse_gram_flat_kernel(const int64_t* __r
   for (int i = lane; i < nr; i += 64) col[i] = acc[i];
 }
 
-// Variant 7 (r04): variant 6 software-pipelined by half-batches.  In variant 6 a wave issues a
-// batch's segment loads, then waits out one memory latency before its adds can start, then issues
-// the next batch's loads only after the adds: latency and issue alternate.  Here each metadata
-// batch of 62 rows is cut into two halves of 31 rows with their own registers, and the loads of the
-// next half are issued before the adds of the current one (the register budget of variant 6's
-// 64-row batch), so a half's memory latency runs under the previous half's adds.  31 rows = 62
-// loads in flight: the most vmcnt (6 bits) can wait past, so the current half's adds never wait for
-// the next half's loads.  Same products in the same row order: G bitwise variant 5's.
-template <typename VT>
-__global__ __launch_bounds__(64) void sparse_gram_db_kernel(const int64_t* __restrict__ colptr,
-                                                            const int* __restrict__ rowidx,
-                                                            const VT* __restrict__ valT,
-                                                            const int64_t* __restrict__ bptr,
-                                                            const uint16_t* __restrict__ lidx,
-                                                            const VT* __restrict__ bval,
-                                                            const double* __restrict__ w, int64_t nrows,
-                                                            int64_t m, int shift, int64_t j0,
-                                                            double* __restrict__ G, int64_t ldg) {
-  constexpr int PR = 62, H = 31;   // rows per metadata batch, per half
-  __shared__ double acc[1 << 12];
-  const int lane = threadIdx.x;
-  const int BS = 1 << shift;
-  const int64_t t = (int64_t)blockIdx.x;
-  const int64_t J0 = j0 >> shift;
-  int64_t J = J0, base = 0;
-  while (true) {
-    const int64_t n = (int64_t)BS * (J + 1);
-    if (t < base + n) break;
-    base += n;
-    ++J;
-  }
-  const int64_t loc = t - base;
-  const int64_t j = J * BS + loc % BS;   // items b-major within a column block
-  const int b = (int)(loc / BS);
-  if (j >= m) return;
-  for (int i = lane; i < BS; i += 64) acc[i] = 0.0;
-  __syncthreads();
-  const int64_t p0 = colptr[j], p1 = colptr[j + 1];
-  const int64_t boff = (int64_t)b * nrows;
-  auto stage1 = [&](int64_t p, int& r, double& a) {   // lane u < PR: row p + u
-    if (lane < PR && p + lane < p1) {
-      r = rowidx[p + lane];
-      a = (double)valT[p + lane];
-    } else {
-      r = -1;
-      a = 0.0;
-    }
-  };
-  auto stage2 = [&](int r, double a, double& s, int& st, int& ln) {
-    if (r >= 0) {
-      s = w[r] * a;
-      const int64_t s0 = bptr[boff + r], s1 = bptr[boff + r + 1];
-      st = (int)s0;
-      ln = (int)(s1 - s0);
-    } else {
-      s = 0.0;
-      st = ln = 0;
-    }
-  };
-  // the first 64 entries of rows h·H .. h·H + H - 1 of a metadata batch (st, ln per lane = row)
-  auto load_half = [&](int stv, int lnv, int h, double* v, int* ix) {
-#pragma unroll
-    for (int u = 0; u < H; ++u) {
-      const int su = __builtin_amdgcn_readlane(stv, h * H + u), lu = __builtin_amdgcn_readlane(lnv, h * H + u);
-      const int q = lane < lu ? su + lane : 0;
-      v[u] = (double)bval[q];
-      ix[u] = lidx[q];
-    }
-  };
-  // rows in order; a lane past its segment adds -0.0 into slot `lane` (x + (-0.0) == x)
-  auto add_half = [&](double sv, int stv, int lnv, int h, const double* v, const int* ix, auto lng) {
-    constexpr bool LONG = decltype(lng)::value;   // a row of this batch has more than 64 entries
-#pragma unroll
-    for (int u = 0; u < H; ++u) {
-      const double su_s = sg_bcast(sv, h * H + u);
-      const int lu = __builtin_amdgcn_readlane(lnv, h * H + u);
-      const bool on = lane < lu;
-      atomicAdd(&acc[on ? ix[u] : lane], on ? su_s * v[u] : -0.0);
-      if (LONG && lu > 64) {   // the rest of this row before the next row
-        const int su = __builtin_amdgcn_readlane(stv, h * H + u);
-        for (int q = 64 + lane; q - lane < lu; q += 64)
-          if (q < lu) atomicAdd(&acc[lidx[su + q]], su_s * (double)bval[su + q]);
-      }
-    }
-  };
-  int rc, rn;
-  double ac, an, s, sN;
-  int st, ln, stN, lnN;
-  stage1(p0, rc, ac);
-  stage2(rc, ac, s, st, ln);
-  stage1(p0 + PR, rn, an);
-  double va[H], vb[H];
-  int ia[H], ib[H];
-  load_half(st, ln, 0, va, ia);
-  for (int64_t p = p0; p < p1; p += PR) {
-    stage2(rn, an, sN, stN, lnN);
-    stage1(p + 2 * PR, rn, an);
-    const bool longseg = __builtin_amdgcn_ballot_w64(ln > 64) != 0;   // lanes >= PR: ln = 0
-    load_half(st, ln, 1, vb, ib);         // second half of this batch in flight ...
-    if (longseg) add_half(s, st, ln, 0, va, ia, std::true_type{});   // ... under the first half's adds
-    else add_half(s, st, ln, 0, va, ia, std::false_type{});
-    if (p + PR < p1) load_half(stN, lnN, 0, va, ia);   // the next batch's first half
-    if (longseg) add_half(s, st, ln, 1, vb, ib, std::true_type{});
-    else add_half(s, st, ln, 1, vb, ib, std::false_type{});
-    s = sN;
-    st = stN;
-    ln = lnN;
-  }
-  __syncthreads();
-  const int64_t r0 = (int64_t)b * BS;
-  const int64_t rend = ((j >> 7) + 1) << 7;
-  const int64_t nr = (rend - r0 < BS) ? rend - r0 : BS;
-  double* col = G + j * ldg + r0;
-  for (int i = lane; i < nr; i += 64) col[i] = acc[i];
-}
-
 // ---- variant 8 (r04): the walk on a per-triple table and interleaved segments ----------------------
 // The PMC passes of variant 6 (profiles/r04/pmc_sgram/) put its fabric reads at 5.1e12 B per Gram
 // (2 x FETCH_SIZE, the gfx950 rule) in 695 ms -- ~7.4 TB/s, i.e. the walk is bandwidth-bound -- about
@@ -1079,15 +963,14 @@ int sparse_gram_requested() {   // SCS_SPARSE_GRAM_KERNEL, default 8 (the host b
 // the variant launch_sparse_gram (the Gram-blocked copy's walks) runs: 8 falls back to 6 there
 static int sparse_gram_variant(int64_t entries) {
   int v = sparse_gram_requested();
-  if (v == 8) v = 6;
-  return (v >= 6 && entries >= ((int64_t)1 << 31)) ? 5 : v;   // variants 6, 7: 32-bit segment positions
+  if (v >= 6) v = 6;   // 8 (and the dropped 7) fall back to 6 on the Gram-blocked copy
+  return (v == 6 && entries >= ((int64_t)1 << 31)) ? 5 : v;   // variant 6: 32-bit segment positions
 }
 
 const char* sparse_gram_kernel_name(int f32, int64_t entries) {
   const int var = sparse_gram_variant(entries);
   if (var == 1) return f32 ? "sparse_gram_kernel<float>" : "sparse_gram_kernel<double>";
   if (var == 6) return f32 ? "sparse_gram_flat_kernel<float>" : "sparse_gram_flat_kernel<double>";
-  if (var == 7) return f32 ? "sparse_gram_db_kernel<float>" : "sparse_gram_db_kernel<double>";
   static const char* names[2][4] = {
       {"sparse_gram_pipe_kernel<double, 32, false>", "sparse_gram_pipe_kernel<double, 64, false>",
        "sparse_gram_pipe_kernel<double, 32, true>", "sparse_gram_pipe_kernel<double, 64, true>"},
@@ -1127,14 +1010,7 @@ hipError_t launch_sparse_gram(const int64_t* colptr, const int* rowidx, const vo
     if (j1 == j0) j1 = j0 + BS;
     const int64_t items = sparse_gram_items(j0, j1, shift);
     const int var = sparse_gram_variant(entries);
-    if (var == 7) {
-      if (f32)
-        hipLaunchKernelGGL(sparse_gram_db_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
-                           (const float*)valT, bptr, lidx, (const float*)bval, w, nrows, m, shift, j0, G, ldg);
-      else
-        hipLaunchKernelGGL(sparse_gram_db_kernel<double>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
-                           (const double*)valT, bptr, lidx, (const double*)bval, w, nrows, m, shift, j0, G, ldg);
-    } else if (var == 6) {
+    if (var == 6) {
       if (f32)
         hipLaunchKernelGGL(sparse_gram_flat_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, rowidx,
                            (const float*)valT, bptr, lidx, (const float*)bval, w, nrows, m, shift, j0, G, ldg);

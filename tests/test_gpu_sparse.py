@@ -283,10 +283,10 @@ def test_sparse_gram_priced_by_nnz(f32, monkeypatch):
     g, p2 = p.ctx.kernel_names()
     assert g.startswith("sparse_gram_seg_kernel<")
     # every variant (the one-round-trip-per-8-rows kernel, the pipelined one at 32 / 64 rows per
-    # batch, j- or b-major items, r03's default 5, the flat-issue walks 6 / 7 on the Gram-blocked copy)
+    # batch, j- or b-major items, r03's default 5, the flat-issue walk 6 on the Gram-blocked copy)
     # accumulates the same products in the same row order as the table-driven walk on the segment
     # records (8, r04 default): bitwise G
-    for var in ("6", "7", "5", "2", "3", "4", "1"):
+    for var in ("6", "5", "2", "3", "4", "1"):
         monkeypatch.setenv("SCS_SPARSE_GRAM_KERNEL", var)
         assert np.array_equal(p.gram(w), G), var
     assert p.ctx.kernel_names()[0].startswith("sparse_gram_kernel<")
