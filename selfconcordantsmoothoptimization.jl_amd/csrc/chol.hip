@@ -645,6 +645,14 @@ static unsigned bulk_skip_mask(int nblk) {
 
 static hipError_t create_bulk_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
 
+// SCS_CHOL_SKIP_MAXTILES (A/B; unset = no limit): bulk launches of more tiles than this run on every
+// CU (skip set 0) -- the bulk-bound early outer blocks -- and only the smaller ones keep the skip set
+static unsigned bulk_skip_for(const CholAux* a, int ntiles) {
+  const char* e = getenv("SCS_CHOL_SKIP_MAXTILES");
+  if (e && ntiles > atoi(e)) return 0u;
+  return a->bskip;
+}
+
 // The bulk stream's bounded launches take counter sets from a->bctr in turn, each zero when taken
 // (r04: a 9-counter memset in front of every bounded launch was 38 fill kernels, 0.21 ms of the
 // bulk stream, per m = 8192 factor -- profiles/r03/chol/trace_end/).  All bounded launches run on
@@ -773,7 +781,8 @@ static hipError_t strip_solve(double* G, int64_t ld, const double* W, const Chol
       hipError_t ez = hipSuccess;
       unsigned* ctr = bulk_ctr(a, st, &ez);
       if (ez != hipSuccess) return ez;
-      return gram_launch_bounded(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, ctr, a->bskip, a->bslots,
+      return gram_launch_bounded(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, ctr, bulk_skip_for(a, ntiles),
+                                 a->bslots,
                                  st, true);
     }
     return gram_launch_gen(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, st);
@@ -1245,7 +1254,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
       unsigned* ctr = bulk_ctr(a, a->st2, &e);
       if (e == hipSuccess)
         e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n2a,
-                                ntri - n2a, trail, ld, 2 | 4, ctr, a->bskip, a->bslots, a->st2, true);
+                                ntri - n2a, trail, ld, 2 | 4, ctr, bulk_skip_for(a, ntri - n2a), a->bslots, a->st2,
+                                true);
     }
     if (e == hipSuccess) e = hipEventRecord(a->ev2, a->st2);
     if (e != hipSuccess) return e;
