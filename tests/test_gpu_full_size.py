@@ -30,6 +30,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def clean_env(monkeypatch):
+    import gc
+    gc.collect()   # contexts left in reference cycles by earlier tests: free their device memory first
     for k in list(os.environ):
         if k.startswith("SCS_"):
             monkeypatch.delenv(k)
