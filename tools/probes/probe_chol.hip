@@ -33,6 +33,19 @@ __global__ void rowsum(const double* G, int64_t n, double* b) {   // b = G * one
   b[i] = s;
 }
 
+// order-independent checksum of the bits of the upper triangle of G (n x n) and of W (n x 128): a
+// wrapping sum of the 64-bit patterns, to compare factor variants bit for bit
+__global__ void bitsum(const double* G, int64_t n, const double* W, unsigned long long* out) {
+  unsigned long long s = 0, t = 0;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n * n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = e / n, r = e % n;
+    if (r <= c) s += __double_as_longlong(G[e]) * (unsigned long long)(e + 1);
+    if (e < n * 128) t += __double_as_longlong(W[e]) * (unsigned long long)(e + 1);
+  }
+  atomicAdd(out, s);
+  atomicAdd(out + 1, t);
+}
+
 int main(int argc, char** argv) {
   // the library's context stream is non-blocking: the factor's (CU-masked, blocking) bulk stream
   // would serialize with the legacy null stream
@@ -100,6 +113,17 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e1, sq)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
       int hinfo; CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost));
       printf("n=%ld factor: %.2f ms (info %d)\n", (long)n, ms, hinfo);
+      if (rep == 0) {
+        unsigned long long* dsum;
+        unsigned long long hs[2];
+        CK(hipMalloc(&dsum, 16));
+        CK(hipMemsetAsync(dsum, 0, 16, sq));
+        hipLaunchKernelGGL(bitsum, dim3(2048), dim3(256), 0, sq, G, n, W, dsum);
+        CK(hipMemcpyAsync(hs, dsum, 16, hipMemcpyDeviceToHost, sq));
+        CK(hipStreamSynchronize(sq));
+        CK(hipFree(dsum));
+        printf("n=%ld bits U %016llx W %016llx\n", (long)n, hs[0], hs[1]);
+      }
       hipLaunchKernelGGL(rowsum, dim3((unsigned)(n / 256)), dim3(256), 0, sq, G0, n, b);
       CK(hipEventRecord(e0, sq));
       CK(scs::chol_solve(G, n, n, W, b, y, &aux, sq));
