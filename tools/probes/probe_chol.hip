@@ -51,7 +51,20 @@ int main(int argc, char** argv) {
   // would serialize with the legacy null stream
   hipStream_t sq;
   CK(hipStreamCreateWithFlags(&sq, hipStreamNonBlocking));
-  for (int64_t n : {(int64_t)8192, (int64_t)16384}) {
+  // PROBE_SIZES: comma-separated m values (multiples of 128), default 8192,16384
+  std::vector<int64_t> sizes;
+  {
+    const char* ps = getenv("PROBE_SIZES");
+    const char* q = ps ? ps : "8192,16384";
+    while (*q) {
+      char* end;
+      const long v = strtol(q, &end, 10);
+      if (end == q) break;
+      sizes.push_back(v);
+      q = *end ? end + 1 : end;
+    }
+  }
+  for (int64_t n : sizes) {
     double *G, *G0, *W, *b, *y;
     int* info;
     CK(hipMalloc(&G, n * n * 8)); CK(hipMalloc(&G0, n * n * 8)); CK(hipMalloc(&W, n * 128 * 8));
