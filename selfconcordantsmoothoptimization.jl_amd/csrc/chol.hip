@@ -677,10 +677,18 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   for (int R = 1; R <= 8; ++R)
     for (int j = 0; j < nblk; ++j)
       for (int i = 0; i < R; ++i) rl.push_back(make_int2(i, j));   // bj-major: first R*C = R x C rectangle
+  std::vector<int2> sb;   // 8 x 8 super-blocks of the lower triangle, super-rows ascending
+  for (int R = 0; R < (nblk + 7) / 8; ++R)
+    for (int C = 0; C <= R; ++C)
+      for (int i = 8 * R; i < 8 * R + 8 && i < nblk; ++i)
+        for (int j = 8 * C; j < 8 * C + 8 && j <= i; ++j) sb.push_back(make_int2(i, j));
   hipError_t e = hipMalloc(&a->w, sizeof(double) * hw.size());
   if (e == hipSuccess) e = hipMalloc(&a->rect, sizeof(int2) * rl.size());
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->rect, rl.data(), sizeof(int2) * rl.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !sb.empty()) e = hipMalloc(&a->sbl, sizeof(int2) * sb.size());
+  if (e == hipSuccess && !sb.empty())
+    e = hipMemcpyAsync(a->sbl, sb.data(), sizeof(int2) * sb.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = create_bulk_stream(&a->st2);
   if (e == hipSuccess) e = hipMalloc(&a->bctr, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned));
   if (e == hipSuccess) e = hipMemsetAsync(a->bctr, 0, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned), st);
@@ -726,6 +734,8 @@ void chol_aux_free(CholAux* a) {
   a->sflags = nullptr;
   if (a->bctr) (void)hipFree(a->bctr);
   a->bctr = nullptr;
+  if (a->sbl) (void)hipFree(a->sbl);
+  a->sbl = nullptr;
   if (a->sscr) (void)hipFree(a->sscr);
   a->sscr = nullptr;
   a->serr = nullptr;
@@ -1154,6 +1164,17 @@ static bool c12_split() {
   return !(e && e[0] == '0');
 }
 
+// SCS_CHOL_SBL (read per call; default on, 0 = row-major): the bulk trailing update C12b takes its
+// tiles in 8 x 8 super-blocks (a->sbl) where the slice is exact (8 | 2OB, 8 | nc).  A workgroup
+// takes tile tix of its XCD's contiguous segment, so an XCD's 64 concurrent tiles are one super-block
+// sharing 8 + 8 operand panels instead of one row sharing 1 + 64: at K = 1024 a panel is 1 MiB, so
+// the row-major band re-fetched its A2 panels from HBM.  m = 65536 factor 1498-1510 -> 1427-1436 ms,
+// m = 32768 204.0-204.7 -> 201.8-202.8 ms, U / W bitwise equal (profiles/r04/sbl/).
+static bool chol_sbl() {
+  const char* e = getenv("SCS_CHOL_SBL");
+  return !(e && e[0] == '0');
+}
+
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* a,
                        const int2* trilist, int* info, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
@@ -1252,8 +1273,9 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     }
     if (e == hipSuccess && ntri > n2a) {
       unsigned* ctr = bulk_ctr(a, a->st2, &e);
+      const bool sbo = split && a->sbl && (2 * OB) % 8 == 0 && nc % 8 == 0 && chol_sbl();
       if (e == hipSuccess)
-        e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n2a,
+        e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, (sbo ? a->sbl : trilist) + n2a,
                                 ntri - n2a, trail, ld, 2 | 4, ctr, bulk_skip_for(a, ntri - n2a), a->bslots, a->st2,
                                 true);
     }

@@ -101,6 +101,9 @@ struct CholAux {             // device constants of the two-level factorization 
   // arrival counters, the skipped CU ids (SCS_CHOL_BULK_SKIP), workgroup slots of the device
   // (BCTR_SLOTS sets of 16, zeroed together; each launch takes the next set -- no memset per launch)
   unsigned* bctr = nullptr;
+  // the lower-triangle tile list in 8 x 8 super-blocks (super-rows ascending): rows < 8R are a
+  // prefix, so the bulk update's tiles of rows [2OB, nc) are one slice when 8 divides 2OB and nc
+  int2* sbl = nullptr;
   unsigned bskip = 0;
   int bslots = 0;
   mutable int bslot = 0;   // the next unused counter set

@@ -673,6 +673,31 @@ def test_cholesky_lookahead_bit_identical(m, ob, monkeypatch):
     assert np.array_equal(bits(la.x), bits(ser.x))
 
 
+@pytest.mark.parametrize("m,ob", [(4608, None), (5120, "8")])
+def test_cholesky_superblock_order_bit_identical(m, ob, monkeypatch):
+    """The bulk trailing update's tiles in 8 x 8 super-block order (the default, r04) against
+    row-major order (SCS_CHOL_SBL=0): tile order changes no element's update sequence, so the
+    ProxNSCORE trajectory is bit-identical.  m = 4608 (4-block outer steps: the super-block slice at
+    nc = 32, 24, 16) and m = 5120 with 8-block outer steps (nc = 32, 24)."""
+    if ob:
+        monkeypatch.setenv("SCS_CHOL_OB", ob)
+    N = 4000
+    x0 = np.random.default_rng(37).standard_normal(m) * 0.3
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+
+    def run():
+        p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=31)
+        sol = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+        p.ctx.close()
+        return sol
+
+    ref = run()
+    monkeypatch.setenv("SCS_CHOL_SBL", "0")
+    got = run()
+    assert got.obj == ref.obj and got.epochs == ref.epochs
+    assert np.array_equal(bits(got.x), bits(ref.x))
+
+
 @pytest.mark.parametrize("skip", ["0x20", "0x30", "0xffff"])
 def test_cholesky_bounded_bulk_bit_identical(skip, monkeypatch):
     """The bulk stream's strip solves and trailing updates as CU-bounded persistent launches
