@@ -791,7 +791,11 @@ __global__ void csc_weight_kernel(const int* __restrict__ rowidx, const VT* __re
     sw[p] = w[rowidx[p]] * (double)valT[p];
 }
 
-template <typename VT>
+// DIAG (timing builds, SCS_SPARSE_GRAM_DIAG; G is WRONG): 1 = every atomic to slot `lane` (the same
+// ds_add_f64 count, no bank conflicts), 2 = no LDS accumulation (a register sum per lane) -- to split
+// the walk's time between its loads and its LDS atomics (tools/sgram_diag.py: C5 shape 533 / 538 /
+// 502 ms, profiles/r04/sgdiag/: the loads bound it, not the atomics)
+template <typename VT, int DIAG = 0>
 __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __restrict__ colptr,
                                                              const double* __restrict__ sw,
                                                              const int64_t* __restrict__ tptr,
@@ -835,6 +839,7 @@ __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __re
   };
   double s, sN;
   int st, ln, stN, lnN;
+  double rsum = 0.0;   // DIAG 2
   stage(0, s, st, ln);
   for (int64_t k = 0; k < nj; k += PR) {
     stage(k + PR, sN, stN, lnN);   // the next batch's scaled entries and segment positions
@@ -853,7 +858,9 @@ __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __re
       const double su_s = sg_bcast(s, u);
       const int lu = __builtin_amdgcn_readlane(ln, u);
       const bool on = lane < lu;
-      atomicAdd(&acc[on ? ix[u] : lane], on ? su_s * v[u] : -0.0);
+      if constexpr (DIAG == 2) rsum += on ? su_s * v[u] + (double)ix[u] : 0.0;
+      else if constexpr (DIAG == 1) atomicAdd(&acc[lane], on ? su_s * v[u] + (double)ix[u] : -0.0);
+      else atomicAdd(&acc[on ? ix[u] : lane], on ? su_s * v[u] : -0.0);
     };
     if (!longseg) {
 #pragma unroll
@@ -877,6 +884,7 @@ __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __re
     st = stN;
     ln = lnN;
   }
+  if constexpr (DIAG == 2) acc[lane] = rsum;
   __syncthreads();
   const int64_t r0 = (int64_t)b * BS;
   const int64_t rend = ((j >> 7) + 1) << 7;
@@ -938,9 +946,17 @@ hipError_t launch_sparse_gram_seg(const int64_t* colptr, const double* sw, const
     while (j1 < m && sparse_gram_items(j0, j1 + BS, shift) < ((int64_t)1 << 30)) j1 += BS;
     if (j1 == j0) j1 = j0 + BS;
     const int64_t items = sparse_gram_items(j0, j1, shift);
+    const char* dg = getenv("SCS_SPARSE_GRAM_DIAG");   // timing builds only (wrong G)
+    const int diag = dg ? atoi(dg) : 0;
     if (f32)
       hipLaunchKernelGGL(sparse_gram_seg_kernel<float>, dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr, T,
                          seg, m, shift, j0, G, ldg);
+    else if (diag == 1)
+      hipLaunchKernelGGL((sparse_gram_seg_kernel<double, 1>), dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr,
+                         T, seg, m, shift, j0, G, ldg);
+    else if (diag == 2)
+      hipLaunchKernelGGL((sparse_gram_seg_kernel<double, 2>), dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr,
+                         T, seg, m, shift, j0, G, ldg);
     else
       hipLaunchKernelGGL(sparse_gram_seg_kernel<double>, dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr, T,
                          seg, m, shift, j0, G, ldg);
