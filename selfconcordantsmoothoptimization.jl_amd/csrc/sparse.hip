@@ -794,7 +794,10 @@ __global__ void csc_weight_kernel(const int* __restrict__ rowidx, const VT* __re
 // DIAG (timing builds, SCS_SPARSE_GRAM_DIAG; G is WRONG): 1 = every atomic to slot `lane` (the same
 // ds_add_f64 count, no bank conflicts), 2 = no LDS accumulation (a register sum per lane) -- to split
 // the walk's time between its loads and its LDS atomics (tools/sgram_diag.py: C5 shape 533 / 538 /
-// 502 ms, profiles/r04/sgdiag/: the loads bound it, not the atomics)
+// 502 ms, profiles/r04/sgdiag/: the loads bound it, not the atomics); 3 = as 2 with two rows per load
+// instruction (lanes 0-31 row u, 32-63 row u+1, one 16-B value and one 4-B index load per lane): 425-433
+// ms.  A real walk on that load structure, kept in row order with three LDS atomic instructions per
+// row pair, measured 646 ms (profiles/r04/v9/): the extra atomics and selects cost more than the loads gain
 template <typename VT, int DIAG = 0>
 __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __restrict__ colptr,
                                                              const double* __restrict__ sw,
@@ -844,6 +847,24 @@ __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __re
   for (int64_t k = 0; k < nj; k += PR) {
     stage(k + PR, sN, stN, lnN);   // the next batch's scaled entries and segment positions
     const bool longseg = __builtin_amdgcn_ballot_w64(ln > 64) != 0;
+    if constexpr (DIAG == 3) {   // two rows per load instruction, two entries per lane (no LDS)
+      const int h = lane >> 5, q2 = 2 * (lane & 31);
+#pragma unroll
+      for (int u = 0; u < PR; u += 2) {
+        const int su0 = __builtin_amdgcn_readlane(st, u), su1 = __builtin_amdgcn_readlane(st, u + 1);
+        const int lu0 = __builtin_amdgcn_readlane(ln, u), lu1 = __builtin_amdgcn_readlane(ln, u + 1);
+        const int su = h ? su1 : su0, lu = h ? lu1 : lu0;
+        const char* rec = reinterpret_cast<const char*>(seg + su);
+        const int q = q2 < lu ? q2 : 0;
+        const v2d a = *reinterpret_cast<const v2d*>(reinterpret_cast<const double*>(rec) + q);
+        const uint32_t i2 = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(rec + 8 * seg_vunits(lu, 8)) + q);
+        rsum += a[0] + a[1] + (double)i2;
+      }
+      s = sN;
+      st = stN;
+      ln = lnN;
+      continue;
+    }
     double v[PR];
     int ix[PR];
 #pragma unroll
@@ -884,7 +905,7 @@ __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __re
     st = stN;
     ln = lnN;
   }
-  if constexpr (DIAG == 2) acc[lane] = rsum;
+  if constexpr (DIAG >= 2) acc[lane] = rsum;
   __syncthreads();
   const int64_t r0 = (int64_t)b * BS;
   const int64_t rend = ((j >> 7) + 1) << 7;
@@ -956,6 +977,9 @@ hipError_t launch_sparse_gram_seg(const int64_t* colptr, const double* sw, const
                          T, seg, m, shift, j0, G, ldg);
     else if (diag == 2)
       hipLaunchKernelGGL((sparse_gram_seg_kernel<double, 2>), dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr,
+                         T, seg, m, shift, j0, G, ldg);
+    else if (diag == 3)
+      hipLaunchKernelGGL((sparse_gram_seg_kernel<double, 3>), dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr,
                          T, seg, m, shift, j0, G, ldg);
     else
       hipLaunchKernelGGL(sparse_gram_seg_kernel<double>, dim3((unsigned)items), dim3(64), 0, st, colptr, sw, tptr, T,
