@@ -1,9 +1,10 @@
 #!/bin/bash
 # Variant 9 of the sparse Gram (two rows per load instruction): the sparse GPU tests (bitwise vs
 # variant 8 and the others), the timing builds + both variants at the C5 shape (tools/sgram_diag.py),
-# (Run once with a build that had variant 9, sparse_gram_seg2_kernel: bitwise correct, 646 vs 539 ms,
-# dropped -- profiles/r04/v9/.)
 # and the c5ggn line under each.  Usage: gpu_r04_v9.sh [outdir]
+# (Run twice with builds that had a variant 9, sparse_gram_seg2_kernel -- three half-wave atomics per
+# row pair, then v_permlane32_swap -- both bitwise equal to variant 8 and slower (646 / 570 vs 539 ms),
+# dropped: profiles/r04/v9/, v9b/.)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=${1:-gpurun_out/r04/v9}; mkdir -p $O
