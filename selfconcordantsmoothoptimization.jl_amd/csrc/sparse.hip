@@ -796,8 +796,9 @@ __global__ void csc_weight_kernel(const int* __restrict__ rowidx, const VT* __re
 // the walk's time between its loads and its LDS atomics (tools/sgram_diag.py: C5 shape 533 / 538 /
 // 502 ms, profiles/r04/sgdiag/: the loads bound it, not the atomics); 3 = as 2 with two rows per load
 // instruction (lanes 0-31 row u, 32-63 row u+1, one 16-B value and one 4-B index load per lane): 425-433
-// ms.  A real walk on that load structure, kept in row order with three LDS atomic instructions per
-// row pair, measured 646 ms (profiles/r04/v9/): the extra atomics and selects cost more than the loads gain
+// ms.  Real walks on that load structure, kept in row order (three LDS atomic instructions per row
+// pair; or the rows put back on whole waves by v_permlane32_swap, one atomic per row), measured 646 and
+// 570 ms (profiles/r04/v9/, v9b/): the load-only gain does not survive the accumulation
 template <typename VT, int DIAG = 0>
 __global__ __launch_bounds__(64) void sparse_gram_seg_kernel(const int64_t* __restrict__ colptr,
                                                              const double* __restrict__ sw,
