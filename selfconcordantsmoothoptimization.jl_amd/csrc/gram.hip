@@ -492,35 +492,35 @@ __global__ __launch_bounds__(512, 1) void gram_glds_kernel(
       }
 }
 
-// Scatter packed tiles (list order) into the upper triangle of a column-major
-// m_pad x m_pad matrix (same placement as GRAM_UPPER).
-__global__ void gram_unpack_kernel(const double* __restrict__ P, const int2* __restrict__ tiles,
-                                   double* __restrict__ G, int64_t ldg) {
-  const int t = blockIdx.y;
+// Scatter packed tiles (list order) into the upper triangle of a column-major m_pad x m_pad matrix
+// (same placement as GRAM_UPPER) and the inverse.  A packed slot holds tile element (i, j) at
+// i + 128 j, G holds it at (x·128 + i)·ldg + y·128 + j: a transpose, so each workgroup moves one
+// 64 x 64 quarter through LDS -- reads and writes both along the contiguous index (r04: the
+// element-wise form wrote G with a stride of ldg between lanes; the exchange path's step at C3's
+// per-rank shape lost 1.3 ms with this, profiles/r04/unpack/).  Grid (4 quarters, ntiles), 256 threads.
+template <bool UNPACK>
+__global__ __launch_bounds__(256) void gram_packx_kernel(const double* __restrict__ src, double* __restrict__ dst,
+                                                         const int2* __restrict__ tiles, int64_t ldg) {
+  __shared__ double q[64][65];
+  const int t = blockIdx.y, i0 = 64 * (blockIdx.x & 1), j0 = 64 * (blockIdx.x >> 1);
   const int2 tl = tiles[t];
-  const double* Pt = P + (int64_t)t * GT * GT;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < GT * GT; e += gridDim.x * blockDim.x) {
-    const int j = e / GT, i = e % GT;   // packed: (row i, col j) column-major
-    G[((int64_t)tl.x * GT + i) * ldg + (int64_t)tl.y * GT + j] = Pt[e];
-  }
-}
-
-// The inverse: the upper triangle's 128 x 128 tiles (list order) into packed slots (a Gram formed in
-// place, e.g. the sparse Gram, entering the multi-rank exchange).
-__global__ void gram_pack_kernel(const double* __restrict__ G, int64_t ldg, const int2* __restrict__ tiles,
-                                 double* __restrict__ P) {
-  const int t = blockIdx.y;
-  const int2 tl = tiles[t];
-  double* Pt = P + (int64_t)t * GT * GT;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < GT * GT; e += gridDim.x * blockDim.x) {
-    const int j = e / GT, i = e % GT;
-    Pt[e] = G[((int64_t)tl.x * GT + i) * ldg + (int64_t)tl.y * GT + j];
+  const int64_t slot = (int64_t)t * GT * GT;
+  const int64_t gbase = ((int64_t)tl.x * GT) * ldg + (int64_t)tl.y * GT;
+  const int a = threadIdx.x & 63, b0 = threadIdx.x >> 6;
+  if (UNPACK) {   // packed -> LDS along i, LDS -> G along j
+    for (int b = b0; b < 64; b += 4) q[b][a] = src[slot + (int64_t)(j0 + b) * GT + i0 + a];   // q[j][i]
+    __syncthreads();
+    for (int b = b0; b < 64; b += 4) dst[gbase + (int64_t)(i0 + b) * ldg + j0 + a] = q[a][b];
+  } else {        // G -> LDS along j, LDS -> packed along i
+    for (int b = b0; b < 64; b += 4) q[b][a] = src[gbase + (int64_t)(i0 + b) * ldg + j0 + a];  // q[i][j]
+    __syncthreads();
+    for (int b = b0; b < 64; b += 4) dst[slot + (int64_t)(j0 + b) * GT + i0 + a] = q[a][b];
   }
 }
 
 hipError_t gram_pack_launch(const double* G, int64_t ldg, const int2* tiles, int ntiles, double* P, hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gram_pack_kernel, dim3(16, ntiles), dim3(256), 0, st, G, ldg, tiles, P);
+  hipLaunchKernelGGL(gram_packx_kernel<false>, dim3(4, ntiles), dim3(256), 0, st, G, P, tiles, ldg);
   return hipGetLastError();
 }
 
@@ -1237,7 +1237,8 @@ int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<
 
 hipError_t gram_unpack_launch(const double* P, const int2* tiles, int ntiles, double* G, int64_t ldg,
                               hipStream_t st) {
-  hipLaunchKernelGGL(gram_unpack_kernel, dim3(16, ntiles), dim3(256), 0, st, P, tiles, G, ldg);
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gram_packx_kernel<true>, dim3(4, ntiles), dim3(256), 0, st, P, G, tiles, ldg);
   return hipGetLastError();
 }
 
