@@ -1572,7 +1572,7 @@ void gram_sparse(scs_ctx* c, const double* w, double* out, int packed) {
     const scs_ctx::SegGram& S = c->sgseg;
     HCK(csc_weight(c->rowidx, c->valT, c->sp_f32, w, c->nnz, S.sw, c->st));
     HCK(launch_sparse_gram_seg(c->colptr, S.sw, S.tptr, S.T, S.seg, c->sp_f32, c->m, S.shift, dst, c->mpad, c->st));
-    c->gram_kname = c->sp_f32 ? "sparse_gram_seg_kernel<float>" : "sparse_gram_seg_kernel<double>";
+    c->gram_kname = c->sp_f32 ? "sparse_gram_seg_kernel<float, 0>" : "sparse_gram_seg_kernel<double, 0>";   // rocprofv3's names
     if (packed & 1) HCK(gram_pack_launch(c->G, c->mpad, c->utiles, c->nslots, out, c->st));
     return;
   }
