@@ -24,6 +24,7 @@
 #ifndef SCSOPT_H
 #define SCSOPT_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -199,7 +200,9 @@ int scs_gen_data(scs_ctx* ctx, const scs_synth* spec);
  * data (a new scs_set_data / scs_gen_data / scs_set_sparse drops the test set).  Row-sharded
  * contexts pass their shard of the held-out rows (N local rows of N_global, every rank calls,
  * a rank may hold none); a multi-device context takes the whole set (N_global = N, row0 = 0)
- * and splits it like the data.  A = y = NULL clears the test set.                             */
+ * and splits it like the data.  A = y = NULL clears the test set; exactly one of A, y NULL is the
+ * reference's xor case (only one of Atest / ytest given, iterate.jl:170-171): recorded, and
+ * scs_iterate_ex then raises the reference's UndefVarError at its first stats push.             */
 int scs_set_test_data(scs_ctx* ctx, int64_t N, const double* A, int64_t lda, const double* y,
                       int64_t N_global, int64_t row0);
 /* CSR held-out rows (0-based, m columns; values stored fp64, or fp32 with val_f32 = 1).       */
@@ -337,9 +340,10 @@ typedef struct scs_history {
                        mean_square_error for reg "gl" (rel_kind = 1)       */
   double* objrel;   /* f_rel_error: max(|obj − obj*| / |obj*|, f_tol)       */
   double* times;    /* seconds since the start, millisecond resolution       */
-  double* fvaltest; /* ftest(x) = f(Atest, ytest, x) of every pushed point when the context
-                       holds test data (scs_set_test_*; iterate.jl:169-175, utils.jl:55-57:
-                       one entry per obj entry); may be NULL                   */
+  double* fvaltest; /* (r04) ftest(x) = f(Atest, ytest, x) of every pushed point when the
+                       context holds test data (scs_set_test_*; iterate.jl:169-175,
+                       utils.jl:55-57: one entry per obj entry); may be NULL.  Written only
+                       through scs_iterate_ex, and only when test data is held  */
 } scs_history;
 /* optim_loop! on the device: init! + per epoch f(x) + get_reg(x) + one step!
  * per batch (the full batch, or the scs_set_batches list in order), the
@@ -351,6 +355,16 @@ typedef struct scs_history {
 int scs_iterate(scs_ctx* ctx, const double* x0, const double* x_star, int64_t max_epoch, double x_tol,
                 double f_tol, int rel_kind, double* x_out, const scs_history* hist, int64_t* n_hist,
                 int64_t* epochs);
+/* The same loop with a sized history: hist_size = sizeof(scs_history) as the caller compiled it.
+ * Fields beyond hist_size are taken as NULL, so a caller built against the six-field (r03) layout
+ * is never written past its struct; scs_iterate itself is scs_iterate_ex with the six-field size
+ * (it never touches fvaltest).  A context given exactly one of Atest / ytest (scs_set_test_data
+ * with A or y NULL: the reference's xor case, iterate.jl:170-171) fails with SCS_ERR_REF
+ * "UndefVarError: `ftest` not defined ..." at the loop's first stats push, as the reference's
+ * first show_stat! (:201) does.                                                                 */
+int scs_iterate_ex(scs_ctx* ctx, const double* x0, const double* x_star, int64_t max_epoch, double x_tol,
+                   double f_tol, int rel_kind, double* x_out, const scs_history* hist, size_t hist_size,
+                   int64_t* n_hist, int64_t* epochs);
 
 /* ---- kernel-level entry points (parity tests) --------------------------- */
 /* hμ.grad(Cmat, x), hμ.hess(Cmat, x)                                       */

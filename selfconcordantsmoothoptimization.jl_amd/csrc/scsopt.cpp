@@ -19,6 +19,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -287,6 +288,10 @@ struct scs_ctx {
   struct TestSet {
     NView v;
     bool on = false, host = false;
+    // exactly one of Atest / ytest given: optim_loop! logs "Will skip testing..." and leaves
+    // `ftest` unassigned (iterate.jl:170-171), so its first show_stat! call (:201) raises
+    // UndefVarError -- scs_iterate fails the same way at its first stats push
+    bool xor_case = false;
     int sp_f32 = 0;
     int64_t nnz = 0;
     SpBlk bcsr;
@@ -906,7 +911,7 @@ void free_test(scs_ctx* c) {
   dfree(c, t.val);
   t.nnz = 0;
   t.sp_f32 = 0;
-  t.on = t.host = false;
+  t.on = t.host = t.xor_case = false;
 }
 
 // scs_step on the selected minibatch view: swapped in (and the data-keyed caches dropped) for
@@ -1172,6 +1177,11 @@ double eval_ftest_dev(scs_ctx* c, const double* xh, const double* xd) {
   if (!c->tset.on) fail(c, SCS_ERR_STATE, "no test data: call scs_set_test_data first");
   if (c->tset.host) return cb_eval(c, SCS_CB_FTEST, xh, xd, 1)[0];
   if (c->loss == SCS_LOSS_QUADRATIC) {   // 1/2*(x'*(Atest*x)) + ytest'*x
+    // Atest*x and x' need Atest to be m x m (and ytest length m); Julia raises DimensionMismatch.
+    // The test view holds only its own rows, so a non-square Atest must not reach eval_f_dev
+    if (c->tset.v.Nglob != c->m)
+      fail(c, SCS_ERR_ARG, "DimensionMismatch: the quadratic loss 1/2*(x'*(Atest*x)) + ytest'*x needs an m x m "
+                           "Atest (m = %lld), got %lld rows", (long long)c->m, (long long)c->tset.v.Nglob);
     TestScope ts(c);
     return eval_f_dev(c, xh, xd);
   }
@@ -2814,7 +2824,10 @@ int scs_set_test_data(scs_ctx* c, int64_t N, const double* A, int64_t lda, const
     HCK(hipSetDevice(c->dev));
     free_test(c);
     if (!A && !y) return;   // clears the held-out set
-    if (!A || !y) fail(c, SCS_ERR_ARG, "test data: Atest and ytest are both required (iterate.jl:169-171)");
+    if (!A || !y) {         // the reference's xor case (iterate.jl:170-171): recorded, not an error here
+      c->tset.xor_case = true;
+      return;
+    }
     if (lda < N) fail(c, SCS_ERR_ARG, "test data: lda (%lld) < N (%lld)", (long long)lda, (long long)N);
     (void)row0;
     test_view_dims(c, N, Nglob, false);
@@ -3310,12 +3323,26 @@ int scs_step_grad(scs_ctx* c, const double* x, const double* x_prev, int64_t ite
 // one push per epoch (the pre-step values), the duplicated entry at max_epoch
 // (:219-231) or the post-step entry on termination (:235-247); pri_res_norm[0] is
 // `nothing` (NaN here).  Termination uses the pre-step f_rel_error (:234, :257).
+// scs_iterate: the r03 six-field history (obj .. times) -- fvaltest is never read or written
 int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_epoch, double x_tol, double f_tol,
                 int rel_kind, double* x_out, const scs_history* h, int64_t* n_hist, int64_t* epochs_out) {
+  return scs_iterate_ex(c, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, x_out, h, offsetof(scs_history, fvaltest),
+                        n_hist, epochs_out);
+}
+
+int scs_iterate_ex(scs_ctx* c, const double* x0, const double* x_star, int64_t max_epoch, double x_tol, double f_tol,
+                   int rel_kind, double* x_out, const scs_history* hist, size_t hist_size, int64_t* n_hist,
+                   int64_t* epochs_out) {
+  // the caller's struct as far as it reaches (a shorter, older layout leaves the later fields NULL)
+  scs_history hcopy{};
+  if (hist) std::memcpy(&hcopy, hist, std::min(hist_size, sizeof(scs_history)));
+  const scs_history* h = hist ? &hcopy : nullptr;
   if (is_group(c)) return group_iterate(c, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, x_out, h, n_hist, epochs_out);
   return guarded(c, [&] {
     require_ready(c, true);
     if (!x0 || !x_star || !x_out || !h || !n_hist || !epochs_out) fail(c, SCS_ERR_ARG, "scs_iterate: null argument");
+    if (hist_size < offsetof(scs_history, fvaltest))
+      fail(c, SCS_ERR_ARG, "scs_iterate_ex: hist_size %zu < the six history arrays", hist_size);
     if (max_epoch < 1) fail(c, SCS_ERR_ARG, "scs_iterate: max_epoch must be >= 1");
     HCK(hipSetDevice(c->dev));
     const int64_t m = c->m;
@@ -3392,13 +3419,16 @@ int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_
     const bool tst = c->tset.on;
     const double nan = std::numeric_limits<double>::quiet_NaN();
     auto push = [&](double ob, double fv, double pr, double rl, double fr, double dt, double ft) {
+      if (c->tset.xor_case)   // iterate.jl:170-171 then :201: ftest is unassigned at the first show_stat!
+        fail(c, SCS_ERR_REF, "UndefVarError: `ftest` not defined (only one of Atest / ytest was given: "
+                             "iterate.jl:170-171 leave ftest unassigned, show_stat! at :201 reads it)");
       h->obj[nh] = ob;
       h->fval[nh] = fv;
       h->pri_res_norm[nh] = pr;
       h->rel[nh] = rl;
       h->objrel[nh] = fr;
       if (h->times) h->times[nh] = dt;
-      if (h->fvaltest) h->fvaltest[nh] = ft;
+      if (tst && h->fvaltest) h->fvaltest[nh] = ft;
       ++nh;
     };
     // init!(method, x): reset the method state (prox-L-BFGS-SCORE.jl:31-36)
@@ -4427,16 +4457,18 @@ int group_iterate(scs_ctx* g, const double* x0, const double* x_star, int64_t ma
   const int rc = group_run(g, [&](scs_ctx* s, int i) {
     double* b = buf[(size_t)i].data();
     scs_history hi{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap, b + 5 * cap, b + 6 * cap};
-    return scs_iterate(s, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, b + 7 * cap, &hi, &nh[(size_t)i],
-                       &ep[(size_t)i]);
+    return scs_iterate_ex(s, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, b + 7 * cap, &hi, sizeof(hi),
+                          &nh[(size_t)i], &ep[(size_t)i]);
   });
   if (rc != SCS_OK) return rc;
   const double* b = buf[0].data();
   const size_t k = (size_t)nh[0];
   double* dst[7] = {h ? h->obj : nullptr, h ? h->fval : nullptr, h ? h->pri_res_norm : nullptr, h ? h->rel : nullptr,
                     h ? h->objrel : nullptr, h ? h->times : nullptr, h ? h->fvaltest : nullptr};
+  int has_test = 0;
+  (void)scs_has_test(g->subs[0], &has_test);
   for (int a = 0; a < 7; ++a)
-    if (dst[a]) std::memcpy(dst[a], b + a * cap, sizeof(double) * k);
+    if (dst[a] && (a < 6 || has_test)) std::memcpy(dst[a], b + a * cap, sizeof(double) * k);
   if (x_out) std::memcpy(x_out, b + 7 * cap, sizeof(double) * m);
   if (n_hist) *n_hist = nh[0];
   if (epochs) *epochs = ep[0];

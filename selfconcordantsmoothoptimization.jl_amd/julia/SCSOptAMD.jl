@@ -86,7 +86,9 @@ function finish_problem(ctx, A, yv, x0, loss, λ, out_fn, scale, L, sol, C_set, 
 end
 
 # Problem(...; Atest, ytest) (problems.jl:27-28,67-68): the held-out rows go to the device; both
-# are required, one alone is the reference's "Will skip testing..." case (iterate.jl:169-171).
+# are required.  One alone is the reference's xor case (iterate.jl:170-171): the model keeps what it
+# was given (so the reference's own optim_loop! takes its xor path and raises by itself at :201), and
+# the device records it, so iterate_device! logs the @info and raises UndefVarError(:ftest) as well.
 # Sharded: this rank's rows of Ntest_global held-out rows starting at global row test_row0.
 function set_test!(model::DeviceProblem, Atest, ytest; Ntest_global::Integer=0, test_row0::Integer=0,
                    val_f32::Bool=false)
@@ -97,7 +99,12 @@ function set_test!(model::DeviceProblem, Atest, ytest; Ntest_global::Integer=0, 
     model.Atest, model.ytest = nothing, nothing
     (Atest === nothing && ytest === nothing) && return model
     if xor(Atest === nothing, ytest === nothing)
-        @info "Both input (Atest) and target (ytest) data are required for testing the model, but only one of these has been provided.\nWill skip testing..."
+        one = zeros(1)
+        chk(ccall((:scs_set_test_data, lib), Cint,
+                  (Ptr{Cvoid}, Int64, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Int64),
+                  ctx, 0, Atest === nothing ? C_NULL : pointer(one), 0, ytest === nothing ? C_NULL : pointer(one),
+                  0, 0), ctx)
+        model.Atest, model.ytest = Atest, ytest
         return model
     end
     yt = Vector{Float64}(vec(ytest))
@@ -484,16 +491,21 @@ function iterate_registered!(method, model, reg_name, hμ, max_epoch, x_tol, f_t
     init_device!(method, model)
     cap = 2 * max_epoch + 1                           # scsopt.h: up to two pushes per epoch
     obj, fval, pri, rel, objrel, tms, ftst = (Vector{Float64}(undef, cap) for _ in 1:7)
-    has_test = model.Atest !== nothing                # iterate.jl:169-175: Solution.fvaltest
+    has_test = model.Atest !== nothing && model.ytest !== nothing   # iterate.jl:169-175: Solution.fvaltest
+    xor_test = xor(model.Atest === nothing, model.ytest === nothing)
+    xor_test && @info "Both input (Atest) and target (ytest) data are required for testing the model, but only one of these has been provided.\nWill skip testing..."
     hist = (pointer(obj), pointer(fval), pointer(pri), pointer(rel), pointer(objrel), pointer(tms),
             has_test ? pointer(ftst) : Ptr{Float64}(C_NULL))
     x_out = similar(model.x0); nh = Ref{Int64}(0); ep = Ref{Int64}(0)
     GC.@preserve obj fval pri rel objrel tms ftst begin
-        chk(ccall((:scs_iterate, lib), Cint,
-                  (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Cint, Ptr{Float64},
-                   Ref{NTuple{7,Ptr{Float64}}}, Ref{Int64}, Ref{Int64}),
-                  model.ctx, model.x0, model.x, max_epoch, x_tol, f_tol, reg_name == "gl" ? 1 : 0, x_out,
-                  hist, nh, ep), model.ctx)
+        rc = ccall((:scs_iterate_ex, lib), Cint,
+                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Cint, Ptr{Float64},
+                    Ref{NTuple{7,Ptr{Float64}}}, Csize_t, Ref{Int64}, Ref{Int64}),
+                   model.ctx, model.x0, model.x, max_epoch, x_tol, f_tol, reg_name == "gl" ? 1 : 0, x_out,
+                   hist, sizeof(NTuple{7,Ptr{Float64}}), nh, ep)
+        # the xor case fails at the first stats push, as show_stat! does at iterate.jl:201
+        (xor_test && rc == SCS_ERR_REF) && throw(UndefVarError(:ftest))
+        chk(rc, model.ctx)
     end
     n = nh[]
     pris = Any[isnan(pri[i]) && i == 1 ? nothing : pri[i] for i in 1:n]

@@ -46,10 +46,14 @@ else:
 
 
 def require_torch_runtime(what):
-    """torch may join the process only when libscsopt is bound to torch's runtime."""
-    if RUNTIME == "rocm" and "torch" not in sys.modules:
-        raise ImportError(f"{what} needs torch, but scsopt was imported first and bound /opt/rocm's HIP runtime; "
-                          "import torch before scsopt in a process that uses torch")
+    """torch may join the process only when libscsopt is bound to torch's runtime.  With RUNTIME ==
+    "rocm" /opt/rocm's HIP runtime is already bound, and a torch imported since (or imported by the
+    caller of `what`) brings its own second copy -- refused either way."""
+    if RUNTIME == "rocm":
+        late = "torch" in sys.modules
+        raise ImportError(f"{what} needs torch, but scsopt was imported first and bound /opt/rocm's HIP runtime"
+                          + (" (torch was imported after scsopt: the process now holds two HIP runtimes)"
+                             if late else "") + "; import torch before scsopt in a process that uses torch")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -136,6 +140,8 @@ _SIGS = {
     "scs_step_grad": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, c_dp, c_dp, c_dp, c_dp]),
     "scs_iterate": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, C.c_double, C.c_double, C.c_int, c_dp,
                               C.POINTER(History), c_i64p, c_i64p]),
+    "scs_iterate_ex": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64, C.c_double, C.c_double, C.c_int, c_dp,
+                                 C.POINTER(History), C.c_size_t, c_i64p, c_i64p]),
     "scs_smoother_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, c_dp]),
     "scs_prox_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_double, C.c_double, c_dp]),
     "scs_gram_eval": (C.c_int, [C.c_void_p, c_dp, c_dp, C.c_int64]),

@@ -175,6 +175,7 @@ def device_optim_loop(method, model, reg_name, hmu, *, alpha=None, max_epoch=100
     if method.name in implemented and method.ss_type == 1 and model.L is None and verbose > 0:
         print("[ Info: Neither L nor α is set for the problem... Now fixing α = 0.5...", file=sys.stderr)
     model.configure(reg_name, hmu)
+    _xor_info(model)                                   # the library raises at the first push
     init_method(method, model)
     m = model.m
     cap = 2 * int(max_epoch) + 1                       # scsopt.h: up to two pushes per epoch
@@ -186,15 +187,30 @@ def device_optim_loop(method, model, reg_name, hmu, *, alpha=None, max_epoch=100
     xs = np.ascontiguousarray(model.x, dtype=np.float64)
     x_out = np.empty(m)
     nh, ep = C.c_int64(), C.c_int64()
-    model.ctx.check(_lib.lib.scs_iterate(model.ctx.h, dptr(x0), dptr(xs), int(max_epoch), float(x_tol), float(f_tol),
-                                         1 if reg_name == "gl" else 0, dptr(x_out), C.byref(h), C.byref(nh),
-                                         C.byref(ep)))
+    model.ctx.check(_lib.lib.scs_iterate_ex(model.ctx.h, dptr(x0), dptr(xs), int(max_epoch), float(x_tol),
+                                            float(f_tol), 1 if reg_name == "gl" else 0, dptr(x_out), C.byref(h),
+                                            C.sizeof(_lib.History), C.byref(nh), C.byref(ep)))
     n = int(nh.value)
     pris = [None if (i == 0 and math.isnan(v)) else float(v) for i, v in enumerate(hist["pri_res_norm"][:n])]
     as_list = lambda k: [float(v) for v in hist[k][:n]]   # noqa: E731
     fvaltest = as_list("fvaltest") if test_model else []
     return Solution(x_out, as_list("obj"), as_list("fval"), pris, fvaltest, as_list("rel"), as_list("objrel"), {},
                     as_list("times"), int(ep.value), model)
+
+
+XOR_INFO = ("Both input (Atest) and target (ytest) data are required for testing the model, but only one of these "
+            "has been provided.\nWill skip testing...")
+XOR_ERROR = ("UndefVarError: `ftest` not defined (only one of Atest / ytest was given: iterate.jl:170-171 leave ftest "
+             "unassigned, show_stat! at :201 reads it)")
+
+
+def _xor_info(model):
+    """iterate.jl:170-171: optim_loop! logs this when exactly one of Atest / ytest is given; its first
+    show_stat! (:201) then raises, since `ftest` was never assigned (the loops below do the same)."""
+    xor = bool(getattr(model, "test_xor", False))
+    if xor:
+        log.info(XOR_INFO)
+    return xor
 
 
 def _show(opt_verbose, label, tag, epoch, obj, fval, pri, rel, dt, ftest=None):
@@ -222,6 +238,7 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
     fvals, pris, objs, rels, frels, times = [], [], [], [], [], []
     fvaltests = []
     test_model = bool(getattr(model, "test_model", False))   # iterate.jl:169-175
+    test_xor = _xor_info(model)
     metric_vals = {k: [] for k in (metrics or {})}
     epochs = 0
     x_star = model.x
@@ -254,7 +271,9 @@ def optim_loop(method, model, reg_name, hmu, *, metrics=None, alpha=None, max_ep
         for k in metric_vals:
             metric_vals[k].append(metrics[k](model, xx))
 
-    def ftest(xx):
+    def ftest(xx):   # evaluated as show_stat!'s argument, before anything is printed or pushed
+        if test_xor:                                  # iterate.jl:201 with ftest unassigned
+            raise _lib.ScsReferenceError(_lib.SCS_ERR_REF, XOR_ERROR)
         return model.ftest(xx) if test_model else None
 
     iend = max(nbatch, 1)

@@ -148,19 +148,31 @@ class Problem:
     def set_test(self, Atest=None, ytest=None, *, Ntest_global=None, row0=0, sparse_f32=False):
         """Atest / ytest: ftest(x) = f(Atest, ytest, x) -- the problem's own f, scale literal
         included -- is pushed into Solution.fvaltest at every stats push.  Both are required; one
-        alone is the reference's "Will skip testing..." case.  Sharded: this rank's rows of the
-        held-out set (Ntest_global rows in all); a devices=[...] problem takes the whole set."""
+        alone is the reference's xor case (iterate.jl:170-171): optim_loop! logs "Will skip
+        testing..." and then, since `ftest` is never assigned, its first show_stat! (:201) raises
+        UndefVarError -- iterate() does the same (scs_iterate_ex / the host loop).  Sharded: this
+        rank's rows of the held-out set (Ntest_global rows in all); a devices=[...] problem takes
+        the whole set."""
         self.ctx.check(_lib.lib.scs_set_test_data(self.ctx.h, 0, None, 0, None, 0, 0))   # clear
         self._cb_test = None
         self.test_model = False
+        self.test_xor = False
         if Atest is None and ytest is None:
-            return
-        if Atest is None or ytest is None:    # iterate.jl:170-171
-            log.info("Both input (Atest) and target (ytest) data are required for testing the model, but only one "
-                     "of these has been provided.\nWill skip testing...")
             return
         if self.generic and getattr(self.f, "kind", None) != "callback":
             raise ValueError("a ProblemGeneric has no test data (problems.jl:5-19)")
+        if Atest is None or ytest is None:    # iterate.jl:170-171: recorded; the loop raises (:201)
+            one = np.zeros(1)
+            self.ctx.check(_lib.lib.scs_set_test_data(self.ctx.h, 0, None if Atest is None else dptr(one), 0,
+                                                      None if ytest is None else dptr(one), 0, 0))
+            self.test_xor = True
+            return
+        if self.f.kind == "quadratic":   # 1/2*(x'*(Atest*x)) + ytest'*x: Julia's DimensionMismatch otherwise
+            shp = Atest.shape if hasattr(Atest, "shape") else np.shape(Atest)
+            nglob = int(Ntest_global) if Ntest_global is not None else int(shp[0])
+            if nglob != self.m or np.size(ytest) != shp[0]:
+                raise ValueError(f"DimensionMismatch: the quadratic loss needs an m x m Atest (m = {self.m}) and "
+                                 f"len(ytest) = m, got Atest {tuple(shp)}")
         if self.f.kind == "callback":
             if self._cb_data is None:
                 raise ValueError("Atest / ytest need a data problem: Problem(A, y, x0, f, λ; Atest, ytest)")
@@ -202,6 +214,7 @@ class Problem:
         spec = _lib.Synth(N_global=int(Ntest), row0=r0 + a, N=b - a, m=self.m, seed=seed, kind=kind, density=density)
         self.ctx.check(_lib.lib.scs_gen_test_data(self.ctx.h, C.byref(spec)))
         self._cb_test = None
+        self.test_xor = False
         self.test_model = True
 
     def ftest(self, x):

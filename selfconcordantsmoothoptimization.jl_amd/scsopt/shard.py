@@ -53,6 +53,7 @@ class Comm:
         self.host_staged = dist.get_backend(group) != "nccl"
         self.force = bool(force)
         self.buf = None
+        self._buf_ctx = None   # the context handle the buffer is bound to
         self._cb = None
         self._ctx = None
 
@@ -98,12 +99,16 @@ class Comm:
         from . import _lib
         n = C.c_int64()
         ctx.check(_lib.lib.scs_reduce_buffer_size(ctx.h, C.byref(n)))
-        if self.buf is not None and self.buf.numel() >= int(n.value):
-            return   # still large enough (a new batch list may need more: Problem.set_batches re-binds)
-        dev = torch.device("cuda", ctx.device) if self.device is None else self.device
-        self.buf = torch.zeros(int(n.value), dtype=torch.float64, device=dev)
+        fits = self.buf is not None and self.buf.numel() >= int(n.value)
+        if fits and self._buf_ctx == ctx.h.value:
+            return   # this context already sums in it (a new batch list may need more: set_batches re-binds)
+        if not fits:
+            dev = torch.device("cuda", ctx.device) if self.device is None else self.device
+            self.buf = torch.zeros(int(n.value), dtype=torch.float64, device=dev)
+        # a Comm reused for a second Problem (a new context) binds the same buffer to it too
         ctx._keep.append(self.buf)
-        ctx.check(_lib.lib.scs_set_reduce_buffer(ctx.h, C.c_void_p(self.buf.data_ptr()), int(n.value)))
+        ctx.check(_lib.lib.scs_set_reduce_buffer(ctx.h, C.c_void_p(self.buf.data_ptr()), int(self.buf.numel())))
+        self._buf_ctx = ctx.h.value
 
     def _callback(self, dev_ptr, count, stream, user):
         try:

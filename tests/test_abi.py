@@ -104,3 +104,20 @@ def test_product_loads_without_torch():
                           capture_output=True, text=True, env=env, timeout=120).stdout
     hip = {ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln}
     assert hip and all(p.startswith(os.environ.get("ROCM_PATH", "/opt/rocm")) or "/rocm" in p for p in hip), hip
+
+
+def test_late_torch_import_is_refused():
+    """`import scsopt; import torch; scsopt.shard.Comm()` -- scsopt bound /opt/rocm's HIP
+    runtime before torch loaded its own, so Comm must refuse even though torch is now in sys.modules."""
+    import subprocess
+    import sys
+    code = ("import scsopt; import torch\n"
+            "try:\n    scsopt.shard.Comm(rank=0, world=1)\n    print('no-error')\n"
+            "except ImportError as e:\n    print('refused' if 'two HIP runtimes' in str(e) else 'other')\n"
+            # the two runtimes' static destructors collide at interpreter exit (free(): invalid
+            # pointer, measured here) -- the very combination the guard exists for; skip them
+            "import os, sys; sys.stdout.flush(); os._exit(0)\n")
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split()[-1] == "refused", out.stdout

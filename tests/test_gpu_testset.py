@@ -143,7 +143,8 @@ def test_callback_loss_test_set():
 
 def test_generated_test_rows_and_skip(caplog):
     """gen_test: the held-out rows are rows [N, N + Nt) of the same generator (same x_true); one of
-    Atest / ytest alone logs the reference's message and records no test history."""
+    Atest / ytest alone logs the reference's message and then raises the reference's UndefVarError at
+    the first stats push (iterate.jl:170-171,201), in both loops and in the multi-device context."""
     N, Nt, m = 2048, 512, 128
     x0 = np.random.default_rng(4).standard_normal(m)
     f, out, of, meth, ometh = _kinds("ggn", N)
@@ -158,11 +159,23 @@ def test_generated_test_rows_and_skip(caplog):
     sol = scsopt.iterate(meth(), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=6, verbose=0)
     osol = O.iterate(ometh(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=6)
     _check(sol, osol)
-    with caplog.at_level(logging.INFO, logger="scsopt"):
-        q = scsopt.Problem(A, y, x0, f, 1e-3, out_fn=out, Atest=Ab[N:])
-    assert "Will skip testing" in caplog.text and not q.test_model
-    s2 = scsopt.iterate(meth(), q, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=3, verbose=0)
-    assert s2.fvaltest == []
+    for kw in ({"Atest": Ab[N:]}, {"ytest": yb[N:]}):
+        for devices in (None, [0]):
+            q = scsopt.Problem(A, y, x0, f, 1e-3, out_fn=out, devices=devices, **kw)
+            assert not q.test_model and q.test_xor
+            for device_loop in (True, False):
+                caplog.clear()
+                with caplog.at_level(logging.INFO, logger="scsopt"):
+                    with pytest.raises(scsopt.ScsReferenceError, match="UndefVarError: `ftest` not defined"):
+                        scsopt.iterate(meth(), q, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=3, verbose=0,
+                                       device_loop=device_loop)
+                assert "Will skip testing" in caplog.text
+        with pytest.raises(O.UndefVarError):
+            O.iterate(ometh(), O.Problem(A, y, x0, of, 1e-3, **kw), "l1", O.PHuberSmootherL1L2(1.0), max_epoch=3)
+    # both given again: the same problem runs (a new set_test clears the xor state)
+    q.set_test(Ab[N:], yb[N:])
+    assert q.test_model and not q.test_xor
+    assert len(scsopt.iterate(meth(), q, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=2, verbose=0).fvaltest) == 3
 
 
 def test_multi_device_context_test_set():

@@ -69,7 +69,7 @@ def _julia_ccalls():
     return calls
 
 
-C_SCALARS = {"Cint": {"int"}, "Int64": {"int64_t"}, "Float64": {"double"}, "UInt64": {"uint64_t"},
+C_SCALARS = {"Cint": {"int"}, "Int64": {"int64_t"}, "Float64": {"double"}, "UInt64": {"uint64_t"}, "Csize_t": {"size_t"},
              "Cuint": {"unsigned"}, "Int32": {"int32_t"}}
 C_POINTEE = {"Float64": "double", "Int64": "int64_t", "Int32": "int32_t", "Cint": "int", "UInt8": "unsigned char"}
 
@@ -112,7 +112,7 @@ def test_every_ccall_matches_the_header():
         seen.add(name)
     # the binding covers the step / loop / comm / sparse entry points a maintainer needs
     for need in ("scs_create", "scs_set_data", "scs_set_sparse", "scs_set_loss", "scs_set_reg", "scs_set_smoother",
-                 "scs_method_init", "scs_step_grad", "scs_iterate", "scs_set_comm", "scs_set_reduce_buffer",
+                 "scs_method_init", "scs_step_grad", "scs_iterate_ex", "scs_set_comm", "scs_set_reduce_buffer",
                  "scs_reduce_buffer_size", "scs_eval_f"):
         assert need in seen, need
 

@@ -241,8 +241,9 @@ def test_set_name_plain_labels():
 def test_oracle_fvaltest_history():
     """iterate.jl:169-175 / utils.jl:55-57: with Atest AND ytest every stats push appends
     ftest(x) = f(Atest, ytest, x) of the pushed point (same f, same scale), so len(fvaltest) ==
-    len(obj), including the duplicated max-epoch push; one of the two alone (the xor case) and a
-    ProblemGeneric record nothing."""
+    len(obj), including the duplicated max-epoch push.  One of the two alone (the xor case,
+    iterate.jl:170-171) logs the @info and leaves `ftest` unassigned, so the first show_stat!
+    (:201) raises UndefVarError; a ProblemGeneric records nothing."""
     A = np.array([[-0.560501, 0.0], [0.0, 1.85278], [-0.0192918, -0.827763], [0.128064, 0.110096],
                   [0.0, -0.251176]])
     y = np.array([-1.0, -1.0, -1.0, 1.0, -1.0])
@@ -259,6 +260,8 @@ def test_oracle_fvaltest_history():
             assert sol.fvaltest[-1] == pytest.approx(loss.f(At, yt, sol.x), rel=1e-12)
         else:   # 2 epoch pushes + the duplicated max-epoch push (iterate.jl:219-231)
             assert len(sol.obj) == 3 and sol.fvaltest[-1] == sol.fvaltest[-2] and sol.obj[-1] == sol.obj[-2]
-    om = O.Problem(A, y, x0, loss, 1.0, Atest=At)
-    assert not om.test_model
-    assert O.iterate(O.ProxNSCORE(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=3).fvaltest == []
+    for kw in ({"Atest": At}, {"ytest": yt}):
+        om = O.Problem(A, y, x0, loss, 1.0, **kw)
+        assert not om.test_model
+        with pytest.raises(O.UndefVarError, match="ftest"):
+            O.iterate(O.ProxNSCORE(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=3)
