@@ -306,20 +306,76 @@ def launch_ranks(n, argv):
     return rc if rc >= 0 else 128 - rc
 
 
+def gather_rank_rows(row, world, dist):
+    """Every rank's record (rows held, its own timed seconds, its timers, what its exchange runs on)
+    on rank 0, in rank order -- the per-rank rows of the JSON line."""
+    if world == 1 or dist is None:
+        return [row]
+    rows = [None] * world
+    dist.all_gather_object(rows, row)
+    return rows
+
+
+def verify_ranks(rows, world, N):
+    """The scaling run checks itself: one row per rank in rank order, the row blocks of
+    shard.row_range tiling [0, N) exactly, and every RCCL communicator counting `world` ranks with
+    its own rank equal to the process's.  Returns the list of problems (empty = consistent)."""
+    bad = []
+    if [r["rank"] for r in rows] != list(range(world)):
+        bad.append(f"rank rows {[r['rank'] for r in rows]} != 0..{world - 1}")
+    edges = [(r["row0"], r["row1"]) for r in rows]
+    if edges and (edges[0][0] != 0 or edges[-1][1] != N or any(a[1] != b[0] for a, b in zip(edges, edges[1:]))):
+        bad.append(f"row blocks {edges} do not tile [0, {N})")
+    for r in rows:
+        c = r.get("comm") or {}
+        if c.get("kind") == "rccl" and (c.get("nranks") != world or c.get("rank") != r["rank"]):
+            bad.append(f"rank {r['rank']}: RCCL communicator reports rank {c.get('rank')} of {c.get('nranks')}, "
+                       f"the launch has {world}")
+    return bad
+
+
 def plumbing_check(world, rank, local, args):
-    """--plumbing-check: the rank processes' world wiring without a GPU (gloo): every rank reports
-    (rank, local, world) and rank 0 prints the gathered list as one JSON line."""
+    """--plumbing-check: the rank processes' wiring without a GPU (gloo), through the same helpers
+    the measured run uses: world and rank, this rank's row block of the config's N (shard.row_range),
+    an in-place SUM all-reduce of a per-rank payload (the exchange's shape, scaled down) checked
+    against its closed form, the MAX-over-ranks of the timed seconds, and the gathered per-rank rows
+    (gather_rank_rows + verify_ranks).  Rank 0 prints one JSON line; any mismatch exits non-zero."""
     import torch
     import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd"))
+    from scsopt.shard import row_range     # pure Python: no HIP runtime is bound
     dist.init_process_group("gloo")
     assert dist.get_world_size() == world and dist.get_rank() == rank
     t = torch.tensor([float(rank), float(local), float(world)])
     got = [torch.zeros(3) for _ in range(world)]
     dist.all_gather(got, t)
+    cfg = CONFIGS[args.config]
+    N = args.N or cfg["N"]
+    r0, r1 = row_range(N, world, rank)
+    n = 4099                                       # payload doubles (odd: no alignment luck)
+    pay = torch.arange(n, dtype=torch.float64) * (rank + 1) + rank
+    dist.all_reduce(pay, op=dist.ReduceOp.SUM)
+    s1 = world * (world + 1) / 2.0
+    want = torch.arange(n, dtype=torch.float64) * s1 + (s1 - world)
+    ok_sum = bool(torch.equal(pay, want))
+    dt = torch.tensor([0.5 + 0.01 * rank], dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    row = {"rank": rank, "local_rank": local, "row0": r0, "row1": r1, "rows": r1 - r0,
+           "comm": {"kind": "callback", "nranks": world, "rank": rank}}
+    rows = gather_rank_rows(row, world, dist)
     dist.barrier()
     if rank == 0:
+        bad = verify_ranks(rows, world, N)
+        if not ok_sum:
+            bad.append("all-reduce SUM mismatch")
+        if abs(float(dt.item()) - (0.5 + 0.01 * (world - 1))) > 1e-12:
+            bad.append("MAX over ranks mismatch")
         print(json.dumps({"plumbing": [[int(v) for v in g.tolist()] for g in got], "gpus": args.gpus,
-                          "comm": args.comm, "backend": "gloo"}))
+                          "comm": args.comm, "backend": "gloo", "config": args.config, "N": N,
+                          "ranks": rows, "allreduce_ok": ok_sum, "max_s": float(dt.item()), "problems": bad}))
+        if bad:
+            dist.destroy_process_group()
+            raise SystemExit("plumbing check FAILED: " + "; ".join(bad))
     dist.destroy_process_group()
 
 
@@ -477,6 +533,15 @@ def main():
     objs = sol.obj
     tm = ctx.timing()
     gram_kname, prod_kname = ctx.kernel_names()
+    cinfo = ctx.comm_info()   # read back from libscsopt: ncclCommCount / ncclCommUserRank, the RCCL loaded
+    r0 = model.row0 if not single else 0
+    my_row = {"rank": rank, "local_rank": local, "device": dev, "row0": int(r0),
+              "row1": int(r0) + int(model.N), "rows": int(model.N), "time_s": dt,
+              "ms_per_step_local": 1e3 * dt / steps,
+              "breakdown_ms_per_step": ({k.replace("_ms", ""): tm[k] / steps for k in tm if k.endswith("_ms")}
+                                        if tevery == 1 else None),
+              "comm": {k: cinfo[k] for k in ("kind", "nranks", "rank")}}
+    rank_rows = gather_rank_rows(my_row, world, dist if comm is not None else None)
     if comm is not None:
         t = torch.tensor([dt], dtype=torch.float64, device="cpu" if gloo else torch.device("cuda", dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -511,6 +576,17 @@ def main():
                                      else "torch.distributed callback (gloo)")
                                     + (" forced at one rank" if world == 1 else "")) if comm is not None else None},
         }
+        line["comm"] = {"kind": cinfo["kind"], "nranks": cinfo["nranks"], "rccl_version": cinfo["rccl_version"],
+                        "rccl_lib": cinfo["rccl_lib"]}
+        if not single:
+            line["ranks"] = rank_rows
+            problems = verify_ranks(rank_rows, world, model.N_global)
+        else:
+            problems = ([] if cinfo["nranks"] == args.gpus or host_x else
+                        [f"the group's RCCL communicator counts {cinfo['nranks']} devices, --gpus {args.gpus}"])
+        line["ranks_consistent"] = not problems
+        if problems:
+            line["ranks_problems"] = problems
         if args.share_device and world > ndev:
             line["config"]["shared_device"] = (f"{world} ranks on {ndev} GPU(s): a launcher rehearsal, "
                                                "not a scaling number")
@@ -673,6 +749,8 @@ def main():
         if isinstance(line.get("cpu_baseline"), dict):
             line["cpu_baseline"]["host"] = host_info()
         print(json.dumps(line))
+        if problems:
+            raise SystemExit("scaling run inconsistent: " + "; ".join(problems))
         if check is not None and not check["pass"]:
             raise SystemExit("full-size parity check FAILED: " + json.dumps(check))
     # release the library context (its streams, a CU-masked one included) before the runtime and

@@ -156,6 +156,19 @@ int scs_set_comm_force(scs_ctx* ctx, int on);
  * on the registered batch list (the sample-space all-gather of batches with
  * N_global + 1 <= m): query it again after scs_set_batches.                 */
 int scs_reduce_buffer_size(scs_ctx* ctx, int64_t* ndoubles);
+/* What the exchange actually runs on, read back from the library (for run records / scaling
+ * checks): *kind = SCS_COMM_NONE / _RCCL (scs_set_comm_rccl) / _CALLBACK (scs_set_comm) /
+ * _GROUP_RCCL (scs_create_multi) / _GROUP_HOST (SCS_MULTI_HOST_EXCHANGE); *nranks / *rank from the
+ * communicator itself (ncclCommCount / ncclCommUserRank for RCCL; the group's device count and 0
+ * for a group; the caller's values for a callback); *rccl_version = ncclGetVersion; lib (cap
+ * bytes, may be NULL) = the path of the RCCL shared object this process resolved ncclAllReduce
+ * from (dladdr).  Any output pointer may be NULL.                                              */
+#define SCS_COMM_NONE 0
+#define SCS_COMM_RCCL 1
+#define SCS_COMM_CALLBACK 2
+#define SCS_COMM_GROUP_RCCL 3
+#define SCS_COMM_GROUP_HOST 4
+int scs_comm_info(scs_ctx* ctx, int* kind, int* nranks, int* rank, int* rccl_version, char* lib, int64_t cap);
 int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
 
 /* ---- user callbacks (Problem(x0, f, λ; grad_fx, hess_fx), problems.jl:44-59; call sites

@@ -272,6 +272,15 @@ hipError_t launch_ls_pair(const double* z0, const double* zd, double alpha, int6
   return hipGetLastError();
 }
 
+// an empty one-wave kernel: a dispatch whose completion timestamp follows everything before it on the
+// stream, including work another library (RCCL) made the stream wait for -- the timers' end marker
+__global__ void marker_kernel() {}
+
+hipError_t launch_marker(hipStream_t st) {
+  hipLaunchKernelGGL(marker_kernel, dim3(1), dim3(64), 0, st);
+  return hipGetLastError();
+}
+
 hipError_t launch_sum_partials(const double* part, int n, double* out, hipStream_t st) {
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, st, part, n, out);
   return hipGetLastError();

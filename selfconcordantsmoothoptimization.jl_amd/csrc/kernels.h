@@ -301,6 +301,7 @@ hipError_t launch_epilogue(int loss, int ggn, int flags, const double* zpart, in
                            double* w, double* v, double* valpart, hipStream_t st);
 // out[0] = Σ part[0..n)  (fixed order)
 hipError_t launch_sum_partials(const double* part, int n, double* out, hipStream_t st);
+hipError_t launch_marker(hipStream_t st);
 // the line search's trial products (incremental form): out[0..Npad) = z0, out[Npad..2 Npad) = α·zd, so
 // the epilogue over these two "partials" forms z0 + α·zd = A x + α·A d
 hipError_t launch_ls_pair(const double* z0, const double* zd, double alpha, int64_t Npad, double* out,

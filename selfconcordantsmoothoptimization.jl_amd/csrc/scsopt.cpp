@@ -609,6 +609,11 @@ void allreduce(scs_ctx* c, double* buf, int64_t count) {
   if (c->rccl) {   // in place, on the context stream (one fp64 sum per exchange)
     const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->rccl, c->st);
     if (r != ncclSuccess) fail(c, SCS_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+    // RCCL's work joins c->st as a stream wait, and an event recorded right after a wait takes the
+    // timestamp of the stream's last dispatch -- before the collective -- so the all-reduce used
+    // to land in the NEXT timer (solve: +7 ms at C3's per-rank shape, profiles/r04/commcmp/).  An
+    // empty dispatch after the wait gives the end event a timestamp behind the collective.
+    if (c->timing) HCK(launch_marker(c->st));
   } else {
     if (!c->ar) fail(c, SCS_ERR_COMM, "multi-rank context without a communicator");
     int rc = c->ar(buf, count, (void*)c->st, c->ar_user);
@@ -4319,6 +4324,48 @@ int scs_create_multi_ex(const int* devs, int ndev, int flags, scs_ctx** out) {
 int scs_group_size(scs_ctx* c, int* ndev) {
   if (!c || !ndev) return SCS_ERR_ARG;
   *ndev = is_group(c) ? (int)c->subs.size() : 1;
+  return SCS_OK;
+}
+
+int scs_comm_info(scs_ctx* c, int* kind, int* nranks, int* rank, int* rccl_version, char* lib, int64_t cap) {
+  if (!c) return SCS_ERR_ARG;
+  int k = SCS_COMM_NONE, n = 1, r = 0;
+  const scs_ctx* s = is_group(c) ? c->subs[0] : c;
+  if (is_group(c)) {
+    k = c->hx ? SCS_COMM_GROUP_HOST : SCS_COMM_GROUP_RCCL;
+    n = (int)c->subs.size();
+    if (!c->hx && s->rccl) {   // the communicator's own view (ncclCommInitAll over the devices)
+      int cn = 0;
+      if (ncclCommCount(s->rccl, &cn) == ncclSuccess) n = cn;
+    }
+  } else if (s->rccl) {
+    k = SCS_COMM_RCCL;
+    int cn = 0, cr = 0;
+    if (ncclCommCount(s->rccl, &cn) != ncclSuccess || ncclCommUserRank(s->rccl, &cr) != ncclSuccess) {
+      c->err = "ncclCommCount / ncclCommUserRank failed";
+      return SCS_ERR_COMM;
+    }
+    n = cn;
+    r = cr;
+  } else if (s->ar) {
+    k = SCS_COMM_CALLBACK;
+    n = s->nranks;
+    r = s->rank;
+  }
+  if (kind) *kind = k;
+  if (nranks) *nranks = n;
+  if (rank) *rank = r;
+  if (rccl_version) {
+    int v = 0;
+    *rccl_version = ncclGetVersion(&v) == ncclSuccess ? v : 0;
+  }
+  if (lib && cap > 0) {
+    Dl_info di{};
+    const char* path = (dladdr((void*)&ncclAllReduce, &di) && di.dli_fname) ? di.dli_fname : "";
+    char real[4096];
+    if (*path && realpath(path, real)) path = real;
+    std::snprintf(lib, (size_t)cap, "%s", path);
+  }
   return SCS_OK;
 }
 

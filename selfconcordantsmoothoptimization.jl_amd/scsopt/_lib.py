@@ -104,6 +104,8 @@ _SIGS = {
     "scs_set_comm_force": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_reduce_buffer_size": (C.c_int, [C.c_void_p, c_i64p]),
     "scs_set_reduce_buffer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "scs_comm_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                C.POINTER(C.c_int), C.c_char_p, C.c_int64]),
     "scs_set_data": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_dp, C.c_int64, c_dp, C.c_int64, C.c_int64]),
     "scs_gen_data": (C.c_int, [C.c_void_p, C.POINTER(Synth)]),
     "scs_get_data": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_dp, C.c_int64, c_dp]),
@@ -248,6 +250,17 @@ class Context:
         g, p = C.create_string_buffer(128), C.create_string_buffer(128)
         self.check(lib.scs_kernel_names(self.h, g, 128, p, 128))
         return g.value.decode(), p.value.decode()
+
+    def comm_info(self):
+        """What the exchange runs on, read back from the library (scs_comm_info): kind, the
+        communicator's own rank count and rank (ncclCommCount / ncclCommUserRank for RCCL), the
+        RCCL version and the path of the RCCL library the process resolved."""
+        k, n, r, v = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        path = C.create_string_buffer(4096)
+        self.check(lib.scs_comm_info(self.h, C.byref(k), C.byref(n), C.byref(r), C.byref(v), path, 4096))
+        kinds = {0: "none", 1: "rccl", 2: "callback", 3: "group_rccl", 4: "group_host"}
+        return {"kind": kinds.get(k.value, str(k.value)), "nranks": n.value, "rank": r.value,
+                "rccl_version": v.value, "rccl_lib": path.value.decode(errors="replace")}
 
     def timing(self):
         t = Timing()

@@ -127,9 +127,10 @@ class Problem:
             N = C.c_int64()
             self.ctx.check(_lib.lib.scs_get_dims(self.ctx.h, C.byref(N), None, None, None))
             self.N = int(N.value)
-        Ng = C.c_int64()
-        self.ctx.check(_lib.lib.scs_get_dims(self.ctx.h, None, None, C.byref(Ng), None))
+        Ng, r0 = C.c_int64(), C.c_int64()
+        self.ctx.check(_lib.lib.scs_get_dims(self.ctx.h, None, None, C.byref(Ng), C.byref(r0)))
         self.N_global = int(Ng.value)   # the rows of all ranks (the minibatch loader's N)
+        self.row0 = int(r0.value)       # this rank's first global row
         if comm is not None and comm.active:
             comm.bind_buffer(self.ctx)
         ggn = ggn_kind(out_fn)

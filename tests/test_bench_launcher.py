@@ -90,3 +90,38 @@ def test_too_few_gpus_exits_nonzero():
 def test_world_mismatch_exits_nonzero():
     r = _bench("--gpus", "4", env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+def test_verify_ranks():
+    rows = [{"rank": r, "row0": a, "row1": b, "comm": {"kind": "rccl", "nranks": 4, "rank": r}}
+            for r, (a, b) in enumerate([(0, 3), (3, 6), (6, 8), (8, 10)])]
+    assert bench.verify_ranks(rows, 4, 10) == []
+    bad = [dict(r) for r in rows]
+    bad[2] = dict(bad[2], comm={"kind": "rccl", "nranks": 1, "rank": 0})   # a communicator of one
+    assert any("RCCL communicator reports rank 0 of 1" in p for p in bench.verify_ranks(bad, 4, 10))
+    gap = [dict(r) for r in rows]
+    gap[1] = dict(gap[1], row1=5)
+    assert any("do not tile" in p for p in bench.verify_ranks(gap, 4, 10))
+    assert bench.verify_ranks(rows[:3], 4, 10)   # a missing rank
+
+
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_eight_rank_plumbing(launcher):
+    """The driver's N=8 SCALE run, rehearsed on CPU with gloo: 8 rank processes (self-launched or
+    under torch.distributed.run, as the driver starts it) form one world, take the C3 row blocks of
+    shard.row_range, sum a payload in place, take the MAX of the timed seconds and gather the
+    per-rank rows through the same helpers the measured run uses (gather_rank_rows / verify_ranks)."""
+    if launcher == "self":
+        r = _bench("--gpus", "8", "--comm", "torch", "--plumbing-check", timeout=400)
+    else:
+        e = dict(os.environ)
+        e.pop("WORLD_SIZE", None)
+        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                            "--master-addr", "127.0.0.1", "--master-port", str(bench.free_port()),
+                            os.path.join(ROOT, "bench.py"), "--gpus", "8", "--comm", "torch", "--plumbing-check"],
+                           capture_output=True, text=True, env=e, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["plumbing"] == [[i, i, 8] for i in range(8)]
+    assert line["allreduce_ok"] and line["problems"] == [] and line["max_s"] == pytest.approx(0.57)
+    assert [x["rows"] for x in line["ranks"]] == [(1 << 20) // 8] * 8
