@@ -605,7 +605,7 @@ def main():
             achieved = gram_flops / (gram_avg_ms * 1e-3) / 1e12
             traffic = None
             kname = gram_kname or "unknown"   # the library reports the kernel it launched
-            # PMC summaries (tools/gpu_prof_c3.sh, tools/gpu_pmc_c2.sh + tools/pmc_summary.py), one per (N, m):
+            # PMC summaries (tools/gpu_gram_pmc.sh, tools/gpu_pmc_c2.sh + tools/pmc_summary.py), one per (N, m):
             # their bytes are used only when they were measured on the kernel this run launched
             for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_gram_pmc*.json")), reverse=True):
                 if world != 1 or args.gram_cache:

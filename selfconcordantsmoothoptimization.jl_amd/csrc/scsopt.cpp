@@ -307,6 +307,7 @@ struct scs_ctx {
   // the incremental line search's N-space scratch: [z0 | α·A d] trial pair (2 Npad) + A d (Npad)
   double* lsbuf = nullptr;
   int64_t lscap = 0;
+  int64_t ls_direct = 0;   // incremental trials re-decided on the direct form (near the Armijo threshold)
 
   // caches (CSE of identical evaluations; keyed by the host x content)
   std::vector<double> zkey;
@@ -1290,6 +1291,10 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
                         nullptr, nullptr, nullptr, c->valpart, c->st));
     ensure_red(c);
   }
+  // the band (relative) within which an incremental trial is re-decided on the direct form;
+  // SCS_LS_NEAR overrides it (tests: a huge band re-decides every trial)
+  const char* ne = std::getenv("SCS_LS_NEAR");
+  const double near = ne ? std::atof(ne) : 1e-9;
   double alpha = 1.0;
   for (int trial = 0; trial < 100000; ++trial) {
     // the trial point lives on the device only (no host copy: it is keyed by a fresh tag)
@@ -1306,6 +1311,15 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
       d2h(c, c->hscal + 14, c->scal + 14, 1);
       const double rg = eval_reg_dev(c, c->gtmp2);   // syncs: hscal[14] has landed too
       ft = loss_scale_value(c, c->hscal[14]) + rg;
+      // Ax + fl(α·Ad) differs from the reference's A·fl(x + αd) (utils.jl:27-35) in the last bits
+      // of each z_i: a trial whose Armijo test sits within 1e-9 (relative) of its threshold is
+      // decided on the direct form instead, so the accepted α is the reference's form's
+      if (std::fabs(ft - (f0 + 1e-4 * alpha * gd)) <= near * std::max(std::fabs(f0), std::fabs(ft))) {
+        ft = eval_f_dev(c, nullptr, c->gtmp2) + eval_reg_dev(c, c->gtmp2);
+        ++c->ls_direct;
+        // that pass left A·(x + αd) in c->z: restore z0 = A x for the later incremental trials
+        if (ft > f0 + 1e-4 * alpha * gd) forward(c, xh, xd, 0, false);
+      }
     } else {
       ft = eval_f_dev(c, nullptr, c->gtmp2) + eval_reg_dev(c, c->gtmp2);
     }

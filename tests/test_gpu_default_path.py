@@ -159,13 +159,23 @@ def test_c5_shape_lqn_sparse(f32, clean_env):
 
 
 @pytest.mark.timeout(600)
-def test_c5_shape_lqn_sparse_fp32_compute(clean_env):
+def test_c5_shape_lqn_sparse_fp32_compute(clean_env, record_property):
     """The fp32-COMPUTE arm (scs_set_compute_f32: fp32 arithmetic in A x, Aᵀ r and the two-loop) on the
-    C5 shape above against the fp64 oracle on the same fp32-stored values.  Stated tolerance: every
-    history entry within rtol 1e-4 of the oracle's objective (an fp32 dot of the ~655 entries of a row
-    is good to ~1e-6 relative; the L-BFGS direction inherits that), x within 1e-2 absolute on the box
-    [-1, 1] (measured on the first run: 2.1e-3 after 10 epochs), the box-active sets identical except
-    for coordinates within 1e-2 of a bound, and the fp32 SpMV kernel is the one that ran."""
+    C5 shape above against the fp64 oracle on the same fp32-stored values.
+
+    Asserted, each bound stated before any run (BASELINE configs[4] is a tolerance STUDY):
+      * every finite history entry within rtol 1e-4 of the oracle's objective -- an fp32 sum of the
+        ~655 terms of a row / ~1300 of a column carries at most n·2⁻²⁴ ≈ 8e-5 relative error
+        (n ≤ 1300), the objective itself is evaluated in fp64 on top of it;
+      * the iterates stay in the box [-1, 1] exactly (the clamp prox, prox-operators.jl:27-46);
+      * the fp32 SpMV kernel is the one that ran.
+    Reported, not asserted (record_property + stdout): max |x_dev − x_oracle|, the count of
+    coordinates whose box-active state differs and their distance to the bound, the worst relative
+    objective gap.  No a-priori bound on x exists here: after 10 L-BFGS epochs neither arm is near
+    the optimum, and the two-loop's curvature pairs amplify the fp32 perturbation by the inverse of
+    the smallest curvature they sample (AᵀA/N ≈ I/m · [0.09, 2.9] at N = 2m), so the
+    x gap is a measured statistic of the study: 2.07e-3 on the r04 box (gpurun_out/r04/t1.log:124),
+    which an earlier version of this test then asserted against a bound fitted to it (r04 verdict)."""
     N, m, rho = 1 << 17, 1 << 16, 0.01
     x0 = np.random.default_rng(1234).standard_normal(m)
     lam, mu = 1e-4, 0.6
@@ -182,9 +192,17 @@ def test_c5_shape_lqn_sparse_fp32_compute(clean_env):
     assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
     fin = [i for i, v in enumerate(osol.obj) if np.isfinite(v)]   # entry 0: x0 outside the box, Inf
     np.testing.assert_allclose(np.array(sol.obj)[fin], np.array(osol.obj)[fin], rtol=1e-4, atol=0)
-    assert np.max(np.abs(sol.x - osol.x)) <= 1e-2
+    assert np.all(sol.x >= -1.0) and np.all(sol.x <= 1.0)
     ad = (np.abs(sol.x) == 1.0) != (np.abs(osol.x) == 1.0)
-    assert np.all(np.minimum(np.abs(np.abs(sol.x) - 1), np.abs(np.abs(osol.x) - 1))[ad] <= 1e-2)
+    dist = np.minimum(np.abs(np.abs(sol.x) - 1), np.abs(np.abs(osol.x) - 1))[ad]
+    stats = {"max_abs_dx": float(np.max(np.abs(sol.x - osol.x))),
+             "active_set_differences": int(ad.sum()),
+             "max_bound_distance_of_differences": float(dist.max()) if dist.size else 0.0,
+             "max_rel_dobj": float(np.max(np.abs(np.array(sol.obj)[fin] - np.array(osol.obj)[fin])
+                                          / np.abs(np.array(osol.obj)[fin])))}
+    for k, v in stats.items():
+        record_property(k, v)
+    print("fp32-compute study (reported):", stats)
 
 
 @pytest.mark.timeout(900)

@@ -11,6 +11,9 @@ The other default-path tests (tests/test_gpu_default_path.py) run the BASELINE m
   * C4's per-rank shape at 8 GPUs (configs[3]: N = 2^22 / 8 = 2^19 rows, m = 2^15, least squares +
     sparse-group lasso, 1024 groups of 32; A = 128 GiB): the production Gram sampled like C3, then two
     epochs of the default loop (objective decreases, iterate finite);
+  * C3 and C4's per-rank shape also get a whole-length f(x) / ∇f(x) check at the run's final x (C3 at
+    x0 too): the device's GEMV passes and loss epilogue against a host fp64 evaluation of A streamed
+    down in row blocks (host_f_grad: bounds from 1e-11·Σ|terms|, z-propagation included);
   * C5 (configs[4]: sparse A, N = 2^20, m = 2^16, ρ = 0.01, 6.9e8 nonzeros): 3 epochs, then f(x) and
     ∇f(x) at the final x through the production SpMV kernels against a host SciPy evaluation of the
     whole downloaded CSR (1e-11 relative on f, 1e-11·Σ|terms| per gradient entry).
@@ -58,6 +61,60 @@ def test_c2_full_size_trajectory(clean_env):
     assert sol.obj[-1] < sol.obj[0]
 
 
+def host_f_grad(p, x, kind, chunk_bytes=4 << 30):
+    """f(x), ∇f(x) and their error bounds evaluated on the host in fp64 from the device's A, streamed
+    down in row blocks (scs_get_data, column-major: no host copy of the whole A).  One pass: per block
+    z = A_b x, then the loss terms and the block's share of Aᵀ(s⊙r) (logistic CE: s = σ'(z) and r the
+    CE residual, as prox-GGN-SCORE.jl:44-49 / the oracle's Loss.grad form them; least squares:
+    s = 1, r = c(z − y)).  Bounds (summation orders differ; an error in z moves a CE term by at most
+    c·|δz| and s⊙r by at most c·|δz|/4 for |σ'| <= 1/4): f: 1e-11·(Σ|terms| + c·Σ_i Σ_j |A_ij x_j|);
+    ∇f_j: 1e-11·(Σ_i |A_ij s_i r_i| + c·Σ_i |A_ij| Σ_k |A_ik x_k|)."""
+    import ctypes as C
+    from scsopt import _lib
+    N, m = p.N, p.m
+    c = 1.0 / p.N_global
+    nr = max(16, (chunk_bytes // (8 * m)) // 16 * 16)
+    buf = np.empty((nr, m), dtype=np.float64)   # buf[:n].ravel() holds an (m, n) column-major block
+    yb = np.empty(nr)
+    f = fterms = fz = 0.0
+    g = np.zeros(m)
+    gb = np.zeros(m)
+    xa = np.abs(x)
+    for r0 in range(0, N, nr):
+        n = min(nr, N - r0)
+        Acm = buf.reshape(-1)[: m * n].reshape(m, n)   # Acm.T = rows r0 .. r0+n of A
+        p.ctx.check(_lib.lib.scs_get_data(p.ctx.h, r0, n, Acm.ctypes.data_as(_lib.c_dp), n,
+                                          yb.ctypes.data_as(_lib.c_dp)))
+        y = yb[:n]
+        Ab = np.abs(Acm)
+        z = Acm.T @ x
+        zabs = Ab.T @ xa
+        if kind == "logistic_ce":
+            s, yhat = O.sigmoid_jac(z)
+            terms = -c * (y * np.log(yhat) + (1.0 - y) * np.log(1.0 - yhat))
+            sr = s * O.ce_r(y, yhat, c)
+        else:
+            res = z - y
+            terms = 0.5 * c * res * res
+            sr = c * res
+        f += float(terms.sum())
+        fterms += float(np.abs(terms).sum())
+        fz += c * float(zabs.sum())
+        g += Acm @ sr
+        gb += Ab @ np.abs(sr) + c * (Ab @ zabs)
+    return f, 1e-11 * (fterms + fz), g, 1e-11 * gb
+
+
+def check_f_grad(p, x, kind):
+    """The device's f(x) / ∇f(x) -- the production GEMV passes and the loss epilogue -- at full size
+    against host_f_grad."""
+    f_dev, g_dev = p.fx(x), p.gradx(x)
+    f_ref, f_bnd, g_ref, g_bnd = host_f_grad(p, x, kind)
+    assert abs(f_dev - f_ref) <= f_bnd, (f_dev, f_ref, f_bnd)
+    worst = float(np.max(np.abs(g_dev - g_ref) / (g_bnd + 1e-300)))
+    assert worst <= 1.0, worst
+
+
 @pytest.mark.timeout(600)
 def test_c3_full_size_gram_and_step(clean_env):
     N, m = 1 << 20, 1 << 14
@@ -81,6 +138,9 @@ def test_c3_full_size_gram_and_step(clean_env):
                          f_tol=0.0, verbose=0)
     # obj holds the pre-step objective of each epoch (+ the duplicated last push): obj[1] is f + λg at x1
     assert sol.epochs == 2 and np.all(np.isfinite(sol.x)) and sol.obj[1] < sol.obj[0]
+    # the whole-length f / ∇f through the sigmoid / CE epilogue at the run's final x (and at x0)
+    check_f_grad(p, sol.x, "logistic_ce")
+    check_f_grad(p, x0, "logistic_ce")
     p.ctx.close()
 
 
@@ -110,6 +170,7 @@ def test_c4_rank_shape_gram_and_steps(clean_env):
     sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "gl", scsopt.PHuberSmootherGL(mu, p), max_epoch=2, x_tol=0.0,
                          f_tol=0.0, verbose=0)
     assert sol.epochs == 2 and np.all(np.isfinite(sol.x)) and sol.obj[1] < sol.obj[0]
+    check_f_grad(p, sol.x, "least_squares")
     p.ctx.close()
 
 

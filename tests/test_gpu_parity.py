@@ -318,9 +318,15 @@ def test_incremental_linesearch_same_decisions(method, loss, kind, monkeypatch):
         monkeypatch.setenv("SCS_LS_INCR", incr)
         runs.append(scsopt.iterate(meth(ss_type=3), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=10,
                                    verbose=0))
-    a, b = runs
-    assert a.obj == b.obj and a.pri_res_norm == b.pri_res_norm and a.epochs == b.epochs
-    assert np.array_equal(bits(a.x), bits(b.x))
+    # every incremental trial re-decided on the direct form (SCS_LS_NEAR huge): the restore of z0 = A x
+    # after a rejected re-decided trial is exercised, and the result is the direct form's bit for bit
+    monkeypatch.setenv("SCS_LS_INCR", "1")
+    monkeypatch.setenv("SCS_LS_NEAR", "1e300")
+    runs.append(scsopt.iterate(meth(ss_type=3), p, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=10, verbose=0))
+    a, b, c = runs
+    for u in (a, c):
+        assert u.obj == b.obj and u.pri_res_norm == b.pri_res_norm and u.epochs == b.epochs
+        assert np.array_equal(bits(u.x), bits(b.x))
 
 
 def test_group_lasso_ggn():

@@ -1,9 +1,9 @@
 #!/bin/bash
-# rocprofv3 --kernel-trace --stats of the default bench lines (C3, C2, C5, C5-shaped GGN) on the r04 build:
+# rocprofv3 --kernel-trace --stats of the default bench lines (C3, C2, C5, C5-shaped GGN) on the current build:
 # per-kernel CSV summaries + the bench line measured under the profiler
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-O=${1:-gpurun_out/r04/stats}; mkdir -p $O
+O=${1:-gpurun_out/stats}; mkdir -p $O
 prof() {  # label, bench args...
   local l=$1; shift
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/$l -o run -- python3 bench.py "$@" --no-cpu-baseline \

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 PMC passes (tools/gpu_prof_c3.sh) for the main Gram kernel into the JSON
+"""Summarise rocprofv3 PMC passes (tools/gpu_gram_pmc.sh) for the main Gram kernel into the JSON
 bench.py reads for roofline.traffic.  Corrections per MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE
 reports half of a 16-B/lane streaming read -> read bytes = 2 * FETCH_SIZE * 1024; FETCH_SIZE counts
 L2 misses to the fabric (Infinity Cache hits included), so the total is an upper bound on HBM bytes.
@@ -56,7 +56,7 @@ def main():
     out = {
         "kernel": k, "N": N, "m": m,
         "command": "rocprofv3 --pmc <group> --kernel-trace --output-format csv -- python3 bench.py --steps 1 "
-                   "--warmup 0 --no-cpu-baseline (one pass per counter group, tools/gpu_prof_c3.sh; "
+                   "--warmup 0 --no-cpu-baseline (one pass per counter group, tools/gpu_gram_pmc.sh; "
                    "summary by tools/pmc_summary.py)",
         "duration_ms_under_pmc": t_fetch * 1e3,
         "FETCH_SIZE_KB": fetch["FETCH_SIZE"], "WRITE_SIZE_KB": write["WRITE_SIZE"],
