@@ -208,6 +208,150 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step_kernel(double* A, int64_t
   if ((int64_t)g * R <= jn && jn < (int64_t)g * R + R && tid < LB) rowj[npar * LB + tid] = A[(r0 + jn) * ld + c0 + tid];
 }
 
+// The same column step with one memory round trip less on each side of the pivot choice (r05; bitwise
+// the same arithmetic).  The r02 kernel issued its loads in dependency order: the candidates, then (after
+// the argmax) the pivot row, then its own rows, and at the end re-read the rows it had just stored to
+// publish the next candidate row and row j + 1 -- four global round trips per column, 7.9 us per step at
+// n = 8192 (63 % of the factor).  Here every thread loads its rows (all columns: NP passes of 32 rows x
+// 8 lanes) together with the candidate reads, before the argmax, and publishes the candidate row and row
+// j + 1 from its registers.  A displaced row j (the pivot's old row) is still read after the argmax.
+template <int NP>
+__global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_t ld, int64_t r0, int64_t c0,
+                                                               int64_t h, int R, int j, double* cand, int* candi,
+                                                               double* candrow, double* rowj, int* ipiv, int* info) {
+  __shared__ double sv[LU_NT / 64];
+  __shared__ int si[LU_NT / 64], sw[LU_NT / 64];
+  const int tid = threadIdx.x, g = blockIdx.x, nwg = gridDim.x;
+  const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
+  const int par = j & 1, npar = (j + 1) & 1;
+  const int jn = j + 1;
+  // 1. this thread's row pieces (rows > j; the pivot row j itself is only ever overwritten), in flight
+  //    together with the candidate reads below
+  double v[NP][16];
+  bool act[NP];
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps) {
+    const int64_t i = (int64_t)g * R + ps * 32 + rr;
+    act[ps] = i < h && i > j;
+    const double* row = A + (r0 + (act[ps] ? i : 0)) * ld + c0 + cq;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = act[ps] ? *(const v2d*)(row + c) : (v2d){0.0, 0.0};
+  }
+  int p = j;
+  double piv = 0.0, rp = 0.0;
+  bool scale = false;
+  const double* urow = nullptr;
+  if (j >= 0) {
+    double cv = -1.0;
+    int ci = INT_MAX, w = -1;
+    if (tid < nwg) {
+      cv = cand[par * LU_MAXWG + tid];
+      ci = candi[par * LU_MAXWG + tid];
+      w = tid;
+      if (!(cv >= 0.0)) {
+        cv = -1.0;
+        ci = INT_MAX;
+      }
+    }
+    lu_block_argmax(cv, ci, w, sv, si, sw);
+    if (cv < 0.0) {
+      p = j;
+      urow = rowj + par * LB;
+    } else {
+      p = ci;
+      urow = candrow + ((int64_t)par * LU_MAXWG + w) * LB;
+    }
+    piv = urow[j];
+    scale = (piv != 0.0);
+    if (!scale) {
+      p = j;
+      urow = rowj + par * LB;
+      piv = urow[j];
+    }
+    rp = 1.0 / piv;
+    if (g == 0 && tid == 0) {
+      ipiv[r0 + j] = (int)(r0 + p);
+      if (!scale && *info == 0) *info = (int)(r0 + j + 1);
+    }
+  }
+  double u[16];
+  const bool need_u = (j >= 0) && (cq + 15 > j);
+  if (need_u) {
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(u + c) = *(const v2d*)(urow + cq + c);
+  }
+  double bv = -1.0;
+  int bi = INT_MAX;
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps) {
+    const int64_t i = (int64_t)g * R + ps * 32 + rr;
+    if (i >= h || i < j) continue;
+    double* row = A + (r0 + i) * ld + c0;
+    if (j < 0) {   // column-0 candidates
+      if (q == 0) {
+        const double a = fabs(v[ps][0]);
+        if (lu_better(a, (int)i, bv, bi)) {
+          bv = a;
+          bi = (int)i;
+        }
+      }
+      continue;
+    }
+    if (i == j) {   // the pivot row: U(j, :) = u
+      if (p != j) {
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) *(v2d*)(row + cq + c) = *(const v2d*)(urow + cq + c);
+      }
+      continue;
+    }
+    const bool bot = (i == p) && (p != j);
+    if (bot) {   // the displaced row j takes row p's place
+#pragma unroll
+      for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = *(const v2d*)(rowj + par * LB + cq + c);
+    }
+    if (!(bot || cq + 15 >= j)) continue;   // columns < j of an unmoved row are final
+    const double x = bot ? rowj[par * LB + j] : __shfl(sel(v[ps], j & 15), (tid & ~7) | (j >> 4), 64);
+    const double l = scale ? (fabs(piv) >= 2.2250738585072014e-308 ? x * rp : x / piv) : x;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int col = cq + c;
+      if (col > j) v[ps][c] -= l * u[c];
+      else if (col == j) v[ps][c] = l;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(row + cq + c) = *(const v2d*)(v[ps] + c);
+    if (jn < LB && q == (jn >> 4)) {
+      const double a = fabs(sel(v[ps], jn & 15));
+      if (lu_better(a, (int)i, bv, bi)) {
+        bv = a;
+        bi = (int)i;
+      }
+    }
+  }
+  if (jn >= LB) return;
+  int bw = g;
+  lu_block_argmax(bv, bi, bw, sv, si, sw);
+  if (tid == 0) {
+    cand[npar * LU_MAXWG + g] = (bi == INT_MAX) ? -1.0 : bv;
+    candi[npar * LU_MAXWG + g] = bi;
+  }
+  // the candidate row and row j + 1 from the registers of the 8 lanes that hold them
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps) {
+    const int64_t i = (int64_t)g * R + ps * 32 + rr;
+    if (i >= h || i < jn) continue;
+    if (i == bi) {
+#pragma unroll
+      for (int c = 0; c < 16; c += 2)
+        *(v2d*)(candrow + ((int64_t)npar * LU_MAXWG + g) * LB + cq + c) = *(const v2d*)(v[ps] + c);
+    }
+    if (i == jn) {
+#pragma unroll
+      for (int c = 0; c < 16; c += 2) *(v2d*)(rowj + npar * LB + cq + c) = *(const v2d*)(v[ps] + c);
+    }
+  }
+}
+
 // Compose block k's 128 interchanges (rows r0+s <-> ipiv[r0+s], in order) into row moves
 // "row dst <- previous row src" (<= 256 of them).  One wave.
 __global__ __launch_bounds__(64) void lu_perm_kernel(const int* __restrict__ ipiv, int r0, int2* __restrict__ pairs,
@@ -484,6 +628,13 @@ void lu_aux_free(LUAux* a) {
   *a = LUAux();
 }
 
+// SCS_LU_PANEL (read per call): unset / 2 = lu_panel_step2_kernel up to two 32-row passes per workgroup
+// (n <= 16384), 1 = the r02 column step everywhere (bitwise the same factor)
+static int lu_panel_mode() {
+  const char* e = getenv("SCS_LU_PANEL");
+  return e ? atoi(e) : 2;
+}
+
 hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st) {
   if (npad % LB != 0 || npad > a->npad || ld < npad) return hipErrorInvalidValue;
   const int nblk = (int)(npad / LB);
@@ -493,9 +644,18 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
     const int64_t r0 = (int64_t)k * LB, c0 = r0, h = npad - r0;
     const int R = 32 * (int)ceil_div(h, 32 * LU_MAXWG);
     const int nwg = (int)ceil_div(h, R);
-    for (int j = -1; j < LB; ++j)
-      hipLaunchKernelGGL(lu_panel_step_kernel, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
-                         a->candi, a->candrow, a->rowj, a->ipiv, info);
+    const int npass = R / 32, mode = lu_panel_mode();
+    for (int j = -1; j < LB; ++j) {
+      if (mode == 2 && npass == 1)
+        hipLaunchKernelGGL(lu_panel_step2_kernel<1>, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
+                           a->candi, a->candrow, a->rowj, a->ipiv, info);
+      else if (mode == 2 && npass == 2)
+        hipLaunchKernelGGL(lu_panel_step2_kernel<2>, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
+                           a->candi, a->candrow, a->rowj, a->ipiv, info);
+      else
+        hipLaunchKernelGGL(lu_panel_step_kernel, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
+                           a->candi, a->candrow, a->rowj, a->ipiv, info);
+    }
     int2* pairs = a->pairs + (int64_t)k * LU_MAXPAIRS;
     hipLaunchKernelGGL(lu_perm_kernel, dim3(1), dim3(64), 0, st, a->ipiv, (int)r0, pairs, a->npairs + k);
     hipLaunchKernelGGL(lu_diag_inv_kernel, dim3(2), dim3(256), 0, st, A, ld, r0, a->Linv + (int64_t)k * LB * LB,

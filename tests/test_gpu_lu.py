@@ -102,3 +102,20 @@ def test_solve_eval_lu_vs_cholesky():
     xr = np.linalg.solve(G, rhs)
     np.testing.assert_allclose(xc, xr, rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(xl, xr, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [300, 2176, 8320])
+def test_lu_prefetch_panel_bit_identical(n, monkeypatch):
+    """The column step with its rows prefetched beside the candidate reads and the next candidate row /
+    row j + 1 published from registers (lu_panel_step2_kernel, r05) does the same arithmetic as the
+    r02 step (SCS_LU_PANEL=1): the same pivots and the same solution bit for bit.  n = 8320: the first
+    panel has two 32-row passes per workgroup (h > 8192)."""
+    rng = np.random.default_rng(n + 7)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    x2, ipiv2, info2 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_PANEL", "1")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info1 == info2 == 0
+    assert np.array_equal(ipiv1, ipiv2)
+    assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
