@@ -262,7 +262,7 @@ __device__ __forceinline__ void diag_trail_tile(double* su, int o, int id, int l
 // same bits in both kernel schedules (PIPE or not).
 template <int J>
 __device__ __forceinline__ void w_column_t(const double* su, const double* swv /*[CB/SB][SB*SB]*/, double* Wk,
-                                           double* WTk, int lane) {
+                                           int lane) {
   const int li = lane & 15, lk = lane >> 4;
   v4d W[J + 1], S[J + 1];
 #pragma unroll
@@ -287,26 +287,18 @@ __device__ __forceinline__ void w_column_t(const double* su, const double* swv /
   for (int i = 0; i < CB / SB; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) col[16 * i + 4 * r] = (i <= J) ? W[i <= J ? i : 0][r] : 0.0;
-  if (WTk) {   // Wᵀ (W row-major): row 16 i + lk + 4 r of W, columns 16 J .. 16 J + 15 -- 128-B runs
-    double* row = WTk + (int64_t)lk * CB + 16 * J + li;
-#pragma unroll
-    for (int i = 0; i < CB / SB; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) row[(int64_t)(16 * i + 4 * r) * CB] = (i <= J) ? W[i <= J ? i : 0][r] : 0.0;
-  }
 }
 
-__device__ __forceinline__ void w_column(const double* su, const double* swv, double* Wk, double* WTk, int J,
-                                         int lane) {
+__device__ __forceinline__ void w_column(const double* su, const double* swv, double* Wk, int J, int lane) {
   switch (J) {
-    case 0: w_column_t<0>(su, swv, Wk, WTk, lane); break;
-    case 1: w_column_t<1>(su, swv, Wk, WTk, lane); break;
-    case 2: w_column_t<2>(su, swv, Wk, WTk, lane); break;
-    case 3: w_column_t<3>(su, swv, Wk, WTk, lane); break;
-    case 4: w_column_t<4>(su, swv, Wk, WTk, lane); break;
-    case 5: w_column_t<5>(su, swv, Wk, WTk, lane); break;
-    case 6: w_column_t<6>(su, swv, Wk, WTk, lane); break;
-    default: w_column_t<7>(su, swv, Wk, WTk, lane); break;
+    case 0: w_column_t<0>(su, swv, Wk, lane); break;
+    case 1: w_column_t<1>(su, swv, Wk, lane); break;
+    case 2: w_column_t<2>(su, swv, Wk, lane); break;
+    case 3: w_column_t<3>(su, swv, Wk, lane); break;
+    case 4: w_column_t<4>(su, swv, Wk, lane); break;
+    case 5: w_column_t<5>(su, swv, Wk, lane); break;
+    case 6: w_column_t<6>(su, swv, Wk, lane); break;
+    default: w_column_t<7>(su, swv, Wk, lane); break;
   }
 }
 
@@ -316,8 +308,7 @@ __device__ __forceinline__ void w_column(const double* su, const double* swv, do
 // of the phase-serial kernel (PIPE = false, SCS_CHOL_DIAG=0).
 template <bool PIPE>
 __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
-                                                        double* __restrict__ W, int* __restrict__ info,
-                                                        double* __restrict__ WT) {
+                                                        double* __restrict__ W, int* __restrict__ info) {
   __shared__ double su[CB * CLD];   // S(r, c) = su[c*CLD + r]
   __shared__ double srinv[CB];      // 1 / U(j, j)
   __shared__ double swinv[CB / SB][SB * SB];   // inverses of the 16 x 16 diagonal blocks (col-major)
@@ -325,7 +316,6 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   __shared__ int tctr;                                        // phase C's tile counter
   double* blk = G + (int64_t)k * CB * ld + (int64_t)k * CB;
   double* Wk = W + (int64_t)k * CB * CB;
-  double* WTk = WT ? WT + (int64_t)k * CB * CB : nullptr;
   const int tid = threadIdx.x;
   // the block into LDS: all 32 16-B loads per thread in flight before their LDS stores, and
   // unconditional (the block is whole in memory; the lower triangle is masked after the load -- a
@@ -434,7 +424,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
           PROF_MARK_T(50 + kb, 64 * wv);
         }
         // W's block column kb - 1 (its last input, swinv[kb - 1], came before this step's barrier)
-        if (W_BY_COLUMNS && kb >= 1 && wv == 1 + (kb + 1) % 3) w_column(su, &swinv[0][0], Wk, WTk, kb - 1, lane);
+        if (W_BY_COLUMNS && kb >= 1 && wv == 1 + (kb + 1) % 3) w_column(su, &swinv[0][0], Wk, kb - 1, lane);
         claim_tiles();
         // row blocks of U are final after their panel step: waves 1..3 store them while wave 0 is
         // on the chain (kb = 3: blocks 0, 1; 4: 2, 3; 5: 4, 5; 6: 6 -- where these waves have slack)
@@ -456,7 +446,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   if (PIPE) {
     if (wv == DNT / 64 - 1) inv16(CB / SB - 1);
     else store_urows(CB / SB - 1, tid, DNT - 64);
-    if (W_BY_COLUMNS && wv == 1) w_column(su, &swinv[0][0], Wk, WTk, CB / SB - 2, lane);   // swinv[6]: step 6
+    if (W_BY_COLUMNS && wv == 1) w_column(su, &swinv[0][0], Wk, CB / SB - 2, lane);   // swinv[6]: step 6
   } else {
     for (int rb = 0; rb < CB / SB; ++rb) store_urows(rb, tid, DNT);
     for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) inv16(kb);
@@ -465,10 +455,10 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   if (W_BY_COLUMNS) {
     PROF_MARK(34);
     if (PIPE) {
-      if (wv == 0) w_column(su, &swinv[0][0], Wk, WTk, CB / SB - 1, lane);
+      if (wv == 0) w_column(su, &swinv[0][0], Wk, CB / SB - 1, lane);
     } else {   // every column here: wave w takes columns w and 7 - w
-      w_column(su, &swinv[0][0], Wk, WTk, wv, lane);
-      w_column(su, &swinv[0][0], Wk, WTk, CB / SB - 1 - wv, lane);
+      w_column(su, &swinv[0][0], Wk, wv, lane);
+      w_column(su, &swinv[0][0], Wk, CB / SB - 1 - wv, lane);
     }
     PROF_MARK(35);
     return;
@@ -491,10 +481,6 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
     v[0] = (r <= c) ? w0 : 0.0;
     v[1] = (r + 1 <= c) ? w1 : 0.0;
     *(v2d*)(Wk + (int64_t)c * CB + r) = v;
-    if (WTk) {
-      WTk[(int64_t)r * CB + c] = v[0];
-      WTk[(int64_t)(r + 1) * CB + c] = v[1];
-    }
   }
   PROF_MARK(35);
 }
@@ -610,11 +596,11 @@ static bool chol_diag_pipe() {   // read per call (A/B within one process)
   return !(e && e[0] == '0');
 }
 
-hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st, double* WT) {
+hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st) {
   if (chol_diag_pipe())
-    hipLaunchKernelGGL(chol_diag_kernel<true>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, WT);
+    hipLaunchKernelGGL(chol_diag_kernel<true>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
   else
-    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, WT);
+    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
   return hipGetLastError();
 }
 
@@ -708,8 +694,6 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipMemsetAsync(a->bctr, 0, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned), st);
   a->bslot = 0;
   if (e == hipSuccess) e = hipMalloc(&a->sscr, sizeof(double) * 2 * (size_t)CB * 16 * CB);
-  if (e == hipSuccess) e = hipMalloc(&a->wt, sizeof(double) * (size_t)mpad * CB);
-  if (e == hipSuccess) e = hipMalloc(&a->fscr, sizeof(double) * 2 * (size_t)CB * 15 * CB);
   if (e == hipSuccess) {
     a->bskip = bulk_skip_mask(nblk);
     int dev = 0, ncu = 0;
@@ -754,10 +738,6 @@ void chol_aux_free(CholAux* a) {
   a->sbl = nullptr;
   if (a->sscr) (void)hipFree(a->sscr);
   a->sscr = nullptr;
-  if (a->wt) (void)hipFree(a->wt);
-  a->wt = nullptr;
-  if (a->fscr) (void)hipFree(a->fscr);
-  a->fscr = nullptr;
   a->serr = nullptr;
   for (void* p : {(void*)a->dtasks, (void*)a->ddeps, (void*)a->dcnt, (void*)a->dper})
     if (p) (void)hipFree(p);
@@ -872,70 +852,6 @@ __global__ __launch_bounds__(256) void strip_step_kernel(double* G, int64_t ld, 
                        G + col0 * ld + (int64_t)q * GT, ld, GRAM_ACCUMULATE, lds);
 }
 
-// The chain's strip solve (Ba) as ONE launch (r05): workgroup (j, s) owns the 16-column strip s of column
-// tile c0 + j through every row r of [lo, hi) and runs the forward substitution down it by itself --
-// T = R_rj[:, s] into LDS, T -= U_qrᵀ X_q for q = lo .. r-1 (X_q: its own strip, already solved in place),
-// X_r = W_rᵀ T in place.  No item reads what another writes, so no scratch; per element the same
-// products in the same order as strip_step_kernel's row-by-row launches (the accumulate into T is the
-// step's accumulate into R_rj, the leaf the same W_rᵀ product): bitwise the same X.  hi - lo launches of
-// ~19 us become one of ~(hi-lo)(hi-lo+1)/2 strip products (~1.7 us each) on nc·8 workgroups.
-// BND: the bulk stream's form (the strip solve beyond the next block, Bb): CU-bounded and persistent like
-// gram_launch_bounded -- workgroups on the skipped CU ids leave (unless last to arrive), the others claim
-// items from per-XCD segments of the item list (bnd_first / bnd_next).
-template <bool BND>
-__global__ __launch_bounds__(256) void ba_fused_kernel(double* G, int64_t ld, const double* __restrict__ W,
-                                                       const double* __restrict__ wv, int lo, int hi, int c0, int nitems,
-                                                       unsigned* ctr, unsigned skip) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * (GT + 16) * GBK];
-  __shared__ __attribute__((aligned(16))) double T[GT * 16];
-  __shared__ int s_claim;
-  int it = BND ? bnd_first(ctr, skip, nitems, &s_claim) : (int)blockIdx.x;
-  while (it >= 0 && it < nitems) {
-    const int j = it >> 3, sx = it & 7;
-    const int64_t col0 = (int64_t)(c0 + j) * GT + 16 * sx;   // the strip's first column of G
-    double* strip = G + col0 * ld;                          // row r of the strip at strip + r·128
-    for (int r = lo; r < hi; ++r) {
-      for (int e = threadIdx.x; e < GT * 8; e += 256) {      // T = R_rj[:, s]
-        const int c = e >> 6, rr = 2 * (e & 63);
-        *(v2d*)(T + c * GT + rr) = *(const v2d*)(strip + (int64_t)c * ld + (int64_t)r * GT + rr);
-      }
-      __syncthreads();
-      for (int q = lo; q < r; ++q) {                         // T -= U_qrᵀ X_q
-        gram_small_strip<16>(G + (int64_t)r * GT * ld + (int64_t)q * GT, ld, strip + (int64_t)q * GT, ld, wv + GT, 0,
-                             GT, T, GT, GRAM_ACCUMULATE, lds);
-        __syncthreads();
-      }
-      gram_small_strip<16>(W + (int64_t)r * GT * GT, GT, T, GT, wv, 0, GT, strip + (int64_t)r * GT, ld, 0, lds);
-      __syncthreads();                                       // X_r (this workgroup's stores) before its reads
-    }
-    if (!BND) break;
-    it = bnd_next(ctr, nitems, &s_claim);
-  }
-}
-
-static unsigned* bulk_ctr(const CholAux* a, hipStream_t st2, hipError_t* e);
-static unsigned bulk_skip_for(const CholAux* a, int ntiles);
-
-static hipError_t strip_solve_fused(double* G, int64_t ld, const double* W, const CholAux* a, int lo, int hi, int c0,
-                                    int nc, hipStream_t st, bool bulk = false) {
-  if (nc <= 0) return hipSuccess;
-  const int nitems = 8 * nc;
-  const unsigned skip = bulk ? bulk_skip_for(a, nc) : 0u;
-  if (bulk && skip && a->bslots > 0) {
-    hipError_t e = hipSuccess;
-    unsigned* ctr = bulk_ctr(a, st, &e);
-    if (e != hipSuccess) return e;
-    // one workgroup per CU (256 VGPRs): a->bslots counts two per CU
-    const int want = nitems + (nitems + 6) / 7 + 8, slots = a->bslots / 2;
-    hipLaunchKernelGGL(ba_fused_kernel<true>, dim3((unsigned)(want < slots ? want : slots)), dim3(256), 0, st, G, ld, W,
-                       a->w, lo, hi, c0, nitems, ctr, skip);
-  } else {
-    hipLaunchKernelGGL(ba_fused_kernel<false>, dim3((unsigned)nitems), dim3(256), 0, st, G, ld, W, a->w, lo, hi, c0,
-                       nitems, nullptr, 0u);
-  }
-  return hipGetLastError();
-}
-
 static hipError_t strip_solve_steps(double* G, int64_t ld, const double* W, const CholAux* a, int lo, int hi, int c0,
                                     int nc, hipStream_t st) {
   if (nc <= 0) return hipSuccess;
@@ -951,121 +867,11 @@ static hipError_t strip_solve_steps(double* G, int64_t ld, const double* W, cons
   return hipGetLastError();
 }
 
-// One inner step k of an outer block's A phase -- the row panel U_k,(k+1..k+nb) and the trailing update
-// of the rest of the outer block -- as ONE launch (r05; was a row-panel launch and a trailing launch, two
-// latency launches of the chain per inner step: 111 gram_small launches at 16.5 us in the m = 8192
-// factor, 224 at 32.6 us at m = 16384, profiles/r04/chol/).  Items, each a 16-column strip s of a tile:
-//   panel    (j, s), j = k+1 .. k+nb:           Y = W_kᵀ A_kj[:, s]                  -> scur
-//   trailing (i, j, s), k < i <= j <= k+nb:     Y = W_kᵀ A_kj[:, s] (recomputed, bitwise the panel
-//            item's), Z = W_k Y, A_ij[:, s] -= A_kiᵀ Z
-//   copy     (t, s): the previous step's scur (row k-1, nbp tiles from block k) into G
-// A_kiᵀ W_k W_kᵀ A_kj = U_kiᵀ U_kj (U_ki = W_kᵀ A_ki), so no item needs another item's output: the panel
-// goes to scratch (the trailing items read the pre-panel row k) and lands in G one launch later, where
-// no item reads row k - 1.  Every product is gram_small_strip<16> (the latency kernel's MFMA order);
-// Z = W_k Y reads Wᵀ_k (WT, from the diagonal kernel) so its A operand is K-contiguous like the others.
-// Diagonal tiles (i = j) are written whole (their strictly lower part is never read: the diagonal
-// kernel masks it).  nb = 0: a copy-only launch (the outer block's last panel row).
-__global__ __launch_bounds__(256) void chol_step_kernel(double* G, int64_t ld, const double* __restrict__ Wk,
-                                                        const double* __restrict__ WTk, const double* __restrict__ wv,
-                                                        int k, int nb, double* __restrict__ scur,
-                                                        const double* __restrict__ sprev, int nbp) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * (GT + 16) * GBK];
-  __shared__ __attribute__((aligned(16))) double YZ[2][GT * 16];
-  const int npanel = 8 * nb, ntrail = 4 * nb * (nb + 1), it = blockIdx.x;
-  if (it >= npanel + ntrail) {   // copy-back of row k - 1: one 128 x 16 strip of tile k + t
-    const int ci = it - npanel - ntrail, t = ci >> 3, sx = ci & 7;
-    (void)nbp;
-    for (int e = threadIdx.x; e < GT * 8; e += 256) {
-      const int col = 16 * sx + (e >> 6), rr = 2 * (e & 63);
-      *(v2d*)(G + ((int64_t)(k + t) * GT + col) * ld + (int64_t)(k - 1) * GT + rr) =
-          *(const v2d*)(sprev + ((int64_t)t * GT + col) * GT + rr);
-    }
-    return;
-  }
-  const double* rowk = G + (int64_t)k * GT;   // row block k: tile (k, j) at rowk + j·128·ld
-  if (it < npanel) {
-    const int t = it >> 3, sx = it & 7;
-    const int64_t col = (int64_t)(k + 1 + t) * GT + 16 * sx;
-    gram_small_strip<16>(Wk, GT, rowk + col * ld, ld, wv, 0, GT, scur + ((int64_t)t * GT + 16 * sx) * GT, GT, 0, lds);
-    return;
-  }
-  const int p = (it - npanel) >> 3, sx = (it - npanel) & 7;
-  int jj = 0;
-  while ((jj + 1) * (jj + 2) / 2 <= p) ++jj;
-  const int ii = p - jj * (jj + 1) / 2;
-  const int64_t colj = (int64_t)(k + 1 + jj) * GT + 16 * sx, coli = (int64_t)(k + 1 + ii) * GT;
-  gram_small_strip<16>(Wk, GT, rowk + colj * ld, ld, wv, 0, GT, YZ[0], GT, 0, lds);      // Y = W_kᵀ A_kj[:, s]
-  __syncthreads();
-  gram_small_strip<16>(WTk, GT, YZ[0], GT, wv, 0, GT, YZ[1], GT, 0, lds);                 // Z = W_k Y
-  __syncthreads();
-  gram_small_strip<16>(rowk + coli * ld, ld, YZ[1], GT, wv + GT, 0, GT, G + colj * ld + (int64_t)(k + 1 + ii) * GT, ld,
-                       GRAM_ACCUMULATE, lds);                                             // A_ij[:, s] -= A_kiᵀ Z
-}
-
-// SCS_CHOL_FUSED (read per call; default on): the A phase's inner steps as chol_step_kernel launches; 0 =
-// a row-panel launch and a trailing launch per step (what the dependency-driven launches replay)
-static bool chol_fused() {
-  const char* e = getenv("SCS_CHOL_FUSED");
-  return !(e && e[0] == '0');
-}
-
-// A: the inner factor of the outer diagonal block [i0, i1) -- per inner block the diagonal kernel, then
-// (fused) one chol_step_kernel launch, or (not) the row panel and the in-block trailing update as two
-// Gram launches; fused, the last panel row lands in G by a copy-only step after the last diagonal kernel.
-static hipError_t chol_inner(double* G, int64_t ld, double* W, const CholAux* a, const int2* trilist, int* info, int i0,
-                             int i1, bool fused, hipStream_t st) {
-  const size_t srow = (size_t)CB * 15 * CB;   // one scratch row: 128 x (15 x 128)
-  fused = fused && a->wt && a->fscr && i1 - i0 <= 16;
-  for (int k = i0; k < i1; ++k) {
-    hipError_t e = launch_chol_diag(G, ld, k, W, info, st, fused ? a->wt : nullptr);
-    if (e != hipSuccess) return e;
-    const int nb = i1 - k - 1;
-    if (fused) {
-      const int nbp = k > i0 ? nb + 1 : 0;   // the previous step's panel tiles (row k - 1)
-      if (nb == 0 && nbp == 0) break;
-      const double* sprev = a->fscr + srow * ((k - i0 + 1) & 1);
-      double* scur = a->fscr + srow * ((k - i0) & 1);
-      const unsigned grid = (unsigned)(8 * nb + 4 * nb * (nb + 1) + 8 * nbp);
-      hipLaunchKernelGGL(chol_step_kernel, dim3(grid), dim3(256), 0, st, G, ld, W + (int64_t)k * CB * CB,
-                         a->wt + (int64_t)k * CB * CB, a->w, k, nb, scur, sprev, nbp);
-      e = hipGetLastError();
-      if (e != hipSuccess) return e;
-      continue;
-    }
-    if (nb == 0) break;
-    double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..i1-1)
-    e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb, rowpanel, ld, 0,
-                        st);
-    if (e != hipSuccess) return e;
-    double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
-    e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld,
-                        /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-
-// SCS_CHOL_BA_STEPS (read per call): the chain's strip solve of the next block's columns -- unset / 2: one
-// ba_fused_kernel launch (r05); 1: strip_solve_steps' row-by-row launches (r03-r04), bitwise the same X;
-// 0: the recursion (also whenever the dependency-driven launches replay it, SCS_CHOL_DAG=1)
-static int ba_mode() {
+// SCS_CHOL_BA_STEPS (default 1): the chain's strip solve by strip_solve_steps; 0 = the recursion
+// (also whenever the dependency-driven launches replay it, SCS_CHOL_DAG=1)
+static bool ba_steps() {
   const char* e = getenv("SCS_CHOL_BA_STEPS");
-  return e ? atoi(e) : 2;
-}
-static bool ba_steps() { return ba_mode() != 0; }
-// the strip solve BEYOND the next block (Bb, the bulk stream's; and the serial order's same columns) in
-// the one-launch form too up to m = 16384 (nblk <= 128), where the factor is chain-bound and Bb's
-// recursion was ~114 latency launches (m = 8192); beyond, the recursion's K-grouped throughput launches
-// keep the bulk-bound factors efficient (a one-launch strip product is latency-bound, ~1 memory round
-// trip per 0.5 MFLOP).  SCS_CHOL_BB_FUSED_MAX overrides the nblk limit.
-static bool bb_fused(int nblk) {
-  const char* e = getenv("SCS_CHOL_BB_FUSED_MAX");
-  return ba_mode() == 2 && nblk <= (e ? atoi(e) : 128);
-}
-static hipError_t ba_solve(double* G, int64_t ld, const double* W, const CholAux* a, int lo, int hi, int c0, int nc,
-                           hipStream_t st) {
-  return ba_mode() == 1 ? strip_solve_steps(G, ld, W, a, lo, hi, c0, nc, st)
-                        : strip_solve_fused(G, ld, W, a, lo, hi, c0, nc, st);
+  return !(e && e[0] == '0');
 }
 
 // Lookahead (default; SCS_CHOL_LA=0 off).  Outer block t's strip solve B and trailing update C
@@ -1391,16 +1197,23 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
   for (int i0 = 0; i0 < nblk; i0 += OB) {
     const int i1 = i0 + OB < nblk ? i0 + OB : nblk;
     // A: inner factor of the outer diagonal block
-    if (dag) {
-      for (int k = i0; k < i1; ++k) {
-        e = launch_chol_diag(G, ld, k, W, info, st);
+    for (int k = i0; k < i1; ++k) {
+      e = launch_chol_diag(G, ld, k, W, info, st);
+      if (e != hipSuccess) return e;
+      const int nb = i1 - k - 1;
+      if (nb == 0) break;
+      if (dag) {   // the row panel and the trailing update of step k as one launch
+        e = chol_dag_launch(a, a->dstep[(size_t)k], G, ld, W, st);
         if (e != hipSuccess) return e;
-        if (i1 - k - 1 == 0) break;
-        e = chol_dag_launch(a, a->dstep[(size_t)k], G, ld, W, st);   // the row panel + trailing update of step k
-        if (e != hipSuccess) return e;
+        continue;
       }
-    } else {
-      e = chol_inner(G, ld, W, a, trilist, info, i0, i1, chol_fused(), st);
+      double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..i1-1)
+      e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb, rowpanel, ld,
+                          0, st);
+      if (e != hipSuccess) return e;
+      double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
+      e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld,
+                          /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
       if (e != hipSuccess) return e;
     }
     const int nc = nblk - i1;
@@ -1419,10 +1232,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
       if (e == hipSuccess) {
         if (steps) {
           const int nb = nc < OB ? nc : OB;
-          e = ba_solve(G, ld, W, a, i0, i1, i1, nb, st);
-          if (e == hipSuccess && nc > nb)
-            e = bb_fused(nblk) ? strip_solve_fused(G, ld, W, a, i0, i1, i1 + nb, nc - nb, st)
-                               : strip_solve(G, ld, W, a, i0, i1, i1 + nb, nc - nb, st);
+          e = strip_solve_steps(G, ld, W, a, i0, i1, i1, nb, st);
+          if (e == hipSuccess && nc > nb) e = strip_solve(G, ld, W, a, i0, i1, i1 + nb, nc - nb, st);
         } else {
           e = strip_solve(G, ld, W, a, i0, i1, i1, nc, st);
         }
@@ -1436,9 +1247,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     // Bb on st2 once A_t is done (stream order keeps C12_{t-1} before it)
     if (e == hipSuccess) e = hipEventRecord(a->ev3, st);
     wait(a->st2, a->ev3);
-    if (e == hipSuccess)
-      e = (steps && bb_fused(nblk)) ? strip_solve_fused(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2, true)
-                                    : strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2, true);
+    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2, true);
     // Ba, C1a on the chain after C12a_{t-1} (and so after everything before it on st2)
     if (c12_pending) wait(st, split ? a->ev4 : a->ev2);
     const int n1a = (OB * (OB + 1)) / 2;
@@ -1446,7 +1255,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
       if (e == hipSuccess) e = chol_dag_launch(a, a->dnext[(size_t)(i0 / OB)], G, ld, W, st);
     } else {
       if (e == hipSuccess)
-        e = steps ? ba_solve(G, ld, W, a, i0, i1, i1, OB, st) : strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
+        e = steps ? strip_solve_steps(G, ld, W, a, i0, i1, i1, OB, st) : strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
       if (e == hipSuccess)
         e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, n1a, trail, ld,
                               2 | 4, st);
@@ -1536,8 +1345,17 @@ hipError_t chol_strip_factor(double* G, int64_t ld, int s, double* W, const Chol
                              hipStream_t st) {
   const int nblk = a->nblk, OB = outer_block();
   const int i0 = s * OB, i1 = std::min(i0 + OB, nblk);
-  {
-    hipError_t e = chol_inner(G, ld, W, a, trilist, info, i0, i1, chol_fused(), st);
+  for (int k = i0; k < i1; ++k) {
+    hipError_t e = launch_chol_diag(G, ld, k, W, info, st);
+    if (e != hipSuccess) return e;
+    const int nb = i1 - k - 1;
+    if (nb == 0) break;
+    double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;
+    e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb, rowpanel, ld, 0,
+                        st);
+    if (e != hipSuccess) return e;
+    double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
+    e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld, 2 | 4, st);
     if (e != hipSuccess) return e;
   }
   const int nc = nblk - i1;

@@ -57,6 +57,41 @@ namespace scs {
 // TI = 64-row wave groups along i: TI = 2 -> 128 x 128 tiles, 4 waves, 2 WG/CU;
 // TI = 4 -> 256 x 128 tiles, 8 waves, 1 WG/CU (25 % less operand traffic per flop).
 // TILED: operands are the panel-blocked A (common.h tiled_off), lda1/lda2 = S stages.
+// CU-bounded persistent launches (BND instances; the Cholesky's bulk stream, chol.hip): a
+// workgroup on a CU whose id within its shader engine (HW_REG_HW_ID bits 11:8) is set in `skip`
+// leaves at once -- unless it is the launch's last arrival, so the tiles never depend on where
+// the dispatcher puts the workgroups -- and every other workgroup claims tiles until none is left.
+// The skipped CUs stay free for the serial chain's launches on the other stream (the effect of a
+// CU-masked queue without one).  Claims keep the plain launch's XCD-aware split: the tile list is
+// cut into 8 contiguous segments, a workgroup claims from its XCD's segment (HW_REG_XCC_ID) first
+// and then from the others in turn.  ctr = {claims per segment [8], arrivals}, zero at launch.
+__device__ __forceinline__ int bnd_claim(unsigned* ctr, int ntiles) {
+  const int q8 = ntiles / 8, r8 = ntiles % 8;
+  const int x0 = (int)((unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u);   // HW_REG_XCC_ID
+  for (int d = 0; d < 8; ++d) {
+    const int x = (x0 + d) & 7, len = q8 + (x < r8 ? 1 : 0);
+    if (len == 0) continue;
+    const unsigned t = atomicAdd(ctr + x, 1u);
+    if ((int)t < len) return x * q8 + (x < r8 ? x : r8) + (int)t;
+  }
+  return ntiles;
+}
+__device__ __forceinline__ int bnd_first(unsigned* ctr, unsigned skip, int ntiles, int* s) {
+  if (threadIdx.x == 0) {
+    const unsigned cu = ((unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 15u;   // HW_REG_HW_ID
+    const unsigned arr = atomicAdd(ctr + 8, 1u);
+    *s = (((skip >> cu) & 1u) && arr + 1 < gridDim.x) ? -1 : bnd_claim(ctr, ntiles);
+  }
+  __syncthreads();
+  return *s;
+}
+__device__ __forceinline__ int bnd_next(unsigned* ctr, int ntiles, int* s) {
+  __syncthreads();   // every wave is done with the previous tile's LDS and with *s
+  if (threadIdx.x == 0) *s = bnd_claim(ctr, ntiles);
+  __syncthreads();
+  return *s;
+}
+
 template <bool NOLOAD, int TI, bool TILED = false, bool BND = false>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
     const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,

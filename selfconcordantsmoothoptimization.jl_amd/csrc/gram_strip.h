@@ -13,42 +13,6 @@ constexpr int GBK = 16;   // samples per stage
 
 __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
 
-// CU-bounded persistent launches (BND instances; the Cholesky's bulk stream, chol.hip): a
-// workgroup on a CU whose id within its shader engine (HW_REG_HW_ID bits 11:8) is set in `skip`
-// leaves at once -- unless it is the launch's last arrival, so the tiles never depend on where
-// the dispatcher puts the workgroups -- and every other workgroup claims tiles until none is left.
-// The skipped CUs stay free for the serial chain's launches on the other stream (the effect of a
-// CU-masked queue without one).  Claims keep the plain launch's XCD-aware split: the tile list is
-// cut into 8 contiguous segments, a workgroup claims from its XCD's segment (HW_REG_XCC_ID) first
-// and then from the others in turn.  ctr = {claims per segment [8], arrivals}, zero at launch.
-__device__ __forceinline__ int bnd_claim(unsigned* ctr, int ntiles) {
-  const int q8 = ntiles / 8, r8 = ntiles % 8;
-  const int x0 = (int)((unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u);   // HW_REG_XCC_ID
-  for (int d = 0; d < 8; ++d) {
-    const int x = (x0 + d) & 7, len = q8 + (x < r8 ? 1 : 0);
-    if (len == 0) continue;
-    const unsigned t = atomicAdd(ctr + x, 1u);
-    if ((int)t < len) return x * q8 + (x < r8 ? x : r8) + (int)t;
-  }
-  return ntiles;
-}
-__device__ __forceinline__ int bnd_first(unsigned* ctr, unsigned skip, int ntiles, int* s) {
-  if (threadIdx.x == 0) {
-    const unsigned cu = ((unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 15u;   // HW_REG_HW_ID
-    const unsigned arr = atomicAdd(ctr + 8, 1u);
-    *s = (((skip >> cu) & 1u) && arr + 1 < gridDim.x) ? -1 : bnd_claim(ctr, ntiles);
-  }
-  __syncthreads();
-  return *s;
-}
-__device__ __forceinline__ int bnd_next(unsigned* ctr, int ntiles, int* s) {
-  __syncthreads();   // every wave is done with the previous tile's LDS and with *s
-  if (threadIdx.x == 0) *s = bnd_claim(ctr, ntiles);
-  __syncthreads();
-  return *s;
-}
-
-
 // Latency variant for the small launches of the Cholesky and the LU (short K or few
 // tiles): each 128 x 128 list tile is computed by 128/QC workgroups, one per QC-column
 // strip (4 waves of 32 rows x QC along the rows).  A workgroup reads the A2 columns it

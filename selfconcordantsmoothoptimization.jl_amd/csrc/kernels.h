@@ -110,11 +110,6 @@ struct CholAux {             // device constants of the two-level factorization 
   // the chain's strip solve as right-looking step launches (strip_solve_steps): two rows of
   // 128 x (16 x 128) doubles for a step's leaf (its copy-back is the next step's)
   double* sscr = nullptr;
-  // the fused inner steps of the A phase (chol_step_kernel, r05): Wᵀ_k of every diagonal block
-  // (mpad x 128, written beside W by the diagonal kernel) and two rows of 128 x (15 x 128) doubles
-  // for a step's row panel (its copy-back into G is the next step's)
-  double* wt = nullptr;
-  double* fscr = nullptr;
   // strip pipeline (chol_pipe_init): the left-looking update of each outer strip s as a
   // tail-balanced scheduled launch over the pairs (i >= j, j < OB) of its trailing columns
   struct StripSched {
@@ -144,8 +139,7 @@ struct CholAux {             // device constants of the two-level factorization 
 hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);
 void chol_aux_free(CholAux* a);
 // the 128 x 128 diagonal block k: factor in place, W_k = U_kk⁻¹ (SCS_CHOL_DIAG=0: phase-serial kernel)
-// WT (may be null): also Wᵀ_k (W_k row-major), the operand of the fused inner steps
-hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st, double* WT = nullptr);
+hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st);
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* aux,
                        const int2* trilist, int* info, hipStream_t st);
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y, CholAux* a,

@@ -924,7 +924,6 @@ def test_cholesky_dag_launches_bit_identical(m, ob, la, monkeypatch):
     if ob:
         monkeypatch.setenv("SCS_CHOL_OB", ob)
     monkeypatch.setenv("SCS_CHOL_LA", la)
-    monkeypatch.setenv("SCS_CHOL_FUSED", "0")   # the DAG replays the two-launch inner step
     monkeypatch.setenv("SCS_CHOL_DAG", "1")   # opt-in (measured slower than one launch per operation)
     monkeypatch.setenv("SCS_CHOL_BA_STEPS", "0")   # the DAG replays the recursive strip solve
     N = 4000 if m < 8192 else 9000
@@ -938,55 +937,6 @@ def test_cholesky_dag_launches_bit_identical(m, ob, la, monkeypatch):
     for r in (b, c):
         assert a.obj == r.obj and a.pri_res_norm == r.pri_res_norm and a.epochs == r.epochs
         assert np.array_equal(bits(a.x), bits(r.x))
-
-
-@pytest.mark.parametrize("m,ob,la", [(2304, None, "1"), (3200, "8", "1"), (3200, None, "0"), (8192, None, "1")])
-def test_cholesky_fused_inner_steps(m, ob, la, monkeypatch):
-    """The A phase's inner steps as ONE chol_step_kernel launch each (r05: the row panel to scratch and
-    the in-block trailing update as A_kiᵀ·(W_k·(W_kᵀ A_kj)), the panel landing in G one launch later)
-    against a row-panel launch + a trailing launch per step (SCS_CHOL_FUSED=0): the same factor up to
-    the association of the products, so the ProxNSCORE trajectories agree to rounding (obj rtol 1e-12,
-    x 1e-9) and the fused run is bitwise the same run to run -- lookahead and serial order, 4- and
-    8-block outer steps, and the C2 shape (m = 8192)."""
-    if ob:
-        monkeypatch.setenv("SCS_CHOL_OB", ob)
-    monkeypatch.setenv("SCS_CHOL_LA", la)
-    N = 4000 if m < 8192 else 9000
-    x0 = np.random.default_rng(37).standard_normal(m) * 0.3
-    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=29)
-    hm = scsopt.PHuberSmootherL1L2(1.0)
-    a = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
-    b = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
-    assert a.obj == b.obj and np.array_equal(bits(a.x), bits(b.x))
-    monkeypatch.setenv("SCS_CHOL_FUSED", "0")
-    c = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
-    assert a.epochs == c.epochs
-    np.testing.assert_allclose(a.obj, c.obj, rtol=1e-12, atol=0)
-    np.testing.assert_allclose(a.x, c.x, rtol=1e-9, atol=1e-12)
-
-
-@pytest.mark.parametrize("m,ob,la", [(2304, None, "1"), (3200, "8", "1"), (3200, None, "0")])
-def test_cholesky_ba_one_launch(m, ob, la, monkeypatch):
-    """The strip solves as ONE launch each (ba_fused_kernel, r05: a workgroup runs the forward
-    substitution down its own 16-column strip; Ba on the chain, Bb beyond the next block on the bulk
-    stream, CU-bounded) against r04's row-by-row step launches for Ba and the recursion for Bb
-    (SCS_CHOL_BA_STEPS=1): Ba is the same products in the same order per element, Bb takes its
-    updates with K = 128 in row order instead of the recursion's K = 128 .. OB/2·128 groups, so the
-    ProxNSCORE trajectories agree to rounding (lookahead vs serial order stays bitwise:
-    test_cholesky_lookahead_bit_identical) -- 4- and 8-block outer steps."""
-    if ob:
-        monkeypatch.setenv("SCS_CHOL_OB", ob)
-    monkeypatch.setenv("SCS_CHOL_LA", la)
-    N = 4000
-    x0 = np.random.default_rng(37).standard_normal(m) * 0.3
-    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=29)
-    hm = scsopt.PHuberSmootherL1L2(1.0)
-    a = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
-    monkeypatch.setenv("SCS_CHOL_BA_STEPS", "1")
-    b = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
-    assert a.epochs == b.epochs
-    np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
-    np.testing.assert_allclose(a.x, b.x, rtol=1e-9, atol=1e-12)
 
 
 @pytest.mark.parametrize("m", [300, 1000, 2304])

@@ -11,6 +11,7 @@
   printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
 namespace scs {
+hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st);
 #ifdef CHOL_PROF
 extern __device__ long long chol_prof[128];
 #endif
