@@ -262,7 +262,7 @@ __device__ __forceinline__ void diag_trail_tile(double* su, int o, int id, int l
 // same bits in both kernel schedules (PIPE or not).
 template <int J>
 __device__ __forceinline__ void w_column_t(const double* su, const double* swv /*[CB/SB][SB*SB]*/, double* Wk,
-                                           int lane) {
+                                           int lane, double* su_w) {
   const int li = lane & 15, lk = lane >> 4;
   v4d W[J + 1], S[J + 1];
 #pragma unroll
@@ -287,18 +287,74 @@ __device__ __forceinline__ void w_column_t(const double* su, const double* swv /
   for (int i = 0; i < CB / SB; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) col[16 * i + 4 * r] = (i <= J) ? W[i <= J ? i : 0][r] : 0.0;
+  // the off-diagonal blocks also into the (unused, zero) strictly-lower triangle of su, transposed:
+  // W(r, c) at su[r·CLD + c] -- w_last_column_par reads them there (r05)
+  if (J < CB / SB - 1) {
+#pragma unroll
+    for (int i = 0; i < J; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) su_w[(16 * i + lk + 4 * r) * CLD + 16 * J + li] = W[i][r];
+  }
 }
 
-__device__ __forceinline__ void w_column(const double* su, const double* swv, double* Wk, int J, int lane) {
+__device__ __forceinline__ void w_column(double* su, const double* swv, double* Wk, int J, int lane) {
   switch (J) {
-    case 0: w_column_t<0>(su, swv, Wk, lane); break;
-    case 1: w_column_t<1>(su, swv, Wk, lane); break;
-    case 2: w_column_t<2>(su, swv, Wk, lane); break;
-    case 3: w_column_t<3>(su, swv, Wk, lane); break;
-    case 4: w_column_t<4>(su, swv, Wk, lane); break;
-    case 5: w_column_t<5>(su, swv, Wk, lane); break;
-    case 6: w_column_t<6>(su, swv, Wk, lane); break;
-    default: w_column_t<7>(su, swv, Wk, lane); break;
+    case 0: w_column_t<0>(su, swv, Wk, lane, su); break;
+    case 1: w_column_t<1>(su, swv, Wk, lane, su); break;
+    case 2: w_column_t<2>(su, swv, Wk, lane, su); break;
+    case 3: w_column_t<3>(su, swv, Wk, lane, su); break;
+    case 4: w_column_t<4>(su, swv, Wk, lane, su); break;
+    case 5: w_column_t<5>(su, swv, Wk, lane, su); break;
+    case 6: w_column_t<6>(su, swv, Wk, lane, su); break;
+    default: w_column_t<7>(su, swv, Wk, lane, su); break;
+  }
+}
+
+// W's last block column J = 7 by all four waves (r05; was w_column_t<7> on one wave after the loop,
+// 7 dependent steps, 5.7 us): the block inverse of an upper-triangular matrix,
+//   W_{0:J, J} = -W_{0:J, 0:J} · (U_{0:J, J} · W_JJ),
+// so V_l = U_lJ W_JJ (W_JJ = swinv[J] as the B operand; every wave forms all J of them, 4 MFMAs each,
+// and the accumulator layout D[(lane>>4) + 4r][lane & 15] is the next MFMA's B operand), then
+// W_iJ = -Σ_{l=i}^{J-1} W_il V_l for the wave's row blocks (W_ii = swinv[i]; W_il, l > i, from the
+// transposed copies w_column_t left in su's strictly-lower triangle).  Row blocks {w, 6-w} per wave
+// w < 3 and {3} for wave 3: 32 / 32 / 32 / 16 MFMAs of the second level.  Fixed order per element.
+__device__ __forceinline__ void w_last_column_par(const double* su, const double* swv, double* Wk, int tid) {
+  constexpr int J = CB / SB - 1;
+  const int lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
+  v4d V[J];
+#pragma unroll
+  for (int l = 0; l < J; ++l) {
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(su[(16 * J + 4 * q + lk) * CLD + 16 * l + li],
+                                                 swv[J * SB * SB + li * SB + 4 * q + lk], acc, 0, 0, 0);
+    V[l] = acc;
+  }
+  auto rowblock = [&](int i) {
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int l = 0; l < J; ++l) {
+      if (l < i) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double a = (l == i) ? swv[i * SB * SB + (4 * q + lk) * SB + li]
+                                  : su[(16 * i + li) * CLD + 16 * l + 4 * q + lk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, V[l][q], acc, 0, 0, 0);
+      }
+    }
+    double* col = Wk + (int64_t)(16 * J + li) * CB + 16 * i + lk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) col[4 * r] = -acc[r];
+  };
+  if (wv < 3) {
+    rowblock(wv);
+    rowblock(J - 1 - wv);
+  } else {
+    rowblock(3);
+    double* col = Wk + (int64_t)(16 * J + li) * CB + 16 * J + lk;   // W_JJ, the column's diagonal block
+#pragma unroll
+    for (int r = 0; r < 4; ++r) col[4 * r] = swv[J * SB * SB + li * SB + lk + 4 * r];
   }
 }
 
@@ -308,7 +364,7 @@ __device__ __forceinline__ void w_column(const double* su, const double* swv, do
 // of the phase-serial kernel (PIPE = false, SCS_CHOL_DIAG=0).
 template <bool PIPE>
 __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
-                                                        double* __restrict__ W, int* __restrict__ info) {
+                                                        double* __restrict__ W, int* __restrict__ info, int wpar) {
   __shared__ double su[CB * CLD];   // S(r, c) = su[c*CLD + r]
   __shared__ double srinv[CB];      // 1 / U(j, j)
   __shared__ double swinv[CB / SB][SB * SB];   // inverses of the 16 x 16 diagonal blocks (col-major)
@@ -455,7 +511,8 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   if (W_BY_COLUMNS) {
     PROF_MARK(34);
     if (PIPE) {
-      if (wv == 0) w_column(su, &swinv[0][0], Wk, CB / SB - 1, lane);
+      if (wpar) w_last_column_par(su, &swinv[0][0], Wk, tid);
+      else if (wv == 0) w_column(su, &swinv[0][0], Wk, CB / SB - 1, lane);
     } else {   // every column here: wave w takes columns w and 7 - w
       w_column(su, &swinv[0][0], Wk, wv, lane);
       w_column(su, &swinv[0][0], Wk, CB / SB - 1 - wv, lane);
@@ -596,11 +653,18 @@ static bool chol_diag_pipe() {   // read per call (A/B within one process)
   return !(e && e[0] == '0');
 }
 
+// SCS_CHOL_WPAR (read per call; default on): W's last block column by all four waves
+// (w_last_column_par, r05); 0 = the one-wave recursion (w_column_t<7>)
+static int chol_wpar() {
+  const char* e = getenv("SCS_CHOL_WPAR");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st) {
   if (chol_diag_pipe())
-    hipLaunchKernelGGL(chol_diag_kernel<true>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+    hipLaunchKernelGGL(chol_diag_kernel<true>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
   else
-    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info);
+    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, 0);
   return hipGetLastError();
 }
 

@@ -939,6 +939,25 @@ def test_cholesky_dag_launches_bit_identical(m, ob, la, monkeypatch):
         assert np.array_equal(bits(a.x), bits(r.x))
 
 
+@pytest.mark.parametrize("m", [2304, 8192])
+def test_cholesky_w_last_column_parallel(m, monkeypatch):
+    """W's last block column in the diagonal kernel by all four waves as the block inverse
+    -W_{0:7,0:7}·(U_{0:7,7}·W_77) (w_last_column_par, r05) against the one-wave recursion
+    (SCS_CHOL_WPAR=0): the same W up to the association of the products, so the ProxNSCORE
+    trajectories agree to rounding; the factor's backward error at m = 8192 / 16384 is
+    test_c3_c2_shape_cholesky_backward_error's."""
+    N = 4000 if m < 8192 else 9000
+    x0 = np.random.default_rng(41).standard_normal(m) * 0.3
+    p = scsopt.Problem.synthetic(N, m, x0, losses.least_squares(1.0 / N), 1e-3, kind=3, seed=31)
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    a = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    monkeypatch.setenv("SCS_CHOL_WPAR", "0")
+    b = scsopt.iterate(scsopt.ProxNSCORE(), p, "l1", hm, max_epoch=3, verbose=0)
+    assert a.epochs == b.epochs
+    np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
+    np.testing.assert_allclose(a.x, b.x, rtol=1e-9, atol=1e-12)
+
+
 @pytest.mark.parametrize("m", [300, 1000, 2304])
 def test_householder_qr_solve(m):
     """The reference solver's Householder QR (qr.hip, scs_solve_eval mode 2: LAPACK dgeqrf / dlarfg
