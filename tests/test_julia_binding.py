@@ -71,7 +71,8 @@ def _julia_ccalls():
 
 C_SCALARS = {"Cint": {"int"}, "Int64": {"int64_t"}, "Float64": {"double"}, "UInt64": {"uint64_t"}, "Csize_t": {"size_t"},
              "Cuint": {"unsigned"}, "Int32": {"int32_t"}}
-C_POINTEE = {"Float64": "double", "Int64": "int64_t", "Int32": "int32_t", "Cint": "int", "UInt8": "unsigned char"}
+C_POINTEE = {"Float64": "double", "Int64": "int64_t", "Int32": "int32_t", "Cint": "int", "UInt8": "unsigned char",
+             "Cchar": "char"}
 
 
 def _compatible(jt, ct):
