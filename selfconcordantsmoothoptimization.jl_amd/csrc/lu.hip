@@ -227,15 +227,17 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_
   const int jn = j + 1;
   // 1. this thread's row pieces (rows > j; the pivot row j itself is only ever overwritten), in flight
   //    together with the candidate reads below
+  // (only the lanes whose 16 columns reach column j: the others' columns of an unmoved row are final,
+  // as in the r02 step -- loading them too measured slower, profiles/r05/lu_prefetch/)
   double v[NP][16];
-  bool act[NP];
+  bool have[NP];
 #pragma unroll
   for (int ps = 0; ps < NP; ++ps) {
     const int64_t i = (int64_t)g * R + ps * 32 + rr;
-    act[ps] = i < h && i > j;
-    const double* row = A + (r0 + (act[ps] ? i : 0)) * ld + c0 + cq;
+    have[ps] = i < h && i > j && (j < 0 || cq + 15 >= j);
+    const double* row = A + (r0 + (have[ps] ? i : 0)) * ld + c0 + cq;
 #pragma unroll
-    for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = act[ps] ? *(const v2d*)(row + c) : (v2d){0.0, 0.0};
+    for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = have[ps] ? *(const v2d*)(row + c) : (v2d){0.0, 0.0};
   }
   int p = j;
   double piv = 0.0, rp = 0.0;
@@ -308,6 +310,7 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_
     if (bot) {   // the displaced row j takes row p's place
 #pragma unroll
       for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = *(const v2d*)(rowj + par * LB + cq + c);
+      have[ps] = true;
     }
     if (!(bot || cq + 15 >= j)) continue;   // columns < j of an unmoved row are final
     const double x = bot ? rowj[par * LB + j] : __shfl(sel(v[ps], j & 15), (tid & ~7) | (j >> 4), 64);
@@ -335,11 +338,17 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_
     cand[npar * LU_MAXWG + g] = (bi == INT_MAX) ? -1.0 : bv;
     candi[npar * LU_MAXWG + g] = bi;
   }
-  // the candidate row and row j + 1 from the registers of the 8 lanes that hold them
+  // the candidate row and row j + 1 from the registers of the 8 lanes that hold them (a lane whose
+  // columns were final and not loaded copies them from the row itself)
 #pragma unroll
   for (int ps = 0; ps < NP; ++ps) {
     const int64_t i = (int64_t)g * R + ps * 32 + rr;
-    if (i >= h || i < jn) continue;
+    if (i >= h || i < jn || (i != bi && i != jn)) continue;
+    if (!have[ps]) {
+      const double* row = A + (r0 + i) * ld + c0 + cq;
+#pragma unroll
+      for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = *(const v2d*)(row + c);
+    }
     if (i == bi) {
 #pragma unroll
       for (int c = 0; c < 16; c += 2)
