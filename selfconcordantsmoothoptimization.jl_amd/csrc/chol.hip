@@ -542,23 +542,11 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   PROF_MARK(35);
 }
 
-// W_k = R_kk⁻¹ for the upper 128 x 128 diagonal blocks of a triangular R (the QR solve): the
-// inverse part of chol_diag_kernel (the 16 x 16 inverses, then recursive doubling on MFMA) on a
-// block whose factor is given; the strictly lower part of the block is ignored.
-__global__ __launch_bounds__(DNT) void tri_inv_kernel(const double* __restrict__ R, int64_t ld,
-                                                      double* __restrict__ W) {
-  __shared__ double su[CB * CLD];
-  __shared__ double srinv[CB];
-  __shared__ double swinv[CB / SB][SB * SB];
-  const int k = blockIdx.x, tid = threadIdx.x;
-  const double* blk = R + (int64_t)k * CB * ld + (int64_t)k * CB;
-  for (int e = tid; e < CB * CB; e += DNT) {
-    const int c = e >> 7, r = e & 127;
-    su[c * CLD + r] = (r <= c) ? blk[(int64_t)c * ld + r] : 0.0;
-  }
-  __syncthreads();
-  if (tid < CB) srinv[tid] = 1.0 / su[tid * CLD + tid];
-  __syncthreads();
+// the inverse of an upper 128 x 128 block already in su (S(r, c) = su[c·CLD + r], zero below the diagonal)
+// with its reciprocal pivots in srinv: the 16 x 16 diagonal inverses (one wave each, in registers), then
+// the doubling levels 16 -> 32 -> 64 on MFMA; W = S⁻¹ ends in su's upper triangle (the strictly-lower
+// triangle is the doubling's scratch)
+__device__ __forceinline__ void tri_inv_loaded(double* su, const double* srinv, double (*swinv)[SB * SB], int tid) {
   for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) {
     const int o = kb * SB, c = tid & 15;
     double w[SB];
@@ -584,12 +572,70 @@ __global__ __launch_bounds__(DNT) void tri_inv_kernel(const double* __restrict__
   chol_inv_double_mfma<16>(su, tid);
   chol_inv_double_mfma<32>(su, tid);
   chol_inv_double_mfma<64>(su, tid);
+}
+
+// W_k = R_kk⁻¹ for the upper 128 x 128 diagonal blocks of a triangular R (the QR solve): the
+// inverse part of chol_diag_kernel (the 16 x 16 inverses, then recursive doubling on MFMA) on a
+// block whose factor is given; the strictly lower part of the block is ignored.
+__global__ __launch_bounds__(DNT) void tri_inv_kernel(const double* __restrict__ R, int64_t ld,
+                                                      double* __restrict__ W) {
+  __shared__ double su[CB * CLD];
+  __shared__ double srinv[CB];
+  __shared__ double swinv[CB / SB][SB * SB];
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const double* blk = R + (int64_t)k * CB * ld + (int64_t)k * CB;
+  for (int e = tid; e < CB * CB; e += DNT) {
+    const int c = e >> 7, r = e & 127;
+    su[c * CLD + r] = (r <= c) ? blk[(int64_t)c * ld + r] : 0.0;
+  }
+  __syncthreads();
+  if (tid < CB) srinv[tid] = 1.0 / su[tid * CLD + tid];
+  __syncthreads();
+  tri_inv_loaded(su, srinv, swinv, tid);
   double* Wk = W + (int64_t)k * CB * CB;
   for (int e = tid; e < CB * CB; e += DNT) {
     const int c = e >> 7, r = e & 127;
     Wk[(int64_t)c * CB + r] = (r <= c) ? su[c * CLD + r] : 0.0;
   }
 }
+
+// L11⁻¹ and U11⁻¹ of the LU's factored 128 x 128 diagonal block (lu.hip: row-major, unit-lower L and
+// upper U sharing the block) by the same 16 x 16 inverses + MFMA doubling (r05; the r02 kernel
+// eliminated one row per barrier, 128 of them: 226 us per launch, 14 % of the n = 8192 factor).
+// Workgroup 0 inverts Lᵀ (upper, unit diagonal; S column c = row c of L), workgroup 1 U; both write
+// row-major 128 x 128: Linv = (Lᵀ)⁻¹ transposed, Uinv = U⁻¹.  A zero pivot of U gives inf / NaN, as
+// the elimination did (info already holds it).
+__global__ __launch_bounds__(DNT) void lu_tri_inv_kernel(const double* __restrict__ A, int64_t ld, int64_t r0,
+                                                         double* __restrict__ Linv, double* __restrict__ Uinv) {
+  __shared__ double su[CB * CLD];
+  __shared__ double srinv[CB];
+  __shared__ double swinv[CB / SB][SB * SB];
+  const bool lower = blockIdx.x == 0;
+  const int tid = threadIdx.x;
+  const double* blk = A + r0 * ld + r0;
+  for (int e = tid; e < CB * CB; e += DNT) {
+    const int i = e >> 7, j = e & 127;   // block row i, column j (coalesced over j)
+    const double v = blk[(int64_t)i * ld + j];
+    if (lower) su[i * CLD + j] = (j < i) ? v : ((j == i) ? 1.0 : 0.0);   // S(j, i) = L(i, j)
+    else su[j * CLD + i] = (i <= j) ? v : 0.0;                             // S(i, j) = U(i, j)
+  }
+  __syncthreads();
+  if (tid < CB) srinv[tid] = lower ? 1.0 : 1.0 / su[tid * CLD + tid];
+  __syncthreads();
+  tri_inv_loaded(su, srinv, swinv, tid);
+  double* out = lower ? Linv : Uinv;
+  for (int e = tid; e < CB * CB; e += DNT) {
+    const int i = e >> 7, j = e & 127;   // out(i, j); W(r, c) = su[c·CLD + r], r <= c
+    const double v = lower ? ((j <= i) ? su[i * CLD + j] : 0.0) : ((i <= j) ? su[j * CLD + i] : 0.0);
+    out[(int64_t)i * CB + j] = v;
+  }
+}
+
+hipError_t launch_lu_tri_inv(const double* A, int64_t ld, int64_t r0, double* Linv, double* Uinv, hipStream_t st) {
+  hipLaunchKernelGGL(lu_tri_inv_kernel, dim3(2), dim3(DNT), 0, st, A, ld, r0, Linv, Uinv);
+  return hipGetLastError();
+}
+
 
 // T of a 128-column compact WY block (dlarft forward, columnwise; qr.hip) from Gv = VᵀV and tau,
 // by the same doubling as W = U⁻¹: T = [T11, -T11 G12 T22; 0, T22] with G12 = V1ᵀV2 in the place

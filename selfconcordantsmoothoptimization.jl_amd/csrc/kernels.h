@@ -140,6 +140,8 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st);
 void chol_aux_free(CholAux* a);
 // the 128 x 128 diagonal block k: factor in place, W_k = U_kk⁻¹ (SCS_CHOL_DIAG=0: phase-serial kernel)
 hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st);
+// L11⁻¹ and U11⁻¹ (row-major 128 x 128) of the LU's factored diagonal block at (r0, r0) (chol.hip)
+hipError_t launch_lu_tri_inv(const double* A, int64_t ld, int64_t r0, double* Linv, double* Uinv, hipStream_t st);
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* aux,
                        const int2* trilist, int* info, hipStream_t st);
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y, CholAux* a,
@@ -170,6 +172,7 @@ struct LUAux {
   int* candi = nullptr;      // [2][256] their rows
   double* candrow = nullptr; // [2][256][128] their panel rows
   double* rowj = nullptr;    // [2][128] copy of row j (the row the pivot row displaces)
+  unsigned long long* gran = nullptr;   // [2][128][4] cooperative panel's {tag, word} candidate granules
   int* ipiv = nullptr;       // [npad] pivot row of each column (0-based, absolute)
   int2* pairs = nullptr;     // [nblk][256] composed row moves of each block (dst, src)
   int* npairs = nullptr;     // [nblk]

@@ -361,6 +361,211 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_
   }
 }
 
+// ---- the cooperative panel (r05) ---------------------------------------------------------------------
+// The whole 128-column panel as ONE launch of G = h / 128 workgroups (one per CU and all resident: G <=
+// 128, h <= 16384), each holding its 128 rows in registers through the 128 column steps (4 passes x 32
+// rows x 8 lanes of 16 columns, the step kernels' layout).  The per-column grid-wide hand-off is the
+// candidate exchange itself, in MI355X_MICROARCH.md's publish / consume forms (§ visibility, Valid forms,
+// row 1): every workgroup publishes its candidate of the next column -- |a| and its row as three 8-byte
+// {tag, word} granules (tag = column + 1), one sc1 store each by one lane -- after write-through (sc1)
+// copies of the candidate's panel row and, by its owner, of row j + 1 (the row a pivot displaces),
+// drained by every storing wave (s_waitcnt vmcnt(0)) and a workgroup barrier.  Every wave sweeps all G
+// granule triples with relaxed sc1 loads (bounded spin) until every tag is the column's, takes the
+// pivot by the step kernels' rule (larger |a|, then the smaller row), and reads the pivot row (and, at
+// the pivot's old position, the displaced row) with sc1 loads.  Two granule / row slots by column
+// parity: a workgroup publishes column j + 2 only after every workgroup has published column j + 1,
+// i.e. after all have read column j.  The arithmetic per element is the step kernels' (l = x·(1/u_j),
+// or x / u_j below DBL_MIN; a_ic -= l·u_c), so the factor and the pivots are theirs bit for bit; the
+// rows go back to A once, after the last column.  A sweep past its bound (a workgroup that never became
+// resident) stores info = -1 and leaves the launch.
+constexpr int LUC_RW = 128;                   // panel rows per workgroup
+constexpr int LUC_MAXWG = 128;                // workgroups (= CUs) at most
+constexpr int LUC_LDS = 96 * 1024;            // dynamic LDS that keeps a second workgroup off the CU
+constexpr unsigned LUC_SPIN_MAX = 1u << 19;   // sweeps before giving up (~0.5 s)
+constexpr int LUC_GRAN = 2 * LUC_MAXWG * 4;   // granule words per slot pair; word LUC_GRAN = the abort word
+typedef __attribute__((address_space(1))) unsigned long long luc_gu64;
+
+__device__ __forceinline__ void luc_st(double* p, double v) {
+  __hip_atomic_store((luc_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double luc_ld(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((luc_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
+                                                              int64_t c0, unsigned long long* gran, double* crow,
+                                                              double* rowj, int* ipiv, int* info) {
+  __shared__ double sv[LU_NT / 64];
+  __shared__ int si[LU_NT / 64], sw[LU_NT / 64];
+  const int tid = threadIdx.x, g = blockIdx.x, nwg = gridDim.x, lane = tid & 63;
+  const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
+  const int base = g * LUC_RW + rr;   // this thread's panel position in pass ps: base + 32 ps
+  if (gran[LUC_GRAN] != 0) return;   // an earlier panel of this factorization gave up (info = -1)
+  double v[4][16];
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+    const double* row = A + (r0 + base + 32 * ps) * ld + c0 + cq;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = *(const v2d*)(row + c);
+  }
+  // this workgroup's candidate of column jn (rows >= jn) with its row, and row jn, then the granules
+  auto publish = [&](int jn) {
+    double bv = -1.0;
+    int bi = INT_MAX;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const int i = base + 32 * ps;
+      if (i >= jn && q == (jn >> 4)) {
+        const double a = fabs(sel(v[ps], jn & 15));
+        if (lu_better(a, i, bv, bi)) {
+          bv = a;
+          bi = i;
+        }
+      }
+    }
+    int bw = g;
+    lu_block_argmax(bv, bi, bw, sv, si, sw);
+    const int par = jn & 1;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const int i = base + 32 * ps;
+      if (i == bi) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) luc_st(crow + ((int64_t)par * LUC_MAXWG + g) * LB + cq + c, v[ps][c]);
+      }
+      if (i == jn) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) luc_st(rowj + par * LB + cq + c, v[ps][c]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned long long tag = (unsigned long long)(jn + 1) << 32;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
+      luc_gu64* gp = (luc_gu64*)(gran + ((int64_t)par * LUC_MAXWG + g) * 4);
+      __hip_atomic_store(gp + 0, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gp + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gp + 2, tag | (unsigned)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  publish(0);
+  for (int j = 0; j < LB; ++j) {
+    const int par = j & 1;
+    const unsigned tag = (unsigned)(j + 1);
+    // 1. every wave: sweep the G candidates of column j until all carry this column's tag
+    double cv;
+    int ci, cw;
+    {
+      const luc_gu64* gp = (const luc_gu64*)(gran + (int64_t)par * LUC_MAXWG * 4);
+      unsigned spins = 0;
+      for (;;) {
+        bool ok = true;
+        cv = -1.0;
+        ci = INT_MAX;
+        cw = -1;
+#pragma unroll
+        for (int t = 0; t < LUC_MAXWG / 64; ++t) {
+          const int w = lane + 64 * t;
+          if (w < nwg) {
+            const unsigned long long x0 = __hip_atomic_load(gp + 4 * w + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long x1 = __hip_atomic_load(gp + 4 * w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long x2 = __hip_atomic_load(gp + 4 * w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag && (unsigned)(x2 >> 32) == tag;
+            double a = __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
+            int r = (int)(unsigned)x2;
+            if (!(a >= 0.0)) {   // no candidate (or NaN): never wins
+              a = -1.0;
+              r = INT_MAX;
+            }
+            if (lu_better(a, r, cv, ci)) {
+              cv = a;
+              ci = r;
+              cw = w;
+            }
+          }
+        }
+        if (__all(ok)) break;
+        if (++spins > LUC_SPIN_MAX) {   // the later panels of this factorization leave at once
+          if (lane == 0) {
+            *info = -1;
+            gran[LUC_GRAN] = 1;
+          }
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double v2 = __shfl_xor(cv, o, 64);
+        const int i2 = __shfl_xor(ci, o, 64);
+        const int w2 = __shfl_xor(cw, o, 64);
+        if (lu_better(v2, i2, cv, ci)) {
+          cv = v2;
+          ci = i2;
+          cw = w2;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: the row loads stay below
+    // 2. the pivot row u (sc1 loads), as the step kernels choose it
+    int p = j;
+    const double* urow = (cv < 0.0) ? rowj + par * LB : crow + ((int64_t)par * LUC_MAXWG + cw) * LB;
+    if (cv >= 0.0) p = ci;
+    double u[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) u[c] = luc_ld(urow + cq + c);
+    double piv = luc_ld(urow + j);
+    const bool scale = (piv != 0.0);
+    if (!scale) {   // getf2: zero pivot -> no interchange, no scaling (the column below is zero)
+      p = j;
+      urow = rowj + par * LB;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) u[c] = luc_ld(urow + cq + c);
+      piv = luc_ld(urow + j);
+    }
+    const double rp = 1.0 / piv;
+    if (g == 0 && tid == 0) {
+      ipiv[r0 + j] = (int)(r0 + p);
+      if (!scale && *info == 0) *info = (int)(r0 + j + 1);
+    }
+    // 3. row j <- u, row p <- the displaced row j, every row i > j: l = a_ij / u_j, a_ic -= l·u_c
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const int i = base + 32 * ps;
+      if (i < j) continue;
+      if (i == j) {
+        if (p != j) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c) v[ps][c] = u[c];
+        }
+        continue;
+      }
+      if (i == p) {   // (p != j here)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[ps][c] = luc_ld(rowj + par * LB + cq + c);
+      }
+      const double x = __shfl(sel(v[ps], j & 15), (tid & ~7) | (j >> 4), 64);
+      const double l = scale ? (fabs(piv) >= 2.2250738585072014e-308 ? x * rp : x / piv) : x;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int col = cq + c;
+        if (col > j) v[ps][c] -= l * u[c];
+        else if (col == j) v[ps][c] = l;
+      }
+    }
+    if (j + 1 < LB) publish(j + 1);
+  }
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+    double* row = A + (r0 + base + 32 * ps) * ld + c0 + cq;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(row + c) = *(const v2d*)(v[ps] + c);
+  }
+}
+
 // Compose block k's 128 interchanges (rows r0+s <-> ipiv[r0+s], in order) into row moves
 // "row dst <- previous row src" (<= 256 of them).  One wave.
 __global__ __launch_bounds__(64) void lu_perm_kernel(const int* __restrict__ ipiv, int r0, int2* __restrict__ pairs,
@@ -368,12 +573,16 @@ __global__ __launch_bounds__(64) void lu_perm_kernel(const int* __restrict__ ipi
   __shared__ int top[LB];         // content of rows r0 .. r0+127
   __shared__ int brow[LB], bval[LB];   // touched rows below the block: (row, content)
   __shared__ int nb;
+  __shared__ int sp[LB];   // the block's pivots, loaded once (r02 read one per step: 64 us per launch)
   const int lane = threadIdx.x;
-  for (int t = lane; t < LB; t += 64) top[t] = r0 + t;
+  for (int t = lane; t < LB; t += 64) {
+    top[t] = r0 + t;
+    sp[t] = ipiv[r0 + t];
+  }
   if (lane == 0) nb = 0;
   __syncthreads();
   for (int s = 0; s < LB; ++s) {
-    const int pr = ipiv[r0 + s];
+    const int pr = sp[s];
     if (pr == r0 + s) continue;
     if (pr < r0 + LB) {
       if (lane == 0) {
@@ -421,16 +630,35 @@ __global__ __launch_bounds__(256) void lu_swap_cols_kernel(double* A, int64_t ld
                                                            const int2* __restrict__ pairs,
                                                            const int* __restrict__ npairs) {
   __shared__ double buf[LU_MAXPAIRS * SW_COLS];
+  __shared__ int2 sp[LU_MAXPAIRS];
   const int np = *npairs;
   if (np == 0) return;
+  // the moves to LDS first, then the row loads eight at a time in flight (r02 chained a pairs[] load in
+  // front of every row load: 52 us per launch)
+  for (int k = threadIdx.x; k < np; k += 256) sp[k] = pairs[k];
+  __syncthreads();
   const int col = threadIdx.x & (SW_COLS - 1), kg = threadIdx.x / SW_COLS;
   const int64_t c = c_lo + (int64_t)blockIdx.x * SW_COLS + col;
   const bool ok = (int64_t)blockIdx.x * SW_COLS + col < w;
-  for (int k = kg; k < np; k += 256 / SW_COLS)
-    if (ok) buf[k * SW_COLS + col] = A[(int64_t)pairs[k].y * ld + c];
+  constexpr int KS = 256 / SW_COLS;
+  if (ok) {
+    for (int k0 = kg; k0 < np; k0 += 8 * KS) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * KS;
+        v[u] = (k < np) ? A[(int64_t)sp[k].y * ld + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * KS;
+        if (k < np) buf[k * SW_COLS + col] = v[u];
+      }
+    }
+  }
   __syncthreads();
-  for (int k = kg; k < np; k += 256 / SW_COLS)
-    if (ok) A[(int64_t)pairs[k].x * ld + c] = buf[k * SW_COLS + col];
+  if (ok)
+    for (int k = kg; k < np; k += KS) A[(int64_t)sp[k].x * ld + c] = buf[k * SW_COLS + col];
 }
 
 // L11⁻¹ (block 0) and U11⁻¹ (block 1) of the factored 128 x 128 diagonal block, row-major.
@@ -610,6 +838,7 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
   al((void**)&a->candi, sizeof(int) * 2 * LU_MAXWG);
   al((void**)&a->candrow, sizeof(double) * 2 * LU_MAXWG * LB);
   al((void**)&a->rowj, sizeof(double) * 2 * LB);
+  al((void**)&a->gran, sizeof(unsigned long long) * (LUC_GRAN + 2));
   al((void**)&a->ipiv, sizeof(int) * npad);
   al((void**)&a->pairs, sizeof(int2) * (size_t)nblk * LU_MAXPAIRS);
   al((void**)&a->npairs, sizeof(int) * nblk);
@@ -630,23 +859,41 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
 }
 
 void lu_aux_free(LUAux* a) {
-  void* ps[] = {a->cand, a->candi, a->candrow, a->rowj, a->ipiv, a->pairs, a->npairs, a->Linv,
-                a->Uinv, a->T,    a->UT,    a->w,       a->sq,   a->row1};
+  void* ps[] = {a->cand, a->candi, a->candrow, a->rowj, a->gran, a->ipiv, a->pairs, a->npairs,
+                a->Linv, a->Uinv, a->T,     a->UT,      a->w,    a->sq,   a->row1};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   *a = LUAux();
 }
 
-// SCS_LU_PANEL (read per call): unset / 2 = lu_panel_step2_kernel up to two 32-row passes per workgroup
-// (n <= 16384), 1 = the r02 column step everywhere (bitwise the same factor)
+// SCS_LU_PANEL (read per call): unset / 3 = the cooperative one-launch panel where G = h / 128 <= 128
+// (lu_panel_coop_kernel, r05), else the column steps; 2 = lu_panel_step2_kernel up to two 32-row passes
+// per workgroup (n <= 16384); 1 = the r02 column step everywhere (all bitwise the same factor)
 static int lu_panel_mode() {
   const char* e = getenv("SCS_LU_PANEL");
+  return e ? atoi(e) : 3;
+}
+
+static hipError_t lu_coop_attr() {   // the dynamic LDS above the 64 KiB default, once per process
+  static hipError_t done = hipFuncSetAttribute((const void*)lu_panel_coop_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LUC_LDS);
+  return done;
+}
+
+// SCS_LU_INV (read per call): unset / 2 = the diagonal block's inverses by 16 x 16 inverses + MFMA doubling
+// (lu_tri_inv_kernel, chol.hip), 1 = the r02 row-by-row elimination (lu_diag_inv_kernel)
+static int lu_inv_mode() {
+  const char* e = getenv("SCS_LU_INV");
   return e ? atoi(e) : 2;
 }
 
 hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st) {
   if (npad % LB != 0 || npad > a->npad || ld < npad) return hipErrorInvalidValue;
   const int nblk = (int)(npad / LB);
+  if (lu_panel_mode() == 3) {   // the cooperative panels' abort word, once per factorization
+    const hipError_t e = hipMemsetAsync(a->gran + LUC_GRAN, 0, sizeof(unsigned long long) * 2, st);
+    if (e != hipSuccess) return e;
+  }
   if (npad > n)
     hipLaunchKernelGGL(lu_pad_kernel, dim3((unsigned)ceil_div(npad - n, 256)), dim3(256), 0, st, A, ld, n, npad);
   for (int k = 0; k < nblk; ++k) {
@@ -654,6 +901,14 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
     const int R = 32 * (int)ceil_div(h, 32 * LU_MAXWG);
     const int nwg = (int)ceil_div(h, R);
     const int npass = R / 32, mode = lu_panel_mode();
+    const int64_t gco = h / LUC_RW;
+    if (mode == 3 && gco <= LUC_MAXWG) {
+      hipError_t e = lu_coop_attr();
+      if (e == hipSuccess) e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * LUC_GRAN, st);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(lu_panel_coop_kernel, dim3((unsigned)gco), dim3(LU_NT), LUC_LDS, st, A, ld, r0, c0, a->gran,
+                         a->candrow, a->rowj, a->ipiv, info);
+    } else
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)
         hipLaunchKernelGGL(lu_panel_step2_kernel<1>, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
@@ -667,8 +922,11 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
     }
     int2* pairs = a->pairs + (int64_t)k * LU_MAXPAIRS;
     hipLaunchKernelGGL(lu_perm_kernel, dim3(1), dim3(64), 0, st, a->ipiv, (int)r0, pairs, a->npairs + k);
-    hipLaunchKernelGGL(lu_diag_inv_kernel, dim3(2), dim3(256), 0, st, A, ld, r0, a->Linv + (int64_t)k * LB * LB,
-                       a->Uinv + (int64_t)k * LB * LB);
+    if (lu_inv_mode() == 1)
+      hipLaunchKernelGGL(lu_diag_inv_kernel, dim3(2), dim3(256), 0, st, A, ld, r0, a->Linv + (int64_t)k * LB * LB,
+                         a->Uinv + (int64_t)k * LB * LB);
+    else
+      (void)launch_lu_tri_inv(A, ld, r0, a->Linv + (int64_t)k * LB * LB, a->Uinv + (int64_t)k * LB * LB, st);
     const int64_t w = npad - c0 - LB;   // columns right of the panel
     if (w == 0) break;
     hipLaunchKernelGGL(lu_swap_cols_kernel, dim3((unsigned)ceil_div(w, SW_COLS)), dim3(256), 0, st, A, ld, c0 + LB, w,

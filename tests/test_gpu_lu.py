@@ -104,18 +104,55 @@ def test_solve_eval_lu_vs_cholesky():
     np.testing.assert_allclose(xl, xr, rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("mode", ["2", "3"])
 @pytest.mark.parametrize("n", [300, 2176, 8320])
-def test_lu_prefetch_panel_bit_identical(n, monkeypatch):
-    """The column step with its rows prefetched beside the candidate reads and the next candidate row /
-    row j + 1 published from registers (lu_panel_step2_kernel, r05) does the same arithmetic as the
-    r02 step (SCS_LU_PANEL=1): the same pivots and the same solution bit for bit.  n = 8320: the first
-    panel has two 32-row passes per workgroup (h > 8192)."""
+def test_lu_panel_variants_bit_identical(n, mode, monkeypatch):
+    """Every panel form does the r02 column step's arithmetic (SCS_LU_PANEL=1): the same pivots and the
+    same solution bit for bit.  2: the column step with its rows prefetched beside the candidate reads
+    (lu_panel_step2_kernel); 3 (default): the cooperative one-launch panel, rows in registers, the
+    candidates exchanged as tagged granules (lu_panel_coop_kernel).  n = 8320: 65 workgroups in the
+    first panel (two 32-row passes per workgroup for mode 2)."""
     rng = np.random.default_rng(n + 7)
     A = rng.standard_normal((n, n))
     b = rng.standard_normal(n)
+    monkeypatch.setenv("SCS_LU_PANEL", mode)
     x2, ipiv2, info2 = scsopt.lu_solve(A, b)
     monkeypatch.setenv("SCS_LU_PANEL", "1")
     x1, ipiv1, info1 = scsopt.lu_solve(A, b)
     assert info1 == info2 == 0
     assert np.array_equal(ipiv1, ipiv2)
     assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
+
+
+def test_lu_coop_panel_largest_grid(monkeypatch):
+    """n = 16384: the cooperative panel at its largest grid (128 workgroups, one per CU) -- bitwise the
+    column steps, backward error <= 1e-13."""
+    n = 16384
+    rng = np.random.default_rng(5)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    x3, ipiv3, info3 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_PANEL", "1")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info1 == info3 == 0
+    assert np.array_equal(ipiv1, ipiv3)
+    assert np.array_equal(x1.view(np.uint64), x3.view(np.uint64))
+    assert _bwd(A, x3, b) <= 1e-13
+
+
+@pytest.mark.parametrize("n", [300, 2176])
+def test_lu_doubling_inverse_matches_elimination(n, monkeypatch):
+    """The diagonal block's L11⁻¹ / U11⁻¹ by 16 x 16 inverses + MFMA doubling (lu_tri_inv_kernel, r05)
+    against the r02 row-by-row elimination (SCS_LU_INV=1): different rounding of the same inverses, so
+    the same pivots (no near-ties here) and solutions within a few ulps of cond(A)."""
+    rng = np.random.default_rng(n + 11)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    x2, ipiv2, info2 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_INV", "1")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info1 == info2 == 0
+    assert np.array_equal(ipiv1, ipiv2)
+    kappa = float(np.linalg.cond(A, np.inf))
+    assert np.max(np.abs(x1 - x2)) <= 1e-14 * kappa * float(np.abs(x1).max())
+    assert _bwd(A, x2, b) <= 1e-13
