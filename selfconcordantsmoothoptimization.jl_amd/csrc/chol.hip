@@ -513,6 +513,11 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
     if (PIPE) {
       if (wpar) w_last_column_par(su, &swinv[0][0], Wk, tid);
       else if (wv == 0) w_column(su, &swinv[0][0], Wk, CB / SB - 1, lane);
+    } else if (wpar) {   // columns 0..6 (wave w: w and 6 - w), then the last one by all waves, as PIPE
+      w_column(su, &swinv[0][0], Wk, wv, lane);
+      if (wv < 3) w_column(su, &swinv[0][0], Wk, CB / SB - 2 - wv, lane);
+      __syncthreads();   // the transposed off-diagonal blocks w_last_column_par reads
+      w_last_column_par(su, &swinv[0][0], Wk, tid);
     } else {   // every column here: wave w takes columns w and 7 - w
       w_column(su, &swinv[0][0], Wk, wv, lane);
       w_column(su, &swinv[0][0], Wk, CB / SB - 1 - wv, lane);
@@ -710,7 +715,7 @@ hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, 
   if (chol_diag_pipe())
     hipLaunchKernelGGL(chol_diag_kernel<true>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
   else
-    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, 0);
+    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
   return hipGetLastError();
 }
 
@@ -754,6 +759,28 @@ static unsigned bulk_skip_mask(int nblk) {
 }
 
 static hipError_t create_bulk_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
+
+// The lookahead's two streams must sit on different hardware queues (r05).  The runtime gives each
+// stream priority its own pool of hardware queues and, once a pool holds GPU_MAX_HW_QUEUES (4) queues,
+// maps a new stream onto the least-used queue of its pool -- so in a process where torch and RCCL have
+// created streams, the caller's stream (the chain) and the bulk stream could land on ONE hardware queue
+// and the two halves of the factor then ran back to back: +6.8 ms of solve per C3-shaped step with the
+// exchange forced at world 1, every kernel of the step on one queue in the trace
+// (profiles/r05/rccltrace/).  Streams of different priority cannot share a queue.  SCS_CHOL_CHAIN (read
+// per call): 2 (default) the bulk stream at the device's greatest priority, the chain on the caller's
+// stream; 1 the chain on a stream of its own at the greatest priority, joined to the caller's by events;
+// 0 both at normal priority (r04).
+static hipError_t create_hiprio_stream(hipStream_t* s) {
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+  return e;
+}
+
+static int chol_chain_mode() {
+  const char* e = getenv("SCS_CHOL_CHAIN");
+  return e ? atoi(e) : 2;
+}
 
 // SCS_CHOL_SKIP_MAXTILES (A/B; unset = no limit): bulk launches of more tiles than this run on every
 // CU (skip set 0) -- the bulk-bound early outer blocks -- and only the smaller ones keep the skip set
@@ -800,6 +827,8 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess && !sb.empty())
     e = hipMemcpyAsync(a->sbl, sb.data(), sizeof(int2) * sb.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = create_bulk_stream(&a->st2);
+  if (e == hipSuccess) e = create_hiprio_stream(&a->stc);
+  if (e == hipSuccess) e = create_hiprio_stream(&a->st2h);
   if (e == hipSuccess) e = hipMalloc(&a->bctr, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned));
   if (e == hipSuccess) e = hipMemsetAsync(a->bctr, 0, (size_t)BCTR_SLOTS * 16 * sizeof(unsigned), st);
   a->bslot = 0;
@@ -816,6 +845,8 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev2, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev3, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev4, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev0, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&a->ev5, hipEventDisableTiming);
   // the one-launch triangular solves' block flags (generation-stamped: never reset) and error flag
   if (e == hipSuccess) e = hipMalloc(&a->sflags, sizeof(unsigned) * 2 * (size_t)nblk + sizeof(int));
   if (e == hipSuccess) e = hipMemsetAsync(a->sflags, 0, sizeof(unsigned) * 2 * (size_t)nblk + sizeof(int), st);
@@ -827,12 +858,16 @@ hipError_t chol_aux_init(CholAux* a, int64_t mpad, hipStream_t st) {
 
 void chol_aux_free(CholAux* a) {
   if (a->st2) (void)hipStreamSynchronize(a->st2);
+  if (a->stc) (void)hipStreamSynchronize(a->stc);
+  if (a->st2h) (void)hipStreamSynchronize(a->st2h);
   if (a->w) (void)hipFree(a->w);
   if (a->rect) (void)hipFree(a->rect);
   if (a->ev1) (void)hipEventDestroy(a->ev1);
   if (a->ev2) (void)hipEventDestroy(a->ev2);
   if (a->ev3) (void)hipEventDestroy(a->ev3);
   if (a->ev4) (void)hipEventDestroy(a->ev4);
+  if (a->ev0) (void)hipEventDestroy(a->ev0);
+  if (a->ev5) (void)hipEventDestroy(a->ev5);
   for (auto& q : a->ssched) {
     if (q.work) (void)hipFree(q.work);
     if (q.comb) (void)hipFree(q.comb);
@@ -858,10 +893,12 @@ void chol_aux_free(CholAux* a) {
   a->dstep.clear();
   a->dnext.clear();
   if (a->st2) (void)hipStreamDestroy(a->st2);
+  if (a->stc) (void)hipStreamDestroy(a->stc);
+  if (a->st2h) (void)hipStreamDestroy(a->st2h);
   a->w = nullptr;
   a->rect = nullptr;
-  a->ev1 = a->ev2 = a->ev3 = a->ev4 = nullptr;
-  a->st2 = nullptr;
+  a->ev1 = a->ev2 = a->ev3 = a->ev4 = a->ev0 = a->ev5 = nullptr;
+  a->st2 = a->stc = a->st2h = nullptr;
 }
 
 static const int2* rect_list(const CholAux* a, int R) { return a->rect + (int64_t)a->nblk * (R - 1) * R / 2; }
@@ -1286,10 +1323,20 @@ static bool chol_sbl() {
 }
 
 hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W, const CholAux* a,
-                       const int2* trilist, int* info, hipStream_t st) {
+                       const int2* trilist, int* info, hipStream_t st_caller) {
   const int nblk = (int)(mpad / CB);
   const int OB = outer_block_for(nblk);
   const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
+  // the chain's and the bulk stream (create_hiprio_stream): never one hardware queue
+  const int cmode = chol_chain_mode();
+  hipStream_t st = st_caller;
+  hipStream_t sb = (cmode == 2 && a->st2h) ? a->st2h : a->st2;
+  if (la && cmode == 1 && a->stc && a->ev0 && a->ev5) {
+    hipError_t ej = hipEventRecord(a->ev0, st_caller);
+    if (ej == hipSuccess) ej = hipStreamWaitEvent(a->stc, a->ev0, 0);
+    if (ej != hipSuccess) return ej;
+    st = a->stc;
+  }
   const bool dag = chol_dag_on() && a->serr;
   const bool steps = !dag && ba_steps() && a->sscr && OB <= 16;
   const bool split = la && c12_split() && a->ev4;
@@ -1356,8 +1403,8 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     }
     // Bb on st2 once A_t is done (stream order keeps C12_{t-1} before it)
     if (e == hipSuccess) e = hipEventRecord(a->ev3, st);
-    wait(a->st2, a->ev3);
-    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, a->st2, true);
+    wait(sb, a->ev3);
+    if (e == hipSuccess) e = strip_solve(G, ld, W, a, i0, i1, i1 + OB, nc - OB, sb, true);
     // Ba, C1a on the chain after C12a_{t-1} (and so after everything before it on st2)
     if (c12_pending) wait(st, split ? a->ev4 : a->ev2);
     const int n1a = (OB * (OB + 1)) / 2;
@@ -1373,27 +1420,31 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     // C12 on st2 after Ba (it reads X's columns of the next block); split: C12a (the tiles the
     // chain's next Ba and C1a read) as a latency launch, its event, then C12b
     if (e == hipSuccess) e = hipEventRecord(a->ev1, st);
-    wait(a->st2, a->ev1);
+    wait(sb, a->ev1);
     const int n2a = split ? std::min(ntri, OB * (2 * OB + 1)) : n1a;   // 2OB(2OB+1)/2 tiles
     if (split) {
       if (e == hipSuccess && n2a > n1a)
         e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist + n1a, n2a - n1a,
-                              trail, ld, 2 | 4, a->st2);
-      if (e == hipSuccess) e = hipEventRecord(a->ev4, a->st2);
+                              trail, ld, 2 | 4, sb);
+      if (e == hipSuccess) e = hipEventRecord(a->ev4, sb);
     }
     if (e == hipSuccess && ntri > n2a) {
-      unsigned* ctr = bulk_ctr(a, a->st2, &e);
+      unsigned* ctr = bulk_ctr(a, sb, &e);
       const bool sbo = split && a->sbl && (2 * OB) % 8 == 0 && nc % 8 == 0 && chol_sbl();
       if (e == hipSuccess)
         e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, (sbo ? a->sbl : trilist) + n2a,
-                                ntri - n2a, trail, ld, 2 | 4, ctr, bulk_skip_for(a, ntri - n2a), a->bslots, a->st2,
+                                ntri - n2a, trail, ld, 2 | 4, ctr, bulk_skip_for(a, ntri - n2a), a->bslots, sb,
                                 true);
     }
-    if (e == hipSuccess) e = hipEventRecord(a->ev2, a->st2);
+    if (e == hipSuccess) e = hipEventRecord(a->ev2, sb);
     if (e != hipSuccess) return e;
     c12_pending = true;
   }
   if (c12_pending) wait(st, a->ev2);
+  if (e == hipSuccess && st != st_caller) {   // the caller's stream continues behind the whole factor
+    e = hipEventRecord(a->ev5, st);
+    wait(st_caller, a->ev5);
+  }
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

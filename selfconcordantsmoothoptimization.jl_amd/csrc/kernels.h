@@ -95,7 +95,9 @@ struct CholAux {             // device constants of the two-level factorization 
   double* w = nullptr;       // [128 x +1.0 | mpad x -1.0] Gram weights (panel solve | block updates)
   int2* rect = nullptr;      // R x nblk rectangle tile lists, R = 1..4 (bj-major)
   hipStream_t st2 = nullptr; // lookahead: the bulk stream (strip solve beyond the next block, C12)
-  hipEvent_t ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
+  hipStream_t stc = nullptr; // lookahead: the chain's own high-priority stream (SCS_CHOL_CHAIN=1)
+  hipStream_t st2h = nullptr;   // lookahead: the bulk stream at high priority (default: its own HW queue)
+  hipEvent_t ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev0 = nullptr, ev5 = nullptr;
   int nblk = 0;
   // the bulk stream's launches as CU-bounded persistent launches (gram_launch_bounded): claim /
   // arrival counters, the skipped CU ids (SCS_CHOL_BULK_SKIP), workgroup slots of the device
@@ -172,7 +174,7 @@ struct LUAux {
   int* candi = nullptr;      // [2][256] their rows
   double* candrow = nullptr; // [2][256][128] their panel rows
   double* rowj = nullptr;    // [2][128] copy of row j (the row the pivot row displaces)
-  unsigned long long* gran = nullptr;   // [2][128][4] cooperative panel's {tag, word} candidate granules
+  unsigned long long* gran = nullptr;   // cooperative panel: {tag, word} granules (candidates, rows), abort word
   int* ipiv = nullptr;       // [npad] pivot row of each column (0-based, absolute)
   int2* pairs = nullptr;     // [nblk][256] composed row moves of each block (dst, src)
   int* npairs = nullptr;     // [nblk]

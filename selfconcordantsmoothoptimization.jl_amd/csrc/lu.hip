@@ -365,44 +365,60 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_
 // The whole 128-column panel as ONE launch of G = h / 128 workgroups (one per CU and all resident: G <=
 // 128, h <= 16384), each holding its 128 rows in registers through the 128 column steps (4 passes x 32
 // rows x 8 lanes of 16 columns, the step kernels' layout).  The per-column grid-wide hand-off is the
-// candidate exchange itself, in MI355X_MICROARCH.md's publish / consume forms (§ visibility, Valid forms,
-// row 1): every workgroup publishes its candidate of the next column -- |a| and its row as three 8-byte
-// {tag, word} granules (tag = column + 1), one sc1 store each by one lane -- after write-through (sc1)
-// copies of the candidate's panel row and, by its owner, of row j + 1 (the row a pivot displaces),
-// drained by every storing wave (s_waitcnt vmcnt(0)) and a workgroup barrier.  Every wave sweeps all G
-// granule triples with relaxed sc1 loads (bounded spin) until every tag is the column's, takes the
-// pivot by the step kernels' rule (larger |a|, then the smaller row), and reads the pivot row (and, at
-// the pivot's old position, the displaced row) with sc1 loads.  Two granule / row slots by column
-// parity: a workgroup publishes column j + 2 only after every workgroup has published column j + 1,
-// i.e. after all have read column j.  The arithmetic per element is the step kernels' (l = x·(1/u_j),
-// or x / u_j below DBL_MIN; a_ic -= l·u_c), so the factor and the pivots are theirs bit for bit; the
-// rows go back to A once, after the last column.  A sweep past its bound (a workgroup that never became
-// resident) stores info = -1 and leaves the launch.
+// candidate exchange itself, as data-tagged 8-byte granules {tag, 32-bit word} (MI355X_MICROARCH.md
+// § visibility: R2, one sc1 store each, no flag and no ordering; tag = panel·256 + column + 1, unique in
+// the factorization, the granules zeroed once per factorization):
+//   * each workgroup publishes its candidate of the next column -- |a| and its row, three granules --
+//     and the candidate's whole panel row (two granules per double), and the owner of row j + 1 that
+//     row (the one a pivot displaces), straight after its argmax (no drain, no barrier);
+//   * every wave sweeps all G candidate triples (relaxed sc1 loads, bounded spin) until every tag is
+//     the column's, takes the pivot by the step kernels' rule (larger |a|, then the smaller row), then
+//     reads its 16 columns of the pivot row (and, at the pivot's old position, of the displaced row)
+//     as granules, re-reading until their tags are the column's.
+// Two slots by column parity: a workgroup publishes column j + 2 only after every workgroup has
+// published column j + 1, i.e. after all have read column j.  The arithmetic per element is the step
+// kernels' (l = x·(1/u_j), or x / u_j below DBL_MIN; a_ic -= l·u_c): the same factor and pivots bit for
+// bit; the rows go back to A once, after the last column.  A sweep past its bound (a workgroup that
+// never became resident) stores info = -1 and the abort word, and every later panel leaves at once.
 constexpr int LUC_RW = 128;                   // panel rows per workgroup
 constexpr int LUC_MAXWG = 128;                // workgroups (= CUs) at most
 constexpr int LUC_LDS = 96 * 1024;            // dynamic LDS that keeps a second workgroup off the CU
 constexpr unsigned LUC_SPIN_MAX = 1u << 19;   // sweeps before giving up (~0.5 s)
-constexpr int LUC_GRAN = 2 * LUC_MAXWG * 4;   // granule words per slot pair; word LUC_GRAN = the abort word
+// granule words (u64): candidates [2][MAXWG][4] | abort word (+pad) | candidate rows [2][MAXWG][128][2]
+// | row j + 1 [2][128][2]
+constexpr int64_t LUC_CAND = 0, LUC_ABORT = 2 * LUC_MAXWG * 4, LUC_CROW = LUC_ABORT + 16;
+constexpr int64_t LUC_ROWJ = LUC_CROW + 2 * LUC_MAXWG * LB * 2, LUC_WORDS = LUC_ROWJ + 2 * LB * 2;
 typedef __attribute__((address_space(1))) unsigned long long luc_gu64;
 
-__device__ __forceinline__ void luc_st(double* p, double v) {
-  __hip_atomic_store((luc_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void luc_put(unsigned long long* p, unsigned long long x) {
+  __hip_atomic_store((luc_gu64*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ double luc_ld(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_load((luc_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+__device__ __forceinline__ unsigned long long luc_get(const unsigned long long* p) {
+  return __hip_atomic_load((luc_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a double as two granules {tag, low word}, {tag, high word}
+__device__ __forceinline__ void luc_put_d(unsigned long long* p, unsigned tag, double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)tag << 32;
+  luc_put(p, t | (b & 0xffffffffull));
+  luc_put(p + 1, t | (b >> 32));
+}
+__device__ __forceinline__ double luc_get_d(const unsigned long long* p, unsigned tag, bool& ok) {
+  const unsigned long long x0 = luc_get(p), x1 = luc_get(p + 1);
+  ok = ok && (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag;
+  return __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
 }
 
 __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
-                                                              int64_t c0, unsigned long long* gran, double* crow,
-                                                              double* rowj, int* ipiv, int* info) {
+                                                              int64_t c0, unsigned long long* gran, unsigned tagbase,
+                                                              int* ipiv, int* info) {
   __shared__ double sv[LU_NT / 64];
   __shared__ int si[LU_NT / 64], sw[LU_NT / 64];
+  __shared__ double su_u[LB], su_rj[LB];   // the pivot row, the displaced row j (staged by wave 0)
+  __shared__ int s_p, s_alive;
   const int tid = threadIdx.x, g = blockIdx.x, nwg = gridDim.x, lane = tid & 63;
   const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
   const int base = g * LUC_RW + rr;   // this thread's panel position in pass ps: base + 32 ps
-  if (gran[LUC_GRAN] != 0) return;   // an earlier panel of this factorization gave up (info = -1)
+  if (gran[LUC_ABORT] != 0) return;   // an earlier panel of this factorization gave up (info = -1)
   double v[4][16];
 #pragma unroll
   for (int ps = 0; ps < 4; ++ps) {
@@ -410,7 +426,15 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
 #pragma unroll
     for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = *(const v2d*)(row + c);
   }
-  // this workgroup's candidate of column jn (rows >= jn) with its row, and row jn, then the granules
+  bool alive = true;
+  auto give_up = [&]() {   // a spin past its bound: this wave leaves, later panels leave at once
+    if (lane == 0) {
+      *info = -1;
+      gran[LUC_ABORT] = 1;
+    }
+    alive = false;
+  };
+  // this workgroup's candidate of column jn (rows >= jn) and its row, and row jn: granules
   auto publish = [&](int jn) {
     double bv = -1.0;
     int bi = INT_MAX;
@@ -428,40 +452,41 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
     int bw = g;
     lu_block_argmax(bv, bi, bw, sv, si, sw);
     const int par = jn & 1;
+    const unsigned tag = tagbase + (unsigned)(jn + 1);
+    if (tid == 0) {
+      const unsigned long long t = (unsigned long long)tag << 32;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
+      unsigned long long* gp = gran + LUC_CAND + ((int64_t)par * LUC_MAXWG + g) * 4;
+      luc_put(gp + 0, t | (bits & 0xffffffffull));
+      luc_put(gp + 1, t | (bits >> 32));
+      luc_put(gp + 2, t | (unsigned)bi);
+    }
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {
       const int i = base + 32 * ps;
       if (i == bi) {
+        unsigned long long* rp = gran + LUC_CROW + (((int64_t)par * LUC_MAXWG + g) * LB + cq) * 2;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) luc_st(crow + ((int64_t)par * LUC_MAXWG + g) * LB + cq + c, v[ps][c]);
+        for (int c = 0; c < 16; ++c) luc_put_d(rp + 2 * c, tag, v[ps][c]);
       }
       if (i == jn) {
+        unsigned long long* rp = gran + LUC_ROWJ + ((int64_t)par * LB + cq) * 2;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) luc_st(rowj + par * LB + cq + c, v[ps][c]);
+        for (int c = 0; c < 16; ++c) luc_put_d(rp + 2 * c, tag, v[ps][c]);
       }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned long long tag = (unsigned long long)(jn + 1) << 32;
-      const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
-      luc_gu64* gp = (luc_gu64*)(gran + ((int64_t)par * LUC_MAXWG + g) * 4);
-      __hip_atomic_store(gp + 0, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gp + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gp + 2, tag | (unsigned)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
   publish(0);
   for (int j = 0; j < LB; ++j) {
     const int par = j & 1;
-    const unsigned tag = (unsigned)(j + 1);
-    // 1. every wave: sweep the G candidates of column j until all carry this column's tag
-    double cv;
-    int ci, cw;
-    {
-      const luc_gu64* gp = (const luc_gu64*)(gran + (int64_t)par * LUC_MAXWG * 4);
-      unsigned spins = 0;
-      for (;;) {
+    const unsigned tag = tagbase + (unsigned)(j + 1);
+    // 1. wave 0 alone: sweep the G candidates of column j until all carry this column's tag, pick the
+    //    pivot, and stage the pivot row (and the displaced row j where this workgroup holds row p) in LDS
+    if (tid < 64) {
+      double cv = -1.0;
+      int ci = INT_MAX, cw = -1;
+      const unsigned long long* gp = gran + LUC_CAND + (int64_t)par * LUC_MAXWG * 4;
+      for (unsigned spins = 0;;) {
         bool ok = true;
         cv = -1.0;
         ci = INT_MAX;
@@ -470,9 +495,8 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
         for (int t = 0; t < LUC_MAXWG / 64; ++t) {
           const int w = lane + 64 * t;
           if (w < nwg) {
-            const unsigned long long x0 = __hip_atomic_load(gp + 4 * w + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long x1 = __hip_atomic_load(gp + 4 * w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long x2 = __hip_atomic_load(gp + 4 * w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long x0 = luc_get(gp + 4 * w + 0), x1 = luc_get(gp + 4 * w + 1),
+                                     x2 = luc_get(gp + 4 * w + 2);
             ok = ok && (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag && (unsigned)(x2 >> 32) == tag;
             double a = __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
             int r = (int)(unsigned)x2;
@@ -488,12 +512,9 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
           }
         }
         if (__all(ok)) break;
-        if (++spins > LUC_SPIN_MAX) {   // the later panels of this factorization leave at once
-          if (lane == 0) {
-            *info = -1;
-            gran[LUC_GRAN] = 1;
-          }
-          return;
+        if (++spins > LUC_SPIN_MAX) {
+          give_up();
+          break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
@@ -508,30 +529,54 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
           cw = w2;
         }
       }
+      // a row of 128 doubles as 256 granules: lane l takes columns 2l, 2l + 1
+      auto stage = [&](const unsigned long long* rp, double* dst) {
+        for (unsigned spins = 0; alive;) {
+          bool ok = true;
+          const double d0 = luc_get_d(rp + 4 * lane, tag, ok), d1 = luc_get_d(rp + 4 * lane + 2, tag, ok);
+          if (__all(ok)) {
+            dst[2 * lane] = d0;
+            dst[2 * lane + 1] = d1;
+            return;
+          }
+          if (++spins > LUC_SPIN_MAX) give_up();
+          __builtin_amdgcn_s_sleep(1);
+        }
+      };
+      const unsigned long long* rowj_g = gran + LUC_ROWJ + (int64_t)par * LB * 2;
+      int p = ci;
+      const unsigned long long* urow = gran + LUC_CROW + ((int64_t)par * LUC_MAXWG + cw) * LB * 2;
+      if (cv < 0.0) {   // no valid candidate anywhere (NaN column): keep row j
+        p = j;
+        urow = rowj_g;
+      }
+      if (alive) stage(urow, su_u);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // this wave's LDS writes, then its reads
+      __builtin_amdgcn_wave_barrier();
+      if (alive && su_u[j] == 0.0) {   // getf2: zero pivot -> no interchange, no scaling (row j's u_j
+        p = j;                           // is then zero too: the column's largest |a| was)
+        stage(rowj_g, su_u);
+      }
+      if (alive && p != j && p >= g * LUC_RW && p < g * LUC_RW + LUC_RW) stage(rowj_g, su_rj);
+      if (lane == 0) {
+        s_p = p;
+        s_alive = alive ? 1 : 0;
+      }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: the row loads stay below
-    // 2. the pivot row u (sc1 loads), as the step kernels choose it
-    int p = j;
-    const double* urow = (cv < 0.0) ? rowj + par * LB : crow + ((int64_t)par * LUC_MAXWG + cw) * LB;
-    if (cv >= 0.0) p = ci;
+    __syncthreads();
+    if (!s_alive) return;   // (every wave: the abort word and info are set)
+    const int p = s_p;
     double u[16];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) u[c] = luc_ld(urow + cq + c);
-    double piv = luc_ld(urow + j);
+    for (int c = 0; c < 16; ++c) u[c] = su_u[cq + c];
+    const double piv = su_u[j];
     const bool scale = (piv != 0.0);
-    if (!scale) {   // getf2: zero pivot -> no interchange, no scaling (the column below is zero)
-      p = j;
-      urow = rowj + par * LB;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) u[c] = luc_ld(urow + cq + c);
-      piv = luc_ld(urow + j);
-    }
     const double rp = 1.0 / piv;
     if (g == 0 && tid == 0) {
       ipiv[r0 + j] = (int)(r0 + p);
       if (!scale && *info == 0) *info = (int)(r0 + j + 1);
     }
-    // 3. row j <- u, row p <- the displaced row j, every row i > j: l = a_ij / u_j, a_ic -= l·u_c
+    // 2. row j <- u, row p <- the displaced row j, every row i > j: l = a_ij / u_j, a_ic -= l·u_c
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {
       const int i = base + 32 * ps;
@@ -545,7 +590,7 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
       }
       if (i == p) {   // (p != j here)
 #pragma unroll
-        for (int c = 0; c < 16; ++c) v[ps][c] = luc_ld(rowj + par * LB + cq + c);
+        for (int c = 0; c < 16; ++c) v[ps][c] = su_rj[cq + c];
       }
       const double x = __shfl(sel(v[ps], j & 15), (tid & ~7) | (j >> 4), 64);
       const double l = scale ? (fabs(piv) >= 2.2250738585072014e-308 ? x * rp : x / piv) : x;
@@ -838,7 +883,7 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
   al((void**)&a->candi, sizeof(int) * 2 * LU_MAXWG);
   al((void**)&a->candrow, sizeof(double) * 2 * LU_MAXWG * LB);
   al((void**)&a->rowj, sizeof(double) * 2 * LB);
-  al((void**)&a->gran, sizeof(unsigned long long) * (LUC_GRAN + 2));
+  al((void**)&a->gran, sizeof(unsigned long long) * LUC_WORDS);
   al((void**)&a->ipiv, sizeof(int) * npad);
   al((void**)&a->pairs, sizeof(int2) * (size_t)nblk * LU_MAXPAIRS);
   al((void**)&a->npairs, sizeof(int) * nblk);
@@ -890,8 +935,8 @@ static int lu_inv_mode() {
 hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st) {
   if (npad % LB != 0 || npad > a->npad || ld < npad) return hipErrorInvalidValue;
   const int nblk = (int)(npad / LB);
-  if (lu_panel_mode() == 3) {   // the cooperative panels' abort word, once per factorization
-    const hipError_t e = hipMemsetAsync(a->gran + LUC_GRAN, 0, sizeof(unsigned long long) * 2, st);
+  if (lu_panel_mode() == 3) {   // the cooperative panels' granules and abort word, once per factorization
+    const hipError_t e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * LUC_WORDS, st);
     if (e != hipSuccess) return e;
   }
   if (npad > n)
@@ -903,11 +948,10 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
     const int npass = R / 32, mode = lu_panel_mode();
     const int64_t gco = h / LUC_RW;
     if (mode == 3 && gco <= LUC_MAXWG) {
-      hipError_t e = lu_coop_attr();
-      if (e == hipSuccess) e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * LUC_GRAN, st);
+      const hipError_t e = lu_coop_attr();
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(lu_panel_coop_kernel, dim3((unsigned)gco), dim3(LU_NT), LUC_LDS, st, A, ld, r0, c0, a->gran,
-                         a->candrow, a->rowj, a->ipiv, info);
+                         (unsigned)k << 8, a->ipiv, info);
     } else
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)

@@ -121,7 +121,6 @@ __global__ __launch_bounds__(256) void qr_col_update(double* __restrict__ A, int
 // workgroup reads what another one of the same launch writes; the next launch takes its x from xs
 // and writes column c's R entries.  Every workgroup reduces the previous column's partials itself,
 // in chunk order: the same beta, tau and w_j everywhere.  Launch c1 only finishes column c1-1.
-template <bool PF>
 __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64_t ld, int64_t npad, int64_t c,
                                                    int64_t c0, int64_t c1, double* __restrict__ b,
                                                    double* __restrict__ part, int64_t pslot, int nrc, int nrc_prev,
@@ -140,19 +139,17 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
   const int64_t j = c + jj;
   double* colj = (jj >= 0 && j < c1) ? A + j * ld : b;
   const double* colc = (c < c1) ? A + c * ld : b;
-  // PF: this thread's (at most QR_RC/256) rows of colj, colc and x are loaded before thread 0's
-  // serial reduction of the previous column's partials, so their latency hides under it.
+  // this thread's (at most QR_RC/256) rows of colj, colc and x are loaded before thread 0's serial
+  // reduction of the previous column's partials (r05; the same arithmetic, 98 vs 100 ms at n = 8192)
   constexpr int NPF = QR_RC / 256;
   double paj[NPF], pac[NPF], px[NPF];
-  if (PF) {
 #pragma unroll
-    for (int k = 0; k < NPF; ++k) {
-      const int64_t r = r0 + tid + 256 * k;
-      const bool in = r < r1;
-      paj[k] = (in && jj >= 0) ? colj[r] : 0.0;
-      pac[k] = (in && jj >= 0) ? colc[r] : 0.0;
-      px[k] = (in && has_prev) ? x[r] : 0.0;
-    }
+  for (int k = 0; k < NPF; ++k) {
+    const int64_t r = r0 + tid + 256 * k;
+    const bool in = r < r1;
+    paj[k] = (in && jj >= 0) ? colj[r] : 0.0;
+    pac[k] = (in && jj >= 0) ? colc[r] : 0.0;
+    px[k] = (in && has_prev) ? x[r] : 0.0;
   }
   if (tid == 0) {
     double t = 0.0, sc = 0.0, beta = 0.0, twj = 0.0, twc = 0.0;
@@ -187,15 +184,10 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
   if (jj < 0) {   // column pv: V, its R entries, tau
     if (!has_prev) return;
     const int64_t vc = (pv - c0) * ldv;
-    if (PF) {
 #pragma unroll
-      for (int k = 0; k < NPF; ++k) {
-        const int64_t r = r0 + tid + 256 * k;
-        if (r < r1 && r > pv) V[vc + (r - c0)] = px[k] * sc;
-      }
-    } else {
-      for (int64_t r = r0 + tid; r < r1; r += 256)
-        if (r > pv) V[vc + (r - c0)] = x[r] * sc;
+    for (int k = 0; k < NPF; ++k) {
+      const int64_t r = r0 + tid + 256 * k;
+      if (r < r1 && r > pv) V[vc + (r - c0)] = px[k] * sc;
     }
     if (rc == 0) {
       for (int64_t r = c0 + tid; r <= pv; r += 256) V[vc + (r - c0)] = (r == pv) ? 1.0 : 0.0;
@@ -221,25 +213,16 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
     if (r == c) rowc[(c & 1) * (QB + 2) + jj] = aj;
     if (r > c) s += ac * aj;
   };
-  if (PF) {
 #pragma unroll
-    for (int k = 0; k < NPF; ++k) {
-      const int64_t r = r0 + tid + 256 * k;
-      if (r < r1) row(r, paj[k], pac[k], px[k]);
-    }
-  } else {
-    for (int64_t r = r0 + tid; r < r1; r += 256) row(r, colj[r], colc[r], has_prev ? x[r] : 0.0);
+  for (int k = 0; k < NPF; ++k) {
+    const int64_t r = r0 + tid + 256 * k;
+    if (r < r1) row(r, paj[k], pac[k], px[k]);
   }
   if (c >= c1) return;
   s = wave_sum(s);
   if ((tid & 63) == 0) ws[tid >> 6] = s;
   __syncthreads();
   if (tid == 0) part[(c & 1) * pslot + (int64_t)jj * nrc + rc] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
-}
-
-static bool qr_step_prefetch() {   // read per call (A/B); SCS_QR_PF=0 is the r04 column step
-  const char* e = getenv("SCS_QR_PF");
-  return !(e && e[0] == '0');
 }
 
 static bool qr_step_fused() {   // read per call (A/B)
@@ -453,12 +436,11 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
     if (qr_step_fused()) {
       const int64_t pslot = (int64_t)(QB + 1) * ((npad + QR_RC - 1) / QR_RC + 1);
       int nrc_prev = 0;
-      const auto step = qr_step_prefetch() ? qr_col_step<true> : qr_col_step<false>;
       for (int64_t c = c0; c <= c1; ++c) {
         const int64_t rbeg = c > c0 ? c - 1 : c;
         const int nrc_c = (int)((npad - rbeg + QR_RC - 1) / QR_RC);
         const int ncol = (int)(c1 - c) + 1;   // columns c .. c1-1 and b
-        hipLaunchKernelGGL(step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad, c,
+        hipLaunchKernelGGL(qr_col_step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad, c,
                            c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, a->V, npad);
         nrc_prev = nrc_c;
       }

@@ -610,10 +610,12 @@ void allreduce(scs_ctx* c, double* buf, int64_t count) {
   if (c->rccl) {   // in place, on the context stream (one fp64 sum per exchange)
     const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->rccl, c->st);
     if (r != ncclSuccess) fail(c, SCS_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-    // RCCL's work joins c->st as a stream wait, and an event recorded right after a wait takes the
-    // timestamp of the stream's last dispatch -- before the collective -- so the all-reduce used
-    // to land in the NEXT timer (solve: +7 ms at C3's per-rank shape, profiles/r04/commcmp/).  An
-    // empty dispatch after the wait gives the end event a timestamp behind the collective.
+    // RCCL launches its kernel on c->st, so the events around it time it.  At world 1 the in-place
+    // all-reduce launches nothing (0.02 ms, profiles/r05/rccltrace/: no RCCL kernel on any queue);
+    // the +7 ms the r04 verdict saw in `solve` with RCCL forced was the factor's two streams sharing
+    // one hardware queue once torch and RCCL had created theirs (chol.hip, create_chain_stream).
+    // The empty dispatch keeps the end event behind the collective should RCCL ever join c->st by a
+    // stream wait instead (an event recorded right after a wait takes the last dispatch's time).
     if (c->timing) HCK(launch_marker(c->st));
   } else {
     if (!c->ar) fail(c, SCS_ERR_COMM, "multi-rank context without a communicator");

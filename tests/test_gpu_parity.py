@@ -980,22 +980,6 @@ def test_householder_qr_solve(m):
     assert np.linalg.norm(M @ x - rhs) <= 1e-12 * np.linalg.norm(M, 2) * np.linalg.norm(x)
 
 
-@pytest.mark.parametrize("m", [300, 2304])
-def test_householder_qr_prefetch_bit_identical(m, monkeypatch):
-    """The column step with its rows of a_j, a_c and the previous column loaded before thread 0's
-    reduction (qr_col_step<true>, r05) does the r04 step's arithmetic (SCS_QR_PF=0): bit for bit."""
-    N = m + 77
-    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=41)
-    rng = np.random.default_rng(43)
-    w = (rng.random(N) + 0.5) / N
-    d = (rng.random(m) + 0.5) * 1e-3
-    rhs = rng.standard_normal(m)
-    x1, _ = p.solve_eval(w, d, rhs, mode=2)
-    monkeypatch.setenv("SCS_QR_PF", "0")
-    x0, _ = p.solve_eval(w, d, rhs, mode=2)
-    assert np.array_equal(x1.view(np.uint64), x0.view(np.uint64))
-
-
 @pytest.mark.parametrize("case", ["ggn_feature", "ggn_sample", "nscore"])
 def test_reference_solver_trajectory(case, monkeypatch):
     """scs_set_solver(SCS_SOLVER_REFERENCE): ProxGGNSCORE's qr(JQJ) \\ Je (feature branch) and
