@@ -408,13 +408,22 @@ __device__ __forceinline__ double luc_get_d(const unsigned long long* p, unsigne
   return __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
 }
 
+// WIDE (default; SCS_LU_COOP_WIDE=0 the first v3 form): the candidate row and row j + 1 go through LDS and
+// are stored by a whole wave each (4 granules per lane instead of 32 per holding lane), before the
+// candidate's own granules
+template <bool WIDE>
 __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
                                                               int64_t c0, unsigned long long* gran, unsigned tagbase,
-                                                              int* ipiv, int* info) {
+                                                              int* ipiv, int* info, int2* pairs, int* npairs) {
   __shared__ double sv[LU_NT / 64];
   __shared__ int si[LU_NT / 64], sw[LU_NT / 64];
   __shared__ double su_u[LB], su_rj[LB];   // the pivot row, the displaced row j (staged by wave 0)
+  __shared__ double su_c[LB], su_n[LB];    // WIDE: this workgroup's candidate row and row j + 1 to publish
   __shared__ int s_p, s_alive;
+  // workgroup 0: the block's interchanges composed into row moves as the pivots come (lu_perm_kernel's
+  // bookkeeping, one swap per column behind the column's publication): rows r0 .. r0+127, and the
+  // touched rows below the block as (row, content)
+  __shared__ int ptop[LB], pbrow[LB], pbval[LB], pnb;
   const int tid = threadIdx.x, g = blockIdx.x, nwg = gridDim.x, lane = tid & 63;
   const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
   const int base = g * LUC_RW + rr;   // this thread's panel position in pass ps: base + 32 ps
@@ -453,6 +462,34 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
     lu_block_argmax(bv, bi, bw, sv, si, sw);
     const int par = jn & 1;
     const unsigned tag = tagbase + (unsigned)(jn + 1);
+    if (WIDE) {
+      const bool hold_jn = jn >= g * LUC_RW && jn < g * LUC_RW + LUC_RW;
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const int i = base + 32 * ps;
+        if (i == bi) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c) su_c[cq + c] = v[ps][c];
+        }
+        if (i == jn) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c) su_n[cq + c] = v[ps][c];
+        }
+      }
+      __syncthreads();
+      const int wv = tid >> 6;
+      if (wv == 1 && bi != INT_MAX) {
+        unsigned long long* rp = gran + LUC_CROW + ((int64_t)par * LUC_MAXWG + g) * LB * 2;
+        luc_put_d(rp + 4 * lane, tag, su_c[2 * lane]);
+        luc_put_d(rp + 4 * lane + 2, tag, su_c[2 * lane + 1]);
+      }
+      if (wv == 2 && hold_jn) {
+        unsigned long long* rp = gran + LUC_ROWJ + (int64_t)par * LB * 2;
+        luc_put_d(rp + 4 * lane, tag, su_n[2 * lane]);
+        luc_put_d(rp + 4 * lane + 2, tag, su_n[2 * lane + 1]);
+      }
+      __syncthreads();   // the rows' granules issued ahead of the candidate's (the tags decide anyway)
+    }
     if (tid == 0) {
       const unsigned long long t = (unsigned long long)tag << 32;
       const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
@@ -462,7 +499,7 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
       luc_put(gp + 2, t | (unsigned)bi);
     }
 #pragma unroll
-    for (int ps = 0; ps < 4; ++ps) {
+    for (int ps = 0; ps < 4 && !WIDE; ++ps) {
       const int i = base + 32 * ps;
       if (i == bi) {
         unsigned long long* rp = gran + LUC_CROW + (((int64_t)par * LUC_MAXWG + g) * LB + cq) * 2;
@@ -476,7 +513,11 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
       }
     }
   };
-  publish(0);
+  if (g == 0) {
+    if (tid < LB) ptop[tid] = (int)r0 + tid;
+    if (tid == 0) pnb = 0;
+  }
+  publish(0);   // (its barriers order the initialisation above)
   for (int j = 0; j < LB; ++j) {
     const int par = j & 1;
     const unsigned tag = tagbase + (unsigned)(j + 1);
@@ -602,6 +643,54 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
       }
     }
     if (j + 1 < LB) publish(j + 1);
+    if (g == 0 && tid < 64 && p != j) {   // compose interchange j (rows r0+j <-> r0+p)
+      if (p < LB) {
+        if (lane == 0) {
+          const int t = ptop[j];
+          ptop[j] = ptop[p];
+          ptop[p] = t;
+        }
+      } else {
+        const int pr = (int)r0 + p;
+        int slot = -1;
+        for (int b = lane; b < pnb; b += 64)
+          if (pbrow[b] == pr) slot = b;
+        const unsigned long long hit = __ballot(slot >= 0);   // rows are unique in the list
+        const int found = hit ? __shfl(slot, __ffsll((long long)hit) - 1, 64) : -1;
+        if (lane == 0) {
+          int sl = found;
+          if (sl < 0) {
+            sl = pnb;
+            pbrow[sl] = pr;
+            pbval[sl] = pr;
+            pnb = sl + 1;
+          }
+          const int t = ptop[j];
+          ptop[j] = pbval[sl];
+          pbval[sl] = t;
+        }
+      }
+    }
+  }
+  if (g == 0 && tid < 64) {   // the moves: top rows (ascending), then the rows below (list order)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int n = 0;
+    for (int t0 = 0; t0 < LB; t0 += 64) {
+      const int t = t0 + lane;
+      const bool mv = ptop[t] != (int)r0 + t;
+      const unsigned long long bm = __ballot(mv);
+      if (mv) pairs[n + __popcll(bm & ((1ull << lane) - 1))] = make_int2((int)r0 + t, ptop[t]);
+      n += __popcll(bm);
+    }
+    for (int b0 = 0; b0 < pnb; b0 += 64) {
+      const int b = b0 + lane;
+      const bool mv = b < pnb && pbval[b] != pbrow[b];
+      const unsigned long long bm = __ballot(mv);
+      if (mv) pairs[n + __popcll(bm & ((1ull << lane) - 1))] = make_int2(pbrow[b], pbval[b]);
+      n += __popcll(bm);
+    }
+    if (lane == 0) *npairs = n;
   }
 #pragma unroll
   for (int ps = 0; ps < 4; ++ps) {
@@ -920,9 +1009,20 @@ static int lu_panel_mode() {
 }
 
 static hipError_t lu_coop_attr() {   // the dynamic LDS above the 64 KiB default, once per process
-  static hipError_t done = hipFuncSetAttribute((const void*)lu_panel_coop_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, LUC_LDS);
+  static hipError_t done = [] {
+    hipError_t e = hipFuncSetAttribute((const void*)lu_panel_coop_kernel<true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LUC_LDS);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)lu_panel_coop_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LUC_LDS);
+    return e;
+  }();
   return done;
+}
+
+static bool lu_coop_wide() {   // read per call (A/B)
+  const char* e = getenv("SCS_LU_COOP_WIDE");
+  return !(e && e[0] == '0');
 }
 
 // SCS_LU_INV (read per call): unset / 2 = the diagonal block's inverses by 16 x 16 inverses + MFMA doubling
@@ -947,11 +1047,16 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
     const int nwg = (int)ceil_div(h, R);
     const int npass = R / 32, mode = lu_panel_mode();
     const int64_t gco = h / LUC_RW;
-    if (mode == 3 && gco <= LUC_MAXWG) {
+    const bool coop = mode == 3 && gco <= LUC_MAXWG;
+    if (coop) {
       const hipError_t e = lu_coop_attr();
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(lu_panel_coop_kernel, dim3((unsigned)gco), dim3(LU_NT), LUC_LDS, st, A, ld, r0, c0, a->gran,
-                         (unsigned)k << 8, a->ipiv, info);
+      if (lu_coop_wide())
+        hipLaunchKernelGGL(lu_panel_coop_kernel<true>, dim3((unsigned)gco), dim3(LU_NT), LUC_LDS, st, A, ld, r0, c0,
+                           a->gran, (unsigned)k << 8, a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
+      else
+        hipLaunchKernelGGL(lu_panel_coop_kernel<false>, dim3((unsigned)gco), dim3(LU_NT), LUC_LDS, st, A, ld, r0, c0,
+                           a->gran, (unsigned)k << 8, a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
     } else
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)
@@ -965,7 +1070,8 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
                            a->candi, a->candrow, a->rowj, a->ipiv, info);
     }
     int2* pairs = a->pairs + (int64_t)k * LU_MAXPAIRS;
-    hipLaunchKernelGGL(lu_perm_kernel, dim3(1), dim3(64), 0, st, a->ipiv, (int)r0, pairs, a->npairs + k);
+    if (!coop)   // (the cooperative panel composes its interchanges itself)
+      hipLaunchKernelGGL(lu_perm_kernel, dim3(1), dim3(64), 0, st, a->ipiv, (int)r0, pairs, a->npairs + k);
     if (lu_inv_mode() == 1)
       hipLaunchKernelGGL(lu_diag_inv_kernel, dim3(2), dim3(256), 0, st, A, ld, r0, a->Linv + (int64_t)k * LB * LB,
                          a->Uinv + (int64_t)k * LB * LB);

@@ -156,3 +156,18 @@ def test_lu_doubling_inverse_matches_elimination(n, monkeypatch):
     kappa = float(np.linalg.cond(A, np.inf))
     assert np.max(np.abs(x1 - x2)) <= 1e-14 * kappa * float(np.abs(x1).max())
     assert _bwd(A, x2, b) <= 1e-13
+
+
+def test_lu_coop_publish_forms_bit_identical(monkeypatch):
+    """The cooperative panel's two publication forms (rows stored by a whole wave through LDS, the
+    default, vs by the eight lanes that hold them, SCS_LU_COOP_WIDE=0): the same factor bit for bit."""
+    n = 2176
+    rng = np.random.default_rng(n + 13)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    x2, ipiv2, info2 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_COOP_WIDE", "0")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info1 == info2 == 0
+    assert np.array_equal(ipiv1, ipiv2)
+    assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
