@@ -45,7 +45,8 @@ __device__ __forceinline__ bool lu_better(double v1, int i1, double v2, int i2) 
 }
 
 // (v, i) argmax over the workgroup (larger |a|, then smaller row); every thread gets the result.
-// sv / si hold LU_NT / 64 entries.
+// sv / si hold NT / 64 entries.
+template <int NT = LU_NT>
 __device__ __forceinline__ void lu_block_argmax(double& v, int& i, int& w, double* sv, int* si, int* sw) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -70,7 +71,7 @@ __device__ __forceinline__ void lu_block_argmax(double& v, int& i, int& w, doubl
   i = si[0];
   w = sw[0];
 #pragma unroll
-  for (int k = 1; k < LU_NT / 64; ++k)
+  for (int k = 1; k < NT / 64; ++k)
     if (lu_better(sv[k], si[k], v, i)) {
       v = sv[k];
       i = si[k];
@@ -380,7 +381,6 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_
 // kernels' (l = x·(1/u_j), or x / u_j below DBL_MIN; a_ic -= l·u_c): the same factor and pivots bit for
 // bit; the rows go back to A once, after the last column.  A sweep past its bound (a workgroup that
 // never became resident) stores info = -1 and the abort word, and every later panel leaves at once.
-constexpr int LUC_RW = 128;                   // panel rows per workgroup
 constexpr int LUC_MAXWG = 128;                // workgroups (= CUs) at most
 constexpr int LUC_LDS = 96 * 1024;            // dynamic LDS that keeps a second workgroup off the CU
 constexpr unsigned LUC_SPIN_MAX = 1u << 19;   // sweeps before giving up (~0.5 s)
@@ -408,15 +408,19 @@ __device__ __forceinline__ double luc_get_d(const unsigned long long* p, unsigne
   return __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
 }
 
-// WIDE (default; SCS_LU_COOP_WIDE=0 the first v3 form): the candidate row and row j + 1 go through LDS and
-// are stored by a whole wave each (4 granules per lane instead of 32 per holding lane), before the
-// candidate's own granules
-template <bool WIDE>
-__global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
-                                                              int64_t c0, unsigned long long* gran, unsigned tagbase,
+// WIDE (SCS_LU_COOP_WIDE=1; measured slower at NT = 256, 84.9 vs 83.2 ms at n = 8192): the candidate row
+// and row j + 1 go through LDS and are stored by a whole wave each (4 granules per lane instead of 32 per
+// holding lane), before the candidate's own granules
+// NT: threads per workgroup -- 256 (128 rows, up to 128 workgroups) or 512 (256 rows, up to 64 workgroups:
+// half the grid to sweep and to wait for, two waves per SIMD)
+template <bool WIDE, int NT>
+__global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
+                                                              int64_t c0, int64_t h, unsigned long long* gran,
+                                                              unsigned tagbase,
                                                               int* ipiv, int* info, int2* pairs, int* npairs) {
-  __shared__ double sv[LU_NT / 64];
-  __shared__ int si[LU_NT / 64], sw[LU_NT / 64];
+  constexpr int RW = NT / 2, RP = NT / 8;   // rows per workgroup, rows per pass
+  __shared__ double sv[NT / 64];
+  __shared__ int si[NT / 64], sw[NT / 64];
   __shared__ double su_u[LB], su_rj[LB];   // the pivot row, the displaced row j (staged by wave 0)
   __shared__ double su_c[LB], su_n[LB];    // WIDE: this workgroup's candidate row and row j + 1 to publish
   __shared__ int s_p, s_alive;
@@ -426,14 +430,15 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
   __shared__ int ptop[LB], pbrow[LB], pbval[LB], pnb;
   const int tid = threadIdx.x, g = blockIdx.x, nwg = gridDim.x, lane = tid & 63;
   const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
-  const int base = g * LUC_RW + rr;   // this thread's panel position in pass ps: base + 32 ps
+  const int base = g * RW + rr;   // this thread's panel position in pass ps: base + RP ps
   if (gran[LUC_ABORT] != 0) return;   // an earlier panel of this factorization gave up (info = -1)
   double v[4][16];
 #pragma unroll
   for (int ps = 0; ps < 4; ++ps) {
-    const double* row = A + (r0 + base + 32 * ps) * ld + c0 + cq;
+    const bool in = base + RP * ps < h;   // (NT = 512: the last workgroup may hold only 128 rows)
+    const double* row = A + (r0 + (in ? base + RP * ps : 0)) * ld + c0 + cq;
 #pragma unroll
-    for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = *(const v2d*)(row + c);
+    for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = in ? *(const v2d*)(row + c) : (v2d){0.0, 0.0};
   }
   bool alive = true;
   auto give_up = [&]() {   // a spin past its bound: this wave leaves, later panels leave at once
@@ -449,8 +454,8 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
     int bi = INT_MAX;
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {
-      const int i = base + 32 * ps;
-      if (i >= jn && q == (jn >> 4)) {
+      const int i = base + RP * ps;
+      if (i >= jn && i < h && q == (jn >> 4)) {
         const double a = fabs(sel(v[ps], jn & 15));
         if (lu_better(a, i, bv, bi)) {
           bv = a;
@@ -459,14 +464,14 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
       }
     }
     int bw = g;
-    lu_block_argmax(bv, bi, bw, sv, si, sw);
+    lu_block_argmax<NT>(bv, bi, bw, sv, si, sw);
     const int par = jn & 1;
     const unsigned tag = tagbase + (unsigned)(jn + 1);
     if (WIDE) {
-      const bool hold_jn = jn >= g * LUC_RW && jn < g * LUC_RW + LUC_RW;
+      const bool hold_jn = jn >= g * RW && jn < g * RW + RW;
 #pragma unroll
       for (int ps = 0; ps < 4; ++ps) {
-        const int i = base + 32 * ps;
+        const int i = base + RP * ps;
         if (i == bi) {
 #pragma unroll
           for (int c = 0; c < 16; ++c) su_c[cq + c] = v[ps][c];
@@ -500,7 +505,7 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
     }
 #pragma unroll
     for (int ps = 0; ps < 4 && !WIDE; ++ps) {
-      const int i = base + 32 * ps;
+      const int i = base + RP * ps;
       if (i == bi) {
         unsigned long long* rp = gran + LUC_CROW + (((int64_t)par * LUC_MAXWG + g) * LB + cq) * 2;
 #pragma unroll
@@ -598,7 +603,7 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
         p = j;                           // is then zero too: the column's largest |a| was)
         stage(rowj_g, su_u);
       }
-      if (alive && p != j && p >= g * LUC_RW && p < g * LUC_RW + LUC_RW) stage(rowj_g, su_rj);
+      if (alive && p != j && p >= g * RW && p < g * RW + RW) stage(rowj_g, su_rj);
       if (lane == 0) {
         s_p = p;
         s_alive = alive ? 1 : 0;
@@ -620,8 +625,8 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
     // 2. row j <- u, row p <- the displaced row j, every row i > j: l = a_ij / u_j, a_ic -= l·u_c
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {
-      const int i = base + 32 * ps;
-      if (i < j) continue;
+      const int i = base + RP * ps;
+      if (i < j || i >= h) continue;
       if (i == j) {
         if (p != j) {
 #pragma unroll
@@ -694,7 +699,8 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_coop_kernel(double* __restrict
   }
 #pragma unroll
   for (int ps = 0; ps < 4; ++ps) {
-    double* row = A + (r0 + base + 32 * ps) * ld + c0 + cq;
+    if (base + RP * ps >= h) continue;
+    double* row = A + (r0 + base + RP * ps) * ld + c0 + cq;
 #pragma unroll
     for (int c = 0; c < 16; c += 2) *(v2d*)(row + c) = *(const v2d*)(v[ps] + c);
   }
@@ -1010,19 +1016,24 @@ static int lu_panel_mode() {
 
 static hipError_t lu_coop_attr() {   // the dynamic LDS above the 64 KiB default, once per process
   static hipError_t done = [] {
-    hipError_t e = hipFuncSetAttribute((const void*)lu_panel_coop_kernel<true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LUC_LDS);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)lu_panel_coop_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LUC_LDS);
+    const void* ks[] = {(const void*)lu_panel_coop_kernel<true, 256>, (const void*)lu_panel_coop_kernel<false, 256>,
+                        (const void*)lu_panel_coop_kernel<true, 512>, (const void*)lu_panel_coop_kernel<false, 512>};
+    hipError_t e = hipSuccess;
+    for (const void* f : ks)
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LUC_LDS);
     return e;
   }();
   return done;
 }
 
-static bool lu_coop_wide() {   // read per call (A/B)
+static int lu_coop_nt() {   // read per call (A/B): SCS_LU_COOP_NT = 256 | 512
+  const char* e = getenv("SCS_LU_COOP_NT");
+  return (e && atoi(e) == 512) ? 512 : 256;
+}
+
+static bool lu_coop_wide() {   // read per call (A/B): SCS_LU_COOP_WIDE=1 (n = 8192: 84.9 vs 83.2 ms narrow)
   const char* e = getenv("SCS_LU_COOP_WIDE");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 // SCS_LU_INV (read per call): unset / 2 = the diagonal block's inverses by 16 x 16 inverses + MFMA doubling
@@ -1046,17 +1057,17 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
     const int R = 32 * (int)ceil_div(h, 32 * LU_MAXWG);
     const int nwg = (int)ceil_div(h, R);
     const int npass = R / 32, mode = lu_panel_mode();
-    const int64_t gco = h / LUC_RW;
-    const bool coop = mode == 3 && gco <= LUC_MAXWG;
+    const int cnt = lu_coop_nt();
+    const int64_t gco = ceil_div(h, (int64_t)(cnt / 2));
+    const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG);
     if (coop) {
       const hipError_t e = lu_coop_attr();
       if (e != hipSuccess) return e;
-      if (lu_coop_wide())
-        hipLaunchKernelGGL(lu_panel_coop_kernel<true>, dim3((unsigned)gco), dim3(LU_NT), LUC_LDS, st, A, ld, r0, c0,
-                           a->gran, (unsigned)k << 8, a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
-      else
-        hipLaunchKernelGGL(lu_panel_coop_kernel<false>, dim3((unsigned)gco), dim3(LU_NT), LUC_LDS, st, A, ld, r0, c0,
-                           a->gran, (unsigned)k << 8, a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
+      const bool wide = lu_coop_wide();
+      auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
+                             : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)gco), dim3(cnt), LUC_LDS, st, A, ld, r0, c0, h, a->gran, (unsigned)k << 8,
+                         a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
     } else
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)

@@ -159,14 +159,30 @@ def test_lu_doubling_inverse_matches_elimination(n, monkeypatch):
 
 
 def test_lu_coop_publish_forms_bit_identical(monkeypatch):
-    """The cooperative panel's two publication forms (rows stored by a whole wave through LDS, the
-    default, vs by the eight lanes that hold them, SCS_LU_COOP_WIDE=0): the same factor bit for bit."""
+    """The cooperative panel's two publication forms (rows stored by the eight lanes that hold them, the
+    default, vs by a whole wave through LDS, SCS_LU_COOP_WIDE=1): the same factor bit for bit."""
     n = 2176
     rng = np.random.default_rng(n + 13)
     A = rng.standard_normal((n, n))
     b = rng.standard_normal(n)
     x2, ipiv2, info2 = scsopt.lu_solve(A, b)
-    monkeypatch.setenv("SCS_LU_COOP_WIDE", "0")
+    monkeypatch.setenv("SCS_LU_COOP_WIDE", "1")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info1 == info2 == 0
+    assert np.array_equal(ipiv1, ipiv2)
+    assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
+
+
+@pytest.mark.parametrize("n", [300, 2176, 8320])
+def test_lu_coop_512_threads_bit_identical(n, monkeypatch):
+    """The cooperative panel with 512-thread workgroups (256 rows each, SCS_LU_COOP_NT=512; the last
+    workgroup holds 128 rows where h is an odd multiple of 128) against the r02 column steps: bit for bit."""
+    rng = np.random.default_rng(n + 17)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    monkeypatch.setenv("SCS_LU_COOP_NT", "512")
+    x2, ipiv2, info2 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_PANEL", "1")
     x1, ipiv1, info1 = scsopt.lu_solve(A, b)
     assert info1 == info2 == 0
     assert np.array_equal(ipiv1, ipiv2)
