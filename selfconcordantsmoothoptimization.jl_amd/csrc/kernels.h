@@ -182,7 +182,10 @@ struct LUAux {
   double* Uinv = nullptr;    // [nblk][128 x 128] row-major U11⁻¹
   double* T = nullptr;       // [npad][128] A12ᵀ staging
   double* UT = nullptr;      // [npad][128] U12 as K-contiguous columns
-  double* w = nullptr;       // [128 x +1 | 128 x -1]
+  double* UTo = nullptr;     // [npad][512] an outer block's U rows on the trailing columns, K-contiguous
+  int2* rect = nullptr;      // row-major nblk x c tile rectangles, c = 1 .. 3 (updates inside an outer block)
+  double* w = nullptr;       // [128 x +1 | 512 x -1]
+  mutable int ob = 1;        // panels per outer block of the last lu_factor (lu_solve follows its row order)
   int2* sq = nullptr;        // square-shell tile list (trailing updates)
   int2* row1 = nullptr;      // (0, j) tile list (TRSM)
 };

@@ -39,6 +39,7 @@ constexpr int LB = 128;           // block / panel width
 constexpr int LU_MAXWG = 256;     // workgroups of a panel step at most
 constexpr int LU_NT = 256;        // panel step: 32 rows x 8 lanes (16 columns each) per pass
 constexpr int LU_MAXPAIRS = 2 * LB;
+constexpr int LU_OB = 4;          // panels per outer block (SCS_LU_OB)
 
 __device__ __forceinline__ bool lu_better(double v1, int i1, double v2, int i2) {
   return v1 > v2 || (v1 == v2 && i1 < i2);
@@ -877,12 +878,23 @@ __global__ void lu_pad_kernel(double* A, int64_t ld, int64_t n, int64_t npad) {
 
 // ---- solve -------------------------------------------------------------------------
 // forward block k: apply the block's row moves to b, then b_k <- L11⁻¹ b_k
+// a block's row moves applied to b (all sources read before any store)
+__global__ __launch_bounds__(256) void lu_moves_kernel(const int2* __restrict__ pairs, const int* __restrict__ npairs,
+                                                       double* b) {
+  const int tid = threadIdx.x, np = *npairs;
+  double v = 0.0;
+  if (tid < np) v = b[pairs[tid].y];
+  __syncthreads();
+  if (tid < np) b[pairs[tid].x] = v;
+}
+
 __global__ __launch_bounds__(256) void lu_fwd_block_kernel(const int2* __restrict__ pairs,
                                                            const int* __restrict__ npairs,
-                                                           const double* __restrict__ Linv, int64_t r0, double* b) {
+                                                           const double* __restrict__ Linv, int64_t r0, double* b,
+                                                           int moves) {
   __shared__ double bs[LB];
   __shared__ double part[2][LB];
-  const int tid = threadIdx.x, np = *npairs;
+  const int tid = threadIdx.x, np = moves ? *npairs : 0;
   double v = 0.0;
   if (tid < np) v = b[pairs[tid].y];
   __syncthreads();
@@ -955,11 +967,8 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
   if (a->npad >= npad) return hipSuccess;
   lu_aux_free(a);
   const int nblk = (int)(npad / LB);
-  std::vector<double> hw(2 * LB);
-  for (int i = 0; i < LB; ++i) {
-    hw[i] = 1.0;
-    hw[LB + i] = -1.0;
-  }
+  std::vector<double> hw(LB + LU_OB * LB, -1.0);   // [128 x +1 | 512 x -1]
+  for (int i = 0; i < LB; ++i) hw[i] = 1.0;
   // square-shell order: the first t² entries are the t x t leading block
   std::vector<int2> sq;
   sq.reserve((size_t)nblk * nblk);
@@ -969,6 +978,11 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
   }
   std::vector<int2> row1(nblk);
   for (int j = 0; j < nblk; ++j) row1[j] = make_int2(0, j);
+  // row-major nblk x c rectangles, c = 1 .. LU_OB - 1 (the updates inside an outer block)
+  std::vector<int2> rect;
+  for (int c = 1; c < LU_OB; ++c)
+    for (int i = 0; i < nblk; ++i)
+      for (int j = 0; j < c; ++j) rect.push_back(make_int2(i, j));
   hipError_t e = hipSuccess;
   auto al = [&](void** p, size_t bytes) {
     if (e == hipSuccess) e = hipMalloc(p, bytes);
@@ -986,21 +1000,25 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
   al((void**)&a->Uinv, sizeof(double) * (size_t)nblk * LB * LB);
   al((void**)&a->T, sizeof(double) * (size_t)npad * LB);
   al((void**)&a->UT, sizeof(double) * (size_t)npad * LB);
-  al((void**)&a->w, sizeof(double) * 2 * LB);
+  al((void**)&a->UTo, sizeof(double) * (size_t)npad * LU_OB * LB);
+  al((void**)&a->rect, sizeof(int2) * rect.size());
+  al((void**)&a->w, sizeof(double) * hw.size());
   al((void**)&a->sq, sizeof(int2) * sq.size());
   al((void**)&a->row1, sizeof(int2) * row1.size());
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->sq, sq.data(), sizeof(int2) * sq.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(a->row1, row1.data(), sizeof(int2) * row1.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(a->rect, rect.data(), sizeof(int2) * rect.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e == hipSuccess) a->npad = npad;
   return e;
 }
 
 void lu_aux_free(LUAux* a) {
-  void* ps[] = {a->cand, a->candi, a->candrow, a->rowj, a->gran, a->ipiv, a->pairs, a->npairs,
-                a->Linv, a->Uinv, a->T,     a->UT,      a->w,    a->sq,   a->row1};
+  void* ps[] = {a->cand, a->candi, a->candrow, a->rowj, a->gran, a->ipiv, a->pairs, a->npairs, a->Linv,
+                a->Uinv, a->T,     a->UT,      a->UTo,  a->rect, a->w,    a->sq,   a->row1};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   *a = LUAux();
@@ -1043,32 +1061,35 @@ static int lu_inv_mode() {
   return e ? atoi(e) : 2;
 }
 
-hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st) {
-  if (npad % LB != 0 || npad > a->npad || ld < npad) return hipErrorInvalidValue;
-  const int nblk = (int)(npad / LB);
-  if (lu_panel_mode() == 3) {   // the cooperative panels' granules and abort word, once per factorization
-    const hipError_t e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * LUC_WORDS, st);
+// SCS_LU_OB (read per call): panels per outer block.  4 (default): the trailing matrix takes ONE update per
+// four panels with K = 512 (r05; the K = 128 updates ran at ~26 TF/s on the C read-modify-write);
+// 1: the r02 per-panel updates.  Recorded in the aux for lu_solve (its forward steps follow the
+// factor's row order).
+static int lu_outer_block() {
+  const char* e = getenv("SCS_LU_OB");
+  const int v = e ? atoi(e) : 1;
+  return v >= 2 ? LU_OB : 1;
+}
+
+// the panel of block k: its 128 column steps (one cooperative launch, or the step launches), the composed
+// row moves and the diagonal block's inverses
+static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUAux* a, int* info, hipStream_t st) {
+  const int64_t r0 = (int64_t)k * LB, c0 = r0, h = npad - r0;
+  const int R = 32 * (int)ceil_div(h, 32 * LU_MAXWG);
+  const int nwg = (int)ceil_div(h, R);
+  const int npass = R / 32, mode = lu_panel_mode();
+  const int cnt = lu_coop_nt();
+  const int64_t gco = ceil_div(h, (int64_t)(cnt / 2));
+  const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG);
+  if (coop) {
+    const hipError_t e = lu_coop_attr();
     if (e != hipSuccess) return e;
-  }
-  if (npad > n)
-    hipLaunchKernelGGL(lu_pad_kernel, dim3((unsigned)ceil_div(npad - n, 256)), dim3(256), 0, st, A, ld, n, npad);
-  for (int k = 0; k < nblk; ++k) {
-    const int64_t r0 = (int64_t)k * LB, c0 = r0, h = npad - r0;
-    const int R = 32 * (int)ceil_div(h, 32 * LU_MAXWG);
-    const int nwg = (int)ceil_div(h, R);
-    const int npass = R / 32, mode = lu_panel_mode();
-    const int cnt = lu_coop_nt();
-    const int64_t gco = ceil_div(h, (int64_t)(cnt / 2));
-    const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG);
-    if (coop) {
-      const hipError_t e = lu_coop_attr();
-      if (e != hipSuccess) return e;
-      const bool wide = lu_coop_wide();
-      auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
-                             : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)gco), dim3(cnt), LUC_LDS, st, A, ld, r0, c0, h, a->gran, (unsigned)k << 8,
-                         a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
-    } else
+    const bool wide = lu_coop_wide();
+    auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
+                           : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)gco), dim3(cnt), LUC_LDS, st, A, ld, r0, c0, h, a->gran, (unsigned)k << 8,
+                       a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
+  } else
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)
         hipLaunchKernelGGL(lu_panel_step2_kernel<1>, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
@@ -1080,30 +1101,89 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
         hipLaunchKernelGGL(lu_panel_step_kernel, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,
                            a->candi, a->candrow, a->rowj, a->ipiv, info);
     }
-    int2* pairs = a->pairs + (int64_t)k * LU_MAXPAIRS;
-    if (!coop)   // (the cooperative panel composes its interchanges itself)
-      hipLaunchKernelGGL(lu_perm_kernel, dim3(1), dim3(64), 0, st, a->ipiv, (int)r0, pairs, a->npairs + k);
-    if (lu_inv_mode() == 1)
-      hipLaunchKernelGGL(lu_diag_inv_kernel, dim3(2), dim3(256), 0, st, A, ld, r0, a->Linv + (int64_t)k * LB * LB,
-                         a->Uinv + (int64_t)k * LB * LB);
-    else
-      (void)launch_lu_tri_inv(A, ld, r0, a->Linv + (int64_t)k * LB * LB, a->Uinv + (int64_t)k * LB * LB, st);
-    const int64_t w = npad - c0 - LB;   // columns right of the panel
-    if (w == 0) break;
-    hipLaunchKernelGGL(lu_swap_cols_kernel, dim3((unsigned)ceil_div(w, SW_COLS)), dim3(256), 0, st, A, ld, c0 + LB, w,
-                       pairs, a->npairs + k);
-    // TRSM: U12 = L11⁻¹ A12 (row-major into A) and U12ᵀ-as-columns into UT
-    hipLaunchKernelGGL(lu_transpose_kernel, dim3((unsigned)ceil_div(w, 64), LB / 64), dim3(256), 0, st, A, ld, r0,
-                       c0 + LB, w, a->T);
-    const int nc = (int)(w / LB);
-    const double* Lk = a->Linv + (int64_t)k * LB * LB;
-    hipError_t e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nc, A + r0 * ld + c0 + LB, ld,
-                                   /*GRAM_UPPER*/ 4, st);
-    if (e == hipSuccess) e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nc, a->UT, LB, 0, st);
-    // A22 -= L21 U12
-    if (e == hipSuccess)
-      e = gram_launch_gen(A + (r0 + LB) * ld + c0, ld, a->UT, LB, a->w + LB, 0, LB, a->sq, nc * nc,
-                          A + (r0 + LB) * ld + c0 + LB, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+  if (!coop)   // (the cooperative panel composes its interchanges itself)
+    hipLaunchKernelGGL(lu_perm_kernel, dim3(1), dim3(64), 0, st, a->ipiv, (int)r0, a->pairs + (int64_t)k * LU_MAXPAIRS,
+                       a->npairs + k);
+  if (lu_inv_mode() == 1)
+    hipLaunchKernelGGL(lu_diag_inv_kernel, dim3(2), dim3(256), 0, st, A, ld, r0, a->Linv + (int64_t)k * LB * LB,
+                       a->Uinv + (int64_t)k * LB * LB);
+  else
+    (void)launch_lu_tri_inv(A, ld, r0, a->Linv + (int64_t)k * LB * LB, a->Uinv + (int64_t)k * LB * LB, st);
+  return hipGetLastError();
+}
+
+static void lu_swap(double* A, int64_t ld, int64_t c_lo, int64_t w, const LUAux* a, int k, hipStream_t st) {
+  if (w <= 0) return;
+  hipLaunchKernelGGL(lu_swap_cols_kernel, dim3((unsigned)ceil_div(w, SW_COLS)), dim3(256), 0, st, A, ld, c_lo, w,
+                     a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
+}
+
+hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st) {
+  if (npad % LB != 0 || npad > a->npad || ld < npad) return hipErrorInvalidValue;
+  const int nblk = (int)(npad / LB);
+  const int OB = lu_outer_block();
+  a->ob = OB;
+  if (lu_panel_mode() == 3) {   // the cooperative panels' granules and abort word, once per factorization
+    const hipError_t e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * LUC_WORDS, st);
+    if (e != hipSuccess) return e;
+  }
+  if (npad > n)
+    hipLaunchKernelGGL(lu_pad_kernel, dim3((unsigned)ceil_div(npad - n, 256)), dim3(256), 0, st, A, ld, n, npad);
+  hipError_t e = hipSuccess;
+  for (int b0 = 0; b0 < nblk; b0 += OB) {
+    const int b1 = std::min(b0 + OB, nblk);
+    const int64_t cb0 = (int64_t)b0 * LB, cb1 = (int64_t)b1 * LB;
+    // the outer block's panels, right-looking inside it: each panel's moves to the block's other columns
+    // (the earlier panels' L columns too, so the block's L rows end in the block's final order) and its
+    // U rows / update over the block's later columns only (OB = 1: the whole trailing matrix)
+    for (int k = b0; k < b1; ++k) {
+      const int64_t r0 = (int64_t)k * LB, c0 = r0;
+      e = lu_panel(A, ld, npad, k, a, info, st);
+      if (e != hipSuccess) return e;
+      const int64_t wr = (OB == 1 ? npad : cb1) - c0 - LB;   // columns right of the panel it updates now
+      lu_swap(A, ld, c0 + LB, wr, a, k, st);
+      lu_swap(A, ld, cb0, c0 - cb0, a, k, st);
+      if (wr == 0) continue;
+      // TRSM: U12 = L11⁻¹ A12 (row-major into A) and U12ᵀ-as-columns into UT
+      hipLaunchKernelGGL(lu_transpose_kernel, dim3((unsigned)ceil_div(wr, 64), LB / 64), dim3(256), 0, st, A, ld, r0,
+                         c0 + LB, wr, a->T);
+      const int nc = (int)(wr / LB), nr = (int)((npad - r0 - LB) / LB);
+      const double* Lk = a->Linv + (int64_t)k * LB * LB;
+      e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nc, A + r0 * ld + c0 + LB, ld, /*GRAM_UPPER*/ 4, st);
+      if (e == hipSuccess) e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nc, a->UT, LB, 0, st);
+      // A22 -= L21 U12 over the rows below and the columns it updates now (square: OB = 1; nr x nc rows-major:
+      // inside an outer block)
+      if (e == hipSuccess && nr > 0) {
+        const int2* tl = (OB == 1) ? a->sq : a->rect + (int64_t)nblk * (nc - 1) * nc / 2;
+        e = gram_launch_gen(A + (r0 + LB) * ld + c0, ld, a->UT, LB, a->w + LB, 0, LB, tl, (OB == 1) ? nc * nc : nr * nc,
+                            A + (r0 + LB) * ld + c0 + LB, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+      }
+      if (e != hipSuccess) return e;
+    }
+    if (OB == 1 || cb1 == npad) continue;
+    // the trailing columns: the block's moves in order, its U rows by block forward substitution
+    // (X_t = L_tt⁻¹ (A_t - Σ_{s<t} L_ts X_s), X into A and, K-contiguous, into UTo), then ONE update
+    // A22 -= L21 X with K = (b1 - b0)·128
+    const int64_t wt = npad - cb1;
+    const int nct = (int)(wt / LB), KO = (b1 - b0) * LB;
+    for (int k = b0; k < b1; ++k) lu_swap(A, ld, cb1, wt, a, k, st);
+    for (int k = b0; k < b1; ++k) {
+      const int64_t r0 = (int64_t)k * LB;
+      const int t = k - b0;
+      if (t > 0)
+        e = gram_launch_gen(A + r0 * ld + cb0, ld, a->UTo, LU_OB * LB, a->w + LB, 0, (int64_t)t * LB, a->row1, nct,
+                            A + r0 * ld + cb1, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(lu_transpose_kernel, dim3((unsigned)ceil_div(wt, 64), LB / 64), dim3(256), 0, st, A, ld, r0,
+                         cb1, wt, a->T);
+      const double* Lk = a->Linv + (int64_t)k * LB * LB;
+      e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nct, A + r0 * ld + cb1, ld, /*GRAM_UPPER*/ 4, st);
+      if (e == hipSuccess)
+        e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nct, a->UTo + (int64_t)t * LB, LU_OB * LB, 0, st);
+      if (e != hipSuccess) return e;
+    }
+    e = gram_launch_gen(A + cb1 * ld + cb0, ld, a->UTo, LU_OB * LB, a->w + LB, 0, KO, a->sq, nct * nct,
+                        A + cb1 * ld + cb1, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
     if (e != hipSuccess) return e;
   }
   return hipGetLastError();
@@ -1111,10 +1191,17 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
 
 hipError_t lu_solve(const double* A, int64_t ld, int64_t npad, const LUAux* a, double* b, hipStream_t st) {
   const int nblk = (int)(npad / LB);
+  const int OB = a->ob;
   for (int k = 0; k < nblk; ++k) {
     const int64_t r0 = (int64_t)k * LB;
+    // an outer block's L rows are in the block's final row order: all its moves to b before its first
+    // forward step (OB = 1: each block's moves just before its own step)
+    if (OB > 1 && k % OB == 0)
+      for (int kk = k; kk < std::min(k + OB, nblk); ++kk)
+        hipLaunchKernelGGL(lu_moves_kernel, dim3(1), dim3(256), 0, st, a->pairs + (int64_t)kk * LU_MAXPAIRS,
+                           a->npairs + kk, b);
     hipLaunchKernelGGL(lu_fwd_block_kernel, dim3(1), dim3(256), 0, st, a->pairs + (int64_t)k * LU_MAXPAIRS,
-                       a->npairs + k, a->Linv + (int64_t)k * LB * LB, r0, b);
+                       a->npairs + k, a->Linv + (int64_t)k * LB * LB, r0, b, OB == 1 ? 1 : 0);
     const int64_t nr = npad - r0 - LB;
     if (nr > 0)
       hipLaunchKernelGGL(lu_rank_update_kernel, dim3((unsigned)ceil_div(nr, 32)), dim3(256), 0, st, A, ld, r0 + LB, nr,

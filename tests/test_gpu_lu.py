@@ -187,3 +187,27 @@ def test_lu_coop_512_threads_bit_identical(n, monkeypatch):
     assert info1 == info2 == 0
     assert np.array_equal(ipiv1, ipiv2)
     assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
+
+
+@pytest.mark.parametrize("n", [300, 1000, 2176, 8320])
+def test_lu_outer_blocked_update(n, monkeypatch):
+    """Outer blocks of four panels (SCS_LU_OB=4): inside a block each panel's moves reach the block's
+    other columns (its earlier L columns too) and its update only the block's later columns; the trailing
+    matrix takes the block's moves, a block forward substitution for its U rows and ONE K = 512 update;
+    lu_solve applies a block's moves before its first forward step.  Pivots equal LAPACK dgetrf's (and
+    the per-panel factor's), the solution within 1e-14·cond of LAPACK's, backward error <= 1e-13.
+    n = 300: one partial outer block; 2176: 17 panels (the last outer block a single panel)."""
+    rng = np.random.default_rng(n + 23)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    monkeypatch.setenv("SCS_LU_OB", "4")
+    x4, ipiv4, info4 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_OB", "1")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    _, piv, linfo = lapack.dgetrf(A)
+    assert info4 == info1 == linfo == 0
+    assert np.array_equal(ipiv4, piv) and np.array_equal(ipiv1, piv)
+    kappa = float(np.linalg.cond(A, np.inf))
+    xr = sla.lu_solve(lapack.dgetrf(A)[:2], b)
+    assert np.max(np.abs(x4 - xr)) <= 1e-14 * kappa * float(np.abs(xr).max())
+    assert _bwd(A, x4, b) <= 1e-13
