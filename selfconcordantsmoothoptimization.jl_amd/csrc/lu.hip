@@ -1062,12 +1062,13 @@ static int lu_inv_mode() {
 }
 
 // SCS_LU_OB (read per call): panels per outer block.  4 (default): the trailing matrix takes ONE update per
-// four panels with K = 512 (r05; the K = 128 updates ran at ~26 TF/s on the C read-modify-write);
-// 1: the r02 per-panel updates.  Recorded in the aux for lu_solve (its forward steps follow the
+// four panels with K = 512 (r05; the K = 128 updates ran at ~26 TF/s on the C read-modify-write: the
+// n = 8192 updates 13.8 -> 8.0 ms, factor + solve 83.7-83.9 -> 82.0-82.9 ms, n = 16384 250.8-251.2 ->
+// 216.8-217.1 ms); 1: the r02 per-panel updates.  Recorded in the aux for lu_solve (its forward steps follow the
 // factor's row order).
 static int lu_outer_block() {
   const char* e = getenv("SCS_LU_OB");
-  const int v = e ? atoi(e) : 1;
+  const int v = e ? atoi(e) : LU_OB;
   return v >= 2 ? LU_OB : 1;
 }
 

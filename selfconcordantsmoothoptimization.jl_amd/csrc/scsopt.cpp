@@ -1294,9 +1294,12 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
     ensure_red(c);
   }
   // the band (relative) within which an incremental trial is re-decided on the direct form;
-  // SCS_LS_NEAR overrides it (tests: a huge band re-decides every trial)
+  // SCS_LS_NEAR overrides it (tests: a huge band re-decides every trial).  The incremental form's own
+  // rounding is one extra addition per z_i (<= eps·(|Ax|_i + α|Ad|_i)): ~1e-16 relative in f; both
+  // forms share the dot products' rounding.  1e-12 leaves four orders of margin -- the r05 first
+  // value, 1e-9, re-decided most late trials at C3 (an A pass each: the C3 step's gemv 23.7 -> 30.1 ms)
   const char* ne = std::getenv("SCS_LS_NEAR");
-  const double near = ne ? std::atof(ne) : 1e-9;
+  const double near = ne ? std::atof(ne) : 1e-12;
   double alpha = 1.0;
   for (int trial = 0; trial < 100000; ++trial) {
     // the trial point lives on the device only (no host copy: it is keyed by a fresh tag)
@@ -1314,7 +1317,7 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
       const double rg = eval_reg_dev(c, c->gtmp2);   // syncs: hscal[14] has landed too
       ft = loss_scale_value(c, c->hscal[14]) + rg;
       // Ax + fl(α·Ad) differs from the reference's A·fl(x + αd) (utils.jl:27-35) in the last bits
-      // of each z_i: a trial whose Armijo test sits within 1e-9 (relative) of its threshold is
+      // of each z_i: a trial whose Armijo test sits within `near` (relative) of its threshold is
       // decided on the direct form instead, so the accepted α is the reference's form's
       if (std::fabs(ft - (f0 + 1e-4 * alpha * gd)) <= near * std::max(std::fabs(f0), std::fabs(ft))) {
         ft = eval_f_dev(c, nullptr, c->gtmp2) + eval_reg_dev(c, c->gtmp2);
