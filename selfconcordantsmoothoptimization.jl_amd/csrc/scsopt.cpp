@@ -1296,8 +1296,8 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
   // the band (relative) within which an incremental trial is re-decided on the direct form;
   // SCS_LS_NEAR overrides it (tests: a huge band re-decides every trial).  The incremental form's own
   // rounding is one extra addition per z_i (<= eps·(|Ax|_i + α|Ad|_i)): ~1e-16 relative in f; both
-  // forms share the dot products' rounding.  1e-12 leaves four orders of margin -- the r05 first
-  // value, 1e-9, re-decided most late trials at C3 (an A pass each: the C3 step's gemv 23.7 -> 30.1 ms)
+  // forms share the dot products' rounding.  1e-12 leaves four orders of margin (the first r05
+  // value, 1e-9, re-decided trials whose margin was a million times the incremental form's rounding)
   const char* ne = std::getenv("SCS_LS_NEAR");
   const double near = ne ? std::atof(ne) : 1e-12;
   double alpha = 1.0;
