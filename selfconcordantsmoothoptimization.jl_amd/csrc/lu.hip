@@ -418,7 +418,8 @@ template <bool WIDE, int NT>
 __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
                                                               int64_t c0, int64_t h, unsigned long long* gran,
                                                               unsigned tagbase,
-                                                              int* ipiv, int* info, int2* pairs, int* npairs) {
+                                                              int* ipiv, int* info, int2* pairs, int* npairs,
+                                                              int pf_on) {
   constexpr int RW = NT / 2, RP = NT / 8;   // rows per workgroup, rows per pass
   __shared__ double sv[NT / 64];
   __shared__ int si[NT / 64], sw[NT / 64];
@@ -496,14 +497,6 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
       }
       __syncthreads();   // the rows' granules issued ahead of the candidate's (the tags decide anyway)
     }
-    if (tid == 0) {
-      const unsigned long long t = (unsigned long long)tag << 32;
-      const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
-      unsigned long long* gp = gran + LUC_CAND + ((int64_t)par * LUC_MAXWG + g) * 4;
-      luc_put(gp + 0, t | (bits & 0xffffffffull));
-      luc_put(gp + 1, t | (bits >> 32));
-      luc_put(gp + 2, t | (unsigned)bi);
-    }
 #pragma unroll
     for (int ps = 0; ps < 4 && !WIDE; ++ps) {
       const int i = base + RP * ps;
@@ -517,6 +510,17 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
 #pragma unroll
         for (int c = 0; c < 16; ++c) luc_put_d(rp + 2 * c, tag, v[ps][c]);
       }
+    }
+    // the record after the rows (a barrier apart): a consumer that prefetches the best row so far
+    // usually finds it landed (the tags decide either way)
+    if (!WIDE) __syncthreads();
+    if (tid == 0) {
+      const unsigned long long t = (unsigned long long)tag << 32;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
+      unsigned long long* gp = gran + LUC_CAND + ((int64_t)par * LUC_MAXWG + g) * 4;
+      luc_put(gp + 0, t | (bits & 0xffffffffull));
+      luc_put(gp + 1, t | (bits >> 32));
+      luc_put(gp + 2, t | (unsigned)bi);
     }
   };
   if (g == 0) {
@@ -533,18 +537,25 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
       double cv = -1.0;
       int ci = INT_MAX, cw = -1;
       const unsigned long long* gp = gran + LUC_CAND + (int64_t)par * LUC_MAXWG * 4;
+      // the row of the best candidate among those already arrived, prefetched while the sweep waits for
+      // the rest (lane l: granules 4l .. 4l+3 = columns 2l, 2l+1); used if that candidate wins
+      int pf_w = -1;
+      unsigned long long pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0;
       for (unsigned spins = 0;;) {
         bool ok = true;
         cv = -1.0;
         ci = INT_MAX;
         cw = -1;
+        double bv = -2.0;   // the best arrived candidate (every lane's arrived records)
+        int bi = INT_MAX, bw = -1;
 #pragma unroll
         for (int t = 0; t < LUC_MAXWG / 64; ++t) {
           const int w = lane + 64 * t;
           if (w < nwg) {
             const unsigned long long x0 = luc_get(gp + 4 * w + 0), x1 = luc_get(gp + 4 * w + 1),
                                      x2 = luc_get(gp + 4 * w + 2);
-            ok = ok && (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag && (unsigned)(x2 >> 32) == tag;
+            const bool okw = (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag && (unsigned)(x2 >> 32) == tag;
+            ok = ok && okw;
             double a = __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
             int r = (int)(unsigned)x2;
             if (!(a >= 0.0)) {   // no candidate (or NaN): never wins
@@ -556,9 +567,33 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
               ci = r;
               cw = w;
             }
+            if (okw && a >= 0.0 && lu_better(a, r, bv, bi)) {
+              bv = a;
+              bi = r;
+              bw = w;
+            }
           }
         }
         if (__all(ok)) break;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const double v2 = __shfl_xor(bv, o, 64);
+          const int i2 = __shfl_xor(bi, o, 64);
+          const int w2 = __shfl_xor(bw, o, 64);
+          if (lu_better(v2, i2, bv, bi)) {
+            bv = v2;
+            bi = i2;
+            bw = w2;
+          }
+        }
+        if (pf_on && bw >= 0 && bw != pf_w) {   // (wave-uniform)
+          const unsigned long long* rp = gran + LUC_CROW + ((int64_t)par * LUC_MAXWG + bw) * LB * 2 + 4 * lane;
+          pf0 = luc_get(rp);
+          pf1 = luc_get(rp + 1);
+          pf2 = luc_get(rp + 2);
+          pf3 = luc_get(rp + 3);
+          pf_w = bw;
+        }
         if (++spins > LUC_SPIN_MAX) {
           give_up();
           break;
@@ -597,7 +632,17 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
         p = j;
         urow = rowj_g;
       }
-      if (alive) stage(urow, su_u);
+      if (alive) {
+        const bool hit = cv >= 0.0 && cw == pf_w &&
+                         __all((unsigned)(pf0 >> 32) == tag && (unsigned)(pf1 >> 32) == tag &&
+                               (unsigned)(pf2 >> 32) == tag && (unsigned)(pf3 >> 32) == tag);
+        if (hit) {
+          su_u[2 * lane] = __longlong_as_double((long long)((pf0 & 0xffffffffull) | (pf1 << 32)));
+          su_u[2 * lane + 1] = __longlong_as_double((long long)((pf2 & 0xffffffffull) | (pf3 << 32)));
+        } else {
+          stage(urow, su_u);
+        }
+      }
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // this wave's LDS writes, then its reads
       __builtin_amdgcn_wave_barrier();
       if (alive && su_u[j] == 0.0) {   // getf2: zero pivot -> no interchange, no scaling (row j's u_j
@@ -1044,6 +1089,11 @@ static hipError_t lu_coop_attr() {   // the dynamic LDS above the 64 KiB default
   return done;
 }
 
+static bool lu_coop_pf() {   // read per call (A/B): SCS_LU_COOP_PF=0 stages the pivot row only after the sweep
+  const char* e = getenv("SCS_LU_COOP_PF");
+  return !(e && e[0] == '0');
+}
+
 static int lu_coop_nt() {   // read per call (A/B): SCS_LU_COOP_NT = 256 | 512
   const char* e = getenv("SCS_LU_COOP_NT");
   return (e && atoi(e) == 512) ? 512 : 256;
@@ -1089,7 +1139,7 @@ static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUA
     auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
                            : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
     hipLaunchKernelGGL(kern, dim3((unsigned)gco), dim3(cnt), LUC_LDS, st, A, ld, r0, c0, h, a->gran, (unsigned)k << 8,
-                       a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
+                       a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k, lu_coop_pf() ? 1 : 0);
   } else
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)
