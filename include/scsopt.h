@@ -401,7 +401,9 @@ int scs_solve_eval(scs_ctx* ctx, const double* w, const double* dvec, const doub
                    double* x, int* used_lu);
 /* Julia's `A \ b` for a dense square Matrix (LAPACK getrf + getrs) by the hand-written
  * blocked LU: A is row-major n x n; ipiv receives getrf's pivot rows (0-based), info its
- * first zero pivot (1-based; x is then not written).  Needs a context only.               */
+ * first zero pivot (1-based; x is then not written), or -1 if the cooperative panel's
+ * candidate exchange timed out (a workgroup never became resident; x not written).
+ * Needs a context only.                                                                    */
 int scs_lu_eval(scs_ctx* ctx, int64_t n, const double* A, const double* b, double* x, int32_t* ipiv,
                 int* info);
 /* Columns cols[0..ncols) of the local (dense) A, column-major N x ncols.                 */

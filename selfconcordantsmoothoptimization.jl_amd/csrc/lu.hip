@@ -1205,7 +1205,8 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
       // A22 -= L21 U12 over the rows below and the columns it updates now (square: OB = 1; nr x nc rows-major:
       // inside an outer block)
       if (e == hipSuccess && nr > 0) {
-        const int2* tl = (OB == 1) ? a->sq : a->rect + (int64_t)nblk * (nc - 1) * nc / 2;
+        const int64_t ncap = a->npad / LB;   // the lists were built for the aux's capacity
+        const int2* tl = (OB == 1) ? a->sq : a->rect + ncap * (nc - 1) * nc / 2;
         e = gram_launch_gen(A + (r0 + LB) * ld + c0, ld, a->UT, LB, a->w + LB, 0, LB, tl, (OB == 1) ? nc * nc : nr * nc,
                             A + (r0 + LB) * ld + c0 + LB, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
       }

@@ -1367,6 +1367,7 @@ void solve_lu_fallback(scs_ctx* c, double* rhs, hipEvent_t e0) {
   HCK(lu_factor(c->Gc, ld, m, ld, &c->lu, c->cinfo, c->st));
   HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
+  if (info < 0) fail(c, SCS_ERR_HIP, "LU: the cooperative panel's candidate exchange timed out (info %d)", info);
   if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
   HCK(lu_solve(c->Gc, ld, ld, &c->lu, rhs, c->st));
   tend(c, T_SOLVE, e0);
@@ -2005,6 +2006,7 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
     HCK(lu_factor(c->Ms, np1, n1, np1, &c->lu, c->cinfo, c->st));
     HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
     sync(c);
+    if (info < 0) fail(c, SCS_ERR_HIP, "LU: the cooperative panel's candidate exchange timed out (info %d)", info);
     if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
     HCK(lu_solve(c->Ms, np1, np1, &c->lu, c->bS, c->st));
   }

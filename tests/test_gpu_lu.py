@@ -211,3 +211,19 @@ def test_lu_outer_blocked_update(n, monkeypatch):
     xr = sla.lu_solve(lapack.dgetrf(A)[:2], b)
     assert np.max(np.abs(x4 - xr)) <= 1e-14 * kappa * float(np.abs(xr).max())
     assert _bwd(A, x4, b) <= 1e-13
+
+
+def test_lu_smaller_system_after_larger_on_one_context():
+    """The LU's work buffers and tile lists are sized for the largest system a context has seen; a
+    smaller system afterwards (outer blocks of four panels, rectangle tile lists at the capacity's
+    offsets) still gets LAPACK's pivots and a backward-stable solution."""
+    ctx = scsopt._lib.Context(0)
+    rng = np.random.default_rng(29)
+    for n in (2176, 1000, 300):
+        A = rng.standard_normal((n, n))
+        b = rng.standard_normal(n)
+        x, ipiv, info = scsopt.lu_solve(A, b, ctx=ctx)
+        _, piv, linfo = lapack.dgetrf(A)
+        assert info == linfo == 0
+        assert np.array_equal(ipiv, piv)
+        assert _bwd(A, x, b) <= 1e-13
