@@ -766,10 +766,13 @@ static hipError_t create_bulk_stream(hipStream_t* s) { return hipStreamCreateWit
 // created streams, the caller's stream (the chain) and the bulk stream could land on ONE hardware queue
 // and the two halves of the factor then ran back to back: +6.8 ms of solve per C3-shaped step with the
 // exchange forced at world 1, every kernel of the step on one queue in the trace
-// (profiles/r05/rccltrace/).  Streams of different priority cannot share a queue.  SCS_CHOL_CHAIN (read
-// per call): 2 (default) the bulk stream at the device's greatest priority, the chain on the caller's
-// stream; 1 the chain on a stream of its own at the greatest priority, joined to the caller's by events;
-// 0 both at normal priority (r04).
+// (profiles/r05/rccltrace/).  Streams of different priority cannot share a queue.  Modes: 2 the bulk
+// stream at the device's greatest priority, the chain on the caller's stream (the default where the
+// context holds an RCCL communicator: CholAux::chain_mode, set by scsopt.cpp); 1 the chain on a stream
+// of its own at the greatest priority, joined to the caller's by events; 0 both at normal priority (r04;
+// the default elsewhere: a high-priority bulk stream wins the dispatcher's free slots over the chain's
+// latency launches, which shows under a kernel tracer -- the m = 8192 probe factor 7.6 -> 13.4 ms under
+// rocprofv3 -- though not in the untraced C2 line).  SCS_CHOL_CHAIN (read per call) overrides.
 static hipError_t create_hiprio_stream(hipStream_t* s) {
   int least = 0, greatest = 0;
   hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
@@ -777,9 +780,9 @@ static hipError_t create_hiprio_stream(hipStream_t* s) {
   return e;
 }
 
-static int chol_chain_mode() {
+static int chol_chain_mode(const CholAux* a) {
   const char* e = getenv("SCS_CHOL_CHAIN");
-  return e ? atoi(e) : 2;
+  return e ? atoi(e) : a->chain_mode;
 }
 
 // SCS_CHOL_SKIP_MAXTILES (A/B; unset = no limit): bulk launches of more tiles than this run on every
@@ -1328,7 +1331,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
   const int OB = outer_block_for(nblk);
   const bool la = chol_lookahead() && a->st2 && nblk > 2 * OB;
   // the chain's and the bulk stream (create_hiprio_stream): never one hardware queue
-  const int cmode = chol_chain_mode();
+  const int cmode = chol_chain_mode(a);
   hipStream_t st = st_caller;
   hipStream_t sb = (cmode == 2 && a->st2h) ? a->st2h : a->st2;
   if (la && cmode == 1 && a->stc && a->ev0 && a->ev5) {

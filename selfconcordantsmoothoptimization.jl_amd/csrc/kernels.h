@@ -109,6 +109,9 @@ struct CholAux {             // device constants of the two-level factorization 
   unsigned bskip = 0;
   int bslots = 0;
   mutable int bslot = 0;   // the next unused counter set
+  // the streams' hardware-queue guard (SCS_CHOL_CHAIN, chol.hip): 2 where the process also holds RCCL's
+  // streams (the caller sets it), else 0
+  mutable int chain_mode = 0;
   // the chain's strip solve as right-looking step launches (strip_solve_steps): two rows of
   // 128 x (16 x 128) doubles for a step's leaf (its copy-back is the next step's)
   double* sscr = nullptr;

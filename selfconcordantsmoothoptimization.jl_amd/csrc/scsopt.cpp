@@ -1434,6 +1434,7 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false, bool force_qr 
   int info = 0;
   if (!force_lu) {
     HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+    c->caux.chain_mode = c->rccl ? 2 : 0;   // RCCL's streams in the process: keep the factor's two apart
     HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
     HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
     int late = 0;   // a dependency wait of the chain launches or the solves gave up (~30 s): never expected
