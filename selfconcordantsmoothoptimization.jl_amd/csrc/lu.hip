@@ -1131,10 +1131,9 @@ static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUA
   const int npass = R / 32, mode = lu_panel_mode();
   const int cnt = lu_coop_nt();
   const int64_t gco = ceil_div(h, (int64_t)(cnt / 2));
-  const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG);
+  // (a runtime that refuses the dynamic-LDS attribute gets the step kernels)
+  const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG) && lu_coop_attr() == hipSuccess;
   if (coop) {
-    const hipError_t e = lu_coop_attr();
-    if (e != hipSuccess) return e;
     const bool wide = lu_coop_wide();
     auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
                            : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
