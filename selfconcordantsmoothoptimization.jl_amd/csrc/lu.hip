@@ -45,21 +45,47 @@ __device__ __forceinline__ bool lu_better(double v1, int i1, double v2, int i2) 
   return v1 > v2 || (v1 == v2 && i1 < i2);
 }
 
+// One DPP combine step of the wave argmax below: every lane takes the better of its (v, i, w) and the one
+// CTRL moves to it (lanes without a source, or outside ROWMASK, compare with themselves).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void lu_dpp_step(double& v, int& i, int& w) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const int lo = (int)(unsigned)u, hi = (int)(unsigned)(u >> 32);
+  const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xF, false);
+  const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xF, false);
+  const int i2 = __builtin_amdgcn_update_dpp(i, i, CTRL, ROWMASK, 0xF, false);
+  const int w2 = __builtin_amdgcn_update_dpp(w, w, CTRL, ROWMASK, 0xF, false);
+  const double v2 = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2));
+  if (lu_better(v2, i2, v, i)) {
+    v = v2;
+    i = i2;
+    w = w2;
+  }
+}
+
+// (v, i, w) argmax over the wave (larger v, then smaller i) by DPP -- the quad swaps, the half-row and
+// row mirrors, the row-15 / row-31 broadcasts leave the wave's best in lane 63, read back into every lane
+// (r05; was six ds_bpermute rounds).  The rule is associative and commutative and the rows are distinct,
+// so the result is the same as any reduction order's.
+__device__ __forceinline__ void lu_wave_argmax(double& v, int& i, int& w) {
+  lu_dpp_step<0xB1, 0xF>(v, i, w);    // quad_perm [1, 0, 3, 2]
+  lu_dpp_step<0x4E, 0xF>(v, i, w);    // quad_perm [2, 3, 0, 1]
+  lu_dpp_step<0x141, 0xF>(v, i, w);   // row_half_mirror
+  lu_dpp_step<0x140, 0xF>(v, i, w);   // row_mirror
+  lu_dpp_step<0x142, 0xA>(v, i, w);   // row_bcast:15 into rows 1, 3
+  lu_dpp_step<0x143, 0xC>(v, i, w);   // row_bcast:31 into rows 2, 3
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned)u, 63), hi = __builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+  v = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  i = __builtin_amdgcn_readlane(i, 63);
+  w = __builtin_amdgcn_readlane(w, 63);
+}
+
 // (v, i) argmax over the workgroup (larger |a|, then smaller row); every thread gets the result.
 // sv / si hold NT / 64 entries.
 template <int NT = LU_NT>
 __device__ __forceinline__ void lu_block_argmax(double& v, int& i, int& w, double* sv, int* si, int* sw) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double v2 = __shfl_xor(v, o, 64);
-    const int i2 = __shfl_xor(i, o, 64);
-    const int w2 = __shfl_xor(w, o, 64);
-    if (lu_better(v2, i2, v, i)) {
-      v = v2;
-      i = i2;
-      w = w2;
-    }
-  }
+  lu_wave_argmax(v, i, w);
   const int wv = threadIdx.x >> 6;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) {
@@ -575,17 +601,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
           }
         }
         if (__all(ok)) break;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const double v2 = __shfl_xor(bv, o, 64);
-          const int i2 = __shfl_xor(bi, o, 64);
-          const int w2 = __shfl_xor(bw, o, 64);
-          if (lu_better(v2, i2, bv, bi)) {
-            bv = v2;
-            bi = i2;
-            bw = w2;
-          }
-        }
+        lu_wave_argmax(bv, bi, bw);
         if (pf_on && bw >= 0 && bw != pf_w) {   // (wave-uniform)
           const unsigned long long* rp = gran + LUC_CROW + ((int64_t)par * LUC_MAXWG + bw) * LB * 2 + 4 * lane;
           pf0 = luc_get(rp);
@@ -600,17 +616,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
         }
         __builtin_amdgcn_s_sleep(1);
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double v2 = __shfl_xor(cv, o, 64);
-        const int i2 = __shfl_xor(ci, o, 64);
-        const int w2 = __shfl_xor(cw, o, 64);
-        if (lu_better(v2, i2, cv, ci)) {
-          cv = v2;
-          ci = i2;
-          cw = w2;
-        }
-      }
+      lu_wave_argmax(cv, ci, cw);
       // a row of 128 doubles as 256 granules: lane l takes columns 2l, 2l + 1
       auto stage = [&](const unsigned long long* rp, double* dst) {
         for (unsigned spins = 0; alive;) {
