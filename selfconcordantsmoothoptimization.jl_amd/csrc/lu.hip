@@ -1096,6 +1096,15 @@ static hipError_t lu_coop_attr() {   // the dynamic LDS above the 64 KiB default
   return done;
 }
 
+static int lu_device_cus() {   // compute units of the current device (per call: contexts may switch devices)
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return ncu;
+}
+
 static bool lu_coop_pf() {   // read per call (A/B): SCS_LU_COOP_PF=0 stages the pivot row only after the sweep
   const char* e = getenv("SCS_LU_COOP_PF");
   return !(e && e[0] == '0');
@@ -1138,8 +1147,11 @@ static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUA
   const int npass = R / 32, mode = lu_panel_mode();
   const int cnt = lu_coop_nt();
   const int64_t gco = ceil_div(h, (int64_t)(cnt / 2));
-  // (a runtime that refuses the dynamic-LDS attribute gets the step kernels)
-  const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG) && lu_coop_attr() == hipSuccess;
+  // (a runtime that refuses the dynamic-LDS attribute gets the step kernels, and so does a device with
+  // fewer than twice as many CUs as the panel needs workgroups -- a partitioned MI355X -- where they
+  // could not all be resident at once)
+  const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG) && 2 * gco <= lu_device_cus() &&
+                    lu_coop_attr() == hipSuccess;
   if (coop) {
     const bool wide = lu_coop_wide();
     auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
