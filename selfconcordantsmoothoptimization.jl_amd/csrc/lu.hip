@@ -83,13 +83,11 @@ __device__ __forceinline__ void lu_wave_argmax(double& v, int& i, int& w) {
 
 // (v, i) argmax over the workgroup (larger |a|, then smaller row); every thread gets the result.
 // sv / si hold NT / 64 entries.
-// GUARD = false: the caller guarantees a workgroup barrier between the previous call's reads of sv / si /
-// sw and this call (the cooperative panel: its post-sweep barrier), so the leading barrier goes.
-template <int NT = LU_NT, bool GUARD = true>
+template <int NT = LU_NT>
 __device__ __forceinline__ void lu_block_argmax(double& v, int& i, int& w, double* sv, int* si, int* sw) {
   lu_wave_argmax(v, i, w);
   const int wv = threadIdx.x >> 6;
-  if (GUARD) __syncthreads();
+  __syncthreads();
   if ((threadIdx.x & 63) == 0) {
     sv[wv] = v;
     si[wv] = i;
@@ -447,7 +445,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
                                                               int64_t c0, int64_t h, unsigned long long* gran,
                                                               unsigned tagbase,
                                                               int* ipiv, int* info, int2* pairs, int* npairs,
-                                                              int pf_on, int rowfirst) {
+                                                              int pf_on) {
   constexpr int RW = NT / 2, RP = NT / 8;   // rows per workgroup, rows per pass
   __shared__ double sv[NT / 64];
   __shared__ int si[NT / 64], sw[NT / 64];
@@ -494,8 +492,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
       }
     }
     int bw = g;
-    if (jn == 0) lu_block_argmax<NT>(bv, bi, bw, sv, si, sw);
-    else lu_block_argmax<NT, false>(bv, bi, bw, sv, si, sw);   // (column jn - 1's post-sweep barrier)
+    lu_block_argmax<NT>(bv, bi, bw, sv, si, sw);
     const int par = jn & 1;
     const unsigned tag = tagbase + (unsigned)(jn + 1);
     if (WIDE) {
@@ -542,7 +539,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
     }
     // the record after the rows (a barrier apart): a consumer that prefetches the best row so far
     // usually finds it landed (the tags decide either way)
-    if (!WIDE && rowfirst) __syncthreads();
+    if (!WIDE) __syncthreads();
     if (tid == 0) {
       const unsigned long long t = (unsigned long long)tag << 32;
       const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
@@ -1108,11 +1105,6 @@ static int lu_device_cus() {   // compute units of the current device (per call:
   return ncu;
 }
 
-static bool lu_coop_rowfirst() {   // read per call (A/B): SCS_LU_COOP_ROWFIRST=0 drops the barrier that puts
-  const char* e = getenv("SCS_LU_COOP_ROWFIRST");   // the rows' granules ahead of the record's
-  return !(e && e[0] == '0');
-}
-
 static bool lu_coop_pf() {   // read per call (A/B): SCS_LU_COOP_PF=0 stages the pivot row only after the sweep
   const char* e = getenv("SCS_LU_COOP_PF");
   return !(e && e[0] == '0');
@@ -1165,7 +1157,7 @@ static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUA
     auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
                            : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
     hipLaunchKernelGGL(kern, dim3((unsigned)gco), dim3(cnt), LUC_LDS, st, A, ld, r0, c0, h, a->gran, (unsigned)k << 8,
-                       a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k, lu_coop_pf() ? 1 : 0, lu_coop_rowfirst() ? 1 : 0);
+                       a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k, lu_coop_pf() ? 1 : 0);
   } else
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)
