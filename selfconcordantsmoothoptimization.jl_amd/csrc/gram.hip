@@ -92,6 +92,46 @@ __device__ __forceinline__ int bnd_next(unsigned* ctr, int ntiles, int* s) {
   return *s;
 }
 
+// The throughput kernels' epilogue for one 16-row MFMA tile row ti of a wave (4 x 4 accumulator
+// registers; the C/D map and placements below).  With GRAM_ACCUMULATE the old values are loaded TJC
+// 16-column tiles (4 TJC values) at a time before their stores: the compiler cannot prove the
+// destinations distinct, and in the persistent (BND) launches it otherwise paid one memory round trip
+// per element (64 per tile).  Same sums.  Only the BND forms use it: in the others the compiler
+// already overlaps the loads, and the helper's register use slowed the main Gram (C2 Gram phase
+// 92.1 -> 93.0 ms, profiles/r05/epi/).
+template <int TJC = 2>
+__device__ __forceinline__ void gram_tile_store_row(const v4d (&acc)[4], int ti, int wr, int wc, int g, int fl,
+                                                    int part, double* P, int GTI, int packed, int upper,
+                                                    int accumulate, double* G, int64_t ldg, int tix, int bi, int bj) {
+  auto addr = [&](int tj, int r) -> double* {
+    const int il = wr * 64 + 16 * ti + g + 4 * r;
+    const int jl = wc * 64 + 16 * tj + fl;
+    if (part >= 0) return P + ((int64_t)part * GT + jl) * GTI + il;
+    if (packed) return G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
+    if (upper) return G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
+    return G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
+  };
+  if (accumulate && part < 0) {
+#pragma unroll
+    for (int t0 = 0; t0 < 4; t0 += TJC) {
+      double old[TJC][4];
+#pragma unroll
+      for (int t = 0; t < TJC; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) old[t][r] = *addr(t0 + t, r);
+#pragma unroll
+      for (int t = 0; t < TJC; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) *addr(t0 + t, r) = old[t][r] + acc[t0 + t][r];
+    }
+  } else {
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) *addr(tj, r) = acc[tj][r];
+  }
+}
+
 template <bool NOLOAD, int TI, bool TILED = false, bool BND = false>
 __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_f64_kernel(
     const double* __restrict__ A1, int64_t lda1, const double* __restrict__ A2, int64_t lda2,
@@ -232,25 +272,31 @@ bnd_tile:
   //   upper  : G[(bi*128+i)*ldg + bj*128+j]       (transposed: row j, col i -- the
   //            upper triangle when bi >= bj; consecutive lanes store consecutive j)
   //   default: G[(bj*128+j)*ldg + bi*128+i]       (lower triangle when bi >= bj)
+  if constexpr (BND || !TILED) {   // the persistent and two-operand gen launches: old values loaded first
 #pragma unroll
-  for (int ti = 0; ti < 4; ++ti)
+    for (int ti = 0; ti < 4; ++ti)
+      gram_tile_store_row(acc[ti], ti, wr, wc, g, fl, part, P, GTI, packed, upper, accumulate, G, ldg, tix, bi, bj);
+  } else {
 #pragma unroll
-    for (int tj = 0; tj < 4; ++tj)
+    for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int il = wr * 64 + 16 * ti + g + 4 * r;
-        const int jl = wc * 64 + 16 * tj + fl;
-        double* dst;
-        if (part >= 0) {
-          P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
-          continue;
+      for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = wr * 64 + 16 * ti + g + 4 * r;
+          const int jl = wc * 64 + 16 * tj + fl;
+          double* dst;
+          if (part >= 0) {
+            P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
+            continue;
+          }
+          if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
+          else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
+          else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
+          if (accumulate) *dst += acc[ti][tj][r];
+          else *dst = acc[ti][tj][r];
         }
-        if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
-        else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
-        else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
-        if (accumulate) *dst += acc[ti][tj][r];
-        else *dst = acc[ti][tj][r];
-      }
+  }
   if constexpr (BND) {
     tix = bnd_next(reinterpret_cast<unsigned*>(P), ntiles, &s_claim);
     if (tix >= ntiles) return;
@@ -809,25 +855,31 @@ bnd_tile:
   }
 
   // epilogue (the C/D map of gram_f64_kernel): element (il, jl) of the GTI x 128 tile
+  if constexpr (BND || CM) {   // the persistent and gen-form launches: old values loaded ahead of the stores
 #pragma unroll
-  for (int ti = 0; ti < NTI; ++ti)
+    for (int ti = 0; ti < NTI; ++ti)
+      gram_tile_store_row(acc[ti], ti, wr, wc, g, fl, part, P, GTI, packed, upper, accumulate, G, ldg, tix, bi, bj);
+  } else {
 #pragma unroll
-    for (int tj = 0; tj < 4; ++tj)
+    for (int ti = 0; ti < NTI; ++ti)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int il = wr * 64 + 16 * ti + g + 4 * r;
-        const int jl = wc * 64 + 16 * tj + fl;
-        double* dst;
-        if (part >= 0) {
-          P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
-          continue;
+      for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = wr * 64 + 16 * ti + g + 4 * r;
+          const int jl = wc * 64 + 16 * tj + fl;
+          double* dst;
+          if (part >= 0) {
+            P[((int64_t)part * GT + jl) * GTI + il] = acc[ti][tj][r];
+            continue;
+          }
+          if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
+          else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
+          else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
+          if (accumulate) *dst += acc[ti][tj][r];
+          else *dst = acc[ti][tj][r];
         }
-        if (packed) dst = G + ((int64_t)tix * (GTI / GT) + il / GT) * GT * GT + jl * GT + (il % GT);
-        else if (upper) dst = G + ((int64_t)bi * GTI + il) * ldg + (int64_t)bj * GT + jl;
-        else dst = G + ((int64_t)bj * GT + jl) * ldg + (int64_t)bi * GTI + il;
-        if (accumulate) *dst += acc[ti][tj][r];
-        else *dst = acc[ti][tj][r];
-      }
+  }
   // strip completion (scsopt.cpp gram_factor_pipelined, one-launch mode): this tile's rows lie in
   // outer strip bj / sob; each thread's stores are released to device scope before one count
   if (!BND && scnt && part < 0) {

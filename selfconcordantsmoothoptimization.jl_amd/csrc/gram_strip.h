@@ -24,6 +24,47 @@ __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
 // the same.  Ai = the tile's A1 columns (feature f at Ai + f·lda1), Aj = the strip's A2
 // columns, Gt = the strip's output origin (element (0, 0) in the chosen placement), lds =
 // 2 (128 + QC) 16 doubles.
+// The strip epilogue: wave wr's 32 x 16 TJ accumulator block into Gt.  With GRAM_ACCUMULATE every old
+// value is loaded before the first store (the compiler cannot prove the 2 x TJ x 4 destinations
+// distinct and would otherwise pay one memory round trip per element); the sums are the same.
+template <int TJ>
+__device__ __forceinline__ void gram_strip_store(const v4d (&acc)[2][TJ], double* Gt, int64_t ldg, int wr, int g,
+                                                 int fl, int accumulate, int upper) {
+  double* dst[2][TJ][4];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t I = wr * 32 + 16 * ti + g + 4 * r;
+        const int64_t J = 16 * tj + fl;
+        dst[ti][tj][r] = upper ? Gt + I * ldg + J : Gt + J * ldg + I;
+      }
+  if (accumulate) {
+    double old[2][TJ][4];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) old[ti][tj][r] = *dst[ti][tj][r];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) *dst[ti][tj][r] = old[ti][tj][r] + acc[ti][tj][r];
+  } else {
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) *dst[ti][tj][r] = acc[ti][tj][r];
+  }
+}
+
 template <int QC>
 __device__ __forceinline__ void gram_small_strip(const double* __restrict__ Ai, int64_t lda1, const double* Aj,
                                                  int64_t lda2, const double* __restrict__ w, int64_t k0, int64_t Nk,
@@ -95,18 +136,7 @@ __device__ __forceinline__ void gram_small_strip(const double* __restrict__ Ai, 
       }
     }
   }
-#pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < TJ; ++tj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t I = wr * 32 + 16 * ti + g + 4 * r;
-        const int64_t J = 16 * tj + fl;
-        double* dst = upper ? Gt + I * ldg + J : Gt + J * ldg + I;
-        if (accumulate) *dst += acc[ti][tj][r];
-        else *dst = acc[ti][tj][r];
-      }
+  gram_strip_store<TJ>(acc, Gt, ldg, wr, g, fl, accumulate, upper);
 }
 
 }  // namespace scs
