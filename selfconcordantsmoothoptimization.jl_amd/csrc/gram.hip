@@ -640,7 +640,8 @@ __global__ __launch_bounds__(128 * TI, (TI == 2 ? 2 : 1)) void gram_sia_kernel(
     const double* __restrict__ A, int64_t S, const double* __restrict__ w, int64_t k0, int64_t Nk,
     const int2* __restrict__ tiles, int ntiles, double* __restrict__ G, int64_t ldg, int flags,
     const int4* __restrict__ work, int seglen, int nsplit, double* __restrict__ P,
-    const double* __restrict__ v, double* __restrict__ VP, int64_t vps, unsigned* __restrict__ scnt, int sob) {
+    const double* __restrict__ v, double* __restrict__ VP, int64_t vps, unsigned* __restrict__ scnt, int sob,
+    const double* __restrict__ A2, int64_t S2) {
   static_assert(!(AV && CM), "the fused Aᵀv runs on the panel-blocked A only");
   constexpr int GTI = 64 * TI;        // tile rows (A1 features)
   constexpr int NT = 128 * TI;        // threads
@@ -694,7 +695,11 @@ bnd_tile:
   // (GTI/128) bi + f/128) and of the A2 rows (panel bj), samples 2 sc, 2 sc + 1.
   const double* srcA = CM ? A + ((int64_t)bi * GTI + sf0) * S + k0 + 2 * sc
                           : A + ((int64_t)bi * (GTI / GT) * S + st0) * GT * GBK + sf0 * GBK + 2 * sc;
-  const double* srcB = CM ? A + ((int64_t)bj * GT + sf0) * S + k0 + 2 * sc
+  // CM with A2: the A2 panels from a second column-major matrix (leading dimension S2; the LU's and
+  // the QR's two-operand products, the Cholesky's strip solves), else from A
+  const double* B2 = (CM && A2) ? A2 : A;
+  const int64_t SB2 = (CM && A2) ? S2 : S;
+  const double* srcB = CM ? B2 + ((int64_t)bj * GT + sf0) * SB2 + k0 + 2 * sc
                           : A + ((int64_t)bj * S + st0) * GT * GBK + sf0 * GBK + 2 * sc;
   const double* srcW = w + k0 + 2 * sc;
   const double* srcV = AV ? v + k0 + 2 * sc : nullptr;
@@ -719,7 +724,7 @@ bnd_tile:
 #pragma unroll
       for (int i = 0; i < NA; ++i) ra[i] = *(const v2d*)(srcA + st * GBK + (int64_t)FS * i * S);
 #pragma unroll
-      for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + st * GBK + (int64_t)FS * i * S);
+      for (int i = 0; i < NB; ++i) rb[i] = *(const v2d*)(srcB + st * GBK + (int64_t)FS * i * SB2);
     } else {
       const int64_t so = st * GT * GBK;
 #pragma unroll
@@ -954,11 +959,11 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
     if (tall) {
       g_main_name = "gram_sia_kernel<1, 4, false, true, false>";
       hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0,
-                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
+                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0, nullptr, (int64_t)0);
     } else {
       g_main_name = "gram_sia_kernel<1, 2, false, true, false>";
       hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0,
-                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0);
+                         Nk, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, v, VP, vps, nullptr, 0, nullptr, (int64_t)0);
     }
     return hipGetLastError();
   }
@@ -969,11 +974,11 @@ hipError_t gram_launch(const double* A, int64_t lda, const double* w, int64_t Nk
   } else if (!tall) {
     g_main_name = "gram_sia_kernel<1, 2, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(ntiles), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
   } else if (gram_tall_mode() == 3) {
     g_main_name = "gram_sia_kernel<1, 4, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(ntiles), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
   } else {
     g_main_name = "gram_glds_kernel<true, 1>";
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(ntiles), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0, Nk,
@@ -1022,6 +1027,20 @@ hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, i
   return hipGetLastError();
 }
 
+// Two-operand column-major products (A1 != A2: the LU's TRSM and trailing updates, the QR's Vᵀ
+// products, the Cholesky's strip solves) on the interleaved-schedule kernel with its second operand
+// (r05; was the register-staged gram_f64_kernel: same MFMA order per tile, the same bits).
+// Only from K = 256 on: the interleaved pipeline's prologue does not pay on the K = 128 launches (the
+// Cholesky's strip solves: m = 16384 factor 32.2-32.5 -> 32.6-33.0 ms with them; the LU's K = 512
+// updates n = 16384 212.0 -> 207.8 ms, the QR's Vᵀ products n = 8192 95.9 -> 93.8 ms,
+// profiles/r05/sia2/).  SCS_GRAM_SIA2=0 restores gram_f64_kernel everywhere, 1 also for K = 128
+// (read per launch: A/B and the tests).
+static bool gram_sia2(int64_t K) {
+  const char* e = getenv("SCS_GRAM_SIA2");
+  if (gram_sia_mode() == 0 || (e && e[0] == '0')) return false;
+  return K >= 256 || (e && e[0] == '1');
+}
+
 // General form: operand panels from two matrices, K range [k0, k1), flags GRAM_*.
 hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                            int64_t k0, int64_t k1, const int2* tiles, int ntiles, double* G, int64_t ldg, int flags,
@@ -1040,7 +1059,10 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
   if (k1 - k0 <= 512 && (k1 - k0) % (8 * GBK) == 0 && k1 > k0 && ntiles <= small_max) return gram_launch_small(A1, lda1, A2, lda2, w, k0, k1, tiles, ntiles, G, ldg, flags, st);
   if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)   // the Cholesky's trailing updates
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
+  else if (gram_sia2(k1 - k0))   // two operands (LU TRSM / updates, strip solves): the interleaved kernel too
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, A2, lda2);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3(ntiles), dim3(256), 0, st, A1, lda1, A2, lda2, w, k0, k1,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -1051,6 +1073,12 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 // QR's Vᵀ products, qr.hip): every item's partial tile to P, slot-major; the caller combines.
 hipError_t gram_launch_work_cm(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                                int64_t K, const int4* work, int seglen, int nsplit, double* P, hipStream_t st) {
+  if (gram_sia2(K)) {
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3((unsigned)(8 * seglen)), dim3(256), 0, st, A1, lda1, w,
+                       (int64_t)0, K, nullptr, 0, nullptr, (int64_t)0, 0, work, seglen, nsplit, P, nullptr, nullptr,
+                       (int64_t)0, nullptr, 0, A2, lda2);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((gram_f64_kernel<false, 2>), dim3((unsigned)(8 * seglen)), dim3(256), 0, st, A1, lda1, A2, lda2, w,
                      (int64_t)0, K, nullptr, 0, nullptr, (int64_t)0, 0, work, seglen, nsplit, P);
   return hipGetLastError();
@@ -1079,7 +1107,11 @@ hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2,
   if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true, false, true>), dim3(grid), dim3(256), 0, st, A1, lda1, w, k0, k1,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, ctr,
-                       (int)skip);
+                       (int)skip, nullptr, (int64_t)0);
+  else if (gram_sia2(k1 - k0))
+    hipLaunchKernelGGL((gram_sia_kernel<1, 2, true, false, true>), dim3(grid), dim3(256), 0, st, A1, lda1, w, k0, k1,
+                       tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, ctr,
+                       (int)skip, A2, lda2);
   else
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, false, true>), dim3(grid), dim3(256), 0, st, A1, lda1, A2, lda2, w,
                        k0, k1, tiles, ntiles, G, ldg, flags, nullptr, (int)skip, 0, reinterpret_cast<double*>(ctr));
@@ -1092,13 +1124,13 @@ hipError_t gram_launch_ex(const double* A, int64_t lda, const double* w, int64_t
   const int flags = GRAM_UPPER | (accumulate ? GRAM_ACCUMULATE : 0);
   if (noload == 16 || noload == 17)   // 256 x 128 interleaved kernel (tall tile list): loaded / no-load
     hipLaunchKernelGGL((noload == 16 ? gram_sia_kernel<1, 4> : gram_sia_kernel<3, 4>), dim3(ntiles), dim3(512), 0,
-                       st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
+                       st, A, (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
   else if (noload == 12)
     hipLaunchKernelGGL((gram_sia_kernel<3>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, w, k0, k1, tiles,
-                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
+                       ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
   else if (noload == 9 || noload == 10)
     hipLaunchKernelGGL((noload == 9 ? gram_sia_kernel<1> : gram_sia_kernel<0>), dim3(ntiles), dim3(256), 0, st, A,
-                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0);
+                       (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
   else if (noload == 11)
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(ntiles), dim3(256), 0, st, A, (k1 - k0) / GBK, A,
                        (k1 - k0) / GBK, w, k0, k1, tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr);
@@ -1160,15 +1192,15 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
   if (v && tall) {
     g_main_name = "gram_sia_kernel<1, 4, false, true, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4, false, true>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w,
-                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob, nullptr, (int64_t)0);
   } else if (v) {
     g_main_name = "gram_sia_kernel<1, 2, false, true, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, false, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w,
-                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob);
+                       (int64_t)0, Nk, nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, v, VP, vps, scnt, sob, nullptr, (int64_t)0);
   } else if (tall && glds == 3) {
     g_main_name = "gram_sia_kernel<1, 4, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 4>), dim3(8 * seglen), dim3(512), 0, st, A, lda, w, (int64_t)0, Nk,
-                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
+                       nullptr, 0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob, nullptr, (int64_t)0);
   } else if (tall && glds == 2) {
     g_main_name = "gram_glds_kernel<true, 1>";
     hipLaunchKernelGGL((gram_glds_kernel<true, 1>), dim3(8 * seglen), dim3(512), 0, st, A, lda, A, lda, w, (int64_t)0,
@@ -1184,11 +1216,11 @@ hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int6
   } else if (gram_sia_mode() == 1) {
     g_main_name = "gram_sia_kernel<1, 2, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<1, 2>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr,
-                       0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
+                       0, G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob, nullptr, (int64_t)0);
   } else if (gram_sia_mode() == 2) {
     g_main_name = "gram_sia_kernel<0, 2, false, false, false>";
     hipLaunchKernelGGL((gram_sia_kernel<0>), dim3(8 * seglen), dim3(256), 0, st, A, lda, w, (int64_t)0, Nk, nullptr, 0,
-                       G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob);
+                       G, ldg, flags, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, scnt, sob, nullptr, (int64_t)0);
   } else {
     g_main_name = "gram_f64_kernel<false, 2, true, false>";
     hipLaunchKernelGGL((gram_f64_kernel<false, 2, true>), dim3(8 * seglen), dim3(256), 0, st, A, lda, A, lda, w,
@@ -1232,7 +1264,7 @@ hipError_t gram_launch_sched_cm(const double* X, int64_t ld, const double* w, in
                                 int flags, hipStream_t st) {
   if (seglen <= 0 || k1 <= k0) return hipSuccess;
   hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(8 * seglen), dim3(256), 0, st, X, ld, w, k0, k1, nullptr, 0,
-                     G, ldg, flags | GRAM_UPPER, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, nullptr, 0);
+                     G, ldg, flags | GRAM_UPPER, work, seglen, nsplit, P, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
   if (ncomb > 0)
     hipLaunchKernelGGL(gram_combine_kernel<2>, dim3(16, ncomb), dim3(256), 0, st, P, comb, nsplit, G, ldg,
                        (flags & GRAM_ACCUMULATE) ? 2 : 0);

@@ -1031,3 +1031,28 @@ def test_reference_solver_ill_conditioned():
     ec = float(np.max(np.abs(xc - xr))) / scale
     print(f"[qr] cond {cond:.2e}: max rel |x_QR - x_LAPACK-QR| = {eq:.2e}, Cholesky {ec:.2e}")
     assert eq <= 1e-13 * cond and ec <= 1e-13 * cond
+
+
+@pytest.mark.parametrize("sia2", ["", "1"])
+@pytest.mark.parametrize("m", [1000, 2304])
+def test_two_operand_interleaved_gram_bit_identical(m, sia2, monkeypatch):
+    """The two-operand column-major products (the LU's TRSM / updates, the QR's Vᵀ products and
+    trailing updates, the Cholesky's strip solves) on the interleaved-schedule kernel with a second
+    operand (gram_sia_kernel A2 / S2, r05) against the register-staged gram_f64_kernel
+    (SCS_GRAM_SIA2=0): the same MFMA order per tile, so every solver mode gives the same bits -- by
+    default (K >= 256 launches) and with SCS_GRAM_SIA2=1 (K = 128 ones too)."""
+    N = m + 300
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=53)
+    rng = np.random.default_rng(54)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-3
+    rhs = rng.standard_normal(m)
+    if sia2:
+        monkeypatch.setenv("SCS_GRAM_SIA2", sia2)
+    else:
+        monkeypatch.delenv("SCS_GRAM_SIA2", raising=False)
+    new = [p.solve_eval(w, d, rhs, mode=mode)[0] for mode in (0, 1, 2)]
+    monkeypatch.setenv("SCS_GRAM_SIA2", "0")
+    old = [p.solve_eval(w, d, rhs, mode=mode)[0] for mode in (0, 1, 2)]
+    for a, b in zip(new, old):
+        assert np.array_equal(bits(a), bits(b))
