@@ -1279,7 +1279,7 @@ hipError_t gram_launch_sched_cm(const double* X, int64_t ld, const double* w, in
 // length with no-op items.  Returns seglen; fills work (8*seglen), comb
 // (combine items), *ncomb, *nsplit, *npart (partial slots).
 int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<int4>& work, std::vector<int4>& comb,
-                  int* nsplit, int* npart) {
+                  int* nsplit, int* npart, int diag_first_gti) {
   const int q = ntiles / 8, r = ntiles % 8;
   // per-XCD tail and a common split factor
   int tail_max = 0;
@@ -1301,6 +1301,13 @@ int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<
       const int2 tl = tiles[t0 + i];
       seg[x].push_back(make_int4(tl.x, tl.y, -1, t0 + i));
     }
+    // diag_first_gti (r05): the whole tiles whose row block holds their column panel -- the tiles an
+    // AV launch gives the fused Aᵀv, the longer ones -- first in the XCD's order, so they run in its
+    // first round instead of lengthening the last (order only: every tile's bits are the same)
+    if (diag_first_gti > 0)
+      std::stable_partition(seg[x].begin(), seg[x].end(), [&](const int4& it) {
+        return it.x == (int)((int64_t)it.y * GT / diag_first_gti);
+      });
     for (int i = n - tail; i < n; ++i) {
       const int2 tl = tiles[t0 + i];
       comb.push_back(make_int4(tl.x, tl.y, t0 + i, pslot));

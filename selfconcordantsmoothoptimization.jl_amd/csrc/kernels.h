@@ -59,7 +59,7 @@ hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, i
 // Tail-balanced schedule of the main Gram (see gram.hip): work items (bi, bj, ks, idx),
 // combine items (bi, bj, tix, first partial slot)
 int gram_schedule(const int2* tiles, int ntiles, int slots_per_xcd, std::vector<int4>& work, std::vector<int4>& comb,
-                  int* nsplit, int* npart);
+                  int* nsplit, int* npart, int diag_first_gti = 0);
 hipError_t gram_launch_sched(const double* A, int64_t lda, const double* w, int64_t Nk, const int4* work, int seglen,
                              int nsplit, const int4* comb, int ncomb, double* P, double* G, int64_t ldg, int packed,
                              int tall, hipStream_t st, const double* v = nullptr, double* VP = nullptr,

@@ -713,7 +713,12 @@ void ensure_gram(scs_ctx* c) {
     if (!(ev && ev[0] == '0')) {
       std::vector<int4> wk, cb;
       int npart = 0;
-      c->gseglen = gram_schedule(tl.data(), nt, 32 * (c->tall ? 1 : 2), wk, cb, &c->gnsplit, &npart);
+      // the AV launches' designated tiles first in each XCD's order on 256 x 128 tiles (C3 Gram
+      // 3863.7 -> 3846.6 ms); on 128 x 128 tiles it measured slower (C2 Gram +0.3 ms unfused, +0.9 fused;
+      // profiles/r05/diagfirst/).  SCS_GRAM_DIAGFIRST=0 / 1: off / also on 128 x 128 tiles (A/B)
+      const char* df = std::getenv("SCS_GRAM_DIAGFIRST");
+      const int dfg = (df && df[0] == '0') ? 0 : c->tall ? 256 : (df && df[0] == '1') ? 128 : 0;
+      c->gseglen = gram_schedule(tl.data(), nt, 32 * (c->tall ? 1 : 2), wk, cb, &c->gnsplit, &npart, dfg);
       c->gncomb = (int)cb.size();
       c->gwork = dalloc<int4>(c, wk.size());
       HCK(hipMemcpyAsync(c->gwork, wk.data(), sizeof(int4) * wk.size(), hipMemcpyHostToDevice, c->st));
