@@ -1030,15 +1030,17 @@ hipError_t gram_launch_small(const double* A1, int64_t lda1, const double* A2, i
 // Two-operand column-major products (A1 != A2: the LU's TRSM and trailing updates, the QR's Vᵀ
 // products, the Cholesky's strip solves) on the interleaved-schedule kernel with its second operand
 // (r05; was the register-staged gram_f64_kernel: same MFMA order per tile, the same bits).
-// Only from K = 256 on: the interleaved pipeline's prologue does not pay on the K = 128 launches (the
-// Cholesky's strip solves: m = 16384 factor 32.2-32.5 -> 32.6-33.0 ms with them; the LU's K = 512
-// updates n = 16384 212.0 -> 207.8 ms, the QR's Vᵀ products n = 8192 95.9 -> 93.8 ms,
-// profiles/r05/sia2/).  SCS_GRAM_SIA2=0 restores gram_f64_kernel everywhere, 1 also for K = 128
-// (read per launch: A/B and the tests).
-static bool gram_sia2(int64_t K) {
+// From K = 256 on, and at K = 128 (the Cholesky's strip solves) only in factors with ld >= 32768:
+// there the launches are large enough (m = 32768 factor 191.7-194.2 -> 187.7-190.8 ms, the m = 65536
+// solve of the C5-shaped GGN step 1420-1426 -> 1414-1420 ms, profiles/r05/sia2k128/), while at
+// m = 16384 the interleaved pipeline's prologue did not pay (factor 32.2-32.5 -> 32.6-33.0 ms).  The
+// LU's K = 512 updates: n = 16384 212.0 -> 207.8 ms; the QR's Vᵀ products: n = 8192 95.9 -> 93.8 ms
+// (profiles/r05/sia2/).  SCS_GRAM_SIA2=0 restores gram_f64_kernel everywhere, 1 takes the
+// interleaved kernel for every two-operand launch (read per launch: A/B and the tests).
+static bool gram_sia2(int64_t K, int64_t ld) {
   const char* e = getenv("SCS_GRAM_SIA2");
   if (gram_sia_mode() == 0 || (e && e[0] == '0')) return false;
-  return K >= 256 || (e && e[0] == '1');
+  return K >= 256 || ld >= 32768 || (e && e[0] == '1');
 }
 
 // General form: operand panels from two matrices, K range [k0, k1), flags GRAM_*.
@@ -1060,7 +1062,7 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
   if (A1 == A2 && lda1 == lda2 && gram_sia_mode() != 0)   // the Cholesky's trailing updates
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, nullptr, (int64_t)0);
-  else if (gram_sia2(k1 - k0))   // two operands (LU TRSM / updates, strip solves): the interleaved kernel too
+  else if (gram_sia2(k1 - k0, lda2))   // two operands (LU TRSM / updates, strip solves): the interleaved kernel too
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3(ntiles), dim3(256), 0, st, A1, lda1, w, k0, k1, tiles,
                        ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, nullptr, 0, A2, lda2);
   else
@@ -1073,7 +1075,7 @@ hipError_t gram_launch_gen(const double* A1, int64_t lda1, const double* A2, int
 // QR's Vᵀ products, qr.hip): every item's partial tile to P, slot-major; the caller combines.
 hipError_t gram_launch_work_cm(const double* A1, int64_t lda1, const double* A2, int64_t lda2, const double* w,
                                int64_t K, const int4* work, int seglen, int nsplit, double* P, hipStream_t st) {
-  if (gram_sia2(K)) {
+  if (gram_sia2(K, lda2)) {
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true>), dim3((unsigned)(8 * seglen)), dim3(256), 0, st, A1, lda1, w,
                        (int64_t)0, K, nullptr, 0, nullptr, (int64_t)0, 0, work, seglen, nsplit, P, nullptr, nullptr,
                        (int64_t)0, nullptr, 0, A2, lda2);
@@ -1108,7 +1110,7 @@ hipError_t gram_launch_bounded(const double* A1, int64_t lda1, const double* A2,
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true, false, true>), dim3(grid), dim3(256), 0, st, A1, lda1, w, k0, k1,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, ctr,
                        (int)skip, nullptr, (int64_t)0);
-  else if (gram_sia2(k1 - k0))
+  else if (gram_sia2(k1 - k0, lda2))
     hipLaunchKernelGGL((gram_sia_kernel<1, 2, true, false, true>), dim3(grid), dim3(256), 0, st, A1, lda1, w, k0, k1,
                        tiles, ntiles, G, ldg, flags, nullptr, 0, 0, nullptr, nullptr, nullptr, (int64_t)0, ctr,
                        (int)skip, A2, lda2);
