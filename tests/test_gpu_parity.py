@@ -1056,3 +1056,28 @@ def test_two_operand_interleaved_gram_bit_identical(m, sia2, monkeypatch):
     old = [p.solve_eval(w, d, rhs, mode=mode)[0] for mode in (0, 1, 2)]
     for a, b in zip(new, old):
         assert np.array_equal(bits(a), bits(b))
+
+
+def test_gram_work_order_bit_identical(monkeypatch):
+    """The main Gram's work order on 256 x 128 tiles puts the fused-Aᵀv tiles first in each XCD's list
+    (gram_schedule diag_first_gti, r05): an order change only, so G entries (diagonal-tile and
+    off-diagonal) and the fused Aᵀv are the bits of the list order (SCS_GRAM_DIAGFIRST=0)."""
+    N, m = 1024, 12288   # nb = 96: the 256 x 128 tile path
+    rng = np.random.default_rng(61)
+    w = rng.random(N) + 0.1
+    v = rng.standard_normal(N)
+    pairs = np.concatenate([rng.integers(0, m, size=(64, 2)),
+                            np.stack([np.arange(0, m, 97), np.arange(0, m, 97)], axis=1),
+                            np.array([[0, 255], [128, 255], [256, 383], [m - 1, m - 128]])])
+    out = []
+    for df in (None, "0"):
+        if df is None:
+            monkeypatch.delenv("SCS_GRAM_DIAGFIRST", raising=False)
+        else:
+            monkeypatch.setenv("SCS_GRAM_DIAGFIRST", df)
+        p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=63)
+        out.append(p.gram_atv_sample(w, v, pairs))
+        p.ctx.close()
+    (g1, a1, f1), (g0, a0, f0) = out
+    assert f1 and f0
+    assert np.array_equal(bits(g1), bits(g0)) and np.array_equal(bits(a1), bits(a0))
