@@ -326,8 +326,50 @@ __global__ __launch_bounds__(256) void gemv_t_kernel(const double* __restrict__ 
   }
 }
 
+// Aᵀ v by panels (r05): one workgroup per (4096-row chunk, 128-feature panel) streams the panel's
+// stage blocks (128 features x 16 samples, 16 KiB contiguous) in address order, 4 KiB per sweep: thread
+// (f0, sc) takes features f0 + 32 k, samples 2 sc, 2 sc + 1 of every stage, then the 8 lanes of a
+// feature sum in a fixed butterfly.  The column-group kernel above reads each block as 2 x 4 x 4
+// scattered 512-B pieces (C2: 1.37 ms per pass, 4.8 TB/s).  SCS_GEMV_T=0: the column-group kernel.
+__global__ __launch_bounds__(256) void gemv_t_panel_kernel(const double* __restrict__ A, int64_t S, int64_t Npad,
+                                                           int64_t m, const double* __restrict__ v,
+                                                           double* __restrict__ part, int64_t ldp) {
+  const int64_t r0 = (int64_t)blockIdx.x * GT_ROWS;
+  const int ns = (int)(((Npad - r0 < GT_ROWS) ? Npad - r0 : GT_ROWS) / 16);   // Npad % 16 == 0
+  const int tid = threadIdx.x, sc = tid & 7, f0 = tid >> 3;
+  const double* blk = A + ((int64_t)blockIdx.y * S + r0 / 16) * (128 * 16) + f0 * 16 + 2 * sc;
+  const double* vp = v + r0 + 2 * sc;
+  v2d acc[4] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+#pragma unroll 4
+  for (int s = 0; s < ns; ++s) {
+    const v2d vv = *(const v2d*)(vp + 16 * s);
+    const double* b = blk + (int64_t)s * (128 * 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += *(const v2d*)(b + 32 * 16 * k) * vv;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double t = acc[k][0] + acc[k][1];
+    t += __shfl_xor(t, 1);
+    t += __shfl_xor(t, 2);
+    t += __shfl_xor(t, 4);
+    const int64_t j = (int64_t)blockIdx.y * 128 + f0 + 32 * k;
+    if (sc == 0 && j < m) part[(int64_t)blockIdx.x * ldp + j] = t;
+  }
+}
+
+static bool gemv_t_panel() {   // read per launch (A/B)
+  const char* e = getenv("SCS_GEMV_T");
+  return !(e && e[0] == '0');
+}
+
 hipError_t launch_gemv_t(const double* A, int64_t S, int64_t Npad, int64_t m, int64_t mpad, const double* v,
                          double* part, hipStream_t st) {
+  if (gemv_t_panel()) {
+    hipLaunchKernelGGL(gemv_t_panel_kernel, dim3((unsigned)gemv_t_chunks(Npad), (unsigned)ceil_div(m, 128)), dim3(256),
+                       0, st, A, S, Npad, m, v, part, mpad);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(gemv_t_kernel, dim3((unsigned)gemv_t_chunks(Npad), (unsigned)ceil_div(m, 64)), dim3(256), 0, st,
                      A, S, Npad, m, v, part, mpad);
   return hipGetLastError();

@@ -30,7 +30,9 @@ import scsopt
 from scsopt import losses, shard
 mode, method = sys.argv[2], sys.argv[3]
 torch.cuda.set_device(0)
-dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+# one rank: a FileStore rendezvous (no TCP port to race other jobs on the host for)
+store = dist.FileStore(sys.argv[4], 1)
+dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", 0))
 N, m = {"ggn_sample": (151, 192), "ggn_sparse": (4096, 256)}.get(method, (3001, 256))
 x0 = np.random.default_rng(1234).standard_normal(m)
 if method in ("ggn", "ggn_sample"):
@@ -69,11 +71,12 @@ def _port():
 
 @pytest.mark.parametrize("mode", ["rccl", "torch"])
 @pytest.mark.parametrize("method", ["ggn", "nscore", "lqn", "ggn_sample", "ggn_sparse"])
-def test_forced_exchange_bit_identical(mode, method):
+def test_forced_exchange_bit_identical(mode, method, tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
     pkg = os.path.join(ROOT, "selfconcordantsmoothoptimization.jl_amd")
-    out = subprocess.run([sys.executable, "-c", _CHILD, pkg, mode, method], env=env, capture_output=True, text=True,
-                         timeout=240)
+    store = str(tmp_path / "store")
+    out = subprocess.run([sys.executable, "-c", _CHILD, pkg, mode, method, store], env=env, capture_output=True,
+                         text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
     import json
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("RESULT ")][-1]

@@ -8,7 +8,6 @@ problem to fp64 tolerance (only the reduction order differs) and be identical
 on both ranks.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -21,14 +20,6 @@ NS = 151          # sample-space case: N + 1 <= M
 METHODS = ("ggn", "nscore", "lqn", "ggn_ls_cached", "ggn_sample", "ggn_batch", "nscore_batch_ordered",
            "ggn_sample_batch", "ggn_ls_gl", "ggn_sample_rebatch")
 GS = 32           # ggn_ls_gl: C4's sparse-group lasso (groups of 32) on the row shards
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _run(method, comm=None):
@@ -101,16 +92,16 @@ def _run(method, comm=None):
     return {"obj": list(sol.obj), "x": sol.x.copy(), "epochs": sol.epochs}
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, store_path, out):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "selfconcordantsmoothoptimization.jl_amd"))
     import torch
     import torch.distributed as dist
     from scsopt import shard
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a FileStore rendezvous: no TCP port to race the host's other jobs for (a free port picked
+    # and released can be taken before rank 0 listens on it: EADDRINUSE)
+    dist.init_process_group("gloo", store=dist.FileStore(store_path, world), rank=rank, world_size=world)
     res = {}
     for method in METHODS:
         comm = shard.Comm(device=torch.device("cuda", 0))
@@ -120,7 +111,7 @@ def _worker(rank, world, port, out):
 
 
 @pytest.mark.parametrize("world,tall", [(2, "0"), (2, "1"), (4, "1")])
-def test_two_rank_shard_matches_single_process(world, tall, monkeypatch):
+def test_two_rank_shard_matches_single_process(world, tall, monkeypatch, tmp_path):
     """tall = "1" forces the 256 x 128 Gram kernel (the C3 kernel) at this small m, so the packed
     multi-rank slots of its tile halves (gram_unpack) are exercised too; world = 4 splits the 3001
     rows unevenly (751/750/750/750) and the 151-row sample-space case into 38/38/38/37.  The
@@ -129,7 +120,7 @@ def test_two_rank_shard_matches_single_process(world, tall, monkeypatch):
     monkeypatch.setenv("SCS_GRAM_TALL", tall)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, str(tmp_path / "store"), out), nprocs=world, join=True)
     for method in METHODS:
         full = _run(method)
         r0 = out[0][method]
