@@ -187,15 +187,23 @@ int scs_set_reduce_buffer(scs_ctx* ctx, void* dev_ptr, int64_t ndoubles);
  *                     q = its eigenvalues), which leaves JᵀQJ, Jᵀr and the sample-space
  *                     system of ggn_score_step unchanged (ProxGGNSCORE; multi-output targets
  *                     ny > 1 are n = N·ny rows)
+ *         SCS_CB_GRAD_X out[0..m) = grad_fx(x) called with x ALONE: ProxGGNSCORE builds
+ *                     grad_f = x -> model.grad_fx(x) (prox-GGN-SCORE.jl:58-59) and its ss_type 3
+ *                     line search calls it (:83-84, utils.jl:31).  A data problem's
+ *                     grad_fx(A, y, x) has no one-argument method: return SCS_CB_NO_METHOD and
+ *                     the calling function fails with SCS_ERR_REF "MethodError: no method
+ *                     matching grad_fx(::Vector{Float64})", the reference's error
  * x (m) and out are host arrays owned by the library, valid for the call; return 0 on
- * success, anything else fails the calling ABI function with SCS_ERR_CALLBACK.  There is no
- * automatic differentiation on this path: ProxNSCORE needs SCS_CB_HESS, ProxGGNSCORE
- * ggn_rows > 0.                                                                            */
+ * success, SCS_CB_NO_METHOD as above, anything else fails the calling ABI function with
+ * SCS_ERR_CALLBACK.  There is no automatic differentiation on this path: ProxNSCORE needs
+ * SCS_CB_HESS, ProxGGNSCORE ggn_rows > 0.                                                  */
 #define SCS_CB_F 0
 #define SCS_CB_GRAD 1
 #define SCS_CB_HESS 2
 #define SCS_CB_GGN 3
 #define SCS_CB_FTEST 4
+#define SCS_CB_GRAD_X 5
+#define SCS_CB_NO_METHOD 2
 typedef int (*scs_loss_fn)(void* user, int what, const double* x, int64_t m, double* out);
 int scs_set_loss_callback(scs_ctx* ctx, scs_loss_fn fn, void* user, int64_t ggn_rows);
 

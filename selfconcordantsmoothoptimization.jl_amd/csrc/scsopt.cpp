@@ -1143,6 +1143,10 @@ double* cb_eval(scs_ctx* c, int what, const double* xh, const double* xd, size_t
     sync(c);
   }
   const int rc = c->cb(c->cb_user, what, xb, m, xb + m);
+  if (rc == SCS_CB_NO_METHOD && what == SCS_CB_GRAD_X)   // prox-GGN-SCORE.jl:59 called grad_fx(x)
+    fail(c, SCS_ERR_REF, "MethodError: no method matching grad_fx(::Vector{Float64}) (ProxGGNSCORE calls "
+                         "model.grad_fx(x) with one argument in its ss_type 3 line search, "
+                         "prox-GGN-SCORE.jl:58-59,83-84)");
   if (rc != 0) fail(c, SCS_ERR_CALLBACK, "loss callback (what = %d) returned %d", what, rc);
   return xb + m;
 }
@@ -1205,13 +1209,14 @@ double eval_ftest_dev(scs_ctx* c, const double* xh, const double* xd) {
 }
 
 // ∇f(x) -> out (device)
-void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
+// (cb_what: SCS_CB_GRAD = grad_fx(A, y, x); SCS_CB_GRAD_X = ProxGGNSCORE's one-argument call)
+void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out, int cb_what = SCS_CB_GRAD) {
   if (c->gfix) {   // step!(...; ∇fx): grad_f = x -> ∇fx at every point (prox-L-BFGS-SCORE.jl:98-100)
     if (out != c->gfix) HCK(hipMemcpyAsync(out, c->gfix, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
     return;
   }
   if (c->loss == SCS_LOSS_CALLBACK) {
-    const double* g = cb_eval(c, SCS_CB_GRAD, xh, xd, c->m);
+    const double* g = cb_eval(c, cb_what, xh, xd, c->m);
     HCK(hipMemcpyAsync(out, g, sizeof(double) * c->m, hipMemcpyHostToDevice, c->st));
     return;
   }
@@ -1233,15 +1238,18 @@ void grad_f_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
 }
 
 // ∇q(x) = ∇f(x) + λ hμ.grad(x) -> out (device); uses the 2-slot cache.
-void grad_q_dev(scs_ctx* c, const double* xh, const double* xd, double* out) {
-  for (int s = 0; s < 2; ++s)
+void grad_q_dev(scs_ctx* c, const double* xh, const double* xd, double* out, int cb_what = SCS_CB_GRAD) {
+  // (a one-argument grad_fx call is always made: a cached grad_fx(A, y, x) must not stand in for it)
+  const bool cacheable = !(c->loss == SCS_LOSS_CALLBACK && cb_what == SCS_CB_GRAD_X);
+  for (int s = 0; s < 2 && cacheable; ++s)
     if (c->gvalid[s] && key_hit(c, c->gkey[s], c->gtag[s], xh)) {
       HCK(hipMemcpyAsync(out, c->gcache[s], sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
       return;
     }
-  grad_f_dev(c, xh, xd, c->gtmp);
+  grad_f_dev(c, xh, xd, c->gtmp, cb_what);
   HCK(launch_smoother(c->smooth, xd, c->m, c->mu, c->slb, c->sub, c->wel, c->zb, c->hinv, c->st));
   HCK(launch_axpby(c->gtmp, c->lam, c->zb, c->m, out, c->st));
+  if (!cacheable) return;
   const int s = c->gnext;
   c->gnext ^= 1;
   HCK(hipMemcpyAsync(c->gcache[s], out, sizeof(double) * c->m, hipMemcpyDeviceToDevice, c->st));
@@ -1272,7 +1280,9 @@ bool ls_incremental(const scs_ctx* c) {
 
 double line_search(scs_ctx* c, const double* xh, const double* xd, const double* dd) {
   const double f0 = eval_f_dev(c, xh, xd) + eval_reg_dev(c, xd);
-  grad_q_dev(c, xh, xd, c->gqn);
+  // ProxGGNSCORE's grad_f is x -> model.grad_fx(x), one argument (prox-GGN-SCORE.jl:58-59,83-84):
+  // a callback loss is asked for that call (a data problem's grad_fx(A, y, x) raises MethodError)
+  grad_q_dev(c, xh, xd, c->gqn, c->method == SCS_PROX_GGNSCORE ? SCS_CB_GRAD_X : SCS_CB_GRAD);
   HCK(launch_dot(c->gqn, dd, c->m, c->scal + 11, c->st));
   d2h(c, c->hscal + 11, c->scal + 11, 1);
   sync(c);

@@ -24,9 +24,18 @@ const LOSS = Dict(:logistic_margin => 1, :logistic_ce => 2, :least_squares => 3,
 const GGN = Dict(nothing => 0, :sigmoid_ce => 1, :linear_ls => 2)
 const REG = Dict("l1" => 1, "l2" => 2, "indbox" => 3, "gl" => 4)
 const SCS_ERR_REF = 5
+const SCS_ERR_CALLBACK = 7
+
+# the exception a loss callback raised on the host (the trampoline cannot throw through C):
+# rethrown by chk, so a user error or the reference's MethodError reaches the caller as itself
+const CB_EXCEPTION = Ref{Any}(nothing)
 
 function chk(rc::Integer, ctx::Ptr{Cvoid})
     rc == 0 && return nothing
+    if (rc == SCS_ERR_CALLBACK || rc == SCS_ERR_REF) && CB_EXCEPTION[] !== nothing
+        err, CB_EXCEPTION[] = CB_EXCEPTION[], nothing
+        throw(err)
+    end
     msg = unsafe_string(ccall((:scs_last_error, lib), Cstring, (Ptr{Cvoid},), ctx))
     error(msg)   # SCS_ERR_REF carries the reference's own Base.error text
 end
@@ -222,13 +231,20 @@ function loss_trampoline(user::Ptr{Cvoid}, what::Cint, xp::Ptr{Float64}, m::Int6
             ggn_pieces!(unsafe_wrap(Array, outp, cbs.nout * (m + 2)), cbs, x)
         elseif what == 4                                   # SCS_CB_FTEST (iterate.jl:173)
             unsafe_store!(outp, Float64(cbs.f(cbs.test..., x)))
+        elseif what == 5                                   # SCS_CB_GRAD_X: ProxGGNSCORE's grad_f =
+            cbs.grad_fx === nothing && error("this method needs grad_fx (no automatic differentiation on the device path)")
+            if !applicable(cbs.grad_fx, x)                 # x -> model.grad_fx(x) (prox-GGN-SCORE.jl:58-59)
+                CB_EXCEPTION[] = MethodError(cbs.grad_fx, (x,))
+                return Cint(2)                             # SCS_CB_NO_METHOD -> SCS_ERR_REF
+            end
+            copyto!(unsafe_wrap(Array, outp, m), cbs.grad_fx(x))
         else
             cbs.hess_fx === nothing && error("ProxNSCORE needs hess_fx (no automatic differentiation on the device path)")
             copyto!(unsafe_wrap(Array, outp, m * m), vec(Matrix{Float64}(cbs.hess_fx(args...))))   # column-major
         end
         return Cint(0)
     catch err
-        @error "loss callback failed" exception = (err, catch_backtrace())
+        CB_EXCEPTION[] = err
         return Cint(1)
     end
 end

@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("SCSOPT_LIB", os.path.join(_HERE, "libscsopt.so"))
 
 SCS_OK, SCS_ERR_ARG, SCS_ERR_HIP, SCS_ERR_SOLVE, SCS_ERR_STATE, SCS_ERR_REF, SCS_ERR_COMM, SCS_ERR_CALLBACK = range(8)
 SCS_MULTI_HOST_EXCHANGE = 1   # scs_create_multi_ex flag
-SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS, SCS_CB_GGN, SCS_CB_FTEST = range(5)
+SCS_CB_F, SCS_CB_GRAD, SCS_CB_HESS, SCS_CB_GGN, SCS_CB_FTEST, SCS_CB_GRAD_X = range(6)
+SCS_CB_NO_METHOD = 2   # a callback's answer to SCS_CB_GRAD_X when grad_fx takes no single argument
 
 LOSS = {"logistic_margin": 1, "logistic_ce": 2, "least_squares": 3, "quadratic": 4, "rosenbrock": 5, "callback": 6}
 GGN = {None: 0, "sigmoid_ce": 1, "linear_ls": 2}

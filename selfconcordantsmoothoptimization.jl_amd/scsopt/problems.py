@@ -24,6 +24,19 @@ from .smoothers import Smoother, bounds_array
 log = logging.getLogger("scsopt")
 
 
+def _accepts_one_arg(fn):
+    """Whether fn(x) binds: the Python reading of Julia's `applicable(grad_fx, x)` (a callable
+    whose signature cannot be inspected is taken at its word and called)."""
+    import inspect
+    try:
+        inspect.signature(fn).bind(None)
+    except TypeError:
+        return False
+    except ValueError:
+        return True
+    return True
+
+
 @dataclass
 class GetP:
     """get_P(n, G, ind) (prox-reg-utils.jl:9-62): group structure for "gl".
@@ -267,6 +280,17 @@ class Problem:
                         raise ValueError("this method needs grad_fx: the device path has no automatic "
                                          "differentiation (the reference's ForwardDiff default)")
                     g = np.asarray(f.grad_fx(*args(x)), dtype=np.float64).reshape(m)
+                    np.ctypeslib.as_array(outp, shape=(m,))[:] = g
+                elif what == _lib.SCS_CB_GRAD_X:
+                    # ProxGGNSCORE: grad_f = x -> model.grad_fx(x), ONE argument (prox-GGN-SCORE.jl:58-59),
+                    # reached from its ss_type 3 line search (:83-84): Julia's MethodError when the
+                    # user's grad_fx has no one-argument method (a data problem's grad_fx(A, y, x))
+                    if f.grad_fx is None:
+                        raise ValueError("this method needs grad_fx: the device path has no automatic "
+                                         "differentiation (the reference's ForwardDiff default)")
+                    if not _accepts_one_arg(f.grad_fx):
+                        return _lib.SCS_CB_NO_METHOD
+                    g = np.asarray(f.grad_fx(x), dtype=np.float64).reshape(m)
                     np.ctypeslib.as_array(outp, shape=(m,))[:] = g
                 elif what == _lib.SCS_CB_HESS:
                     if f.hess_fx is None:

@@ -246,3 +246,48 @@ def test_ggn_callback_multioutput_softmax_vs_oracle(N, d):
     assert sol.epochs == osol.epochs
     np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
     np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("device_loop", [False, True])
+def test_ggn_callback_ss3_grad_fx_one_argument(device_loop):
+    """ProxGGNSCORE builds grad_f = x -> model.grad_fx(x) with ONE argument
+    (prox-GGN-SCORE.jl:58-59) and its ss_type 3 line search calls it (:83-84, utils.jl:31).  A
+    data problem's grad_fx(A, y, x) has no such method: the reference raises MethodError, and so
+    do the oracle and the device path (SCS_ERR_REF through SCS_CB_GRAD_X), in the host loop and in
+    scs_iterate_ex.  A grad_fx that does take x alone is called as the reference calls it: the
+    trajectory then matches the oracle (rtol 1e-8).  ss_type 1 never calls grad_f: unchanged."""
+    rng = np.random.default_rng(13)
+    N, m = 200, 24
+    A = rng.standard_normal((N, m)) / np.sqrt(m)
+    y = (rng.random(N) < 1.0 / (1.0 + np.exp(-A @ rng.standard_normal(m)))).astype(np.float64)
+    x0 = rng.standard_normal(m) * 0.2
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    cb3 = _sigmoid_ce_cbs(N)                                   # grad_fx(A, y, x)
+    p3 = scsopt.Problem(A, y, x0, cb3, 2e-3)
+    with pytest.raises(scsopt.ScsReferenceError, match=r"MethodError: no method matching grad_fx\(::Vector"):
+        scsopt.iterate(scsopt.ProxGGNSCORE(ss_type=3), p3, "l1", hm, max_epoch=3, verbose=0,
+                       device_loop=device_loop)
+    ocb3 = O.CallbackLoss(cb3.f, cb3.grad_fx, out_fn=cb3.out_fn, jac_yx=cb3.jac_yx, grad_fy=cb3.grad_fy,
+                          hess_fy=cb3.hess_fy)
+    with pytest.raises(O.MethodError):
+        O.iterate(O.ProxGGNSCORE(ss_type=3), O.Problem(A, y, x0, ocb3, 2e-3), "l1", O.PHuberSmootherL1L2(1.0),
+                  max_epoch=3)
+    # the same problem at ss_type 1: grad_f is never called (the existing GGN callback path)
+    s1 = scsopt.iterate(scsopt.ProxGGNSCORE(ss_type=1), p3, "l1", hm, max_epoch=3, verbose=0,
+                        device_loop=device_loop)
+    o1 = O.iterate(O.ProxGGNSCORE(ss_type=1), O.Problem(A, y, x0, ocb3, 2e-3), "l1", O.PHuberSmootherL1L2(1.0),
+                   max_epoch=3)
+    np.testing.assert_allclose(s1.obj, o1.obj, rtol=1e-8)
+
+    # a one-argument grad_fx (a closure over the data) is applicable: the line search runs
+    def g1(x):
+        return cb3.grad_fx(A, y, x)
+    cb1 = losses.callback(cb3.f, g1, out_fn=cb3.out_fn, jac_yx=cb3.jac_yx, grad_fy=cb3.grad_fy, hess_fy=cb3.hess_fy)
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(ss_type=3), scsopt.Problem(A, y, x0, cb1, 2e-3), "l1", hm,
+                         max_epoch=4, verbose=0, device_loop=device_loop)
+    ocb1 = O.CallbackLoss(cb3.f, g1, out_fn=cb3.out_fn, jac_yx=cb3.jac_yx, grad_fy=cb3.grad_fy, hess_fy=cb3.hess_fy)
+    osol = O.iterate(O.ProxGGNSCORE(ss_type=3), O.Problem(A, y, x0, ocb1, 2e-3), "l1", O.PHuberSmootherL1L2(1.0),
+                     max_epoch=4)
+    assert sol.epochs == osol.epochs
+    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8)
+    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-10)

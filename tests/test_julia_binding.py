@@ -169,3 +169,20 @@ def test_integration_doc_matches_module():
             assert _compatible(a, ct), (name, a, ct)
         n += 1
     assert n >= 5
+
+
+def test_ggn_grad_fx_one_argument_request():
+    """the trampoline answers SCS_CB_GRAD_X (5) by calling grad_fx(x) with x
+    alone when applicable (prox-GGN-SCORE.jl:58-59), else stores Julia's own MethodError and returns
+    SCS_CB_NO_METHOD (2); chk rethrows a stored callback exception instead of a text error."""
+    src = open(JL).read()
+    hdr = open(os.path.join(ROOT, "include", "scsopt.h")).read()
+    assert re.search(r"#define SCS_CB_GRAD_X 5\b", hdr) and re.search(r"#define SCS_CB_NO_METHOD 2\b", hdr)
+    tr = src[src.index("function loss_trampoline("):]
+    tr = tr[:tr.index("\nend\n")]
+    assert "what == 5" in tr and "applicable(cbs.grad_fx, x)" in tr
+    assert "MethodError(cbs.grad_fx, (x,))" in tr and "return Cint(2)" in tr
+    assert "cbs.grad_fx(x)" in tr
+    ck = src[src.index("function chk("):]
+    ck = ck[:ck.index("\nend\n")]
+    assert "CB_EXCEPTION[]" in ck and "throw(err)" in ck

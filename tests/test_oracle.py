@@ -265,3 +265,45 @@ def test_oracle_fvaltest_history():
         assert not om.test_model
         with pytest.raises(O.UndefVarError, match="ftest"):
             O.iterate(O.ProxNSCORE(), om, "l1", O.PHuberSmootherL1L2(1.0), max_epoch=3)
+
+
+def test_oracle_ggn_ss3_grad_fx_one_argument():
+    """SURVEY Appendix A #8 (prox-GGN-SCORE.jl:58-59,83-84): ProxGGNSCORE's grad_f is
+    x -> model.grad_fx(x), one argument, called only by the ss_type 3 line search (utils.jl:31,
+    after f(x + αd) and f(x)).  A data problem's grad_fx(A, y, x) raises MethodError at the first
+    trial; a one-argument grad_fx is applicable and gives the same steps as the loss kind (whose
+    gradient plays ForwardDiff's part, grad_fx === nothing); ss_type 1 never calls it."""
+    rng = np.random.default_rng(4)
+    N, m = 40, 6
+    A = rng.standard_normal((N, m)) / np.sqrt(m)
+    y = (rng.random(N) < 0.5).astype(np.float64)
+    x0 = rng.standard_normal(m) * 0.3
+    kind = O.Loss("logistic_ce", 1.0 / N, ggn="sigmoid_ce")
+    sig = lambda z: 1.0 / (1.0 + np.exp(-z))  # noqa: E731
+    calls = []
+
+    def f(A, y, x):
+        calls.append("f")
+        return kind.f(A, y, x)
+
+    def g3(A, y, x):
+        return kind.grad(A, y, x)
+
+    pieces = dict(out_fn=lambda A, x: sig(A @ x),
+                  jac_yx=lambda A, y, yh, x: (yh * (1 - yh))[:, None] * A,
+                  grad_fy=lambda A, y, yh: (-(y / yh) + (1 - y) / (1 - yh)) / N,
+                  hess_fy=lambda A, y, yh: (y / yh ** 2 + (1 - y) / (1 - yh) ** 2) / N)
+    hm = O.PHuberSmootherL1L2(1.0)
+    p3 = O.Problem(A, y, x0, O.CallbackLoss(f, g3, **pieces), 1e-2)
+    with pytest.raises(O.MethodError, match=r"no method matching grad_fx\(::Vector\{Float64\}\)"):
+        O.iterate(O.ProxGGNSCORE(ss_type=3), p3, "l1", hm, max_epoch=3)
+    assert calls.count("f") >= 2      # f(x + αd) and f(x) ran before grad_f (utils.jl:31 order)
+    a = O.iterate(O.ProxGGNSCORE(ss_type=1), p3, "l1", hm, max_epoch=3)
+    b = O.iterate(O.ProxGGNSCORE(ss_type=1), O.Problem(A, y, x0, kind, 1e-2), "l1", hm, max_epoch=3)
+    np.testing.assert_allclose(a.obj, b.obj, rtol=1e-9)
+    g1 = lambda x: kind.grad(A, y, x)  # noqa: E731
+    c = O.iterate(O.ProxGGNSCORE(ss_type=3), O.Problem(A, y, x0, O.CallbackLoss(f, g1, **pieces), 1e-2), "l1", hm,
+                  max_epoch=4)
+    d = O.iterate(O.ProxGGNSCORE(ss_type=3), O.Problem(A, y, x0, kind, 1e-2), "l1", hm, max_epoch=4)
+    assert c.epochs == d.epochs
+    np.testing.assert_allclose(c.obj, d.obj, rtol=1e-9)
