@@ -409,8 +409,9 @@ int scs_solve_eval(scs_ctx* ctx, const double* w, const double* dvec, const doub
                    double* x, int* used_lu);
 /* Julia's `A \ b` for a dense square Matrix (LAPACK getrf + getrs) by the hand-written
  * blocked LU: A is row-major n x n; ipiv receives getrf's pivot rows (0-based), info its
- * first zero pivot (1-based; x is then not written), or -1 if the cooperative panel's
- * candidate exchange timed out (a workgroup never became resident; x not written).
+ * first zero pivot (1-based; x is then not written, ipiv is dgetrf's).  A cooperative panel whose
+ * candidate exchange timed out (a workgroup never became resident) is redone with the
+ * column-step panels, the same factor bit for bit (scs_fallback_counts).
  * Needs a context only.                                                                    */
 int scs_lu_eval(scs_ctx* ctx, int64_t n, const double* A, const double* b, double* x, int32_t* ipiv,
                 int* info);
@@ -431,6 +432,27 @@ int scs_timing_reset(scs_ctx* ctx);
 /* The kernels of the latest main Gram launch and sparse product launch, as rocprofv3 names them
  * ("" when none ran), NUL-terminated, truncated to the capacities.                          */
 int scs_kernel_names(scs_ctx* ctx, char* gram, int64_t gram_cap, char* product, int64_t product_cap);
+/* Fallbacks taken instead of failing (r06), counted since the context was created (a
+ * multi-device context: summed over its devices).  counts[i] for i < n:
+ *   SCS_FB_LU_COOP_REFUSED  LU panels whose cooperative launch the runtime refused (run as column steps)
+ *   SCS_FB_LU_COOP_REDO     LU factorizations redone with column-step panels after the one-launch
+ *                           panel's candidate exchange timed out (info = -1)
+ *   SCS_FB_SOLVE_BLOCKS     Cholesky solves redone by per-block launches after a one-launch solve's
+ *                           dependency wait gave up
+ *   SCS_FB_QR_BLOCKS        QR backward solves redone by per-block launches (the same, for QR)
+ *   SCS_FB_CHAIN_REDO       Cholesky factors redone with one launch per operation after a wait of
+ *                           the dependency-driven chain (SCS_CHOL_DAG=1) gave up
+ *   SCS_FB_PIPE_REDO        steps whose Gram + factor were redone unpipelined after a strip wait of
+ *                           the pipelined factor (SCS_CHOL_PIPE) gave up
+ * Each redo gives the bits of the mode it falls back to.                                   */
+#define SCS_FB_LU_COOP_REFUSED 0
+#define SCS_FB_LU_COOP_REDO 1
+#define SCS_FB_SOLVE_BLOCKS 2
+#define SCS_FB_QR_BLOCKS 3
+#define SCS_FB_CHAIN_REDO 4
+#define SCS_FB_PIPE_REDO 5
+#define SCS_FB_N 6
+int scs_fallback_counts(scs_ctx* ctx, int64_t* counts, int n);
 /* Wait for all work on the context stream.                                 */
 int scs_sync(scs_ctx* ctx);
 

@@ -64,6 +64,15 @@ __device__ long long chol_prof[128];
 #define PROF_MARK(i)
 #define PROF_MARK_T(i, t)
 #endif
+#ifdef CHOL_DTIME
+// probe_chol -DCHOL_DTIME: every diagonal-kernel launch's entry / exit (s_memrealtime, 100 MHz) by
+// block index, to split its traced duration into waiting for a CU and running
+__device__ long long chol_dtime[2 * 1024];
+#define DTIME_MARK(i) \
+  if (threadIdx.x == 0) chol_dtime[2 * k + (i)] = (long long)__builtin_amdgcn_s_memrealtime()
+#else
+#define DTIME_MARK(i)
+#endif
 
 constexpr int DNT = 256;
 // W = U⁻¹ by block columns beside the factor (w_column_t) instead of the recursive doubling after it
@@ -132,6 +141,28 @@ __device__ __forceinline__ double quad_bcast(double v) {
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// LDS layouts of the diagonal block S (upper triangle + zeros below the diagonal of the 16 x 16
+// diagonal sub-blocks).  idxb(I, C, rr, cc) = S(16 I + rr, 16 C + cc), I <= C.
+//   LayFull: the whole 128 x 128 block column-major with pitch CLD = 129 (132 KiB).
+//   LayPack (r06): only the 36 upper 16 x 16 blocks, block (I, C) at (C (C + 1) / 2 + I)·272, each
+//     column-major with pitch 17 (the same bank spread as CLD within a block): 76.5 KiB, so that with
+//     the rest (~96 KiB) the kernel fits beside one workgroup of the trailing-update Gram kernel
+//     (32 KiB LDS, 256 VGPRs per lane) instead of waiting for a whole CU to drain.
+// Every element takes the same arithmetic in the same order in both: the same U, W and pivots.
+constexpr int PBP = 17, PBS = SB * PBP, NPB = (CB / SB) * (CB / SB + 1) / 2;
+struct LayFull {
+  static constexpr bool packed = false;
+  static constexpr int words = CB * CLD;
+  __device__ static __forceinline__ int idxb(int I, int C, int rr, int cc) { return (16 * C + cc) * CLD + 16 * I + rr; }
+};
+struct LayPack {
+  static constexpr bool packed = true;
+  static constexpr int words = NPB * PBS;
+  __device__ static __forceinline__ int idxb(int I, int C, int rr, int cc) {
+    return (C * (C + 1) / 2 + I) * PBS + cc * PBP + rr;
+  }
+};
+
 // Phase A: wave 0 factors the 16 x 16 diagonal sub-block at o in registers, reciprocal pivots to
 // srinv.  Lane 4c + q holds rows 4q .. 4q+3 of column c (a[s] = S(o+4q+s, o+c)), so all 64 lanes
 // work and a column step is ~35 instructions instead of ~80 (the one-column-per-lane form
@@ -141,14 +172,16 @@ __device__ __forceinline__ double quad_bcast(double v) {
 // The serial chain is pivot -> rsq -> row scale -> DPP -> the next pivot's update (pnext), computed
 // ahead of the LDS-fed updates.  Every element takes the same fused multiply-subtracts in the same
 // j order as the one-column-per-lane form: bitwise the same U and pivots.
+template <class L>
 __device__ __forceinline__ void diag_factor16(double* su, double* srinv, double* urow, int o, int k, int* info,
                                               int tid) {
+  const int kb = o >> 4;
   int c = (tid & 63) >> 2, q = tid & 3;
   // opaque per call: keeps the compiler from hoisting the lane masks out of the inner-block loop
   asm volatile("" : "+v"(c), "+v"(q));
   double a[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) a[s] = su[(o + c) * CLD + o + 4 * q + s];   // zero below the diagonal
+  for (int s = 0; s < 4; ++s) a[s] = su[L::idxb(kb, kb, 4 * q + s, c)];   // zero below the diagonal
   double pnext = a[0];   // S(j, j) of the next pivot, in lane 4j + j/4
   double rr[SB];         // the reciprocal pivots (wave-uniform), to srinv after the loop
   int bad = -1;
@@ -195,7 +228,7 @@ __device__ __forceinline__ void diag_factor16(double* su, double* srinv, double*
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s)
-    if (4 * q + s <= c) su[(o + c) * CLD + o + 4 * q + s] = a[s];
+    if (4 * q + s <= c) su[L::idxb(kb, kb, 4 * q + s, c)] = a[s];
   if (tid == 0) {
 #pragma unroll
     for (int j = 0; j < SB; ++j) srinv[o + j] = rr[j];
@@ -204,12 +237,14 @@ __device__ __forceinline__ void diag_factor16(double* su, double* srinv, double*
 }
 
 // Phase B: panel, forward substitution Dᵀ p = x per column (D(u, t) reads are wave-uniform)
+template <class L>
 __device__ __forceinline__ void diag_panel16(double* su, const double* srinv, int o, int np, int tid) {
   if (tid < np) {
-    const int c = o + SB + tid;
+    const int kb = o >> 4;
+    const int c = o + SB + tid, C = c >> 4, cc = c & 15;
     double X[SB];
 #pragma unroll
-    for (int u = 0; u < SB; ++u) X[u] = su[c * CLD + o + u];
+    for (int u = 0; u < SB; ++u) X[u] = su[L::idxb(kb, C, u, cc)];
     // right-looking: X[t] takes D(u, t) X[u] as soon as X[u] is final -- the same fused
     // multiply-subtracts in the same u order as the dot-product form (bit-identical), but the
     // dependent chain is 16 x (fma + mul) instead of all 120 fmas in a row
@@ -217,10 +252,10 @@ __device__ __forceinline__ void diag_panel16(double* su, const double* srinv, in
     for (int u = 0; u < SB; ++u) {
       X[u] *= srinv[o + u];
 #pragma unroll
-      for (int t = u + 1; t < SB; ++t) X[t] -= su[(o + t) * CLD + o + u] * X[u];
+      for (int t = u + 1; t < SB; ++t) X[t] -= su[L::idxb(kb, kb, u, t)] * X[u];
     }
 #pragma unroll
-    for (int u = 0; u < SB; ++u) su[c * CLD + o + u] = X[u];
+    for (int u = 0; u < SB; ++u) su[L::idxb(kb, C, u, cc)] = X[u];
   }
 }
 
@@ -229,23 +264,23 @@ __device__ __forceinline__ void diag_panel16(double* su, const double* srinv, in
 // (A[i][k] = U(o+t0+k, i0+i), B[k][j] = U(o+t0+k, c0+j); lane l feeds i|j = l&15, k = l>>4;
 // D row = (l>>4) + 4r, col = l&15).  Diagonal tiles update only i <= c: phase A reads the
 // zeros below the diagonal.  Tile 0 is the next diagonal sub-block.
+template <class L>
 __device__ __forceinline__ void diag_trail_tile(double* su, int o, int id, int lane) {
   const int li = lane & 15, lk = lane >> 4;
   int C = 0;
   while ((C + 1) * (C + 2) / 2 <= id) ++C;
   const int I = id - C * (C + 1) / 2;
-  const int i0 = o + SB + 16 * I, c0 = o + SB + 16 * C;
+  const int kb = o >> 4, BI = kb + 1 + I, BC = kb + 1 + C;   // the tile's block row / column of S
   v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int t0 = 0; t0 < SB; t0 += 4) {
-    const double a = su[(i0 + li) * CLD + o + t0 + lk];
-    const double b = su[(c0 + li) * CLD + o + t0 + lk];
+    const double a = su[L::idxb(kb, BI, t0 + lk, li)];
+    const double b = su[L::idxb(kb, BC, t0 + lk, li)];
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int i = i0 + lk + 4 * r, c = c0 + li;
-    if (i <= c) su[c * CLD + i] -= acc[r];
+    if (I < C || lk + 4 * r <= li) su[L::idxb(BI, BC, lk + 4 * r, li)] -= acc[r];   // i <= c
   }
 }
 
@@ -260,7 +295,7 @@ __device__ __forceinline__ void diag_trail_tile(double* su, int o, int id, int l
 // factor (the doubling needed all of U first: 11.5 us after the loop).  The column goes straight to
 // global W (zeros below its diagonal block).  Fixed order per element: bitwise run to run, and the
 // same bits in both kernel schedules (PIPE or not).
-template <int J>
+template <int J, class L>
 __device__ __forceinline__ void w_column_t(const double* su, const double* swv /*[CB/SB][SB*SB]*/, double* Wk,
                                            int lane, double* su_w) {
   const int li = lane & 15, lk = lane >> 4;
@@ -275,7 +310,7 @@ __device__ __forceinline__ void w_column_t(const double* su, const double* swv /
     for (int i = l - 1; i >= 0; --i)   // S_i += U_il W_lJ (i = l - 1 first: the chain)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        S[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(su[(16 * l + 4 * q + lk) * CLD + 16 * i + li], W[l][q], S[i], 0, 0, 0);
+        S[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(su[L::idxb(i, l, li, 4 * q + lk)], W[l][q], S[i], 0, 0, 0);
     v4d acc = {0.0, 0.0, 0.0, 0.0};   // W_{l-1,J} = -inv(U_{l-1,l-1}) S_{l-1}
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -288,8 +323,9 @@ __device__ __forceinline__ void w_column_t(const double* su, const double* swv /
 #pragma unroll
     for (int r = 0; r < 4; ++r) col[16 * i + 4 * r] = (i <= J) ? W[i <= J ? i : 0][r] : 0.0;
   // the off-diagonal blocks also into the (unused, zero) strictly-lower triangle of su, transposed:
-  // W(r, c) at su[r·CLD + c] -- w_last_column_par reads them there (r05)
-  if (J < CB / SB - 1) {
+  // W(r, c) at su[r·CLD + c] -- w_last_column_par reads them there (r05).  LayPack has no lower
+  // triangle: w_last_column_par reads them back from Wk
+  if (!L::packed && J < CB / SB - 1) {
 #pragma unroll
     for (int i = 0; i < J; ++i)
 #pragma unroll
@@ -297,16 +333,17 @@ __device__ __forceinline__ void w_column_t(const double* su, const double* swv /
   }
 }
 
+template <class L>
 __device__ __forceinline__ void w_column(double* su, const double* swv, double* Wk, int J, int lane) {
   switch (J) {
-    case 0: w_column_t<0>(su, swv, Wk, lane, su); break;
-    case 1: w_column_t<1>(su, swv, Wk, lane, su); break;
-    case 2: w_column_t<2>(su, swv, Wk, lane, su); break;
-    case 3: w_column_t<3>(su, swv, Wk, lane, su); break;
-    case 4: w_column_t<4>(su, swv, Wk, lane, su); break;
-    case 5: w_column_t<5>(su, swv, Wk, lane, su); break;
-    case 6: w_column_t<6>(su, swv, Wk, lane, su); break;
-    default: w_column_t<7>(su, swv, Wk, lane, su); break;
+    case 0: w_column_t<0, L>(su, swv, Wk, lane, su); break;
+    case 1: w_column_t<1, L>(su, swv, Wk, lane, su); break;
+    case 2: w_column_t<2, L>(su, swv, Wk, lane, su); break;
+    case 3: w_column_t<3, L>(su, swv, Wk, lane, su); break;
+    case 4: w_column_t<4, L>(su, swv, Wk, lane, su); break;
+    case 5: w_column_t<5, L>(su, swv, Wk, lane, su); break;
+    case 6: w_column_t<6, L>(su, swv, Wk, lane, su); break;
+    default: w_column_t<7, L>(su, swv, Wk, lane, su); break;
   }
 }
 
@@ -318,20 +355,35 @@ __device__ __forceinline__ void w_column(double* su, const double* swv, double* 
 // W_iJ = -Σ_{l=i}^{J-1} W_il V_l for the wave's row blocks (W_ii = swinv[i]; W_il, l > i, from the
 // transposed copies w_column_t left in su's strictly-lower triangle).  Row blocks {w, 6-w} per wave
 // w < 3 and {3} for wave 3: 32 / 32 / 32 / 16 MFMAs of the second level.  Fixed order per element.
+template <class L>
 __device__ __forceinline__ void w_last_column_par(const double* su, const double* swv, double* Wk, int tid) {
   constexpr int J = CB / SB - 1;
   const int lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
+  // LayPack: W_il (i < l < J) from Wk, where w_column_t<l> stored it before the kernel's last barrier;
+  // all of a wave's loads are issued first, so their latency runs under the V products
+  const int i1 = wv < 3 ? wv : 3, i2 = wv < 3 ? J - 1 - wv : -1;
+  double g1[J][4], g2[J][4];
+  if (L::packed) {
+#pragma unroll
+    for (int l = 0; l < J; ++l)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t off = (int64_t)(16 * l + 4 * q + lk) * CB + li;
+        g1[l][q] = (l > i1) ? Wk[off + 16 * i1] : 0.0;
+        g2[l][q] = (i2 >= 0 && l > i2) ? Wk[off + 16 * i2] : 0.0;
+      }
+  }
   v4d V[J];
 #pragma unroll
   for (int l = 0; l < J; ++l) {
     v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(su[(16 * J + 4 * q + lk) * CLD + 16 * l + li],
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(su[L::idxb(l, J, li, 4 * q + lk)],
                                                  swv[J * SB * SB + li * SB + 4 * q + lk], acc, 0, 0, 0);
     V[l] = acc;
   }
-  auto rowblock = [&](int i) {
+  auto rowblock = [&](int i, const double (*g)[4]) {
     v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int l = 0; l < J; ++l) {
@@ -339,7 +391,7 @@ __device__ __forceinline__ void w_last_column_par(const double* su, const double
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const double a = (l == i) ? swv[i * SB * SB + (4 * q + lk) * SB + li]
-                                  : su[(16 * i + li) * CLD + 16 * l + 4 * q + lk];
+                                  : (L::packed ? g[l][q] : su[(16 * i + li) * CLD + 16 * l + 4 * q + lk]);
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, V[l][q], acc, 0, 0, 0);
       }
     }
@@ -348,10 +400,10 @@ __device__ __forceinline__ void w_last_column_par(const double* su, const double
     for (int r = 0; r < 4; ++r) col[4 * r] = -acc[r];
   };
   if (wv < 3) {
-    rowblock(wv);
-    rowblock(J - 1 - wv);
+    rowblock(i1, g1);
+    rowblock(i2, g2);
   } else {
-    rowblock(3);
+    rowblock(3, g1);
     double* col = Wk + (int64_t)(16 * J + li) * CB + 16 * J + lk;   // W_JJ, the column's diagonal block
 #pragma unroll
     for (int r = 0; r < 4; ++r) col[4 * r] = swv[J * SB * SB + li * SB + lk + 4 * r];
@@ -362,21 +414,33 @@ __device__ __forceinline__ void w_last_column_par(const double* su, const double
 // on to A(kb+1) while waves 1..3 run the rest of C(kb); one barrier per inner block instead of
 // three.  Every element receives the same updates in the same order, so U and W are bitwise those
 // of the phase-serial kernel (PIPE = false, SCS_CHOL_DIAG=0).
-template <bool PIPE>
-__global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
+// LayPack (r06, default): launch bounds for two workgroups per CU, i.e. <= 256 registers per lane
+// (VGPRs + AGPRs): with ~96 KiB of LDS the kernel then fits beside one workgroup of the bulk stream's
+// gram_sia_kernel (32 KiB, 256 registers); LayFull (SCS_CHOL_DIAG_PACK=0) keeps r05's bounds.
+template <bool PIPE, class L>
+__global__ __launch_bounds__(DNT, L::packed ? 2 : 1) void chol_diag_kernel(double* __restrict__ G, int64_t ld, int k,
                                                         double* __restrict__ W, int* __restrict__ info, int wpar) {
-  __shared__ double su[CB * CLD];   // S(r, c) = su[c*CLD + r]
+  // S(r, c) = su[L::idxb(r / 16, c / 16, r % 16, c % 16)]; swinv: inverses of the 16 x 16 diagonal blocks
+  // (col-major).  LayPack takes both as DYNAMIC LDS (CHOL_DIAG_PACK_LDS bytes at launch): with ~94 KiB of
+  // static LDS the backend infers one wave per SIMD and pads the descriptor's VGPRs to 264 to match
+  // (NumVGPRsForWavesPerEU), which no bulk workgroup's 256 registers leave room for; with the LDS dynamic
+  // the descriptor carries the 235 the kernel uses
+  extern __shared__ double chol_dlds[];
+  __shared__ double su_st[L::packed ? 1 : L::words];
+  __shared__ double swinv_st[L::packed ? 1 : CB / SB][SB * SB];
+  double* su = L::packed ? chol_dlds : su_st;
+  double (*swinv)[SB * SB] = L::packed ? reinterpret_cast<double (*)[SB * SB]>(chol_dlds + L::words) : swinv_st;
   __shared__ double srinv[CB];      // 1 / U(j, j)
-  __shared__ double swinv[CB / SB][SB * SB];   // inverses of the 16 x 16 diagonal blocks (col-major)
   __shared__ __attribute__((aligned(16))) double urow[SB];   // phase A's row-j copy
   __shared__ int tctr;                                        // phase C's tile counter
   double* blk = G + (int64_t)k * CB * ld + (int64_t)k * CB;
   double* Wk = W + (int64_t)k * CB * CB;
   const int tid = threadIdx.x;
+  DTIME_MARK(0);
   // the block into LDS: all 32 16-B loads per thread in flight before their LDS stores, and
   // unconditional (the block is whole in memory; the lower triangle is masked after the load -- a
   // masked load compiled to a branch with a kernel-argument reload and an lgkmcnt wait per element)
-  {
+  if (!L::packed) {
     v2d t[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
@@ -388,6 +452,29 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
       const int e = tid + DNT * i, c = e >> 6, r = 2 * (e & 63);
       su[c * CLD + r] = (r <= c) ? t[i][0] : 0.0;
       su[c * CLD + r + 1] = (r + 1 <= c) ? t[i][1] : 0.0;
+    }
+  } else {
+    // the 36 upper blocks only: 128 row pairs per block (8 threads read one column's 16 rows, 128 B),
+    // item e = tid + 256 i lies in block 2 i + (tid >> 7); the diagonal blocks' lower parts are zeroed
+    constexpr int NI = NPB * SB * SB / 2 / DNT;   // 18
+    v2d t[NI];
+    const int h = tid >> 7, cc = (tid >> 3) & 15, rp = 2 * (tid & 7);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int b = 2 * i + h;
+      int C = 0;
+      while ((C + 1) * (C + 2) / 2 <= b) ++C;
+      const int I = b - C * (C + 1) / 2;
+      t[i] = *(const v2d*)(blk + (int64_t)(16 * C + cc) * ld + 16 * I + rp);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int b = 2 * i + h;
+      int C = 0;
+      while ((C + 1) * (C + 2) / 2 <= b) ++C;
+      const int I = b - C * (C + 1) / 2;
+      su[b * PBS + cc * PBP + rp] = (I < C || rp <= cc) ? t[i][0] : 0.0;
+      su[b * PBS + cc * PBP + rp + 1] = (I < C || rp + 1 <= cc) ? t[i][1] : 0.0;
     }
   }
   // inverse of the (final) 16 x 16 diagonal block kb by one wave (lane c = column c)
@@ -403,7 +490,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
     for (int t = SB - 1; t >= 0; --t) {
       w[t] *= srinv[o + t];
 #pragma unroll
-      for (int i = 0; i < t; ++i) w[i] -= su[(o + t) * CLD + o + i] * w[t];
+      for (int i = 0; i < t; ++i) w[i] -= su[L::idxb(kb, kb, i, t)] * w[t];
     }
     if ((tid & 63) < SB) {
 #pragma unroll
@@ -416,13 +503,14 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
     const int o = rb * SB, n = (CB - o) * (SB / 2);
     for (int e = t0; e < n; e += nt) {
       const int c = o + (e >> 3), r = o + 2 * (e & 7);
+      const int sidx = L::idxb(rb, c >> 4, r & 15, c & 15);
       if (r + 1 <= c) {
         v2d v;
-        v[0] = su[c * CLD + r];
-        v[1] = su[c * CLD + r + 1];
+        v[0] = su[sidx];
+        v[1] = su[sidx + 1];
         *(v2d*)(blk + (int64_t)c * ld + r) = v;
       } else if (r == c) {
-        blk[(int64_t)c * ld + r] = su[c * CLD + r];
+        blk[(int64_t)c * ld + r] = su[sidx];
       }
     }
   };
@@ -431,20 +519,20 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   PROF_MARK(0);
   const int wv = tid >> 6, lane = tid & 63;
   if (PIPE) {
-    if (tid < 64) diag_factor16(su, srinv, urow, 0, k, info, tid);
+    if (tid < 64) diag_factor16<L>(su, srinv, urow, 0, k, info, tid);
     __syncthreads();
   }
   for (int kb = 0; kb < CB / SB; ++kb) {
     const int o = kb * SB;
     PROF_MARK(1 + 4 * kb);
     if (!PIPE) {
-      if (tid < 64) diag_factor16(su, srinv, urow, o, k, info, tid);
+      if (tid < 64) diag_factor16<L>(su, srinv, urow, o, k, info, tid);
       __syncthreads();
     }
     PROF_MARK(2 + 4 * kb);
     const int np = CB - o - SB;  // columns right of the sub-block
     if (np == 0) break;
-    diag_panel16(su, srinv, o, np, tid);
+    diag_panel16<L>(su, srinv, o, np, tid);
     if (tid == 0) tctr = 1;   // C(kb)'s tile counter (tile 0 is wave 0's)
     __syncthreads();
     PROF_MARK(3 + 4 * kb);
@@ -458,18 +546,18 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
           if (lane == 0) id = __hip_atomic_fetch_add(&tctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           id = __builtin_amdgcn_readfirstlane(id);
           if (id >= ntl) break;
-          diag_trail_tile(su, o, id, lane);
+          diag_trail_tile<L>(su, o, id, lane);
         }
       };
       if (wv == 0) {
-        diag_trail_tile(su, o, 0, lane);
+        diag_trail_tile<L>(su, o, 0, lane);
         PROF_MARK_T(36 + kb, 0);
         // tile 0's elements go from the lanes that updated them to the lanes that factor them (lane
         // 4c + q reads rows 4q.. of column c): an intra-wave LDS hand-off with no barrier, so order it
         // for the compiler (instruction-free wavefront fence + wave barrier, as in diag_factor16)
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        diag_factor16(su, srinv, urow, o + SB, k, info, tid);
+        diag_factor16<L>(su, srinv, urow, o + SB, k, info, tid);
         PROF_MARK_T(43 + kb, 0);
 #ifndef CHOL_NO_W0CLAIM
         claim_tiles();
@@ -480,7 +568,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
           PROF_MARK_T(50 + kb, 64 * wv);
         }
         // W's block column kb - 1 (its last input, swinv[kb - 1], came before this step's barrier)
-        if (W_BY_COLUMNS && kb >= 1 && wv == 1 + (kb + 1) % 3) w_column(su, &swinv[0][0], Wk, kb - 1, lane);
+        if (W_BY_COLUMNS && kb >= 1 && wv == 1 + (kb + 1) % 3) w_column<L>(su, &swinv[0][0], Wk, kb - 1, lane);
         claim_tiles();
         // row blocks of U are final after their panel step: waves 1..3 store them while wave 0 is
         // on the chain (kb = 3: blocks 0, 1; 4: 2, 3; 5: 4, 5; 6: 6 -- where these waves have slack)
@@ -491,7 +579,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
         PROF_MARK_T(57 + 3 * kb + wv - 1, 64 * wv);
       }
     } else {
-      for (int id = wv; id < ntl; id += DNT / 64) diag_trail_tile(su, o, id, lane);
+      for (int id = wv; id < ntl; id += DNT / 64) diag_trail_tile<L>(su, o, id, lane);
     }
     __syncthreads();
   }
@@ -502,7 +590,7 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   if (PIPE) {
     if (wv == DNT / 64 - 1) inv16(CB / SB - 1);
     else store_urows(CB / SB - 1, tid, DNT - 64);
-    if (W_BY_COLUMNS && wv == 1) w_column(su, &swinv[0][0], Wk, CB / SB - 2, lane);   // swinv[6]: step 6
+    if (W_BY_COLUMNS && wv == 1) w_column<L>(su, &swinv[0][0], Wk, CB / SB - 2, lane);   // swinv[6]: step 6
   } else {
     for (int rb = 0; rb < CB / SB; ++rb) store_urows(rb, tid, DNT);
     for (int kb = tid >> 6; kb < CB / SB; kb += DNT / 64) inv16(kb);
@@ -511,20 +599,22 @@ __global__ __launch_bounds__(DNT) void chol_diag_kernel(double* __restrict__ G, 
   if (W_BY_COLUMNS) {
     PROF_MARK(34);
     if (PIPE) {
-      if (wpar) w_last_column_par(su, &swinv[0][0], Wk, tid);
-      else if (wv == 0) w_column(su, &swinv[0][0], Wk, CB / SB - 1, lane);
+      if (wpar) w_last_column_par<L>(su, &swinv[0][0], Wk, tid);
+      else if (wv == 0) w_column<L>(su, &swinv[0][0], Wk, CB / SB - 1, lane);
     } else if (wpar) {   // columns 0..6 (wave w: w and 6 - w), then the last one by all waves, as PIPE
-      w_column(su, &swinv[0][0], Wk, wv, lane);
-      if (wv < 3) w_column(su, &swinv[0][0], Wk, CB / SB - 2 - wv, lane);
+      w_column<L>(su, &swinv[0][0], Wk, wv, lane);
+      if (wv < 3) w_column<L>(su, &swinv[0][0], Wk, CB / SB - 2 - wv, lane);
       __syncthreads();   // the transposed off-diagonal blocks w_last_column_par reads
-      w_last_column_par(su, &swinv[0][0], Wk, tid);
+      w_last_column_par<L>(su, &swinv[0][0], Wk, tid);
     } else {   // every column here: wave w takes columns w and 7 - w
-      w_column(su, &swinv[0][0], Wk, wv, lane);
-      w_column(su, &swinv[0][0], Wk, CB / SB - 1 - wv, lane);
+      w_column<L>(su, &swinv[0][0], Wk, wv, lane);
+      w_column<L>(su, &swinv[0][0], Wk, CB / SB - 1 - wv, lane);
     }
     PROF_MARK(35);
+    DTIME_MARK(1);
     return;
   }
+  if constexpr (L::packed) return;   // (W_BY_COLUMNS only)
   // ---- diagonal 16 x 16 inverses into the diagonal blocks of S (start of the doubling)
   for (int e = tid; e < CB * SB; e += DNT) {
     const int kb = e >> 8, c = (e >> 4) & 15, i = e & 15;
@@ -711,11 +801,40 @@ static int chol_wpar() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
+// SCS_CHOL_DIAG_PACK (read per call; default on): the packed-LDS diagonal kernel (LayPack, r06);
+// 0 = r05's full 128 x 129 LDS copy (LayFull).  The same U, W and pivots either way.
+static bool chol_diag_pack() {
+  const char* e = getenv("SCS_CHOL_DIAG_PACK");
+  return !(e && e[0] == '0');
+}
+
+constexpr int CHOL_DIAG_PACK_LDS = (LayPack::words + (CB / SB) * SB * SB) * (int)sizeof(double);   // 94,720 B
+
+static hipError_t chol_diag_pack_attr() {   // the dynamic LDS above the 64 KiB default, once per process
+  static hipError_t done = [] {
+    hipError_t e = hipFuncSetAttribute((const void*)chol_diag_kernel<true, LayPack>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, CHOL_DIAG_PACK_LDS);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)chol_diag_kernel<false, LayPack>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              CHOL_DIAG_PACK_LDS);
+    if (e != hipSuccess) (void)hipGetLastError();   // the LayFull kernel runs instead
+    return e;
+  }();
+  return done;
+}
+
 hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st) {
-  if (chol_diag_pipe())
-    hipLaunchKernelGGL(chol_diag_kernel<true>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
+  const bool pipe = chol_diag_pipe(), pack = chol_diag_pack() && chol_diag_pack_attr() == hipSuccess;
+  if (pipe && pack)
+    hipLaunchKernelGGL((chol_diag_kernel<true, LayPack>), dim3(1), dim3(DNT), CHOL_DIAG_PACK_LDS, st, G, ld, k, W, info,
+                       chol_wpar());
+  else if (pipe)
+    hipLaunchKernelGGL((chol_diag_kernel<true, LayFull>), dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
+  else if (pack)
+    hipLaunchKernelGGL((chol_diag_kernel<false, LayPack>), dim3(1), dim3(DNT), CHOL_DIAG_PACK_LDS, st, G, ld, k, W,
+                       info, chol_wpar());
   else
-    hipLaunchKernelGGL(chol_diag_kernel<false>, dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
+    hipLaunchKernelGGL((chol_diag_kernel<false, LayFull>), dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
   return hipGetLastError();
 }
 
@@ -791,6 +910,26 @@ static unsigned bulk_skip_for(const CholAux* a, int ntiles) {
   const char* e = getenv("SCS_CHOL_SKIP_MAXTILES");
   if (e && ntiles > atoi(e)) return 0u;
   return a->bskip;
+}
+
+// SCS_CHOL_BULK_RESERVE (read per call): where no CU is skipped (m >= 16384), the bulk stream's
+// launches as persistent launches of 2·CUs − r workgroups, r slots left to the chain.  A plain bulk
+// launch of thousands of tiles refills every slot it frees, and the chain's diagonal kernel -- which
+// (packed, r06) fits in one free slot beside a bulk workgroup -- then waited for the whole trailing
+// update (up to 3.3 ms, once per outer block, profiles/r06/pack/).  BULK_BND_ONLY marks a persistent
+// launch that skips no CU (bits above 15 match no CU id).
+constexpr unsigned BULK_BND_ONLY = 1u << 16;
+static int bulk_reserve(const CholAux* a) {
+  const char* e = getenv("SCS_CHOL_BULK_RESERVE");
+  (void)a;
+  return e ? atoi(e) : 0;
+}
+static unsigned bulk_mask(const CholAux* a, int ntiles) {
+  const unsigned s = bulk_skip_for(a, ntiles);
+  return (s == 0 && bulk_reserve(a) > 0) ? BULK_BND_ONLY : s;
+}
+static int bulk_slots(const CholAux* a, unsigned mask) {
+  return mask == BULK_BND_ONLY ? a->bslots - bulk_reserve(a) : a->bslots;
 }
 
 // The bulk stream's bounded launches take counter sets from a->bctr in turn, each zero when taken
@@ -941,8 +1080,8 @@ static hipError_t strip_solve(double* G, int64_t ld, const double* W, const Chol
       hipError_t ez = hipSuccess;
       unsigned* ctr = bulk_ctr(a, st, &ez);
       if (ez != hipSuccess) return ez;
-      return gram_launch_bounded(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, ctr, bulk_skip_for(a, ntiles),
-                                 a->bslots,
+      const unsigned mk = bulk_mask(a, ntiles);
+      return gram_launch_bounded(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, ctr, mk, bulk_slots(a, mk),
                                  st, true);
     }
     return gram_launch_gen(A1, lda1, A2, lda2, w, 0, k1, tiles, ntiles, R, ld, flags, st);
@@ -1096,6 +1235,9 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(const DagTask* __restrict
     if (t.sig1 >= 0) __hip_atomic_fetch_add(cnt + t.sig1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+
+static bool chol_dag_on();
+bool chol_dag_active(const CholAux* a) { return chol_dag_on() && a->serr && !a->no_dag; }
 
 static bool chol_dag_on() {
   const char* e = getenv("SCS_CHOL_DAG");
@@ -1340,7 +1482,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (ej != hipSuccess) return ej;
     st = a->stc;
   }
-  const bool dag = chol_dag_on() && a->serr;
+  const bool dag = chol_dag_on() && a->serr && !a->no_dag;
   const bool steps = !dag && ba_steps() && a->sscr && OB <= 16;
   const bool split = la && c12_split() && a->ev4;
   if (dag) {
@@ -1434,10 +1576,10 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (e == hipSuccess && ntri > n2a) {
       unsigned* ctr = bulk_ctr(a, sb, &e);
       const bool sbo = split && a->sbl && (2 * OB) % 8 == 0 && nc % 8 == 0 && chol_sbl();
+      const unsigned mk = bulk_mask(a, ntri - n2a);
       if (e == hipSuccess)
         e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, (sbo ? a->sbl : trilist) + n2a,
-                                ntri - n2a, trail, ld, 2 | 4, ctr, bulk_skip_for(a, ntri - n2a), a->bslots, sb,
-                                true);
+                                ntri - n2a, trail, ld, 2 | 4, ctr, mk, bulk_slots(a, mk), sb, true);
     }
     if (e == hipSuccess) e = hipEventRecord(a->ev2, sb);
     if (e != hipSuccess) return e;
@@ -1908,12 +2050,29 @@ static bool solve_persist() {
   return !(e && e[0] == '0');
 }
 
-hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, const double* y, double* x,
+hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, double* y, double* x,
                            unsigned* flags, unsigned gen, int* err, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
+  if (!solve_persist()) return chol_back_blocks(U, ld, mpad, W, y, x, st);   // SCS_SOLVE_PERSIST=0 (y consumed)
   if (!flags || !err || gen == 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(chol_bwd_persist_kernel, dim3((unsigned)nblk), dim3(PS_NT), 0, st, U, ld, W, y, x, flags, gen,
                      err, nblk);
+  return hipGetLastError();
+}
+
+// U x = y by outer blocks of OB 128-blocks in descending order: the x of block [i0, i1) to x, y
+// updated in place (the per-block form of chol_bwd_persist_kernel)
+static hipError_t chol_back_blocks_ob(const double* G, int64_t ld, int nblk, const double* W, double* y, double* b,
+                                      int OB, hipStream_t st) {
+  const int nout = (nblk + OB - 1) / OB;
+  for (int q = nout - 1; q >= 0; --q) {
+    const int i0 = q * OB, i1 = i0 + OB < nblk ? i0 + OB : nblk;
+    hipLaunchKernelGGL(chol_bwd_inner_kernel, dim3(1), dim3(SOLVE_NT), 0, st, G, ld, W, i0, i1, y, b);
+    const int64_t nr = (int64_t)i0 * CB;
+    if (nr > 0)
+      hipLaunchKernelGGL(chol_bwd_update_kernel, dim3((unsigned)ceil_div(nr, 64)), dim3(256), 0, st, G, ld,
+                         (int64_t)i0 * CB, (int64_t)i1 * CB, b, nr, y);
+  }
   return hipGetLastError();
 }
 
@@ -1922,7 +2081,7 @@ hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const doub
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y,
                       CholAux* a, hipStream_t st) {
   const int nblk = (int)(mpad / CB);
-  if (a && a->sflags && solve_persist()) {
+  if (a && a->sflags && solve_persist() && !a->no_persist) {
     // y (forward) then b := x (backward); flags [0, nblk) forward, [nblk, 2 nblk) backward
     const unsigned gen = ++a->sgen == 0 ? ++a->sgen : a->sgen;
     hipLaunchKernelGGL(chol_fwd_persist_kernel, dim3((unsigned)nblk), dim3(PS_NT), 0, st, G, ld, W, b, y, a->sflags,
@@ -1948,16 +2107,12 @@ hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W
                          (int64_t)i0 * CB, (int64_t)i1 * CB, y, (int64_t)i1 * CB, nc, b);
   }
   // backward: outer blocks in descending order; the x of block [i0, i1) goes to b
-  const int nout = (nblk + OB - 1) / OB;
-  for (int q = nout - 1; q >= 0; --q) {
-    const int i0 = q * OB, i1 = i0 + OB < nblk ? i0 + OB : nblk;
-    hipLaunchKernelGGL(chol_bwd_inner_kernel, dim3(1), dim3(SOLVE_NT), 0, st, G, ld, W, i0, i1, y, b);
-    const int64_t nr = (int64_t)i0 * CB;
-    if (nr > 0)
-      hipLaunchKernelGGL(chol_bwd_update_kernel, dim3((unsigned)ceil_div(nr, 64)), dim3(256), 0, st, G, ld,
-                         (int64_t)i0 * CB, (int64_t)i1 * CB, b, nr, y);
-  }
-  return hipGetLastError();
+  return chol_back_blocks_ob(G, ld, nblk, W, y, b, OB, st);
+}
+
+hipError_t chol_back_blocks(const double* U, int64_t ld, int64_t mpad, const double* W, double* y, double* x,
+                            hipStream_t st) {
+  return chol_back_blocks_ob(U, ld, (int)(mpad / CB), W, y, x, 1, st);
 }
 
 }  // namespace scs

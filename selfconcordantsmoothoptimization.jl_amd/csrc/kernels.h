@@ -130,6 +130,10 @@ struct CholAux {             // device constants of the two-level factorization 
   unsigned* sflags = nullptr;
   int* serr = nullptr;
   unsigned sgen = 0;
+  // fallbacks (scsopt.cpp): the per-block solves instead of the one-launch ones after a solve's wait gave
+  // up; the launch-per-operation chain instead of the dependency-driven one after a chain wait gave up
+  mutable bool no_persist = false;
+  mutable bool no_dag = false;
   // dependency-driven chain launches (chol_dag_build, built for one outer block size dag_ob): per
   // inner block k the A-phase step (row panel + trailing strips inside the outer block), per outer
   // block t the next block's strip solve + diagonal triangle (Ba + C1a)
@@ -151,6 +155,11 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
                        const int2* trilist, int* info, hipStream_t st);
 hipError_t chol_solve(const double* G, int64_t ld, int64_t mpad, const double* W, double* b, double* y, CholAux* a,
                       hipStream_t st);
+// whether chol_factor would run the dependency-driven chain (SCS_CHOL_DAG=1, not switched off)
+bool chol_dag_active(const CholAux* a);
+// U x = y by the per-block launches (y is consumed as scratch), the fallback of chol_back_solve
+hipError_t chol_back_blocks(const double* U, int64_t ld, int64_t mpad, const double* W, double* y, double* x,
+                            hipStream_t st);
 // Strip pipeline (scsopt.cpp gram_factor_pipelined): the factor runs left-looking behind a Gram
 // computed strip by strip.  Strip s = inner blocks [s·OB, min((s+1)·OB, nblk)).
 int chol_outer_block();
@@ -191,6 +200,10 @@ struct LUAux {
   mutable int ob = 1;        // panels per outer block of the last lu_factor (lu_solve follows its row order)
   int2* sq = nullptr;        // square-shell tile list (trailing updates)
   int2* row1 = nullptr;      // (0, j) tile list (TRSM)
+  // the cooperative one-launch panel: off for a redo after a timed-out candidate exchange (info = -1,
+  // scsopt.cpp lu_factor_checked); launches the runtime refused (the panel ran as column steps)
+  mutable bool no_coop = false;
+  mutable int64_t coop_refused = 0;
 };
 hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st);
 void lu_aux_free(LUAux* a);
@@ -234,7 +247,7 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
 // T (128 x 128, upper) of a compact WY block from Gv = VᵀV and tau (chol.hip; the QR's panels)
 hipError_t wy_t_build(const double* Gv, const double* tau, double* T, hipStream_t st);
 hipError_t chol_tri_inverse(const double* R, int64_t ld, int nblk, double* W, hipStream_t st);
-hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, const double* y, double* x,
+hipError_t chol_back_solve(const double* U, int64_t ld, int64_t mpad, const double* W, double* y, double* x,
                            unsigned* flags, unsigned gen, int* err, hipStream_t st);
 
 // ---- vec.hip

@@ -410,7 +410,7 @@ __global__ __launch_bounds__(LU_NT) void lu_panel_step2_kernel(double* A, int64_
 // never became resident) stores info = -1 and the abort word, and every later panel leaves at once.
 constexpr int LUC_MAXWG = 128;                // workgroups (= CUs) at most
 constexpr int LUC_LDS = 96 * 1024;            // dynamic LDS that keeps a second workgroup off the CU
-constexpr unsigned LUC_SPIN_MAX = 1u << 19;   // sweeps before giving up (~0.5 s)
+constexpr unsigned LUC_SPIN_MAX = 1u << 19;   // sweeps before giving up (~0.5 s; SCS_LU_COOP_SPIN overrides)
 // granule words (u64): candidates [2][MAXWG][4] | abort word (+pad) | candidate rows [2][MAXWG][128][2]
 // | row j + 1 [2][128][2]
 constexpr int64_t LUC_CAND = 0, LUC_ABORT = 2 * LUC_MAXWG * 4, LUC_CROW = LUC_ABORT + 16;
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
                                                               int64_t c0, int64_t h, unsigned long long* gran,
                                                               unsigned tagbase,
                                                               int* ipiv, int* info, int2* pairs, int* npairs,
-                                                              int pf_on) {
+                                                              int pf_on, unsigned spin_max) {
   constexpr int RW = NT / 2, RP = NT / 8;   // rows per workgroup, rows per pass
   __shared__ double sv[NT / 64];
   __shared__ int si[NT / 64], sw[NT / 64];
@@ -460,6 +460,13 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
   const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
   const int base = g * RW + rr;   // this thread's panel position in pass ps: base + RP ps
   if (gran[LUC_ABORT] != 0) return;   // an earlier panel of this factorization gave up (info = -1)
+  if (spin_max == 0) {   // (tests: SCS_LU_COOP_SPIN=0 gives up at once, as a never-resident workgroup would)
+    if (threadIdx.x == 0) {
+      *info = -1;
+      gran[LUC_ABORT] = 1;
+    }
+    return;
+  }
   double v[4][16];
 #pragma unroll
   for (int ps = 0; ps < 4; ++ps) {
@@ -610,7 +617,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
           pf3 = luc_get(rp + 3);
           pf_w = bw;
         }
-        if (++spins > LUC_SPIN_MAX) {
+        if (++spins > spin_max) {
           give_up();
           break;
         }
@@ -627,7 +634,7 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
             dst[2 * lane + 1] = d1;
             return;
           }
-          if (++spins > LUC_SPIN_MAX) give_up();
+          if (++spins > spin_max) give_up();
           __builtin_amdgcn_s_sleep(1);
         }
       };
@@ -1115,6 +1122,19 @@ static int lu_coop_nt() {   // read per call (A/B): SCS_LU_COOP_NT = 256 | 512
   return (e && atoi(e) == 512) ? 512 : 256;
 }
 
+static unsigned lu_coop_spin() {   // read per call: SCS_LU_COOP_SPIN (sweeps; 0 = give up at once, tests)
+  const char* e = getenv("SCS_LU_COOP_SPIN");
+  return e ? (unsigned)strtoul(e, nullptr, 10) : LUC_SPIN_MAX;
+}
+
+// SCS_LU_COOP_LAUNCH (read per call; default 1): the one-launch panel through hipLaunchCooperativeKernel,
+// which guarantees that all its workgroups are resident together or refuses the launch (the panel then
+// runs as column steps); 0 = a plain launch, residency by the 96 KiB of LDS and the CU-count check only
+static bool lu_coop_api() {
+  const char* e = getenv("SCS_LU_COOP_LAUNCH");
+  return !(e && e[0] == '0');
+}
+
 static bool lu_coop_wide() {   // read per call (A/B): SCS_LU_COOP_WIDE=1 (n = 8192: 84.9 vs 83.2 ms narrow)
   const char* e = getenv("SCS_LU_COOP_WIDE");
   return e && e[0] == '1';
@@ -1150,15 +1170,34 @@ static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUA
   // (a runtime that refuses the dynamic-LDS attribute gets the step kernels, and so does a device with
   // fewer than twice as many CUs as the panel needs workgroups -- a partitioned MI355X -- where they
   // could not all be resident at once)
-  const bool coop = mode == 3 && gco <= (cnt == 512 ? 64 : LUC_MAXWG) && 2 * gco <= lu_device_cus() &&
-                    lu_coop_attr() == hipSuccess;
+  bool coop = mode == 3 && !a->no_coop && gco <= (cnt == 512 ? 64 : LUC_MAXWG) && 2 * gco <= lu_device_cus() &&
+              lu_coop_attr() == hipSuccess;
   if (coop) {
     const bool wide = lu_coop_wide();
     auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
                            : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)gco), dim3(cnt), LUC_LDS, st, A, ld, r0, c0, h, a->gran, (unsigned)k << 8,
-                       a->ipiv, info, a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k, lu_coop_pf() ? 1 : 0);
-  } else
+    double* pA = A;
+    int64_t pld = ld, pr0 = r0, pc0 = c0, ph = h;
+    unsigned long long* pgran = a->gran;
+    unsigned ptag = (unsigned)k << 8, pspin = lu_coop_spin();
+    int* pipiv = a->ipiv;
+    int* pinfo = info;
+    int2* ppairs = a->pairs + (int64_t)k * LU_MAXPAIRS;
+    int* pnp = a->npairs + k;
+    int ppf = lu_coop_pf() ? 1 : 0;
+    if (lu_coop_api()) {
+      void* args[] = {&pA, &pld, &pr0, &pc0, &ph, &pgran, &ptag, &pipiv, &pinfo, &ppairs, &pnp, &ppf, &pspin};
+      if (hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)gco), dim3(cnt), args, LUC_LDS, st) != hipSuccess) {
+        (void)hipGetLastError();   // refused (the grid cannot be resident at once): this panel by column steps
+        ++a->coop_refused;
+        coop = false;
+      }
+    } else {
+      hipLaunchKernelGGL(kern, dim3((unsigned)gco), dim3(cnt), LUC_LDS, st, pA, pld, pr0, pc0, ph, pgran, ptag, pipiv,
+                         pinfo, ppairs, pnp, ppf, pspin);
+    }
+  }
+  if (!coop)
     for (int j = -1; j < LB; ++j) {
       if (mode == 2 && npass == 1)
         hipLaunchKernelGGL(lu_panel_step2_kernel<1>, dim3(nwg), dim3(LU_NT), 0, st, A, ld, r0, c0, h, R, j, a->cand,

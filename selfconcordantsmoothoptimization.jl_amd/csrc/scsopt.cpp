@@ -308,6 +308,11 @@ struct scs_ctx {
   double* lsbuf = nullptr;
   int64_t lscap = 0;
   int64_t ls_direct = 0;   // incremental trials re-decided on the direct form (near the Armijo threshold)
+  // fallbacks taken instead of failing (scs_fallback_counts): SCS_FB_* in include/scsopt.h
+  int64_t fb[SCS_FB_N] = {};
+  double* rbk = nullptr;   // (m_pad) the right-hand side before a one-launch solve, for its per-block redo
+  double* Gbk = nullptr;   // (m_pad²) the system before a cooperative-panel LU, for its column-step redo
+  int64_t Gbk_n = 0;
 
   // caches (CSE of identical evaluations; keyed by the host x content)
   std::vector<double> zkey;
@@ -631,7 +636,7 @@ void allreduce(scs_ctx* c, double* buf, int64_t count) {
 void alloc_mspace(scs_ctx* c) {
   const int64_t mp = c->mpad;
   double** vs[] = {&c->x, &c->xp, &c->xn, &c->dxv, &c->gr, &c->Hr, &c->hinv, &c->zb, &c->d,
-                   &c->gq, &c->gqn, &c->gtmp, &c->gtmp2, &c->q, &c->gcache[0], &c->gcache[1]};
+                   &c->gq, &c->gqn, &c->gtmp, &c->gtmp2, &c->q, &c->gcache[0], &c->gcache[1], &c->rbk};
   for (double** v : vs) {
     dfree_t(c, *v);
     *v = dalloc<double>(c, mp);
@@ -1354,6 +1359,66 @@ double line_search(scs_ctx* c, const double* xh, const double* xd, const double*
 // partial pivoting (lu.hip; the reference's `\`, prox-N-SCORE.jl:70) from the saved copy when
 // a pivot is not positive (e.g. the indefinite Q of a CE loss on ±1 labels,
 // test/test_algs.jl:10), or always with force_lu (scs_solve_eval).
+// SCS_FAULT_LATE (tests; read per call): a bit mask of the dependency waits to report as timed out,
+// as the device would after ~30 s (never expected), so that each fallback below can be driven:
+// 1 the one-launch triangular solves, 2 the QR's one-launch backward solve, 4 the dependency-driven
+// Cholesky chain (SCS_CHOL_DAG=1), 8 the pipelined factor's strip wait (SCS_CHOL_PIPE).  The
+// cooperative LU panel's own give-up path is driven on the device instead (SCS_LU_COOP_SPIN=0).
+static bool fault_late(int bit) {
+  const char* e = std::getenv("SCS_FAULT_LATE");
+  return e && (std::atoi(e) & bit);
+}
+
+// lu_factor(M) with the cooperative panel's fallback (r06).  A panel launch the runtime refuses runs as
+// column steps inside lu_factor; a candidate exchange that timed out (info = -1: a workgroup of the
+// one-launch panel never became resident -- the plain launch mode, SCS_LU_COOP_LAUNCH=0, or a device
+// shared with other work) leaves M undefined, so `rebuild` restores the system and the factorization
+// is redone with the column-step panels, which give the same factor and pivots bit for bit
+// (test_lu_coop_panel_largest_grid).  Returns the factorization's info (0, or the first zero pivot).
+template <class F>
+int lu_factor_checked(scs_ctx* c, double* M, int64_t ld, int64_t n, int64_t npad, int* dinfo, F&& rebuild) {
+  int info = 0;
+  const int64_t refused0 = c->lu.coop_refused;
+  HCK(hipMemsetAsync(dinfo, 0, sizeof(int), c->st));
+  HCK(lu_factor(M, ld, n, npad, &c->lu, dinfo, c->st));
+  HCK(hipMemcpyAsync(&info, dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  c->fb[SCS_FB_LU_COOP_REFUSED] += c->lu.coop_refused - refused0;
+  if (info != -1) return info;
+  ++c->fb[SCS_FB_LU_COOP_REDO];
+  rebuild();
+  c->lu.no_coop = true;
+  HCK(hipMemsetAsync(dinfo, 0, sizeof(int), c->st));
+  const hipError_t e = lu_factor(M, ld, n, npad, &c->lu, dinfo, c->st);
+  c->lu.no_coop = false;
+  HCK(e);
+  HCK(hipMemcpyAsync(&info, dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  if (info < 0) fail(c, SCS_ERR_HIP, "LU: info %d from the column-step panels", info);
+  return info;
+}
+
+// chol_solve with the one-launch solves' fallback (r06): a dependency wait of chol_fwd/bwd_persist_kernel
+// that gave up (~30 s, never expected: a block waits only on blocks dispatched before it) sets caux.serr
+// and leaves rhs undefined; the solve is redone from the saved right-hand side by the per-block launches
+// (SCS_SOLVE_PERSIST=0's form)
+void chol_solve_checked(scs_ctx* c, double* rhs) {
+  const int64_t ld = c->mpad;
+  HCK(hipMemcpyAsync(c->rbk, rhs, sizeof(double) * ld, hipMemcpyDeviceToDevice, c->st));
+  HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, &c->caux, c->st));
+  int late = 0;
+  if (c->caux.serr) HCK(hipMemcpyAsync(&late, c->caux.serr, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  sync(c);
+  if (!late && !fault_late(1)) return;
+  if (c->caux.serr) HCK(hipMemsetAsync(c->caux.serr, 0, sizeof(int), c->st));
+  ++c->fb[SCS_FB_SOLVE_BLOCKS];
+  HCK(hipMemcpyAsync(rhs, c->rbk, sizeof(double) * ld, hipMemcpyDeviceToDevice, c->st));
+  c->caux.no_persist = true;
+  const hipError_t e = chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, &c->caux, c->st);
+  c->caux.no_persist = false;
+  HCK(e);
+}
+
 // the LU fallback: the full symmetric system from the copy Gc (rebuilt from the cached Gram when
 // this step's Gram came from the cache), the reference's `\` (prox-N-SCORE.jl:70)
 void solve_lu_fallback(scs_ctx* c, double* rhs, hipEvent_t e0) {
@@ -1378,11 +1443,16 @@ void solve_lu_fallback(scs_ctx* c, double* rhs, hipEvent_t e0) {
     return;
   }
   HCK(lu_aux_init(&c->lu, ld, c->st));
-  HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
-  HCK(lu_factor(c->Gc, ld, m, ld, &c->lu, c->cinfo, c->st));
-  HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
-  sync(c);
-  if (info < 0) fail(c, SCS_ERR_HIP, "LU: the cooperative panel's candidate exchange timed out (info %d)", info);
+  // the system the factor overwrites, kept for a column-step redo (lu_factor_checked)
+  if (c->Gbk_n != ld) {
+    dfree_t(c, c->Gbk);
+    c->Gbk = dalloc<double>(c, (size_t)ld * ld);
+    c->Gbk_n = ld;
+  }
+  HCK(hipMemcpyAsync(c->Gbk, c->Gc, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+  info = lu_factor_checked(c, c->Gc, ld, m, ld, c->cinfo, [&] {
+    HCK(hipMemcpyAsync(c->Gc, c->Gbk, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+  });
   if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
   HCK(lu_solve(c->Gc, ld, ld, &c->lu, rhs, c->st));
   tend(c, T_SOLVE, e0);
@@ -1402,9 +1472,12 @@ static void qr_run(scs_ctx* c, double* A, int64_t npad, double* b) {
   int late = 0;
   HCK(hipMemcpyAsync(&late, c->qr.err, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
-  if (late) {
+  if (late || fault_late(2)) {
+    // R is complete and qr.Ym still holds Qᵀb (the one-launch kernel only reads it): the backward
+    // solve again by the per-block launches
     HCK(hipMemsetAsync(c->qr.err, 0, sizeof(int), c->st));
-    fail(c, SCS_ERR_HIP, "QR: a dependency wait of the backward solve timed out");
+    ++c->fb[SCS_FB_QR_BLOCKS];
+    HCK(chol_back_blocks(A, npad, npad, c->qr.W, c->qr.Ym, b, c->st));
   }
 }
 
@@ -1452,15 +1525,30 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false, bool force_qr 
     c->caux.chain_mode = c->rccl ? 2 : 0;   // RCCL's streams in the process: keep the factor's two apart
     HCK(chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st));
     HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
-    int late = 0;   // a dependency wait of the chain launches or the solves gave up (~30 s): never expected
+    int late = 0;   // a dependency wait of the chain launches gave up (~30 s): never expected
     HCK(hipMemcpyAsync(&late, c->caux.serr, sizeof(int), hipMemcpyDeviceToHost, c->st));
     sync(c);
-    if (late) {
+    if (late || (fault_late(4) && chol_dag_active(&c->caux))) {
+      // the factor is incomplete: the system again (Gc, or the cached Gram + λ diag Hr), and the
+      // factor redone with one launch per operation (r06; was SCS_ERR_HIP)
       HCK(hipMemsetAsync(c->caux.serr, 0, sizeof(int), c->st));
-      fail(c, SCS_ERR_HIP, "Cholesky: a dependency wait of the chain launches timed out");
+      ++c->fb[SCS_FB_CHAIN_REDO];
+      if (c->g_from_cache) {
+        HCK(hipMemcpyAsync(c->G, c->Gk, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+        HCK(launch_diag_add(c->G, c->mpad, m, c->lam, c->Hr, c->st));
+      } else {
+        HCK(hipMemcpyAsync(c->G, c->Gc, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice, c->st));
+      }
+      HCK(hipMemsetAsync(c->cinfo, 0, sizeof(int), c->st));
+      c->caux.no_dag = true;
+      const hipError_t e = chol_factor(c->G, ld, m, ld, c->W, &c->caux, c->trilist, c->cinfo, c->st);
+      c->caux.no_dag = false;
+      HCK(e);
+      HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
+      sync(c);
     }
     if (info == 0) {
-      HCK(chol_solve(c->G, ld, ld, c->W, rhs, c->ysol, &c->caux, c->st));
+      chol_solve_checked(c, rhs);
       solve_flag_copy(c);
       c->lu_fallback_used = false;
       tend(c, T_SOLVE, e0);
@@ -1471,24 +1559,29 @@ void solve_system(scs_ctx* c, double* rhs, bool force_lu = false, bool force_qr 
 }
 
 // the pipelined path's solve: the factor (and Gc) are already enqueued (gram_factor_pipelined,
-// which opened the T_SOLVE interval at the end of the Gram)
-void solve_factored(scs_ctx* c, double* rhs, hipEvent_t e0) {
+// which opened the T_SOLVE interval at the end of the Gram).  false: a strip wait gave up (~30 s,
+// never expected) and the strip was factored incomplete -- the caller redoes the Gram, the factor
+// and the solve without the pipeline (r06; was SCS_ERR_STATE)
+bool solve_factored(scs_ctx* c, double* rhs, hipEvent_t e0) {
   int info = 0, late = 0;
   HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
   if (c->gp_flag) HCK(hipMemcpyAsync(&late, c->gp_flag, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
-  if (late) {
-    HCK(hipMemsetAsync(c->gp_flag, 0, sizeof(int), c->st));
-    fail(c, SCS_ERR_STATE, "pipelined factor: a strip wait timed out (the strip was factored incomplete)");
+  if (late || fault_late(8)) {
+    if (c->gp_flag) HCK(hipMemsetAsync(c->gp_flag, 0, sizeof(int), c->st));
+    ++c->fb[SCS_FB_PIPE_REDO];
+    tend(c, T_SOLVE, e0);
+    return false;
   }
   if (info == 0) {
-    HCK(chol_solve(c->G, c->mpad, c->mpad, c->W, rhs, c->ysol, &c->caux, c->st));
+    chol_solve_checked(c, rhs);
     solve_flag_copy(c);
     c->lu_fallback_used = false;
     tend(c, T_SOLVE, e0);
-    return;
+    return true;
   }
   solve_lu_fallback(c, rhs, e0);
+  return true;
 }
 
 // the main Gram launch (scheduled when gram_schedule built a work list)
@@ -2019,10 +2112,10 @@ void ggn_sample_direction(scs_ctx* c, const double* xh) {
     qr_run(c, c->qrM, np1, c->bS);
   } else {
     HCK(lu_aux_init(&c->lu, np1, c->st));
-    HCK(lu_factor(c->Ms, np1, n1, np1, &c->lu, c->cinfo, c->st));
-    HCK(hipMemcpyAsync(&info, c->cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
-    sync(c);
-    if (info < 0) fail(c, SCS_ERR_HIP, "LU: the cooperative panel's candidate exchange timed out (info %d)", info);
+    info = lu_factor_checked(c, c->Ms, np1, n1, np1, c->cinfo, [&] {   // the system assembled again
+      HCK(launch_ggn_sample_assemble(c->Ps, c->NpS, c->gN, c->hN, c->wN, c->uN, nullptr, N, c->Ms, c->n1pad, c->bS,
+                                     c->st));
+    });
     if (info != 0) fail(c, SCS_ERR_SOLVE, "SingularException(%d)", info);
     HCK(lu_solve(c->Ms, np1, np1, &c->lu, c->bS, c->st));
   }
@@ -2139,9 +2232,11 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
         const hipEvent_t es = gram_factor_pipelined(c, c->hN, c->gN, c->gtmp);
         if (c->gfix) grad_f_dev(c, xh, c->x, c->gtmp);   // ∇fx replaces the fused Aᵀg
         HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
-        solve_factored(c, c->gq, es);
-        HCK(launch_neg(c->gq, m, c->d, c->st));
-        goto newton_tail;
+        if (solve_factored(c, c->gq, es)) {
+          HCK(launch_neg(c->gq, m, c->d, c->st));
+          goto newton_tail;
+        }
+        // (a strip wait gave up: the unpipelined Gram, factor and solve below)
       }
       gram_and_reduce(c, c->hN, c->gN, c->gtmp);
     }
@@ -2156,9 +2251,11 @@ void step_newton(scs_ctx* c, const double* xh, int64_t iter, double* x_new, doub
       ensure_gram(c);
       const hipEvent_t es = gram_factor_pipelined(c, c->wN, c->vN, c->gtmp);
       HCK(launch_axpby(c->gtmp, c->lam, c->gr, m, c->gq, c->st));
-      solve_factored(c, c->gq, es);
-      HCK(launch_neg(c->gq, m, c->d, c->st));
-      goto newton_tail;
+      if (solve_factored(c, c->gq, es)) {
+        HCK(launch_neg(c->gq, m, c->d, c->st));
+        goto newton_tail;
+      }
+      // (a strip wait gave up: the unpipelined Gram, factor and solve below)
     }
     gram_and_reduce(c, c->wN, c->vN, c->gtmp);   // Gram + Jᵀr in one pass over A
   }
@@ -3941,23 +4038,23 @@ int scs_lu_eval(scs_ctx* c, int64_t n, const double* A, const double* b, double*
     }
     double* M = c->luM;
     double* bb = c->lub;
-    int* dinfo = c->luinfo;
-    HCK(hipMemsetAsync(M, 0, sizeof(double) * np * np, c->st));
-    HCK(hipMemsetAsync(bb, 0, sizeof(double) * np, c->st));
-    HCK(hipMemsetAsync(dinfo, 0, sizeof(int), c->st));
-    HCK(hipMemcpy2DAsync(M, sizeof(double) * np, A, sizeof(double) * n, sizeof(double) * n, n, hipMemcpyHostToDevice,
-                         c->st));
-    HCK(hipMemcpyAsync(bb, b, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    auto upload = [&] {   // (also the system of a column-step redo, lu_factor_checked)
+      HCK(hipMemsetAsync(M, 0, sizeof(double) * np * np, c->st));
+      HCK(hipMemsetAsync(bb, 0, sizeof(double) * np, c->st));
+      HCK(hipMemcpy2DAsync(M, sizeof(double) * np, A, sizeof(double) * n, sizeof(double) * n, n,
+                           hipMemcpyHostToDevice, c->st));
+      HCK(hipMemcpyAsync(bb, b, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    };
+    upload();
     HCK(lu_aux_init(&c->lu, np, c->st));
     hipEvent_t e0;
     tbegin(c, T_SOLVE, &e0);
-    HCK(lu_factor(M, np, n, np, &c->lu, dinfo, c->st));
-    int hinfo = 0;
-    HCK(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
-    sync(c);
+    const int hinfo = lu_factor_checked(c, M, np, n, np, c->luinfo, upload);
     if (hinfo == 0) HCK(lu_solve(M, np, np, &c->lu, bb, c->st));
     tend(c, T_SOLVE, e0);
-    HCK(hipMemcpyAsync(x, bb, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
+    // x only without a zero pivot; ipiv whenever the factorization completed -- dgetrf's pivots with
+    // info > 0 too (the header's contract)
+    if (hinfo == 0) HCK(hipMemcpyAsync(x, bb, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
     if (ipiv) HCK(hipMemcpyAsync(ipiv, c->lu.ipiv, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->st));
     sync(c);
     if (info) *info = hinfo;
@@ -4097,6 +4194,20 @@ int scs_timing_reset(scs_ctx* c) {
       c->tcalls[i] = 0;
     }
   });
+}
+
+int scs_fallback_counts(scs_ctx* c, int64_t* counts, int n) {
+  if (!c) return SCS_ERR_ARG;
+  if (!counts || n < 0) {
+    c->err = "scs_fallback_counts: bad arguments";
+    return SCS_ERR_ARG;
+  }
+  for (int i = 0; i < n; ++i) counts[i] = 0;
+  // a multi-device context: the sum over its devices
+  std::vector<scs_ctx*> cs = is_group(c) ? c->subs : std::vector<scs_ctx*>{c};
+  for (scs_ctx* s_ : cs)
+    for (int i = 0; i < n && i < SCS_FB_N; ++i) counts[i] += s_->fb[i];
+  return SCS_OK;
 }
 
 int scs_sync(scs_ctx* c) {

@@ -157,6 +157,7 @@ _SIGS = {
     "scs_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "scs_timing_get": (C.c_int, [C.c_void_p, C.POINTER(Timing)]),
     "scs_timing_reset": (C.c_int, [C.c_void_p]),
+    "scs_fallback_counts": (C.c_int, [C.c_void_p, c_i64p, C.c_int]),
     "scs_kernel_names": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]),
     "scs_sync": (C.c_int, [C.c_void_p]),
 }
@@ -245,6 +246,16 @@ class Context:
         s = C.c_void_p()
         self.check(lib.scs_get_stream(self.h, C.byref(s)))
         return s.value
+
+    FALLBACKS = ("lu_coop_refused", "lu_coop_redo", "solve_blocks", "qr_blocks", "chain_redo", "pipe_redo")
+
+    def fallback_counts(self):
+        """The fallbacks taken instead of failing since the context was created (scs_fallback_counts;
+        SCS_FB_* in include/scsopt.h), as {name: count}."""
+        n = len(self.FALLBACKS)
+        out = (C.c_int64 * n)()
+        self.check(lib.scs_fallback_counts(self.h, out, n))
+        return dict(zip(self.FALLBACKS, (int(v) for v in out)))
 
     def kernel_names(self):
         """(main Gram kernel, sparse product kernel) of the latest launches, rocprofv3's names."""

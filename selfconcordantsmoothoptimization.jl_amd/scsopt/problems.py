@@ -564,7 +564,8 @@ class Problem:
 
 def lu_solve(A, b, device=0, ctx=None):
     """Julia's `A \\ b` for a dense square matrix (getrf + getrs) on the device: the hand-written
-    blocked LU with partial pivoting (lu.hip).  Returns (x, ipiv (0-based), info)."""
+    blocked LU with partial pivoting (lu.hip).  Returns (x, ipiv (0-based), info); with info > 0 (a
+    zero pivot, dgetrf's info) x is None and ipiv holds dgetrf's pivots."""
     A = np.ascontiguousarray(A, dtype=np.float64)
     b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
     n = A.shape[0]
@@ -576,5 +577,5 @@ def lu_solve(A, b, device=0, ctx=None):
     info = C.c_int()
     ctx.check(_lib.lib.scs_lu_eval(ctx.h, n, dptr(A), dptr(b), dptr(x), ipiv.ctypes.data_as(_lib.c_i32p),
                                    C.byref(info)))
-    return x, ipiv, int(info.value)
+    return (x if info.value == 0 else None), ipiv, int(info.value)
 

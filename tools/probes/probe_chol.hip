@@ -15,6 +15,9 @@ hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, 
 #ifdef CHOL_PROF
 extern __device__ long long chol_prof[128];
 #endif
+#ifdef CHOL_DTIME
+extern __device__ long long chol_dtime[2 * 1024];
+#endif
 }
 
 __global__ void spd_fill(double* G, int64_t n) {   // G = I*n + small symmetric noise (upper valid)
@@ -126,6 +129,22 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e1, sq)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
       int hinfo; CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost));
       printf("n=%ld factor: %.2f ms (info %d)\n", (long)n, ms, hinfo);
+#ifdef CHOL_DTIME
+      {   // the diagonal kernels' in-kernel time (entry -> exit of wave 0), and the gap from one's exit
+          // to the next one's entry (the rest of the chain between them)
+        std::vector<long long> dt(2 * 1024);
+        CK(hipMemcpyFromSymbol(dt.data(), HIP_SYMBOL(scs::chol_dtime), sizeof(long long) * 2 * 1024));
+        double run = 0, gap = 0, rmax = 0;
+        for (int k = 0; k < nb; ++k) {
+          const double r = (dt[2 * k + 1] - dt[2 * k]) / 100.0;
+          run += r;
+          rmax = r > rmax ? r : rmax;
+          if (k > 0) gap += (dt[2 * k] - dt[2 * k - 1]) / 100.0;
+        }
+        printf("n=%ld diag in-kernel: avg %.1f us, max %.1f us; exit->next entry avg %.1f us (%d blocks)\n", (long)n,
+               run / nb, rmax, gap / (nb - 1), nb);
+      }
+#endif
       if (rep == 0) {
         unsigned long long* dsum;
         unsigned long long hs[2];
