@@ -801,11 +801,14 @@ static int chol_wpar() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
-// SCS_CHOL_DIAG_PACK (read per call; default on): the packed-LDS diagonal kernel (LayPack, r06);
-// 0 = r05's full 128 x 129 LDS copy (LayFull).  The same U, W and pivots either way.
+// SCS_CHOL_DIAG_PACK (read per call; default off): 1 = the packed-LDS diagonal kernel (LayPack, r06),
+// else r05's full 128 x 129 LDS copy (LayFull).  The same U, W and pivots either way (probe bit sums).
+// Measured (profiles/r06/chol_pack/): LayPack fits beside one bulk workgroup and starts sooner, but
+// sharing the CU's SIMDs with the bulk's MFMA waves it runs 128 us instead of 51 (in-kernel, m = 16384):
+// factor 33.0-33.3 vs 31.9-32.1 ms, m = 8192 8.3 vs 7.6 ms -- so LayFull stays the default.
 static bool chol_diag_pack() {
   const char* e = getenv("SCS_CHOL_DIAG_PACK");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 constexpr int CHOL_DIAG_PACK_LDS = (LayPack::words + (CB / SB) * SB * SB) * (int)sizeof(double);   // 94,720 B
@@ -871,10 +874,13 @@ static int outer_block();
 // none above: m = 16384 38.6 vs 39.3 ms, m = 32768 212.6 vs 228.8 ms with it (the bulk stream
 // bounds those factors; profiles/r03/chol/bounded/).  Which CUs a harvested part lacks only
 // changes how many are left free.
+// SCS_CHOL_BULK_SKIP_XCC (r06, A/B): a bit mask of the XCDs where the skip set applies (default all)
 static unsigned bulk_skip_mask(int nblk) {
   const char* e = getenv("SCS_CHOL_BULK_SKIP");
-  if (e) return (unsigned)strtoul(e, nullptr, 0);
-  return nblk <= 64 ? 0x20u : 0u;
+  const char* x = getenv("SCS_CHOL_BULK_SKIP_XCC");
+  const unsigned xm = x ? ((unsigned)strtoul(x, nullptr, 0) & 0xffu) << 24 : 0u;
+  if (e) return ((unsigned)strtoul(e, nullptr, 0) & 0xffffu) | xm;
+  return nblk <= 64 ? (0x20u | xm) : 0u;
 }
 
 static hipError_t create_bulk_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }

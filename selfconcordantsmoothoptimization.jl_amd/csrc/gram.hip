@@ -76,11 +76,16 @@ __device__ __forceinline__ int bnd_claim(unsigned* ctr, int ntiles) {
   }
   return ntiles;
 }
+// skip: bits 0..15 the CU ids left free, bits 24..31 the XCDs (HW_REG_XCC_ID) where that applies
+// (0: every XCD; r06, so that a few CUs of the chip -- not one per shader engine -- can be left free)
 __device__ __forceinline__ int bnd_first(unsigned* ctr, unsigned skip, int ntiles, int* s) {
   if (threadIdx.x == 0) {
     const unsigned cu = ((unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 15u;   // HW_REG_HW_ID
+    const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;       // HW_REG_XCC_ID
+    const unsigned xm = skip >> 24;
+    const bool here = ((skip >> cu) & 1u) && (xm == 0 || ((xm >> xcc) & 1u));
     const unsigned arr = atomicAdd(ctr + 8, 1u);
-    *s = (((skip >> cu) & 1u) && arr + 1 < gridDim.x) ? -1 : bnd_claim(ctr, ntiles);
+    *s = (here && arr + 1 < gridDim.x) ? -1 : bnd_claim(ctr, ntiles);
   }
   __syncthreads();
   return *s;
