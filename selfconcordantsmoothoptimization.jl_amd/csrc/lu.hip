@@ -1147,7 +1147,8 @@ static int lu_inv_mode() {
   return e ? atoi(e) : 2;
 }
 
-// SCS_LU_OB (read per call): panels per outer block.  4 (default): the trailing matrix takes ONE update per
+// SCS_LU_OB (read per call): an on/off switch -- 1 = per-panel updates, any other value (default) = outer
+// blocks of LU_OB = 4 panels (the only outer size built: 2, 3 or 8 also run with 4).  With 4 the trailing matrix takes ONE update per
 // four panels with K = 512 (r05; the K = 128 updates ran at ~26 TF/s on the C read-modify-write: the
 // n = 8192 updates 13.8 -> 8.0 ms, factor + solve 83.7-83.9 -> 82.0-82.9 ms, n = 16384 250.8-251.2 ->
 // 216.8-217.1 ms); 1: the r02 per-panel updates.  Recorded in the aux for lu_solve (its forward steps follow the
