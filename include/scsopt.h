@@ -370,9 +370,11 @@ typedef struct scs_history {
  * per batch (the full batch, or the scs_set_batches list in order), the
  * reference's termination tests and history pushes.  x_star is
  * model.x (the comparison solution).  Outputs: final x, *n_hist entries,
- * *epochs (Solution.epochs).  With test data, hist->fvaltest gets ftest(x) at
- * every push.  Metrics / verbose printing stay in the host loop
- * (scsopt.iterate).  Requires scs_method_init.                              */
+ * *epochs (Solution.epochs).  Metrics / verbose printing stay in the host loop
+ * (scsopt.iterate).  Requires scs_method_init.
+ * ABI note (r05 -> r06): scs_iterate reads the six-field (r03) history and never writes
+ * fvaltest; a context holding test data (scs_set_test_*) is refused with SCS_ERR_STATE --
+ * callers built against the r04 seven-field struct call scs_iterate_ex instead.          */
 int scs_iterate(scs_ctx* ctx, const double* x0, const double* x_star, int64_t max_epoch, double x_tol,
                 double f_tol, int rel_kind, double* x_out, const scs_history* hist, int64_t* n_hist,
                 int64_t* epochs);

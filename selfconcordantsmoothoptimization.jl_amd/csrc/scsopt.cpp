@@ -3465,6 +3465,15 @@ int scs_step_grad(scs_ctx* c, const double* x, const double* x_prev, int64_t ite
 // scs_iterate: the r03 six-field history (obj .. times) -- fvaltest is never read or written
 int scs_iterate(scs_ctx* c, const double* x0, const double* x_star, int64_t max_epoch, double x_tol, double f_tol,
                 int rel_kind, double* x_out, const scs_history* h, int64_t* n_hist, int64_t* epochs_out) {
+  // r05 made this entry the six-field (r03) layout: it never writes fvaltest.  A context that holds test
+  // data expects Solution.fvaltest, which only scs_iterate_ex returns -- refused rather than dropped
+  // silently (r04 C callers: call scs_iterate_ex with sizeof(scs_history))
+  int on = 0;
+  if (c && scs_has_test(c, &on) == SCS_OK && on) {
+    c->err = "scs_iterate has no fvaltest (six-field history) and this context holds test data: call scs_iterate_ex "
+             "with sizeof(scs_history)";
+    return SCS_ERR_STATE;
+  }
   return scs_iterate_ex(c, x0, x_star, max_epoch, x_tol, f_tol, rel_kind, x_out, h, offsetof(scs_history, fvaltest),
                         n_hist, epochs_out);
 }

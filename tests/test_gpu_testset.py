@@ -189,3 +189,34 @@ def test_multi_device_context_test_set():
     sa = scsopt.iterate(meth(), a, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=5, verbose=0)
     sb = scsopt.iterate(meth(), b, "l1", scsopt.PHuberSmootherL1L2(1.0), max_epoch=5, verbose=0)
     assert sa.fvaltest == sb.fvaltest and sa.obj == sb.obj and len(sa.fvaltest) == len(sa.obj)
+
+
+def test_six_field_scs_iterate_refuses_test_data():
+    """ABI note: scs_iterate reads the six-field (r03) history and never writes fvaltest,
+    so with test data held it refuses (SCS_ERR_STATE, pointing at scs_iterate_ex) instead of returning
+    a Solution whose fvaltest was silently dropped; without test data it runs as before."""
+    import ctypes as C
+    from scsopt import _lib
+    from scsopt.iterate import init_method
+    N, Nt, m = 400, 120, 30
+    A, y, At, yt = _data("lqn", N, Nt, m, 5)
+    f, out = _kinds("lqn", N)[:2]
+    x0 = np.random.default_rng(6).standard_normal(m) * 0.2
+    hm = scsopt.PHuberSmootherL1L2(1.0)
+    for with_test in (True, False):
+        kw = dict(Atest=At, ytest=yt) if with_test else {}
+        p = scsopt.Problem(A, y, x0, f, 1e-3, out_fn=out, **kw)
+        M = scsopt.ProxLQNSCORE(m=5)
+        p.configure("l1", hm)
+        init_method(M, p)
+        hist = {k: np.empty(9) for k in ("obj", "fval", "pri_res_norm", "rel", "objrel", "times", "fvaltest")}
+        h = _lib.History(*(hist[k].ctypes.data_as(_lib.c_dp) for k in hist))
+        xo, nh, ep = np.empty(m), C.c_int64(), C.c_int64()
+        x0c, xs = np.ascontiguousarray(x0), np.zeros(m)
+        rc = _lib.lib.scs_iterate(p.ctx.h, x0c.ctypes.data_as(_lib.c_dp), xs.ctypes.data_as(_lib.c_dp), 4, 0.0, 0.0, 0,
+                                  xo.ctypes.data_as(_lib.c_dp), C.byref(h), C.byref(nh), C.byref(ep))
+        if with_test:
+            assert rc == _lib.SCS_ERR_STATE
+            assert "scs_iterate_ex" in _lib.lib.scs_last_error(p.ctx.h).decode()
+        else:
+            assert rc == _lib.SCS_OK and ep.value == 4
