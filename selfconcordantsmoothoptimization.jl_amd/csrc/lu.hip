@@ -417,6 +417,17 @@ constexpr int64_t LUC_CAND = 0, LUC_ABORT = 2 * LUC_MAXWG * 4, LUC_CROW = LUC_AB
 constexpr int64_t LUC_ROWJ = LUC_CROW + 2 * LUC_MAXWG * LB * 2, LUC_WORDS = LUC_ROWJ + 2 * LB * 2;
 typedef __attribute__((address_space(1))) unsigned long long luc_gu64;
 
+#ifdef LU_PROF
+// probe_lu -DLU_PROF: workgroup 0's thread 0 splits each column of every cooperative panel into
+// sweep | pick + stage | barrier | update | publish (s_memrealtime, 100 MHz ticks, summed) + columns
+__device__ unsigned long long lu_prof[8];
+#define LUP_MARK(v) const long long v = (g == 0 && tid == 0) ? (long long)__builtin_amdgcn_s_memrealtime() : 0
+#define LUP_SET(v) v = (g == 0 && tid == 0) ? (long long)__builtin_amdgcn_s_memrealtime() : 0
+#else
+#define LUP_MARK(v)
+#define LUP_SET(v)
+#endif
+
 __device__ __forceinline__ void luc_put(unsigned long long* p, unsigned long long x) {
   __hip_atomic_store((luc_gu64*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -440,7 +451,12 @@ __device__ __forceinline__ double luc_get_d(const unsigned long long* p, unsigne
 // holding lane), before the candidate's own granules
 // NT: threads per workgroup -- 256 (128 rows, up to 128 workgroups) or 512 (256 rows, up to 64 workgroups:
 // half the grid to sweep and to wait for, two waves per SIMD)
-template <bool WIDE, int NT>
+// EARLY (r06, default; SCS_LU_COOP_EARLY=0 off; !WIDE only): each column step updates column j + 1 of
+// its rows first, publishes the column's candidate RECORD, then updates the other columns and
+// publishes the rows -- so the records every workgroup's sweep waits for leave ~1 update earlier,
+// and the rows (fetched after the sweep, or prefetched) land while the sweep runs.  Every element
+// takes the same operations: the same factor and pivots bit for bit.
+template <bool WIDE, int NT, bool EARLY = false>
 __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
                                                               int64_t c0, int64_t h, unsigned long long* gran,
                                                               unsigned tagbase,
@@ -452,6 +468,8 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
   __shared__ double su_u[LB], su_rj[LB];   // the pivot row, the displaced row j (staged by wave 0)
   __shared__ double su_c[LB], su_n[LB];    // WIDE: this workgroup's candidate row and row j + 1 to publish
   __shared__ int s_p, s_alive;
+  __shared__ double ev[2][NT / 64];   // EARLY: the wave argmax partials by column parity
+  __shared__ int ei[2][NT / 64];
   // workgroup 0: the block's interchanges composed into row moves as the pivots come (lu_perm_kernel's
   // bookkeeping, one swap per column behind the column's publication): rows r0 .. r0+127, and the
   // touched rows below the block as (row, content)
@@ -556,14 +574,82 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
       luc_put(gp + 2, t | (unsigned)bi);
     }
   };
+  // EARLY: the candidate record of column jn (column jn of the rows already updated), returning the
+  // workgroup's candidate row; then, after the rest of the update, its row and row jn
+  auto publish_record = [&](int jn) -> int {
+    double bv = -1.0;
+    int bi = INT_MAX, bw_dummy = g;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const int i = base + RP * ps;
+      if (i >= jn && i < h && q == (jn >> 4)) {
+        const double a = fabs(sel(v[ps], jn & 15));
+        if (lu_better(a, i, bv, bi)) {
+          bv = a;
+          bi = i;
+        }
+      }
+    }
+    // the workgroup's argmax with ONE barrier: the wave partials go to a slot by column parity, last
+    // read two columns ago (the column loop's barrier lies between), so no barrier before the writes
+    lu_wave_argmax(bv, bi, bw_dummy);
+    {
+      const int wv = tid >> 6, sl = jn & 1;
+      if (lane == 0) {
+        ev[sl][wv] = bv;
+        ei[sl][wv] = bi;
+      }
+      __syncthreads();
+      bv = ev[sl][0];
+      bi = ei[sl][0];
+#pragma unroll
+      for (int k = 1; k < NT / 64; ++k)
+        if (lu_better(ev[sl][k], ei[sl][k], bv, bi)) {
+          bv = ev[sl][k];
+          bi = ei[sl][k];
+        }
+    }
+    if (tid == 0) {
+      const unsigned long long t = (unsigned long long)(tagbase + (unsigned)(jn + 1)) << 32;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
+      unsigned long long* gp = gran + LUC_CAND + ((int64_t)(jn & 1) * LUC_MAXWG + g) * 4;
+      luc_put(gp + 0, t | (bits & 0xffffffffull));
+      luc_put(gp + 1, t | (bits >> 32));
+      luc_put(gp + 2, t | (unsigned)bi);
+    }
+    return bi;
+  };
+  auto publish_rows = [&](int jn, int bi) {
+    const int par = jn & 1;
+    const unsigned tag = tagbase + (unsigned)(jn + 1);
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const int i = base + RP * ps;
+      if (i == bi) {
+        unsigned long long* rp = gran + LUC_CROW + (((int64_t)par * LUC_MAXWG + g) * LB + cq) * 2;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) luc_put_d(rp + 2 * c, tag, v[ps][c]);
+      }
+      if (i == jn) {
+        unsigned long long* rp = gran + LUC_ROWJ + ((int64_t)par * LB + cq) * 2;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) luc_put_d(rp + 2 * c, tag, v[ps][c]);
+      }
+    }
+  };
   if (g == 0) {
     if (tid < LB) ptop[tid] = (int)r0 + tid;
     if (tid == 0) pnb = 0;
   }
   publish(0);   // (its barriers order the initialisation above)
+#ifdef LU_PROF
+  long long lp_acc[5] = {0, 0, 0, 0, 0};
+  long long lp_t1 = 0, lp_t2 = 0;
+#endif
   for (int j = 0; j < LB; ++j) {
     const int par = j & 1;
     const unsigned tag = tagbase + (unsigned)(j + 1);
+    LUP_MARK(lp_t0);
     // 1. wave 0 alone: sweep the G candidates of column j until all carry this column's tag, pick the
     //    pivot, and stage the pivot row (and the displaced row j where this workgroup holds row p) in LDS
     if (tid < 64) {
@@ -623,6 +709,9 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
         }
         __builtin_amdgcn_s_sleep(1);
       }
+#ifdef LU_PROF
+      if (g == 0 && tid == 0) lp_t1 = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
       lu_wave_argmax(cv, ci, cw);
       // a row of 128 doubles as 256 granules: lane l takes columns 2l, 2l + 1
       auto stage = [&](const unsigned long long* rp, double* dst) {
@@ -667,9 +756,13 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
         s_p = p;
         s_alive = alive ? 1 : 0;
       }
+#ifdef LU_PROF
+      if (g == 0 && tid == 0) lp_t2 = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
     }
     __syncthreads();
     if (!s_alive) return;   // (every wave: the abort word and info are set)
+    LUP_MARK(lp_t3);
     const int p = s_p;
     double u[16];
 #pragma unroll
@@ -682,6 +775,9 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
       if (!scale && *info == 0) *info = (int)(r0 + j + 1);
     }
     // 2. row j <- u, row p <- the displaced row j, every row i > j: l = a_ij / u_j, a_ic -= l·u_c
+    //    (EARLY: column j + 1 first, its record, then the other columns)
+    const int jn = j + 1;
+    double lv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {
       const int i = base + RP * ps;
@@ -699,14 +795,55 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
       }
       const double x = __shfl(sel(v[ps], j & 15), (tid & ~7) | (j >> 4), 64);
       const double l = scale ? (fabs(piv) >= 2.2250738585072014e-308 ? x * rp : x / piv) : x;
+      lv[ps] = l;
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const int col = cq + c;
-        if (col > j) v[ps][c] -= l * u[c];
-        else if (col == j) v[ps][c] = l;
+        if (EARLY) {
+          if (col == jn) v[ps][c] -= l * u[c];
+          else if (col == j) v[ps][c] = l;
+        } else {
+          if (col > j) v[ps][c] -= l * u[c];
+          else if (col == j) v[ps][c] = l;
+        }
       }
     }
-    if (j + 1 < LB) publish(j + 1);
+#ifdef LU_PROF
+    long long lp_t4 = 0;
+#endif
+    if constexpr (EARLY) {
+      const int bi = jn < LB ? publish_record(jn) : INT_MAX;
+      // the rest of the update -- first the two rows the next column's consumers fetch (the candidate row
+      // bi and row jn), published at once, then the others
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int ps = 0; ps < 4; ++ps) {
+          const int i = base + RP * ps;
+          if (i <= j || i >= h || ((i == bi || i == jn) != (pass == 0))) continue;
+#pragma unroll
+          for (int c = 0; c < 16; ++c) {
+            const int col = cq + c;
+            if (col > j && col != jn) v[ps][c] -= lv[ps] * u[c];
+          }
+        }
+        if (pass == 0 && jn < LB) publish_rows(jn, bi);
+      }
+      LUP_SET(lp_t4);
+    } else {
+      LUP_SET(lp_t4);
+      if (j + 1 < LB) publish(j + 1);
+    }
+#ifdef LU_PROF
+    if (g == 0 && tid == 0) {
+      const long long t5 = (long long)__builtin_amdgcn_s_memrealtime();
+      lp_acc[0] += lp_t1 - lp_t0;
+      lp_acc[1] += lp_t2 - lp_t1;
+      lp_acc[2] += lp_t3 - lp_t2;
+      lp_acc[3] += lp_t4 - lp_t3;
+      lp_acc[4] += t5 - lp_t4;
+    }
+#endif
     if (g == 0 && tid < 64 && p != j) {   // compose interchange j (rows r0+j <-> r0+p)
       if (p < LB) {
         if (lane == 0) {
@@ -736,6 +873,12 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
       }
     }
   }
+#ifdef LU_PROF
+  if (g == 0 && tid == 0) {
+    for (int q = 0; q < 5; ++q) atomicAdd(&lu_prof[q], (unsigned long long)lp_acc[q]);
+    atomicAdd(&lu_prof[5], (unsigned long long)LB);
+  }
+#endif
   if (g == 0 && tid < 64) {   // the moves: top rows (ascending), then the rows below (list order)
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1093,7 +1236,9 @@ static int lu_panel_mode() {
 static hipError_t lu_coop_attr() {   // the dynamic LDS above the 64 KiB default, once per process
   static hipError_t done = [] {
     const void* ks[] = {(const void*)lu_panel_coop_kernel<true, 256>, (const void*)lu_panel_coop_kernel<false, 256>,
-                        (const void*)lu_panel_coop_kernel<true, 512>, (const void*)lu_panel_coop_kernel<false, 512>};
+                        (const void*)lu_panel_coop_kernel<true, 512>, (const void*)lu_panel_coop_kernel<false, 512>,
+                        (const void*)lu_panel_coop_kernel<false, 256, true>,
+                        (const void*)lu_panel_coop_kernel<false, 512, true>};
     hipError_t e = hipSuccess;
     for (const void* f : ks)
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LUC_LDS);
@@ -1132,6 +1277,11 @@ static unsigned lu_coop_spin() {   // read per call: SCS_LU_COOP_SPIN (sweeps; 0
 // runs as column steps); 0 = a plain launch, residency by the 96 KiB of LDS and the CU-count check only
 static bool lu_coop_api() {
   const char* e = getenv("SCS_LU_COOP_LAUNCH");
+  return !(e && e[0] == '0');
+}
+
+static bool lu_coop_early() {   // read per call (A/B): SCS_LU_COOP_EARLY=0 publishes rows before the record
+  const char* e = getenv("SCS_LU_COOP_EARLY");
   return !(e && e[0] == '0');
 }
 
@@ -1175,8 +1325,11 @@ static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUA
               lu_coop_attr() == hipSuccess;
   if (coop) {
     const bool wide = lu_coop_wide();
-    auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512> : lu_panel_coop_kernel<false, 512>)
-                           : (wide ? lu_panel_coop_kernel<true, 256> : lu_panel_coop_kernel<false, 256>);
+    const bool early = !wide && lu_coop_early();
+    auto kern = cnt == 512 ? (wide ? lu_panel_coop_kernel<true, 512>
+                                   : (early ? lu_panel_coop_kernel<false, 512, true> : lu_panel_coop_kernel<false, 512>))
+                           : (wide ? lu_panel_coop_kernel<true, 256>
+                                   : (early ? lu_panel_coop_kernel<false, 256, true> : lu_panel_coop_kernel<false, 256>));
     double* pA = A;
     int64_t pld = ld, pr0 = r0, pc0 = c0, ph = h;
     unsigned long long* pgran = a->gran;
