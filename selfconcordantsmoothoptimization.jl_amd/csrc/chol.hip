@@ -1468,6 +1468,15 @@ static bool c12_split() {
 // sharing 8 + 8 operand panels instead of one row sharing 1 + 64: at K = 1024 a panel is 1 MiB, so
 // the row-major band re-fetched its A2 panels from HBM.  m = 65536 factor 1498-1510 -> 1427-1436 ms,
 // m = 32768 204.0-204.7 -> 201.8-202.8 ms, U / W bitwise equal (profiles/r04/sbl/).
+// SCS_CHOL_C12B_CHUNK (read per call; 0 = one launch): where the bulk stream launches plainly (no skip
+// set: m >= 16384), C12b as launches of this many tiles.  One launch of thousands of tiles refills every
+// slot it frees, and the chain's diagonal kernel then waited for all of it, once per outer block
+// (profiles/r06/chol_pack/); between launches of about one round the CUs drain and the chain gets one.
+static int c12b_chunk() {
+  const char* e = getenv("SCS_CHOL_C12B_CHUNK");
+  return e ? atoi(e) : 0;
+}
+
 static bool chol_sbl() {
   const char* e = getenv("SCS_CHOL_SBL");
   return !(e && e[0] == '0');
@@ -1583,9 +1592,16 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
       unsigned* ctr = bulk_ctr(a, sb, &e);
       const bool sbo = split && a->sbl && (2 * OB) % 8 == 0 && nc % 8 == 0 && chol_sbl();
       const unsigned mk = bulk_mask(a, ntri - n2a);
-      if (e == hipSuccess)
-        e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, (sbo ? a->sbl : trilist) + n2a,
-                                ntri - n2a, trail, ld, 2 | 4, ctr, mk, bulk_slots(a, mk), sb, true);
+      const int2* tl = (sbo ? a->sbl : trilist) + n2a;
+      const int tot = ntri - n2a, ck = c12b_chunk();
+      if (ck > 0 && mk == 0) {   // (r06, A/B) C12b as launches of ck tiles: the chain finds CUs between them
+        for (int t0 = 0; t0 < tot && e == hipSuccess; t0 += ck)
+          e = gram_launch_gen(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, tl + t0,
+                              std::min(ck, tot - t0), trail, ld, 2 | 4, sb);
+      } else if (e == hipSuccess) {
+        e = gram_launch_bounded(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, tl, tot, trail, ld, 2 | 4,
+                                ctr, mk, bulk_slots(a, mk), sb, true);
+      }
     }
     if (e == hipSuccess) e = hipEventRecord(a->ev2, sb);
     if (e != hipSuccess) return e;
