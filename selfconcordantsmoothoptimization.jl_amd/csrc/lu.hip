@@ -28,6 +28,7 @@
 // Layout: A is npad x npad, row stride ld >= npad, npad % 128 == 0.  Rows/columns
 // [n, npad) must be zero on entry; lu_factor puts ones on their diagonal (block-diag(A, I)).
 #include <climits>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -908,6 +909,396 @@ __global__ __launch_bounds__(NT) void lu_panel_coop_kernel(double* __restrict__ 
   }
 }
 
+// ---- the cooperative panel, block-deferred (r06; SCS_LU_COOP_BLK) -------------------------------------
+// The exchange, records, rows and interchanges of lu_panel_coop_kernel, but a column step j updates only
+// the columns of its 16-column block b = j / 16 right of j -- held, for each row, by ONE lane (q = b),
+// whose multiplier l = a_ij / u_j it forms itself (no shuffle) at compile-time register indices (the
+// block's 16 steps are unrolled).  The columns right of the block take the block's 16 rank-1 updates at
+// its end, in step order (what the column steps would have done to them, delayed):
+//   * the pivot rows as staged (sU) carry the block's columns current and the columns right of it as
+//     they stood at the block's start; their final values there are the 16-row unit-lower solve
+//     u_kc -= l_kk'·u_k'c (k' < k, ascending), formed by every workgroup from sU itself (no exchange);
+//   * a row at position i then takes a_ic -= l_ik·u_kc for the steps k < i of the block, ascending
+//     (the rows above the block: none; the block's pivot rows: those before them; all others: 16).
+// Every element sees the column steps' operations (x - l·u, contracted alike) in the same order: the
+// factor and pivots bit for bit (test_lu_panel_variants_bit_identical).  A row published for the next
+// column (its candidate, or row j + 1) is current in the block and stale right of it, which is what the
+// consumers' own deferred updates expect.  The column step costs ~(15 - j % 16) FMAs on one lane of eight
+// instead of 16 masked FMAs on all; the block's updates ~1024 FMAs per thread on the lanes right of it.
+template <class F, int... I>
+__device__ __forceinline__ void luc_unroll(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+// wave 0 of a cooperative panel's workgroup, column j: sweep the G candidate records until all carry the
+// column's tag (prefetching the best arrived candidate's row), pick the pivot by the step kernels' rule,
+// stage its row in su and, where this workgroup holds row p, the displaced row j in srj; returns p
+// (lu_panel_coop_kernel's step 1; a sweep past spin_max clears alive and sets info = -1 and the abort word)
+__device__ __forceinline__ int luc_sweep_stage(unsigned long long* gran, int j, unsigned tag, int nwg, int lane,
+                                               int lo, int hi, int pf_on, unsigned spin_max, int* info,
+                                               bool& alive, double* su, double* srj) {
+  const int par = j & 1;
+  auto give_up = [&]() {
+    if (lane == 0) {
+      *info = -1;
+      gran[LUC_ABORT] = 1;
+    }
+    alive = false;
+  };
+  double cv = -1.0;
+  int ci = INT_MAX, cw = -1;
+  const unsigned long long* gp = gran + LUC_CAND + (int64_t)par * LUC_MAXWG * 4;
+  int pf_w = -1;
+  unsigned long long pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0;
+  for (unsigned spins = 0;;) {
+    bool ok = true;
+    cv = -1.0;
+    ci = INT_MAX;
+    cw = -1;
+    double bv = -2.0;
+    int bi = INT_MAX, bw = -1;
+#pragma unroll
+    for (int t = 0; t < LUC_MAXWG / 64; ++t) {
+      const int w = lane + 64 * t;
+      if (w < nwg) {
+        const unsigned long long x0 = luc_get(gp + 4 * w + 0), x1 = luc_get(gp + 4 * w + 1),
+                                 x2 = luc_get(gp + 4 * w + 2);
+        const bool okw = (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag && (unsigned)(x2 >> 32) == tag;
+        ok = ok && okw;
+        double a = __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
+        int r = (int)(unsigned)x2;
+        if (!(a >= 0.0)) {
+          a = -1.0;
+          r = INT_MAX;
+        }
+        if (lu_better(a, r, cv, ci)) {
+          cv = a;
+          ci = r;
+          cw = w;
+        }
+        if (okw && a >= 0.0 && lu_better(a, r, bv, bi)) {
+          bv = a;
+          bi = r;
+          bw = w;
+        }
+      }
+    }
+    if (__all(ok)) break;
+    lu_wave_argmax(bv, bi, bw);
+    if (pf_on && bw >= 0 && bw != pf_w) {
+      const unsigned long long* rp = gran + LUC_CROW + ((int64_t)par * LUC_MAXWG + bw) * LB * 2 + 4 * lane;
+      pf0 = luc_get(rp);
+      pf1 = luc_get(rp + 1);
+      pf2 = luc_get(rp + 2);
+      pf3 = luc_get(rp + 3);
+      pf_w = bw;
+    }
+    if (++spins > spin_max) {
+      give_up();
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  lu_wave_argmax(cv, ci, cw);
+  auto stage = [&](const unsigned long long* rp, double* dst) {
+    for (unsigned spins = 0; alive;) {
+      bool ok = true;
+      const double d0 = luc_get_d(rp + 4 * lane, tag, ok), d1 = luc_get_d(rp + 4 * lane + 2, tag, ok);
+      if (__all(ok)) {
+        dst[2 * lane] = d0;
+        dst[2 * lane + 1] = d1;
+        return;
+      }
+      if (++spins > spin_max) give_up();
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  const unsigned long long* rowj_g = gran + LUC_ROWJ + (int64_t)par * LB * 2;
+  int p = ci;
+  const unsigned long long* urow = gran + LUC_CROW + ((int64_t)par * LUC_MAXWG + cw) * LB * 2;
+  if (cv < 0.0) {
+    p = j;
+    urow = rowj_g;
+  }
+  if (alive) {
+    const bool hit = cv >= 0.0 && cw == pf_w &&
+                     __all((unsigned)(pf0 >> 32) == tag && (unsigned)(pf1 >> 32) == tag &&
+                           (unsigned)(pf2 >> 32) == tag && (unsigned)(pf3 >> 32) == tag);
+    if (hit) {
+      su[2 * lane] = __longlong_as_double((long long)((pf0 & 0xffffffffull) | (pf1 << 32)));
+      su[2 * lane + 1] = __longlong_as_double((long long)((pf2 & 0xffffffffull) | (pf3 << 32)));
+    } else {
+      stage(urow, su);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (alive && su[j] == 0.0) {   // getf2: zero pivot -> row j, no interchange, no scaling
+    p = j;
+    stage(rowj_g, su);
+  }
+  if (alive && p != j && p >= lo && p < hi) stage(rowj_g, srj);
+  return p;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void lu_panel_blk_kernel(double* __restrict__ A, int64_t ld, int64_t r0,
+                                                             int64_t c0, int64_t h, unsigned long long* gran,
+                                                             unsigned tagbase, int* ipiv, int* info, int2* pairs,
+                                                             int* npairs, int pf_on, unsigned spin_max) {
+  constexpr int RW = NT / 2, RP = NT / 8, NBK = LB / 16;
+  __shared__ double sU[16][LB];    // the block's pivot rows as staged; at its end, final right of it
+  __shared__ double sL[RW][17];    // at a block's end: its multipliers of this workgroup's rows
+  __shared__ double su_rj[LB];
+  __shared__ double ev[2][NT / 64];
+  __shared__ int ei[2][NT / 64];
+  __shared__ int s_p, s_alive;
+  __shared__ int ptop[LB], pbrow[LB], pbval[LB], pnb;
+  const int tid = threadIdx.x, g = blockIdx.x, lane = tid & 63;
+  const int q = tid & 7, rr = tid >> 3, cq = 16 * q;
+  const int base = g * RW + rr;
+  if (gran[LUC_ABORT] != 0) return;
+  if (spin_max == 0) {
+    if (threadIdx.x == 0) {
+      *info = -1;
+      gran[LUC_ABORT] = 1;
+    }
+    return;
+  }
+  double v[4][16];
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+    const bool in = base + RP * ps < h;
+    const double* row = A + (r0 + (in ? base + RP * ps : 0)) * ld + c0 + cq;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(v[ps] + c) = in ? *(const v2d*)(row + c) : (v2d){0.0, 0.0};
+  }
+  bool alive = true;
+  // the candidate record of column jn (its column K = jn % 16 on the lanes q = jn / 16), one barrier
+  // (lu_panel_coop_kernel's publish_record); returns the workgroup's candidate row
+  auto record = [&](int jn, auto Kc) __attribute__((always_inline)) -> int {
+    constexpr int K = decltype(Kc)::value;
+    double bv = -1.0;
+    int bi = INT_MAX, bw_dummy = g;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const int i = base + RP * ps;
+      if (i >= jn && i < h && q == (jn >> 4)) {
+        const double a = fabs(v[ps][K]);
+        if (lu_better(a, i, bv, bi)) {
+          bv = a;
+          bi = i;
+        }
+      }
+    }
+    lu_wave_argmax(bv, bi, bw_dummy);
+    {
+      const int wv = tid >> 6, sl = jn & 1;
+      if (lane == 0) {
+        ev[sl][wv] = bv;
+        ei[sl][wv] = bi;
+      }
+      __syncthreads();
+      bv = ev[sl][0];
+      bi = ei[sl][0];
+#pragma unroll
+      for (int k = 1; k < NT / 64; ++k)
+        if (lu_better(ev[sl][k], ei[sl][k], bv, bi)) {
+          bv = ev[sl][k];
+          bi = ei[sl][k];
+        }
+    }
+    if (tid == 0) {
+      const unsigned long long t = (unsigned long long)(tagbase + (unsigned)(jn + 1)) << 32;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(bi == INT_MAX ? -1.0 : bv);
+      unsigned long long* gp = gran + LUC_CAND + ((int64_t)(jn & 1) * LUC_MAXWG + g) * 4;
+      luc_put(gp + 0, t | (bits & 0xffffffffull));
+      luc_put(gp + 1, t | (bits >> 32));
+      luc_put(gp + 2, t | (unsigned)bi);
+    }
+    return bi;
+  };
+  auto publish_rows = [&](int jn, int bi) __attribute__((always_inline)) {
+    const int par = jn & 1;
+    const unsigned tag = tagbase + (unsigned)(jn + 1);
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const int i = base + RP * ps;
+      if (i == bi) {
+        unsigned long long* rp = gran + LUC_CROW + (((int64_t)par * LUC_MAXWG + g) * LB + cq) * 2;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) luc_put_d(rp + 2 * c, tag, v[ps][c]);
+      }
+      if (i == jn) {
+        unsigned long long* rp = gran + LUC_ROWJ + ((int64_t)par * LB + cq) * 2;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) luc_put_d(rp + 2 * c, tag, v[ps][c]);
+      }
+    }
+  };
+  if (g == 0) {
+    if (tid < LB) ptop[tid] = (int)r0 + tid;
+    if (tid == 0) pnb = 0;
+  }
+  publish_rows(0, record(0, std::integral_constant<int, 0>{}));   // (its barrier orders the initialisation)
+  bool dead = false;
+  for (int b = 0; b < NBK; ++b) {
+    luc_unroll(
+        [&](auto JJc) __attribute__((always_inline)) {
+          constexpr int jj = decltype(JJc)::value;
+          if (dead) return;
+          const int j = 16 * b + jj;
+          const unsigned tag = tagbase + (unsigned)(j + 1);
+          if (tid < 64) {
+            const int p = luc_sweep_stage(gran, j, tag, (int)gridDim.x, lane, g * RW, g * RW + RW, pf_on, spin_max,
+                                          info, alive, sU[jj], su_rj);
+            if (lane == 0) {
+              s_p = p;
+              s_alive = alive ? 1 : 0;
+            }
+          }
+          __syncthreads();
+          if (!s_alive) {   // (every wave: the abort word and info are set)
+            dead = true;
+            return;
+          }
+          const int p = s_p;
+          const double piv = sU[jj][j];
+          const bool scale = (piv != 0.0);
+          const double rp = 1.0 / piv;
+          if (g == 0 && tid == 0) {
+            ipiv[r0 + j] = (int)(r0 + p);
+            if (!scale && *info == 0) *info = (int)(r0 + j + 1);
+          }
+          const bool mine = q == b;   // this lane holds the block's columns of its rows
+          double u[16];
+#pragma unroll
+          for (int c = jj + 1; c < 16; ++c) u[c] = sU[jj][16 * b + c];
+#pragma unroll
+          for (int ps = 0; ps < 4; ++ps) {
+            const int i = base + RP * ps;
+            if (i < j || i >= h) continue;
+            if (i == j) {
+              if (p != j) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) v[ps][c] = sU[jj][cq + c];
+              }
+              continue;
+            }
+            if (i == p) {
+#pragma unroll
+              for (int c = 0; c < 16; ++c) v[ps][c] = su_rj[cq + c];
+            }
+            if (mine) {
+              const double x = v[ps][jj];
+              const double l = scale ? (fabs(piv) >= 2.2250738585072014e-308 ? x * rp : x / piv) : x;
+              v[ps][jj] = l;
+#pragma unroll
+              for (int c = jj + 1; c < 16; ++c) v[ps][c] -= l * u[c];
+            }
+          }
+          if constexpr (jj == 15) {
+            if (b + 1 < NBK) {   // the block's 16 updates of the columns right of it
+              if (mine) {
+#pragma unroll
+                for (int ps = 0; ps < 4; ++ps)
+#pragma unroll
+                  for (int k = 0; k < 16; ++k) sL[rr + RP * ps][k] = v[ps][k];
+              }
+              if (tid >= 16 * (b + 1) && tid < LB) {   // the pivot rows' final values right of the block
+                double col[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) col[k] = sU[k][tid];
+#pragma unroll
+                for (int k = 1; k < 16; ++k)
+#pragma unroll
+                  for (int kk = 0; kk < k; ++kk) col[k] -= sU[k][16 * b + kk] * col[kk];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) sU[k][tid] = col[k];
+              }
+              __syncthreads();
+              if (q > b) {
+#pragma unroll 2
+                for (int k = 0; k < 16; ++k) {
+                  double uk[16];
+#pragma unroll
+                  for (int c = 0; c < 16; ++c) uk[c] = sU[k][cq + c];
+#pragma unroll
+                  for (int ps = 0; ps < 4; ++ps) {
+                    const int i = base + RP * ps;
+                    if (i > 16 * b + k && i < h) {
+                      const double lk = sL[rr + RP * ps][k];
+#pragma unroll
+                      for (int c = 0; c < 16; ++c) v[ps][c] -= lk * uk[c];
+                    }
+                  }
+                }
+              }
+            }
+          }
+          const int jn = j + 1;
+          if (jn < LB) publish_rows(jn, record(jn, std::integral_constant<int, (jj + 1) & 15>{}));
+          if (g == 0 && tid < 64 && p != j) {   // compose interchange j (rows r0+j <-> r0+p)
+            if (p < LB) {
+              if (lane == 0) {
+                const int t = ptop[j];
+                ptop[j] = ptop[p];
+                ptop[p] = t;
+              }
+            } else {
+              const int pr = (int)r0 + p;
+              int slot = -1;
+              for (int bb = lane; bb < pnb; bb += 64)
+                if (pbrow[bb] == pr) slot = bb;
+              const unsigned long long hit = __ballot(slot >= 0);
+              const int found = hit ? __shfl(slot, __ffsll((long long)hit) - 1, 64) : -1;
+              if (lane == 0) {
+                int sl = found;
+                if (sl < 0) {
+                  sl = pnb;
+                  pbrow[sl] = pr;
+                  pbval[sl] = pr;
+                  pnb = sl + 1;
+                }
+                const int t = ptop[j];
+                ptop[j] = pbval[sl];
+                pbval[sl] = t;
+              }
+            }
+          }
+        },
+        std::make_integer_sequence<int, 16>{});
+    if (dead) return;
+  }
+  if (g == 0 && tid < 64) {   // the moves (lu_panel_coop_kernel's)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int n = 0;
+    for (int t0 = 0; t0 < LB; t0 += 64) {
+      const int t = t0 + lane;
+      const bool mv = ptop[t] != (int)r0 + t;
+      const unsigned long long bm = __ballot(mv);
+      if (mv) pairs[n + __popcll(bm & ((1ull << lane) - 1))] = make_int2((int)r0 + t, ptop[t]);
+      n += __popcll(bm);
+    }
+    for (int b0 = 0; b0 < pnb; b0 += 64) {
+      const int bb = b0 + lane;
+      const bool mv = bb < pnb && pbval[bb] != pbrow[bb];
+      const unsigned long long bm = __ballot(mv);
+      if (mv) pairs[n + __popcll(bm & ((1ull << lane) - 1))] = make_int2(pbrow[bb], pbval[bb]);
+      n += __popcll(bm);
+    }
+    if (lane == 0) *npairs = n;
+  }
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+    if (base + RP * ps >= h) continue;
+    double* row = A + (r0 + base + RP * ps) * ld + c0 + cq;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *(v2d*)(row + c) = *(const v2d*)(v[ps] + c);
+  }
+}
+
 // Compose block k's 128 interchanges (rows r0+s <-> ipiv[r0+s], in order) into row moves
 // "row dst <- previous row src" (<= 256 of them).  One wave.
 __global__ __launch_bounds__(64) void lu_perm_kernel(const int* __restrict__ ipiv, int r0, int2* __restrict__ pairs,
@@ -1238,7 +1629,8 @@ static hipError_t lu_coop_attr() {   // the dynamic LDS above the 64 KiB default
     const void* ks[] = {(const void*)lu_panel_coop_kernel<true, 256>, (const void*)lu_panel_coop_kernel<false, 256>,
                         (const void*)lu_panel_coop_kernel<true, 512>, (const void*)lu_panel_coop_kernel<false, 512>,
                         (const void*)lu_panel_coop_kernel<false, 256, true>,
-                        (const void*)lu_panel_coop_kernel<false, 512, true>};
+                        (const void*)lu_panel_coop_kernel<false, 512, true>, (const void*)lu_panel_blk_kernel<256>,
+                        (const void*)lu_panel_blk_kernel<512>};
     hipError_t e = hipSuccess;
     for (const void* f : ks)
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LUC_LDS);
@@ -1282,6 +1674,13 @@ static bool lu_coop_api() {
 
 static bool lu_coop_early() {   // read per call (A/B): SCS_LU_COOP_EARLY=0 publishes rows before the record
   const char* e = getenv("SCS_LU_COOP_EARLY");
+  return !(e && e[0] == '0');
+}
+
+// SCS_LU_COOP_BLK (read per call; default 1): the block-deferred panel (lu_panel_blk_kernel; n = 8192
+// factor + solve 77.0 -> 55.9 ms, 16384 197.4-198.5 -> 159.8-160.1 ms, same bits); 0 = lu_panel_coop_kernel
+static bool lu_coop_blk() {
+  const char* e = getenv("SCS_LU_COOP_BLK");
   return !(e && e[0] == '0');
 }
 
@@ -1330,6 +1729,7 @@ static hipError_t lu_panel(double* A, int64_t ld, int64_t npad, int k, const LUA
                                    : (early ? lu_panel_coop_kernel<false, 512, true> : lu_panel_coop_kernel<false, 512>))
                            : (wide ? lu_panel_coop_kernel<true, 256>
                                    : (early ? lu_panel_coop_kernel<false, 256, true> : lu_panel_coop_kernel<false, 256>));
+    if (!wide && lu_coop_blk()) kern = cnt == 512 ? lu_panel_blk_kernel<512> : lu_panel_blk_kernel<256>;
     double* pA = A;
     int64_t pld = ld, pr0 = r0, pc0 = c0, ph = h;
     unsigned long long* pgran = a->gran;

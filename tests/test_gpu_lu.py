@@ -189,6 +189,56 @@ def test_lu_coop_512_threads_bit_identical(n, monkeypatch):
     assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
 
 
+@pytest.mark.parametrize("nt", ["256", "512"])
+@pytest.mark.parametrize("n", [5, 300, 2176, 8320])
+def test_lu_coop_block_deferred_bit_identical(n, nt, monkeypatch):
+    """The block-deferred cooperative panel (default, SCS_LU_COOP_BLK; lu_panel_blk_kernel): each column step
+    updates its 16-column block only, the columns right of it take the block's 16 updates at its end in
+    step order -- the column steps' operations per element, so the same pivots and bits as SCS_LU_PANEL=1,
+    with 256- and 512-thread workgroups."""
+    rng = np.random.default_rng(n + 29)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    monkeypatch.setenv("SCS_LU_COOP_NT", nt)
+    x2, ipiv2, info2 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_PANEL", "1")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info1 == info2 == 0
+    assert np.array_equal(ipiv1, ipiv2)
+    assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
+
+
+@pytest.mark.parametrize("n", [300, 8320])
+def test_lu_coop_record_first_panel_bit_identical(n, monkeypatch):
+    """The r05/r06 cooperative panel without the block deferral (SCS_LU_COOP_BLK=0, the record-first
+    lu_panel_coop_kernel) stays bitwise the column steps'."""
+    rng = np.random.default_rng(n + 37)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    monkeypatch.setenv("SCS_LU_COOP_BLK", "0")
+    x2, ipiv2, info2 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_PANEL", "1")
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info1 == info2 == 0
+    assert np.array_equal(ipiv1, ipiv2)
+    assert np.array_equal(x1.view(np.uint64), x2.view(np.uint64))
+
+
+@pytest.mark.parametrize("n,zcol", [(300, 0), (300, 15), (300, 16), (700, 150), (700, 255)])
+def test_lu_coop_block_deferred_zero_pivot(n, zcol, monkeypatch):
+    """A zero column at a block's first / last step and inside one: info and the pivots (every column,
+    the zero one kept in place as getf2 does) equal the column steps'."""
+    rng = np.random.default_rng(n + zcol + 31)
+    A = rng.standard_normal((n, n))
+    A[:, zcol] = 0.0
+    _, ipiv2, info2 = scsopt.lu_solve(A, np.ones(n))
+    monkeypatch.setenv("SCS_LU_PANEL", "1")
+    _, ipiv1, info1 = scsopt.lu_solve(A, np.ones(n))
+    _, piv, linfo = lapack.dgetrf(A)
+    assert info1 == info2 == linfo == zcol + 1
+    assert np.array_equal(ipiv1, ipiv2) and np.array_equal(ipiv2[:zcol], piv[:zcol])
+
+
 @pytest.mark.parametrize("n", [300, 1000, 2176, 8320])
 def test_lu_outer_blocked_update(n, monkeypatch):
     """Outer blocks of four panels (SCS_LU_OB=4): inside a block each panel's moves reach the block's
