@@ -446,6 +446,9 @@ int scs_kernel_names(scs_ctx* ctx, char* gram, int64_t gram_cap, char* product, 
  *                           the dependency-driven chain (SCS_CHOL_DAG=1) gave up
  *   SCS_FB_PIPE_REDO        steps whose Gram + factor were redone unpipelined after a strip wait of
  *                           the pipelined factor (SCS_CHOL_PIPE) gave up
+ *   SCS_FB_QR_COOP_REFUSED  QR panels whose cooperative launch the runtime refused (run as column steps)
+ *   SCS_FB_QR_COOP_REDO     QR solves redone from the saved system with the per-column launches after
+ *                           a one-launch panel's record exchange timed out
  * Each redo gives the bits of the mode it falls back to.                                   */
 #define SCS_FB_LU_COOP_REFUSED 0
 #define SCS_FB_LU_COOP_REDO 1
@@ -453,7 +456,9 @@ int scs_kernel_names(scs_ctx* ctx, char* gram, int64_t gram_cap, char* product, 
 #define SCS_FB_QR_BLOCKS 3
 #define SCS_FB_CHAIN_REDO 4
 #define SCS_FB_PIPE_REDO 5
-#define SCS_FB_N 6
+#define SCS_FB_QR_COOP_REFUSED 6
+#define SCS_FB_QR_COOP_REDO 7
+#define SCS_FB_N 8
 int scs_fallback_counts(scs_ctx* ctx, int64_t* counts, int n);
 /* Wait for all work on the context stream.                                 */
 int scs_sync(scs_ctx* ctx);

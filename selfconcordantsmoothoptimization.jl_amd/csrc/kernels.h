@@ -234,6 +234,12 @@ struct QRAux {
   unsigned* flags = nullptr;
   int* err = nullptr;
   unsigned gen = 0;
+  // the cooperative one-launch panel (r06): {tag, word} granules (records, row c, abort word), its info
+  // (-1: a sweep gave up -- scsopt.cpp qr_run redoes the solve with no_coop); launches the runtime refused
+  unsigned long long* gran = nullptr;
+  int* cinfo = nullptr;
+  mutable bool no_coop = false;
+  mutable int64_t coop_refused = 0;
 };
 // set the identity padding of a column-major system in place / build it from a row-major one
 hipError_t qr_prepare(double* A, int64_t ld, int64_t n, int64_t npad, hipStream_t st);
@@ -242,6 +248,9 @@ hipError_t qr_from_rowmajor(const double* S, int64_t lds, double* D, int64_t ldd
 hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st);
 void qr_aux_free(QRAux* a);
 hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hipStream_t st);
+// whether qr_solve of order npad may run cooperative panels (SCS_QR_COOP, read per call): the caller then
+// keeps a copy of A and b for a redo after a sweep that gave up (QRAux::cinfo = -1)
+bool qr_coop_wanted(int64_t npad);
 // chol.hip pieces the QR solve reuses: the inverses of the 128 x 128 upper diagonal blocks of R
 // (W, as the Cholesky's), and the one-launch backward solve U x = y
 // T (128 x 128, upper) of a compact WY block from Gv = VᵀV and tau (chol.hip; the QR's panels)

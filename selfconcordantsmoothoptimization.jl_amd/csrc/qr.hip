@@ -230,6 +230,297 @@ static bool qr_step_fused() {   // read per call (A/B)
   return !(e && e[0] == '0');
 }
 
+// ---- the panel as ONE cooperative launch (r06, opt-in: SCS_QR_COOP=1; measured slower than the per-column
+// launches above, see qr_coop_mode).  The LU's cooperative panel (lu.hip) transposed to the QR: workgroup g
+// (NT = 512 threads: 4 row groups x 128 columns) holds the panel's rows [128 g, 128 g + 128) in registers,
+// column-major -- thread (j, rg) column j, rows 32 rg .. 32 rg + 31 (a wave: one row range, 64 columns) --
+// and b in LDS, through the 128 column steps.  Per column c ONE grid-wide hand-off: every workgroup
+// publishes its record (c) -- for the panel's columns j >= c the partial Σ_{r > c} a_rc a_rj over its rows
+// (j = c: Σ x_r², dlarfg's xnorm²) and the same for b -- as data-tagged 8-byte granules (tag = panel·256 +
+// c + 1, zeroed once per factorization, two slots by column parity as the LU's records), and workgroup 0 the
+// row c itself (alpha = a_cc, a_cj, b_c).  Every workgroup sweeps all G records (4 threads per slot,
+// records part, part + 4, ...; the parts then in order: the same sums, beta, tau and w_j = vᵀ a_j in every
+// workgroup), then applies reflector c to its rows of columns j > c and b (A_j -= tau (a_cj + sc d_j) v,
+// v_c = 1, v_r = x_r sc: LAPACK's dlarf arithmetic), and in the same pass forms record (c + 1) from the
+// UPDATED column c + 1 (x'_r recomputed from an LDS copy of column c + 1, so no barrier separates the update
+// from the next column's partials).  Three LDS barriers + one memory hop per column instead of a kernel
+// boundary.  A sweep past its bound (a workgroup that never became resident) stores info = -1 and the abort
+// word; the host then redoes the whole solve from a saved copy by the per-column launches (scsopt.cpp
+// qr_run).  Sums differ from the per-column launches' order (the QR is checked against LAPACK within
+// tolerance, not bitwise).
+constexpr int QC_RPT = 32;               // rows per thread
+constexpr int QC_MAXWG = 512;            // workgroups at most
+constexpr int QC_SWK = 4;                // records per sweep thread in flight (16: slower, the fabric's load rate)
+constexpr int QC_SL = 130;               // record slots: the panel's columns, b (128), pad
+constexpr int QC_BS = QB;                // b's slot
+constexpr int64_t QC_REC = 0;                                    // records [2][MAXWG][SL] x 2 granules
+constexpr int64_t QC_ROW = QC_REC + 2LL * QC_MAXWG * QC_SL * 2;   // row c [2][SL] x 2
+constexpr int64_t QC_ABORT = QC_ROW + 2LL * QC_SL * 2;
+constexpr int64_t QC_WORDS = QC_ABORT + 16;
+constexpr unsigned QC_SPIN_MAX = 1u << 19;   // sweeps before giving up (~0.5 s; SCS_QR_COOP_SPIN overrides)
+typedef __attribute__((address_space(1))) unsigned long long qc_gu64;
+
+#ifdef QR_PROF
+// probe_qr -DQR_PROF: workgroup 0's thread 0 splits each column of every cooperative panel into
+// sweep | reflector + v | rows | B2 | publish (s_memrealtime, 100 MHz ticks, summed) + columns
+__device__ unsigned long long qr_prof[8];
+#define QRP_MARK(v) const long long v = (g == 0 && tid == 0) ? (long long)__builtin_amdgcn_s_memrealtime() : 0
+#define QRP_ADD(k, a, b) if (g == 0 && tid == 0) qr_prof[k] += (unsigned long long)((b) - (a))
+// the last wave's column pass (slot 6)
+#define QRP_MARK2(v) const long long v = (g == 0 && tid == NT - 64) ? (long long)__builtin_amdgcn_s_memrealtime() : 0
+#define QRP_ADD2(k, a, b) if (g == 0 && tid == NT - 64) qr_prof[k] += (unsigned long long)((b) - (a))
+#else
+#define QRP_MARK2(v)
+#define QRP_ADD2(k, a, b)
+#define QRP_MARK(v)
+#define QRP_ADD(k, a, b)
+#endif
+
+__device__ __forceinline__ void qc_put(unsigned long long* p, unsigned long long x) {
+  __hip_atomic_store((qc_gu64*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long qc_get(const unsigned long long* p) {
+  return __hip_atomic_load((qc_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a double as two granules {tag, low word}, {tag, high word}
+__device__ __forceinline__ void qc_put_d(unsigned long long* p, unsigned tag, double v) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)tag << 32;
+  qc_put(p, t | (bits & 0xffffffffull));
+  qc_put(p + 1, t | (bits >> 32));
+}
+__device__ __forceinline__ double qc_get_d(const unsigned long long* p, unsigned tag, bool& ok) {
+  const unsigned long long x0 = qc_get(p), x1 = qc_get(p + 1);
+  ok = ok && (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag;
+  return __longlong_as_double((long long)((x0 & 0xffffffffull) | (x1 << 32)));
+}
+
+// Panel [c0, c0 + 128) of the column-major A (rows c0 .. c0 + h - 1), b rows likewise; tau[0 .. 128) and V
+// (rows relative to c0: zeros above the diagonal, one on it, v below) as qr_col_step leaves them; A gets R
+// on and above the diagonal (below it the columns as they stood before their own reflector: unused, as with
+// the column steps).  Per column, after the sweep: the ROW PASS (thread r < 256: row r of the workgroup)
+// forms v_r (into LDS and V), column c + 1's updated x'_r, and b's update and partial; then the COLUMN PASS
+// (thread (j, rg)) updates its 32 rows of column j > c and forms its partial of record (c + 1) -- two
+// fma per element, no branch, the owner lane idle (tw = 0).
+template <int NT>
+__global__ __launch_bounds__(NT) void qr_panel_coop_kernel(double* __restrict__ A, int64_t ld, int64_t c0, int64_t h,
+                                                              double* __restrict__ b, unsigned long long* gran,
+                                                              unsigned tagbase, double* __restrict__ tau,
+                                                              double* __restrict__ V, int64_t ldv, int* info,
+                                                              unsigned spin_max) {
+  constexpr int QC_RG = NT / QB;             // row groups (and sweep parts)
+  constexpr int QC_RW = QC_RG * QC_RPT;      // rows per workgroup (>= QB: row c is always workgroup 0's)
+  __shared__ double sX[2][QC_RW];      // column c as its owner holds it (x_r), by column parity
+  __shared__ double sN[2][QC_RW];      // column c + 1 before reflector c
+  __shared__ double sb[QC_RW];         // b (row r: the row pass's thread r)
+  __shared__ double sV[QC_RW], sXN[QC_RW];   // this column's v_r; column c + 1's updated x'_r (0 at r <= c + 1)
+  __shared__ double sp[QC_RG][QC_SL];  // the row groups' partials of the next record
+  __shared__ double red[QC_SL][QC_RG]; // the sweep: per slot, per part
+  __shared__ double srow[QC_SL];       // row c
+  __shared__ double sbeta[QB];         // R(c, c)
+  __shared__ int s_dead;
+  const int tid = threadIdx.x, g = blockIdx.x, G = gridDim.x;
+  const int j = tid & (QB - 1);
+  const int rg = __builtin_amdgcn_readfirstlane(tid >> 7), jlo = __builtin_amdgcn_readfirstlane(tid & 64);   // per wave
+  const int r0w = g * QC_RW;                // the workgroup's first row (panel-local; h <= 65536)
+  const int rw0 = rg * QC_RPT;              // this thread's first row within the workgroup
+  const int rb = r0w + rw0;                 // ... panel-local
+  const bool rows_in = rb < h;              // (h and rb are multiples of 32: all of a thread's rows or none)
+  const int rr = r0w + tid;                 // the row pass: this thread's row (tid < QC_RW)
+  if (gran[QC_ABORT] != 0) return;
+  if (spin_max == 0) {   // (tests: every workgroup gives up at once, as one that never became resident would)
+    if (tid == 0) {
+      *info = -1;
+      gran[QC_ABORT] = 1;
+    }
+    return;
+  }
+  double v[QC_RPT];
+  {
+    const double* src = A + (c0 + j) * ld + c0 + (rows_in ? rb : 0);
+#pragma unroll
+    for (int i = 0; i < QC_RPT; ++i) v[i] = src[i];
+    if (!rows_in)
+#pragma unroll
+      for (int i = 0; i < QC_RPT; ++i) v[i] = 0.0;
+  }
+  if (tid < QC_RW) sb[tid] = rr < h ? b[c0 + rr] : 0.0;
+  if (tid == 0) s_dead = 0;
+  if (j == 0)
+#pragma unroll
+    for (int i = 0; i < QC_RPT; ++i) sX[0][rw0 + i] = v[i];
+  if (j == 1)
+#pragma unroll
+    for (int i = 0; i < QC_RPT; ++i) sN[1][rw0 + i] = v[i];
+  __syncthreads();
+  auto rec_at = [&](int c, int gg, int s) { return gran + QC_REC + (((int64_t)(c & 1) * QC_MAXWG + gg) * QC_SL + s) * 2; };
+  auto row_at = [&](int c, int s) { return gran + QC_ROW + ((int64_t)(c & 1) * QC_SL + s) * 2; };
+  auto publish_record = [&](int c) {   // after the barrier that completes sp: slots c .. 127 and b
+    if (tid >= c && tid <= QC_BS) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < QC_RG; ++q) s += sp[q][tid];
+      qc_put_d(rec_at(c, g, tid), tagbase + (unsigned)c + 1, s);
+    }
+  };
+  auto b_partial = [&](double pb) {   // the row pass: b's partial per row group (32 rows: half a wave)
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) pb += __shfl_xor(pb, o, 64);
+    if ((tid & 31) == 0) sp[tid >> 5][QC_BS] = pb;
+  };
+  {   // record (0): the panel's columns as loaded
+    double p = 0.0;
+#pragma unroll
+    for (int i = 0; i < QC_RPT; ++i) p = fma(rb + i > 0 ? sX[0][rw0 + i] : 0.0, v[i], p);
+    sp[rg][j] = p;
+    if (tid < QC_RW) b_partial((rr > 0 ? sX[0][tid] : 0.0) * sb[tid]);
+    if (g == 0 && rg == 0) qc_put_d(row_at(0, j), tagbase + 1, v[0]);   // row 0
+    if (g == 0 && tid == 0) qc_put_d(row_at(0, QC_BS), tagbase + 1, sb[0]);
+  }
+  __syncthreads();
+  publish_record(0);
+  for (int c = 0; c < QB; ++c) {
+    const unsigned tag = tagbase + (unsigned)c + 1;
+    QRP_MARK(t_a);
+    {   // the sweep of record (c) and row c: thread (slot s, part) sums records part, part + 8, ... of slot s
+      const int s = tid / QC_RG, part = tid % QC_RG;
+      const int sa = s >= c ? s : -1;
+      const bool hb = s == 0;   // and b's slot
+      const int rs = (part == 1 && s >= c) ? s : ((part == 2 && s == 0) ? QC_BS : -1);
+      double aa = 0.0, ab = 0.0, rv = 0.0;
+      for (unsigned spins = 0;;) {
+        bool ok = true;
+        aa = 0.0;
+        ab = 0.0;
+        for (int k0 = part; k0 < G; k0 += QC_SWK * QC_RG) {   // QC_SWK records in flight
+          double xs[QC_SWK];
+#pragma unroll
+          for (int q = 0; q < QC_SWK; ++q) {
+            const int k = k0 + q * QC_RG;
+            xs[q] = (sa >= 0 && k < G) ? qc_get_d(rec_at(c, k, sa), tag, ok) : 0.0;
+          }
+#pragma unroll
+          for (int q = 0; q < QC_SWK; ++q) aa += xs[q];
+          if (hb) {
+#pragma unroll
+            for (int q = 0; q < QC_SWK; ++q) {
+              const int k = k0 + q * QC_RG;
+              xs[q] = k < G ? qc_get_d(rec_at(c, k, QC_BS), tag, ok) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < QC_SWK; ++q) ab += xs[q];
+          }
+        }
+        if (rs >= 0) rv = qc_get_d(row_at(c, rs), tag, ok);
+        if (ok) break;
+        if (++spins > spin_max) {
+          *info = -1;
+          gran[QC_ABORT] = 1;
+          s_dead = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (sa >= 0) red[sa][part] = aa;
+      if (hb) red[QC_BS][part] = ab;
+      if (rs >= 0) srow[rs] = rv;
+    }
+    __syncthreads();
+    if (s_dead) return;
+    QRP_MARK(t_b);
+    // the reflector (dlarfg) -- every thread the same sums in the same order
+    double xx = 0.0;
+#pragma unroll
+    for (int q = 0; q < QC_RG; ++q) xx += red[c][q];
+    const double alpha = srow[c];
+    double t = 0.0, sc = 0.0, beta = alpha;
+    if (xx > 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + xx), alpha);
+      t = (beta - alpha) / beta;
+      sc = 1.0 / (alpha - beta);
+    }
+    auto twf = [&](int s) {   // tau · vᵀ a_s (v_c = 1)
+      double d = 0.0;
+#pragma unroll
+      for (int q = 0; q < QC_RG; ++q) d += red[s][q];
+      return t * (srow[s] + sc * d);
+    };
+    const bool last = c + 1 >= QB;
+    const double tw = j > c ? twf(j) : 0.0;
+    if (tid < QC_RW) {   // the row pass
+      const double vr = rr < c ? 0.0 : (rr == c ? 1.0 : sX[c & 1][tid] * sc);
+      sV[tid] = vr;
+      if (rr < h) V[(int64_t)c * ldv + rr] = vr;
+      const double bb = fma(-twf(QC_BS), vr, sb[tid]);
+      sb[tid] = bb;
+      if (!last) {
+        const double xn = rr > c + 1 ? fma(-twf(c + 1), vr, sN[(c + 1) & 1][tid]) : 0.0;
+        sXN[tid] = xn;
+        b_partial(xn * bb);
+        if (g == 0 && rr == c + 1) qc_put_d(row_at(c + 1, QC_BS), tag + 1, bb);
+      }
+    }
+    if (tid == 0) {
+      sbeta[c] = beta;
+      if (g == 0) tau[c] = t;
+    }
+    __syncthreads();
+    QRP_MARK(t_c);
+    QRP_MARK2(u_c);
+    double p = 0.0;
+    if (rows_in && jlo + 63 > c && rb + QC_RPT - 1 >= c) {   // the column pass: lanes j > c, rows >= c
+      double rowv = 0.0, pq[4] = {0.0, 0.0, 0.0, 0.0};   // four partial chains, summed in order at the end
+#pragma unroll
+      for (int i0 = 0; i0 < QC_RPT; i0 += 8) {   // 8 rows' v_r and x'_r loaded before their updates
+        v2d vv[4], xv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          vv[q] = *(const v2d*)(sV + rw0 + i0 + 2 * q);
+          xv[q] = *(const v2d*)(sXN + rw0 + i0 + 2 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int i = i0 + q;
+          const double a = fma(-tw, vv[q >> 1][q & 1], v[i]);
+          pq[q & 3] = fma(xv[q >> 1][q & 1], a, pq[q & 3]);
+          rowv = (rb + i == c + 1) ? a : rowv;
+          v[i] = a;
+        }
+      }
+      p = (pq[0] + pq[1]) + (pq[2] + pq[3]);
+      if (g == 0 && !last && rb <= c + 1 && c + 1 < rb + QC_RPT && j > c)   // row c + 1 for the next step
+        qc_put_d(row_at(c + 1, j), tag + 1, rowv);
+    }
+    QRP_MARK(t_d);
+    QRP_MARK2(u_d);
+    QRP_ADD2(6, u_c, u_d);
+    if (last) break;
+    if (j == c + 1)
+#pragma unroll
+      for (int i = 0; i < QC_RPT; ++i) sX[(c + 1) & 1][rw0 + i] = v[i];
+    if (j == c + 2)
+#pragma unroll
+      for (int i = 0; i < QC_RPT; ++i) sN[(c + 2) & 1][rw0 + i] = v[i];
+    sp[rg][j] = p;
+    __syncthreads();
+    QRP_MARK(t_e);
+    publish_record(c + 1);
+    QRP_MARK(t_f);
+    QRP_ADD(0, t_a, t_b);
+    QRP_ADD(1, t_b, t_c);
+    QRP_ADD(2, t_c, t_d);
+    QRP_ADD(3, t_d, t_e);
+    QRP_ADD(4, t_e, t_f);
+    QRP_ADD(5, 0, 1);
+  }
+  __syncthreads();   // (the last row pass's b, sbeta, before they go back)
+  if (rows_in) {
+    double* dst = A + (c0 + j) * ld + c0 + rb;
+#pragma unroll
+    for (int i = 0; i < QC_RPT; ++i) dst[i] = (rb + i == j) ? sbeta[j] : v[i];
+  }
+  if (tid < QC_RW && rr < h) b[c0 + rr] = sb[tid];
+}
+
 // T (QB x QB, column-major, upper) of the panel's compact WY form from Gv = VᵀV (dlarft forward,
 // columnwise): T(i, i) = tau_i, T(0:i, i) = -tau_i T(0:i, 0:i) Gv(0:i, i)
 __global__ __launch_bounds__(QB) void qr_build_t(const double* __restrict__ Gv, const double* __restrict__ tau, int nb,
@@ -314,6 +605,9 @@ static void qr_free_bufs(QRAux* a) {
   if (a->flags) (void)hipFree(a->flags);
   a->flags = nullptr;
   a->err = nullptr;
+  if (a->gran) (void)hipFree(a->gran);
+  a->gran = nullptr;
+  a->cinfo = nullptr;
   a->gen = 0;
   a->npad = 0;
 }
@@ -388,6 +682,9 @@ hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st) {
   if (e == hipSuccess) e = hipMalloc(&a->flags, sizeof(unsigned) * (size_t)nbk + sizeof(int));
   if (e == hipSuccess) e = hipMemsetAsync(a->flags, 0, sizeof(unsigned) * (size_t)nbk + sizeof(int), st);
   if (e == hipSuccess) a->err = (int*)(a->flags + nbk);
+  // the cooperative panel's granules + its info word (zeroed per solve)
+  if (e == hipSuccess) e = hipMalloc(&a->gran, sizeof(unsigned long long) * (QC_WORDS + 2));
+  if (e == hipSuccess) a->cinfo = (int*)(a->gran + QC_WORDS);
   if (e == hipSuccess) {
     // ones[0, npad) = +1, ones[npad, npad + QB) = -1 (the Gram kernels' weights)
     hipLaunchKernelGGL(qr_fill_kernel, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, st, a->ones, npad, 1.0);
@@ -426,14 +723,78 @@ static hipError_t qr_ksplit(const double* V, int64_t ldv, const double* B, int64
   return hipGetLastError();
 }
 
+// read per call: SCS_QR_COOP=1 the cooperative panel (opt-in: measured slower than the per-column launches --
+// n = 8192 89 vs 83 ms, 16384 318 vs 293 ms -- its per-column record sweep reads G x 129 tagged values per
+// workgroup, G² x 129 across the chip, and costs 1.7-5.7 µs as G grows; DESIGN §3 QR)
+static int qr_coop_mode() {
+  const char* e = getenv("SCS_QR_COOP");
+  return e && e[0] == '1';
+}
+
+static unsigned qr_coop_spin() {   // read per call: SCS_QR_COOP_SPIN (sweeps; 0 = give up at once, tests)
+  const char* e = getenv("SCS_QR_COOP_SPIN");
+  return e ? (unsigned)strtoul(e, nullptr, 10) : QC_SPIN_MAX;
+}
+
+static int qr_device_cus() {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return ncu;
+}
+
+static int qr_coop_nt() {   // read per call (A/B): SCS_QR_COOP_NT = 512 (default) | 1024
+  const char* e = getenv("SCS_QR_COOP_NT");
+  return (e && atoi(e) == 1024) ? 1024 : 512;
+}
+
+// the first panel needs the most workgroups (npad / rows per workgroup); later panels fewer.  One
+// workgroup per CU at most (the 512-thread form holds > 128 registers per lane)
+bool qr_coop_wanted(int64_t npad) {
+  const int64_t G = ceil_div(npad, (int64_t)(qr_coop_nt() / QB) * QC_RPT);
+  return qr_coop_mode() && G <= QC_MAXWG && G <= qr_device_cus();
+}
+
+// panel p by the cooperative kernel; false when the runtime refused the launch (the caller runs it by
+// column steps)
+static bool qr_panel_coop(double* A, int64_t ld, int64_t npad, int p, QRAux* a, double* b, hipStream_t st) {
+  const int64_t c0 = (int64_t)p * QB, h = npad - c0;
+  const int nt = qr_coop_nt();
+  const int G = (int)ceil_div(h, (int64_t)(nt / QB) * QC_RPT);
+  double* pA = A;
+  int64_t pld = ld, pc0 = c0, ph = h, pldv = npad;
+  double* pb = b;
+  unsigned long long* pgran = a->gran;
+  unsigned ptag = (unsigned)p << 8, pspin = qr_coop_spin();
+  double* ptau = a->tau;
+  double* pV = a->V;
+  int* pinfo = a->cinfo;
+  void* args[] = {&pA, &pld, &pc0, &ph, &pb, &pgran, &ptag, &ptau, &pV, &pldv, &pinfo, &pspin};
+  const void* kern = nt == 1024 ? (const void*)qr_panel_coop_kernel<1024> : (const void*)qr_panel_coop_kernel<512>;
+  if (hipLaunchCooperativeKernel(kern, dim3((unsigned)G), dim3(nt), args, 0, st) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    ++a->coop_refused;
+    return false;
+  }
+  return true;
+}
+
 hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hipStream_t st) {
   hipError_t e = qr_aux_init(a, npad, st);
   if (e != hipSuccess) return e;
   const int nbk = (int)(npad / QB);
+  const bool coop = !a->no_coop && qr_coop_wanted(npad);
+  e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * (QC_WORDS + 2), st);   // tags, abort word, cinfo
+  if (e != hipSuccess) return e;
   for (int p = 0; p < nbk; ++p) {
     const int64_t c0 = (int64_t)p * QB, c1 = c0 + QB, rows = npad - c0;
     const int nrc = (int)((rows + QR_RC - 1) / QR_RC);
-    if (qr_step_fused()) {
+    if (coop && qr_panel_coop(A, ld, npad, p, a, b, st)) {
+      // (the panel, its V, tau and R rows as the column steps leave them)
+    } else if (qr_step_fused()) {
       const int64_t pslot = (int64_t)(QB + 1) * ((npad + QR_RC - 1) / QR_RC + 1);
       int nrc_prev = 0;
       for (int64_t c = c0; c <= c1; ++c) {

@@ -313,6 +313,8 @@ struct scs_ctx {
   double* rbk = nullptr;   // (m_pad) the right-hand side before a one-launch solve, for its per-block redo
   double* Gbk = nullptr;   // (m_pad²) the system before a cooperative-panel LU, for its column-step redo
   int64_t Gbk_n = 0;
+  double* qbk = nullptr;   // (npad² + npad) A and b before a cooperative-panel QR solve, for its redo
+  int64_t qbk_n = 0;
 
   // caches (CSE of identical evaluations; keyed by the host x content)
   std::vector<double> zkey;
@@ -1467,11 +1469,39 @@ void solve_lu_fallback(scs_ctx* c, double* rhs, hipEvent_t e0) {
 // (prox-GGN-SCORE.jl:131) on the symmetrized copy Gc; a NaN / Inf system gives a NaN direction
 // Householder QR solve of the column-major npad x npad system A (identity-padded) with b := A \ b;
 // a backward-solve dependency wait that gave up (~30 s, never expected) fails the call
+// r06: the panels as cooperative launches (qr.hip qr_panel_coop_kernel) -- a refused launch runs that panel
+// by column steps inside qr_solve; a sweep that gave up (cinfo = -1: a workgroup never became resident)
+// leaves A and b undefined, so the solve is redone from the saved copy with the per-column launches
 static void qr_run(scs_ctx* c, double* A, int64_t npad, double* b) {
+  const bool coop = qr_coop_wanted(npad);
+  const size_t nA = (size_t)npad * npad;
+  if (coop) {
+    if (c->qbk_n != npad) {
+      dfree_t(c, c->qbk);
+      c->qbk = dalloc<double>(c, nA + (size_t)npad);
+      c->qbk_n = npad;
+    }
+    HCK(hipMemcpyAsync(c->qbk, A, sizeof(double) * nA, hipMemcpyDeviceToDevice, c->st));
+    HCK(hipMemcpyAsync(c->qbk + nA, b, sizeof(double) * npad, hipMemcpyDeviceToDevice, c->st));
+  }
+  const int64_t refused0 = c->qr.coop_refused;
   HCK(qr_solve(A, npad, npad, &c->qr, b, c->st));
-  int late = 0;
+  int late = 0, cinfo = 0;
   HCK(hipMemcpyAsync(&late, c->qr.err, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  if (coop) HCK(hipMemcpyAsync(&cinfo, c->qr.cinfo, sizeof(int), hipMemcpyDeviceToHost, c->st));
   sync(c);
+  c->fb[SCS_FB_QR_COOP_REFUSED] += c->qr.coop_refused - refused0;
+  if (cinfo == -1) {
+    ++c->fb[SCS_FB_QR_COOP_REDO];
+    HCK(hipMemcpyAsync(A, c->qbk, sizeof(double) * nA, hipMemcpyDeviceToDevice, c->st));
+    HCK(hipMemcpyAsync(b, c->qbk + nA, sizeof(double) * npad, hipMemcpyDeviceToDevice, c->st));
+    c->qr.no_coop = true;
+    const hipError_t e = qr_solve(A, npad, npad, &c->qr, b, c->st);
+    c->qr.no_coop = false;
+    HCK(e);
+    HCK(hipMemcpyAsync(&late, c->qr.err, sizeof(int), hipMemcpyDeviceToHost, c->st));
+    sync(c);
+  }
   if (late || fault_late(2)) {
     // R is complete and qr.Ym still holds Qᵀb (the one-launch kernel only reads it): the backward
     // solve again by the per-block launches

@@ -247,7 +247,8 @@ class Context:
         self.check(lib.scs_get_stream(self.h, C.byref(s)))
         return s.value
 
-    FALLBACKS = ("lu_coop_refused", "lu_coop_redo", "solve_blocks", "qr_blocks", "chain_redo", "pipe_redo")
+    FALLBACKS = ("lu_coop_refused", "lu_coop_redo", "solve_blocks", "qr_blocks", "chain_redo", "pipe_redo",
+                 "qr_coop_refused", "qr_coop_redo")
 
     def fallback_counts(self):
         """The fallbacks taken instead of failing since the context was created (scs_fallback_counts;

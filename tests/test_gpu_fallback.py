@@ -7,6 +7,8 @@ a clean iterate!, and be counted (scs_fallback_counts):
     redone with the column-step panels -- bitwise SCS_LU_PANEL=1 -- for Julia's `A \\ b`
     (scs_lu_eval), ProxNSCORE's reference-solver LU (prox-N-SCORE.jl:70) and the GGN sample-space
     system (prox-GGN-SCORE.jl:124-127);
+  * the opt-in cooperative one-launch QR panel (qr.hip, SCS_QR_COOP=1): SCS_QR_COOP_SPIN=0 likewise; the
+    solve is redone from the saved system with the per-column launches -- bitwise the default;
   * the ~30 s dependency waits that are never expected (a block waits only on blocks dispatched before
     it): SCS_FAULT_LATE reports them as timed out at the host check, and the one-launch Cholesky
     solves redo by per-block launches (bitwise SCS_SOLVE_PERSIST=0), the QR's backward solve likewise,
@@ -159,3 +161,19 @@ def test_pipeline_strip_wait_timeout_redone_unpipelined(mode, clean_env):
     b, fb = _run(clean_env, mk, {"SCS_CHOL_PIPE": mode, "SCS_FAULT_LATE": "8"})
     assert np.array_equal(_bits(a.x), _bits(b.x)) and np.array_equal(_bits(a.obj), _bits(b.obj))
     assert fb["pipe_redo"] == 4, fb
+
+
+@pytest.mark.parametrize("m", [640, 2304])
+def test_qr_coop_timeout_redone_by_column_steps(m, clean_env):
+    """Reference-solver mode (qr(JQJ) \\ Je, prox-GGN-SCORE.jl:131) with the opt-in cooperative QR panel
+    (SCS_QR_COOP=1): every panel gives up at once (SCS_QR_COOP_SPIN=0); each solve is redone from the
+    saved system by the per-column launches -- the trajectory bitwise the default's, one redo per step."""
+    mk = _ggn_problem(3000, m, m + 3)
+    a, fa = _run(clean_env, mk, {}, solver="reference")
+    b, fb = _run(clean_env, mk, {"SCS_QR_COOP": "1", "SCS_QR_COOP_SPIN": "0"}, solver="reference")
+    c, fc = _run(clean_env, mk, {"SCS_QR_COOP": "1"}, solver="reference")
+    assert np.array_equal(_bits(a.x), _bits(b.x)) and np.array_equal(_bits(a.obj), _bits(b.obj))
+    assert fa["qr_coop_redo"] == 0 and fb["qr_coop_redo"] == 4 and fc["qr_coop_redo"] == 0, (fa, fb, fc)
+    assert fc["qr_coop_refused"] == 0, fc
+    # the cooperative panels themselves: the same trajectory to rounding (other summation order)
+    np.testing.assert_allclose(c.obj, a.obj, rtol=1e-10, atol=0)

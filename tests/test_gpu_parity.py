@@ -958,11 +958,16 @@ def test_cholesky_w_last_column_parallel(m, monkeypatch):
     np.testing.assert_allclose(a.x, b.x, rtol=1e-9, atol=1e-12)
 
 
-@pytest.mark.parametrize("m", [300, 1000, 2304])
-def test_householder_qr_solve(m):
+@pytest.mark.parametrize("coop", ["", "1"])
+@pytest.mark.parametrize("m", [300, 1000, 2304, 4100])
+def test_householder_qr_solve(m, coop, monkeypatch):
     """The reference solver's Householder QR (qr.hip, scs_solve_eval mode 2: LAPACK dgeqrf / dlarfg
     conventions, 128-column compact-WY panels, identity padding for m not a multiple of 128) on
-    (Aᵀ diag(w) A + diag d) x = rhs: against LAPACK's own QR solve (numpy), and its backward error."""
+    (Aᵀ diag(w) A + diag d) x = rhs: against LAPACK's own QR solve (numpy), and its backward error.
+    Panels as per-column launches (default) and as cooperative launches (SCS_QR_COOP=1, r06: 3 .. 33
+    workgroups here)."""
+    if coop:
+        monkeypatch.setenv("SCS_QR_COOP", coop)
     N = m + 77
     p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=41)
     rng = np.random.default_rng(42)
