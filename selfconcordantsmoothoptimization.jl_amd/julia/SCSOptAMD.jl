@@ -15,7 +15,7 @@ using SelfConcordantSmoothOptimization
 import SelfConcordantSmoothOptimization: step!, init!, ProximalMethod, ProxModel, is_interval_set
 
 export DeviceProblem, configure!, iterate_device!, set_gram_cache!, set_solver!, rccl_unique_id, set_comm_rccl!,
-       set_comm_callback!, set_test!, set_compute_f32!
+       set_comm_callback!, set_test!, set_compute_f32!, fallback_counts
 
 const lib = joinpath(@__DIR__, "..", "scsopt", "libscsopt.so")
 
@@ -418,6 +418,17 @@ set_solver!(model::DeviceProblem, reference::Bool=true) =
 # products of fp32-stored values (val_f32 = true) and the L-BFGS two-loop (scs_set_compute_f32).
 set_compute_f32!(model::DeviceProblem, on::Bool=true) =
     chk(ccall((:scs_set_compute_f32, lib), Cint, (Ptr{Cvoid}, Cint), model.ctx, on ? 1 : 0), model.ctx)
+
+# The fallbacks taken instead of failing since the problem's context was created (scs_fallback_counts;
+# SCS_FB_* in include/scsopt.h, in that order), as name => count.
+const FALLBACKS = (:lu_coop_refused, :lu_coop_redo, :solve_blocks, :qr_blocks, :chain_redo, :pipe_redo,
+                   :qr_coop_refused, :qr_coop_redo)
+function fallback_counts(model::DeviceProblem)
+    out = zeros(Int64, length(FALLBACKS))
+    chk(ccall((:scs_fallback_counts, lib), Cint, (Ptr{Cvoid}, Ptr{Int64}, Cint), model.ctx, out, length(out)),
+        model.ctx)
+    return Dict(zip(FALLBACKS, out))
+end
 
 method_code(m) = m isa ProxNSCORE ? 1 : m isa ProxGGNSCORE ? 2 : m isa ProxLQNSCORE ? 3 : error("unknown method")
 
