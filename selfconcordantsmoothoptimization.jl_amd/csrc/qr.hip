@@ -263,12 +263,12 @@ typedef __attribute__((address_space(1))) unsigned long long qc_gu64;
 #ifdef QR_PROF
 // probe_qr -DQR_PROF: workgroup 0's thread 0 splits each column of every cooperative panel into
 // sweep | reflector + v | rows | B2 | publish (s_memrealtime, 100 MHz ticks, summed) + columns
-__device__ unsigned long long qr_prof[8];
+__device__ unsigned long long qr_prof[32];
 #define QRP_MARK(v) const long long v = (g == 0 && tid == 0) ? (long long)__builtin_amdgcn_s_memrealtime() : 0
 #define QRP_ADD(k, a, b) if (g == 0 && tid == 0) qr_prof[k] += (unsigned long long)((b) - (a))
 // the last wave's column pass (slot 6)
-#define QRP_MARK2(v) const long long v = (g == 0 && tid == NT - 64) ? (long long)__builtin_amdgcn_s_memrealtime() : 0
-#define QRP_ADD2(k, a, b) if (g == 0 && tid == NT - 64) qr_prof[k] += (unsigned long long)((b) - (a))
+#define QRP_MARK2(v) const long long v = (g == 0 && (tid & 63) == 0) ? (long long)__builtin_amdgcn_s_memrealtime() : 0
+#define QRP_ADD2(k, a, b) if (g == 0 && (tid & 63) == 0) qr_prof[k] += (unsigned long long)((b) - (a))
 #else
 #define QRP_MARK2(v)
 #define QRP_ADD2(k, a, b)
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(NT) void qr_panel_coop_kernel(double* __restrict__ 
     }
     QRP_MARK(t_d);
     QRP_MARK2(u_d);
-    QRP_ADD2(6, u_c, u_d);
+    QRP_ADD2(8 + (tid >> 6), u_c, u_d);
     if (last) break;
     if (j == c + 1)
 #pragma unroll
@@ -501,6 +501,8 @@ __global__ __launch_bounds__(NT) void qr_panel_coop_kernel(double* __restrict__ 
 #pragma unroll
       for (int i = 0; i < QC_RPT; ++i) sN[(c + 2) & 1][rw0 + i] = v[i];
     sp[rg][j] = p;
+    QRP_MARK2(u_e);
+    QRP_ADD2(16 + (tid >> 6), u_d, u_e);
     __syncthreads();
     QRP_MARK(t_e);
     publish_record(c + 1);

@@ -54,7 +54,7 @@ int main() {
       CK(scs::qr_aux_init(&aux, np, st));
       CK(hipStreamSynchronize(st));
 #ifdef QR_PROF
-      unsigned long long z[8] = {0};
+      unsigned long long z[32] = {0};
       CK(hipMemcpyToSymbol(HIP_SYMBOL(scs::qr_prof), z, sizeof(z)));
 #endif
       CK(hipEventRecord(e0, st));
@@ -67,7 +67,7 @@ int main() {
       double cs = 0; for (double v : x) cs += v;
       printf("n=%ld qr_solve: %.2f ms (coop info %d, refused %ld) sum(x) %.17g\n", (long)n, ms, ci, (long)aux.coop_refused, cs);
 #ifdef QR_PROF
-      unsigned long long p[8];
+      unsigned long long p[32];
       CK(hipMemcpyFromSymbol(p, HIP_SYMBOL(scs::qr_prof), sizeof(p)));
       const double nc = (double)p[5];
       if (nc > 0)
@@ -75,6 +75,13 @@ int main() {
                "(last wave's rows %.2f)\n",
                (long)p[5], p[0] / nc / 100.0, p[1] / nc / 100.0, p[2] / nc / 100.0, p[3] / nc / 100.0, p[4] / nc / 100.0,
                p[6] / nc / 100.0);
+      if (nc > 0) {
+        printf("  per wave (us): column pass");
+        for (int w = 0; w < 16; ++w) if (p[8 + w]) printf(" %.2f", p[8 + w] / nc / 100.0);
+        printf(" | owner writes");
+        for (int w = 0; w < 16; ++w) if (p[16 + w]) printf(" %.2f", p[16 + w] / nc / 100.0);
+        printf("\n");
+      }
 #endif
     }
     CK(hipFree(A)); CK(hipFree(A0)); CK(hipFree(b)); CK(hipFree(b0));
