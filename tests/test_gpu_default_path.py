@@ -10,7 +10,8 @@ C2 m = 8192, C3 m = 16384, C4 m = 32768, C5 m = 65536), against the oracle:
     blocks = 16 outer blocks of 8) with its second-stream lookahead -- 3 epochs at rtol 1e-8;
   * C2 shape: ProxNSCORE logistic (margin) + l1, m = 8192 (128 x 128 tiles, 8 outer blocks);
   * C4 shape: the m = 32768 Cholesky solve (256 inner blocks) by its backward error, with the
-    residual formed by the independent streaming GEMV kernels; the m = 32768 LU likewise;
+    residual formed by the independent streaming GEMV kernels; the m = 32768 LU likewise; the
+    2-epoch group-lasso trajectory against the oracle's, committed as tests/golden/c4_shape_oracle.npz;
   * C5 shape: ProxLQNSCORE(mem 20) box least squares on a sparse A with m = 65536 (4 LDS column
     blocks of the CSR product, the multi-workgroup two-loop / tail / L-BFGS update) and
     N = 2^17 (8 row blocks of the CSC product), 10 epochs at rtol 1e-8.
@@ -218,30 +219,26 @@ def test_c4_shape_ggn_group_lasso(clean_env):
     two-level Cholesky (no CU reserve above m = 16384), the multi-workgroup PHuberSmootherGL with its
     global dot(Dg, Dg) (phuber-smooth.jl:137-164) and the group prox over 1024 groups
     (prox-operators.jl:48-66, prox-reg-utils.jl:84-119).  2 epochs vs the oracle at rtol 1e-8 on
-    obj / fval and on rel (the mean_square_error of reg "gl", iterate.jl:171-175)."""
-    N, m, gs, mu = 36864, 32768, 32, 1e-2
-    ng = m // gs
-    x0 = np.random.default_rng(1234).standard_normal(m)
-    f, out = losses.least_squares(1.0 / N), losses.linear_ls(1.0 / N)
-    p = scsopt.Problem.synthetic(N, m, x0, f, 1.0, kind=3, seed=2026, out_fn=out)
-    g0 = p.gradx(np.zeros(m))
-    lam = [1e-8, 0.1 * float(np.max(np.linalg.norm(g0.reshape(ng, gs), axis=1)))]
-    p.λ = lam
-    ind = np.array([[1 + gs * g for g in range(ng)], [gs * (g + 1) for g in range(ng)], [1] * ng])
-    p.P = scsopt.get_P(m, np.arange(1, m + 1), ind)
-    A, y = p.get_data()
-    om = O.Problem(A, y, x0, O.Loss("least_squares", 1.0 / N, ggn="linear_ls"), lam,
-                   P=O.GroupP(m, ind, np.arange(1, m + 1)))
-    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "gl", scsopt.PHuberSmootherGL(mu, p), max_epoch=2, x_tol=0.0,
-                         f_tol=0.0, verbose=0)
-    del A
-    osol = O.iterate(O.ProxGGNSCORE(), om, "gl", O.PHuberSmootherGL(mu, om), max_epoch=2, x_tol=0.0, f_tol=0.0)
-    assert sol.epochs == osol.epochs and len(sol.obj) == len(osol.obj)
-    np.testing.assert_allclose(sol.obj, osol.obj, rtol=1e-8, atol=0)
-    np.testing.assert_allclose(sol.fval, osol.fval, rtol=1e-8, atol=0)
-    np.testing.assert_allclose(sol.rel, osol.rel, rtol=1e-8, atol=0)
-    np.testing.assert_allclose(sol.x, osol.x, rtol=1e-6, atol=1e-9)
+    obj / fval and on rel (the mean_square_error of reg "gl", iterate.jl:171-175).  The oracle's
+    trajectory on this data is the committed fixture tests/golden/c4_shape_oracle.npz (made by
+    tests/golden/c4_shape.py: ~2.5 min of host BLAS, r06 moved it out of the suite); the data's
+    fingerprint (exact sums of three columns of A) and λ are checked against it first."""
+    import c4_shape as C
+    fx = np.load(C.FIXTURE)
+    assert tuple(fx["shape"]) == (C.N, C.M, C.GS, C.SEED) and int(fx["epochs"]) == C.EPOCHS
+    p, x0, lam = C.setup()
+    assert np.array_equal(C.fingerprint(p), fx["fp"]), "the device data is not the fixture's"
+    np.testing.assert_allclose(lam, fx["lam"], rtol=1e-14, atol=0)
+    p.λ = [float(v) for v in fx["lam"]]
+    sol = scsopt.iterate(scsopt.ProxGGNSCORE(), p, "gl", scsopt.PHuberSmootherGL(C.MU, p), max_epoch=C.EPOCHS,
+                         x_tol=0.0, f_tol=0.0, verbose=0)
+    assert sol.epochs == int(fx["epochs"]) and len(sol.obj) == len(fx["obj"])
+    np.testing.assert_allclose(sol.obj, fx["obj"], rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.fval, fx["fval"], rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.rel, fx["rel"], rtol=1e-8, atol=0)
+    np.testing.assert_allclose(sol.x, fx["x"], rtol=1e-6, atol=1e-9)
     # the group prox zeroes whole groups: the support pattern is group-aligned on both sides
-    zd = (sol.x.reshape(ng, gs) == 0).all(axis=1)
-    zo = (osol.x.reshape(ng, gs) == 0).all(axis=1)
+    ng = C.M // C.GS
+    zd = (sol.x.reshape(ng, C.GS) == 0).all(axis=1)
+    zo = (fx["x"].reshape(ng, C.GS) == 0).all(axis=1)
     assert np.array_equal(zd, zo)
