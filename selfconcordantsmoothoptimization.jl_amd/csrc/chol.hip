@@ -861,6 +861,16 @@ __global__ void diag_pad_kernel(double* __restrict__ G, int64_t ld, int64_t m, i
 // that C tile traffic: 2·128 KiB per 4.2 MFLOP tile).
 static int outer_block();
 
+// SCS_CHOL_PRIO (read per call; r06): the chain's latency launches (row panels, in-block updates, Ba's strip
+// steps, C1a) run their waves at s_setprio 3, so that on a SIMD shared with the bulk stream's MFMA waves
+// they win the issue arbitration (MI355X_MICROARCH.md: priority, then age).  Default on: the same bits;
+// probe factor, three rounds per arm on one box (profiles/r06/prio/): m = 16384 31.37-31.83 vs 32.17-32.58 ms,
+// m = 8192 7.17-7.28 vs 7.23-7.30 ms.  0 = r05's normal priority.
+static int chol_prio() {
+  const char* e = getenv("SCS_CHOL_PRIO");
+  return e ? atoi(e) : 1;
+}
+
 // The bulk stream (the lookahead's trailing updates) is a plain non-blocking stream.  (r02 kept 32
 // CUs from it with a CU-masked queue, hipExtStreamCreateWithCUMask; a process that created one
 // faulted at exit under rocprofv3 -- in librocprofiler-sdk's static destructors, profiles/r03/segv/
@@ -1120,9 +1130,10 @@ static hipError_t strip_solve(double* G, int64_t ld, const double* W, const Chol
 __global__ __launch_bounds__(256) void strip_step_kernel(double* G, int64_t ld, const double* __restrict__ W,
                                                          const double* __restrict__ wv, int r, int hi, int c0,
                                                          int nc, double* __restrict__ scur,
-                                                         const double* __restrict__ sprev) {
+                                                         const double* __restrict__ sprev, int prio) {
   __shared__ __attribute__((aligned(16))) double lds[2 * (GT + 16) * GBK];
   __shared__ __attribute__((aligned(16))) double Y[GT * 16];
+  if (prio) __builtin_amdgcn_s_setprio(3);
   const int nitem = (hi - r) * nc * 8, it = blockIdx.x;
   if (it >= nitem) {   // copy-back of the previous step's row r - 1: one 128 x 16 strip
     const int ci = it - nitem, j = ci >> 3, s = ci & 7;
@@ -1157,7 +1168,8 @@ static hipError_t strip_solve_steps(double* G, int64_t ld, const double* W, cons
     double* scur = last ? nullptr : a->sscr + row * ((r - lo) & 1);
     const double* sprev = a->sscr + row * ((r - lo + 1) & 1);
     const unsigned grid = (unsigned)((hi - r) * nc * 8 + (r > lo ? nc * 8 : 0));
-    hipLaunchKernelGGL(strip_step_kernel, dim3(grid), dim3(256), 0, st, G, ld, W, a->w, r, hi, c0, nc, scur, sprev);
+    hipLaunchKernelGGL(strip_step_kernel, dim3(grid), dim3(256), 0, st, G, ld, W, a->w, r, hi, c0, nc, scur, sprev,
+                       chol_prio());
   }
   return hipGetLastError();
 }
@@ -1505,6 +1517,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
     if (eb != hipSuccess) return eb;
   }
   bool c12_pending = false;
+  const int pf = (la && chol_prio()) ? GRAM_PRIO : 0;   // the chain's latency launches (SCS_CHOL_PRIO)
   hipError_t e = hipSuccess;
   auto wait = [&](hipStream_t s, hipEvent_t ev) {
     if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
@@ -1526,11 +1539,11 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
       }
       double* rowpanel = G + (int64_t)(k + 1) * CB * ld + (int64_t)k * CB;   // U_k,(k+1..i1-1)
       e = gram_launch_gen(W + (int64_t)k * CB * CB, CB, rowpanel, ld, a->w, 0, CB, rect_list(a, 1), nb, rowpanel, ld,
-                          0, st);
+                          pf, st);
       if (e != hipSuccess) return e;
       double* trail = G + (int64_t)(k + 1) * CB * ld + (int64_t)(k + 1) * CB;
       e = gram_launch_gen(rowpanel, ld, rowpanel, ld, a->w + CB, 0, CB, trilist, nb * (nb + 1) / 2, trail, ld,
-                          /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+                          /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4 | pf, st);
       if (e != hipSuccess) return e;
     }
     const int nc = nblk - i1;
@@ -1575,7 +1588,7 @@ hipError_t chol_factor(double* G, int64_t ld, int64_t m, int64_t mpad, double* W
         e = steps ? strip_solve_steps(G, ld, W, a, i0, i1, i1, OB, st) : strip_solve(G, ld, W, a, i0, i1, i1, OB, st);
       if (e == hipSuccess)
         e = gram_launch_small(X, ld, X, ld, a->w + CB, (int64_t)i0 * CB, (int64_t)i1 * CB, trilist, n1a, trail, ld,
-                              2 | 4, st);
+                              2 | 4 | pf, st);
     }
     // C12 on st2 after Ba (it reads X's columns of the next block); split: C12a (the tiles the
     // chain's next Ba and C1a read) as a latency launch, its event, then C12b

@@ -1011,6 +1011,7 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const double* __restric
                                                          int flags) {
   constexpr int NQ = GT / QC;
   __shared__ __attribute__((aligned(16))) double lds[2 * (GT + QC) * GBK];
+  if (flags & GRAM_PRIO) __builtin_amdgcn_s_setprio(3);
   const int2 tl = tiles[blockIdx.x / NQ];
   const int64_t I0 = (int64_t)tl.x * GT, J0 = (int64_t)tl.y * GT + (blockIdx.x % NQ) * QC;
   double* Gt = (flags & GRAM_UPPER) ? G + I0 * ldg + J0 : G + J0 * ldg + I0;

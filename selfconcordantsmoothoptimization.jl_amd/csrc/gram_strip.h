@@ -8,7 +8,9 @@
 namespace scs {
 
 constexpr int GT = 128;   // output tile edge
-enum { GRAM_PACKED = 1, GRAM_ACCUMULATE = 2, GRAM_UPPER = 4 };
+// GRAM_PRIO (r06): the latency kernel's waves at s_setprio 3 -- the Cholesky chain's launches, which
+// share SIMDs with the bulk stream's MFMA waves (chol.hip SCS_CHOL_PRIO)
+enum { GRAM_PACKED = 1, GRAM_ACCUMULATE = 2, GRAM_UPPER = 4, GRAM_PRIO = 8 };
 constexpr int GBK = 16;   // samples per stage
 
 __device__ __forceinline__ int swz(int f) { return (f >> 1) & 7; }
