@@ -540,6 +540,7 @@ def main():
               "ms_per_step_local": 1e3 * dt / steps,
               "breakdown_ms_per_step": ({k.replace("_ms", ""): tm[k] / steps for k in tm if k.endswith("_ms")}
                                         if tevery == 1 else None),
+              "launch_counts": {k.replace("_calls", ""): int(tm[k]) for k in tm if k.endswith("_calls")},
               "comm": {k: cinfo[k] for k in ("kind", "nranks", "rank")}}
     rank_rows = gather_rank_rows(my_row, world, dist if comm is not None else None)
     if comm is not None:
