@@ -30,6 +30,7 @@ constexpr int QB = 128;         // panel width
 constexpr int QR_RC = 1024;     // rows per partial-sum chunk
 constexpr int QR_KS = 512;      // rows per K piece of the panel's Vᵀ products (qr_ksplit)
 constexpr int QR_KMAXITEMS = 1024;   // K-split work items per launch at most (partial buffer: 128 MiB)
+constexpr int QR_MAXRC = 64;         // chunks whose partials qr_col_step stages in LDS (npad <= 65536)
 
 // partial[(j - c) * nrc + rc]: Σ_{r in chunk rc, r > c} A[r, c] · A[r, j] for the panel's columns
 // j = c .. c1-1, and (j = c1) the right-hand side b
@@ -125,7 +126,8 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
                                                    int64_t c0, int64_t c1, double* __restrict__ b,
                                                    double* __restrict__ part, int64_t pslot, int nrc, int nrc_prev,
                                                    double* __restrict__ rowc, double* __restrict__ xs,
-                                                   double* __restrict__ tau, double* __restrict__ V, int64_t ldv) {
+                                                   double* __restrict__ tau, double* __restrict__ V, int64_t ldv,
+                                                   int stage) {
   const int rc = blockIdx.x;
   const int jj = (int)blockIdx.y - 1;
   const int tid = threadIdx.x;
@@ -151,27 +153,50 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
     pac[k] = (in && jj >= 0) ? colc[r] : 0.0;
     px[k] = (in && has_prev) ? x[r] : 0.0;
   }
+  // r06: the previous column's chunk partials (its xnorm², w_j, w_c) are fetched by wave 0's lanes at once
+  // into LDS and summed by thread 0 in chunk order as before -- one memory latency instead of up to
+  // 3·nrc_prev dependent loads in thread 0's loops; the same sums and bits (SCS_QR_STAGE=0: the r05
+  // loops).  probe_qr, same box, two rounds: n = 16384 307.4-310.0 -> 291.5-292.3 ms, 8192 85.8-86.3 ->
+  // 85.1-85.5 ms (profiles/r06/qrstage/); from 8 chunks on (n = 2048, two chunks: 13.4-13.5 vs 14.1 ms)
+  __shared__ double sxx[QR_MAXRC], sbj[QR_MAXRC], sbc[QR_MAXRC];
+  const bool staged = has_prev && nrc_prev >= 8 && nrc_prev <= QR_MAXRC && stage;   // (2 chunks: the loop is cheaper)
+  if (staged && tid < 64) {
+    const double* pp = part + (pv & 1) * pslot;
+    for (int q = tid; q < nrc_prev; q += 64) {
+      sxx[q] = pp[q];
+      if (jj >= 0) sbj[q] = pp[(c + jj - pv) * nrc_prev + q];
+      if (c < c1) sbc[q] = pp[(c - pv) * nrc_prev + q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
   if (tid == 0) {
     double t = 0.0, sc = 0.0, beta = 0.0, twj = 0.0, twc = 0.0;
     if (has_prev) {
       const double* pp = part + (pv & 1) * pslot;
       const double* rp = rowc + (pv & 1) * (QB + 2);
+      const double alpha = rp[0], rpj = jj >= 0 ? rp[c + jj - pv] : 0.0, rpc = c < c1 ? rp[c - pv] : 0.0;
       double xx = 0.0;
-      for (int q = 0; q < nrc_prev; ++q) xx += pp[q];
-      const double alpha = rp[0];
+      if (staged)
+        for (int q = 0; q < nrc_prev; ++q) xx += sxx[q];
+      else
+        for (int q = 0; q < nrc_prev; ++q) xx += pp[q];
       beta = alpha;
       if (xx > 0.0) {
         beta = -copysign(sqrt(alpha * alpha + xx), alpha);
         t = (beta - alpha) / beta;
         sc = 1.0 / (alpha - beta);
       }
-      auto twf = [&](int64_t j) {   // tau · vᵀ a_j, v(pv) = 1
+      auto twf = [&](int64_t j, const double* sb, double rpv) {   // tau · vᵀ a_j, v(pv) = 1
         double d = 0.0;
-        for (int q = 0; q < nrc_prev; ++q) d += pp[(j - pv) * nrc_prev + q];
-        return t * (rp[j - pv] + sc * d);
+        if (staged)
+          for (int q = 0; q < nrc_prev; ++q) d += sb[q];
+        else
+          for (int q = 0; q < nrc_prev; ++q) d += pp[(j - pv) * nrc_prev + q];
+        return t * (rpv + sc * d);
       };
-      if (jj >= 0) twj = twf(c + jj);
-      if (c < c1) twc = twf(c);
+      if (jj >= 0) twj = twf(c + jj, sbj, rpj);
+      if (c < c1) twc = twf(c, sbc, rpc);
     }
     sh[0] = t;
     sh[1] = sc;
@@ -223,6 +248,11 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
   if ((tid & 63) == 0) ws[tid >> 6] = s;
   __syncthreads();
   if (tid == 0) part[(c & 1) * pslot + (int64_t)jj * nrc + rc] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+}
+
+static bool qr_stage() {   // read per call (A/B): SCS_QR_STAGE=0 thread 0 loads the partials itself (r05)
+  const char* e = getenv("SCS_QR_STAGE");
+  return !(e && e[0] == '0');
 }
 
 static bool qr_step_fused() {   // read per call (A/B)
@@ -794,6 +824,7 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
   for (int p = 0; p < nbk; ++p) {
     const int64_t c0 = (int64_t)p * QB, c1 = c0 + QB, rows = npad - c0;
     const int nrc = (int)((rows + QR_RC - 1) / QR_RC);
+    const int stage = qr_stage() ? 1 : 0;
     if (coop && qr_panel_coop(A, ld, npad, p, a, b, st)) {
       // (the panel, its V, tau and R rows as the column steps leave them)
     } else if (qr_step_fused()) {
@@ -804,7 +835,7 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
         const int nrc_c = (int)((npad - rbeg + QR_RC - 1) / QR_RC);
         const int ncol = (int)(c1 - c) + 1;   // columns c .. c1-1 and b
         hipLaunchKernelGGL(qr_col_step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad, c,
-                           c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, a->V, npad);
+                           c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, a->V, npad, stage);
         nrc_prev = nrc_c;
       }
     } else
