@@ -433,6 +433,7 @@ __global__ __launch_bounds__(DNT, L::packed ? 2 : 1) void chol_diag_kernel(doubl
   __shared__ double srinv[CB];      // 1 / U(j, j)
   __shared__ __attribute__((aligned(16))) double urow[SB];   // phase A's row-j copy
   __shared__ int tctr;                                        // phase C's tile counter
+  if (wpar & 2) __builtin_amdgcn_s_setprio(3);   // SCS_CHOL_PRIO: beside bulk waves (the packed form) it wins issue
   double* blk = G + (int64_t)k * CB * ld + (int64_t)k * CB;
   double* Wk = W + (int64_t)k * CB * CB;
   const int tid = threadIdx.x;
@@ -599,9 +600,9 @@ __global__ __launch_bounds__(DNT, L::packed ? 2 : 1) void chol_diag_kernel(doubl
   if (W_BY_COLUMNS) {
     PROF_MARK(34);
     if (PIPE) {
-      if (wpar) w_last_column_par<L>(su, &swinv[0][0], Wk, tid);
+      if (wpar & 1) w_last_column_par<L>(su, &swinv[0][0], Wk, tid);
       else if (wv == 0) w_column<L>(su, &swinv[0][0], Wk, CB / SB - 1, lane);
-    } else if (wpar) {   // columns 0..6 (wave w: w and 6 - w), then the last one by all waves, as PIPE
+    } else if (wpar & 1) {   // columns 0..6 (wave w: w and 6 - w), then the last one by all waves, as PIPE
       w_column<L>(su, &swinv[0][0], Wk, wv, lane);
       if (wv < 3) w_column<L>(su, &swinv[0][0], Wk, CB / SB - 2 - wv, lane);
       __syncthreads();   // the transposed off-diagonal blocks w_last_column_par reads
@@ -789,6 +790,8 @@ hipError_t chol_tri_inverse(const double* R, int64_t ld, int nblk, double* W, hi
   return hipGetLastError();
 }
 
+static int chol_prio();   // SCS_CHOL_PRIO (below)
+
 static bool chol_diag_pipe() {   // read per call (A/B within one process)
   const char* e = getenv("SCS_CHOL_DIAG");
   return !(e && e[0] == '0');
@@ -828,16 +831,17 @@ static hipError_t chol_diag_pack_attr() {   // the dynamic LDS above the 64 KiB 
 
 hipError_t launch_chol_diag(double* G, int64_t ld, int k, double* W, int* info, hipStream_t st) {
   const bool pipe = chol_diag_pipe(), pack = chol_diag_pack() && chol_diag_pack_attr() == hipSuccess;
+  const int dflag = chol_wpar() | (chol_prio() ? 2 : 0);
   if (pipe && pack)
     hipLaunchKernelGGL((chol_diag_kernel<true, LayPack>), dim3(1), dim3(DNT), CHOL_DIAG_PACK_LDS, st, G, ld, k, W, info,
-                       chol_wpar());
+                       dflag);
   else if (pipe)
-    hipLaunchKernelGGL((chol_diag_kernel<true, LayFull>), dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
+    hipLaunchKernelGGL((chol_diag_kernel<true, LayFull>), dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, dflag);
   else if (pack)
     hipLaunchKernelGGL((chol_diag_kernel<false, LayPack>), dim3(1), dim3(DNT), CHOL_DIAG_PACK_LDS, st, G, ld, k, W,
-                       info, chol_wpar());
+                       info, dflag);
   else
-    hipLaunchKernelGGL((chol_diag_kernel<false, LayFull>), dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, chol_wpar());
+    hipLaunchKernelGGL((chol_diag_kernel<false, LayFull>), dim3(1), dim3(DNT), 0, st, G, ld, k, W, info, dflag);
   return hipGetLastError();
 }
 
