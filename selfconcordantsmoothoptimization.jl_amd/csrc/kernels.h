@@ -195,7 +195,8 @@ struct LUAux {
   double* T = nullptr;       // [npad][128] A12ᵀ staging
   double* UT = nullptr;      // [npad][128] U12 as K-contiguous columns
   double* UTo = nullptr;     // [npad][512] an outer block's U rows on the trailing columns, K-contiguous
-  int2* rect = nullptr;      // row-major nblk x c tile rectangles, c = 1 .. 3 (updates inside an outer block)
+  int2* rect = nullptr;      // row-major nblk x c tile rectangles, c = 1 .. 4 (updates inside an outer block;
+                             // 4: the lookahead's next outer block)
   double* w = nullptr;       // [128 x +1 | 512 x -1]
   mutable int ob = 1;        // panels per outer block of the last lu_factor (lu_solve follows its row order)
   int2* sq = nullptr;        // square-shell tile list (trailing updates)
@@ -204,6 +205,16 @@ struct LUAux {
   // scsopt.cpp lu_factor_checked); launches the runtime refused (the panel ran as column steps)
   mutable bool no_coop = false;
   mutable int64_t coop_refused = 0;
+  // the lookahead outer step (SCS_LU_LA, r06): the bulk stream that updates the trailing columns beyond
+  // the next outer block while the next block's panels run, its two events (panels done / bulk done),
+  // its own A12ᵀ staging, the (i < LU_OB, j) tile list of the bulk's top rows and the counter sets of
+  // its CU-bounded launches (LU_LCTR sets of 16, zeroed once per factorization)
+  mutable hipStream_t st2 = nullptr;
+  mutable hipEvent_t evp = nullptr, evb = nullptr;
+  double* T2 = nullptr;
+  int2* col4 = nullptr;
+  unsigned* lctr = nullptr;
+  mutable int lslot = 0;
 };
 hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st);
 void lu_aux_free(LUAux* a);

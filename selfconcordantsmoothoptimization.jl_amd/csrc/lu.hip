@@ -41,6 +41,7 @@ constexpr int LU_MAXWG = 256;     // workgroups of a panel step at most
 constexpr int LU_NT = 256;        // panel step: 32 rows x 8 lanes (16 columns each) per pass
 constexpr int LU_MAXPAIRS = 2 * LB;
 constexpr int LU_OB = 4;          // panels per outer block (SCS_LU_OB)
+constexpr int LU_LCTR = 256;      // counter sets of the lookahead bulk's bounded launches (per factorization)
 
 __device__ __forceinline__ bool lu_better(double v1, int i1, double v2, int i2) {
   return v1 > v2 || (v1 == v2 && i1 < i2);
@@ -1570,11 +1571,16 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
   }
   std::vector<int2> row1(nblk);
   for (int j = 0; j < nblk; ++j) row1[j] = make_int2(0, j);
-  // row-major nblk x c rectangles, c = 1 .. LU_OB - 1 (the updates inside an outer block)
+  // row-major nblk x c rectangles, c = 1 .. LU_OB (the updates inside an outer block; LU_OB: the
+  // lookahead's update of the next outer block's columns)
   std::vector<int2> rect;
-  for (int c = 1; c < LU_OB; ++c)
+  for (int c = 1; c <= LU_OB; ++c)
     for (int i = 0; i < nblk; ++i)
       for (int j = 0; j < c; ++j) rect.push_back(make_int2(i, j));
+  // column-major LU_OB x nblk (the lookahead bulk's rows of the next outer block)
+  std::vector<int2> col4;
+  for (int j = 0; j < nblk; ++j)
+    for (int i = 0; i < LU_OB; ++i) col4.push_back(make_int2(i, j));
   hipError_t e = hipSuccess;
   auto al = [&](void** p, size_t bytes) {
     if (e == hipSuccess) e = hipMalloc(p, bytes);
@@ -1597,12 +1603,17 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
   al((void**)&a->w, sizeof(double) * hw.size());
   al((void**)&a->sq, sizeof(int2) * sq.size());
   al((void**)&a->row1, sizeof(int2) * row1.size());
+  al((void**)&a->T2, sizeof(double) * (size_t)npad * LB);
+  al((void**)&a->col4, sizeof(int2) * col4.size());
+  al((void**)&a->lctr, sizeof(unsigned) * 16 * LU_LCTR);
   if (e == hipSuccess) e = hipMemcpyAsync(a->w, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(a->sq, sq.data(), sizeof(int2) * sq.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(a->row1, row1.data(), sizeof(int2) * row1.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(a->rect, rect.data(), sizeof(int2) * rect.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(a->col4, col4.data(), sizeof(int2) * col4.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e == hipSuccess) a->npad = npad;
   return e;
@@ -1610,9 +1621,13 @@ hipError_t lu_aux_init(LUAux* a, int64_t npad, hipStream_t st) {
 
 void lu_aux_free(LUAux* a) {
   void* ps[] = {a->cand, a->candi, a->candrow, a->rowj, a->gran, a->ipiv, a->pairs, a->npairs, a->Linv,
-                a->Uinv, a->T,     a->UT,      a->UTo,  a->rect, a->w,    a->sq,   a->row1};
+                a->Uinv, a->T,     a->UT,      a->UTo,  a->rect, a->w,    a->sq,   a->row1,
+                a->T2,   a->col4,  a->lctr};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  if (a->st2) (void)hipStreamDestroy(a->st2);
+  if (a->evp) (void)hipEventDestroy(a->evp);
+  if (a->evb) (void)hipEventDestroy(a->evb);
   *a = LUAux();
 }
 
@@ -1780,6 +1795,80 @@ static void lu_swap(double* A, int64_t ld, int64_t c_lo, int64_t w, const LUAux*
                      a->pairs + (int64_t)k * LU_MAXPAIRS, a->npairs + k);
 }
 
+// SCS_LU_LA (read per call; default 1, 0 = the one-stream outer step): the lookahead outer step.  After an outer block's panels, the
+// trailing columns of the NEXT outer block (the next panels' input) are updated on the caller's stream
+// and every column beyond them on a bulk stream, which runs beside the next outer block's panels --
+// the panels (37 of the 55 ms of an n = 8192 factor + solve, r06) hold a cooperative launch of one
+// workgroup per CU on h / 128 of the 256 CUs, the rest idle.  Per tile the same kernels and K order as
+// the one-stream step: the same factor bit for bit (test_lu_lookahead_bit_identical).
+static bool lu_lookahead() {
+  const char* e = getenv("SCS_LU_LA");
+  return !(e && e[0] == '0');
+}
+
+// SCS_LU_LA_SKIP (read per call): CU ids per shader engine the bulk's throughput launches leave free
+// (gram_launch_bounded; 0 = full-grid launches).  Unset: full-grid launches while the bulk outweighs
+// the next outer block's panels -- more than SCS_LU_LA_FULL (default 8192) trailing columns: its
+// update is 2·h²·512 flop, 4.6 ms at h = 16384 against ~2.3 ms of panels (~0.58 ms each, latency-bound)
+// -- then a skip set sized to the next panel's cooperative launch of h / 128 CUs: k = ceil(h / 4096)
+// ids (1..4) of each of the 32 shader engines, from id 4 up.  Measured (r06, factor + solve, 3 rounds
+// alternated): n = 8192 55.6-57.4 -> 54.3-54.4 ms, 16384 157.7-159.2 -> 147.3-148.1 ms; full grid
+// throughout 54.6-55.7 / 148.9-150.3, threshold 4096 55.4-55.9 / 149.1-150.5, 12288 53.9-54.3 /
+// 146.7-147.6; sized skip sets throughout 16384 178-180 (profiles/r06/lu_la/).
+static unsigned lu_la_skip(int64_t h_next) {
+  const char* e = getenv("SCS_LU_LA_SKIP");
+  if (e) return (unsigned)strtoul(e, nullptr, 0) & 0xffffu;
+  const char* f = getenv("SCS_LU_LA_FULL");
+  if (h_next > (f ? atoll(f) : 8192)) return 0u;
+  const int k = (int)std::min<int64_t>(4, std::max<int64_t>(1, ceil_div(h_next, (int64_t)32 * LB)));
+  return ((1u << k) - 1u) << 4;
+}
+
+// The trailing columns [cb1 + coff, cb1 + coff + w) of the outer block [b0, b1) on stream s: the block's
+// row moves in order, its U rows by block forward substitution (X_t = L_tt⁻¹ (A_t - Σ_{s<t} L_ts X_s),
+// X into A and, K-contiguous, into UTo), then A22 -= L21 X with K = (b1 - b0)·128 over all the rows
+// below the block.  coff = 0: the columns from cb1 (rect / square tile lists); coff = LU_OB·128: the
+// lookahead bulk (the square below the next outer block's rows + those rows' LU_OB x nc strip), its
+// throughput launches CU-bounded when ctr is given.
+static hipError_t lu_outer_trailing(double* A, int64_t ld, int64_t npad, int b0, int b1, int64_t coff, int64_t w,
+                                    double* Tb, const LUAux* a, unsigned* ctr, hipStream_t s) {
+  const int64_t cb0 = (int64_t)b0 * LB, cb1 = (int64_t)b1 * LB, c_lo = cb1 + coff;
+  const int ncr = (int)(w / LB), nr = (int)((npad - cb1) / LB), KO = (b1 - b0) * LB;
+  const int64_t ncap = a->npad / LB;   // the lists were built for the aux's capacity
+  double* U = a->UTo + coff * (LU_OB * LB);
+  hipError_t e = hipSuccess;
+  for (int k = b0; k < b1; ++k) lu_swap(A, ld, c_lo, w, a, k, s);
+  for (int k = b0; k < b1; ++k) {
+    const int64_t r0 = (int64_t)k * LB;
+    const int t = k - b0;
+    if (t > 0)
+      e = gram_launch_gen(A + r0 * ld + cb0, ld, U, LU_OB * LB, a->w + LB, 0, (int64_t)t * LB, a->row1, ncr,
+                          A + r0 * ld + c_lo, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lu_transpose_kernel, dim3((unsigned)ceil_div(w, 64), LB / 64), dim3(256), 0, s, A, ld, r0, c_lo,
+                       w, Tb);
+    const double* Lk = a->Linv + (int64_t)k * LB * LB;
+    e = gram_launch_gen(Lk, LB, Tb, LB, a->w, 0, LB, a->row1, ncr, A + r0 * ld + c_lo, ld, /*GRAM_UPPER*/ 4, s);
+    if (e == hipSuccess)
+      e = gram_launch_gen(Lk, LB, Tb, LB, a->w, 0, LB, a->row1, ncr, U + (int64_t)t * LB, LU_OB * LB, 0, s);
+    if (e != hipSuccess) return e;
+  }
+  if (coff == 0) {
+    const int2* tl = ncr == nr ? a->sq : a->rect + ncap * (ncr - 1) * ncr / 2;
+    return gram_launch_gen(A + cb1 * ld + cb0, ld, U, LU_OB * LB, a->w + LB, 0, KO, tl, ncr == nr ? nr * nr : nr * ncr,
+                           A + cb1 * ld + c_lo, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, s);
+  }
+  // (coff = LU_OB·128 and ncr = nr - LU_OB: the rows below the next outer block form a square)
+  const unsigned skip = ctr ? lu_la_skip(npad - cb1) : 0u;
+  const int slots = 2 * lu_device_cus();
+  e = gram_launch_bounded(A + c_lo * ld + cb0, ld, U, LU_OB * LB, a->w + LB, 0, KO, a->sq, ncr * ncr,
+                          A + c_lo * ld + c_lo, ld, 2 | 4, ctr, skip, slots, s, true);
+  if (e == hipSuccess)
+    e = gram_launch_bounded(A + cb1 * ld + cb0, ld, U, LU_OB * LB, a->w + LB, 0, KO, a->col4, LU_OB * ncr,
+                            A + cb1 * ld + c_lo, ld, 2 | 4, ctr ? ctr + 16 : nullptr, skip, slots, s, true);
+  return e;
+}
+
 hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux* a, int* info, hipStream_t st) {
   if (npad % LB != 0 || npad > a->npad || ld < npad) return hipErrorInvalidValue;
   const int nblk = (int)(npad / LB);
@@ -1789,9 +1878,21 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
     const hipError_t e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * LUC_WORDS, st);
     if (e != hipSuccess) return e;
   }
+  // the lookahead: only where some outer block has columns beyond the next one
+  const bool la = lu_lookahead() && OB == LU_OB && nblk > 2 * LU_OB;
+  if (la) {
+    hipError_t e = hipSuccess;
+    if (!a->st2) e = hipStreamCreateWithFlags(&a->st2, hipStreamNonBlocking);
+    if (e == hipSuccess && !a->evp) e = hipEventCreateWithFlags(&a->evp, hipEventDisableTiming);
+    if (e == hipSuccess && !a->evb) e = hipEventCreateWithFlags(&a->evb, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMemsetAsync(a->lctr, 0, sizeof(unsigned) * 16 * LU_LCTR, st);
+    if (e != hipSuccess) return e;
+    a->lslot = 0;
+  }
   if (npad > n)
     hipLaunchKernelGGL(lu_pad_kernel, dim3((unsigned)ceil_div(npad - n, 256)), dim3(256), 0, st, A, ld, n, npad);
   hipError_t e = hipSuccess;
+  bool bulk = false;   // a bulk update is in flight on st2 (evb recorded after it)
   for (int b0 = 0; b0 < nblk; b0 += OB) {
     const int b1 = std::min(b0 + OB, nblk);
     const int64_t cb0 = (int64_t)b0 * LB, cb1 = (int64_t)b1 * LB;
@@ -1824,29 +1925,36 @@ hipError_t lu_factor(double* A, int64_t ld, int64_t n, int64_t npad, const LUAux
       if (e != hipSuccess) return e;
     }
     if (OB == 1 || cb1 == npad) continue;
-    // the trailing columns: the block's moves in order, its U rows by block forward substitution
-    // (X_t = L_tt⁻¹ (A_t - Σ_{s<t} L_ts X_s), X into A and, K-contiguous, into UTo), then ONE update
-    // A22 -= L21 X with K = (b1 - b0)·128
+    // the trailing columns (lu_outer_trailing).  Lookahead: the previous bulk update wrote the columns
+    // this step starts from, so the caller's stream waits for it here -- after this block's panels, which
+    // ran beside it -- and columns beyond the next outer block go to the bulk stream
     const int64_t wt = npad - cb1;
-    const int nct = (int)(wt / LB), KO = (b1 - b0) * LB;
-    for (int k = b0; k < b1; ++k) lu_swap(A, ld, cb1, wt, a, k, st);
-    for (int k = b0; k < b1; ++k) {
-      const int64_t r0 = (int64_t)k * LB;
-      const int t = k - b0;
-      if (t > 0)
-        e = gram_launch_gen(A + r0 * ld + cb0, ld, a->UTo, LU_OB * LB, a->w + LB, 0, (int64_t)t * LB, a->row1, nct,
-                            A + r0 * ld + cb1, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+    if (bulk) {
+      e = hipStreamWaitEvent(st, a->evb, 0);
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(lu_transpose_kernel, dim3((unsigned)ceil_div(wt, 64), LB / 64), dim3(256), 0, st, A, ld, r0,
-                         cb1, wt, a->T);
-      const double* Lk = a->Linv + (int64_t)k * LB * LB;
-      e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nct, A + r0 * ld + cb1, ld, /*GRAM_UPPER*/ 4, st);
-      if (e == hipSuccess)
-        e = gram_launch_gen(Lk, LB, a->T, LB, a->w, 0, LB, a->row1, nct, a->UTo + (int64_t)t * LB, LU_OB * LB, 0, st);
-      if (e != hipSuccess) return e;
+      bulk = false;
     }
-    e = gram_launch_gen(A + cb1 * ld + cb0, ld, a->UTo, LU_OB * LB, a->w + LB, 0, KO, a->sq, nct * nct,
-                        A + cb1 * ld + cb1, ld, /*GRAM_ACCUMULATE|GRAM_UPPER*/ 2 | 4, st);
+    if (la && wt > (int64_t)LU_OB * LB) {
+      const int64_t wa = (int64_t)LU_OB * LB;
+      unsigned* ctr = nullptr;
+      if (a->lslot + 2 <= LU_LCTR) {
+        ctr = a->lctr + 16 * a->lslot;
+        a->lslot += 2;
+      }
+      e = hipEventRecord(a->evp, st);
+      if (e == hipSuccess) e = hipStreamWaitEvent(a->st2, a->evp, 0);
+      if (e == hipSuccess) e = lu_outer_trailing(A, ld, npad, b0, b1, wa, wt - wa, a->T2, a, ctr, a->st2);
+      if (e == hipSuccess) e = hipEventRecord(a->evb, a->st2);
+      if (e != hipSuccess) return e;
+      bulk = true;
+      e = lu_outer_trailing(A, ld, npad, b0, b1, 0, wa, a->T, a, nullptr, st);
+    } else {
+      e = lu_outer_trailing(A, ld, npad, b0, b1, 0, wt, a->T, a, nullptr, st);
+    }
+    if (e != hipSuccess) return e;
+  }
+  if (bulk) {
+    e = hipStreamWaitEvent(st, a->evb, 0);
     if (e != hipSuccess) return e;
   }
   return hipGetLastError();

@@ -277,3 +277,27 @@ def test_lu_smaller_system_after_larger_on_one_context():
         assert info == linfo == 0
         assert np.array_equal(ipiv, piv)
         assert _bwd(A, x, b) <= 1e-13
+
+
+@pytest.mark.parametrize("skip", ["0", "0x30", "auto"])
+@pytest.mark.parametrize("n", [1100, 2176, 8320])
+def test_lu_lookahead_bit_identical(n, skip, monkeypatch):
+    """The lookahead outer step (SCS_LU_LA, the default since r06) against the one-stream step
+    (SCS_LU_LA=0): the columns beyond the next outer block updated on a bulk stream beside the next
+    block's panels, as full-grid (skip 0) or CU-bounded launches (a fixed skip set, or the default: full
+    grid above 8192 trailing columns, then sized to the next panel) -- the same tiles, kernels and K
+    order as the one-stream step, so the same pivots and solution bit for bit.  n = 1100: 9 blocks, one
+    bulk update of a single block column; 8320: 65 blocks (15 bulk updates, both default forms)."""
+    rng = np.random.default_rng(n + 19)
+    A = rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    monkeypatch.setenv("SCS_LU_LA", "0")
+    x0, ipiv0, info0 = scsopt.lu_solve(A, b)
+    monkeypatch.setenv("SCS_LU_LA", "1")
+    if skip != "auto":
+        monkeypatch.setenv("SCS_LU_LA_SKIP", skip)
+    x1, ipiv1, info1 = scsopt.lu_solve(A, b)
+    assert info0 == info1 == 0
+    assert np.array_equal(ipiv0, ipiv1)
+    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+    assert _bwd(A, x1, b) <= 1e-13
