@@ -251,6 +251,12 @@ struct QRAux {
   int* cinfo = nullptr;
   mutable bool no_coop = false;
   mutable int64_t coop_refused = 0;
+  // the lookahead trailing update (SCS_QR_LA, r06): the bulk stream that applies panel p's block
+  // reflector to the columns beyond the next panel while panel p + 1 runs, its events, the second V / T
+  // (panel parity) and the bulk's own Wm / Ym / Vᵀ / K-split partials; klists[2 nbk + p]: its Wm list
+  hipStream_t st2 = nullptr;
+  hipEvent_t evp = nullptr, evb = nullptr;
+  double *V2 = nullptr, *T2 = nullptr, *Wm2 = nullptr, *Ym2 = nullptr, *Vt2 = nullptr, *kpart2 = nullptr;
 };
 // set the identity padding of a column-major system in place / build it from a row-major one
 hipError_t qr_prepare(double* A, int64_t ld, int64_t n, int64_t npad, hipStream_t st);

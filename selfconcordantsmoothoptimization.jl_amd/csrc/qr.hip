@@ -623,7 +623,7 @@ hipError_t qr_from_rowmajor(const double* S, int64_t lds, double* D, int64_t ldd
 
 static void qr_free_bufs(QRAux* a) {
   for (double** p : {&a->part, &a->tw, &a->tau, &a->scal, &a->V, &a->Vt, &a->Wm, &a->Ym, &a->Gv, &a->T, &a->ones,
-                     &a->W, &a->rowc, &a->xs, &a->kpart})
+                     &a->W, &a->rowc, &a->xs, &a->kpart, &a->V2, &a->T2, &a->Wm2, &a->Ym2, &a->Vt2, &a->kpart2})
     if (*p) {
       (void)hipFree(*p);
       *p = nullptr;
@@ -640,6 +640,11 @@ static void qr_free_bufs(QRAux* a) {
   if (a->gran) (void)hipFree(a->gran);
   a->gran = nullptr;
   a->cinfo = nullptr;
+  if (a->st2) (void)hipStreamDestroy(a->st2);
+  if (a->evp) (void)hipEventDestroy(a->evp);
+  if (a->evb) (void)hipEventDestroy(a->evb);
+  a->st2 = nullptr;
+  a->evp = a->evb = nullptr;
   a->gen = 0;
   a->npad = 0;
 }
@@ -704,10 +709,39 @@ hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st) {
       kmax = std::max(kmax, (size_t)n);
     }
   }
+  // the lookahead's Wm lists, klists[2 nbk + 2p + {0, 1}]: the next panel's column block and the
+  // trailing column blocks beyond it, K split as the whole update's list 2p + 1 (the same pieces and
+  // combine order per column block: the same bits)
+  for (int p = 0; p < 2 * nbk; ++p) {
+    const int pp = p / 2;
+    const int64_t rows = npad - (int64_t)pp * QB;
+    const int nj = (p & 1) ? std::max(nbk - pp - 2, 1) : 1;
+    int ns = (int)((rows + QR_KS - 1) / QR_KS);
+    ns = std::max(1, std::min(ns, QR_KMAXITEMS / std::max(nbk - pp - 1, 1)));
+    const int n = nj * ns, seglen = (n + 7) / 8;
+    QRAux::KList L;
+    L.off = (int64_t)kw.size();
+    L.seglen = seglen;
+    L.nsplit = ns;
+    L.nj = nj;
+    a->klists.push_back(L);
+    kw.resize(kw.size() + (size_t)8 * seglen, make_int4(-1, 0, 0, 0));
+    for (int i = 0; i < n; ++i) {
+      const int j = i / ns, s = i % ns;
+      kw[(size_t)L.off + (size_t)(i % 8) * seglen + i / 8] = make_int4(0, j, s, j * ns + s);
+    }
+    kmax = std::max(kmax, (size_t)n);
+  }
   if (e == hipSuccess) e = hipMalloc(&a->kwork, sizeof(int4) * std::max<size_t>(kw.size(), 1));
   if (e == hipSuccess && !kw.empty())
     e = hipMemcpyAsync(a->kwork, kw.data(), sizeof(int4) * kw.size(), hipMemcpyHostToDevice, st);
   al(&a->kpart, kmax * QB * QB);
+  al(&a->kpart2, kmax * QB * QB);
+  al(&a->V2, (size_t)npad * QB);
+  al(&a->T2, (size_t)QB * QB);
+  al(&a->Wm2, (size_t)npad * QB);
+  al(&a->Ym2, (size_t)npad * QB);
+  al(&a->Vt2, (size_t)npad * QB);
   if (e == hipSuccess) e = hipMalloc(&a->tiles, sizeof(int2) * std::max<size_t>(tl.size(), 1));
   if (e == hipSuccess && !tl.empty())
     e = hipMemcpyAsync(a->tiles, tl.data(), sizeof(int2) * tl.size(), hipMemcpyHostToDevice, st);
@@ -791,7 +825,7 @@ bool qr_coop_wanted(int64_t npad) {
 
 // panel p by the cooperative kernel; false when the runtime refused the launch (the caller runs it by
 // column steps)
-static bool qr_panel_coop(double* A, int64_t ld, int64_t npad, int p, QRAux* a, double* b, hipStream_t st) {
+static bool qr_panel_coop(double* A, int64_t ld, int64_t npad, int p, QRAux* a, double* V, double* b, hipStream_t st) {
   const int64_t c0 = (int64_t)p * QB, h = npad - c0;
   const int nt = qr_coop_nt();
   const int G = (int)ceil_div(h, (int64_t)(nt / QB) * QC_RPT);
@@ -801,7 +835,7 @@ static bool qr_panel_coop(double* A, int64_t ld, int64_t npad, int p, QRAux* a, 
   unsigned long long* pgran = a->gran;
   unsigned ptag = (unsigned)p << 8, pspin = qr_coop_spin();
   double* ptau = a->tau;
-  double* pV = a->V;
+  double* pV = V;
   int* pinfo = a->cinfo;
   void* args[] = {&pA, &pld, &pc0, &ph, &pb, &pgran, &ptag, &ptau, &pV, &pldv, &pinfo, &pspin};
   const void* kern = nt == 1024 ? (const void*)qr_panel_coop_kernel<1024> : (const void*)qr_panel_coop_kernel<512>;
@@ -814,18 +848,62 @@ static bool qr_panel_coop(double* A, int64_t ld, int64_t npad, int p, QRAux* a, 
   return true;
 }
 
+// SCS_QR_LA (read per call; default 0): the lookahead trailing update.  After panel p's block
+// reflector (V, T) is formed, the next panel's 128 columns take it on the caller's stream and every
+// column beyond them on a bulk stream, which runs beside panel p + 1 (its 129 column-step launches);
+// V and T alternate between two buffers by panel parity.  Per tile the same kernels, K pieces and
+// combine order as the one-stream update: the same factor bit for bit (test_qr_lookahead_bit_identical).
+static bool qr_lookahead() {
+  const char* e = getenv("SCS_QR_LA");
+  return e && e[0] == '1';
+}
+
+// A(:, cb .. cb + 128 nj) -= V T (Vᵀ A(:, cb ..)) over the panel's rows (c0 .. npad): Wm = Vᵀ A_t (K split,
+// klists[list]), Ym = Tᵀ Wm, Vt = Vᵀ as K-contiguous columns, A_t -= Vt-features x Ym over the panel's
+// update rectangle (tiles i < rows / 128, j < nj: j-major, the first nj columns of panel p's rectangle)
+static hipError_t qr_apply_block(double* A, int64_t ld, int64_t npad, int p, int64_t cb, int nj, int list,
+                                 const double* V, const double* T, double* Wm, double* Ym, double* Vt, double* kpart,
+                                 QRAux* a, hipStream_t s) {
+  const int64_t c0 = (int64_t)p * QB, rows = npad - c0;
+  double* At = A + cb * ld + c0;
+  const QRAux::KList& L = a->klists[(size_t)list];
+  if (L.nj != nj) return hipErrorInvalidValue;
+  hipError_t e = gram_launch_work_cm(V, npad, At, ld, a->ones, rows, a->kwork + L.off, L.seglen, L.nsplit, kpart, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(qr_combine_kernel, dim3(16, (unsigned)nj), dim3(256), 0, s, kpart, L.nsplit, Wm, (int64_t)QB);
+  // Ym = Tᵀ Wm: Ym(i, j) = Σ_q T(q, i) Wm(q, j)
+  e = gram_launch_gen(T, QB, Wm, QB, a->ones, 0, QB, a->tiles, nj, Ym, QB, 0, s);
+  if (e != hipSuccess) return e;
+  // A_t -= V Ym: A(r, j) -= Σ_i Vt(i, r) Ym(i, j) (features r of Vt, K = i)
+  hipLaunchKernelGGL(qr_transpose_v, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, V, npad, rows, Vt);
+  return gram_launch_gen(Vt, QB, Ym, QB, a->ones + npad, 0, QB, a->tiles + a->rect_off[(size_t)p],
+                         (int)(rows / QB) * nj, At, ld, /*ACCUMULATE*/ 2, s);
+}
+
 hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hipStream_t st) {
   hipError_t e = qr_aux_init(a, npad, st);
   if (e != hipSuccess) return e;
   const int nbk = (int)(npad / QB);
   const bool coop = !a->no_coop && qr_coop_wanted(npad);
+  const bool la = qr_lookahead() && nbk > 2;
+  if (la) {
+    if (!a->st2) e = hipStreamCreateWithFlags(&a->st2, hipStreamNonBlocking);
+    if (e == hipSuccess && !a->evp) e = hipEventCreateWithFlags(&a->evp, hipEventDisableTiming);
+    if (e == hipSuccess && !a->evb) e = hipEventCreateWithFlags(&a->evb, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
   e = hipMemsetAsync(a->gran, 0, sizeof(unsigned long long) * (QC_WORDS + 2), st);   // tags, abort word, cinfo
   if (e != hipSuccess) return e;
+  bool bulk = false;   // a bulk update is in flight on st2 (evb recorded after it)
   for (int p = 0; p < nbk; ++p) {
     const int64_t c0 = (int64_t)p * QB, c1 = c0 + QB, rows = npad - c0;
     const int nrc = (int)((rows + QR_RC - 1) / QR_RC);
     const int stage = qr_stage() ? 1 : 0;
-    if (coop && qr_panel_coop(A, ld, npad, p, a, b, st)) {
+    // panel p's reflectors (V) and T: the second buffers on odd panels under the lookahead (the bulk
+    // update of panel p - 1 may still read the other pair)
+    double* V = (la && (p & 1)) ? a->V2 : a->V;
+    double* T = (la && (p & 1)) ? a->T2 : a->T;
+    if (coop && qr_panel_coop(A, ld, npad, p, a, V, b, st)) {
       // (the panel, its V, tau and R rows as the column steps leave them)
     } else if (qr_step_fused()) {
       const int64_t pslot = (int64_t)(QB + 1) * ((npad + QR_RC - 1) / QR_RC + 1);
@@ -835,7 +913,7 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
         const int nrc_c = (int)((npad - rbeg + QR_RC - 1) / QR_RC);
         const int ncol = (int)(c1 - c) + 1;   // columns c .. c1-1 and b
         hipLaunchKernelGGL(qr_col_step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad, c,
-                           c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, a->V, npad, stage);
+                           c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad, stage);
         nrc_prev = nrc_c;
       }
     } else
@@ -844,33 +922,46 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
       hipLaunchKernelGGL(qr_col_partials, dim3((unsigned)nrc, (unsigned)ncol), dim3(256), 0, st, A, ld, npad, c, c1, b,
                          a->part, nrc);
       hipLaunchKernelGGL(qr_col_reflect, dim3(1), dim3(256), 0, st, A, ld, c, c1, c0, b, a->part, nrc, a->tw, a->tau,
-                         a->scal, a->V, npad);
+                         a->scal, V, npad);
       hipLaunchKernelGGL(qr_col_update, dim3((unsigned)((npad - c + 255) / 256), (unsigned)ncol), dim3(256), 0, st, A,
-                         ld, npad, c, c1, c0, b, a->tw, a->scal, a->V, npad);
+                         ld, npad, c, c1, c0, b, a->tw, a->scal, V, npad);
     }
     const int ntr = nbk - p - 1;   // trailing column blocks
     if (ntr == 0) break;
     // T from Gv = VᵀV over the panel's rows (K split)
-    e = qr_ksplit(a->V, npad, a->V, npad, rows, 1, a, 2 * p, a->Gv, QB, st);
+    e = qr_ksplit(V, npad, V, npad, rows, 1, a, 2 * p, a->Gv, QB, st);
     if (e != hipSuccess) return e;
     if (qr_step_fused()) {   // T by MFMA doubling (chol.hip wy_t_kernel); SCS_QR_STEP=0: the plain recurrence
-      e = wy_t_build(a->Gv, a->tau, a->T, st);
+      e = wy_t_build(a->Gv, a->tau, T, st);
       if (e != hipSuccess) return e;
     } else {
-      hipLaunchKernelGGL(qr_build_t, dim3(1), dim3(QB), 0, st, a->Gv, a->tau, QB, a->T);
+      hipLaunchKernelGGL(qr_build_t, dim3(1), dim3(QB), 0, st, a->Gv, a->tau, QB, T);
     }
-    // Wm (QB x trailing) = Vᵀ A_trail: features = reflectors (A1 = V) x trailing columns (A2), the
-    // tiles (0, j < ntr), K split, in one launch
-    double* At = A + c1 * ld + c0;
-    e = qr_ksplit(a->V, npad, At, ld, rows, ntr, a, 2 * p + 1, a->Wm, QB, st);
+    // the trailing columns.  Lookahead: the previous bulk update wrote the columns this one starts
+    // from, so the caller's stream waits for it here -- after this panel, which ran beside it
+    if (bulk) {
+      e = hipStreamWaitEvent(st, a->evb, 0);
+      if (e != hipSuccess) return e;
+      bulk = false;
+    }
+    if (la && ntr > 1) {
+      e = hipEventRecord(a->evp, st);
+      if (e == hipSuccess) e = hipStreamWaitEvent(a->st2, a->evp, 0);
+      if (e == hipSuccess)
+        e = qr_apply_block(A, ld, npad, p, c1 + QB, ntr - 1, 2 * nbk + 2 * p + 1, V, T, a->Wm2, a->Ym2, a->Vt2,
+                           a->kpart2, a, a->st2);
+      if (e == hipSuccess) e = hipEventRecord(a->evb, a->st2);
+      if (e != hipSuccess) return e;
+      bulk = true;
+      // the next panel's columns
+      e = qr_apply_block(A, ld, npad, p, c1, 1, 2 * nbk + 2 * p, V, T, a->Wm, a->Ym, a->Vt, a->kpart, a, st);
+    } else {
+      e = qr_apply_block(A, ld, npad, p, c1, ntr, 2 * p + 1, V, T, a->Wm, a->Ym, a->Vt, a->kpart, a, st);
+    }
     if (e != hipSuccess) return e;
-    // Ym = Tᵀ Wm: Ym(i, j) = Σ_q T(q, i) Wm(q, j)
-    e = gram_launch_gen(a->T, QB, a->Wm, QB, a->ones, 0, QB, a->tiles, ntr, a->Ym, QB, 0, st);
-    if (e != hipSuccess) return e;
-    // A_trail -= V Ym: A(r, j) -= Σ_i Vt(i, r) Ym(i, j) (features r of Vt, K = i), panel p's rectangle
-    hipLaunchKernelGGL(qr_transpose_v, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, a->V, npad, rows, a->Vt);
-    e = gram_launch_gen(a->Vt, QB, a->Ym, QB, a->ones + npad, 0, QB, a->tiles + a->rect_off[(size_t)p],
-                        (int)(rows / QB) * ntr, At, ld, /*ACCUMULATE*/ 2, st);
+  }
+  if (bulk) {
+    e = hipStreamWaitEvent(st, a->evb, 0);
     if (e != hipSuccess) return e;
   }
   // R x = Qᵀ b: the diagonal blocks' inverses, then the one-launch backward solve (b holds Qᵀ b)

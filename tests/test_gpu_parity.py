@@ -985,6 +985,30 @@ def test_householder_qr_solve(m, coop, monkeypatch):
     assert np.linalg.norm(M @ x - rhs) <= 1e-12 * np.linalg.norm(M, 2) * np.linalg.norm(x)
 
 
+@pytest.mark.parametrize("m,coop", [(300, ""), (1000, ""), (2304, "1"), (8320, "")])
+def test_qr_lookahead_bit_identical(m, coop, monkeypatch):
+    """The QR's lookahead trailing update (SCS_QR_LA=1, r06): panel p's block reflector applied to the
+    next panel's columns on the caller's stream and to the columns beyond on a bulk stream beside panel
+    p + 1, V / T alternating by panel parity -- the same K pieces, combine order and tiles per column
+    block as the one-stream update, so the same solution bit for bit (per-column launches, and the
+    cooperative panel at m = 2304).  m = 300: 3 panels, one bulk update; 8320: 65 panels, the K split
+    clamped by the trailing width (16 pieces, not 17)."""
+    if coop:
+        monkeypatch.setenv("SCS_QR_COOP", coop)
+    N = m + 77
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=43)
+    rng = np.random.default_rng(44)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-3
+    rhs = rng.standard_normal(m)
+    monkeypatch.setenv("SCS_QR_LA", "0")
+    x0, used0 = p.solve_eval(w, d, rhs, mode=2)
+    monkeypatch.setenv("SCS_QR_LA", "1")
+    x1, used1 = p.solve_eval(w, d, rhs, mode=2)
+    assert not used0 and not used1
+    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+
+
 @pytest.mark.parametrize("case", ["ggn_feature", "ggn_sample", "nscore"])
 def test_reference_solver_trajectory(case, monkeypatch):
     """scs_set_solver(SCS_SOLVER_REFERENCE): ProxGGNSCORE's qr(JQJ) \\ Je (feature branch) and
