@@ -250,6 +250,171 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
   if (tid == 0) part[(c & 1) * pslot + (int64_t)jj * nrc + rc] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
 }
 
+// qr_col_step with CPW of the panel's columns per workgroup (r06, late; SCS_QR_CPW): workgroup (rc, 0)
+// is column c-1's reflector as before, workgroup (rc, 1 + g) takes columns jj = g·CPW .. g·CPW + CPW-1
+// (jj = c1 - c: b) of row chunk rc.  Column c and x (the previous column) are loaded once for the CPW
+// columns instead of once per column, and the launch has CPW times fewer workgroups; per column the
+// same operations in the same order (each thread's rows, wave sums, the ws combine, the previous
+// column's partials summed in chunk order by one lane each), so the same bits.
+template <int CPW>
+__global__ __launch_bounds__(256) void qr_col_step_g(double* __restrict__ A, int64_t ld, int64_t npad, int64_t c,
+                                                     int64_t c0, int64_t c1, double* __restrict__ b,
+                                                     double* __restrict__ part, int64_t pslot, int nrc, int nrc_prev,
+                                                     double* __restrict__ rowc, double* __restrict__ xs,
+                                                     double* __restrict__ tau, double* __restrict__ V, int64_t ldv) {
+  const int rc = blockIdx.x;
+  const int g = (int)blockIdx.y - 1;
+  const int tid = threadIdx.x;
+  const bool has_prev = c > c0;
+  const int64_t pv = c - 1;
+  const int64_t rbeg = has_prev ? pv : c;
+  const int64_t r0 = rbeg + (int64_t)rc * QR_RC, r1 = min(r0 + QR_RC, npad);
+  const int jmax = (int)(c1 - c);   // jj = jmax: b
+  __shared__ double sh[3 + CPW + 1];
+  __shared__ double ws[CPW][4];
+  __shared__ double sxx[QR_MAXRC], sbc[QR_MAXRC], sbj[CPW][QR_MAXRC];
+  const double* x = xs + (pv & 1) * npad;
+  const double* colc = (c < c1) ? A + c * ld : b;
+  constexpr int NPF = QR_RC / 256;
+  double pac[NPF], px[NPF], paj[CPW][NPF];
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) {
+    const int64_t r = r0 + tid + 256 * k;
+    const bool in = r < r1;
+    pac[k] = (in && g >= 0) ? colc[r] : 0.0;
+    px[k] = (in && has_prev) ? x[r] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < CPW; ++q) {
+    const int jj = g * CPW + q;
+    const bool live = g >= 0 && jj <= jmax;
+    const double* colj = (jj < jmax) ? A + (c + jj) * ld : b;
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int64_t r = r0 + tid + 256 * k;
+      paj[q][k] = (live && r < r1) ? colj[r] : 0.0;
+    }
+  }
+  // the previous column's chunk partials: staged by wave 0 into LDS (any chunk count up to QR_MAXRC)
+  const bool staged = has_prev && nrc_prev <= QR_MAXRC;
+  const double* pp = part + (pv & 1) * pslot;
+  if (staged && tid < 64) {
+    for (int q = tid; q < nrc_prev; q += 64) {
+      sxx[q] = pp[q];
+      if (c < c1) sbc[q] = pp[(c - pv) * nrc_prev + q];
+#pragma unroll
+      for (int u = 0; u < CPW; ++u) {
+        const int jj = g * CPW + u;
+        if (g >= 0 && jj <= jmax) sbj[u][q] = pp[(c + jj - pv) * nrc_prev + q];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // lanes 0 .. CPW of wave 0: the reflector (every lane the same sums in the same order) and one
+  // tau · vᵀ a_j each (lane CPW: column c's)
+  if (tid <= CPW) {
+    double t = 0.0, sc = 0.0, beta = 0.0, tw = 0.0;
+    if (has_prev) {
+      const double* rp = rowc + (pv & 1) * (QB + 2);
+      const double alpha = rp[0];
+      double xx = 0.0;
+      if (staged)
+        for (int q = 0; q < nrc_prev; ++q) xx += sxx[q];
+      else
+        for (int q = 0; q < nrc_prev; ++q) xx += pp[q];
+      beta = alpha;
+      if (xx > 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + xx), alpha);
+        t = (beta - alpha) / beta;
+        sc = 1.0 / (alpha - beta);
+      }
+      const int jj = tid < CPW ? g * CPW + tid : 0;   // lane CPW: column c (jj = 0)
+      const bool want = tid < CPW ? (g >= 0 && jj <= jmax) : (c < c1);
+      if (want) {
+        const double* sb = tid < CPW ? sbj[tid] : sbc;
+        const int64_t j = c + jj;
+        double d = 0.0;
+        if (staged)
+          for (int q = 0; q < nrc_prev; ++q) d += sb[q];
+        else
+          for (int q = 0; q < nrc_prev; ++q) d += pp[(j - pv) * nrc_prev + q];
+        tw = t * (rp[j - pv] + sc * d);
+      }
+    }
+    if (tid == 0) {
+      sh[0] = t;
+      sh[1] = sc;
+      sh[2] = beta;
+    }
+    sh[3 + tid] = tw;
+  }
+  __syncthreads();
+  const double t = sh[0], sc = sh[1];
+  if (g < 0) {   // column pv: V, its R entries, tau
+    if (!has_prev) return;
+    const int64_t vc = (pv - c0) * ldv;
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int64_t r = r0 + tid + 256 * k;
+      if (r < r1 && r > pv) V[vc + (r - c0)] = px[k] * sc;
+    }
+    if (rc == 0) {
+      for (int64_t r = c0 + tid; r <= pv; r += 256) V[vc + (r - c0)] = (r == pv) ? 1.0 : 0.0;
+      if (tid == 0) {
+        A[pv * ld + pv] = sh[2];
+        if (pv - 1 >= c0) A[pv * ld + pv - 1] = x[pv - 1];   // R(pv-1, pv): updated by launch pv
+        tau[pv - c0] = t;
+      }
+    }
+    return;
+  }
+  double* xo = xs + (c & 1) * npad;
+  const double twc = sh[3 + CPW];
+  double s[CPW];
+#pragma unroll
+  for (int q = 0; q < CPW; ++q) s[q] = 0.0;
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) {
+    const int64_t r = r0 + tid + 256 * k;
+    if (r >= r1) continue;
+    const double v = has_prev ? ((r == pv) ? 1.0 : px[k] * sc) : 0.0;
+    const double ac = has_prev ? pac[k] - twc * v : pac[k];
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const int jj = g * CPW + q;
+      if (jj > jmax) continue;
+      double aj = paj[q][k];
+      if (has_prev) aj -= sh[3 + q] * v;
+      if (jj == 0 && c < c1) xo[r] = aj;              // column c itself: to the scratch column
+      else if (has_prev) ((jj < jmax) ? A + (c + jj) * ld : b)[r] = aj;   // later columns and b: in place
+      if (r == c) rowc[(c & 1) * (QB + 2) + jj] = aj;
+      if (r > c) s[q] += ac * aj;
+    }
+  }
+  if (c >= c1) return;
+#pragma unroll
+  for (int q = 0; q < CPW; ++q) {
+    const double w = wave_sum(s[q]);
+    if ((tid & 63) == 0) ws[q][tid >> 6] = w;
+  }
+  __syncthreads();
+  if (tid < CPW) {
+    const int jj = g * CPW + tid;
+    if (jj <= jmax) part[(c & 1) * pslot + (int64_t)jj * nrc + rc] = ((ws[tid][0] + ws[tid][1]) + ws[tid][2]) + ws[tid][3];
+  }
+}
+
+// SCS_QR_CPW (read per call): panel columns per workgroup of the column step, unset / 2 (default) | 4 | 8,
+// 1 = qr_col_step.  probe_qr alternated, same box (profiles/r06/qr_cpw/): n = 16384 292.9 -> 277.8-278.0 ms,
+// 8192 84.9-85.3 -> 83.1-83.8 ms; 4: 300-301 / 95 ms, 8: 361 / 123 ms (a quarter / an eighth of the
+// workgroups, each thread's loads in series: too little memory parallelism per launch)
+static int qr_cpw() {
+  const char* e = getenv("SCS_QR_CPW");
+  const int v = e ? atoi(e) : 2;
+  return (v == 2 || v == 4 || v == 8) ? v : 1;
+}
+
 static bool qr_stage() {   // read per call (A/B): SCS_QR_STAGE=0 thread 0 loads the partials itself (r05)
   const char* e = getenv("SCS_QR_STAGE");
   return !(e && e[0] == '0');
@@ -912,8 +1077,20 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
         const int64_t rbeg = c > c0 ? c - 1 : c;
         const int nrc_c = (int)((npad - rbeg + QR_RC - 1) / QR_RC);
         const int ncol = (int)(c1 - c) + 1;   // columns c .. c1-1 and b
-        hipLaunchKernelGGL(qr_col_step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad, c,
-                           c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad, stage);
+        const int cpw = qr_cpw();
+        const unsigned gy = 1u + (unsigned)((ncol + cpw - 1) / cpw);
+        if (cpw == 2)
+          hipLaunchKernelGGL(qr_col_step_g<2>, dim3((unsigned)nrc_c, gy), dim3(256), 0, st, A, ld, npad, c, c0, c1, b,
+                             a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad);
+        else if (cpw == 4)
+          hipLaunchKernelGGL(qr_col_step_g<4>, dim3((unsigned)nrc_c, gy), dim3(256), 0, st, A, ld, npad, c, c0, c1, b,
+                             a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad);
+        else if (cpw == 8)
+          hipLaunchKernelGGL(qr_col_step_g<8>, dim3((unsigned)nrc_c, gy), dim3(256), 0, st, A, ld, npad, c, c0, c1, b,
+                             a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad);
+        else
+          hipLaunchKernelGGL(qr_col_step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad,
+                             c, c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad, stage);
         nrc_prev = nrc_c;
       }
     } else

@@ -985,6 +985,27 @@ def test_householder_qr_solve(m, coop, monkeypatch):
     assert np.linalg.norm(M @ x - rhs) <= 1e-12 * np.linalg.norm(M, 2) * np.linalg.norm(x)
 
 
+@pytest.mark.parametrize("cpw", ["2", "4", "8"])
+@pytest.mark.parametrize("m", [300, 2304, 8320])
+def test_qr_column_groups_bit_identical(m, cpw, monkeypatch):
+    """The QR column step with CPW panel columns per workgroup (qr_col_step_g, SCS_QR_CPW, r06): column
+    c and the previous column loaded once per group -- per column the same operations and sums as one
+    column per workgroup (SCS_QR_CPW=1), so the same solution bit for bit; groups that overhang the
+    panel's last column and b included (129 - c columns per launch)."""
+    N = m + 77
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=45)
+    rng = np.random.default_rng(46)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-3
+    rhs = rng.standard_normal(m)
+    monkeypatch.setenv("SCS_QR_CPW", "1")
+    x0, used0 = p.solve_eval(w, d, rhs, mode=2)
+    monkeypatch.setenv("SCS_QR_CPW", cpw)
+    x1, used1 = p.solve_eval(w, d, rhs, mode=2)
+    assert not used0 and not used1
+    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+
+
 @pytest.mark.parametrize("m,coop", [(300, ""), (1000, ""), (2304, "1"), (8320, "")])
 def test_qr_lookahead_bit_identical(m, coop, monkeypatch):
     """The QR's lookahead trailing update (SCS_QR_LA=1, r06): panel p's block reflector applied to the
