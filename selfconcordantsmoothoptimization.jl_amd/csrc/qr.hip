@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void qr_col_step(double* __restrict__ A, int64
 // columns instead of once per column, and the launch has CPW times fewer workgroups; per column the
 // same operations in the same order (each thread's rows, wave sums, the ws combine, the previous
 // column's partials summed in chunk order by one lane each), so the same bits.
-template <int CPW>
+template <int CPW, int RC>
 __global__ __launch_bounds__(256) void qr_col_step_g(double* __restrict__ A, int64_t ld, int64_t npad, int64_t c,
                                                      int64_t c0, int64_t c1, double* __restrict__ b,
                                                      double* __restrict__ part, int64_t pslot, int nrc, int nrc_prev,
@@ -268,14 +268,14 @@ __global__ __launch_bounds__(256) void qr_col_step_g(double* __restrict__ A, int
   const bool has_prev = c > c0;
   const int64_t pv = c - 1;
   const int64_t rbeg = has_prev ? pv : c;
-  const int64_t r0 = rbeg + (int64_t)rc * QR_RC, r1 = min(r0 + QR_RC, npad);
+  const int64_t r0 = rbeg + (int64_t)rc * RC, r1 = min(r0 + RC, npad);
   const int jmax = (int)(c1 - c);   // jj = jmax: b
   __shared__ double sh[3 + CPW + 1];
   __shared__ double ws[CPW][4];
   __shared__ double sxx[QR_MAXRC], sbc[QR_MAXRC], sbj[CPW][QR_MAXRC];
   const double* x = xs + (pv & 1) * npad;
   const double* colc = (c < c1) ? A + c * ld : b;
-  constexpr int NPF = QR_RC / 256;
+  constexpr int NPF = RC / 256;
   double pac[NPF], px[NPF], paj[CPW][NPF];
 #pragma unroll
   for (int k = 0; k < NPF; ++k) {
@@ -409,6 +409,25 @@ __global__ __launch_bounds__(256) void qr_col_step_g(double* __restrict__ A, int
 // 1 = qr_col_step.  probe_qr alternated, same box (profiles/r06/qr_cpw/): n = 16384 292.9 -> 277.8-278.0 ms,
 // 8192 84.9-85.3 -> 83.1-83.8 ms; 4: 300-301 / 95 ms, 8: 361 / 123 ms (a quarter / an eighth of the
 // workgroups, each thread's loads in series: too little memory parallelism per launch)
+// SCS_QR_RC (read per call; the grouped step only): rows per partial-sum chunk, 256 | unset / 512 | 1024.
+// Another chunking is another summation order of the column norms and dots (checked against LAPACK, as
+// every QR here).  probe_qr alternated with CPW = 2 (profiles/r06/qr_rc/): n = 8192 83.2-83.5 -> 79.7 ms,
+// 2048 14.6 -> 13.5 ms, 16384 277.7-279.9 -> 277.7-277.8 ms; 256: 82.2-82.8 / 13.1 / 304.8-305.3 ms;
+// CPW = 4 slower at every chunk
+static int qr_rc() {
+  const char* e = getenv("SCS_QR_RC");
+  const int v = e ? atoi(e) : 512;
+  return (v == 256 || v == 1024) ? v : 512;
+}
+
+template <int CPW, int RC>
+static void qr_step_launch(int nrc_c, unsigned gy, hipStream_t st, double* A, int64_t ld, int64_t npad, int64_t c,
+                           int64_t c0, int64_t c1, double* b, double* part, int64_t pslot, int nrc_prev, double* rowc,
+                           double* xs, double* tau, double* V) {
+  hipLaunchKernelGGL((qr_col_step_g<CPW, RC>), dim3((unsigned)nrc_c, gy), dim3(256), 0, st, A, ld, npad, c, c0, c1, b,
+                     part, pslot, nrc_c, nrc_prev, rowc, xs, tau, V, npad);
+}
+
 static int qr_cpw() {
   const char* e = getenv("SCS_QR_CPW");
   const int v = e ? atoi(e) : 2;
@@ -817,7 +836,7 @@ static void qr_free_bufs(QRAux* a) {
 hipError_t qr_aux_init(QRAux* a, int64_t npad, hipStream_t st) {
   if (a->npad == npad) return hipSuccess;
   qr_free_bufs(a);
-  const int64_t nrc = (npad + QR_RC - 1) / QR_RC;
+  const int64_t nrc = (npad + 255) / 256;   // (the partials' slots: the smallest chunk, SCS_QR_RC = 256)
   const int nbk = (int)(npad / QB);
   hipError_t e = hipSuccess;
   auto al = [&](double** p, size_t n) {
@@ -1078,18 +1097,21 @@ hipError_t qr_solve(double* A, int64_t ld, int64_t npad, QRAux* a, double* b, hi
         const int nrc_c = (int)((npad - rbeg + QR_RC - 1) / QR_RC);
         const int ncol = (int)(c1 - c) + 1;   // columns c .. c1-1 and b
         const int cpw = qr_cpw();
+        const int rcg = cpw > 1 ? qr_rc() : QR_RC;   // the grouped step's chunk
+        const int nrc_g = (int)((npad - rbeg + rcg - 1) / rcg);
+        const int64_t pslot_g = (int64_t)(QB + 1) * ((npad + rcg - 1) / rcg + 1);
         const unsigned gy = 1u + (unsigned)((ncol + cpw - 1) / cpw);
-        if (cpw == 2)
-          hipLaunchKernelGGL(qr_col_step_g<2>, dim3((unsigned)nrc_c, gy), dim3(256), 0, st, A, ld, npad, c, c0, c1, b,
-                             a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad);
-        else if (cpw == 4)
-          hipLaunchKernelGGL(qr_col_step_g<4>, dim3((unsigned)nrc_c, gy), dim3(256), 0, st, A, ld, npad, c, c0, c1, b,
-                             a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad);
-        else if (cpw == 8)
-          hipLaunchKernelGGL(qr_col_step_g<8>, dim3((unsigned)nrc_c, gy), dim3(256), 0, st, A, ld, npad, c, c0, c1, b,
-                             a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad);
-        else
-          hipLaunchKernelGGL(qr_col_step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad,
+#define QR_STEP(CW, R) qr_step_launch<CW, R>(nrc_g, gy, st, A, ld, npad, c, c0, c1, b, a->part, pslot_g, nrc_prev, \
+                                            a->rowc, a->xs, a->tau, V)
+        if (cpw > 1) {
+          if (cpw == 2) { if (rcg == 256) QR_STEP(2, 256); else if (rcg == 512) QR_STEP(2, 512); else QR_STEP(2, 1024); }
+          else if (cpw == 4) { if (rcg == 256) QR_STEP(4, 256); else if (rcg == 512) QR_STEP(4, 512); else QR_STEP(4, 1024); }
+          else QR_STEP(8, 1024);
+          nrc_prev = nrc_g;
+          continue;
+        }
+#undef QR_STEP
+        hipLaunchKernelGGL(qr_col_step, dim3((unsigned)nrc_c, (unsigned)(ncol + 1)), dim3(256), 0, st, A, ld, npad,
                              c, c0, c1, b, a->part, pslot, nrc_c, nrc_prev, a->rowc, a->xs, a->tau, V, npad, stage);
         nrc_prev = nrc_c;
       }

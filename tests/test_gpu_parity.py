@@ -998,12 +998,37 @@ def test_qr_column_groups_bit_identical(m, cpw, monkeypatch):
     w = (rng.random(N) + 0.5) / N
     d = (rng.random(m) + 0.5) * 1e-3
     rhs = rng.standard_normal(m)
+    monkeypatch.setenv("SCS_QR_RC", "1024")   # (qr_col_step's chunk: the same sums)
     monkeypatch.setenv("SCS_QR_CPW", "1")
     x0, used0 = p.solve_eval(w, d, rhs, mode=2)
     monkeypatch.setenv("SCS_QR_CPW", cpw)
     x1, used1 = p.solve_eval(w, d, rhs, mode=2)
     assert not used0 and not used1
     assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+
+
+@pytest.mark.parametrize("rc", ["256", "1024"])
+@pytest.mark.parametrize("m", [300, 4100])
+def test_qr_chunk_rows_vs_lapack(m, rc, monkeypatch):
+    """The grouped QR column step at the other chunk sizes (SCS_QR_RC; 512 is the default, covered by
+    test_householder_qr_solve): another summation order of the same reflectors -- against LAPACK's QR
+    solve within the same bound as the default."""
+    monkeypatch.setenv("SCS_QR_RC", rc)
+    N = m + 77
+    p = scsopt.Problem.synthetic(N, m, np.zeros(m), losses.least_squares(1.0 / N), 1.0, kind=3, seed=41)
+    rng = np.random.default_rng(42)
+    w = (rng.random(N) + 0.5) / N
+    d = (rng.random(m) + 0.5) * 1e-3
+    rhs = rng.standard_normal(m)
+    x, used_lu = p.solve_eval(w, d, rhs, mode=2)
+    assert not used_lu
+    A, _ = p.get_data()
+    M = A.T @ (w[:, None] * A) + np.diag(d)
+    Q, R = np.linalg.qr(M)
+    xr = np.linalg.solve(R, Q.T @ rhs)
+    cond = np.linalg.cond(M)
+    np.testing.assert_allclose(x, xr, rtol=0, atol=1e-13 * cond * float(np.max(np.abs(xr))))
+    assert np.linalg.norm(M @ x - rhs) <= 1e-12 * np.linalg.norm(M, 2) * np.linalg.norm(x)
 
 
 @pytest.mark.parametrize("m,coop", [(300, ""), (1000, ""), (2304, "1"), (8320, "")])
